@@ -1,0 +1,295 @@
+/*
+ * vqx.h — C ABI of libvqx.so, the MI355X (gfx950) kernels behind the
+ * vae_npvc VQ-VAE training step.
+ *
+ * The reference (Sinica-SLAM/vae_npvc) has no native layer: every op on its
+ * hot path is a stock PyTorch call.  Each entry point below replaces one of
+ * those calls (or a fused group of them); the reference site is cited per
+ * function.  Paths are relative to the reference repository root.
+ *
+ * Conventions (all entry points):
+ *   - every pointer is a DEVICE pointer owned by the caller (PyTorch's caching
+ *     allocator in the Python host layer); nothing here allocates or frees;
+ *   - calls are stream-ordered on `stream` (a hipStream_t, NULL = legacy
+ *     stream) and never synchronise the host, so they can be captured into a
+ *     hipGraph;
+ *   - activations are "frame-major": row n = b*T + t, channels contiguous
+ *     (the reference's (B, C, T) tensors transposed to (B*T, C));
+ *   - return 0 on success, <0 on an invalid argument (-1) or a HIP launch
+ *     error (-2); vqx_last_error() then holds thread-local text.
+ */
+#ifndef VQX_H
+#define VQX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* vqx_stream_t; /* hipStream_t */
+
+/* element types of activation / weight operands */
+enum { VQX_F32 = 0, VQX_BF16 = 1 };
+
+/* operand prologues, applied elementwise while a tile is staged into LDS */
+enum {
+  VQX_PRO_NONE = 0,
+  VQX_PRO_LRELU = 1,      /* LeakyReLU(0.2)   layers.py:152, vqvae.py:171   */
+  VQX_PRO_RELU = 2,       /* ReLU             vqvae.py:283,285              */
+  VQX_PRO_SCALE_RELU = 3  /* ReLU(pro_scale*x) vqvae.py:316-317            */
+};
+
+/* epilogue flags of vqx_conv1d_fwd / vqx_conv1d_dgrad, applied in this order */
+enum {
+  VQX_EPI_BIAS = 1 << 0,    /* v += bias[c]                                    */
+  VQX_EPI_ROWBIAS = 1 << 1, /* v += rowbias[(n/T)*cout + c]  (conv_cond term)  */
+  VQX_EPI_MASK = 1 << 2,    /* v *= (mask[n][c] > 0 ? 1 : mask_slope)*mask_scale */
+  VQX_EPI_RES = 1 << 3,     /* v += res[n][c]                                  */
+  VQX_EPI_GNADD = 1 << 4,   /* v += (gn_h[n][c]-mean[b])*rstd[b]*gamma[c]+beta[c] */
+  VQX_EPI_SPLIT = 1 << 5,   /* cols >= split_col -> out2[n][c-split_col] (f32,
+                               '+=' when out2_accumulate)                      */
+  VQX_EPI_OUTF32 = 1 << 6   /* y stored as f32 instead of `dtype`              */
+};
+
+/*
+ * Stride-1 Conv1d / ConvTranspose1d as an implicit-im2col GEMM on MFMA.
+ *   fwd  : y[n][co] = epi( sum_{j,ci} w[co][j*cin+ci] * pro(x[n+j-pad][ci]) )
+ *          rows n+j-pad outside the utterance of n read as zero (padding).
+ *   dgrad: the same args with x = dy [N][cin], w = the FORWARD layer's packed
+ *          weight [cout][ntaps*cin_fwd]; computes
+ *          dx[n][ci] = epi( sum_{j,c} w[c][(ntaps-1-j)*cout_total.. ] ... )
+ *          i.e. the transposed, tap-flipped conv; here `cin` = channels of dy
+ *          (the forward layer's cout) and `cout` = the forward layer's cin.
+ * Reference: nn.Conv1d / nn.ConvTranspose1d forward and autograd backward,
+ * vqvae.py:156,174,257-265,286; layers.py:157,164,196,208,213.
+ */
+typedef struct vqx_conv_args {
+  const void* x;             /* [N][ldx]                                       */
+  const void* w;             /* packed weight [cout_fwd][ntaps*cin_fwd]        */
+  void* y;                   /* [N][ldy]                                       */
+  const float* bias;         /* [cout]                                         */
+  const float* rowbias;      /* [B][cout]                                      */
+  const void* res;           /* [N][ldres]  dtype                              */
+  const void* mask;          /* [N][ldmask] dtype                              */
+  const void* gn_h;          /* [N][ldgn]   dtype                              */
+  const float* gn_mean_rstd; /* [B][2]                                         */
+  const float* gn_gamma;     /* [cout]                                         */
+  const float* gn_beta;      /* [cout]                                         */
+  float* out2;               /* [N][ldo2] f32                                  */
+  int64_t n_rows;            /* N = B*T                                        */
+  int32_t T;                 /* frames per utterance                           */
+  int32_t cin, cout, ntaps, pad;
+  int32_t ldx, ldy, ldres, ldmask, ldgn, ldo2;
+  int32_t dtype;             /* VQX_F32 | VQX_BF16                             */
+  int32_t prologue;          /* VQX_PRO_*  (applied to x)                      */
+  int32_t epilogue;          /* VQX_EPI_* flags                                */
+  int32_t split_col, out2_accumulate;
+  float pro_scale, mask_slope, mask_scale;
+} vqx_conv_args;
+
+int vqx_conv1d_fwd(const vqx_conv_args* a, vqx_stream_t stream);
+int vqx_conv1d_dgrad(const vqx_conv_args* a, vqx_stream_t stream);
+
+/*
+ * Weight gradient of a stride-1 conv as split-K partial slabs:
+ *   slabs[s][r][j*c_dim + c] = sum_{n in split s} p[n][r] * pro(q[n + sign*(j-pad)][c])
+ * Conv1d  (dW[co][ci][j]): p = dy, q = x,  sign = +1.
+ * ConvT1d (dW[ci][co][k-1-j]): p = x, q = du, sign = -1.
+ * vqx_weight_norm_bwd reduces the slabs.  Reference: autograd of the convs
+ * above (convolution_backward, 49% of the reference CPU step).
+ */
+typedef struct vqx_wgrad_args {
+  const void* p;
+  const void* q;
+  float* slabs;      /* [splits][r_dim][ntaps*c_dim] */
+  int64_t n_rows;
+  int32_t T, r_dim, c_dim, ntaps, pad, shift_sign, ldp, ldq;
+  int32_t dtype, q_prologue, splits;
+  float pro_scale;
+} vqx_wgrad_args;
+
+int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream);
+
+/*
+ * Weight norm (torch.nn.utils.weight_norm, dim=0; applied at vqvae.py:203-208,
+ * 329-334): w = g * v / ||v|| per row o of v[rows][cols] (Conv1d rows = cout,
+ * ConvT rows = cin).  The forward packs w into the effective-conv layout the
+ * GEMMs read: w_packed[co][j*cin + ci] in `dtype`.
+ * kind 0: Conv1d v[cout][cin][k]; kind 1: ConvTranspose1d v[cin][cout][k]
+ * (effective tap j' = k-1-j).  Descriptors are batched: one launch packs
+ * every layer of the model.
+ */
+typedef struct vqx_wn_layer {
+  const float* v;       /* [rows][cols] */
+  const float* g;       /* [rows]       */
+  void* w_packed;       /* [cout][k*cin] dtype */
+  float* norm;          /* [rows] ||v_o|| saved for the backward */
+  float* dv;            /* bwd: [rows][cols] */
+  float* dg;            /* bwd: [rows] */
+  const float* slabs;   /* bwd: wgrad slabs */
+  int32_t kind, cout, cin, k, splits, dtype;
+} vqx_wn_layer;
+
+/* `layers_host` sizes the launch; the kernels read the same table from the
+ * device copy `layers_dev` (built once by the caller, so a captured graph
+ * replays without host work). */
+int vqx_weight_norm_fwd(const vqx_wn_layer* layers_host, const vqx_wn_layer* layers_dev,
+                        int32_t n_layers, vqx_stream_t stream);
+int vqx_weight_norm_bwd(const vqx_wn_layer* layers_host, const vqx_wn_layer* layers_dev,
+                        int32_t n_layers, vqx_stream_t stream);
+
+/*
+ * GroupNorm statistics (nn.GroupNorm, layers.py:154 (G=1), layers.py:201
+ * (G=2); eps 1e-5): mean and 1/sqrt(var+eps) over (C/G, T) per utterance.
+ * x [N][ldx] dtype, C channels; out mean_rstd[B][G][2] f32.  Two-pass
+ * (mean, then centred sum of squares) per (b, g).
+ */
+int vqx_groupnorm_stats(const void* x, int32_t ldx, int32_t dtype, int64_t n_rows, int32_t T,
+                        int32_t C, int32_t G, float eps, float* partials /* >= B*G*24 */,
+                        float* mean_rstd, vqx_stream_t stream);
+
+/*
+ * Fused GroupNorm(G=2) + gated tanh/sigmoid unit, decoder ResSkip block
+ * (layers.py:236-242):  g[n][c] = tanh(h(n,c)) * sigmoid(h(n,c+C/2)),
+ * h = (u - mean)*rstd*gamma + beta.  u [N][ldu], g [N][ldg], C = 2*half.
+ */
+int vqx_gn_glu_fwd(const void* u, int32_t ldu, void* g, int32_t ldg, int32_t dtype, int64_t n_rows,
+                   int32_t T, int32_t C, const float* mean_rstd, const float* gamma, const float* beta,
+                   vqx_stream_t stream);
+
+/*
+ * Backward of GroupNorm(G) optionally preceded by the gated unit:
+ *   glu=1: dy is dL/dg [N][C/2], u is the GN input [N][C]: computes dL/dh
+ *          through tanh*sigmoid, then through GroupNorm, into du [N][C].
+ *   glu=0: dy is dL/d(GN output) [N][C].
+ * Also accumulates per-utterance column sums of du (for the conv bias and
+ * conv_cond gradients) into colsum[B][C] and dgamma/dbeta partials
+ * [B][C] (summed over B by the caller's reduction).
+ * Reference: autograd of layers.py:236-242 and 170-176.
+ */
+int vqx_gn_bwd(const void* dy, int32_t lddy, const void* u, int32_t ldu, void* du, int32_t lddu,
+               int32_t dtype, int64_t n_rows, int32_t T, int32_t C, int32_t G, int32_t glu,
+               const float* mean_rstd, const float* gamma, const float* beta,
+               float* partials /* >= B*16*G */, float* colsum_b, float* dgamma_b, float* dbeta_b,
+               vqx_stream_t stream);
+
+/*
+ * Sum over rows: out[c] (+)= sum_n x[n][c] (f32 accumulation, deterministic
+ * two-level tree).  Used for conv bias gradients and for reducing [B][C]
+ * partials.  accumulate=1 adds into out.
+ */
+int vqx_colsum(const void* x, int32_t ldx, int32_t dtype, int64_t n_rows, int32_t C,
+               float* partials /* >= 64*C */, float* out, int32_t accumulate, vqx_stream_t stream);
+
+/*
+ * Frame-major copy of the (B, C, T) input batch, with dtype conversion
+ * (the reference's z.transpose(1,2).contiguous(), layers_vq.py:274-276).
+ */
+int vqx_nct_to_ntc(const float* x_nct, int32_t B, int32_t C, int32_t T, void* y, int32_t ldy,
+                   int32_t dtype, vqx_stream_t stream);
+int vqx_ntc_to_nct(const void* y, int32_t ldy, int32_t dtype, int32_t B, int32_t C, int32_t T,
+                   float* x_nct, vqx_stream_t stream);
+
+/*
+ * log_loss (layers.py:283-296, reduction 'frame_mean') fused with its
+ * gradient: loss = sum 0.5*(log2pi + (x - xhat)^2) / (B*T);
+ * dxhat = (xhat - x) * grad_scale (grad_scale = dL/dloss / (B*T)).
+ * x is the reference (B, C, T) f32 batch; xhat is frame-major f32.
+ * loss_out[0] receives the loss (deterministic reduction).
+ */
+int vqx_logloss_fwd_bwd(const float* x_nct, const float* xhat, int32_t ldxh, int32_t B, int32_t C,
+                        int32_t T, float grad_scale, void* dxhat, int32_t lddx, int32_t dtype,
+                        float* loss_out, float* partials, vqx_stream_t stream);
+
+/*
+ * EMA vector-quantizer forward (EMAVectorQuantizer.forward,
+ * layers_vq.py:268-323, distances :285-289, argmin :291, gather :292,
+ * commitment loss :301,308-309; update_emb statistics :207-211):
+ *   dist[n][k] = (||z_n||^2 + ||e_k||^2) - 2 z_n.e_k   (fp32 MFMA)
+ *   idx[n]     = first argmin_k dist[n][k]               (int64)
+ *   zq[n]      = E[idx[n]]  (f32 [N][D]) and zq_c (dtype, decoder input)
+ *   sqerr      : sum_n ||zq_n - z_n||^2  into sqerr_out[0] (deterministic)
+ *   bsum[k][d] += sum_{n: idx=k} z[n][d], bcnt[k] += |{n: idx=k}|
+ *                 (fp32 atomics; pass NULL to skip, e.g. eval / encode())
+ * z [N][D] f32 (frame-major, D = 128), E [K][D] f32, K % 16 == 0.
+ * `partials` is a caller workspace of >= ceil(N/64) floats.
+ */
+int vqx_vq_forward(const float* z, int64_t n_rows, int32_t D, const float* E, int32_t K,
+                   int64_t* idx, float* zq, void* zq_c, int32_t zq_c_dtype, float* sqerr_out,
+                   float* partials, float* bsum, float* bcnt, vqx_stream_t stream);
+
+/*
+ * EMA codebook update (update_emb, layers_vq.py:203-233; init_emb :192-201):
+ *   emb_sum  = mu*emb_sum  + (1-mu)*bsum;  emb_elem = mu*emb_elem + (1-mu)*bcnt
+ *   usage    = emb_elem >= threshold
+ *   E        = usage ? emb_sum/emb_elem : rand_rows
+ *   diag[0..3] = {entropy (perplexity of bcnt), used_curr, usage, diff_emb}
+ * rand_rows [K][D] are the rows z[perm[:K]] gathered by vqx_gather_rows.
+ * Single workgroup, deterministic.
+ */
+int vqx_vq_ema_update(float* emb_sum, float* emb_elem, float* E, const float* bsum,
+                      const float* bcnt, const float* rand_rows, int32_t K, int32_t D, float mu,
+                      float threshold, float* diag, vqx_stream_t stream);
+
+/* out[i][:] = src[rows[i]][:] for i < n_out  (f32, row length D).  rows are
+ * int64 indices; negative indices write zero rows (rows owned by another
+ * rank in data-parallel training). */
+int vqx_gather_rows(const float* src, int32_t ld_src, const int64_t* rows, int32_t n_out,
+                    int32_t D, float* out, vqx_stream_t stream);
+
+/* Commitment-loss gradient (layers_vq.py:301 backward):
+ *   dz[n][d] = scale * (z[n][d] - zq[n][d])  written in dtype. */
+int vqx_vq_commit_bwd(const float* z, const float* zq, int64_t count, float scale, void* dz,
+                      int32_t dtype, vqx_stream_t stream);
+
+/* Jitter (layers_vq.py:353-379): y[b][t][:] = x[b][src_t[t]][:]. */
+int vqx_time_gather(const void* x, void* y, int32_t B, int32_t T, int32_t C, const int32_t* src_t,
+                    int32_t dtype, vqx_stream_t stream);
+
+/* Speaker embedding lookup (layers.py:42-54, nn.Embedding) and its
+ * backward scatter-add (dense weight gradient). */
+int vqx_embedding_fwd(const float* weight, const int64_t* ids, int32_t B, int32_t D, float* out,
+                      vqx_stream_t stream);
+int vqx_embedding_bwd(const float* dout, const int64_t* ids, int32_t B, int32_t D, float* dweight,
+                      vqx_stream_t stream);
+
+/* Small dense GEMM for the time-constant conv_cond term (vqvae.py:309-312):
+ * out[b][o] = sum_i W[o][i] * c[b][i] + bias[o]   (f32, W from weight norm
+ * in f32).  And its backward:  dW[o][i] += sum_b dout[b][o] * c[b][i],
+ * dc[b][i] += sum_o dout[b][o] * W[o][i]. */
+int vqx_linear_f32(const float* c, const float* W, const float* bias, int32_t B, int32_t I,
+                   int32_t O, float* out, vqx_stream_t stream);
+int vqx_linear_bwd_f32(const float* dout, const float* c, const float* W, int32_t B, int32_t I,
+                       int32_t O, float* dW, float* dc, vqx_stream_t stream);
+
+/*
+ * Global gradient norm + fused Adam (trainer/basic.py:63-69:
+ * clip_grad_norm_(max_norm) then torch.optim.Adam(betas, eps, wd=0)).
+ * grad_sq_norm: out[0] = sum g^2 over the flat buffer (deterministic;
+ *   partials >= 1024 floats).
+ * adam_hyper: increments the device step counter t and writes
+ *   hyper[8] = {lr_t, lr_t/(1-b1^t), sqrt(1-b2^t), t, 1-b1, b2, 1-b2, eps}
+ *   with every scalar formed in double like torch's Python-float math, then
+ *   rounded to f32; lr_t = lr0*gamma^floor((t-1)/step_size) (StepLR,
+ *   basic.py:43-46, stepped once per iteration).  Graph-capturable.
+ * adam_step: coef = min(1, max_norm/(sqrt(sumsq)+1e-6)) when max_norm > 0;
+ *   g' = g*coef; m = lerp(m, g', 1-b1); v = v*b2 + ((1-b2)*g')*g';
+ *   p += -(lr/bc1) * (m / (sqrt(v)/sqrt(bc2) + eps))   (torch single-tensor
+ *   Adam operation order).
+ */
+int vqx_grad_sq_norm(const float* g, int64_t n, float* partials, float* out, vqx_stream_t stream);
+int vqx_adam_hyper(int64_t* step, double lr0, double gamma, int32_t step_size, double beta1,
+                   double beta2, double eps, float* hyper, vqx_stream_t stream);
+int vqx_adam_step(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper,
+                  const float* sumsq, float max_norm, vqx_stream_t stream);
+
+/* Thread-local description of the last failure. */
+const char* vqx_last_error(void);
+/* ABI version (major*100 + minor). */
+int vqx_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VQX_H */

@@ -1,0 +1,346 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+CPU fp32 restatement (plain torch-CPU ops) of the reference VQ-VAE training
+step of Sinica-SLAM/vae_npvc, used as the parity checker for the HIP path
+and as the CPU baseline timed by bench.py.  Only tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg may import this module; the product package
+(vae_npvc_amd) never does.
+
+Pinned against golden vectors produced by importing the reference itself in
+the survey container (tests/golden/make_golden.py -> tests/golden/*.npz);
+tests/test_oracle_golden.py checks this restatement against them.
+
+Scope: the single-stage Encoder/Decoder of
+egs/vcc20/vae1/conf/train_pytorch_vqvae.yaml and
+egs/aishell3/vc2/conf/train_pytorch_vqvae.yaml (one resolution stage, k=3,
+stack_layers 1, no dilation), EMAVectorQuantizer, Jitter, log_loss and
+Trainer.train_step (Adam, clip_grad_norm_, StepLR).  Every function cites the
+reference file:line it restates (paths relative to the reference root).
+"""
+import math
+from collections import OrderedDict
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+LOG_2PI = math.log(2.0 * math.pi)  # vae_npvc/model/layers.py:8
+
+
+# ----------------------------------------------------------------- structure
+def layer_specs(cfg):
+    """Ordered parameter spec [(name, shape)] of vae_npvc.model.vqvae.Model in
+    registration order (== model.parameters() order; vqvae.py:15-40,
+    layers.py:139-165,191-215; weight_norm registers weight_g/weight_v after
+    bias).  Only the single-stage architecture of the baseline YAMLs."""
+    enc, dec = cfg["encoder"], cfg["decoder"]
+    assert len(enc["in_channels"]) == 1 and enc.get("stack_layers", 2) == 1 and not enc.get("dilation", True)
+    assert len(dec["in_channels"]) == 1 and not dec.get("dilation", True)
+    assert enc.get("kernel_size", 3) == 3 and enc.get("stack_kernel_size", 3) == 3
+    assert dec.get("kernel_size", 5) == 3 and dec.get("stack_kernel_size", 3) == 3
+    mel, C = enc["in_channels"][0], enc["out_channels"][0]
+    Z = enc.get("z_channels", 128)
+    ns = enc["stacks"][0]
+    Cd = dec["out_channels"][0]
+    cond, skip, fin = dec["cond_channels"], dec["skip_channels"], dec["final_channels"]
+    nd = dec["stacks"][0]
+    spec = []
+
+    def conv(name, cin, cout, k, transposed=False):
+        spec.append((name + ".bias", (cout,)))
+        g = (cin, 1, 1) if transposed else (cout, 1, 1)
+        v = (cin, cout, k) if transposed else (cout, cin, k)
+        spec.append((name + ".weight_g", g))
+        spec.append((name + ".weight_v", v))
+
+    def gn(name, c):
+        spec.append((name + ".weight", (c,)))
+        spec.append((name + ".bias", (c,)))
+
+    conv("encoder.encode.0", mel, C, 3)
+    for i in range(1, ns + 1):
+        conv(f"encoder.encode.{i}.stack.1", C, C, 3)
+        gn(f"encoder.encode.{i}.stack.2", C)
+        conv(f"encoder.encode.{i}.skip_layer", C, C, 1)
+    conv(f"encoder.encode.{ns + 2}", C, Z, 1)
+    conv("decoder.layers.0", dec["in_channels"][0], Cd, 3, transposed=True)
+    for i in range(1, nd + 1):
+        conv(f"decoder.layers.{i}.conv_in", Cd, 2 * Cd, 3, transposed=True)
+        gn(f"decoder.layers.{i}.norm_layer", 2 * Cd)
+        conv(f"decoder.layers.{i}.conv_cond", cond, 2 * Cd, 1)
+        conv(f"decoder.layers.{i}.res_skip_layers", Cd, Cd + skip, 1)
+    conv("decoder.final_layer.1", skip, skip, 1)
+    conv("decoder.final_layer.3", skip, fin, 1)
+    spec.append(("embeds._embedding.weight", (cfg.get("y_num", 10), cfg.get("y_dim", 128))))
+    return spec
+
+
+def buffer_specs(cfg):
+    K, D = cfg.get("z_num", 512), cfg.get("z_dim", 128)
+    return [("quantizer.emb_init", ()), ("quantizer.emb_sum", (K, D)), ("quantizer.emb_elem", (K,)),
+            ("quantizer.embeddings", (K, D))]
+
+
+def seeded_state_dict(cfg, seed):
+    """Deterministic weights from a numpy PCG64 stream (platform independent),
+    shaped like the reference default init: v ~ U(-1/sqrt(fan_in), +), g =
+    ||v_o|| * U(0.8, 1.2), biases U(-b, b), GroupNorm affine near (1, 0),
+    embedding N(0, 1).  Fresh EMA buffers (layers_vq.py:170-173)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    sd = OrderedDict()
+    pending_v = {}
+    for name, shape in layer_specs(cfg):
+        if name.endswith(".weight_v"):
+            fan_in = int(np.prod(shape[1:])) if "decoder.layers.0." not in name and ".conv_in." not in name else \
+                int(shape[0] * shape[2])
+            b = 1.0 / math.sqrt(fan_in)
+            v = rng.uniform(-b, b, size=shape).astype(np.float32)
+            sd[name] = torch.from_numpy(v)
+            g = sd[name[:-1] + "g"]
+            norm = np.sqrt((v.astype(np.float64) ** 2).reshape(shape[0], -1).sum(1)).astype(np.float32)
+            sd[name[:-1] + "g"] = torch.from_numpy((norm * g.numpy().reshape(-1)).reshape(g.shape).astype(np.float32))
+        elif name.endswith(".weight_g"):
+            sd[name] = torch.from_numpy(rng.uniform(0.8, 1.2, size=shape).astype(np.float32))
+        elif name.endswith(".bias") and (".stack.2." in name or ".norm_layer." in name):
+            sd[name] = torch.from_numpy((0.1 * rng.standard_normal(shape)).astype(np.float32))
+        elif name.endswith(".weight") and (".stack.2." in name or ".norm_layer." in name):
+            sd[name] = torch.from_numpy((1.0 + 0.1 * rng.standard_normal(shape)).astype(np.float32))
+        elif name.endswith(".bias"):
+            sd[name] = torch.from_numpy(rng.uniform(-0.05, 0.05, size=shape).astype(np.float32))
+        elif name == "embeds._embedding.weight":
+            sd[name] = torch.from_numpy(rng.standard_normal(shape).astype(np.float32))
+        else:
+            raise KeyError(name)
+    K, D = cfg.get("z_num", 512), cfg.get("z_dim", 128)
+    sd["quantizer.emb_init"] = torch.tensor(False)
+    sd["quantizer.emb_sum"] = torch.zeros(K, D)
+    sd["quantizer.emb_elem"] = torch.ones(K)
+    sd["quantizer.embeddings"] = torch.zeros(K, D)
+    del pending_v
+    return sd
+
+
+def seeded_batch(cfg, B, T, seed):
+    """Synthetic CMVN-like mel batch x ~ N(0,1) (B, mel, T) f32 and speaker ids
+    y (B, 1) int64 (the utt2mel_spk.py:42-74 contract)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    mel = cfg["encoder"]["in_channels"][0]
+    x = rng.standard_normal((B, mel, T)).astype(np.float32)
+    y = rng.integers(0, cfg.get("y_num", 10), size=(B, 1)).astype(np.int64)
+    return torch.from_numpy(x), torch.from_numpy(y)
+
+
+# ----------------------------------------------------------------- the model
+class OracleVQVAE:
+    """Functional restatement of vae_npvc.model.vqvae.Model with the EMA
+    quantizer (use_ema: true).  Parameters are CPU fp32 leaf tensors keyed by
+    the reference state_dict names."""
+
+    def __init__(self, cfg, state_dict):
+        self.cfg = cfg
+        self.params = OrderedDict()
+        for name, shape in layer_specs(cfg):
+            t = state_dict[name].detach().clone().float().contiguous()
+            assert tuple(t.shape) == tuple(shape), (name, t.shape, shape)
+            self.params[name] = t.requires_grad_(True)
+        self.emb_init = bool(state_dict["quantizer.emb_init"])
+        self.emb_sum = state_dict["quantizer.emb_sum"].clone().float()
+        self.emb_elem = state_dict["quantizer.emb_elem"].clone().float()
+        self.embeddings = state_dict["quantizer.embeddings"].clone().float()
+        self.mu = cfg.get("mu", 0.9)
+        self.beta = cfg.get("beta", 0.01)
+        self.jitter_p = cfg.get("jitter_p", 0.0)
+        self.K, self.D = cfg.get("z_num", 512), cfg.get("z_dim", 128)
+        self.threshold = 1.0
+        self.ns = cfg["encoder"]["stacks"][0]
+        self.nd = cfg["decoder"]["stacks"][0]
+        self.training = True
+        self.last = {}
+
+    def state_dict(self):
+        sd = OrderedDict((k, v.detach().clone()) for k, v in self.params.items())
+        sd["quantizer.emb_init"] = torch.tensor(self.emb_init)
+        sd["quantizer.emb_sum"] = self.emb_sum.clone()
+        sd["quantizer.emb_elem"] = self.emb_elem.clone()
+        sd["quantizer.embeddings"] = self.embeddings.clone()
+        return sd
+
+    # nn.utils.weight_norm pre-hook, torch._weight_norm(v, g, dim=0)
+    def _w(self, name):
+        return torch._weight_norm(self.params[name + ".weight_v"], self.params[name + ".weight_g"], 0)
+
+    def _conv(self, x, name, pad, transposed=False):
+        f = F.conv_transpose1d if transposed else F.conv1d
+        return f(x, self._w(name), self.params[name + ".bias"], padding=pad)
+
+    # vqvae.py:185-192 with the Sequential of :144-176; block layers.py:168-178
+    def encoder(self, x):
+        p = self.params
+        h = self._conv(x, "encoder.encode.0", 1)
+        for i in range(1, self.ns + 1):
+            pre = f"encoder.encode.{i}"
+            a = F.leaky_relu(h, 0.2)
+            a = self._conv(a, pre + ".stack.1", 1)
+            a = F.group_norm(a, 1, p[pre + ".stack.2.weight"], p[pre + ".stack.2.bias"], 1e-5)
+            h = a + self._conv(h, pre + ".skip_layer", 0)
+        h = F.leaky_relu(h, 0.2)
+        return self._conv(h, f"encoder.encode.{self.ns + 2}", 0)
+
+    # vqvae.py:298-318; block layers.py:218-249
+    def decoder(self, zq, c):
+        p = self.params
+        x = self._conv(zq, "decoder.layers.0", 1, transposed=True)
+        T = x.size(2)
+        c = c[:, :, :1]
+        x_out = 0.0
+        Cd = x.size(1)
+        for i in range(1, self.nd + 1):
+            pre = f"decoder.layers.{i}"
+            xr = self._conv(x, pre + ".conv_in", 1, transposed=True)
+            xc = self._conv(c.repeat(1, 1, T), pre + ".conv_cond", 0)
+            h = F.group_norm(xr + xc, 2, p[pre + ".norm_layer.weight"], p[pre + ".norm_layer.bias"], 1e-5)
+            g = torch.tanh(h[:, :Cd]) * torch.sigmoid(h[:, Cd:])
+            r = self._conv(g, pre + ".res_skip_layers", 0)
+            x = r[:, :Cd, :] + x
+            x_out += r[:, Cd:, :]
+        x = x_out * math.sqrt(1.0 / (self.nd + 1))
+        x = F.relu(x)
+        x = self._conv(x, "decoder.final_layer.1", 0)
+        x = F.relu(x)
+        return self._conv(x, "decoder.final_layer.3", 0)
+
+    # ---- EMAVectorQuantizer (layers_vq.py:166-334)
+    def _tile(self, z):  # layers_vq.py:183-190
+        n, d = z.shape
+        if n < self.K:
+            rep = (self.K + n - 1) // n
+            std = 0.01 / np.sqrt(d)
+            z = z.repeat(rep, 1)
+            z = z + torch.randn_like(z) * std
+        return z
+
+    def init_emb(self, z):  # layers_vq.py:192-201
+        self.emb_init = not self.emb_init
+        _z = self._tile(z)
+        self.embeddings = _z[torch.randperm(_z.shape[0])][: self.K]
+        self.emb_sum = self.embeddings.clone()
+        self.emb_elem = torch.ones(self.K)
+
+    def update_emb(self, z, idx):  # layers_vq.py:203-233
+        mu, K, D = self.mu, self.K, self.D
+        with torch.no_grad():
+            onehot = torch.zeros(K, z.shape[0])
+            onehot.scatter_(0, idx.view(1, z.shape[0]), 1)
+            s = torch.matmul(onehot, z)
+            n = onehot.sum(dim=-1)
+            _z = self._tile(z)
+            rand = _z[torch.randperm(_z.shape[0])][:K]
+            old = self.embeddings.clone()
+            self.emb_sum = mu * self.emb_sum + (1.0 - mu) * s
+            self.emb_elem = mu * self.emb_elem + (1.0 - mu) * n
+            usage = (self.emb_elem.view(K, 1) >= self.threshold).float()
+            self.embeddings = usage * (self.emb_sum.view(K, D) / self.emb_elem.view(K, 1)) + (1 - usage) * rand
+            kp = n / torch.sum(n)
+            entropy = torch.exp(-torch.sum(kp * torch.log(kp + 1e-8)))
+            used_curr = (n >= self.threshold).sum()
+            usage = torch.sum(usage)
+            dk = torch.norm(self.embeddings - old) / np.sqrt(np.prod(old.shape))
+        return {"entropy": entropy.item(), "used_curr": used_curr.item(), "usage": usage.item(), "diff_emb": dk.item()}
+
+    def distances(self, zf, E):  # layers_vq.py:285-289
+        return (torch.sum(zf.pow(2), dim=1, keepdim=True) + torch.sum(E.pow(2), dim=1) - 2 * torch.matmul(zf, E.t()))
+
+    def quantize(self, z):  # layers_vq.py:268-323 (reduction 'frame_mean')
+        B, D, T = z.shape
+        zf = z.transpose(1, 2).contiguous().view(-1, D)
+        if not self.emb_init and self.training:
+            self.init_emb(zf)
+        with torch.no_grad():
+            dist = self.distances(zf, self.embeddings)
+            idx = torch.argmin(dist, dim=1)
+            zq = self.embeddings.index_select(dim=0, index=idx)
+        self.last["idx"] = idx.detach().clone()
+        self.last["dist"] = dist
+        detail = self.update_emb(zf, idx) if self.training else {}
+        enc_loss = F.mse_loss(zq.detach(), zf, reduction="none").sum() / (B * T)
+        zq = zq.view(B, T, D).transpose(1, 2).contiguous()
+        return zq, 0.0, enc_loss, detail
+
+    def encode(self, x):  # vqvae.py:45-52 / layers_vq.py:236-252
+        z = self.encoder(x)
+        B, D, T = z.shape
+        zf = z.transpose(1, 2).contiguous().view(-1, D)
+        return torch.argmin(self.distances(zf, self.embeddings), dim=1).view(B, T)
+
+    def decode(self, z_idx, y_idx):  # vqvae.py:55-60 / layers_vq.py:255-265
+        y = F.embedding(y_idx, self.params["embeds._embedding.weight"]).transpose(1, 2).contiguous()
+        B, T = z_idx.shape
+        zq = self.embeddings.index_select(0, z_idx.flatten()).view(B, T, -1).transpose(1, 2).contiguous()
+        return self.decoder(zq, y)
+
+    def jitter(self, zq):  # layers_vq.py:353-379 (replaces with probability 1-p: the reference's quirk)
+        p = self.jitter_p
+        if p == 0.0 or not self.training:
+            return zq
+        orig = zq.detach().clone()
+        L = orig.size(2)
+        for i in range(L):
+            replace = [True, False][np.random.choice([1, 0], p=[p, 1 - p])]
+            if replace:
+                if i == 0:
+                    nb = i + 1
+                elif i == L - 1:
+                    nb = i - 1
+                else:
+                    nb = i + np.random.choice([-1, 1], p=[0.5, 0.5])
+                zq[:, :, i] = orig[:, :, nb]
+        return zq
+
+    def forward(self, x, y_idx):  # vqvae.py:70-90
+        y = F.embedding(y_idx, self.params["embeds._embedding.weight"]).transpose(1, 2).contiguous()
+        z = self.encoder(x)
+        self.last["z"] = z
+        zq, zq_loss, enc_loss, detail = self.quantize(z)
+        zq = self.jitter(zq)
+        xhat = self.decoder(zq, y)
+        B, D, T = x.shape
+        x_loss = (0.5 * (LOG_2PI + (xhat - x).pow(2))).sum() / (B * T)  # layers.py:283-296
+        loss = x_loss + zq_loss + self.beta * enc_loss
+        losses = {"Total": loss.item(), "VQ loss": enc_loss.item(), "X like": x_loss.item()}
+        losses.update(detail)
+        return xhat, loss, losses
+
+
+class OracleTrainer:
+    """Trainer.train_step (trainer/basic.py:55-79) on CPU: zero_grad, forward,
+    backward, clip_grad_norm_, Adam(betas=(0.5, 0.999), wd 0), StepLR."""
+
+    def __init__(self, cfg, state_dict):
+        self.model = OracleVQVAE(cfg, state_dict)
+        params = list(self.model.params.values())
+        self.max_grad_norm = cfg.get("max_grad_norm", 5)
+        self.optimizer = torch.optim.Adam(params, lr=cfg.get("learning_rate", 1e-3), betas=(0.5, 0.999),
+                                          weight_decay=0.0)
+        self.scheduler = None
+        if cfg.get("lr_scheduler", None) is not None:
+            lp = cfg.get("lr_param", {"step_size": 100000, "gamma": 0.5, "last_epoch": -1})
+            self.scheduler = torch.optim.lr_scheduler.StepLR(optimizer=self.optimizer, **lp)
+        self.iteration = 0
+        self.grads = None
+
+    def train_step(self, batch, keep_grads=False):
+        for p in self.model.params.values():
+            p.grad = None
+        x, y = batch
+        xhat, loss, detail = self.model.forward(x, y)
+        loss.backward()
+        if keep_grads:
+            self.grads = OrderedDict((k, v.grad.detach().clone()) for k, v in self.model.params.items())
+        if self.max_grad_norm > 0:
+            torch.nn.utils.clip_grad_norm_(list(self.model.params.values()), self.max_grad_norm)
+        self.optimizer.step()
+        if self.scheduler is not None:
+            self.scheduler.step()
+        self.iteration += 1
+        self.last_xhat = xhat.detach()
+        return self.iteration, detail

@@ -1,0 +1,150 @@
+"""Kernel-level parity of libvqx against plain PyTorch fp32/fp64 references of
+the same ops (conv fwd / dgrad / wgrad, ConvTranspose packing, VQ argmin).
+Runs on the MI355X only (-m gpu)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _ops():
+    from vae_npvc_amd import ops
+    return ops
+
+
+def ref_conv(x_ntc, w, B, T, pad, pro=None):
+    x = x_ntc.double().view(B, T, -1).permute(0, 2, 1)
+    if pro == "lrelu":
+        x = F.leaky_relu(x, 0.2)
+    elif pro == "relu":
+        x = F.relu(x)
+    y = F.conv1d(x, w.double(), padding=pad)
+    return y.permute(0, 2, 1).reshape(B * T, -1)
+
+
+def pack(w):  # Conv1d weight [cout, cin, k] -> [cout, k*cin]
+    cout, cin, k = w.shape
+    return w.permute(0, 2, 1).reshape(cout, k * cin).contiguous()
+
+
+TOL = {torch.float32: 2e-5, torch.bfloat16: 2e-2}
+
+
+def relerr(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cin,cout,k,pro", [(80, 512, 3, None), (512, 512, 3, "lrelu"), (512, 128, 1, "lrelu"),
+                                            (128, 80, 1, "relu"), (512, 640, 1, None), (512, 1024, 3, None)])
+def test_conv_fwd(dtype, cin, cout, k, pro):
+    ops = _ops()
+    from vae_npvc_amd import _lib as L
+    torch.manual_seed(0)
+    B, T = 3, 64
+    x = torch.randn(B * T, cin, device=DEV).to(dtype)
+    w = (torch.randn(cout, cin, k, device=DEV) / (cin * k) ** 0.5)
+    bias = torch.randn(cout, device=DEV)
+    y = torch.empty(B * T, cout, device=DEV, dtype=torch.float32)
+    proc = {None: L.PRO_NONE, "lrelu": L.PRO_LRELU, "relu": L.PRO_RELU}[pro]
+    ops.conv_fwd(x, pack(w).to(dtype), y, T=T, cin=cin, cout=cout, ntaps=k, pad=(k - 1) // 2, prologue=proc,
+                 bias=bias, out_f32=True)
+    torch.cuda.synchronize()
+    ref = ref_conv(x.float().cpu(), pack(w).to(dtype).float().cpu().view(cout, k, cin).permute(0, 2, 1), B, T,
+                   (k - 1) // 2, pro) + bias.double().cpu()
+    assert relerr(y, ref) < TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cin,cout,k", [(512, 512, 3), (512, 128, 1), (128, 80, 1), (512, 1024, 3), (80, 512, 3)])
+def test_conv_dgrad_wgrad(dtype, cin, cout, k):
+    ops = _ops()
+    torch.manual_seed(1)
+    B, T = 2, 128
+    pad = (k - 1) // 2
+    x = torch.randn(B * T, cin, device=DEV).to(dtype)
+    dy = torch.randn(B * T, cout, device=DEV).to(dtype)
+    w = (torch.randn(cout, cin, k, device=DEV) / (cin * k) ** 0.5).to(dtype).float()
+    # reference via autograd in fp64
+    xr = x.double().cpu().view(B, T, cin).permute(0, 2, 1).clone().requires_grad_(True)
+    wr = w.double().cpu().clone().requires_grad_(True)
+    yr = F.conv1d(xr, wr, padding=pad)
+    yr.backward(dy.double().cpu().view(B, T, cout).permute(0, 2, 1))
+    dx_ref = xr.grad.permute(0, 2, 1).reshape(B * T, cin)
+    dw_ref = pack(wr.grad)
+    if cin % 8 == 0:
+        dx = torch.empty(B * T, cin, device=DEV, dtype=torch.float32)
+        ops.conv_dgrad(dy, pack(w).to(dtype), dx, T=T, cin=cout, cout=cin, ntaps=k, pad=pad, out_f32=True)
+        torch.cuda.synchronize()
+        assert relerr(dx, dx_ref) < TOL[dtype]
+    splits = 3
+    slabs = torch.empty(splits, cout, k * cin, device=DEV)
+    ops.conv_wgrad(dy, x, slabs, T=T, r_dim=cout, c_dim=cin, ntaps=k, pad=pad, splits=splits)
+    torch.cuda.synchronize()
+    assert relerr(slabs.sum(0), dw_ref) < TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_convtranspose_via_weight_norm_pack(dtype):
+    """ConvTranspose1d(cin->cout, k3, p1) through the weight-norm pack kernel
+    (dim 0 = in-channels) and the conv GEMM, fwd + wgrad(sign -1)."""
+    ops = _ops()
+    torch.manual_seed(2)
+    B, T, cin, cout, k = 2, 64, 128, 512, 3
+    v = torch.randn(cin, cout, k, device=DEV)
+    g = torch.rand(cin, device=DEV) + 0.5
+    wp = torch.empty(cout, k * cin, device=DEV, dtype=dtype)
+    norm = torch.empty(cin, device=DEV)
+    tab = ops.wn_table([dict(v=v, g=g, w_packed=wp, norm=norm, kind=1, cout=cout, cin=cin, k=k,
+                             dtype=ops.dt_code(dtype))])
+    ops.weight_norm_fwd(tab)
+    x = torch.randn(B * T, cin, device=DEV).to(dtype)
+    y = torch.empty(B * T, cout, device=DEV)
+    ops.conv_fwd(x, wp, y, T=T, cin=cin, cout=cout, ntaps=k, pad=1, out_f32=True)
+    torch.cuda.synchronize()
+    wt = torch._weight_norm(v.cpu().double(), g.cpu().double().view(cin, 1, 1), 0)
+    xr = x.double().cpu().view(B, T, cin).permute(0, 2, 1).clone().requires_grad_(True)
+    wr = wt.clone().requires_grad_(True)
+    yr = F.conv_transpose1d(xr, wr, padding=1)
+    assert relerr(y, yr.detach().permute(0, 2, 1).reshape(B * T, cout)) < TOL[dtype]
+    du = torch.randn(B * T, cout, device=DEV).to(dtype)
+    yr.backward(du.double().cpu().view(B, T, cout).permute(0, 2, 1))
+    slabs = torch.empty(2, cin, k * cout, device=DEV)
+    ops.conv_wgrad(x, du, slabs, T=T, r_dim=cin, c_dim=cout, ntaps=k, pad=1, shift_sign=-1, splits=2)
+    torch.cuda.synchronize()
+    # slab[ci][j'*cout + co] = dW[ci][co][k-1-j']
+    dwt = slabs.sum(0).view(cin, k, cout).permute(0, 2, 1).flip(-1)
+    assert relerr(dwt, wr.grad) < TOL[dtype]
+
+
+@pytest.mark.parametrize("K", [128, 512, 1024])
+def test_vq_argmin_exact(K):
+    ops = _ops()
+    torch.manual_seed(3)
+    N, D = 4096, 128
+    z = torch.randn(N, D)
+    E = torch.randn(K, D)
+    dist = (z.pow(2).sum(1, keepdim=True) + E.pow(2).sum(1)) - 2 * z @ E.t()
+    ref = dist.argmin(1)
+    zd, Ed = z.to(DEV), E.to(DEV)
+    idx = torch.empty(N, dtype=torch.int64, device=DEV)
+    zq = torch.empty(N, D, device=DEV)
+    zqc = torch.empty(N, D, device=DEV, dtype=torch.bfloat16)
+    sq = torch.zeros(1, device=DEV)
+    part = torch.empty((N + 63) // 64, device=DEV)
+    bsum = torch.zeros(K, D, device=DEV)
+    bcnt = torch.zeros(K, device=DEV)
+    ops.vq_forward(zd, Ed, idx, zq, zqc, sq, part, bsum, bcnt)
+    torch.cuda.synchronize()
+    idx = idx.cpu()
+    assert (idx == ref).float().mean().item() == 1.0, (idx != ref).sum()
+    assert torch.equal(zq.cpu(), E[ref])
+    sq_ref = (E[ref] - z).pow(2).sum()
+    assert abs(sq.item() - sq_ref.item()) / sq_ref.item() < 1e-5
+    onehot = F.one_hot(ref, K).float()
+    assert torch.allclose(bcnt.cpu(), onehot.sum(0))
+    assert torch.allclose(bsum.cpu(), onehot.t() @ z, atol=1e-4, rtol=1e-5)

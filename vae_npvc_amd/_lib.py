@@ -1,0 +1,141 @@
+"""ctypes binding of libvqx.so (the C ABI declared in include/vqx.h).
+
+The product path has no fallback: if the shared library is missing or was
+built for another ABI, importing the ops raises.  Build it with
+``python -m vae_npvc_amd.csrc.build`` (``__graft_entry__.build()`` does).
+
+torch must be imported before the library is loaded so that libvqx.so binds
+to the HIP runtime torch already loaded (same SONAME, one runtime per
+process, shared streams and allocations).
+"""
+import ctypes
+import os
+from pathlib import Path
+
+import torch  # noqa: F401  (loads the HIP runtime first; see module docstring)
+
+LIB_PATH = Path(__file__).resolve().parent / "lib" / "libvqx.so"
+ABI_VERSION = 100
+
+VQX_F32, VQX_BF16 = 0, 1
+PRO_NONE, PRO_LRELU, PRO_RELU, PRO_SCALE_RELU = 0, 1, 2, 3
+EPI_BIAS, EPI_ROWBIAS, EPI_MASK, EPI_RES, EPI_GNADD, EPI_SPLIT, EPI_OUTF32 = (1 << i for i in range(7))
+
+c_void_p, c_int32, c_int64, c_float, c_double = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
+                                                 ctypes.c_float, ctypes.c_double)
+
+
+class ConvArgs(ctypes.Structure):
+    _fields_ = [
+        ("x", c_void_p), ("w", c_void_p), ("y", c_void_p), ("bias", c_void_p), ("rowbias", c_void_p),
+        ("res", c_void_p), ("mask", c_void_p), ("gn_h", c_void_p), ("gn_mean_rstd", c_void_p),
+        ("gn_gamma", c_void_p), ("gn_beta", c_void_p), ("out2", c_void_p),
+        ("n_rows", c_int64), ("T", c_int32), ("cin", c_int32), ("cout", c_int32), ("ntaps", c_int32),
+        ("pad", c_int32), ("ldx", c_int32), ("ldy", c_int32), ("ldres", c_int32), ("ldmask", c_int32),
+        ("ldgn", c_int32), ("ldo2", c_int32), ("dtype", c_int32), ("prologue", c_int32),
+        ("epilogue", c_int32), ("split_col", c_int32), ("out2_accumulate", c_int32),
+        ("pro_scale", c_float), ("mask_slope", c_float), ("mask_scale", c_float),
+    ]
+
+
+class WgradArgs(ctypes.Structure):
+    _fields_ = [
+        ("p", c_void_p), ("q", c_void_p), ("slabs", c_void_p), ("n_rows", c_int64), ("T", c_int32),
+        ("r_dim", c_int32), ("c_dim", c_int32), ("ntaps", c_int32), ("pad", c_int32),
+        ("shift_sign", c_int32), ("ldp", c_int32), ("ldq", c_int32), ("dtype", c_int32),
+        ("q_prologue", c_int32), ("splits", c_int32), ("pro_scale", c_float),
+    ]
+
+
+class WNLayer(ctypes.Structure):
+    _fields_ = [
+        ("v", c_void_p), ("g", c_void_p), ("w_packed", c_void_p), ("norm", c_void_p), ("dv", c_void_p),
+        ("dg", c_void_p), ("slabs", c_void_p), ("kind", c_int32), ("cout", c_int32), ("cin", c_int32),
+        ("k", c_int32), ("splits", c_int32), ("dtype", c_int32),
+    ]
+
+
+# name -> argtypes (restype is int for every entry point except the two below)
+_SIGS = {
+    "vqx_conv1d_fwd": [ctypes.POINTER(ConvArgs), c_void_p],
+    "vqx_conv1d_dgrad": [ctypes.POINTER(ConvArgs), c_void_p],
+    "vqx_conv1d_wgrad": [ctypes.POINTER(WgradArgs), c_void_p],
+    "vqx_weight_norm_fwd": [c_void_p, c_void_p, c_int32, c_void_p],
+    "vqx_weight_norm_bwd": [c_void_p, c_void_p, c_int32, c_void_p],
+    "vqx_groupnorm_stats": [c_void_p, c_int32, c_int32, c_int64, c_int32, c_int32, c_int32, c_float, c_void_p,
+                            c_void_p, c_void_p],
+    "vqx_gn_glu_fwd": [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int64, c_int32, c_int32, c_void_p,
+                       c_void_p, c_void_p, c_void_p],
+    "vqx_gn_bwd": [c_void_p, c_int32, c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int64, c_int32, c_int32,
+                   c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                   c_void_p],
+    "vqx_colsum": [c_void_p, c_int32, c_int32, c_int64, c_int32, c_void_p, c_void_p, c_int32, c_void_p],
+    "vqx_nct_to_ntc": [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_int32, c_int32, c_void_p],
+    "vqx_ntc_to_nct": [c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p],
+    "vqx_logloss_fwd_bwd": [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_float, c_void_p, c_int32,
+                            c_int32, c_void_p, c_void_p, c_void_p],
+    "vqx_vq_forward": [c_void_p, c_int64, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_int32,
+                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "vqx_vq_ema_update": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_float,
+                          c_float, c_void_p, c_void_p],
+    "vqx_gather_rows": [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_void_p, c_void_p],
+    "vqx_vq_commit_bwd": [c_void_p, c_void_p, c_int64, c_float, c_void_p, c_int32, c_void_p],
+    "vqx_time_gather": [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_int32, c_void_p],
+    "vqx_embedding_fwd": [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p],
+    "vqx_embedding_bwd": [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p],
+    "vqx_linear_f32": [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p],
+    "vqx_linear_bwd_f32": [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p],
+    "vqx_grad_sq_norm": [c_void_p, c_int64, c_void_p, c_void_p, c_void_p],
+    "vqx_adam_hyper": [c_void_p, c_double, c_double, c_int32, c_double, c_double, c_double, c_void_p, c_void_p],
+    "vqx_adam_step": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_float, c_void_p],
+}
+EXPORTS = tuple(_SIGS) + ("vqx_last_error", "vqx_version")
+
+
+class VqxError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(path: os.PathLike = LIB_PATH):
+    """Load libvqx.so once; raise if it is absent (no CPU fallback exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = Path(path)
+    if not path.exists():
+        raise VqxError(f"libvqx.so not found at {path}; build it with `python -m vae_npvc_amd.csrc.build` "
+                       "(the HIP kernels are the only implementation of this path)")
+    lib = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
+    for name, argtypes in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = ctypes.c_int
+    lib.vqx_last_error.restype = ctypes.c_char_p
+    lib.vqx_last_error.argtypes = []
+    lib.vqx_version.restype = ctypes.c_int
+    lib.vqx_version.argtypes = []
+    if lib.vqx_version() != ABI_VERSION:
+        raise VqxError(f"libvqx ABI {lib.vqx_version()} != expected {ABI_VERSION}; rebuild")
+    _lib = lib
+    return lib
+
+
+def call(name: str, *args):
+    """Invoke an entry point and turn a non-zero status into VqxError."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        raise VqxError(f"{name} failed ({rc}): {lib.vqx_last_error().decode(errors='replace')}")
+    return rc
+
+
+def stream_ptr() -> int:
+    """hipStream_t of torch's current stream on the current device."""
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()

@@ -1,0 +1,69 @@
+// Shared device helpers for libvqx (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/vqx.h"
+
+typedef unsigned short bf16_t;  // storage type of bf16 activations/weights
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+#define VQX_LDS(T) __attribute__((address_space(3))) T
+
+namespace vqx {
+
+void set_error(const char* fmt, ...);
+int launch_status(const char* what);
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((unsigned)v) << 16); }
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32: round-to-nearest-even, NaN-preserving
+  return *reinterpret_cast<bf16_t*>(&b);
+}
+
+template <typename T> struct Elem;
+template <> struct Elem<float> {
+  __device__ static __forceinline__ float ld(const void* p, int64_t i) { return ((const float*)p)[i]; }
+  __device__ static __forceinline__ void st(void* p, int64_t i, float v) { ((float*)p)[i] = v; }
+};
+template <> struct Elem<bf16_t> {
+  __device__ static __forceinline__ float ld(const void* p, int64_t i) { return bf2f(((const bf16_t*)p)[i]); }
+  __device__ static __forceinline__ void st(void* p, int64_t i, float v) { ((bf16_t*)p)[i] = f2bf(v); }
+};
+
+__device__ __forceinline__ float ld_dt(const void* p, int64_t i, int dt) {
+  return dt == VQX_BF16 ? bf2f(((const bf16_t*)p)[i]) : ((const float*)p)[i];
+}
+__device__ __forceinline__ void st_dt(void* p, int64_t i, float v, int dt) {
+  if (dt == VQX_BF16) ((bf16_t*)p)[i] = f2bf(v); else ((float*)p)[i] = v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block-wide sum (blockDim.x multiple of 64, <= 1024); result valid in all threads.
+__device__ __forceinline__ float block_sum(float v, float* scratch /* >= 16 floats */) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (l == 0) scratch[w] = v;
+  __syncthreads();
+  float s = 0.f;
+  for (int i = 0; i < nw; ++i) s += scratch[i];  // fixed order: deterministic
+  return s;
+}
+
+// Bijective XCD-aware remap of a linear block id (guide §5 "XCD swizzle must
+// be bijective"): blocks b and b+8 share an XCD, so give each XCD group a
+// contiguous range of logical tiles.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, x = bid % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
+}  // namespace vqx

@@ -1,0 +1,702 @@
+// Weight norm, GroupNorm (+gated unit), layout, loss, embedding and optimizer
+// kernels of the VQ-VAE training step (gfx950).  All reductions are
+// deterministic fixed-shape trees (no float atomics), so a step is bitwise
+// reproducible apart from the EMA scatter statistics of vq_forward.
+#include "vqx_common.h"
+#include <math.h>
+
+namespace vqx {
+
+constexpr float kLog2Pi = 1.8378770664093453f;  // log(2*pi), layers.py:8
+
+// ------------------------------------------------------------- weight norm
+// torch.nn.utils.weight_norm(dim=0): w = v * (g / ||v||), norm over all dims
+// but 0.  Conv1d: v[cout][cin][k], row o = co.  ConvT: v[cin][cout][k], row
+// o = ci, effective tap j' = k-1-j.  Packed effective weight:
+// wp[co][j*cin + ci].
+__global__ __launch_bounds__(256) void wn_norm_kernel(const vqx_wn_layer* __restrict__ L, int n_layers) {
+  const vqx_wn_layer& l = L[blockIdx.y];
+  const int rows = l.kind == 0 ? l.cout : l.cin;
+  const int cols = (l.kind == 0 ? l.cin : l.cout) * l.k;
+  const int o = blockIdx.x;
+  if (o >= rows) return;
+  __shared__ float red[16];
+  const float* v = l.v + (int64_t)o * cols;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < cols; i += blockDim.x) s = fmaf(v[i], v[i], s);
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) l.norm[o] = sqrtf(s);
+}
+
+__global__ __launch_bounds__(256) void wn_pack_kernel(const vqx_wn_layer* __restrict__ L, int n_layers) {
+  const vqx_wn_layer& l = L[blockIdx.y];
+  const int64_t total = (int64_t)l.cout * l.cin * l.k;
+  const int K = l.k, cin = l.cin, cout = l.cout;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    // e indexes wp[co][j][ci]
+    const int ci = (int)(e % cin);
+    const int64_t r = e / cin;
+    const int j = (int)(r % K);
+    const int co = (int)(r / K);
+    float w;
+    if (l.kind == 0) {
+      const float sc = l.g[co] / l.norm[co];
+      w = l.v[((int64_t)co * cin + ci) * K + j] * sc;
+    } else {
+      const float sc = l.g[ci] / l.norm[ci];
+      w = l.v[((int64_t)ci * cout + co) * K + (K - 1 - j)] * sc;
+    }
+    st_dt(l.w_packed, e, w, l.dtype);
+  }
+}
+
+// Backward per weight-norm row o.  slabs[s][o][x] with x = j*cin+ci (Conv1d,
+// row co) or x = j'*cout+co (ConvT, row ci); dW of the effective conv.
+__global__ __launch_bounds__(256) void wn_bwd_kernel(const vqx_wn_layer* __restrict__ L, int n_layers) {
+  const vqx_wn_layer& l = L[blockIdx.y];
+  const int rows = l.kind == 0 ? l.cout : l.cin;
+  const int o = blockIdx.x;
+  if (o >= rows) return;
+  const int other = l.kind == 0 ? l.cin : l.cout;
+  const int K = l.k;
+  const int cols = other * K;
+  __shared__ float dw[4096];
+  __shared__ float red[16];
+  const int64_t slab_stride = (int64_t)rows * cols;
+  const float* v = l.v + (int64_t)o * cols;
+  float dot = 0.f;
+  for (int x = threadIdx.x; x < cols; x += blockDim.x) {
+    float s = 0.f;
+    for (int sp = 0; sp < l.splits; ++sp) s += l.slabs[sp * slab_stride + (int64_t)o * cols + x];
+    // slab col x = j*other + c  -> v index c*K + (kind==0 ? j : K-1-j)
+    const int j = x / other, c = x - j * other;
+    const int vi = c * K + (l.kind == 0 ? j : K - 1 - j);
+    dw[vi] = s;
+    dot = fmaf(s, v[vi], dot);
+  }
+  dot = block_sum(dot, red);  // includes __syncthreads: dw[] complete
+  const float nrm = l.norm[o];
+  const float gg = l.g[o];
+  const float dg = dot / nrm;
+  if (threadIdx.x == 0) l.dg[o] = dg;
+  const float sc = gg / nrm, t = dg / nrm;
+  for (int i = threadIdx.x; i < cols; i += blockDim.x) l.dv[(int64_t)o * cols + i] = sc * (dw[i] - v[i] * t);
+}
+
+// --------------------------------------------------------------- groupnorm
+// Partial moments per (b, g, part): two-pass within the part (mean, then
+// centred sum of squares), combined with Chan's formula in finalize.
+constexpr int kGnParts = 8;
+
+template <typename T>
+__global__ __launch_bounds__(256) void gn_partial_kernel(const T* __restrict__ x, int ldx, int T_, int C, int G,
+                                                         float* __restrict__ part) {
+  const int p = blockIdx.x, bg = blockIdx.y;
+  const int b = bg / G, g = bg - b * G;
+  const int cg = C / G;
+  const int r0 = p * T_ / kGnParts, r1 = (p + 1) * T_ / kGnParts;
+  const int64_t nrows = r1 - r0;
+  const int64_t cnt = nrows * cg;
+  __shared__ float red[16];
+  const T* base = x + ((int64_t)b * T_ + r0) * ldx + g * cg;
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < cnt; i += blockDim.x) {
+    const int64_t rr = i / cg, cc = i - rr * cg;
+    s += Elem<T>::ld(base, rr * ldx + cc);
+  }
+  s = block_sum(s, red);
+  const float mean = cnt ? s / (float)cnt : 0.f;
+  float m2 = 0.f;
+  for (int64_t i = threadIdx.x; i < cnt; i += blockDim.x) {
+    const int64_t rr = i / cg, cc = i - rr * cg;
+    const float d = Elem<T>::ld(base, rr * ldx + cc) - mean;
+    m2 = fmaf(d, d, m2);
+  }
+  m2 = block_sum(m2, red);
+  if (threadIdx.x == 0) {
+    float* o = part + ((int64_t)bg * kGnParts + p) * 3;
+    o[0] = (float)cnt;
+    o[1] = mean;
+    o[2] = m2;
+  }
+}
+
+__global__ void gn_finalize_kernel(const float* __restrict__ part, int nbg, float eps, float* __restrict__ mr) {
+  const int bg = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bg >= nbg) return;
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  for (int p = 0; p < kGnParts; ++p) {
+    const float* o = part + ((int64_t)bg * kGnParts + p) * 3;
+    const double nb = o[0];
+    if (nb == 0.0) continue;
+    const double d = (double)o[1] - mean;
+    const double nn = n + nb;
+    mean += d * nb / nn;
+    m2 += (double)o[2] + d * d * n * nb / nn;
+    n = nn;
+  }
+  const float var = n > 0.0 ? (float)(m2 / n) : 0.f;
+  mr[2 * bg] = (float)mean;
+  mr[2 * bg + 1] = 1.0f / sqrtf(var + eps);
+}
+
+// g = tanh(GN(u)[:, :half]) * sigmoid(GN(u)[:, half:]), GroupNorm with G=2.
+template <typename T>
+__global__ __launch_bounds__(256) void gn_glu_fwd_kernel(const T* __restrict__ u, int ldu, T* __restrict__ g, int ldg,
+                                                         int64_t n_rows, int T_, int half, const float* __restrict__ mr,
+                                                         const float* __restrict__ gamma, const float* __restrict__ beta) {
+  const int64_t total = n_rows * half;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t n = e / half;
+    const int c = (int)(e - n * half);
+    const int b = (int)(n / T_);
+    const float ua = Elem<T>::ld(u, n * ldu + c), ub = Elem<T>::ld(u, n * ldu + c + half);
+    const float ha = (ua - mr[4 * b + 0]) * mr[4 * b + 1] * gamma[c] + beta[c];
+    const float hb = (ub - mr[4 * b + 2]) * mr[4 * b + 3] * gamma[c + half] + beta[c + half];
+    const float sg = 1.f / (1.f + expf(-hb));
+    Elem<T>::st(g, n * ldg + c, tanhf(ha) * sg);
+  }
+}
+
+// dL/dh (gradient w.r.t. the GroupNorm output) of channel c at row n.
+template <typename T>
+__device__ __forceinline__ float gn_bwd_dh(const T* dy, int lddy, const T* u, int ldu, int64_t n, int c, int C,
+                                           int glu, int b, const float* mr, const float* gamma, const float* beta,
+                                           float* xhat_out) {
+  const int G = glu ? 2 : 0;  // glu implies G == 2
+  (void)G;
+  if (!glu) {
+    // caller supplies xhat via mr group 0..G-1 outside
+    return Elem<T>::ld(dy, n * lddy + c);
+  }
+  const int half = C / 2;
+  const int ca = c < half ? c : c - half;
+  const float ua = Elem<T>::ld(u, n * ldu + ca), ub = Elem<T>::ld(u, n * ldu + ca + half);
+  const float xa = (ua - mr[4 * b + 0]) * mr[4 * b + 1];
+  const float xb = (ub - mr[4 * b + 2]) * mr[4 * b + 3];
+  const float ha = xa * gamma[ca] + beta[ca];
+  const float hb = xb * gamma[ca + half] + beta[ca + half];
+  const float ta = tanhf(ha);
+  const float sb = 1.f / (1.f + expf(-hb));
+  const float dg = Elem<T>::ld(dy, n * lddy + ca);
+  if (c < half) {
+    *xhat_out = xa;
+    return dg * sb * (1.f - ta * ta);
+  }
+  *xhat_out = xb;
+  return dg * ta * (sb * (1.f - sb));
+}
+
+// pass 1: per (b, part) sums  S1_g = sum gamma*dh, S2_g = sum gamma*dh*xhat
+template <typename T>
+__global__ __launch_bounds__(256) void gn_bwd_reduce_kernel(const T* __restrict__ dy, int lddy, const T* __restrict__ u,
+                                                            int ldu, int T_, int C, int G, int glu,
+                                                            const float* __restrict__ mr, const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, float* __restrict__ part) {
+  const int p = blockIdx.x, b = blockIdx.y;
+  const int r0 = p * T_ / kGnParts, r1 = (p + 1) * T_ / kGnParts;
+  const int cg = C / G;
+  __shared__ float red[16];
+  for (int g = 0; g < G; ++g) {
+    float s1 = 0.f, s2 = 0.f;
+    const int64_t cnt = (int64_t)(r1 - r0) * cg;
+    for (int64_t i = threadIdx.x; i < cnt; i += blockDim.x) {
+      const int64_t rr = i / cg;
+      const int c = g * cg + (int)(i - rr * cg);
+      const int64_t n = (int64_t)b * T_ + r0 + rr;
+      float xh;
+      float dh;
+      if (glu) {
+        dh = gn_bwd_dh<T>(dy, lddy, u, ldu, n, c, C, 1, b, mr, gamma, beta, &xh);
+      } else {
+        dh = Elem<T>::ld(dy, n * lddy + c);
+        xh = (Elem<T>::ld(u, n * ldu + c) - mr[(b * G + g) * 2]) * mr[(b * G + g) * 2 + 1];
+      }
+      const float gd = gamma[c] * dh;
+      s1 += gd;
+      s2 = fmaf(gd, xh, s2);
+    }
+    s1 = block_sum(s1, red);
+    __syncthreads();
+    s2 = block_sum(s2, red);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float* o = part + (((int64_t)b * kGnParts + p) * G + g) * 2;
+      o[0] = s1;
+      o[1] = s2;
+    }
+  }
+}
+
+// pass 2: du and per-(b, c) column sums.  Block: one utterance b, 64 columns.
+template <typename T>
+__global__ __launch_bounds__(256) void gn_bwd_apply_kernel(const T* __restrict__ dy, int lddy, const T* __restrict__ u,
+                                                           int ldu, T* __restrict__ du, int lddu, int T_, int C, int G,
+                                                           int glu, const float* __restrict__ mr,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta,
+                                                           const float* __restrict__ part, float* __restrict__ colsum_b,
+                                                           float* __restrict__ dgamma_b, float* __restrict__ dbeta_b) {
+  const int b = blockIdx.y;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;  // 4 row groups
+  const int cg = C / G;
+  __shared__ float acc[3][4][64];
+  float s_du = 0.f, s_dgam = 0.f, s_dbet = 0.f;
+  if (c < C) {
+    const int g = c / cg;
+    float S1 = 0.f, S2 = 0.f;
+    for (int p = 0; p < kGnParts; ++p) {
+      const float* o = part + (((int64_t)b * kGnParts + p) * G + g) * 2;
+      S1 += o[0];
+      S2 += o[1];
+    }
+    const float M = (float)T_ * (float)cg;
+    const float m1 = S1 / M, m2 = S2 / M;
+    const float rstd = mr[(b * G + g) * 2 + 1];
+    const float mean = mr[(b * G + g) * 2];
+    const float gm = gamma[c];
+    for (int t = rg; t < T_; t += 4) {
+      const int64_t n = (int64_t)b * T_ + t;
+      float xh, dh;
+      if (glu) {
+        dh = gn_bwd_dh<T>(dy, lddy, u, ldu, n, c, C, 1, b, mr, gamma, beta, &xh);
+      } else {
+        dh = Elem<T>::ld(dy, n * lddy + c);
+        xh = (Elem<T>::ld(u, n * ldu + c) - mean) * rstd;
+      }
+      const float d = rstd * (gm * dh - m1 - xh * m2);
+      Elem<T>::st(du, n * lddu + c, d);
+      s_du += d;
+      s_dgam = fmaf(dh, xh, s_dgam);
+      s_dbet += dh;
+    }
+  }
+  acc[0][rg][threadIdx.x & 63] = s_du;
+  acc[1][rg][threadIdx.x & 63] = s_dgam;
+  acc[2][rg][threadIdx.x & 63] = s_dbet;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    const int l = threadIdx.x & 63;
+    const float a0 = acc[0][0][l] + acc[0][1][l] + acc[0][2][l] + acc[0][3][l];
+    const float a1 = acc[1][0][l] + acc[1][1][l] + acc[1][2][l] + acc[1][3][l];
+    const float a2 = acc[2][0][l] + acc[2][1][l] + acc[2][2][l] + acc[2][3][l];
+    if (colsum_b) colsum_b[(int64_t)b * C + c] = a0;
+    if (dgamma_b) dgamma_b[(int64_t)b * C + c] = a1;
+    if (dbeta_b) dbeta_b[(int64_t)b * C + c] = a2;
+  }
+}
+
+// ------------------------------------------------------------------ colsum
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const T* __restrict__ x, int ldx, int64_t n_rows, int C,
+                                                             int nparts, float* __restrict__ part) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  const int p = blockIdx.y;
+  const int64_t r0 = n_rows * p / nparts, r1 = n_rows * (p + 1) / nparts;
+  __shared__ float acc[4][64];
+  float s = 0.f;
+  if (c < C)
+    for (int64_t r = r0 + rg; r < r1; r += 4) s += Elem<T>::ld(x, r * ldx + c);
+  acc[rg][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    const int l = threadIdx.x & 63;
+    part[(int64_t)p * C + c] = acc[0][l] + acc[1][l] + acc[2][l] + acc[3][l];
+  }
+}
+
+__global__ void colsum_final_kernel(const float* __restrict__ part, int nparts, int C, float* __restrict__ out, int accum) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int p = 0; p < nparts; ++p) s += part[(int64_t)p * C + c];
+  out[c] = accum ? out[c] + s : s;
+}
+
+// ------------------------------------------------------------------ layout
+template <typename T>
+__global__ void nct_to_ntc_kernel(const float* __restrict__ x, int B, int C, int T_, T* __restrict__ y, int ldy) {
+  __shared__ float tile[32][33];
+  const int b = blockIdx.z;
+  const int t0 = blockIdx.x * 32, c0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 8 rows per pass
+  for (int i = ty; i < 32; i += 8) {
+    const int c = c0 + i, t = t0 + tx;
+    tile[i][tx] = (c < C && t < T_) ? x[((int64_t)b * C + c) * T_ + t] : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int t = t0 + i, c = c0 + tx;
+    if (c < C && t < T_) Elem<T>::st(y, ((int64_t)b * T_ + t) * ldy + c, tile[tx][i]);
+  }
+}
+
+template <typename T>
+__global__ void ntc_to_nct_kernel(const T* __restrict__ y, int ldy, int B, int C, int T_, float* __restrict__ x) {
+  __shared__ float tile[32][33];
+  const int b = blockIdx.z;
+  const int t0 = blockIdx.x * 32, c0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int i = ty; i < 32; i += 8) {
+    const int t = t0 + i, c = c0 + tx;
+    tile[i][tx] = (c < C && t < T_) ? Elem<T>::ld(y, ((int64_t)b * T_ + t) * ldy + c) : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int c = c0 + i, t = t0 + tx;
+    if (c < C && t < T_) x[((int64_t)b * C + c) * T_ + t] = tile[tx][i];
+  }
+}
+
+// ----------------------------------------------------------------- logloss
+template <typename T>
+__global__ __launch_bounds__(256) void logloss_kernel(const float* __restrict__ x, const float* __restrict__ xh, int ldxh,
+                                                      int B, int C, int T_, float gscale, T* __restrict__ dx, int lddx,
+                                                      float* __restrict__ part) {
+  __shared__ float red[16];
+  const int64_t total = (int64_t)B * T_ * C;
+  float s = 0.f;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t n = e / C;
+    const int c = (int)(e - n * C);
+    const int b = (int)(n / T_), t = (int)(n - (int64_t)b * T_);
+    const float xv = x[((int64_t)b * C + c) * T_ + t];
+    const float d = xh[n * ldxh + c] - xv;
+    s += 0.5f * (kLog2Pi + d * d);
+    if (dx) Elem<T>::st(dx, n * lddx + c, d * gscale);
+  }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ void sum_partials_scale_kernel(const float* __restrict__ p, int n, float scale, float* __restrict__ out) {
+  __shared__ float red[16];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += p[i];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) out[0] = s * scale;
+}
+
+// ------------------------------------------------------------ small kernels
+template <typename T>
+__global__ void time_gather_kernel(const T* __restrict__ x, T* __restrict__ y, int B, int T_, int C,
+                                   const int* __restrict__ src) {
+  const int64_t total = (int64_t)B * T_ * C;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t n = e / C;
+    const int c = (int)(e - n * C);
+    const int b = (int)(n / T_), t = (int)(n - (int64_t)b * T_);
+    y[e] = x[((int64_t)b * T_ + src[t]) * C + c];
+  }
+}
+
+__global__ void embedding_fwd_kernel(const float* __restrict__ w, const int64_t* __restrict__ ids, int B, int D,
+                                     float* __restrict__ out) {
+  const int b = blockIdx.x;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) out[(int64_t)b * D + d] = w[ids[b] * D + d];
+}
+
+// dense embedding gradient, deterministic: one thread per (row used, d), summing the batch in order
+__global__ void embedding_bwd_kernel(const float* __restrict__ dout, const int64_t* __restrict__ ids, int B, int D,
+                                     float* __restrict__ dw) {
+  const int b = blockIdx.x;
+  // only the first occurrence of each id accumulates all occurrences (in batch order)
+  for (int p = 0; p < b; ++p)
+    if (ids[p] == ids[b]) return;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float s = 0.f;
+    for (int q = b; q < B; ++q)
+      if (ids[q] == ids[b]) s += dout[(int64_t)q * D + d];
+    dw[ids[b] * D + d] += s;
+  }
+}
+
+__global__ void linear_fwd_kernel(const float* __restrict__ c, const float* __restrict__ W, const float* __restrict__ bias,
+                                  int B, int I, int O, float* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)B * O) return;
+  const int b = (int)(e / O), o = (int)(e - (int64_t)b * O);
+  float s = 0.f;
+  for (int i = 0; i < I; ++i) s = fmaf(W[(int64_t)o * I + i], c[(int64_t)b * I + i], s);
+  out[e] = s + (bias ? bias[o] : 0.f);
+}
+
+__global__ void linear_bwd_w_kernel(const float* __restrict__ dout, const float* __restrict__ c, int B, int I, int O,
+                                    float* __restrict__ dW) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)O * I) return;
+  const int o = (int)(e / I), i = (int)(e - (int64_t)o * I);
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) s = fmaf(dout[(int64_t)b * O + o], c[(int64_t)b * I + i], s);
+  dW[e] += s;
+}
+
+__global__ void linear_bwd_x_kernel(const float* __restrict__ dout, const float* __restrict__ W, int B, int I, int O,
+                                    float* __restrict__ dc) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)B * I) return;
+  const int b = (int)(e / I), i = (int)(e - (int64_t)b * I);
+  float s = 0.f;
+  for (int o = 0; o < O; ++o) s = fmaf(dout[(int64_t)b * O + o], W[(int64_t)o * I + i], s);
+  dc[e] += s;
+}
+
+// --------------------------------------------------------------- optimizer
+constexpr int kNormBlocks = 1024;
+
+__global__ __launch_bounds__(256) void sqnorm_partial_kernel(const float* __restrict__ g, int64_t n,
+                                                             float* __restrict__ part) {
+  __shared__ float red[16];
+  float s = 0.f;
+  const int64_t n4 = n / 4;
+  const f32x4_t* g4 = (const f32x4_t*)g;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const f32x4_t v = g4[i];
+    s = fmaf(v[0], v[0], s); s = fmaf(v[1], v[1], s); s = fmaf(v[2], v[2], s); s = fmaf(v[3], v[3], s);
+  }
+  if (blockIdx.x == 0)
+    for (int64_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) s = fmaf(g[i], g[i], s);
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ void adam_hyper_kernel(int64_t* __restrict__ step, double lr0, double gamma, int step_size, double b1,
+                                  double b2, double eps, float* __restrict__ hyper) {
+  const int64_t t = step[0] + 1;
+  step[0] = t;
+  const double lr = lr0 * pow(gamma, (double)((t - 1) / step_size));
+  const double bc1 = 1.0 - pow(b1, (double)t);
+  const double bc2 = 1.0 - pow(b2, (double)t);
+  hyper[0] = (float)lr;
+  hyper[1] = (float)(lr / bc1);
+  hyper[2] = (float)sqrt(bc2);
+  hyper[3] = (float)t;
+  hyper[4] = (float)(1.0 - b1);
+  hyper[5] = (float)b2;
+  hyper[6] = (float)(1.0 - b2);
+  hyper[7] = (float)eps;
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                   const float* __restrict__ hyper, const float* __restrict__ sumsq,
+                                                   float max_norm) {
+  float coef = 1.f;
+  if (max_norm > 0.f && sumsq) {
+    const float tn = sqrtf(sumsq[0]);
+    coef = max_norm / (tn + 1e-6f);
+    coef = coef < 1.f ? coef : 1.f;
+  }
+  const float step_size = hyper[1], bc2s = hyper[2];
+  const float w = hyper[4], b2 = hyper[5], omb2 = hyper[6], eps = hyper[7];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float gi = __fmul_rn(g[i], coef);
+    float mi = m[i];
+    // torch.lerp: weight < 0.5 ? m + w*(g-m) : g - (g-m)*(1-w)
+    mi = (w < 0.5f) ? __fadd_rn(mi, __fmul_rn(w, __fsub_rn(gi, mi)))
+                    : __fsub_rn(gi, __fmul_rn(__fsub_rn(gi, mi), 1.f - w));
+    float vi = __fmul_rn(v[i], b2);
+    vi = __fadd_rn(vi, __fmul_rn(__fmul_rn(omb2, gi), gi));
+    const float den = __fadd_rn(__fdiv_rn(__fsqrt_rn(vi), bc2s), eps);
+    p[i] = __fadd_rn(p[i], __fmul_rn(-step_size, __fdiv_rn(mi, den)));
+    m[i] = mi;
+    v[i] = vi;
+  }
+}
+
+}  // namespace vqx
+
+using namespace vqx;
+
+static int grid_for(int64_t n, int block = 256, int cap = 8192) {
+  int64_t g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  return (int)(g > cap ? cap : g);
+}
+
+extern "C" int vqx_weight_norm_fwd(const vqx_wn_layer* lh, const vqx_wn_layer* ld, int32_t n_layers,
+                                   vqx_stream_t stream) {
+  if (!lh || !ld || n_layers <= 0) { set_error("vqx_weight_norm_fwd: bad tables"); return -1; }
+  int max_rows = 1;
+  int64_t max_el = 1;
+  for (int i = 0; i < n_layers; ++i) {
+    const vqx_wn_layer& l = lh[i];
+    if (l.kind != 0 && l.kind != 1) { set_error("vqx_weight_norm_fwd: layer %d bad kind", i); return -1; }
+    const int rows = l.kind == 0 ? l.cout : l.cin;
+    max_rows = rows > max_rows ? rows : max_rows;
+    const int64_t el = (int64_t)l.cout * l.cin * l.k;
+    max_el = el > max_el ? el : max_el;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(wn_norm_kernel, dim3(max_rows, n_layers), dim3(256), 0, s, ld, n_layers);
+  hipLaunchKernelGGL(wn_pack_kernel, dim3(grid_for(max_el, 256, 2048), n_layers), dim3(256), 0, s, ld, n_layers);
+  return launch_status("vqx_weight_norm_fwd");
+}
+
+extern "C" int vqx_weight_norm_bwd(const vqx_wn_layer* lh, const vqx_wn_layer* ld, int32_t n_layers,
+                                   vqx_stream_t stream) {
+  if (!lh || !ld || n_layers <= 0) { set_error("vqx_weight_norm_bwd: bad tables"); return -1; }
+  int max_rows = 1;
+  for (int i = 0; i < n_layers; ++i) {
+    const vqx_wn_layer& l = lh[i];
+    const int rows = l.kind == 0 ? l.cout : l.cin;
+    const int cols = (l.kind == 0 ? l.cin : l.cout) * l.k;
+    if (cols > 4096) { set_error("vqx_weight_norm_bwd: row length %d > 4096", cols); return -1; }
+    if (!l.slabs || !l.dv || !l.dg || l.splits < 1) { set_error("vqx_weight_norm_bwd: layer %d missing buffers", i); return -1; }
+    max_rows = rows > max_rows ? rows : max_rows;
+  }
+  hipLaunchKernelGGL(wn_bwd_kernel, dim3(max_rows, n_layers), dim3(256), 0, (hipStream_t)stream, ld, n_layers);
+  return launch_status("vqx_weight_norm_bwd");
+}
+
+extern "C" int vqx_groupnorm_stats(const void* x, int32_t ldx, int32_t dtype, int64_t n_rows, int32_t T, int32_t C,
+                                   int32_t G, float eps, float* partials, float* mean_rstd, vqx_stream_t stream) {
+  if (G < 1 || C % G || n_rows % T) { set_error("vqx_groupnorm_stats: bad shape"); return -1; }
+  const int B = (int)(n_rows / T);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == VQX_BF16)
+    hipLaunchKernelGGL(gn_partial_kernel<bf16_t>, dim3(kGnParts, B * G), dim3(256), 0, s, (const bf16_t*)x, ldx, T, C, G, partials);
+  else
+    hipLaunchKernelGGL(gn_partial_kernel<float>, dim3(kGnParts, B * G), dim3(256), 0, s, (const float*)x, ldx, T, C, G, partials);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3((B * G + 127) / 128), dim3(128), 0, s, partials, B * G, eps, mean_rstd);
+  return launch_status("vqx_groupnorm_stats");
+}
+
+extern "C" int vqx_gn_glu_fwd(const void* u, int32_t ldu, void* g, int32_t ldg, int32_t dtype, int64_t n_rows,
+                              int32_t T, int32_t C, const float* mean_rstd, const float* gamma, const float* beta,
+                              vqx_stream_t stream) {
+  if (C % 2) { set_error("vqx_gn_glu_fwd: odd C"); return -1; }
+  const int grid = grid_for(n_rows * (C / 2));
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == VQX_BF16)
+    hipLaunchKernelGGL(gn_glu_fwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)u, ldu, (bf16_t*)g, ldg, n_rows, T, C / 2, mean_rstd, gamma, beta);
+  else
+    hipLaunchKernelGGL(gn_glu_fwd_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)u, ldu, (float*)g, ldg, n_rows, T, C / 2, mean_rstd, gamma, beta);
+  return launch_status("vqx_gn_glu_fwd");
+}
+
+extern "C" int vqx_gn_bwd(const void* dy, int32_t lddy, const void* u, int32_t ldu, void* du, int32_t lddu,
+                          int32_t dtype, int64_t n_rows, int32_t T, int32_t C, int32_t G, int32_t glu,
+                          const float* mean_rstd, const float* gamma, const float* beta, float* partials,
+                          float* colsum_b, float* dgamma_b, float* dbeta_b, vqx_stream_t stream) {
+  if (glu && G != 2) { set_error("vqx_gn_bwd: glu requires G=2"); return -1; }
+  if (G < 1 || C % G || n_rows % T) { set_error("vqx_gn_bwd: bad shape"); return -1; }
+  const int B = (int)(n_rows / T);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == VQX_BF16) {
+    hipLaunchKernelGGL(gn_bwd_reduce_kernel<bf16_t>, dim3(kGnParts, B), dim3(256), 0, s, (const bf16_t*)dy, lddy, (const bf16_t*)u, ldu, T, C, G, glu, mean_rstd, gamma, beta, partials);
+    hipLaunchKernelGGL(gn_bwd_apply_kernel<bf16_t>, dim3((C + 63) / 64, B), dim3(256), 0, s, (const bf16_t*)dy, lddy, (const bf16_t*)u, ldu, (bf16_t*)du, lddu, T, C, G, glu, mean_rstd, gamma, beta, partials, colsum_b, dgamma_b, dbeta_b);
+  } else {
+    hipLaunchKernelGGL(gn_bwd_reduce_kernel<float>, dim3(kGnParts, B), dim3(256), 0, s, (const float*)dy, lddy, (const float*)u, ldu, T, C, G, glu, mean_rstd, gamma, beta, partials);
+    hipLaunchKernelGGL(gn_bwd_apply_kernel<float>, dim3((C + 63) / 64, B), dim3(256), 0, s, (const float*)dy, lddy, (const float*)u, ldu, (float*)du, lddu, T, C, G, glu, mean_rstd, gamma, beta, partials, colsum_b, dgamma_b, dbeta_b);
+  }
+  return launch_status("vqx_gn_bwd");
+}
+
+extern "C" int vqx_colsum(const void* x, int32_t ldx, int32_t dtype, int64_t n_rows, int32_t C, float* partials,
+                          float* out, int32_t accumulate, vqx_stream_t stream) {
+  if (n_rows <= 0 || C <= 0) { set_error("vqx_colsum: bad shape"); return -1; }
+  int nparts = (int)((n_rows + 255) / 256);
+  nparts = nparts > 64 ? 64 : nparts;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == VQX_BF16)
+    hipLaunchKernelGGL(colsum_partial_kernel<bf16_t>, dim3((C + 63) / 64, nparts), dim3(256), 0, s, (const bf16_t*)x, ldx, n_rows, C, nparts, partials);
+  else
+    hipLaunchKernelGGL(colsum_partial_kernel<float>, dim3((C + 63) / 64, nparts), dim3(256), 0, s, (const float*)x, ldx, n_rows, C, nparts, partials);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 255) / 256), dim3(256), 0, s, partials, nparts, C, out, accumulate);
+  return launch_status("vqx_colsum");
+}
+
+extern "C" int vqx_nct_to_ntc(const float* x, int32_t B, int32_t C, int32_t T, void* y, int32_t ldy, int32_t dtype,
+                              vqx_stream_t stream) {
+  dim3 grid((T + 31) / 32, (C + 31) / 32, B);
+  if (dtype == VQX_BF16)
+    hipLaunchKernelGGL(nct_to_ntc_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, x, B, C, T, (bf16_t*)y, ldy);
+  else
+    hipLaunchKernelGGL(nct_to_ntc_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, x, B, C, T, (float*)y, ldy);
+  return launch_status("vqx_nct_to_ntc");
+}
+
+extern "C" int vqx_ntc_to_nct(const void* y, int32_t ldy, int32_t dtype, int32_t B, int32_t C, int32_t T, float* x,
+                              vqx_stream_t stream) {
+  dim3 grid((T + 31) / 32, (C + 31) / 32, B);
+  if (dtype == VQX_BF16)
+    hipLaunchKernelGGL(ntc_to_nct_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)y, ldy, B, C, T, x);
+  else
+    hipLaunchKernelGGL(ntc_to_nct_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, (const float*)y, ldy, B, C, T, x);
+  return launch_status("vqx_ntc_to_nct");
+}
+
+extern "C" int vqx_logloss_fwd_bwd(const float* x, const float* xhat, int32_t ldxh, int32_t B, int32_t C, int32_t T,
+                                   float grad_scale, void* dxhat, int32_t lddx, int32_t dtype, float* loss_out,
+                                   float* partials, vqx_stream_t stream) {
+  const int64_t total = (int64_t)B * C * T;
+  const int grid = grid_for(total, 256, 1024);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == VQX_BF16)
+    hipLaunchKernelGGL(logloss_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, x, xhat, ldxh, B, C, T, grad_scale, (bf16_t*)dxhat, lddx, partials);
+  else
+    hipLaunchKernelGGL(logloss_kernel<float>, dim3(grid), dim3(256), 0, s, x, xhat, ldxh, B, C, T, grad_scale, (float*)dxhat, lddx, partials);
+  hipLaunchKernelGGL(sum_partials_scale_kernel, dim3(1), dim3(1024), 0, s, partials, grid, 1.0f / ((float)B * (float)T), loss_out);
+  return launch_status("vqx_logloss_fwd_bwd");
+}
+
+extern "C" int vqx_time_gather(const void* x, void* y, int32_t B, int32_t T, int32_t C, const int32_t* src_t,
+                               int32_t dtype, vqx_stream_t stream) {
+  const int grid = grid_for((int64_t)B * T * C);
+  if (dtype == VQX_BF16)
+    hipLaunchKernelGGL(time_gather_kernel<bf16_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, (bf16_t*)y, B, T, C, src_t);
+  else
+    hipLaunchKernelGGL(time_gather_kernel<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float*)x, (float*)y, B, T, C, src_t);
+  return launch_status("vqx_time_gather");
+}
+
+extern "C" int vqx_embedding_fwd(const float* weight, const int64_t* ids, int32_t B, int32_t D, float* out,
+                                 vqx_stream_t stream) {
+  hipLaunchKernelGGL(embedding_fwd_kernel, dim3(B), dim3(128), 0, (hipStream_t)stream, weight, ids, B, D, out);
+  return launch_status("vqx_embedding_fwd");
+}
+
+extern "C" int vqx_embedding_bwd(const float* dout, const int64_t* ids, int32_t B, int32_t D, float* dweight,
+                                 vqx_stream_t stream) {
+  hipLaunchKernelGGL(embedding_bwd_kernel, dim3(B), dim3(128), 0, (hipStream_t)stream, dout, ids, B, D, dweight);
+  return launch_status("vqx_embedding_bwd");
+}
+
+extern "C" int vqx_linear_f32(const float* c, const float* W, const float* bias, int32_t B, int32_t I, int32_t O,
+                              float* out, vqx_stream_t stream) {
+  hipLaunchKernelGGL(linear_fwd_kernel, dim3(grid_for((int64_t)B * O, 256, 1 << 20)), dim3(256), 0, (hipStream_t)stream, c, W, bias, B, I, O, out);
+  return launch_status("vqx_linear_f32");
+}
+
+extern "C" int vqx_linear_bwd_f32(const float* dout, const float* c, const float* W, int32_t B, int32_t I, int32_t O,
+                                  float* dW, float* dc, vqx_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (dW) hipLaunchKernelGGL(linear_bwd_w_kernel, dim3(grid_for((int64_t)O * I, 256, 1 << 20)), dim3(256), 0, s, dout, c, B, I, O, dW);
+  if (dc) hipLaunchKernelGGL(linear_bwd_x_kernel, dim3(grid_for((int64_t)B * I, 256, 1 << 20)), dim3(256), 0, s, dout, W, B, I, O, dc);
+  return launch_status("vqx_linear_bwd_f32");
+}
+
+extern "C" int vqx_grad_sq_norm(const float* g, int64_t n, float* partials, float* out, vqx_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(sqnorm_partial_kernel, dim3(kNormBlocks), dim3(256), 0, s, g, n, partials);
+  hipLaunchKernelGGL(sum_partials_scale_kernel, dim3(1), dim3(1024), 0, s, partials, kNormBlocks, 1.0f, out);
+  return launch_status("vqx_grad_sq_norm");
+}
+
+extern "C" int vqx_adam_hyper(int64_t* step, double lr0, double gamma, int32_t step_size, double beta1,
+                              double beta2, double eps, float* hyper, vqx_stream_t stream) {
+  if (step_size < 1) { set_error("vqx_adam_hyper: step_size < 1"); return -1; }
+  hipLaunchKernelGGL(adam_hyper_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step, lr0, gamma, step_size, beta1,
+                     beta2, eps, hyper);
+  return launch_status("vqx_adam_hyper");
+}
+
+extern "C" int vqx_adam_step(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper,
+                             const float* sumsq, float max_norm, vqx_stream_t stream) {
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
+                     hyper, sumsq, max_norm);
+  return launch_status("vqx_adam_step");
+}

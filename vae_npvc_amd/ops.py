@@ -1,0 +1,229 @@
+"""Thin tensor-level wrappers over the libvqx C ABI (device tensors in, no
+allocation inside the kernels).  Every function here launches HIP kernels on
+torch's current stream; there is no CPU path.
+
+Layout convention: activations are frame-major 2-D tensors [N = B*T, C]
+(the reference's (B, C, T) transposed), weights of a conv are "packed
+effective" [cout, ntaps*cin] (see include/vqx.h).
+"""
+import ctypes
+
+import torch
+
+from . import _lib as L
+from ._lib import call, ptr, stream_ptr
+
+_DT = {torch.float32: L.VQX_F32, torch.bfloat16: L.VQX_BF16}
+
+
+def dt_code(dtype: torch.dtype) -> int:
+    try:
+        return _DT[dtype]
+    except KeyError:
+        raise L.VqxError(f"unsupported dtype {dtype}") from None
+
+
+def _check_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise L.VqxError("libvqx ops need device tensors (the HIP kernels are the only implementation)")
+
+
+def conv_args(x, w, y, *, T, cin, cout, ntaps, pad, prologue=L.PRO_NONE, pro_scale=1.0, bias=None,
+              rowbias=None, res=None, mask=None, mask_slope=0.0, mask_scale=1.0, gn_h=None, gn_mr=None,
+              gn_gamma=None, gn_beta=None, out2=None, split_col=0, out2_accumulate=False, out_f32=False):
+    epi = 0
+    if bias is not None:
+        epi |= L.EPI_BIAS
+    if rowbias is not None:
+        epi |= L.EPI_ROWBIAS
+    if mask is not None:
+        epi |= L.EPI_MASK
+    if res is not None:
+        epi |= L.EPI_RES
+    if gn_h is not None:
+        epi |= L.EPI_GNADD
+    if out2 is not None:
+        epi |= L.EPI_SPLIT
+    if out_f32:
+        epi |= L.EPI_OUTF32
+    a = L.ConvArgs()
+    a.x, a.w, a.y = ptr(x), ptr(w), ptr(y)
+    a.bias, a.rowbias, a.res, a.mask = ptr(bias), ptr(rowbias), ptr(res), ptr(mask)
+    a.gn_h, a.gn_mean_rstd, a.gn_gamma, a.gn_beta, a.out2 = ptr(gn_h), ptr(gn_mr), ptr(gn_gamma), ptr(gn_beta), ptr(out2)
+    a.n_rows, a.T, a.cin, a.cout, a.ntaps, a.pad = x.shape[0], T, cin, cout, ntaps, pad
+    a.ldx, a.ldy = x.stride(0), y.stride(0)
+    a.ldres = res.stride(0) if res is not None else 0
+    a.ldmask = mask.stride(0) if mask is not None else 0
+    a.ldgn = gn_h.stride(0) if gn_h is not None else 0
+    a.ldo2 = out2.stride(0) if out2 is not None else 0
+    a.dtype = dt_code(x.dtype)
+    a.prologue, a.epilogue = prologue, epi
+    a.split_col, a.out2_accumulate = split_col, int(bool(out2_accumulate))
+    a.pro_scale, a.mask_slope, a.mask_scale = pro_scale, mask_slope, mask_scale
+    return a
+
+
+def conv_fwd(x, w, y, **kw):
+    """y = epi(conv(pro(x), w)); x [N, cin], w packed [cout, ntaps*cin], y [N, cout]."""
+    _check_cuda(x, w, y)
+    a = conv_args(x, w, y, **kw)
+    call("vqx_conv1d_fwd", ctypes.byref(a), stream_ptr())
+    return y
+
+
+def conv_dgrad(dy, w, dx, **kw):
+    """dx = epi(conv_transpose(dy, w)); dy [N, cout_f], w packed [cout_f, ntaps*cin_f], dx [N, cin_f].
+    Pass cin=cout_f, cout=cin_f."""
+    _check_cuda(dy, w, dx)
+    a = conv_args(dy, w, dx, **kw)
+    call("vqx_conv1d_dgrad", ctypes.byref(a), stream_ptr())
+    return dx
+
+
+def conv_wgrad(p, q, slabs, *, T, r_dim, c_dim, ntaps, pad, shift_sign=1, q_prologue=L.PRO_NONE, pro_scale=1.0,
+               splits=1):
+    """slabs[s, r, j*c_dim + c] = sum_{n in split s} p[n, r] * pro(q[n + sign*(j-pad), c])."""
+    _check_cuda(p, q, slabs)
+    a = L.WgradArgs()
+    a.p, a.q, a.slabs = ptr(p), ptr(q), ptr(slabs)
+    a.n_rows, a.T, a.r_dim, a.c_dim, a.ntaps, a.pad, a.shift_sign = p.shape[0], T, r_dim, c_dim, ntaps, pad, shift_sign
+    a.ldp, a.ldq = p.stride(0), q.stride(0)
+    a.dtype, a.q_prologue, a.splits, a.pro_scale = dt_code(p.dtype), q_prologue, splits, pro_scale
+    call("vqx_conv1d_wgrad", ctypes.byref(a), stream_ptr())
+    return slabs
+
+
+def wn_table(layers):
+    """Pack a list of dicts into a ctypes WNLayer array (host copy) and a device byte tensor copy."""
+    arr = (L.WNLayer * len(layers))()
+    for i, d in enumerate(layers):
+        e = arr[i]
+        for k in ("v", "g", "w_packed", "norm", "dv", "dg", "slabs"):
+            setattr(e, k, ptr(d.get(k)))
+        e.kind, e.cout, e.cin, e.k = d["kind"], d["cout"], d["cin"], d["k"]
+        e.splits, e.dtype = d.get("splits", 1), d["dtype"]
+    raw = bytes(arr)
+    dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to("cuda")
+    return arr, dev
+
+
+def weight_norm_fwd(table):
+    arr, dev = table
+    call("vqx_weight_norm_fwd", ctypes.addressof(arr), dev.data_ptr(), len(arr), stream_ptr())
+
+
+def weight_norm_bwd(table):
+    arr, dev = table
+    call("vqx_weight_norm_bwd", ctypes.addressof(arr), dev.data_ptr(), len(arr), stream_ptr())
+
+
+def groupnorm_stats(x, T, G, partials, mean_rstd, eps=1e-5):
+    call("vqx_groupnorm_stats", ptr(x), x.stride(0), dt_code(x.dtype), x.shape[0], T, x.shape[1], G, eps,
+         ptr(partials), ptr(mean_rstd), stream_ptr())
+    return mean_rstd
+
+
+def gn_glu_fwd(u, g, T, mean_rstd, gamma, beta):
+    call("vqx_gn_glu_fwd", ptr(u), u.stride(0), ptr(g), g.stride(0), dt_code(u.dtype), u.shape[0], T, u.shape[1],
+         ptr(mean_rstd), ptr(gamma), ptr(beta), stream_ptr())
+    return g
+
+
+def gn_bwd(dy, u, du, T, G, glu, mean_rstd, gamma, beta, partials, colsum_b=None, dgamma_b=None, dbeta_b=None):
+    call("vqx_gn_bwd", ptr(dy), dy.stride(0), ptr(u), u.stride(0), ptr(du), du.stride(0), dt_code(u.dtype),
+         u.shape[0], T, u.shape[1], G, int(glu), ptr(mean_rstd), ptr(gamma), ptr(beta), ptr(partials),
+         ptr(colsum_b), ptr(dgamma_b), ptr(dbeta_b), stream_ptr())
+    return du
+
+
+def colsum(x, partials, out, accumulate=False, C=None):
+    C = x.shape[1] if C is None else C
+    call("vqx_colsum", ptr(x), x.stride(0), dt_code(x.dtype), x.shape[0], C, ptr(partials), ptr(out),
+         int(accumulate), stream_ptr())
+    return out
+
+
+def nct_to_ntc(x_nct, y):
+    B, C, T = x_nct.shape
+    call("vqx_nct_to_ntc", ptr(x_nct), B, C, T, ptr(y), y.stride(0), dt_code(y.dtype), stream_ptr())
+    return y
+
+
+def ntc_to_nct(y, x_nct):
+    B, C, T = x_nct.shape
+    call("vqx_ntc_to_nct", ptr(y), y.stride(0), dt_code(y.dtype), B, C, T, ptr(x_nct), stream_ptr())
+    return x_nct
+
+
+def logloss_fwd_bwd(x_nct, xhat, grad_scale, dxhat, loss_out, partials):
+    B, C, T = x_nct.shape
+    call("vqx_logloss_fwd_bwd", ptr(x_nct), ptr(xhat), xhat.stride(0), B, C, T, grad_scale, ptr(dxhat),
+         dxhat.stride(0) if dxhat is not None else 0, dt_code(dxhat.dtype) if dxhat is not None else 0,
+         ptr(loss_out), ptr(partials), stream_ptr())
+    return loss_out
+
+
+def vq_forward(z, E, idx, zq, zq_c, sqerr, partials, bsum=None, bcnt=None):
+    N, D = z.shape
+    call("vqx_vq_forward", ptr(z), N, D, ptr(E), E.shape[0], ptr(idx), ptr(zq), ptr(zq_c),
+         dt_code(zq_c.dtype) if zq_c is not None else 0, ptr(sqerr), ptr(partials), ptr(bsum), ptr(bcnt),
+         stream_ptr())
+
+
+def vq_ema_update(emb_sum, emb_elem, E, bsum, bcnt, rand_rows, mu, threshold, diag):
+    K, D = E.shape
+    call("vqx_vq_ema_update", ptr(emb_sum), ptr(emb_elem), ptr(E), ptr(bsum), ptr(bcnt), ptr(rand_rows), K, D,
+         mu, threshold, ptr(diag), stream_ptr())
+
+
+def gather_rows(src, rows, out):
+    call("vqx_gather_rows", ptr(src), src.stride(0), ptr(rows), out.shape[0], out.shape[1], ptr(out), stream_ptr())
+    return out
+
+
+def vq_commit_bwd(z, zq, scale, dz):
+    call("vqx_vq_commit_bwd", ptr(z), ptr(zq), z.numel(), scale, ptr(dz), dt_code(dz.dtype), stream_ptr())
+    return dz
+
+
+def time_gather(x, y, B, T, src_t):
+    call("vqx_time_gather", ptr(x), ptr(y), B, T, x.shape[1], ptr(src_t), dt_code(x.dtype), stream_ptr())
+    return y
+
+
+def embedding_fwd(weight, ids, out):
+    call("vqx_embedding_fwd", ptr(weight), ptr(ids), ids.numel(), weight.shape[1], ptr(out), stream_ptr())
+    return out
+
+
+def embedding_bwd(dout, ids, dweight):
+    call("vqx_embedding_bwd", ptr(dout), ptr(ids), ids.numel(), dweight.shape[1], ptr(dweight), stream_ptr())
+    return dweight
+
+
+def linear_f32(c, W, bias, out):
+    B, I = c.shape
+    O = W.shape[0]
+    call("vqx_linear_f32", ptr(c), ptr(W), ptr(bias), B, I, O, ptr(out), stream_ptr())
+    return out
+
+
+def linear_bwd_f32(dout, c, W, dW=None, dc=None):
+    B, I = c.shape
+    O = W.shape[0]
+    call("vqx_linear_bwd_f32", ptr(dout), ptr(c), ptr(W), B, I, O, ptr(dW), ptr(dc), stream_ptr())
+
+
+def grad_sq_norm(g, partials, out):
+    call("vqx_grad_sq_norm", ptr(g), g.numel(), ptr(partials), ptr(out), stream_ptr())
+    return out
+
+
+def adam_hyper(step, lr0, gamma, step_size, beta1, beta2, eps, hyper):
+    call("vqx_adam_hyper", ptr(step), lr0, gamma, step_size, beta1, beta2, eps, ptr(hyper), stream_ptr())
+
+
+def adam_step(p, g, m, v, hyper, sumsq, max_norm):
+    call("vqx_adam_step", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), ptr(hyper), ptr(sumsq), max_norm,
+         stream_ptr())
