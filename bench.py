@@ -1,0 +1,163 @@
+#!/usr/bin/env python3
+"""Benchmark of the VQ-VAE training step (BASELINE.json metric): mel-frames/s
+of one full Trainer.train_step (forward, backward, grad all-reduce, clip,
+Adam, StepLR, EMA codebook) on synthetic 80-dim mel batches.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+
+N > 1: launched by torch.distributed.run, one rank per GPU (RCCL over xGMI);
+each rank trains 64 x 256 frames (weak scaling, global batch 64*N).
+Rank 0 prints ONE JSON line.  Workload = BASELINE configs[1] (vcc20 VQ-VAE,
+codebook 512, 80 mel, batch 64 x 256 frames per GPU, bf16 conv GEMMs with
+fp32 accumulation; statistics, VQ and optimizer in fp32).  Weights are random
+(seeded), data synthetic N(0,1) mel + uniform speaker ids: no network.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+import yaml  # noqa: E402
+
+B_PER_GPU, T_FRAMES = 64, 256
+FLOP_PER_FRAME = 178.9e6        # algorithmic conv GEMM + VQ distance FLOPs per mel-frame
+PEAK_BF16 = 2.5e15              # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_F32 = 157.3e12
+HBM_PEAK = 8.0e12
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--config", default="vcc20", choices=["vcc20", "aishell3"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--no-probe", action="store_true", help="skip the per-launch GEMM event probe")
+    return ap.parse_args()
+
+
+def cpu_baseline(cfg, steps):
+    """The CPU oracle (torch-CPU fp32 restatement of the reference step, validated
+    against the reference's golden vectors) on this host's cores, same workload."""
+    from oracle.vqvae_cpu import OracleTrainer, seeded_batch, seeded_state_dict
+    threads = os.cpu_count() or 1
+    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+    torch.set_num_threads(threads)
+    ocfg = dict(cfg)
+    tr = OracleTrainer(ocfg, seeded_state_dict(ocfg, 1))
+    x, y = seeded_batch(ocfg, B_PER_GPU, T_FRAMES, 0)
+    tr.train_step((x, y))  # warm-up (includes EMA init)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tr.train_step((x, y))
+    dt = (time.perf_counter() - t0) / steps
+    return {"value": B_PER_GPU * T_FRAMES / dt, "unit": "mel-frames/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} timed steps (+1 warm-up) of the oracle train step at B={B_PER_GPU}x{T_FRAMES}, fp32, "
+                      f"torch-CPU {torch.__version__}, s/step={dt:.2f}"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    cfg = yaml.safe_load(open(os.path.join(ROOT, "vae_npvc_amd", "conf", f"{a.config}.yaml")))
+    cfg["compute_dtype"] = a.dtype
+    cfg["batch_size"] = B_PER_GPU
+
+    from vae_npvc_amd import ops
+    from vae_npvc_amd.trainer.basic import Trainer
+    torch.manual_seed(777)
+    np.random.seed(777)
+    tr = Trainer(cfg)
+    mel = cfg["encoder"]["in_channels"][0]
+    gen = torch.Generator(device="cpu").manual_seed(1234 + rank)
+    n_batches = 4
+    xs = [torch.randn(B_PER_GPU, mel, T_FRAMES, generator=gen).to(dev) for _ in range(n_batches)]
+    ys = [torch.randint(0, cfg["y_num"], (B_PER_GPU, 1), generator=gen).to(dev) for _ in range(n_batches)]
+
+    for i in range(a.warmup):
+        _, det = tr.train_step((xs[i % n_batches], ys[i % n_batches]))
+    if a.warmup:
+        dict(det)  # materialise once: surfaces any asynchronous error before timing
+    probe = None if a.no_probe else ops.LaunchProbe()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ops.set_probe(probe)
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        _, det = tr.train_step((xs[i % n_batches], ys[i % n_batches]))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    ops.set_probe(None)
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    detail = dict(det)
+    frames = B_PER_GPU * T_FRAMES * world * a.steps
+    value = frames / elapsed
+    ms = 1e3 * elapsed / a.steps
+
+    roof = None
+    kernels = None
+    if probe is not None:
+        summ = probe.summary()
+        kernels = {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in v.items()}
+                   for k, v in summ.items()}
+        dom = max(summ.items(), key=lambda kv: kv[1]["seconds"])
+        name, s = dom
+        peak = PEAK_BF16 if a.dtype == "bf16" else PEAK_F32
+        ach = s["flops"] / s["seconds"]
+        roof = {"bound": "mfma", "kernel": name, "achieved": round(ach / 1e12, 2), "peak": peak / 1e12,
+                "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": None,
+                "launches_per_step": s["launches"] / a.steps, "avg_launch_us": round(s["avg_us"], 2),
+                "flops_per_launch": s["flops"] / s["launches"]}
+
+    out = {
+        "metric": "mel-frames/sec/GPU VQ-VAE train step (80-dim mel, batch=64x256f) at 1/2/4/8 GPUs",
+        "value": round(value, 1), "unit": "mel-frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": a.dtype, "data": "synthetic (N(0,1) 80-mel, random speaker ids; seeded random-init weights)",
+        "config": {"workload": f"{a.config} VQ-VAE (K={cfg['z_num']}, {mel}-mel), {B_PER_GPU}x{T_FRAMES} frames per GPU",
+                   "global_batch": B_PER_GPU * world, "seq_len": T_FRAMES, "parallelism": f"dp{world}"},
+        "step_mfma_frac": round(FLOP_PER_FRAME * value / world / (PEAK_BF16 if a.dtype == "bf16" else PEAK_F32), 4),
+        "roofline": roof,
+        "loss": {k: round(v, 4) for k, v in detail.items()},
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cfg, a.cpu_steps)
+    else:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        if kernels is not None and os.environ.get("VQX_BENCH_KERNELS"):
+            out["kernels"] = kernels
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

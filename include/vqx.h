@@ -171,8 +171,8 @@ int vqx_gn_glu_fwd(const void* u, int32_t ldu, void* g, int32_t ldg, int32_t dty
 int vqx_gn_bwd(const void* dy, int32_t lddy, const void* u, int32_t ldu, void* du, int32_t lddu,
                int32_t dtype, int64_t n_rows, int32_t T, int32_t C, int32_t G, int32_t glu,
                const float* mean_rstd, const float* gamma, const float* beta,
-               float* partials /* >= B*16*G */, float* colsum_b, float* dgamma_b, float* dbeta_b,
-               vqx_stream_t stream);
+               float* partials /* >= B*64*G */, float* colsum_b /* [B][C] */,
+               float* dgamma_b /* [B][C] */, float* dbeta_b /* [B][C] */, vqx_stream_t stream);
 
 /*
  * Sum over rows: out[c] (+)= sum_n x[n][c] (f32 accumulation, deterministic
@@ -283,6 +283,12 @@ int vqx_adam_hyper(int64_t* step, double lr0, double gamma, int32_t step_size, d
                    double beta2, double eps, float* hyper, vqx_stream_t stream);
 int vqx_adam_step(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper,
                   const float* sumsq, float max_norm, vqx_stream_t stream);
+
+/* 2-D strided copy with dtype conversion: dst[r][c] = src[r][c] for r < rows,
+ * c < cols; src == NULL fills zeros.  Used for the decoder's skip-sum cast
+ * and the residual/skip gradient buffers of the backward. */
+int vqx_convert_2d(const void* src, int32_t ld_src, int32_t src_dtype, void* dst, int32_t ld_dst,
+                   int32_t dst_dtype, int64_t rows, int32_t cols, vqx_stream_t stream);
 
 /* Thread-local description of the last failure. */
 const char* vqx_last_error(void);

@@ -88,11 +88,9 @@ def seeded_state_dict(cfg, seed):
     embedding N(0, 1).  Fresh EMA buffers (layers_vq.py:170-173)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     sd = OrderedDict()
-    pending_v = {}
     for name, shape in layer_specs(cfg):
         if name.endswith(".weight_v"):
-            fan_in = int(np.prod(shape[1:])) if "decoder.layers.0." not in name and ".conv_in." not in name else \
-                int(shape[0] * shape[2])
+            fan_in = int(np.prod(shape[1:]))  # torch's fan_in for Conv1d and ConvTranspose1d weights
             b = 1.0 / math.sqrt(fan_in)
             v = rng.uniform(-b, b, size=shape).astype(np.float32)
             sd[name] = torch.from_numpy(v)
@@ -116,7 +114,6 @@ def seeded_state_dict(cfg, seed):
     sd["quantizer.emb_sum"] = torch.zeros(K, D)
     sd["quantizer.emb_elem"] = torch.ones(K)
     sd["quantizer.embeddings"] = torch.zeros(K, D)
-    del pending_v
     return sd
 
 

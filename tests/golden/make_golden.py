@@ -1,0 +1,231 @@
+"""Generate the golden fixtures of tests/golden/ by running the REFERENCE
+implementation (Sinica-SLAM/vae_npvc, read-only at /root/reference) on CPU.
+
+Run in the survey/build container only (the reference never travels):
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+What it records (all inputs are regenerated from seeds, so only outputs are
+stored):
+  * structure.json        reference Model state_dict keys/shapes/order per config
+  * step_<cfg>.npz/.json  3 training steps of Model + a restatement of
+                          Trainer.train_step (trainer/basic.py:55-79 without
+                          .cuda(), which is hard-coded there) from
+                          oracle.seeded_state_dict / seeded_batch
+  * vq_K<k>.npz/.json     EMAVectorQuantizer.forward (layers_vq.py:268-323) at
+                          N = 16384 frames, K in {128, 512, 1024}
+  * vq_tile.npz/.json     the N < K tiling path (layers_vq.py:183-190)
+  * jitter.json           Jitter.forward neighbour map (layers_vq.py:353-379)
+  * full_step.npz/.json   2 steps at the config-2 size B=64 x T=256
+Weights/inputs come from numpy PCG64 seeds (oracle/vqvae_cpu.py), so the GPU
+box regenerates them bit-identically without receiving any weights.
+"""
+import json
+import os
+import sys
+import warnings
+from pathlib import Path
+
+import numpy as np
+import torch
+import yaml
+
+HERE = Path(__file__).resolve().parent
+ROOT = HERE.parent.parent
+REF = Path(os.environ.get("VQX_REFERENCE", "/root/reference"))
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(REF))
+warnings.filterwarnings("ignore")
+
+from oracle.vqvae_cpu import buffer_specs, layer_specs, seeded_batch, seeded_state_dict  # noqa: E402
+
+CFGS = {
+    "vcc20": REF / "egs/vcc20/vae1/conf/train_pytorch_vqvae.yaml",
+    "aishell3": REF / "egs/aishell3/vc2/conf/train_pytorch_vqvae.yaml",
+}
+
+
+def load_cfg(name):
+    return yaml.safe_load(open(CFGS[name]))
+
+
+def ref_model(cfg, sd):
+    from vae_npvc.model.vqvae import Model
+    m = Model(cfg)
+    m.load_state_dict(sd)
+    m.train()
+    return m
+
+
+class Recorder:
+    """Wraps quantizer.update_emb to capture (z, idx, E_used) of each step."""
+
+    def __init__(self, q):
+        self.q = q
+        self.orig = q.update_emb
+        self.calls = []
+        q.update_emb = self
+
+    def __call__(self, z, z_idx):
+        E = self.q.embeddings.detach().clone()
+        z = z.detach()
+        dist = (z.pow(2).sum(1, keepdim=True) + E.pow(2).sum(1)) - 2 * z @ E.t()
+        top2 = torch.topk(dist, 2, dim=1, largest=False).values
+        gap = (top2[:, 1] - top2[:, 0]) / top2[:, 1].abs().clamp_min(1e-30)
+        self.calls.append(dict(idx=z_idx.detach().clone(), z=z.clone(), E=E, gap=gap))
+        return self.orig(z, z_idx)
+
+
+def ref_train_step(model, opt, sched, batch, max_grad_norm):
+    """trainer/basic.py:55-79 on CPU."""
+    model.zero_grad()
+    out, loss, detail = model(list(batch))
+    loss.backward()
+    grads = {k: p.grad.detach().clone() for k, p in model.named_parameters()}
+    if max_grad_norm > 0:
+        torch.nn.utils.clip_grad_norm_(model.parameters(), max_grad_norm)
+    opt.step()
+    if sched is not None:
+        sched.step()
+    return out.detach(), detail, grads
+
+
+def summarize(t, n=16):
+    t = t.detach().double().reshape(-1)
+    return dict(norm=float(t.norm()), sum=float(t.sum()), head=[float(v) for v in t[:n]])
+
+
+def step_fixture(name, B, T, steps, wseed, bseed, tseed, nseed, out_prefix, keep_idx=True):
+    cfg = load_cfg(name)
+    sd = seeded_state_dict(cfg, wseed)
+    model = ref_model(cfg, sd)
+    rec = Recorder(model.quantizer)
+    opt = torch.optim.Adam(model.parameters(), lr=cfg.get("learning_rate", 1e-3), betas=(0.5, 0.999),
+                           weight_decay=0.0)
+    sched = torch.optim.lr_scheduler.StepLR(optimizer=opt, **cfg["lr_param"]) if cfg.get("lr_scheduler") else None
+    torch.manual_seed(tseed)
+    np.random.seed(nseed)
+    meta = dict(config=name, B=B, T=T, steps=steps, wseed=wseed, bseed=bseed, tseed=tseed, nseed=nseed,
+                torch=torch.__version__, numpy=np.__version__, detail=[], grads={}, params_after={}, xhat={})
+    arrays = {}
+    for s in range(steps):
+        batch = seeded_batch(cfg, B, T, bseed + s)
+        xhat, detail, grads = ref_train_step(model, opt, sched, batch, cfg.get("max_grad_norm", 5))
+        meta["detail"].append({k: float(v) for k, v in detail.items()})
+        meta["xhat"][str(s)] = summarize(xhat)
+        if s == 0:
+            meta["grads"] = {k: summarize(g) for k, g in grads.items()}
+            arrays["xhat0_slice"] = xhat[:, :, :16].numpy().astype(np.float32)
+        c = rec.calls[-1]
+        if keep_idx:
+            arrays[f"idx{s}"] = c["idx"].numpy().astype(np.int16)
+            arrays[f"gap{s}"] = c["gap"].numpy().astype(np.float32)
+        q = model.quantizer
+        arrays[f"emb_elem{s}"] = q.emb_elem.detach().numpy().astype(np.float32)
+        meta[f"embeddings{s}"] = summarize(q.embeddings)
+        meta[f"emb_sum{s}"] = summarize(q.emb_sum)
+    meta["params_after"] = {k: summarize(p, 8) for k, p in model.named_parameters()}
+    np.savez_compressed(HERE / f"{out_prefix}.npz", **arrays)
+    json.dump(meta, open(HERE / f"{out_prefix}.json", "w"), indent=1)
+    print(f"[golden] {out_prefix}: {[round(d['Total'], 5) for d in meta['detail']]}")
+
+
+def vq_fixture(K, N_B, N_T, seed, out_prefix):
+    from vae_npvc.model.layers_vq import EMAVectorQuantizer
+    D = 128
+    rng = np.random.Generator(np.random.PCG64(seed))
+    z = torch.from_numpy(rng.standard_normal((N_B, D, N_T)).astype(np.float32))
+    E = torch.from_numpy(rng.standard_normal((K, D)).astype(np.float32))
+    emb_sum = torch.from_numpy((1.5 * rng.standard_normal((K, D))).astype(np.float32))
+    emb_elem = torch.from_numpy(rng.uniform(0.5, 3.0, size=(K,)).astype(np.float32))
+    q = EMAVectorQuantizer(K, D, 0.9, reduction="frame_mean")
+    q.emb_init = torch.tensor(True)
+    q.embeddings = E.clone()
+    q.emb_sum = emb_sum.clone()
+    q.emb_elem = emb_elem.clone()
+    q.train()
+    rec = Recorder(q)
+    idx_eval = q.encode(z)
+    torch.manual_seed(seed + 1)
+    zq, _, enc_loss, detail = q(z)
+    c = rec.calls[-1]
+    arrays = dict(idx=c["idx"].numpy().astype(np.int16), gap=c["gap"].numpy().astype(np.float32),
+                  idx_eval=idx_eval.reshape(-1).numpy().astype(np.int16),
+                  emb_elem=q.emb_elem.numpy().astype(np.float32),
+                  emb_row_norm=q.embeddings.norm(dim=1).numpy().astype(np.float32),
+                  emb_sum_row_norm=q.emb_sum.norm(dim=1).numpy().astype(np.float32),
+                  emb_head=q.embeddings[:4].numpy().astype(np.float32))
+    meta = dict(K=K, D=D, B=N_B, T=N_T, seed=seed, torch_seed=seed + 1, enc_loss=float(enc_loss),
+                detail={k: float(v) for k, v in detail.items()}, zq=summarize(zq),
+                embeddings=summarize(q.embeddings), emb_sum=summarize(q.emb_sum),
+                min_gap=float(c["gap"].min()), n_gap_lt_1e5=int((c["gap"] < 1e-5).sum()))
+    np.savez_compressed(HERE / f"{out_prefix}.npz", **arrays)
+    json.dump(meta, open(HERE / f"{out_prefix}.json", "w"), indent=1)
+    print(f"[golden] {out_prefix}: loss={meta['enc_loss']:.6f} detail={meta['detail']} min_gap={meta['min_gap']:.3g}")
+
+
+def vq_tile_fixture(seed, out_prefix):
+    """N < K: init_emb and update_emb tile z with N(0, (0.01/sqrt(D))^2) noise."""
+    from vae_npvc.model.layers_vq import EMAVectorQuantizer
+    K, D, B, T = 512, 128, 1, 96
+    rng = np.random.Generator(np.random.PCG64(seed))
+    z = torch.from_numpy(rng.standard_normal((B, D, T)).astype(np.float32))
+    q = EMAVectorQuantizer(K, D, 0.9, reduction="frame_mean")
+    q.train()
+    torch.manual_seed(seed + 1)
+    zq, _, enc_loss, detail = q(z)  # first call: init_emb + update_emb
+    arrays = dict(emb_row_norm=q.embeddings.norm(dim=1).numpy().astype(np.float32),
+                  emb_elem=q.emb_elem.numpy().astype(np.float32))
+    meta = dict(K=K, D=D, B=B, T=T, seed=seed, torch_seed=seed + 1, enc_loss=float(enc_loss),
+                detail={k: float(v) for k, v in detail.items()}, embeddings=summarize(q.embeddings),
+                emb_sum=summarize(q.emb_sum))
+    np.savez_compressed(HERE / f"{out_prefix}.npz", **arrays)
+    json.dump(meta, open(HERE / f"{out_prefix}.json", "w"), indent=1)
+    print(f"[golden] {out_prefix}: {meta['detail']}")
+
+
+def jitter_fixture():
+    from vae_npvc.model.layers_vq import Jitter
+    out = {}
+    for p, T, seed in [(0.12, 256, 5), (0.12, 64, 6), (0.5, 33, 7)]:
+        j = Jitter(probability=p)
+        j.train()
+        np.random.seed(seed)
+        x = torch.arange(T, dtype=torch.float32).view(1, 1, T).repeat(2, 3, 1)
+        y = j(x.clone())
+        out[f"{p}_{T}_{seed}"] = dict(p=p, T=T, seed=seed, src=[int(v) for v in y[0, 0].tolist()],
+                                      next_uniform=float(np.random.random_sample()))
+    json.dump(out, open(HERE / "jitter.json", "w"), indent=1)
+    print("[golden] jitter:", {k: sum(a != b for a, b in zip(v["src"], range(v["T"]))) for k, v in out.items()})
+
+
+def structure_fixture():
+    from vae_npvc.model.vqvae import Model
+    out = {}
+    for name in CFGS:
+        cfg = load_cfg(name)
+        m = Model(cfg)
+        out[name] = dict(state_dict=[[k, list(v.shape)] for k, v in m.state_dict().items()],
+                         parameters=[k for k, _ in m.named_parameters()],
+                         n_params=int(sum(p.numel() for p in m.parameters())))
+        ours = [[k, list(s)] for k, s in layer_specs(cfg)]
+        assert [k for k, _ in ours] == out[name]["parameters"], "oracle parameter order != reference"
+        ref_shapes = dict((k, s) for k, s in out[name]["state_dict"])
+        for k, s in ours + [[k, list(s)] for k, s in buffer_specs(cfg)]:
+            assert ref_shapes[k] == list(s), (k, ref_shapes[k], s)
+    json.dump(out, open(HERE / "structure.json", "w"), indent=1)
+    print("[golden] structure:", {k: v["n_params"] for k, v in out.items()})
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(os.cpu_count() or 8)
+    structure_fixture()
+    jitter_fixture()
+    step_fixture("vcc20", B=4, T=128, steps=3, wseed=1001, bseed=2001, tseed=3001, nseed=4001, out_prefix="step_vcc20")
+    step_fixture("aishell3", B=4, T=128, steps=3, wseed=1002, bseed=2002, tseed=3002, nseed=4002,
+                 out_prefix="step_aishell3")
+    for K in (128, 512, 1024):
+        vq_fixture(K, 64, 256, 5000 + K, f"vq_K{K}")
+    vq_tile_fixture(6001, "vq_tile")
+    if "--no-full" not in sys.argv:
+        step_fixture("vcc20", B=64, T=256, steps=2, wseed=1003, bseed=2003, tseed=3003, nseed=4003,
+                     out_prefix="full_step_vcc20")

@@ -1,48 +1,58 @@
 // Conv1d / ConvTranspose1d (stride 1) as implicit-im2col GEMMs on gfx950 MFMA.
 //
 // One kernel template covers the three products of a conv layer:
-//   FWD   C[n][co]       = sum_{j,ci} pro(x[n+j-pad][ci]) * We[co][j][ci]
-//   DGRAD C[n][ci]       = sum_{j,co} dy[n+j-pad][co]     * We[co][k-1-j][ci]
-//   WGRAD C[r][j*cd+c]   = sum_n      p[n][r]             * pro(q[n+s(j-pad)][c])
-// C rows of FWD/DGRAD are frames (B*T), so every conv of the VQ-VAE step is a
-// GEMM with a 16,384-long M dimension at config 2.
+//   FWD   Y[n][co]      = sum_{j,ci} pro(x[n+j-pad][ci]) * We[co][j][ci]
+//   DGRAD Y[n][ci]      = sum_{j,co} dy[n+j-pad][co]     * We[co][k-1-j][ci]
+//   WGRAD S[r][j*cd+c]  = sum_n      p[n][r]             * pro(q[n+s(j-pad)][c])
+// Frames (n = b*T + t) are the long GEMM dimension: 16,384 at config 2.
 //
-// Tile: 128x128 C tile per 256-thread workgroup, 4 waves in a 2x2 grid, each
-// wave a 64x64 sub-tile = 2x2 MFMA blocks of 32x32.  bf16 operands use
-// v_mfma_f32_32x32x16_bf16 (BK=64), f32 operands v_mfma_f32_32x32x2_f32
-// (BK=32, exact fp32 fmaf chain: the parity mode).  Operands are staged
-// global->registers->LDS (double-buffered LDS, one barrier per K-tile, the
-// next tile's global loads in flight during the MFMAs), which lets the
-// staging pass apply the im2col shift/zero-padding, the activation prologue
-// (LeakyReLU/ReLU) and dtype-agnostic 16-B chunk moves.  Operands whose K
-// dimension is contiguous in memory are stored K-major in LDS and read with
-// ds_read_b128; operands whose K dimension is strided (the weight in DGRAD,
-// both operands in WGRAD) are stored as they lie in memory and read with the
-// gfx950 transposing LDS read ds_read_b64_tr_b16 (bf16) or ds_read_b32 (f32).
+// Workgroup: 256 threads, 128x128 output tile, 4 waves in 2x2, each wave a
+// 64x64 sub-tile = 2x2 MFMA blocks of 32x32.  bf16: v_mfma_f32_32x32x16_bf16,
+// BK = 64; f32 (parity mode): v_mfma_f32_32x32x2_f32, BK = 32, an exact fp32
+// fmaf chain.
+//
+// Staging: global -> registers -> LDS, double-buffered LDS, one barrier per
+// K-tile, next tile's loads in flight during the MFMAs.  Loads are raw buffer
+// loads: an offset past the descriptor's range returns zeros, which is how
+// the im2col zero padding at utterance edges, the ragged M/N edges and the
+// K tail are produced without branches.  When a K-tile lies inside one tap
+// (cin % BK == 0: every large layer) the tap shift and the channel offset are
+// folded into the wave-uniform descriptor base, so the per-chunk VALU work is
+// one select.  K-contiguous operands live K-major in LDS (ds_read_b128, XOR
+// swizzle); K-strided operands (weights in DGRAD, both operands in WGRAD) are
+// stored as they lie in memory and read with ds_read_b64_tr_b16 (bf16) or
+// ds_read_b32 (f32).
+//
+// The MFMA's first operand is the one whose index is contiguous in the output
+// (channels for FWD/DGRAD, j*cd+c for WGRAD), so each lane ends up holding 4
+// consecutive output elements per register group: the epilogue does vector
+// loads/stores (8 B bf16, 16 B f32) for bias, residual, masks and results.
 #include "vqx_common.h"
 
 namespace vqx {
 
 constexpr int kBM = 128, kBN = 128, kThreads = 256;
+constexpr unsigned kOOB = 0x80000000u;  // buffer offset that is always out of range -> loads 0
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 
 struct GemmParams {
-  const void* a;   // FWD/DGRAD: activation [N][lda]; WGRAD: p [N][lda]
-  const void* b;   // FWD/DGRAD: packed We [cout_f][ntaps*cin_f]; WGRAD: q [N][ldb]
+  const void* a;   // FWD/DGRAD: activation [N][lda]   WGRAD: p [N][lda]
+  const void* b;   // FWD/DGRAD: packed We [cout_f][ntaps*cin_f]   WGRAD: q [N][ldb]
+  int64_t a_bytes, b_bytes;
   int64_t n_rows;  // frames
   int T, lda, ldb;
   int kcin;        // FWD/DGRAD: channels per tap on the K side
   int K;           // FWD/DGRAD: ntaps*kcin
-  int Mc, Nc;      // C dims
+  int Mc, Nc;      // output dims: FWD/DGRAD rows = frames, cols = channels; WGRAD rows = r, cols = j*cd+c
   int ntaps, pad, sign;
   int cdim;        // DGRAD: cin of the forward layer (= Nc); WGRAD: c_dim
   int pro;
   float pro_scale;
   int tiles_m, tiles_n, splits;
-  int64_t k_per_split;  // WGRAD
+  int64_t k_per_split;
   // epilogue
   void* y;
-  int ldy, epi, dtype_out_f32;
+  int ldy, epi, out_f32;
   const float* bias;
   const float* rowbias;
   const void* res;
@@ -92,8 +102,20 @@ __device__ __forceinline__ uint4 pro_chunk(uint4 u, float s) {
   }
 }
 
-// tap index of a K offset (ntaps <= 3)
 __device__ __forceinline__ int tap_of(int k, int c) { return (k >= c) + (k >= 2 * c); }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_at(const void* base, int64_t shift_bytes, int64_t total_bytes) {
+  int64_t rec = total_bytes - shift_bytes;
+  if (rec < 0) rec = 0;
+  if (rec > 0x7fffffff) rec = 0x7fffffff;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + shift_bytes), (short)0, (int)rec, 0x00020000);
+}
+
+__device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
 
 // LDS byte offsets of a 16-B chunk.
 __device__ __forceinline__ int kmaj_off(int row, int ch) { return row * 128 + 16 * (ch ^ ((row >> 1) & 7)); }
@@ -104,17 +126,41 @@ __device__ __forceinline__ int mnmaj_off(int row, int ch) {
   else return row * 512 + 16 * ch;
 }
 
-template <typename T, int MODE, int PRO>
+// 4 consecutive elements (8 B bf16 / 16 B f32) at p+i
+template <typename T>
+__device__ __forceinline__ void ld4(const void* p, int64_t i, float* f) {
+  if constexpr (sizeof(T) == 2) {
+    const uint2 u = *(const uint2*)((const bf16_t*)p + i);
+    f[0] = __uint_as_float(u.x << 16); f[1] = __uint_as_float(u.x & 0xffff0000u);
+    f[2] = __uint_as_float(u.y << 16); f[3] = __uint_as_float(u.y & 0xffff0000u);
+  } else {
+    const f32x4_t v = *(const f32x4_t*)((const float*)p + i);
+    f[0] = v[0]; f[1] = v[1]; f[2] = v[2]; f[3] = v[3];
+  }
+}
+template <typename T>
+__device__ __forceinline__ void st4(void* p, int64_t i, const float* f) {
+  if constexpr (sizeof(T) == 2) {
+    uint2 u;
+    u.x = (unsigned)f2bf(f[0]) | ((unsigned)f2bf(f[1]) << 16);
+    u.y = (unsigned)f2bf(f[2]) | ((unsigned)f2bf(f[3]) << 16);
+    *(uint2*)((bf16_t*)p + i) = u;
+  } else {
+    f32x4_t v = {f[0], f[1], f[2], f[3]};
+    *(f32x4_t*)((float*)p + i) = v;
+  }
+}
+
+template <typename T, int MODE, int PRO, bool GEN>
 __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
   using C = Cfg<T>;
-  constexpr int BK = C::BK, EPC = C::EPC, CPR = C::MNCPR;
+  constexpr int BK = C::BK, EPC = C::EPC, CPR = C::MNCPR, ES = sizeof(T);
   constexpr int TILE_BYTES = 16384;
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int nwg = gridDim.x;
-  const int lin = xcd_remap(blockIdx.x, nwg);
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
   const int tiles_mn = P.tiles_m * P.tiles_n;
   const int split = lin / tiles_mn;
   const int tmn = lin - split * tiles_mn;
@@ -131,96 +177,133 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
   }
   const int nk = (kend > kbeg) ? (int)((kend - kbeg + BK - 1) / BK) : 0;
 
-  // Per-thread constant row info for the FWD/DGRAD activation operand.
-  int64_t a_n[4];
-  int a_t[4];
-  if constexpr (MODE != MODE_WGRAD) {
+  // ---------------- per-thread constant addressing (chunk i = tid + 256*i)
+  unsigned aoff[4], boff[4];
+  int amask[4];  // FWD/DGRAD: bit j set <=> tap j keeps the frame inside its utterance
+  int bsh[4];    // WGRAD: krow + shift of the q chunk
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + kThreads * i;
-      a_n[i] = (int64_t)m0 + (c >> 3);
-      a_t[i] = (int)(a_n[i] % P.T);
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + kThreads * i;
+    if constexpr (MODE != MODE_WGRAD) {
+      const int row = c >> 3, kch = c & 7;
+      const int64_t n = (int64_t)m0 + row;
+      const int t = (int)(n % P.T);
+      int msk = 0;
+      if (n < P.n_rows)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) msk |= ((t + j - P.pad >= 0) && (t + j - P.pad < P.T)) ? (1 << j) : 0;
+      amask[i] = msk;
+      aoff[i] = (unsigned)((n * P.lda + (GEN ? 0 : kch * EPC)) * ES);
+      if constexpr (MODE == MODE_FWD) {
+        const int co = n0 + row;
+        boff[i] = co < P.Nc ? (unsigned)(((int64_t)co * P.K + kch * EPC) * ES) : kOOB;
+      } else {
+        const int krow = c / CPR, cch = c % CPR;
+        const int ci = n0 + cch * EPC;
+        boff[i] = ci < P.Nc ? (unsigned)(((int64_t)krow * P.ntaps * P.cdim + ci) * ES) : kOOB;
+      }
+      bsh[i] = 0;
+    } else {
+      const int krow = c / CPR, cch = c % CPR;
+      const int r = m0 + cch * EPC;
+      aoff[i] = r < P.Mc ? (unsigned)(((int64_t)krow * P.lda + r) * ES) : kOOB;
+      const int col = n0 + cch * EPC;
+      const int j = tap_of(col, P.cdim);
+      const int cc = col - j * P.cdim;
+      const int sh = P.sign * (j - P.pad);
+      bsh[i] = krow + sh;
+      // the q descriptor base sits (ntaps-1) rows before the tile so shifted offsets stay >= 0
+      boff[i] = col < P.Nc ? (unsigned)(((int64_t)(krow + sh + P.ntaps - 1) * P.ldb + cc) * ES) : kOOB;
+      amask[i] = 0;
     }
   }
 
-  const char* A = (const char*)P.a;
-  const char* B = (const char*)P.b;
   uint4 ra[4], rb[4];
-  const uint4 zero4 = make_uint4(0, 0, 0, 0);
 
   auto load_tile = [&](int kt) {
     const int64_t k0 = kbeg + (int64_t)kt * BK;
     if constexpr (MODE != MODE_WGRAD) {
-      // A: activation, K-major rows = C rows (frames)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int c = tid + kThreads * i;
-        const int kch = c & 7;
-        const int k = (int)k0 + kch * EPC;
-        const int tap = tap_of(k, P.kcin);
-        const int ci = k - tap * P.kcin;
-        const int tt = a_t[i] + tap - P.pad;
-        const bool ok = (a_n[i] < P.n_rows) && (k < P.K) && (tt >= 0) && (tt < P.T);
-        uint4 u = zero4;
-        if (ok) u = *(const uint4*)(A + ((a_n[i] + tap - P.pad) * (int64_t)P.lda + ci) * sizeof(T));
-        ra[i] = pro_chunk<T, PRO>(u, P.pro_scale);
-      }
-      if constexpr (MODE == MODE_FWD) {
-        // B: packed weight, K-major rows = output channels
+      if constexpr (!GEN) {
+        const int tap = (int)k0 / P.kcin;
+        const int ci0 = (int)k0 - tap * P.kcin;
+        const __amdgpu_buffer_rsrc_t ra_r =
+            rsrc_at(P.a, ((int64_t)(tap - P.pad) * P.lda + ci0) * ES, P.a_bytes);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int c = tid + kThreads * i;
-          const int row = c >> 3, kch = c & 7;
-          const int co = n0 + row;
-          const int k = (int)k0 + kch * EPC;
-          uint4 u = zero4;
-          if (co < P.Nc && k < P.K) u = *(const uint4*)(B + ((int64_t)co * P.K + k) * sizeof(T));
-          rb[i] = u;
+          const unsigned off = ((amask[i] >> tap) & 1) ? aoff[i] : kOOB;
+          ra[i] = pro_chunk<T, PRO>(bload(ra_r, off), P.pro_scale);
         }
       } else {
-        // B: forward weight We[co][j][ci] read as [k=(j,co)][ci], taps flipped
+        const __amdgpu_buffer_rsrc_t ra_r = rsrc_at(P.a, 0, P.a_bytes);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int c = tid + kThreads * i;
-          const int krow = c / CPR, cch = c % CPR;
-          const int k = (int)k0 + krow;
-          const int j = tap_of(k, P.kcin);
-          const int co = k - j * P.kcin;
-          const int ci = n0 + cch * EPC;
-          uint4 u = zero4;
-          if (k < P.K && ci < P.Nc)
-            u = *(const uint4*)(B + ((int64_t)co * (P.ntaps * P.cdim) + (P.ntaps - 1 - j) * P.cdim + ci) * sizeof(T));
-          rb[i] = u;
+          const int k = (int)k0 + (c & 7) * EPC;
+          const int tap = tap_of(k, P.kcin);
+          const int ci = k - tap * P.kcin;
+          const bool ok = k < P.K && ((amask[i] >> tap) & 1);
+          const unsigned off = ok ? aoff[i] + (unsigned)((((tap - P.pad) * P.lda) + ci) * ES) : kOOB;
+          ra[i] = pro_chunk<T, PRO>(bload(ra_r, off), P.pro_scale);
+        }
+      }
+      if constexpr (MODE == MODE_FWD) {
+        const __amdgpu_buffer_rsrc_t rb_r = rsrc_at(P.b, k0 * ES, P.b_bytes);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          unsigned off = boff[i];
+          if constexpr (GEN) {
+            const int c = tid + kThreads * i;
+            if ((int)k0 + (c & 7) * EPC >= P.K) off = kOOB;
+          }
+          rb[i] = bload(rb_r, off);
+        }
+      } else {
+        if constexpr (!GEN) {
+          const int j = (int)k0 / P.kcin;
+          const int co0 = (int)k0 - j * P.kcin;
+          const __amdgpu_buffer_rsrc_t rb_r =
+              rsrc_at(P.b, ((int64_t)co0 * P.ntaps * P.cdim + (int64_t)(P.ntaps - 1 - j) * P.cdim) * ES, P.b_bytes);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) rb[i] = bload(rb_r, boff[i]);
+        } else {
+          const __amdgpu_buffer_rsrc_t rb_r = rsrc_at(P.b, 0, P.b_bytes);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int c = tid + kThreads * i;
+            const int krow = c / CPR, cch = c % CPR;
+            const int k = (int)k0 + krow;
+            const int j = tap_of(k, P.kcin);
+            const int co = k - j * P.kcin;
+            const int ci = n0 + cch * EPC;
+            const bool ok = k < P.K && ci < P.Nc;
+            rb[i] = bload(rb_r, ok ? (unsigned)(((int64_t)co * P.ntaps * P.cdim + (P.ntaps - 1 - j) * P.cdim + ci) * ES)
+                                   : kOOB);
+          }
         }
       }
     } else {
-      const int t0 = (int)(k0 % P.T);
-      const bool tfast = (P.T % BK) == 0;
+      const __amdgpu_buffer_rsrc_t ra_r = rsrc_at(P.a, k0 * P.lda * ES, P.a_bytes);
+      const __amdgpu_buffer_rsrc_t rb_r = rsrc_at(P.b, (k0 - (P.ntaps - 1)) * P.ldb * ES, P.b_bytes);
+      const int t0 = (int)((int)k0 % P.T);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int c = tid + kThreads * i;
-        const int krow = c / CPR, cch = c % CPR;
-        const int64_t n = k0 + krow;
-        const int r = m0 + cch * EPC;
-        uint4 u = zero4;
-        if (n < kend && r < P.Mc) u = *(const uint4*)(A + (n * P.lda + r) * sizeof(T));
-        ra[i] = u;
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int c = tid + kThreads * i;
-        const int krow = c / CPR, cch = c % CPR;
-        const int64_t n = k0 + krow;
-        const int col = n0 + cch * EPC;
-        const int j = tap_of(col, P.cdim);
-        const int cc = col - j * P.cdim;
-        const int sh = P.sign * (j - P.pad);
-        const int t = tfast ? t0 + krow : (int)(n % P.T);
-        const int tt = t + sh;
-        uint4 u = zero4;
-        if (n < kend && col < P.Nc && tt >= 0 && tt < P.T)
-          u = *(const uint4*)(B + ((n + sh) * P.ldb + cc) * sizeof(T));
-        rb[i] = pro_chunk<T, PRO>(u, P.pro_scale);
+        unsigned offa = aoff[i];
+        if constexpr (GEN) {
+          const int c = tid + kThreads * i;
+          if (k0 + c / CPR >= kend) offa = kOOB;
+        }
+        ra[i] = bload(ra_r, offa);
+        int tt;
+        if constexpr (!GEN) {
+          tt = t0 + bsh[i];
+        } else {
+          const int c = tid + kThreads * i;
+          const int64_t n = k0 + c / CPR;
+          tt = (int)(n % P.T) + (bsh[i] - c / CPR);
+          if (n >= kend) tt = -1;
+        }
+        const unsigned offb = (tt >= 0 && tt < P.T) ? boff[i] : kOOB;
+        rb[i] = pro_chunk<T, PRO>(bload(rb_r, offb), P.pro_scale);
       }
     }
   };
@@ -231,19 +314,16 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int c = tid + kThreads * i;
-      if constexpr (MODE != MODE_WGRAD) {
-        *(uint4*)(la + kmaj_off(c >> 3, c & 7)) = ra[i];
-      } else {
-        *(uint4*)(la + mnmaj_off<T>(c / CPR, c % CPR)) = ra[i];
-      }
-      if constexpr (MODE == MODE_FWD) {
-        *(uint4*)(lb + kmaj_off(c >> 3, c & 7)) = rb[i];
-      } else {
-        *(uint4*)(lb + mnmaj_off<T>(c / CPR, c % CPR)) = rb[i];
-      }
+      if constexpr (MODE != MODE_WGRAD) *(uint4*)(la + kmaj_off(c >> 3, c & 7)) = ra[i];
+      else *(uint4*)(la + mnmaj_off<T>(c / CPR, c % CPR)) = ra[i];
+      if constexpr (MODE == MODE_FWD) *(uint4*)(lb + kmaj_off(c >> 3, c & 7)) = rb[i];
+      else *(uint4*)(lb + mnmaj_off<T>(c / CPR, c % CPR)) = rb[i];
     }
   };
 
+  // acc[mi][ni]: mi = 32-block of the "row" operand (A tile), ni = of the B tile.
+  // MFMA D = first(32 x k) * second(k x 32): first = B-tile fragment (contiguous
+  // output index), second = A-tile fragment; D[row of first][col of second].
   f32x16_t acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -261,49 +341,32 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
     constexpr bool B_KMAJ = (MODE == MODE_FWD);
     if constexpr (sizeof(T) == 2) {
       const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+      typedef short s16x8_t __attribute__((ext_vector_type(8)));
+      auto tr_frag = [&](const char* base, int colbase, int s) {
+        const int kb = 16 * s + (g >> 1) * 8;
+        const int ch = (colbase >> 3) + (p >> 1);
+        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (VQX_LDS(s16x4_t)*)(base + mnmaj_off<T>(kb + q, ch) + 8 * (p & 1)));
+        const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (VQX_LDS(s16x4_t)*)(base + mnmaj_off<T>(kb + 4 + q, ch) + 8 * (p & 1)));
+        const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(bf16x8_t, v);
+      };
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         bf16x8_t af[2], bfr[2];
 #pragma unroll
         for (int x = 0; x < 2; ++x) {
-          if constexpr (A_KMAJ) {
-            const int row = wm * 64 + x * 32 + r32;
-            af[x] = *(const bf16x8_t*)(la + kmaj_off(row, 2 * s + h));
-          } else {
-            const int colbase = wm * 64 + x * 32 + (g & 1) * 16;
-            const int kb = 16 * s + (g >> 1) * 8;
-            const int r0 = kb + q, r1 = kb + 4 + q;
-            const int ch = (colbase >> 3) + (p >> 1);
-            s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (VQX_LDS(s16x4_t)*)(la + mnmaj_off<T>(r0, ch) + 8 * (p & 1)));
-            s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (VQX_LDS(s16x4_t)*)(la + mnmaj_off<T>(r1, ch) + 8 * (p & 1)));
-            typedef short s16x8_t __attribute__((ext_vector_type(8)));
-            s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            af[x] = __builtin_bit_cast(bf16x8_t, v);
-          }
-          if constexpr (B_KMAJ) {
-            const int row = wn * 64 + x * 32 + r32;
-            bfr[x] = *(const bf16x8_t*)(lb + kmaj_off(row, 2 * s + h));
-          } else {
-            const int colbase = wn * 64 + x * 32 + (g & 1) * 16;
-            const int kb = 16 * s + (g >> 1) * 8;
-            const int r0 = kb + q, r1 = kb + 4 + q;
-            const int ch = (colbase >> 3) + (p >> 1);
-            s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (VQX_LDS(s16x4_t)*)(lb + mnmaj_off<T>(r0, ch) + 8 * (p & 1)));
-            s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (VQX_LDS(s16x4_t)*)(lb + mnmaj_off<T>(r1, ch) + 8 * (p & 1)));
-            typedef short s16x8_t __attribute__((ext_vector_type(8)));
-            s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            bfr[x] = __builtin_bit_cast(bf16x8_t, v);
-          }
+          if constexpr (A_KMAJ) af[x] = *(const bf16x8_t*)(la + kmaj_off(wm * 64 + x * 32 + r32, 2 * s + h));
+          else af[x] = tr_frag(la, wm * 64 + x * 32 + (g & 1) * 16, s);
+          if constexpr (B_KMAJ) bfr[x] = *(const bf16x8_t*)(lb + kmaj_off(wn * 64 + x * 32 + r32, 2 * s + h));
+          else bfr[x] = tr_frag(lb, wn * 64 + x * 32 + (g & 1) * 16, s);
         }
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
           for (int ni = 0; ni < 2; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[ni], af[mi], acc[mi][ni], 0, 0, 0);
       }
     } else {
 #pragma unroll
@@ -312,16 +375,14 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
 #pragma unroll
         for (int x = 0; x < 2; ++x) {
           if constexpr (A_KMAJ) {
-            const int row = wm * 64 + x * 32 + r32;
-            af[x] = *(const f32x4_t*)(la + kmaj_off(row, 2 * s + h));
+            af[x] = *(const f32x4_t*)(la + kmaj_off(wm * 64 + x * 32 + r32, 2 * s + h));
           } else {
             const int col = wm * 64 + x * 32 + r32;
 #pragma unroll
             for (int qq = 0; qq < 4; ++qq) af[x][qq] = *(const float*)(la + (8 * s + 4 * h + qq) * 512 + col * 4);
           }
           if constexpr (B_KMAJ) {
-            const int row = wn * 64 + x * 32 + r32;
-            bfr[x] = *(const f32x4_t*)(lb + kmaj_off(row, 2 * s + h));
+            bfr[x] = *(const f32x4_t*)(lb + kmaj_off(wn * 64 + x * 32 + r32, 2 * s + h));
           } else {
             const int col = wn * 64 + x * 32 + r32;
 #pragma unroll
@@ -334,7 +395,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
           for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
             for (int ni = 0; ni < 2; ++ni)
-              acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[mi][qq], bfr[ni][qq], acc[mi][ni], 0, 0, 0);
+              acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(bfr[ni][qq], af[mi][qq], acc[mi][ni], 0, 0, 0);
       }
     }
   };
@@ -352,109 +413,147 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
     }
   }
 
-  // ---------------- epilogue ----------------
+  // ---------------- epilogue
+  // lane holds output row (A-tile index) R = m0 + wm*64 + mi*32 + r32 and, per
+  // register group gq, output columns Cb = n0 + wn*64 + ni*32 + 8*gq + 4*h + (0..3).
   if constexpr (MODE == MODE_WGRAD) {
     float* out = (float*)P.y + (int64_t)split * P.Mc * P.Nc;
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
+    for (int mi = 0; mi < 2; ++mi) {
+      const int row = m0 + wm * 64 + mi * 32 + r32;
+      if (row >= P.Mc) continue;
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni) {
-        const int col = n0 + wn * 64 + ni * 32 + r32;
+      for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int row = m0 + wm * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-          if (row < P.Mc && col < P.Nc) out[(int64_t)row * P.Nc + col] = acc[mi][ni][e];
+        for (int gq = 0; gq < 4; ++gq) {
+          const int col = n0 + wn * 64 + ni * 32 + 8 * gq + 4 * h;
+          if (col >= P.Nc) continue;  // Nc % 4 == 0
+          f32x4_t v = {acc[mi][ni][4 * gq], acc[mi][ni][4 * gq + 1], acc[mi][ni][4 * gq + 2], acc[mi][ni][4 * gq + 3]};
+          *(f32x4_t*)(out + (int64_t)row * P.Nc + col) = v;
         }
-      }
+    }
   } else {
     const int epi = P.epi;
-    const int odt = P.dtype_out_f32 ? VQX_F32 : (sizeof(T) == 2 ? VQX_BF16 : VQX_F32);
-    constexpr int idt = sizeof(T) == 2 ? VQX_BF16 : VQX_F32;
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
+    for (int mi = 0; mi < 2; ++mi) {
+      const int64_t row = (int64_t)m0 + wm * 64 + mi * 32 + r32;
+      if (row >= P.n_rows) continue;
+      const int bidx = (epi & (VQX_EPI_ROWBIAS | VQX_EPI_GNADD)) ? (int)(row / P.T) : 0;
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni) {
-        const int col = n0 + wn * 64 + ni * 32 + r32;
-        if (col >= P.Nc) continue;
-        float bcol = (epi & VQX_EPI_BIAS) ? P.bias[col] : 0.f;
-        float gam = 0.f, bet = 0.f;
-        if (epi & VQX_EPI_GNADD) { gam = P.gn_gamma[col]; bet = P.gn_beta[col]; }
-        const bool to2 = (epi & VQX_EPI_SPLIT) && col >= P.split_col;
+      for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int64_t row = (int64_t)m0 + wm * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-          if (row >= P.n_rows) continue;
-          float v = acc[mi][ni][e] + bcol;
-          int bidx = 0;
-          if (epi & (VQX_EPI_ROWBIAS | VQX_EPI_GNADD)) bidx = (int)(row / P.T);
-          if (epi & VQX_EPI_ROWBIAS) v += P.rowbias[(int64_t)bidx * P.Nc + col];
-          if (epi & VQX_EPI_MASK) {
-            const float mv = ld_dt(P.mask, row * P.ldmask + col, idt);
-            v *= (mv > 0.f ? 1.f : P.mask_slope) * P.mask_scale;
+        for (int gq = 0; gq < 4; ++gq) {
+          const int col = n0 + wn * 64 + ni * 32 + 8 * gq + 4 * h;
+          if (col >= P.Nc) continue;  // Nc % 4 == 0
+          float v[4] = {acc[mi][ni][4 * gq], acc[mi][ni][4 * gq + 1], acc[mi][ni][4 * gq + 2], acc[mi][ni][4 * gq + 3]};
+          if (epi & VQX_EPI_BIAS) {
+            const f32x4_t bb = *(const f32x4_t*)(P.bias + col);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += bb[e];
           }
-          if (to2) {
+          if (epi & VQX_EPI_ROWBIAS) {
+            const f32x4_t rb4 = *(const f32x4_t*)(P.rowbias + (int64_t)bidx * P.Nc + col);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += rb4[e];
+          }
+          if (epi & VQX_EPI_MASK) {
+            float mk[4];
+            ld4<T>(P.mask, row * P.ldmask + col, mk);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] *= (mk[e] > 0.f ? 1.f : P.mask_slope) * P.mask_scale;
+          }
+          if ((epi & VQX_EPI_SPLIT) && col >= P.split_col) {
             float* o2 = P.out2 + row * P.ldo2 + (col - P.split_col);
-            *o2 = P.out2_acc ? (*o2 + v) : v;
+            f32x4_t cur = {0.f, 0.f, 0.f, 0.f};
+            if (P.out2_acc) cur = *(const f32x4_t*)o2;
+            f32x4_t nv = {cur[0] + v[0], cur[1] + v[1], cur[2] + v[2], cur[3] + v[3]};
+            *(f32x4_t*)o2 = nv;
             continue;
           }
-          if (epi & VQX_EPI_RES) v += ld_dt(P.res, row * P.ldres + col, idt);
-          if (epi & VQX_EPI_GNADD) {
-            const float hv = ld_dt(P.gn_h, row * P.ldgn + col, idt);
-            v += (hv - P.gn_mr[2 * bidx]) * P.gn_mr[2 * bidx + 1] * gam + bet;
+          if (epi & VQX_EPI_RES) {
+            float rr[4];
+            ld4<T>(P.res, row * P.ldres + col, rr);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += rr[e];
           }
-          st_dt(P.y, row * P.ldy + col, v, odt);
+          if (epi & VQX_EPI_GNADD) {
+            float hv[4];
+            ld4<T>(P.gn_h, row * P.ldgn + col, hv);
+            const float mean = P.gn_mr[2 * bidx], rstd = P.gn_mr[2 * bidx + 1];
+            const f32x4_t ga = *(const f32x4_t*)(P.gn_gamma + col);
+            const f32x4_t be = *(const f32x4_t*)(P.gn_beta + col);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += (hv[e] - mean) * rstd * ga[e] + be[e];
+          }
+          if (P.out_f32) st4<float>(P.y, row * P.ldy + col, v);
+          else st4<T>(P.y, row * P.ldy + col, v);
         }
-      }
+    }
+  }
+}
+
+template <typename T, int MODE, bool GEN>
+static void launch_pro(const GemmParams& P, int grid, hipStream_t s) {
+  switch (P.pro) {
+    case VQX_PRO_NONE: hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, VQX_PRO_NONE, GEN>), dim3(grid), dim3(kThreads), 0, s, P); break;
+    case VQX_PRO_LRELU: hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, VQX_PRO_LRELU, GEN>), dim3(grid), dim3(kThreads), 0, s, P); break;
+    case VQX_PRO_RELU: hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, VQX_PRO_RELU, GEN>), dim3(grid), dim3(kThreads), 0, s, P); break;
+    default: hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, VQX_PRO_SCALE_RELU, GEN>), dim3(grid), dim3(kThreads), 0, s, P); break;
   }
 }
 
 template <typename T, int MODE>
-static void launch_mode(const GemmParams& P, int grid, hipStream_t s) {
-  switch (P.pro) {
-    case VQX_PRO_NONE: hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, VQX_PRO_NONE>), dim3(grid), dim3(kThreads), 0, s, P); break;
-    case VQX_PRO_LRELU: hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, VQX_PRO_LRELU>), dim3(grid), dim3(kThreads), 0, s, P); break;
-    case VQX_PRO_RELU: hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, VQX_PRO_RELU>), dim3(grid), dim3(kThreads), 0, s, P); break;
-    default: hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, VQX_PRO_SCALE_RELU>), dim3(grid), dim3(kThreads), 0, s, P); break;
-  }
+static void launch_mode(const GemmParams& P, int grid, bool gen, hipStream_t s) {
+  if (gen) launch_pro<T, MODE, true>(P, grid, s);
+  else launch_pro<T, MODE, false>(P, grid, s);
 }
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 static int conv_common(const vqx_conv_args* a, int mode, hipStream_t s) {
   if (!a) { set_error("vqx_conv: null args"); return -1; }
-  const int epc = a->dtype == VQX_BF16 ? 8 : 4;
   if (a->dtype != VQX_F32 && a->dtype != VQX_BF16) { set_error("vqx_conv: bad dtype %d", a->dtype); return -1; }
-  if (a->ntaps < 1 || a->ntaps > 3) { set_error("vqx_conv: ntaps %d not in [1,3]", a->ntaps); return -1; }
+  const int epc = a->dtype == VQX_BF16 ? 8 : 4;
+  const int es = a->dtype == VQX_BF16 ? 2 : 4;
+  const int bk = a->dtype == VQX_BF16 ? 64 : 32;
+  if (a->ntaps < 1 || a->ntaps > 3 || a->pad < 0 || a->pad >= a->ntaps + 1) { set_error("vqx_conv: ntaps %d / pad %d", a->ntaps, a->pad); return -1; }
   if (a->n_rows <= 0 || a->T <= 0 || a->n_rows % a->T) { set_error("vqx_conv: n_rows %lld not a multiple of T %d", (long long)a->n_rows, a->T); return -1; }
-  if (a->cin <= 0 || a->cout <= 0 || a->cin % epc || a->ldx % epc) { set_error("vqx_conv: cin %d / ldx %d must be multiples of %d", a->cin, a->ldx, epc); return -1; }
+  if (a->cin <= 0 || a->cout <= 0 || a->cin % epc || a->ldx % epc || a->cin > a->ldx) { set_error("vqx_conv: cin %d / ldx %d must be multiples of %d", a->cin, a->ldx, epc); return -1; }
+  if (a->cout % 4 || a->ldy % 4) { set_error("vqx_conv: cout %d / ldy %d must be multiples of 4", a->cout, a->ldy); return -1; }
   if (mode == MODE_DGRAD && a->cout % epc) { set_error("vqx_conv_dgrad: cout %d must be a multiple of %d", a->cout, epc); return -1; }
   if (!aligned16(a->x) || !aligned16(a->w)) { set_error("vqx_conv: x/w must be 16-byte aligned"); return -1; }
   if (a->prologue < 0 || a->prologue > 3 || (mode == MODE_DGRAD && a->prologue)) { set_error("vqx_conv: bad prologue %d", a->prologue); return -1; }
-  if ((a->epilogue & VQX_EPI_BIAS) && !a->bias) { set_error("vqx_conv: BIAS without bias"); return -1; }
-  if ((a->epilogue & VQX_EPI_ROWBIAS) && !a->rowbias) { set_error("vqx_conv: ROWBIAS without rowbias"); return -1; }
-  if ((a->epilogue & VQX_EPI_RES) && !a->res) { set_error("vqx_conv: RES without res"); return -1; }
-  if ((a->epilogue & VQX_EPI_MASK) && !a->mask) { set_error("vqx_conv: MASK without mask"); return -1; }
-  if ((a->epilogue & VQX_EPI_GNADD) && !(a->gn_h && a->gn_mean_rstd && a->gn_gamma && a->gn_beta)) { set_error("vqx_conv: GNADD operands missing"); return -1; }
-  if ((a->epilogue & VQX_EPI_SPLIT) && !a->out2) { set_error("vqx_conv: SPLIT without out2"); return -1; }
+  const int epi = a->epilogue;
+  if ((epi & VQX_EPI_BIAS) && (!a->bias || !aligned16(a->bias))) { set_error("vqx_conv: BIAS needs a 16-B aligned bias"); return -1; }
+  if ((epi & VQX_EPI_ROWBIAS) && (!a->rowbias || !aligned16(a->rowbias))) { set_error("vqx_conv: ROWBIAS needs an aligned rowbias"); return -1; }
+  if ((epi & VQX_EPI_RES) && (!a->res || a->ldres % 4)) { set_error("vqx_conv: RES operand"); return -1; }
+  if ((epi & VQX_EPI_MASK) && (!a->mask || a->ldmask % 4)) { set_error("vqx_conv: MASK operand"); return -1; }
+  if ((epi & VQX_EPI_GNADD) && !(a->gn_h && a->gn_mean_rstd && a->gn_gamma && a->gn_beta && a->ldgn % 4 == 0)) { set_error("vqx_conv: GNADD operands"); return -1; }
+  if ((epi & VQX_EPI_SPLIT) && (!a->out2 || a->split_col % 4 || a->ldo2 % 4)) { set_error("vqx_conv: SPLIT operands"); return -1; }
   if (!a->y) { set_error("vqx_conv: null y"); return -1; }
 
   GemmParams P = {};
-  P.a = a->x; P.b = a->w; P.n_rows = a->n_rows; P.T = a->T; P.lda = a->ldx;
+  P.a = a->x; P.b = a->w;
+  P.a_bytes = ((a->n_rows - 1) * (int64_t)a->ldx + a->cin) * es;
+  P.n_rows = a->n_rows; P.T = a->T; P.lda = a->ldx;
   P.kcin = a->cin; P.K = a->ntaps * a->cin; P.Mc = (int)a->n_rows; P.Nc = a->cout;
+  P.b_bytes = (int64_t)a->ntaps * a->cin * a->cout * es;  // packed weight, either orientation
   P.ntaps = a->ntaps; P.pad = a->pad; P.sign = 1;
-  P.cdim = a->cout;  // DGRAD: cin of the forward layer
+  P.cdim = a->cout;
   P.pro = a->prologue; P.pro_scale = a->pro_scale;
   P.tiles_m = (int)((a->n_rows + kBM - 1) / kBM); P.tiles_n = (a->cout + kBN - 1) / kBN; P.splits = 1;
-  P.y = a->y; P.ldy = a->ldy; P.epi = a->epilogue; P.dtype_out_f32 = (a->epilogue & VQX_EPI_OUTF32) ? 1 : 0;
+  P.y = a->y; P.ldy = a->ldy; P.epi = epi; P.out_f32 = (epi & VQX_EPI_OUTF32) ? 1 : 0;
   P.bias = a->bias; P.rowbias = a->rowbias; P.res = a->res; P.ldres = a->ldres;
   P.mask = a->mask; P.ldmask = a->ldmask; P.mask_slope = a->mask_slope; P.mask_scale = a->mask_scale;
   P.gn_h = a->gn_h; P.ldgn = a->ldgn; P.gn_mr = a->gn_mean_rstd; P.gn_gamma = a->gn_gamma; P.gn_beta = a->gn_beta;
   P.out2 = a->out2; P.ldo2 = a->ldo2; P.split_col = a->split_col; P.out2_acc = a->out2_accumulate;
+  if (P.a_bytes > 0x7fffffffLL || P.b_bytes > 0x7fffffffLL) { set_error("vqx_conv: operand larger than 2 GiB"); return -1; }
+  const bool gen = (a->cin % bk) != 0;
   const int grid = P.tiles_m * P.tiles_n;
   if (a->dtype == VQX_BF16) {
-    if (mode == MODE_FWD) launch_mode<bf16_t, MODE_FWD>(P, grid, s); else launch_mode<bf16_t, MODE_DGRAD>(P, grid, s);
+    if (mode == MODE_FWD) launch_mode<bf16_t, MODE_FWD>(P, grid, gen, s); else launch_mode<bf16_t, MODE_DGRAD>(P, grid, gen, s);
   } else {
-    if (mode == MODE_FWD) launch_mode<float, MODE_FWD>(P, grid, s); else launch_mode<float, MODE_DGRAD>(P, grid, s);
+    if (mode == MODE_FWD) launch_mode<float, MODE_FWD>(P, grid, gen, s); else launch_mode<float, MODE_DGRAD>(P, grid, gen, s);
   }
   return launch_status(mode == MODE_FWD ? "vqx_conv1d_fwd" : "vqx_conv1d_dgrad");
 }
@@ -475,15 +574,19 @@ extern "C" int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream) {
   if (!a) { set_error("vqx_conv1d_wgrad: null args"); return -1; }
   if (a->dtype != VQX_F32 && a->dtype != VQX_BF16) { set_error("vqx_conv1d_wgrad: bad dtype"); return -1; }
   const int epc = a->dtype == VQX_BF16 ? 8 : 4;
+  const int es = a->dtype == VQX_BF16 ? 2 : 4;
+  const int BK = a->dtype == VQX_BF16 ? 64 : 32;
   if (a->ntaps < 1 || a->ntaps > 3) { set_error("vqx_conv1d_wgrad: ntaps %d", a->ntaps); return -1; }
   if (a->n_rows <= 0 || a->T <= 0 || a->n_rows % a->T) { set_error("vqx_conv1d_wgrad: bad n_rows/T"); return -1; }
   if (a->r_dim % epc || a->c_dim % epc || a->ldp % epc || a->ldq % epc) { set_error("vqx_conv1d_wgrad: dims must be multiples of %d", epc); return -1; }
   if (a->splits < 1) { set_error("vqx_conv1d_wgrad: splits < 1"); return -1; }
-  if (!aligned16(a->p) || !aligned16(a->q) || !a->slabs) { set_error("vqx_conv1d_wgrad: bad pointers"); return -1; }
+  if (!aligned16(a->p) || !aligned16(a->q) || !a->slabs || !aligned16(a->slabs)) { set_error("vqx_conv1d_wgrad: bad pointers"); return -1; }
   if (a->shift_sign != 1 && a->shift_sign != -1) { set_error("vqx_conv1d_wgrad: shift_sign must be +-1"); return -1; }
-  const int BK = a->dtype == VQX_BF16 ? 64 : 32;
   GemmParams P = {};
   P.a = a->p; P.b = a->q; P.n_rows = a->n_rows; P.T = a->T; P.lda = a->ldp; P.ldb = a->ldq;
+  P.a_bytes = ((a->n_rows - 1) * (int64_t)a->ldp + a->r_dim) * es;
+  P.b_bytes = ((a->n_rows - 1) * (int64_t)a->ldq + a->c_dim) * es;
+  if (P.a_bytes > 0x7fffffffLL || P.b_bytes > 0x7fffffffLL) { set_error("vqx_conv1d_wgrad: operand larger than 2 GiB"); return -1; }
   P.Mc = a->r_dim; P.Nc = a->ntaps * a->c_dim; P.ntaps = a->ntaps; P.pad = a->pad; P.sign = a->shift_sign;
   P.cdim = a->c_dim; P.pro = a->q_prologue; P.pro_scale = a->pro_scale;
   P.tiles_m = (P.Mc + kBM - 1) / kBM; P.tiles_n = (P.Nc + kBN - 1) / kBN; P.splits = a->splits;
@@ -491,9 +594,10 @@ extern "C" int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream) {
   kps = (kps + BK - 1) / BK * BK;
   P.k_per_split = kps;
   P.y = a->slabs;
+  const bool gen = (a->T % BK) != 0 || (a->n_rows % BK) != 0;
   const int grid = P.tiles_m * P.tiles_n * P.splits;
   hipStream_t s = (hipStream_t)stream;
-  if (a->dtype == VQX_BF16) launch_mode<bf16_t, MODE_WGRAD>(P, grid, s);
-  else launch_mode<float, MODE_WGRAD>(P, grid, s);
+  if (a->dtype == VQX_BF16) launch_mode<bf16_t, MODE_WGRAD>(P, grid, gen, s);
+  else launch_mode<float, MODE_WGRAD>(P, grid, gen, s);
   return launch_status("vqx_conv1d_wgrad");
 }

@@ -40,10 +40,10 @@ __global__ __launch_bounds__(256) void wn_pack_kernel(const vqx_wn_layer* __rest
     const int co = (int)(r / K);
     float w;
     if (l.kind == 0) {
-      const float sc = l.g[co] / l.norm[co];
+      const float sc = l.g ? l.g[co] / l.norm[co] : 1.f;
       w = l.v[((int64_t)co * cin + ci) * K + j] * sc;
     } else {
-      const float sc = l.g[ci] / l.norm[ci];
+      const float sc = l.g ? l.g[ci] / l.norm[ci] : 1.f;
       w = l.v[((int64_t)ci * cout + co) * K + (K - 1 - j)] * sc;
     }
     st_dt(l.w_packed, e, w, l.dtype);
@@ -75,6 +75,10 @@ __global__ __launch_bounds__(256) void wn_bwd_kernel(const vqx_wn_layer* __restr
     dot = fmaf(s, v[vi], dot);
   }
   dot = block_sum(dot, red);  // includes __syncthreads: dw[] complete
+  if (!l.g) {  // plain weight (weight norm removed): dv is the weight gradient itself
+    for (int i = threadIdx.x; i < cols; i += blockDim.x) l.dv[(int64_t)o * cols + i] = dw[i];
+    return;
+  }
   const float nrm = l.norm[o];
   const float gg = l.g[o];
   const float dg = dot / nrm;
@@ -87,6 +91,7 @@ __global__ __launch_bounds__(256) void wn_bwd_kernel(const vqx_wn_layer* __restr
 // Partial moments per (b, g, part): two-pass within the part (mean, then
 // centred sum of squares), combined with Chan's formula in finalize.
 constexpr int kGnParts = 8;
+constexpr int kGnBwdParts = 32;  // row parts of the GroupNorm-backward reduction
 
 template <typename T>
 __global__ __launch_bounds__(256) void gn_partial_kernel(const T* __restrict__ x, int ldx, int T_, int C, int G,
@@ -140,150 +145,333 @@ __global__ void gn_finalize_kernel(const float* __restrict__ part, int nbg, floa
   mr[2 * bg + 1] = 1.0f / sqrtf(var + eps);
 }
 
-// g = tanh(GN(u)[:, :half]) * sigmoid(GN(u)[:, half:]), GroupNorm with G=2.
-template <typename T>
-__global__ __launch_bounds__(256) void gn_glu_fwd_kernel(const T* __restrict__ u, int ldu, T* __restrict__ g, int ldg,
-                                                         int64_t n_rows, int T_, int half, const float* __restrict__ mr,
-                                                         const float* __restrict__ gamma, const float* __restrict__ beta) {
-  const int64_t total = n_rows * half;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t n = e / half;
-    const int c = (int)(e - n * half);
-    const int b = (int)(n / T_);
-    const float ua = Elem<T>::ld(u, n * ldu + c), ub = Elem<T>::ld(u, n * ldu + c + half);
-    const float ha = (ua - mr[4 * b + 0]) * mr[4 * b + 1] * gamma[c] + beta[c];
-    const float hb = (ub - mr[4 * b + 2]) * mr[4 * b + 3] * gamma[c + half] + beta[c + half];
-    const float sg = 1.f / (1.f + expf(-hb));
-    Elem<T>::st(g, n * ldg + c, tanhf(ha) * sg);
-  }
-}
+// fast sigmoid / tanh on v_exp_f32 (|rel err| ~1e-7, far inside the parity tolerance)
+__device__ __forceinline__ float fsigmoid(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float ftanh(float x) { return 2.f / (1.f + __expf(-2.f * x)) - 1.f; }
 
-// dL/dh (gradient w.r.t. the GroupNorm output) of channel c at row n.
-template <typename T>
-__device__ __forceinline__ float gn_bwd_dh(const T* dy, int lddy, const T* u, int ldu, int64_t n, int c, int C,
-                                           int glu, int b, const float* mr, const float* gamma, const float* beta,
-                                           float* xhat_out) {
-  const int G = glu ? 2 : 0;  // glu implies G == 2
-  (void)G;
-  if (!glu) {
-    // caller supplies xhat via mr group 0..G-1 outside
-    return Elem<T>::ld(dy, n * lddy + c);
+// ---- 16-byte chunk helpers (8 bf16 or 4 f32 per chunk) -------------------
+template <typename T> struct Vec;
+template <> struct Vec<bf16_t> {
+  static constexpr int N = 8;
+  __device__ static __forceinline__ void load(const bf16_t* p, float* f) {
+    const uint4 u = *(const uint4*)p;
+    const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { f[2 * i] = __uint_as_float(w[i] << 16); f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u); }
   }
-  const int half = C / 2;
-  const int ca = c < half ? c : c - half;
-  const float ua = Elem<T>::ld(u, n * ldu + ca), ub = Elem<T>::ld(u, n * ldu + ca + half);
-  const float xa = (ua - mr[4 * b + 0]) * mr[4 * b + 1];
-  const float xb = (ub - mr[4 * b + 2]) * mr[4 * b + 3];
-  const float ha = xa * gamma[ca] + beta[ca];
-  const float hb = xb * gamma[ca + half] + beta[ca + half];
-  const float ta = tanhf(ha);
-  const float sb = 1.f / (1.f + expf(-hb));
-  const float dg = Elem<T>::ld(dy, n * lddy + ca);
-  if (c < half) {
-    *xhat_out = xa;
-    return dg * sb * (1.f - ta * ta);
+  __device__ static __forceinline__ void store(bf16_t* p, const float* f) {
+    unsigned w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (unsigned)f2bf(f[2 * i]) | ((unsigned)f2bf(f[2 * i + 1]) << 16);
+    *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
   }
-  *xhat_out = xb;
-  return dg * ta * (sb * (1.f - sb));
-}
+};
+template <> struct Vec<float> {
+  static constexpr int N = 4;
+  __device__ static __forceinline__ void load(const float* p, float* f) {
+    const f32x4_t v = *(const f32x4_t*)p;
+    f[0] = v[0]; f[1] = v[1]; f[2] = v[2]; f[3] = v[3];
+  }
+  __device__ static __forceinline__ void store(float* p, const float* f) {
+    f32x4_t v = {f[0], f[1], f[2], f[3]};
+    *(f32x4_t*)p = v;
+  }
+};
 
-// pass 1: per (b, part) sums  S1_g = sum gamma*dh, S2_g = sum gamma*dh*xhat
+// GroupNorm partial moments, vectorised: block (part p, utterance-group bg);
+// thread = (chunk of the group's columns, row group).  Requires the group's
+// chunk count cpr to divide 256.
 template <typename T>
-__global__ __launch_bounds__(256) void gn_bwd_reduce_kernel(const T* __restrict__ dy, int lddy, const T* __restrict__ u,
-                                                            int ldu, int T_, int C, int G, int glu,
-                                                            const float* __restrict__ mr, const float* __restrict__ gamma,
-                                                            const float* __restrict__ beta, float* __restrict__ part) {
-  const int p = blockIdx.x, b = blockIdx.y;
+__global__ __launch_bounds__(256) void gn_partial_vec_kernel(const T* __restrict__ x, int ldx, int T_, int C, int G,
+                                                             int cpr, float* __restrict__ part) {
+  constexpr int V = Vec<T>::N;
+  const int p = blockIdx.x, bg = blockIdx.y;
+  const int b = bg / G, g = bg - b * G;
+  const int cg = C / G;
   const int r0 = p * T_ / kGnParts, r1 = (p + 1) * T_ / kGnParts;
-  const int cg = C / G;
+  const int ch = threadIdx.x % cpr, rg = threadIdx.x / cpr, nrg = 256 / cpr;
   __shared__ float red[16];
-  for (int g = 0; g < G; ++g) {
-    float s1 = 0.f, s2 = 0.f;
-    const int64_t cnt = (int64_t)(r1 - r0) * cg;
-    for (int64_t i = threadIdx.x; i < cnt; i += blockDim.x) {
-      const int64_t rr = i / cg;
-      const int c = g * cg + (int)(i - rr * cg);
-      const int64_t n = (int64_t)b * T_ + r0 + rr;
-      float xh;
-      float dh;
-      if (glu) {
-        dh = gn_bwd_dh<T>(dy, lddy, u, ldu, n, c, C, 1, b, mr, gamma, beta, &xh);
-      } else {
-        dh = Elem<T>::ld(dy, n * lddy + c);
-        xh = (Elem<T>::ld(u, n * ldu + c) - mr[(b * G + g) * 2]) * mr[(b * G + g) * 2 + 1];
-      }
-      const float gd = gamma[c] * dh;
-      s1 += gd;
-      s2 = fmaf(gd, xh, s2);
-    }
-    s1 = block_sum(s1, red);
-    __syncthreads();
-    s2 = block_sum(s2, red);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      float* o = part + (((int64_t)b * kGnParts + p) * G + g) * 2;
-      o[0] = s1;
-      o[1] = s2;
-    }
+  const T* base = x + ((int64_t)b * T_) * ldx + g * cg + ch * V;
+  float s = 0.f;
+  for (int r = r0 + rg; r < r1; r += nrg) {
+    float f[V];
+    Vec<T>::load(base + (int64_t)r * ldx, f);
+#pragma unroll
+    for (int i = 0; i < V; ++i) s += f[i];
+  }
+  s = block_sum(s, red);
+  const int64_t cnt = (int64_t)(r1 - r0) * cg;
+  const float mean = cnt ? s / (float)cnt : 0.f;
+  float m2 = 0.f;
+  for (int r = r0 + rg; r < r1; r += nrg) {
+    float f[V];
+    Vec<T>::load(base + (int64_t)r * ldx, f);
+#pragma unroll
+    for (int i = 0; i < V; ++i) { const float d = f[i] - mean; m2 = fmaf(d, d, m2); }
+  }
+  m2 = block_sum(m2, red);
+  if (threadIdx.x == 0) {
+    float* o = part + ((int64_t)bg * kGnParts + p) * 3;
+    o[0] = (float)cnt;
+    o[1] = mean;
+    o[2] = m2;
   }
 }
 
-// pass 2: du and per-(b, c) column sums.  Block: one utterance b, 64 columns.
+// Gradient w.r.t. the GroupNorm output h for a chunk of V channels.
+//   glu: channels [c, c+V) of the tanh half AND [c+half, c+half+V) of the
+//        sigmoid half (dy = dL/dg has `half` columns);
+//   else: channels [c, c+V) (dy = dL/dh), single group set by the caller.
 template <typename T>
-__global__ __launch_bounds__(256) void gn_bwd_apply_kernel(const T* __restrict__ dy, int lddy, const T* __restrict__ u,
-                                                           int ldu, T* __restrict__ du, int lddu, int T_, int C, int G,
-                                                           int glu, const float* __restrict__ mr,
-                                                           const float* __restrict__ gamma,
-                                                           const float* __restrict__ beta,
-                                                           const float* __restrict__ part, float* __restrict__ colsum_b,
-                                                           float* __restrict__ dgamma_b, float* __restrict__ dbeta_b) {
-  const int b = blockIdx.y;
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int rg = threadIdx.x >> 6;  // 4 row groups
-  const int cg = C / G;
-  __shared__ float acc[3][4][64];
-  float s_du = 0.f, s_dgam = 0.f, s_dbet = 0.f;
-  if (c < C) {
-    const int g = c / cg;
-    float S1 = 0.f, S2 = 0.f;
-    for (int p = 0; p < kGnParts; ++p) {
-      const float* o = part + (((int64_t)b * kGnParts + p) * G + g) * 2;
-      S1 += o[0];
-      S2 += o[1];
-    }
-    const float M = (float)T_ * (float)cg;
-    const float m1 = S1 / M, m2 = S2 / M;
-    const float rstd = mr[(b * G + g) * 2 + 1];
-    const float mean = mr[(b * G + g) * 2];
-    const float gm = gamma[c];
-    for (int t = rg; t < T_; t += 4) {
-      const int64_t n = (int64_t)b * T_ + t;
-      float xh, dh;
+__device__ __forceinline__ void gn_dh_chunk(const T* dy, int lddy, const T* u, int ldu, int64_t n, int c, int half,
+                                            bool glu, const float* mr4, const float* gamma, const float* beta,
+                                            float* dha, float* xa, float* dhb, float* xb) {
+  constexpr int V = Vec<T>::N;
+  float g[V], ua[V];
+  Vec<T>::load(dy + n * lddy + c, g);
+  Vec<T>::load(u + n * ldu + c, ua);
+  if (!glu) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) { dha[i] = g[i]; xa[i] = (ua[i] - mr4[0]) * mr4[1]; }
+    return;
+  }
+  float ub[V];
+  Vec<T>::load(u + n * ldu + c + half, ub);
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const float xha = (ua[i] - mr4[0]) * mr4[1];
+    const float xhb = (ub[i] - mr4[2]) * mr4[3];
+    const float ha = xha * gamma[c + i] + beta[c + i];
+    const float hb = xhb * gamma[c + half + i] + beta[c + half + i];
+    const float ta = ftanh(ha);
+    const float sb = fsigmoid(hb);
+    dha[i] = g[i] * sb * (1.f - ta * ta);
+    dhb[i] = g[i] * ta * (sb * (1.f - sb));
+    xa[i] = xha;
+    xb[i] = xhb;
+  }
+}
+
+// pass 1 (vectorised): per (utterance, part) S1_g = sum gamma*dh, S2_g = sum gamma*dh*xhat
+template <typename T>
+__global__ __launch_bounds__(256) void gn_bwd_reduce_vec_kernel(const T* __restrict__ dy, int lddy,
+                                                                const T* __restrict__ u, int ldu, int T_, int C, int G,
+                                                                int glu, int cpr, const float* __restrict__ mr,
+                                                                const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta,
+                                                                float* __restrict__ part) {
+  constexpr int V = Vec<T>::N;
+  const int p = blockIdx.x, b = blockIdx.y;
+  const int r0 = p * T_ / kGnBwdParts, r1 = (p + 1) * T_ / kGnBwdParts;
+  const int ch = threadIdx.x % cpr, rg = threadIdx.x / cpr, nrg = 256 / cpr;
+  const int half = C / 2;
+  const int c = ch * V;
+  const float* mr4 = mr + (int64_t)b * G * 2;
+  __shared__ float red[16];
+  float s1a = 0.f, s2a = 0.f, s1b = 0.f, s2b = 0.f;
+  for (int r = r0 + rg; r < r1; r += nrg) {
+    const int64_t n = (int64_t)b * T_ + r;
+    float dha[V], xa[V], dhb[V], xb[V];
+    gn_dh_chunk<T>(dy, lddy, u, ldu, n, c, half, glu, mr4, gamma, beta, dha, xa, dhb, xb);
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      const float ga = gamma[c + i] * dha[i];
+      s1a += ga;
+      s2a = fmaf(ga, xa[i], s2a);
       if (glu) {
-        dh = gn_bwd_dh<T>(dy, lddy, u, ldu, n, c, C, 1, b, mr, gamma, beta, &xh);
-      } else {
-        dh = Elem<T>::ld(dy, n * lddy + c);
-        xh = (Elem<T>::ld(u, n * ldu + c) - mean) * rstd;
+        const float gb = gamma[c + half + i] * dhb[i];
+        s1b += gb;
+        s2b = fmaf(gb, xb[i], s2b);
       }
-      const float d = rstd * (gm * dh - m1 - xh * m2);
-      Elem<T>::st(du, n * lddu + c, d);
-      s_du += d;
-      s_dgam = fmaf(dh, xh, s_dgam);
-      s_dbet += dh;
     }
   }
-  acc[0][rg][threadIdx.x & 63] = s_du;
-  acc[1][rg][threadIdx.x & 63] = s_dgam;
-  acc[2][rg][threadIdx.x & 63] = s_dbet;
+  s1a = block_sum(s1a, red);
+  __syncthreads();
+  s2a = block_sum(s2a, red);
+  __syncthreads();
+  if (glu) {
+    s1b = block_sum(s1b, red);
+    __syncthreads();
+    s2b = block_sum(s2b, red);
+  }
+  if (threadIdx.x == 0) {
+    float* o = part + ((int64_t)b * kGnBwdParts + p) * G * 2;
+    o[0] = s1a;
+    o[1] = s2a;
+    if (glu) { o[2] = s1b; o[3] = s2b; }
+  }
+}
+
+// pass 2 (vectorised): du and per-(utterance, channel) sums of du (bias /
+// conv_cond gradients), dh*xhat (dgamma) and dh (dbeta).  Block = one
+// utterance x 8 channel chunks x all T rows (32 row groups), so the per-
+// utterance sums are complete inside the block (deterministic, no atomics).
+template <typename T>
+__global__ __launch_bounds__(256) void gn_bwd_apply_vec_kernel(const T* __restrict__ dy, int lddy,
+                                                               const T* __restrict__ u, int ldu, T* __restrict__ du,
+                                                               int lddu, int T_, int C, int G, int glu, int cpr,
+                                                               const float* __restrict__ mr,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta,
+                                                               const float* __restrict__ part,
+                                                               float* __restrict__ colsum_b, float* __restrict__ dgamma_b,
+                                                               float* __restrict__ dbeta_b) {
+  constexpr int V = Vec<T>::N;
+  const int b = blockIdx.y;
+  const int ch = blockIdx.x * 8 + (threadIdx.x & 7), rg = threadIdx.x >> 3;
+  const bool active = ch < cpr;
+  const int half = C / 2;
+  const int c = ch * V;
+  const float* mr4 = mr + (int64_t)b * G * 2;
+  const int ng = glu ? 2 : 1;
+  float m1a = 0.f, m2a = 0.f, m1b = 0.f, m2b = 0.f;
+  {
+    const int cg = C / G;
+    const float M = (float)T_ * (float)cg;
+    float S1a = 0.f, S2a = 0.f, S1b = 0.f, S2b = 0.f;
+    for (int q = 0; q < kGnBwdParts; ++q) {
+      const float* o = part + ((int64_t)b * kGnBwdParts + q) * G * 2;
+      S1a += o[0];
+      S2a += o[1];
+      if (glu) { S1b += o[2]; S2b += o[3]; }
+    }
+    m1a = S1a / M; m2a = S2a / M; m1b = S1b / M; m2b = S2b / M;
+  }
+  float a_du[2][V], a_dg[2][V], a_db[2][V];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int i = 0; i < V; ++i) { a_du[s][i] = 0.f; a_dg[s][i] = 0.f; a_db[s][i] = 0.f; }
+  if (active) {
+    for (int r = rg; r < T_; r += 32) {
+      const int64_t n = (int64_t)b * T_ + r;
+      float dha[V], xa[V], dhb[V], xb[V];
+      gn_dh_chunk<T>(dy, lddy, u, ldu, n, c, half, glu, mr4, gamma, beta, dha, xa, dhb, xb);
+      float oa[V];
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        oa[i] = mr4[1] * (gamma[c + i] * dha[i] - m1a - xa[i] * m2a);
+        a_du[0][i] += oa[i];
+        a_dg[0][i] = fmaf(dha[i], xa[i], a_dg[0][i]);
+        a_db[0][i] += dha[i];
+      }
+      Vec<T>::store(du + n * lddu + c, oa);
+      if (glu) {
+        float ob[V];
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          ob[i] = mr4[3] * (gamma[c + half + i] * dhb[i] - m1b - xb[i] * m2b);
+          a_du[1][i] += ob[i];
+          a_dg[1][i] = fmaf(dhb[i], xb[i], a_dg[1][i]);
+          a_db[1][i] += dhb[i];
+        }
+        Vec<T>::store(du + n * lddu + c + half, ob);
+      }
+    }
+  }
+  __shared__ float lds[32][8][2 * V];
+  auto dump = [&](const float (&a)[2][V], float* out) {
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < V; ++i) lds[rg][threadIdx.x & 7][s * V + i] = a[s][i];
+    __syncthreads();
+    // 256 threads finish 8 chunks x 2 halves x V columns
+    for (int e = threadIdx.x; e < 8 * 2 * V; e += 256) {
+      const int cl = e / (2 * V), rem = e - cl * 2 * V, s = rem / V, i = rem - s * V;
+      const int chg = blockIdx.x * 8 + cl;
+      if (chg >= cpr || s >= ng || !out) continue;
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < 32; ++q) t += lds[q][cl][rem];
+      out[(int64_t)b * C + chg * V + s * half + i] = t;
+    }
+  };
+  dump(a_du, colsum_b);
+  dump(a_dg, dgamma_b);
+  dump(a_db, dbeta_b);
+}
+
+
+// g = tanh(GN(u)[:, :half]) * sigmoid(GN(u)[:, half:]), GroupNorm with G=2,
+// one 16-B chunk of V channels per thread (layers.py:236-242).
+template <typename T>
+__global__ __launch_bounds__(256) void gn_glu_fwd_vec_kernel(const T* __restrict__ u, int ldu, T* __restrict__ g,
+                                                             int ldg, int n_rows, int T_, int half, int cpr,
+                                                             const float* __restrict__ mr,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta) {
+  // block = 16 frames; thread = (chunk, row slot); cpr divides 256
+  constexpr int V = Vec<T>::N;
+  const int ch = threadIdx.x % cpr, rs = threadIdx.x / cpr, nrs = 256 / cpr;
+  const int c = ch * V;
+  float ga[V], ba[V], gb[V], bb[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) { ga[i] = gamma[c + i]; ba[i] = beta[c + i]; gb[i] = gamma[c + half + i]; bb[i] = beta[c + half + i]; }
+  for (int r = blockIdx.x * 16 + rs; r < min(n_rows, blockIdx.x * 16 + 16); r += nrs) {
+    const int b = r / T_;
+    const float ma = mr[4 * b + 0], ra = mr[4 * b + 1], mb = mr[4 * b + 2], rb = mr[4 * b + 3];
+    float ua[V], ub[V], o[V];
+    Vec<T>::load(u + (int64_t)r * ldu + c, ua);
+    Vec<T>::load(u + (int64_t)r * ldu + c + half, ub);
+#pragma unroll
+    for (int i = 0; i < V; ++i)
+      o[i] = ftanh((ua[i] - ma) * ra * ga[i] + ba[i]) * fsigmoid((ub[i] - mb) * rb * gb[i] + bb[i]);
+    Vec<T>::store(g + (int64_t)r * ldg + c, o);
+  }
+}
+
+// single-pass column sums for short inputs (rows <= ~2048): 64 columns x 4 row groups per block
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_small_kernel(const T* __restrict__ x, int ldx, int64_t n_rows, int C,
+                                                           float* __restrict__ out, int accum) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  __shared__ float acc[4][64];
+  float s = 0.f;
+  if (c < C)
+    for (int64_t r = rg; r < n_rows; r += 4) s += Elem<T>::ld(x, r * ldx + c);
+  acc[rg][threadIdx.x & 63] = s;
   __syncthreads();
   if (rg == 0 && c < C) {
     const int l = threadIdx.x & 63;
-    const float a0 = acc[0][0][l] + acc[0][1][l] + acc[0][2][l] + acc[0][3][l];
-    const float a1 = acc[1][0][l] + acc[1][1][l] + acc[1][2][l] + acc[1][3][l];
-    const float a2 = acc[2][0][l] + acc[2][1][l] + acc[2][2][l] + acc[2][3][l];
-    if (colsum_b) colsum_b[(int64_t)b * C + c] = a0;
-    if (dgamma_b) dgamma_b[(int64_t)b * C + c] = a1;
-    if (dbeta_b) dbeta_b[(int64_t)b * C + c] = a2;
+    const float t = acc[0][l] + acc[1][l] + acc[2][l] + acc[3][l];
+    out[c] = accum ? out[c] + t : t;
+  }
+}
+
+// vectorised partial column sums: 32 chunks x 8 row groups per block
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_partial_vec_kernel(const T* __restrict__ x, int ldx, int64_t n_rows,
+                                                                 int C, int nparts, float* __restrict__ part) {
+  constexpr int V = Vec<T>::N;
+  const int chunk = blockIdx.x * 32 + (threadIdx.x & 31);
+  const int rg = threadIdx.x >> 5;
+  const int p = blockIdx.y;
+  const int64_t r0 = n_rows * p / nparts, r1 = n_rows * (p + 1) / nparts;
+  const int c = chunk * V;
+  float s[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) s[i] = 0.f;
+  if (c < C)
+    for (int64_t r = r0 + rg; r < r1; r += 8) {
+      float f[V];
+      Vec<T>::load(x + r * ldx + c, f);
+#pragma unroll
+      for (int i = 0; i < V; ++i) s[i] += f[i];
+    }
+  __shared__ float lds[8][32 * V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) lds[rg][(threadIdx.x & 31) * V + i] = s[i];
+  __syncthreads();
+  for (int e = threadIdx.x; e < 32 * V; e += 256) {
+    const int cc = blockIdx.x * 32 * V + e;
+    if (cc < C) {
+      float t = 0.f;
+      for (int q = 0; q < 8; ++q) t += lds[q][e];
+      part[(int64_t)p * C + cc] = t;
+    }
   }
 }
 
@@ -311,6 +499,7 @@ __global__ void colsum_final_kernel(const float* __restrict__ part, int nparts, 
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   float s = 0.f;
+#pragma unroll 8
   for (int p = 0; p < nparts; ++p) s += part[(int64_t)p * C + c];
   out[c] = accum ? out[c] + s : s;
 }
@@ -419,6 +608,7 @@ __global__ void linear_fwd_kernel(const float* __restrict__ c, const float* __re
   if (e >= (int64_t)B * O) return;
   const int b = (int)(e / O), o = (int)(e - (int64_t)b * O);
   float s = 0.f;
+#pragma unroll 8
   for (int i = 0; i < I; ++i) s = fmaf(W[(int64_t)o * I + i], c[(int64_t)b * I + i], s);
   out[e] = s + (bias ? bias[o] : 0.f);
 }
@@ -429,18 +619,36 @@ __global__ void linear_bwd_w_kernel(const float* __restrict__ dout, const float*
   if (e >= (int64_t)O * I) return;
   const int o = (int)(e / I), i = (int)(e - (int64_t)o * I);
   float s = 0.f;
+#pragma unroll 8
   for (int b = 0; b < B; ++b) s = fmaf(dout[(int64_t)b * O + o], c[(int64_t)b * I + i], s);
   dW[e] += s;
 }
 
-__global__ void linear_bwd_x_kernel(const float* __restrict__ dout, const float* __restrict__ W, int B, int I, int O,
-                                    float* __restrict__ dc) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (int64_t)B * I) return;
-  const int b = (int)(e / I), i = (int)(e - (int64_t)b * I);
+// dc[b][i] += sum_o dout[b][o] * W[o][i]: block (b, 64 columns i), 4 groups of o
+__global__ __launch_bounds__(256) void linear_bwd_x_kernel(const float* __restrict__ dout, const float* __restrict__ W,
+                                                           int B, int I, int O, float* __restrict__ dc) {
+  const int b = blockIdx.y;
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int og = threadIdx.x >> 6;
+  __shared__ float acc[4][64];
   float s = 0.f;
-  for (int o = 0; o < O; ++o) s = fmaf(dout[(int64_t)b * O + o], W[(int64_t)o * I + i], s);
-  dc[e] += s;
+  if (i < I) {
+    float s2 = 0.f;
+    int o = og;
+#pragma unroll 4
+    for (; o + 4 < O; o += 8) {
+      s = fmaf(dout[(int64_t)b * O + o], W[(int64_t)o * I + i], s);
+      s2 = fmaf(dout[(int64_t)b * O + o + 4], W[(int64_t)(o + 4) * I + i], s2);
+    }
+    for (; o < O; o += 4) s = fmaf(dout[(int64_t)b * O + o], W[(int64_t)o * I + i], s);
+    s += s2;
+  }
+  acc[og][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (og == 0 && i < I) {
+    const int l = threadIdx.x & 63;
+    dc[(int64_t)b * I + i] += (acc[0][l] + acc[1][l]) + (acc[2][l] + acc[3][l]);
+  }
 }
 
 // --------------------------------------------------------------- optimizer
@@ -506,6 +714,18 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   }
 }
 
+__global__ __launch_bounds__(256) void convert_2d_kernel(const void* __restrict__ src, int lds, int sdt,
+                                                         void* __restrict__ dst, int ldd, int ddt, int64_t rows,
+                                                         int cols) {
+  const int64_t total = rows * cols;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / cols;
+    const int c = (int)(e - r * cols);
+    const float v = src ? ld_dt(src, r * lds + c, sdt) : 0.f;
+    st_dt(dst, r * ldd + c, v, ddt);
+  }
+}
+
 }  // namespace vqx
 
 using namespace vqx;
@@ -544,7 +764,7 @@ extern "C" int vqx_weight_norm_bwd(const vqx_wn_layer* lh, const vqx_wn_layer* l
     const int rows = l.kind == 0 ? l.cout : l.cin;
     const int cols = (l.kind == 0 ? l.cin : l.cout) * l.k;
     if (cols > 4096) { set_error("vqx_weight_norm_bwd: row length %d > 4096", cols); return -1; }
-    if (!l.slabs || !l.dv || !l.dg || l.splits < 1) { set_error("vqx_weight_norm_bwd: layer %d missing buffers", i); return -1; }
+    if (!l.slabs || !l.dv || (l.g && !l.dg) || l.splits < 1) { set_error("vqx_weight_norm_bwd: layer %d missing buffers", i); return -1; }
     max_rows = rows > max_rows ? rows : max_rows;
   }
   hipLaunchKernelGGL(wn_bwd_kernel, dim3(max_rows, n_layers), dim3(256), 0, (hipStream_t)stream, ld, n_layers);
@@ -556,10 +776,16 @@ extern "C" int vqx_groupnorm_stats(const void* x, int32_t ldx, int32_t dtype, in
   if (G < 1 || C % G || n_rows % T) { set_error("vqx_groupnorm_stats: bad shape"); return -1; }
   const int B = (int)(n_rows / T);
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == VQX_BF16)
-    hipLaunchKernelGGL(gn_partial_kernel<bf16_t>, dim3(kGnParts, B * G), dim3(256), 0, s, (const bf16_t*)x, ldx, T, C, G, partials);
-  else
-    hipLaunchKernelGGL(gn_partial_kernel<float>, dim3(kGnParts, B * G), dim3(256), 0, s, (const float*)x, ldx, T, C, G, partials);
+  const int V = dtype == VQX_BF16 ? 8 : 4;
+  const int cg = C / G, cpr = cg / V;
+  const bool vec = (cg % V == 0) && (ldx % V == 0) && cpr <= 256 && (256 % cpr == 0) && (((uintptr_t)x & 15) == 0);
+  if (dtype == VQX_BF16) {
+    if (vec) hipLaunchKernelGGL(gn_partial_vec_kernel<bf16_t>, dim3(kGnParts, B * G), dim3(256), 0, s, (const bf16_t*)x, ldx, T, C, G, cpr, partials);
+    else hipLaunchKernelGGL(gn_partial_kernel<bf16_t>, dim3(kGnParts, B * G), dim3(256), 0, s, (const bf16_t*)x, ldx, T, C, G, partials);
+  } else {
+    if (vec) hipLaunchKernelGGL(gn_partial_vec_kernel<float>, dim3(kGnParts, B * G), dim3(256), 0, s, (const float*)x, ldx, T, C, G, cpr, partials);
+    else hipLaunchKernelGGL(gn_partial_kernel<float>, dim3(kGnParts, B * G), dim3(256), 0, s, (const float*)x, ldx, T, C, G, partials);
+  }
   hipLaunchKernelGGL(gn_finalize_kernel, dim3((B * G + 127) / 128), dim3(128), 0, s, partials, B * G, eps, mean_rstd);
   return launch_status("vqx_groupnorm_stats");
 }
@@ -568,29 +794,45 @@ extern "C" int vqx_gn_glu_fwd(const void* u, int32_t ldu, void* g, int32_t ldg, 
                               int32_t T, int32_t C, const float* mean_rstd, const float* gamma, const float* beta,
                               vqx_stream_t stream) {
   if (C % 2) { set_error("vqx_gn_glu_fwd: odd C"); return -1; }
-  const int grid = grid_for(n_rows * (C / 2));
+  const int V = dtype == VQX_BF16 ? 8 : 4;
+  if ((C / 2) % V || ldu % V || ldg % V || (((uintptr_t)u | (uintptr_t)g) & 15)) {
+    set_error("vqx_gn_glu_fwd: channels/strides must be multiples of %d", V);
+    return -1;
+  }
+  const int cpr = (C / 2) / V;
+  if (cpr > 256 || 256 % cpr) { set_error("vqx_gn_glu_fwd: C/2/%d must divide 256", V); return -1; }
+  const int grid = (int)((n_rows + 15) / 16);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == VQX_BF16)
-    hipLaunchKernelGGL(gn_glu_fwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)u, ldu, (bf16_t*)g, ldg, n_rows, T, C / 2, mean_rstd, gamma, beta);
+    hipLaunchKernelGGL(gn_glu_fwd_vec_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)u, ldu, (bf16_t*)g, ldg, (int)n_rows, T, C / 2, cpr, mean_rstd, gamma, beta);
   else
-    hipLaunchKernelGGL(gn_glu_fwd_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)u, ldu, (float*)g, ldg, n_rows, T, C / 2, mean_rstd, gamma, beta);
+    hipLaunchKernelGGL(gn_glu_fwd_vec_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)u, ldu, (float*)g, ldg, (int)n_rows, T, C / 2, cpr, mean_rstd, gamma, beta);
   return launch_status("vqx_gn_glu_fwd");
 }
 
 extern "C" int vqx_gn_bwd(const void* dy, int32_t lddy, const void* u, int32_t ldu, void* du, int32_t lddu,
                           int32_t dtype, int64_t n_rows, int32_t T, int32_t C, int32_t G, int32_t glu,
                           const float* mean_rstd, const float* gamma, const float* beta, float* partials,
-                          float* colsum_b, float* dgamma_b, float* dbeta_b, vqx_stream_t stream) {
+                          float* colsum_p, float* dgamma_p, float* dbeta_p, vqx_stream_t stream) {
   if (glu && G != 2) { set_error("vqx_gn_bwd: glu requires G=2"); return -1; }
-  if (G < 1 || C % G || n_rows % T) { set_error("vqx_gn_bwd: bad shape"); return -1; }
+  if (!glu && G != 1) { set_error("vqx_gn_bwd: non-glu path supports G=1"); return -1; }
+  if (C % G || n_rows % T) { set_error("vqx_gn_bwd: bad shape"); return -1; }
   const int B = (int)(n_rows / T);
+  const int V = dtype == VQX_BF16 ? 8 : 4;
+  const int span = glu ? C / 2 : C;  // channels covered by the chunk index
+  const int cpr = span / V;
+  if (span % V || lddy % V || ldu % V || lddu % V || cpr > 256 || 256 % cpr ||
+      (((uintptr_t)dy | (uintptr_t)u | (uintptr_t)du) & 15)) {
+    set_error("vqx_gn_bwd: channel count / strides must give a power-of-two chunk count <= 256 (C=%d)", C);
+    return -1;
+  }
   hipStream_t s = (hipStream_t)stream;
   if (dtype == VQX_BF16) {
-    hipLaunchKernelGGL(gn_bwd_reduce_kernel<bf16_t>, dim3(kGnParts, B), dim3(256), 0, s, (const bf16_t*)dy, lddy, (const bf16_t*)u, ldu, T, C, G, glu, mean_rstd, gamma, beta, partials);
-    hipLaunchKernelGGL(gn_bwd_apply_kernel<bf16_t>, dim3((C + 63) / 64, B), dim3(256), 0, s, (const bf16_t*)dy, lddy, (const bf16_t*)u, ldu, (bf16_t*)du, lddu, T, C, G, glu, mean_rstd, gamma, beta, partials, colsum_b, dgamma_b, dbeta_b);
+    hipLaunchKernelGGL(gn_bwd_reduce_vec_kernel<bf16_t>, dim3(kGnBwdParts, B), dim3(256), 0, s, (const bf16_t*)dy, lddy, (const bf16_t*)u, ldu, T, C, G, glu, cpr, mean_rstd, gamma, beta, partials);
+    hipLaunchKernelGGL(gn_bwd_apply_vec_kernel<bf16_t>, dim3((cpr + 7) / 8, B), dim3(256), 0, s, (const bf16_t*)dy, lddy, (const bf16_t*)u, ldu, (bf16_t*)du, lddu, T, C, G, glu, cpr, mean_rstd, gamma, beta, partials, colsum_p, dgamma_p, dbeta_p);
   } else {
-    hipLaunchKernelGGL(gn_bwd_reduce_kernel<float>, dim3(kGnParts, B), dim3(256), 0, s, (const float*)dy, lddy, (const float*)u, ldu, T, C, G, glu, mean_rstd, gamma, beta, partials);
-    hipLaunchKernelGGL(gn_bwd_apply_kernel<float>, dim3((C + 63) / 64, B), dim3(256), 0, s, (const float*)dy, lddy, (const float*)u, ldu, (float*)du, lddu, T, C, G, glu, mean_rstd, gamma, beta, partials, colsum_b, dgamma_b, dbeta_b);
+    hipLaunchKernelGGL(gn_bwd_reduce_vec_kernel<float>, dim3(kGnBwdParts, B), dim3(256), 0, s, (const float*)dy, lddy, (const float*)u, ldu, T, C, G, glu, cpr, mean_rstd, gamma, beta, partials);
+    hipLaunchKernelGGL(gn_bwd_apply_vec_kernel<float>, dim3((cpr + 7) / 8, B), dim3(256), 0, s, (const float*)dy, lddy, (const float*)u, ldu, (float*)du, lddu, T, C, G, glu, cpr, mean_rstd, gamma, beta, partials, colsum_p, dgamma_p, dbeta_p);
   }
   return launch_status("vqx_gn_bwd");
 }
@@ -598,13 +840,32 @@ extern "C" int vqx_gn_bwd(const void* dy, int32_t lddy, const void* u, int32_t l
 extern "C" int vqx_colsum(const void* x, int32_t ldx, int32_t dtype, int64_t n_rows, int32_t C, float* partials,
                           float* out, int32_t accumulate, vqx_stream_t stream) {
   if (n_rows <= 0 || C <= 0) { set_error("vqx_colsum: bad shape"); return -1; }
-  int nparts = (int)((n_rows + 255) / 256);
-  nparts = nparts > 64 ? 64 : nparts;
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == VQX_BF16)
+  if (n_rows <= 64) {
+    if (dtype == VQX_BF16)
+      hipLaunchKernelGGL(colsum_small_kernel<bf16_t>, dim3((C + 63) / 64), dim3(256), 0, s, (const bf16_t*)x, ldx, n_rows, C, out, accumulate);
+    else
+      hipLaunchKernelGGL(colsum_small_kernel<float>, dim3((C + 63) / 64), dim3(256), 0, s, (const float*)x, ldx, n_rows, C, out, accumulate);
+    return launch_status("vqx_colsum");
+  }
+  const int V = dtype == VQX_BF16 ? 8 : 4;
+  const int colblocks = (C / V + 31) / 32;
+  int nparts = (256 + colblocks - 1) / colblocks;
+  if (nparts > 64) nparts = 64;
+  if (nparts > n_rows / 8) nparts = (int)(n_rows / 8);
+  if (nparts < 1) nparts = 1;
+  const bool vec = (C % V == 0) && (ldx % V == 0) && (((uintptr_t)x & 15) == 0);
+  if (vec) {
+    const int nch = C / V;
+    if (dtype == VQX_BF16)
+      hipLaunchKernelGGL(colsum_partial_vec_kernel<bf16_t>, dim3((nch + 31) / 32, nparts), dim3(256), 0, s, (const bf16_t*)x, ldx, n_rows, C, nparts, partials);
+    else
+      hipLaunchKernelGGL(colsum_partial_vec_kernel<float>, dim3((nch + 31) / 32, nparts), dim3(256), 0, s, (const float*)x, ldx, n_rows, C, nparts, partials);
+  } else if (dtype == VQX_BF16) {
     hipLaunchKernelGGL(colsum_partial_kernel<bf16_t>, dim3((C + 63) / 64, nparts), dim3(256), 0, s, (const bf16_t*)x, ldx, n_rows, C, nparts, partials);
-  else
+  } else {
     hipLaunchKernelGGL(colsum_partial_kernel<float>, dim3((C + 63) / 64, nparts), dim3(256), 0, s, (const float*)x, ldx, n_rows, C, nparts, partials);
+  }
   hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 255) / 256), dim3(256), 0, s, partials, nparts, C, out, accumulate);
   return launch_status("vqx_colsum");
 }
@@ -675,7 +936,7 @@ extern "C" int vqx_linear_bwd_f32(const float* dout, const float* c, const float
                                   float* dW, float* dc, vqx_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   if (dW) hipLaunchKernelGGL(linear_bwd_w_kernel, dim3(grid_for((int64_t)O * I, 256, 1 << 20)), dim3(256), 0, s, dout, c, B, I, O, dW);
-  if (dc) hipLaunchKernelGGL(linear_bwd_x_kernel, dim3(grid_for((int64_t)B * I, 256, 1 << 20)), dim3(256), 0, s, dout, W, B, I, O, dc);
+  if (dc) hipLaunchKernelGGL(linear_bwd_x_kernel, dim3((I + 63) / 64, B), dim3(256), 0, s, dout, W, B, I, O, dc);
   return launch_status("vqx_linear_bwd_f32");
 }
 
@@ -699,4 +960,13 @@ extern "C" int vqx_adam_step(float* p, const float* g, float* m, float* v, int64
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
                      hyper, sumsq, max_norm);
   return launch_status("vqx_adam_step");
+}
+
+extern "C" int vqx_convert_2d(const void* src, int32_t ld_src, int32_t src_dtype, void* dst, int32_t ld_dst,
+                              int32_t dst_dtype, int64_t rows, int32_t cols, vqx_stream_t stream) {
+  if (rows <= 0 || cols <= 0) return 0;
+  if (!dst) { set_error("vqx_convert_2d: null dst"); return -1; }
+  hipLaunchKernelGGL(convert_2d_kernel, dim3(grid_for(rows * cols, 256, 8192)), dim3(256), 0, (hipStream_t)stream,
+                     src, ld_src, src_dtype, dst, ld_dst, dst_dtype, rows, cols);
+  return launch_status("vqx_convert_2d");
 }

@@ -171,10 +171,7 @@ __global__ __launch_bounds__(256) void vq_forward_kernel(const float* __restrict
 
   float sq = 0.f;
   if (row_ok) {
-    if (q == 0) {
-      idx_out[my_row] = my_idx;
-      if (bcnt) atomicAdd(bcnt + my_idx, 1.0f);
-    }
+    if (q == 0) idx_out[my_row] = my_idx;
 #pragma unroll
     for (int kb = 0; kb < 8; ++kb) {
       const int d0 = 16 * kb + 4 * q;
@@ -195,8 +192,59 @@ __global__ __launch_bounds__(256) void vq_forward_kernel(const float* __restrict
       for (int m = 0; m < 4; ++m) {
         const float df = __fsub_rn(e[m], zf[kb][m]);
         sq = fmaf(df, df, sq);
-        if (bsum) atomicAdd(bsum + (int64_t)my_idx * VQ_D + d0 + m, zf[kb][m]);
       }
+    }
+  }
+
+  // ---- EMA statistics: per-code sums of z over this workgroup's 64 frames.
+  // Sort the (code, frame) pairs with a wave-wide bitonic network, then each
+  // thread walks a run of the sorted frames for one dimension d and flushes a
+  // partial sum per code segment: one contiguous 256-B atomic wave-instruction
+  // per (segment, 64 dims) instead of one scattered atomic per element, and no
+  // same-address pile-up when the codebook usage is concentrated.
+  if (bsum) {
+    float* zl = (float*)smem;                       // [64][128] frame block (tile buffers are free now)
+    int* codes = (int*)(smem + 64 * VQ_D * 4);      // [64] code per local frame (K = invalid)
+    int* order = codes + 64;                        // [64] frames sorted by code
+#pragma unroll
+    for (int kb = 0; kb < 8; ++kb) *(f32x4_t*)(zl + (w * 16 + j16) * VQ_D + 16 * kb + 4 * q) = zf[kb];
+    if (q == 0) codes[w * 16 + j16] = row_ok ? my_idx : K;
+    __syncthreads();
+    if (w == 0) {
+      int key = codes[lane] * 64 + lane;
+#pragma unroll
+      for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          const int other = __shfl_xor(key, j, 64);
+          const bool up = (lane & k) == 0, lower = (lane & j) == 0;
+          key = (lower == up) ? min(key, other) : max(key, other);
+        }
+      }
+      order[lane] = key & 63;
+    }
+    __syncthreads();
+    const int d = tid & 127, half = tid >> 7;
+    int cur = -1, cnt = 0;
+    float acc = 0.f;
+    for (int p = 32 * half; p < 32 * half + 32; ++p) {
+      const int r = order[p];
+      const int c = codes[r];
+      if (c != cur) {
+        if (cur >= 0 && cur < K) {
+          atomicAdd(bsum + (int64_t)cur * VQ_D + d, acc);
+          if (d == 0 && bcnt) atomicAdd(bcnt + cur, (float)cnt);
+        }
+        cur = c;
+        acc = 0.f;
+        cnt = 0;
+      }
+      acc += zl[r * VQ_D + d];
+      ++cnt;
+    }
+    if (cur >= 0 && cur < K) {
+      atomicAdd(bsum + (int64_t)cur * VQ_D + d, acc);
+      if (d == 0 && bcnt) atomicAdd(bcnt + cur, (float)cnt);
     }
   }
   const float tot = block_sum(sq, red);

@@ -1,0 +1,605 @@
+"""The VQ-VAE training step on MI355X: every arithmetic op of the reference's
+hot path is a libvqx HIP kernel launched here on
+torch's current stream; torch is used only for device memory and streams.
+
+Step anatomy (frame-major activations [N = B*T, C], see include/vqx.h):
+
+  pack     weight norm of all 44 convs -> packed effective weights (1 launch pair)
+  encoder  conv0 | 10 x {k3 conv (LReLU prologue) -> GN stats -> 1x1 skip conv
+           with the GroupNorm-apply + residual fused in its epilogue} | 1x1 out
+           conv (LReLU prologue, f32 out)                       (vqvae.py:185-192)
+  vq       fused distance/argmin/gather/commitment/EMA-statistics kernel
+                                                                 (layers_vq.py:268-323)
+  decoder  ConvT0 | 10 x {ConvT k3 (+ speaker term as a per-utterance row bias)
+           -> GN stats -> GN+tanh*sigmoid -> 1x1 res/skip conv with the
+           residual add and the skip accumulation split in its epilogue} |
+           ReLU(s*skip) 1x1 | ReLU 1x1                           (vqvae.py:298-318)
+  loss     log-likelihood + its gradient in one pass            (layers.py:283-296)
+  backward encoder (driven only by beta*commitment, the reference quirk:
+           z_vq carries no gradient, layers_vq.py:315) and decoder: dgrad GEMMs
+           with activation-derivative / residual epilogues, wgrad split-K slabs
+           reduced by the weight-norm backward, GN backward (2 passes).
+  update   global grad norm -> fused clip + Adam (+ StepLR on device); EMA codebook.
+
+The engine owns flat fp32 buffers for parameters, gradients and Adam moments;
+model parameters are views into them, so `model.state_dict()` stays the
+reference's and the optimizer touches one contiguous buffer.
+"""
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from .. import _lib as L
+from .. import ops
+
+F32 = torch.float32
+
+
+def _pow2_floor(x):
+    p = 1
+    while p * 2 <= x:
+        p *= 2
+    return p
+
+
+@dataclass
+class ConvLayer:
+    mod: object          # WNConv1d
+    name: str
+    kind: int            # 0 Conv1d, 1 ConvTranspose1d
+    cin: int             # effective-conv input channels
+    cout: int            # effective-conv output channels
+    k: int
+    pad: int
+    wp: torch.Tensor = None     # packed effective weight [cout, k*cin]
+    norm: torch.Tensor = None   # ||v_o||
+    slab: torch.Tensor = None   # wgrad partials [splits, rows, cols]
+    splits: int = 1
+
+    @property
+    def rows(self):
+        return self.cin if self.kind == 1 else self.cout
+
+    @property
+    def cols(self):
+        return (self.cout if self.kind == 1 else self.cin) * self.k
+
+
+class Workspace:
+    """All activations / gradients of one (B, T) shape (allocated once)."""
+
+    def __init__(self, eng, B, T, train=True):
+        d, cd, dev = eng.dims, eng.cd, eng.device
+        N = B * T
+        self.B, self.T, self.N = B, T, N
+        e = lambda *s, dt=cd: torch.empty(*s, device=dev, dtype=dt)  # noqa: E731
+        C, Z, Cd, S, Fo, mel = d["C"], d["Z"], d["Cd"], d["S"], d["F"], d["mel"]
+        ns, nd, K, D = d["ns"], d["nd"], d["K"], d["Z"]
+        self.x = e(N, mel)
+        self.c = [e(N, C) for _ in range(ns + 1)]
+        self.h = [e(N, C) for _ in range(ns)]
+        self.enc_mr = e(ns, B, 2, dt=F32)
+        self.z = e(N, Z, dt=F32)
+        self.idx = torch.empty(N, device=dev, dtype=torch.int64)
+        self.zq = e(N, Z, dt=F32)
+        self.zq_c = e(N, Z)
+        self.zq_j = e(N, Z) if d["jitter_p"] > 0 else None
+        self.src_t = torch.empty(T, device=dev, dtype=torch.int32)
+        self.vq_part = e((N + 63) // 64, dt=F32)
+        # EMA statistics bundle (all-reduced as one buffer in data parallel)
+        self.ema = e(K * D + K + K * D, dt=F32)
+        self.bsum = self.ema[: K * D].view(K, D)
+        self.bcnt = self.ema[K * D: K * D + K]
+        self.rand_rows = self.ema[K * D + K:].view(K, D)
+        self.yemb = e(B, d["ydim"], dt=F32)
+        self.condbias = e(nd, B, 2 * Cd, dt=F32)
+        self.xs = [e(N, Cd) for _ in range(nd + 1)]
+        self.u = [e(N, 2 * Cd) for _ in range(nd)]
+        self.g = [e(N, Cd) for _ in range(nd)]
+        self.dec_mr = e(nd, B, 4, dt=F32)
+        self.skip32 = e(N, S, dt=F32)
+        self.skip_c = e(N, S) if cd != F32 else self.skip32
+        self.f1 = e(N, S)
+        self.xhat = e(N, Fo, dt=F32)
+        self.xhat_nct = e(B, Fo, T, dt=F32)
+        # scalars: 0 x_loss, 1 sqerr, 4..7 EMA diagnostics
+        self.stats = torch.zeros(8, device=dev, dtype=F32)
+        self.loss_part = e(1024, dt=F32)
+        self.gn_part = e(B * 2 * 8 * 3, dt=F32)
+        if not train:
+            return
+        self.dxhat = e(N, Fo)
+        self.df1 = e(N, S)
+        self.dr = [e(N, Cd + S) for _ in range(2)]
+        self.dg = e(N, Cd)
+        self.du = e(N, 2 * Cd)
+        self.gnb_part = e(B * 64 * 2, dt=F32)
+        self.colsum_b = e(B * 2 * max(Cd, C), dt=F32)   # per-utterance column sums of du
+        self.dgam_b = e(B * 2 * max(Cd, C), dt=F32)
+        self.dbet_b = e(B * 2 * max(Cd, C), dt=F32)
+        self.dz = e(N, Z)
+        self.dc = [e(N, C) for _ in range(2)]
+        self.dh = e(N, C)
+        self.tmp = e(N, C)
+        self.dyemb = e(B, d["ydim"], dt=F32)
+        self.cs_part = e(64 * max(C, 2 * Cd, Cd + S, mel, 1024), dt=F32)
+
+
+class VQVAEEngine:
+    def __init__(self, model, device, compute_dtype="fp32"):
+        self.m = model
+        self.device = torch.device(device)
+        self.cd = torch.bfloat16 if compute_dtype in ("bf16", "bfloat16") else F32
+        self.dt = ops.dt_code(self.cd)
+        L.load()
+        enc, dec = model.encoder, model.decoder
+        self.dims = d = dict(mel=enc.in_ch, C=enc.ch, Z=enc.z_ch, ns=enc.n_stacks, Cd=dec.ch, S=dec.skip_ch,
+                             F=dec.final_ch, cond=dec.cond_ch, nd=dec.n_stacks, K=model.quantizer.z_num,
+                             ydim=model.embeds._embedding.weight.shape[1], jitter_p=model.jitter.probability)
+        assert d["Z"] == 128 and model.quantizer.z_dim == 128, "the fused VQ kernel is built for z_dim = 128"
+        self._flatten()
+        self._build_layers()
+        self._ws = {}
+        self.opt_ready = False
+
+    # ------------------------------------------------------------ parameters
+    def _flatten(self):
+        params = list(self.m.parameters())
+        self.params = params
+        total = sum(p.numel() for p in params)
+        self.flat_p = torch.empty(total, device=self.device, dtype=F32)
+        self.flat_g = torch.zeros(total, device=self.device, dtype=F32)
+        self.gviews = {}
+        off = 0
+        with torch.no_grad():
+            for p in params:
+                n = p.numel()
+                self.flat_p[off:off + n].copy_(p.detach().reshape(-1))
+                p.data = self.flat_p[off:off + n].view_as(p)
+                self.gviews[p] = self.flat_g[off:off + n].view_as(p)
+                off += n
+        self.n_params = total
+        self._p0_ptr = params[0].data_ptr()
+        enc_ids = {id(p) for p in self.m.encoder.parameters()}
+        self.enc_end = sum(p.numel() for p in params if id(p) in enc_ids)
+        assert all(id(p) in enc_ids for p in params[: len(enc_ids)]), 'encoder parameters must come first'
+
+    def params_intact(self):
+        return self.params[0].data_ptr() == self._p0_ptr and all(
+            p.data_ptr() == self.flat_p.data_ptr() + 4 * o for p, o in self._offsets())
+
+    def _offsets(self):
+        off = 0
+        for p in self.params:
+            yield p, off
+            off += p.numel()
+
+    def g(self, p):
+        return self.gviews[p]
+
+    def _build_layers(self):
+        m, d, dev = self.m, self.dims, self.device
+        enc, dec = m.encoder.encode, m.decoder
+        ns, nd = d["ns"], d["nd"]
+
+        def mk(mod, name, dtype=None):
+            kind = 1 if mod.transposed else 0
+            Lr = ConvLayer(mod, name, kind, mod.cin, mod.cout, mod.k, mod.k - 1 - mod.padding if kind else mod.padding)
+            Lr.wp = torch.empty(Lr.cout, Lr.k * Lr.cin, device=dev, dtype=dtype or self.cd)
+            Lr.norm = torch.empty(Lr.rows, device=dev, dtype=F32)
+            return Lr
+
+        self.enc0 = mk(enc[0], "encoder.encode.0")
+        self.enc_k3 = [mk(enc[i].stack[1], f"encoder.encode.{i}.stack.1") for i in range(1, ns + 1)]
+        self.enc_gn = [enc[i].stack[2] for i in range(1, ns + 1)]
+        self.enc_sk = [mk(enc[i].skip_layer, f"encoder.encode.{i}.skip_layer") for i in range(1, ns + 1)]
+        self.enc_out = mk(enc[ns + 2], f"encoder.encode.{ns + 2}")
+        self.dec0 = mk(dec.layers[0], "decoder.layers.0")
+        self.dec_in = [mk(dec.layers[i].conv_in, f"decoder.layers.{i}.conv_in") for i in range(1, nd + 1)]
+        self.dec_gn = [dec.layers[i].norm_layer for i in range(1, nd + 1)]
+        self.dec_cond = [mk(dec.layers[i].conv_cond, f"decoder.layers.{i}.conv_cond", F32) for i in range(1, nd + 1)]
+        self.dec_rs = [mk(dec.layers[i].res_skip_layers, f"decoder.layers.{i}.res_skip_layers")
+                       for i in range(1, nd + 1)]
+        self.fin1 = mk(dec.final_layer[1], "decoder.final_layer.1")
+        self.fin2 = mk(dec.final_layer[3], "decoder.final_layer.3")
+        self.convs = ([self.enc0] + [x for pair in zip(self.enc_k3, self.enc_sk) for x in pair] + [self.enc_out, self.dec0]
+                      + [x for tr in zip(self.dec_in, self.dec_cond, self.dec_rs) for x in tr] + [self.fin1, self.fin2])
+        # split-K factors for the wgrad GEMMs (config-2 sized: ~512-768 workgroups)
+        N_ref = 64 * 256
+        for Lr in self.convs:
+            if Lr in self.dec_cond:
+                Lr.splits = 1
+                continue
+            r, c = (Lr.cin, Lr.k * Lr.cout) if Lr.kind else (Lr.cout, Lr.k * Lr.cin)
+            tiles = math.ceil(r / 128) * math.ceil(c / 128)
+            Lr.splits = max(1, min(16, _pow2_floor(max(1, 640 // tiles)), N_ref // 512))
+        # slab arena: one backward group's slabs at a time (kept L2/MALL-resident)
+        groups = self._bwd_groups()
+        arena = max(sum(Lr.splits * Lr.rows * Lr.cols for Lr in grp) for grp in groups)
+        self.arena = torch.empty(arena, device=dev, dtype=F32)
+        for grp in groups:
+            off = 0
+            for Lr in grp:
+                n = Lr.splits * Lr.rows * Lr.cols
+                Lr.slab = self.arena[off:off + n].view(Lr.splits, Lr.rows, Lr.cols)
+                off += n
+        self.wn_fwd_table = ops.wn_table([self._wn_entry(Lr, bwd=False) for Lr in self.convs])
+        self.wn_bwd_tables = {id(grp[0]): ops.wn_table([self._wn_entry(Lr, bwd=True) for Lr in grp]) for grp in groups}
+        self.groups = groups
+
+    def _bwd_groups(self):
+        ns, nd = self.dims["ns"], self.dims["nd"]
+        gr = [[self.fin1, self.fin2]]
+        gr += [[self.dec_in[i], self.dec_cond[i], self.dec_rs[i]] for i in range(nd)]
+        gr += [[self.dec0], [self.enc_out]]
+        gr += [[self.enc_k3[i], self.enc_sk[i]] for i in range(ns)]
+        gr += [[self.enc0]]
+        return gr
+
+    def _wn_entry(self, Lr, bwd):
+        mod = Lr.mod
+        wn = mod.has_weight_norm
+        v = mod.weight_v if wn else mod.weight
+        e = dict(v=v, g=mod.weight_g if wn else None, w_packed=Lr.wp, norm=Lr.norm, kind=Lr.kind, cout=Lr.cout,
+                 cin=Lr.cin, k=Lr.k, dtype=ops.dt_code(Lr.wp.dtype), splits=Lr.splits)
+        if bwd:
+            e.update(dv=self.g(v), dg=self.g(mod.weight_g) if wn else None, slabs=Lr.slab)
+        return e
+
+    def refresh_tables(self):
+        """Rebuild descriptor tables (after remove_weight_norm or a re-flatten)."""
+        self.wn_fwd_table = ops.wn_table([self._wn_entry(Lr, bwd=False) for Lr in self.convs])
+        self.wn_bwd_tables = {id(g[0]): ops.wn_table([self._wn_entry(Lr, bwd=True) for Lr in g]) for g in self.groups}
+
+    def ws(self, B, T, train=True):
+        key = (B, T, train)
+        w = self._ws.get(key)
+        if w is None:
+            if train and (B, T, False) in self._ws:
+                del self._ws[(B, T, False)]
+            w = self._ws[key] = Workspace(self, B, T, train)
+        return w
+
+    # ------------------------------------------------------------ conv helpers
+    def fwd(self, Lr, x, y, T, **kw):
+        ops.conv_fwd(x, Lr.wp, y, T=T, cin=Lr.cin, cout=Lr.cout, ntaps=Lr.k, pad=Lr.pad, **kw)
+
+    def dgrad(self, Lr, dy, dx, T, **kw):
+        ops.conv_dgrad(dy, Lr.wp, dx, T=T, cin=Lr.cout, cout=Lr.cin, ntaps=Lr.k, pad=Lr.pad, **kw)
+
+    def wgrad(self, Lr, dy, x, T, pro=L.PRO_NONE, scale=1.0):
+        if Lr.kind == 0:
+            ops.conv_wgrad(dy, x, Lr.slab, T=T, r_dim=Lr.cout, c_dim=Lr.cin, ntaps=Lr.k, pad=Lr.pad, shift_sign=1,
+                           q_prologue=pro, pro_scale=scale, splits=Lr.splits)
+        else:
+            assert pro == L.PRO_NONE
+            ops.conv_wgrad(x, dy, Lr.slab, T=T, r_dim=Lr.cin, c_dim=Lr.cout, ntaps=Lr.k, pad=Lr.pad, shift_sign=-1,
+                           splits=Lr.splits)
+
+    def bias_grad(self, Lr, dy, w):
+        ops.colsum(dy, w.cs_part, self.g(Lr.mod.bias))
+
+    # ------------------------------------------------------------ forward
+    def pack_weights(self):
+        ops.weight_norm_fwd(self.wn_fwd_table)
+
+    def embed_and_cond(self, w, y):
+        ops.embedding_fwd(self.m.embeds._embedding.weight, y.reshape(-1), w.yemb)
+        for i, Lr in enumerate(self.dec_cond):
+            ops.linear_f32(w.yemb, Lr.wp, Lr.mod.bias, w.condbias[i])
+
+    def encoder_fwd(self, w, x_nct):
+        T = w.T
+        ops.nct_to_ntc(x_nct, w.x)
+        self.fwd(self.enc0, w.x, w.c[0], T, bias=self.enc0.mod.bias)
+        for i in range(self.dims["ns"]):
+            k3, sk, gn = self.enc_k3[i], self.enc_sk[i], self.enc_gn[i]
+            self.fwd(k3, w.c[i], w.h[i], T, prologue=L.PRO_LRELU, bias=k3.mod.bias)
+            ops.groupnorm_stats(w.h[i], T, 1, w.gn_part, w.enc_mr[i])
+            self.fwd(sk, w.c[i], w.c[i + 1], T, bias=sk.mod.bias, gn_h=w.h[i], gn_mr=w.enc_mr[i],
+                     gn_gamma=gn.weight, gn_beta=gn.bias)
+        self.fwd(self.enc_out, w.c[-1], w.z, T, prologue=L.PRO_LRELU, bias=self.enc_out.mod.bias, out_f32=True)
+
+    def decoder_fwd(self, w, zq_c):
+        T, nd, Cd = w.T, self.dims["nd"], self.dims["Cd"]
+        self.fwd(self.dec0, zq_c, w.xs[0], T, bias=self.dec0.mod.bias)
+        for i in range(nd):
+            ci, gn, rs = self.dec_in[i], self.dec_gn[i], self.dec_rs[i]
+            self.fwd(ci, w.xs[i], w.u[i], T, bias=ci.mod.bias, rowbias=w.condbias[i])
+            ops.groupnorm_stats(w.u[i], T, 2, w.gn_part, w.dec_mr[i])
+            ops.gn_glu_fwd(w.u[i], w.g[i], T, w.dec_mr[i], gn.weight, gn.bias)
+            self.fwd(rs, w.g[i], w.xs[i + 1], T, bias=rs.mod.bias, res=w.xs[i], out2=w.skip32, split_col=Cd,
+                     out2_accumulate=(i > 0))
+        if w.skip_c is not w.skip32:
+            ops.convert_2d(w.skip32, w.skip_c)
+        self.fwd(self.fin1, w.skip_c, w.f1, T, prologue=L.PRO_SCALE_RELU, pro_scale=math.sqrt(1.0 / (nd + 1)),
+                 bias=self.fin1.mod.bias)
+        self.fwd(self.fin2, w.f1, w.xhat, T, prologue=L.PRO_RELU, bias=self.fin2.mod.bias, out_f32=True)
+
+    # ------------------------------------------------------------ quantizer host logic
+    def _perm_rows(self, n, K, rank_offset=0, n_local=None):
+        """torch.randperm(n)[:K] on the CPU generator (layers_vq.py:197,213),
+        mapped to local row ids (-1 = row owned by another rank)."""
+        perm = torch.randperm(n)[:K]
+        if n_local is not None:
+            loc = perm - rank_offset
+            perm = torch.where((loc >= 0) & (loc < n_local), loc, torch.full_like(loc, -1))
+        return perm.pin_memory().to(self.device, non_blocking=True)
+
+    def _tile_rows(self, w):
+        """N < K path of _tile (layers_vq.py:183-190): repeat z with N(0, 0.01/sqrt(D))
+        noise drawn on the CPU generator, then take perm rows.  Host side; rare."""
+        z = w.z.detach().cpu()
+        n, dd = z.shape
+        K = self.dims["K"]
+        rep = (K + n - 1) // n
+        zt = z.repeat(rep, 1)
+        zt = zt + torch.randn_like(zt) * (0.01 / np.sqrt(dd))
+        rows = zt[torch.randperm(zt.shape[0])][:K]
+        return rows.to(self.device, non_blocking=False)
+
+    def jitter_map(self, T):
+        """Jitter (layers_vq.py:353-379): numpy-RNG neighbour map, consuming the
+        global numpy stream exactly like np.random.choice (one uniform per
+        choice).  Replaces with probability 1-p (the reference's indexing)."""
+        p = self.dims["jitter_p"]
+        src = np.arange(T, dtype=np.int32)
+        cdf0 = np.cumsum([p, 1 - p])
+        cdf0 = cdf0 / cdf0[-1]
+        rs = np.random.random_sample
+        for i in range(T):
+            u = rs()
+            choice = 1 if u < cdf0[0] else 0  # np.random.choice([1, 0], p=[p, 1-p])
+            if choice == 0:  # [True, False][0] -> replace
+                if i == 0:
+                    src[i] = 1
+                elif i == T - 1:
+                    src[i] = T - 2
+                else:
+                    u2 = rs()
+                    src[i] = i + (-1 if u2 < 0.5 else 1)
+        return src
+
+    # ------------------------------------------------------------ backward
+    def _bview(self, buf, B, C):
+        return buf.view(-1)[: B * C].view(B, C)
+
+    def encoder_bwd(self, w, grad_scale=1.0):
+        """Backward of beta*z_enc_loss through the encoder: the commitment term is
+        the encoder's only gradient source (z_vq is a no-grad gather under
+        reduction='frame_mean', layers_vq.py:292,315)."""
+        T, N, ns, C = w.T, w.N, self.dims["ns"], self.dims["C"]
+        B = w.B
+        ops.vq_commit_bwd(w.z, w.zq, 2.0 * self.m.beta * grad_scale / N, w.dz)
+        eo = self.enc_out
+        self.bias_grad(eo, w.dz, w)
+        self.wgrad(eo, w.dz, w.c[ns], T, pro=L.PRO_LRELU)
+        cur = w.dc[0]
+        self.dgrad(eo, w.dz, cur, T, mask=w.c[ns], mask_slope=0.2)
+        ops.weight_norm_bwd(self.wn_bwd_tables[id(eo)])
+        cs_b, dg_b, db_b = (self._bview(t, B, C) for t in (w.colsum_b, w.dgam_b, w.dbet_b))
+        for i in reversed(range(ns)):
+            k3, sk, gn = self.enc_k3[i], self.enc_sk[i], self.enc_gn[i]
+            nxt = w.dc[(ns - i) % 2]
+            # cur = dL/dc_{i+1}, the gradient w.r.t. block i's output GN(h_i) + skip(c_i)
+            self.bias_grad(sk, cur, w)
+            self.wgrad(sk, cur, w.c[i], T)
+            ops.gn_bwd(cur, w.h[i], w.dh, T, 1, False, w.enc_mr[i], gn.weight, gn.bias, w.gnb_part, cs_b, dg_b, db_b)
+            ops.colsum(cs_b, w.cs_part, self.g(k3.mod.bias))
+            ops.colsum(dg_b, w.cs_part, self.g(gn.weight))
+            ops.colsum(db_b, w.cs_part, self.g(gn.bias))
+            self.wgrad(k3, w.dh, w.c[i], T, pro=L.PRO_LRELU)
+            self.dgrad(k3, w.dh, w.tmp, T, mask=w.c[i], mask_slope=0.2)
+            self.dgrad(sk, cur, nxt, T, res=w.tmp)
+            ops.weight_norm_bwd(self.wn_bwd_tables[id(k3)])
+            cur = nxt
+        # cur = dL/dc_0 (conv0 output); conv0's input (the mel batch) needs no gradient
+        self.bias_grad(self.enc0, cur, w)
+        self.wgrad(self.enc0, cur, w.x, T)
+        ops.weight_norm_bwd(self.wn_bwd_tables[id(self.enc0)])
+
+    def decoder_bwd(self, w):
+        T, nd, Cd, B = w.T, self.dims["nd"], self.dims["Cd"], w.B
+        f1, f2 = self.fin1, self.fin2
+        dxhat = w.dxhat
+        self.bias_grad(f2, dxhat, w)
+        self.wgrad(f2, dxhat, w.f1, T, pro=L.PRO_RELU)
+        self.dgrad(f2, dxhat, w.df1, T, mask=w.f1, mask_slope=0.0)
+        s = math.sqrt(1.0 / (nd + 1))
+        self.bias_grad(f1, w.df1, w)
+        self.wgrad(f1, w.df1, w.skip_c, T, pro=L.PRO_SCALE_RELU, scale=s)
+        cur, nxt = w.dr[0], w.dr[1]
+        # dL/dskip (identical for every block) -> tail columns of both [dx | dskip] buffers
+        self.dgrad(f1, w.df1, cur[:, Cd:], T, mask=w.skip_c, mask_slope=0.0, mask_scale=s)
+        ops.convert_2d(cur[:, Cd:], nxt[:, Cd:])
+        ops.convert_2d(None, cur, cols=Cd)  # dL/dx_{nd+1} = 0: the last residual output is unused
+        ops.weight_norm_bwd(self.wn_bwd_tables[id(f1)])
+        ops.zero_(w.dyemb)
+        C2 = 2 * Cd
+        cs_b, dg_b, db_b = (self._bview(t, B, C2) for t in (w.colsum_b, w.dgam_b, w.dbet_b))
+        for i in reversed(range(nd)):
+            ci, cond, gn, rs = self.dec_in[i], self.dec_cond[i], self.dec_gn[i], self.dec_rs[i]
+            # cur = [dL/dx_{i+1} | dL/dskip]
+            self.bias_grad(rs, cur, w)
+            self.wgrad(rs, cur, w.g[i], T)
+            self.dgrad(rs, cur, w.dg, T)
+            ops.gn_bwd(w.dg, w.u[i], w.du, T, 2, True, w.dec_mr[i], gn.weight, gn.bias, w.gnb_part, cs_b, dg_b,
+                       db_b)
+            ops.colsum(cs_b, w.cs_part, self.g(ci.mod.bias))
+            ops.colsum(cs_b, w.cs_part, self.g(cond.mod.bias))
+            ops.colsum(dg_b, w.cs_part, self.g(gn.weight))
+            ops.colsum(db_b, w.cs_part, self.g(gn.bias))
+            ops.zero_(cond.slab)
+            ops.linear_bwd_f32(cs_b, w.yemb, cond.wp, dW=cond.slab.view(cond.rows, cond.cols), dc=w.dyemb)
+            self.wgrad(ci, w.du, w.xs[i], T)
+            self.dgrad(ci, w.du, nxt[:, :Cd], T, res=cur[:, :Cd])
+            ops.weight_norm_bwd(self.wn_bwd_tables[id(ci)])
+            cur, nxt = nxt, cur
+        dx1 = cur[:, :Cd]  # dL/dx_1, the ConvT0 output; z_vq itself receives no gradient
+        self.bias_grad(self.dec0, dx1, w)
+        self.wgrad(self.dec0, dx1, w.zq_in, T)
+        ops.weight_norm_bwd(self.wn_bwd_tables[id(self.dec0)])
+        emb_g = self.g(self.m.embeds._embedding.weight)
+        ops.zero_(emb_g)
+        ops.embedding_bwd(w.dyemb, w.y_dev, emb_g)
+
+    # ------------------------------------------------------------ quantizer
+    def vq_init_if_needed(self, w):
+        """init_emb (layers_vq.py:192-201) on the first training forward."""
+        q = self.m.quantizer
+        if q.initialized:
+            return False
+        K = self.dims["K"]
+        if w.N < K:
+            rows = self._tile_rows(w)
+            q.embeddings.copy_(rows)
+        else:
+            perm = self._perm_rows(w.N * self.world, K, self.rank * w.N, w.N if self.world > 1 else None)
+            ops.gather_rows(w.z, perm, q.embeddings)
+            if self.world > 1:
+                self.comm.all_reduce_sum(q.embeddings)
+        ops.convert_2d(q.embeddings, q.emb_sum)
+        q.emb_elem.fill_(1.0)
+        q.mark_initialized()
+        return True
+
+    def vq_forward_train(self, w):
+        q = self.m.quantizer
+        K = self.dims["K"]
+        self.vq_init_if_needed(w)
+        ops.zero_(w.ema)
+        ops.vq_forward(w.z, q.embeddings, w.idx, w.zq, w.zq_c, w.stats[1:2], w.vq_part, w.bsum, w.bcnt)
+        # rows for dead-code replacement: z[randperm(N)[:K]] (update_emb, layers_vq.py:212-213)
+        if w.N * self.world < K:
+            w.rand_rows.copy_(self._tile_rows(w))
+        else:
+            perm = self._perm_rows(w.N * self.world, K, self.rank * w.N, w.N if self.world > 1 else None)
+            ops.gather_rows(w.z, perm, w.rand_rows)
+        if self.world > 1:
+            self._ema_work = self.comm.all_reduce_sum(w.ema, async_op=True)
+
+    def vq_ema_update(self, w):
+        q = self.m.quantizer
+        if getattr(self, "_ema_work", None) is not None:
+            self._ema_work.wait()
+            self._ema_work = None
+        ops.vq_ema_update(q.emb_sum, q.emb_elem, q.embeddings, w.bsum, w.bcnt, w.rand_rows, q.mu, q.threshold,
+                          w.stats[4:8])
+
+    # ------------------------------------------------------------ full step
+    world, rank, comm = 1, 0, None
+
+    def forward_train(self, x, y):
+        """Training forward (saves every activation the backward needs).
+        x (B, mel, T) f32 device, y (B, 1) int64 device."""
+        B, _, T = x.shape
+        w = self.ws(B, T, train=True)
+        w.y_dev = y.reshape(-1)
+        w.x_nct = x
+        self.pack_weights()
+        self.embed_and_cond(w, w.y_dev)
+        self.encoder_fwd(w, x)
+        self.vq_forward_train(w)
+        w.zq_in = w.zq_c
+        if self.dims["jitter_p"] > 0 and self.m.jitter.training:
+            src = torch.from_numpy(self.jitter_map(T)).pin_memory()
+            w.src_t.copy_(src, non_blocking=True)
+            ops.time_gather(w.zq_c, w.zq_j, B, T, w.src_t)
+            w.zq_in = w.zq_j
+        self.decoder_fwd(w, w.zq_in)
+        ops.logloss_fwd_bwd(x, w.xhat, 1.0 / (B * T), w.dxhat, w.stats[0:1], w.loss_part)
+        return w
+
+    def backward(self, w, grad_loss=None):
+        self.encoder_bwd(w)
+        if self.world > 1:
+            self.comm.grads_ready(self.flat_g, 0, self.enc_end)
+        self.decoder_bwd(w)
+        if self.world > 1:
+            self.comm.grads_ready(self.flat_g, self.enc_end, self.n_params)
+            self.comm.finish()
+
+    def init_optimizer(self, lr, betas=(0.5, 0.999), eps=1e-8, max_grad_norm=10.0, sched_step=None, sched_gamma=1.0):
+        dev = self.device
+        self.exp_avg = torch.zeros(self.n_params, device=dev, dtype=F32)
+        self.exp_avg_sq = torch.zeros(self.n_params, device=dev, dtype=F32)
+        self.opt_step = torch.zeros(1, device=dev, dtype=torch.int64)
+        self.hyper = torch.zeros(8, device=dev, dtype=F32)
+        self.sumsq = torch.zeros(1, device=dev, dtype=F32)
+        self.norm_part = torch.zeros(1024, device=dev, dtype=F32)
+        self.lr0, self.betas, self.eps, self.max_grad_norm = lr, betas, eps, max_grad_norm
+        self.sched_step = sched_step or (1 << 30)
+        self.sched_gamma = sched_gamma
+        self.opt_ready = True
+
+    def optimizer_step(self):
+        if self.max_grad_norm > 0:
+            ops.grad_sq_norm(self.flat_g, self.norm_part, self.sumsq)
+        ops.adam_hyper(self.opt_step, self.lr0, self.sched_gamma, self.sched_step, self.betas[0], self.betas[1],
+                       self.eps, self.hyper)
+        ops.adam_step(self.flat_p, self.flat_g, self.exp_avg, self.exp_avg_sq, self.hyper,
+                      self.sumsq if self.max_grad_norm > 0 else None, float(self.max_grad_norm))
+
+    def train_step(self, x, y):
+        """One full training step (trainer/basic.py:55-79): forward, backward,
+        clip, Adam, StepLR, EMA codebook update.  Returns the device stats
+        vector [x_loss, sqerr, -, -, entropy, used_curr, usage, diff_emb]."""
+        assert self.opt_ready, "init_optimizer() first"
+        w = self.forward_train(x, y)
+        self.backward(w)
+        self.optimizer_step()
+        self.vq_ema_update(w)
+        return w
+
+    def loss_detail(self, w, stats_host):
+        """The reference's loss dict (vqvae.py:85-87, layers_vq.py:228-233)."""
+        s = stats_host.tolist()
+        n = w.N
+        vq = s[1] / n
+        xl = s[0]
+        d = {"Total": float(np.float32(xl) + np.float32(self.m.beta) * np.float32(vq)), "VQ loss": vq, "X like": xl}
+        d.update({"entropy": s[4], "used_curr": s[5], "usage": s[6], "diff_emb": s[7]})
+        return d
+
+    # ------------------------------------------------------------ inference
+    def forward_eval(self, x, y):
+        """model.eval() forward: no EMA init/update, no jitter (layers_vq.py:282,295,354)."""
+        B, _, T = x.shape
+        w = self.ws(B, T, train=False) if (B, T, True) not in self._ws else self._ws[(B, T, True)]
+        w.y_dev = y.reshape(-1)
+        self.pack_weights()
+        self.embed_and_cond(w, w.y_dev)
+        self.encoder_fwd(w, x)
+        q = self.m.quantizer
+        ops.vq_forward(w.z, q.embeddings, w.idx, w.zq, w.zq_c, w.stats[1:2], w.vq_part, None, None)
+        w.zq_in = w.zq_c
+        self.decoder_fwd(w, w.zq_c)
+        ops.logloss_fwd_bwd(x, w.xhat, 1.0 / (B * T), None, w.stats[0:1], w.loss_part)
+        ops.ntc_to_nct(w.xhat, w.xhat_nct)
+        return w
+
+    def encode(self, x):
+        """Model.encode (vqvae.py:45-52): encoder + nearest-code index, (B, T) int64."""
+        B, _, T = x.shape
+        w = self.ws(B, T, train=False) if (B, T, True) not in self._ws else self._ws[(B, T, True)]
+        self.pack_weights()
+        self.encoder_fwd(w, x)
+        q = self.m.quantizer
+        ops.vq_forward(w.z, q.embeddings, w.idx, None, None, None, w.vq_part, None, None)
+        return w.idx.view(B, T).clone()
+
+    def decode(self, z_idx, y):
+        """Model.decode (vqvae.py:55-60): codebook gather + decoder, (B, F, T) f32."""
+        B, T = z_idx.shape
+        w = self.ws(B, T, train=False) if (B, T, True) not in self._ws else self._ws[(B, T, True)]
+        w.y_dev = y.reshape(-1)
+        self.pack_weights()
+        self.embed_and_cond(w, w.y_dev)
+        q = self.m.quantizer
+        ops.gather_rows(q.embeddings, z_idx.reshape(-1).contiguous(), w.zq)
+        ops.convert_2d(w.zq, w.zq_c)
+        self.decoder_fwd(w, w.zq_c)
+        ops.ntc_to_nct(w.xhat, w.xhat_nct)
+        return w.xhat_nct.clone()

@@ -1,0 +1,91 @@
+"""Parameter containers of the VQ-VAE with the reference's module tree and
+state_dict keys (vae_npvc/model/layers.py, vqvae.py).
+
+These modules only own parameters: the arithmetic of the whole training step
+runs in the HIP engine (vae_npvc_amd/engine/step.py).  Registration order is
+bias -> weight_g -> weight_v for every weight-normed conv, the order
+nn.utils.weight_norm leaves in the reference (so model.parameters() order,
+and therefore optimizer state_dicts, line up with reference checkpoints).
+"""
+import math
+
+import torch
+import torch.nn as nn
+
+
+class WNConv1d(nn.Module):
+    """Weight-normed stride-1 Conv1d (kind 0, v [cout, cin, k], g [cout,1,1]) or
+    ConvTranspose1d (kind 1, v [cin, cout, k], g [cin,1,1]); nn.utils.weight_norm
+    with dim=0 as applied at vqvae.py:203-208,329-334."""
+
+    def __init__(self, cin, cout, k, transposed=False, padding=None):
+        super().__init__()
+        self.cin, self.cout, self.k, self.transposed = cin, cout, k, transposed
+        self.padding = (k - 1) // 2 if padding is None else padding
+        bound = 1.0 / math.sqrt((cout if transposed else cin) * k)
+        self.bias = nn.Parameter(torch.empty(cout).uniform_(-bound, bound))
+        vshape = (cin, cout, k) if transposed else (cout, cin, k)
+        v = torch.empty(vshape).uniform_(-bound, bound)
+        self.weight_g = nn.Parameter(v.flatten(1).norm(dim=1).view(vshape[0], 1, 1))
+        self.weight_v = nn.Parameter(v)
+        self.has_weight_norm = True
+
+    @property
+    def kind(self):
+        return 1 if self.transposed else 0
+
+    def effective_weight(self):
+        """w = g * v/||v|| in the reference's (torch) layout, for export/inspection."""
+        if not self.has_weight_norm:
+            return self.weight
+        return torch._weight_norm(self.weight_v, self.weight_g, 0)
+
+    def remove_weight_norm(self):
+        """Bake w into a plain `weight` parameter (torch.nn.utils.remove_weight_norm)."""
+        if not self.has_weight_norm:
+            raise ValueError("weight_norm not present")
+        w = self.effective_weight().detach()
+        del self.weight_g
+        del self.weight_v
+        self.weight = nn.Parameter(w)
+        self.has_weight_norm = False
+
+    def extra_repr(self):
+        return f"{self.cin}, {self.cout}, kernel_size={self.k}, padding={self.padding}, transposed={self.transposed}"
+
+
+class ResidualBlock(nn.Module):
+    """Conv1d_Layernorm_LRelu_Residual (layers.py:129-178) with layers=1:
+    out = GroupNorm(1, C)(Conv_k(LReLU0.2(c))) + Conv_1(c)."""
+
+    def __init__(self, channels, kernel_size=3):
+        super().__init__()
+        self.stack = nn.Sequential(nn.LeakyReLU(0.2), WNConv1d(channels, channels, kernel_size),
+                                   nn.GroupNorm(1, channels, eps=1e-5, affine=True))
+        self.skip_layer = WNConv1d(channels, channels, 1)
+
+
+class ResSkipBlock(nn.Module):
+    """DeConv1d_Layernorm_GLU_ResSkip (layers.py:181-249): h = GN(2, 2C)(ConvT(x) +
+    Conv_1(c)); g = tanh(h[:C])*sigmoid(h[C:]); r = Conv_1(g); x' = r[:C] + x;
+    skip = r[C:]."""
+
+    def __init__(self, channels, cond_channels, skip_channels, kernel_size=3):
+        super().__init__()
+        self.conv_in = WNConv1d(channels, 2 * channels, kernel_size, transposed=True)
+        self.norm_layer = nn.GroupNorm(2, 2 * channels, eps=1e-5, affine=True)
+        self.conv_cond = WNConv1d(cond_channels, 2 * channels, 1)
+        self.res_skip_layers = WNConv1d(channels, channels + skip_channels, 1)
+        self.in_channels = channels
+
+
+class Conditions(nn.Module):
+    """Speaker embedding (layers.py:12-60, normalize=False => nn.Embedding)."""
+
+    def __init__(self, cond_num, cond_dim):
+        super().__init__()
+        self._embedding = nn.Embedding(cond_num, cond_dim)
+        self.cond_num = cond_num
+
+
+LOG_2PI = math.log(2.0 * math.pi)

@@ -1,0 +1,175 @@
+"""Drop-in `Model` for `model_type: vae_npvc_amd.model.vqvae` (the reference's
+plugin seam, vae_npvc/trainer/basic.py:13,24-26): same constructor
+`Model(arch_dict)`, same methods (forward / encode / decode / infer /
+remove_weight_norm / load_state_dict, vqvae.py:11-119), same module tree and
+state_dict keys (210 for the vcc20 config), so reference checkpoints load
+unchanged.  The computation is the MI355X engine (vae_npvc_amd/engine/step.py);
+there is no CPU implementation — calling the model on CPU tensors raises.
+
+Extra config key (not in the reference YAMLs): `compute_dtype: fp32|bf16`
+(default fp32 = the reference's arithmetic; bf16 runs the conv GEMMs on bf16
+MFMA with fp32 accumulation, GroupNorm statistics, VQ and optimizer in fp32).
+"""
+import math
+
+import torch
+import torch.nn as nn
+
+from ..engine.step import VQVAEEngine
+from .layers import Conditions, ResidualBlock, ResSkipBlock, WNConv1d
+from .layers_vq import EMAVectorQuantizer, Jitter
+
+
+def _single(lst, what):
+    if len(lst) != 1:
+        raise NotImplementedError(f"{what}: only single-stage models (the baseline recipes) are supported")
+    return lst[0]
+
+
+class Encoder(nn.Module):
+    """vqvae.py:122-217 restricted to the baseline recipes' single stage
+    (stride 1, stack_layers 1, no dilation, non-causal)."""
+
+    def __init__(self, in_channels=(513,), out_channels=(1024,), downsample_scales=(1,), kernel_size=3,
+                 z_channels=128, dilation=True, stack_kernel_size=3, stack_layers=2, stacks=(3,),
+                 use_weight_norm=True, use_causal_conv=False):
+        super().__init__()
+        cin = _single(in_channels, "encoder.in_channels")
+        ch = _single(out_channels, "encoder.out_channels")
+        ns = _single(stacks, "encoder.stacks")
+        if _single(downsample_scales, "encoder.downsample_scales") != 1 or dilation or stack_layers != 1 \
+                or use_causal_conv or not use_weight_norm or kernel_size != 3 or stack_kernel_size != 3:
+            raise NotImplementedError("encoder: supported = k3, stride 1, stack_layers 1, no dilation, weight norm")
+        layers = [WNConv1d(cin, ch, kernel_size)]
+        layers += [ResidualBlock(ch, stack_kernel_size) for _ in range(ns)]
+        layers += [nn.LeakyReLU(negative_slope=0.2), WNConv1d(ch, z_channels, 1)]
+        self.encode = nn.Sequential(*layers)
+        self.in_ch, self.ch, self.z_ch, self.n_stacks = cin, ch, z_channels, ns
+
+
+class Decoder(nn.Module):
+    """vqvae.py:220-343 restricted to the single stage of the baseline recipes."""
+
+    def __init__(self, in_channels=(128,), out_channels=(256,), upsample_scales=(1,), cond_channels=128,
+                 skip_channels=80, final_channels=80, kernel_size=5, dilation=True, stack_kernel_size=3,
+                 stacks=(3,), use_weight_norm=True, use_causal_conv=False):
+        super().__init__()
+        cin = _single(in_channels, "decoder.in_channels")
+        ch = _single(out_channels, "decoder.out_channels")
+        nd = _single(stacks, "decoder.stacks")
+        if _single(upsample_scales, "decoder.upsample_scales") != 1 or dilation or use_causal_conv \
+                or not use_weight_norm or kernel_size != 3 or stack_kernel_size != 3:
+            raise NotImplementedError("decoder: supported = k3, stride 1, no dilation, weight norm")
+        self.layers = nn.ModuleList([WNConv1d(cin, ch, kernel_size, transposed=True)]
+                                    + [ResSkipBlock(ch, cond_channels, skip_channels, stack_kernel_size)
+                                       for _ in range(nd)])
+        self.final_layer = nn.Sequential(nn.ReLU(), WNConv1d(skip_channels, skip_channels, 1), nn.ReLU(),
+                                         WNConv1d(skip_channels, final_channels, 1))
+        self.ch, self.skip_ch, self.final_ch, self.cond_ch, self.n_stacks = (ch, skip_channels, final_channels,
+                                                                             cond_channels, nd)
+
+
+class _StepFunction(torch.autograd.Function):
+    """Autograd bridge: the engine's fused forward saves every activation and
+    its backward fills the flat gradient buffer; grads are returned per
+    parameter so a stock torch optimizer (the reference Trainer) works too."""
+
+    @staticmethod
+    def forward(ctx, engine, x, y, *params):
+        w = engine.forward_train(x, y)
+        ctx.engine, ctx.w = engine, w
+        loss = w.stats[0:1].clone()  # x_loss; beta * z_enc_loss is added below
+        vq = w.stats[1:2] / w.N
+        total = loss + engine.m.beta * vq
+        stats = w.stats.clone()
+        ctx.mark_non_differentiable(vq, stats)
+        return total.view(()), vq.view(()), stats
+
+    @staticmethod
+    def backward(ctx, g_total, g_vq, g_stats):
+        eng, w = ctx.engine, ctx.w
+        if g_total is None:
+            return (None, None, None) + tuple(None for _ in eng.params)
+        # The engine's backward assumes dL/dloss = 1; scale the flat gradient otherwise.
+        eng.backward(w)
+        grads = [eng.g(p).clone() for p in eng.params]
+        if not torch.equal(g_total, torch.ones_like(g_total)):
+            grads = [g * g_total for g in grads]
+        return (None, None, None) + tuple(grads)
+
+
+class Model(nn.Module):
+    def __init__(self, arch):
+        super().__init__()
+        self.encoder = Encoder(**arch["encoder"])
+        self.decoder = Decoder(**arch["decoder"])
+        self.use_ema = arch.get("use_ema", False)
+        if not self.use_ema:
+            raise NotImplementedError("use_ema: false (plain VectorQuantizer) is SURVEY §8f 'next' #1; "
+                                      "the baseline recipes use the EMA quantizer")
+        self.quantizer = EMAVectorQuantizer(arch.get("z_num", 512), arch.get("z_dim", 128), arch.get("mu", 0.9),
+                                            reduction="frame_mean")
+        self.embeds = Conditions(arch.get("y_num", 10), arch.get("y_dim", 128))
+        self.jitter = Jitter(probability=arch.get("jitter_p", 0.0))
+        self.beta = arch.get("beta", 0.01)
+        self.compute_dtype = arch.get("compute_dtype", "fp32")
+        self._engine = None
+
+    # ------------------------------------------------------------ engine
+    def engine(self, device=None):
+        dev = device if device is not None else self.quantizer.embeddings.device
+        if dev.type != "cuda":
+            raise RuntimeError("vae_npvc_amd.Model runs only on the MI355X (HIP) path; move it with .cuda()")
+        e = self._engine
+        if e is None or e.device != dev or not e.params_intact():
+            e = self._engine = VQVAEEngine(self, dev, self.compute_dtype)
+        return e
+
+    # ------------------------------------------------------------ reference API
+    def forward(self, input):
+        """(x (B, mel, T), y (B, 1)) -> (xhat (B, mel, T), loss, loss dict) (vqvae.py:70-90)."""
+        x, y_idx = input
+        eng = self.engine(x.device)
+        x = x.float().contiguous()
+        if self.training:
+            total, vq, stats = _StepFunction.apply(eng, x, y_idx, *eng.params)
+            w = eng._ws[(x.shape[0], x.shape[2], True)]
+            eng.vq_ema_update(w)  # update_emb runs inside the reference forward (layers_vq.py:295-296)
+            stats = w.stats.clone()
+            xhat = torch.empty_like(w.xhat_nct)
+            from .. import ops
+            ops.ntc_to_nct(w.xhat, xhat)
+            detail = eng.loss_detail(w, stats.cpu())
+            return xhat, total, detail
+        w = eng.forward_eval(x, y_idx)
+        stats = w.stats.cpu()
+        n = w.N
+        vq = stats[1].item() / n
+        xl = stats[0].item()
+        total = torch.tensor(xl + self.beta * vq, device=x.device)
+        return w.xhat_nct.clone(), total, {"Total": float(total), "VQ loss": vq, "X like": xl}
+
+    def encode(self, input):
+        x = input[0] if isinstance(input, (list, tuple)) else input
+        return self.engine(x.device).encode(x.float().contiguous())
+
+    def decode(self, input):
+        z_idx, y_idx = input
+        return self.engine(z_idx.device).decode(z_idx, y_idx)
+
+    def infer(self, input):
+        x, y_idx = input
+        return self.decode((self.encode(x), y_idx))
+
+    def remove_weight_norm(self):
+        for m in self.modules():
+            if isinstance(m, WNConv1d) and m.has_weight_norm:
+                m.remove_weight_norm()
+        self._engine = None
+
+    def load_state_dict(self, state_dict, strict=True):
+        out = super().load_state_dict(state_dict, strict=strict)
+        return out
+
+
+LOG_2PI = math.log(2.0 * math.pi)

@@ -64,11 +64,53 @@ def conv_args(x, w, y, *, T, cin, cout, ntaps, pad, prologue=L.PRO_NONE, pro_sca
     return a
 
 
+class LaunchProbe:
+    """Per-launch HIP-event timing of the conv GEMM kernels (bench.py's roofline
+    leg).  Records (kernel symbol, algorithmic FLOPs, start, end) per launch on
+    torch's current stream, i.e. the stream the kernels run on."""
+
+    _DT = {L.VQX_F32: "float", L.VQX_BF16: "unsigned short"}
+
+    def __init__(self):
+        self.records = []
+
+    def run(self, mode, dtype_code, pro, flops, fn):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        self.records.append((f"vqx::conv_gemm_kernel<{self._DT[dtype_code]}, {mode}, {pro}>", flops, e0, e1))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        agg = {}
+        for key, fl, e0, e1 in self.records:
+            a = agg.setdefault(key, [0, 0.0, 0.0])
+            a[0] += 1
+            a[1] += fl
+            a[2] += e0.elapsed_time(e1) * 1e-3
+        return {k: {"launches": n, "flops": f, "seconds": t, "avg_us": 1e6 * t / n, "tflops": f / t / 1e12}
+                for k, (n, f, t) in agg.items()}
+
+
+_probe = None
+
+
+def set_probe(p):
+    global _probe
+    _probe = p
+
+
 def conv_fwd(x, w, y, **kw):
     """y = epi(conv(pro(x), w)); x [N, cin], w packed [cout, ntaps*cin], y [N, cout]."""
     _check_cuda(x, w, y)
     a = conv_args(x, w, y, **kw)
-    call("vqx_conv1d_fwd", ctypes.byref(a), stream_ptr())
+    fn = lambda: call("vqx_conv1d_fwd", ctypes.byref(a), stream_ptr())  # noqa: E731
+    if _probe is None:
+        fn()
+    else:
+        _probe.run(0, a.dtype, a.prologue, 2.0 * a.n_rows * a.cout * a.ntaps * a.cin, fn)
     return y
 
 
@@ -77,7 +119,11 @@ def conv_dgrad(dy, w, dx, **kw):
     Pass cin=cout_f, cout=cin_f."""
     _check_cuda(dy, w, dx)
     a = conv_args(dy, w, dx, **kw)
-    call("vqx_conv1d_dgrad", ctypes.byref(a), stream_ptr())
+    fn = lambda: call("vqx_conv1d_dgrad", ctypes.byref(a), stream_ptr())  # noqa: E731
+    if _probe is None:
+        fn()
+    else:
+        _probe.run(1, a.dtype, a.prologue, 2.0 * a.n_rows * a.cout * a.ntaps * a.cin, fn)
     return dx
 
 
@@ -90,7 +136,11 @@ def conv_wgrad(p, q, slabs, *, T, r_dim, c_dim, ntaps, pad, shift_sign=1, q_prol
     a.n_rows, a.T, a.r_dim, a.c_dim, a.ntaps, a.pad, a.shift_sign = p.shape[0], T, r_dim, c_dim, ntaps, pad, shift_sign
     a.ldp, a.ldq = p.stride(0), q.stride(0)
     a.dtype, a.q_prologue, a.splits, a.pro_scale = dt_code(p.dtype), q_prologue, splits, pro_scale
-    call("vqx_conv1d_wgrad", ctypes.byref(a), stream_ptr())
+    fn = lambda: call("vqx_conv1d_wgrad", ctypes.byref(a), stream_ptr())  # noqa: E731
+    if _probe is None:
+        fn()
+    else:
+        _probe.run(2, a.dtype, a.q_prologue, 2.0 * a.n_rows * r_dim * ntaps * c_dim, fn)
     return slabs
 
 
@@ -227,3 +277,19 @@ def adam_hyper(step, lr0, gamma, step_size, beta1, beta2, eps, hyper):
 def adam_step(p, g, m, v, hyper, sumsq, max_norm):
     call("vqx_adam_step", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), ptr(hyper), ptr(sumsq), max_norm,
          stream_ptr())
+
+
+def convert_2d(src, dst, rows=None, cols=None):
+    """dst[:rows, :cols] = src (dtype-converting, strided); src=None zero-fills."""
+    rows = dst.shape[0] if rows is None else rows
+    cols = dst.shape[1] if cols is None else cols
+    call("vqx_convert_2d", ptr(src), src.stride(0) if src is not None else 0,
+         dt_code(src.dtype) if src is not None else 0, ptr(dst), dst.stride(0), dt_code(dst.dtype), rows, cols,
+         stream_ptr())
+    return dst
+
+
+def zero_(t):
+    """Zero a contiguous f32/bf16 device tensor with the native fill."""
+    flat = t.view(1, -1)
+    return convert_2d(None, flat)

@@ -1,0 +1,59 @@
+"""Data parallelism for the VQ-VAE step: one process per GPU, torch.distributed
+over RCCL (backend "nccl" on ROCm) across the node's xGMI links.
+
+Per step:
+  * gradients — the flat fp32 gradient buffer is all-reduced (mean) in
+    buckets as soon as a region is final: the encoder's region right after the
+    encoder backward (the encoder depends only on the commitment loss, so it
+    runs first), overlapping the decoder backward; the decoder/embedding region
+    at the end.  Mean over ranks of per-rank frame_mean losses equals the
+    global-batch loss, so clipping after the reduce is identical on all ranks.
+  * EMA statistics — bsum [K, D], bcnt [K] and the dead-code rows are summed
+    in ONE all-reduce right after the VQ kernel; it overlaps the decoder and
+    the backward (the codebook update runs at the end of the step).  Every
+    rank draws the same CPU randperm(N_global); each fills the rows it owns,
+    so the sum assembles exactly the global batch's z[perm[:K]].
+No other collective sits on the data path.
+"""
+import torch
+import torch.distributed as dist
+
+BUCKET_BYTES = 64 << 20  # ~16M fp32 gradients per all-reduce (per-link ring ≈ 0.5 ms at 8 GPUs)
+
+
+class Comm:
+    def __init__(self, group=None, bucket_bytes=BUCKET_BYTES):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.backend = dist.get_backend(group)
+        self.bucket = max(1, bucket_bytes // 4)
+        self.pending = []
+
+    def _avg_op(self):
+        return dist.ReduceOp.AVG if self.backend == "nccl" else dist.ReduceOp.SUM
+
+    def all_reduce_sum(self, t, async_op=False):
+        return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
+
+    def grads_ready(self, flat, lo, hi):
+        """Launch async mean all-reduces over flat[lo:hi] in buckets."""
+        op = self._avg_op()
+        for s in range(lo, hi, self.bucket):
+            view = flat[s: min(hi, s + self.bucket)]
+            work = dist.all_reduce(view, op=op, group=self.group, async_op=True)
+            self.pending.append((work, view))
+
+    def finish(self):
+        """Make the current stream wait for every launched reduce."""
+        for work, view in self.pending:
+            work.wait()
+            if self.backend != "nccl":
+                view.div_(self.world)
+        self.pending = []
+
+    def mean_scalars(self, t):
+        dist.all_reduce(t, op=self._avg_op(), group=self.group)
+        if self.backend != "nccl":
+            t.div_(self.world)
+        return t
