@@ -49,7 +49,11 @@ enum {
   VQX_EPI_GNADD = 1 << 4,   /* v += (gn_h[n][c]-mean[b])*rstd[b]*gamma[c]+beta[c] */
   VQX_EPI_SPLIT = 1 << 5,   /* cols >= split_col -> out2[n][c-split_col] (f32,
                                '+=' when out2_accumulate)                      */
-  VQX_EPI_OUTF32 = 1 << 6   /* y stored as f32 instead of `dtype`              */
+  VQX_EPI_OUTF32 = 1 << 6,  /* y stored as f32 instead of `dtype`              */
+  VQX_EPI_ACT = 1 << 7,     /* y = act(v), act = epi_act (VQX_PRO_LRELU/RELU)  */
+  VQX_EPI_ACT2 = 1 << 8     /* also y2[n][c] = act(v) (dtype): the producer writes
+                               the pre-activated copy its consumers read, so no
+                               GEMM applies an activation while staging        */
 };
 
 /*
@@ -86,6 +90,8 @@ typedef struct vqx_conv_args {
   int32_t epilogue;          /* VQX_EPI_* flags                                */
   int32_t split_col, out2_accumulate;
   float pro_scale, mask_slope, mask_scale;
+  void* y2;                  /* ACT2 destination [N][ldy2]                     */
+  int32_t ldy2, epi_act;
 } vqx_conv_args;
 
 int vqx_conv1d_fwd(const vqx_conv_args* a, vqx_stream_t stream);
@@ -283,6 +289,12 @@ int vqx_adam_hyper(int64_t* step, double lr0, double gamma, int32_t step_size, d
                    double beta2, double eps, float* hyper, vqx_stream_t stream);
 int vqx_adam_step(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper,
                   const float* sumsq, float max_norm, vqx_stream_t stream);
+
+/* dst[r][c] = act(scale * src[r][c]) with dtype conversion (act = VQX_PRO_*;
+ * the decoder's ReLU(sqrt(1/11) * skip) operand, vqvae.py:316-317). */
+int vqx_scale_act_2d(const void* src, int32_t ld_src, int32_t src_dtype, void* dst, int32_t ld_dst,
+                     int32_t dst_dtype, int64_t rows, int32_t cols, float scale, int32_t act,
+                     vqx_stream_t stream);
 
 /* 2-D strided copy with dtype conversion: dst[r][c] = src[r][c] for r < rows,
  * c < cols; src == NULL fills zeros.  Used for the decoder's skip-sum cast

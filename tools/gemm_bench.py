@@ -1,0 +1,70 @@
+"""Isolated conv-GEMM timing for profiling: the config-2 layer shapes.
+python tools/gemm_bench.py [--iters N] [--only NAME] [--dtype bf16]"""
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from vae_npvc_amd import _lib as L  # noqa: E402
+from vae_npvc_amd import ops  # noqa: E402
+
+SHAPES = {  # name: (mode, cin, cout, k, prologue)
+    "dec_in_fwd": ("fwd", 512, 1024, 3, L.PRO_NONE),
+    "enc_k3_fwd": ("fwd", 512, 512, 3, L.PRO_LRELU),
+    "enc_sk_fwd": ("fwd", 512, 512, 1, L.PRO_NONE),
+    "dec_rs_fwd": ("fwd", 512, 640, 1, L.PRO_NONE),
+    "dec_in_dgrad": ("dgrad", 512, 1024, 3, L.PRO_NONE),
+    "enc_k3_dgrad": ("dgrad", 512, 512, 3, L.PRO_NONE),
+    "dec_in_wgrad": ("wgrad", 512, 1024, 3, L.PRO_NONE),
+    "enc_k3_wgrad": ("wgrad", 512, 512, 3, L.PRO_LRELU),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--only", default=None)
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--splits", type=int, default=8)
+    a = ap.parse_args()
+    dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    B, T = 64, 256
+    N = B * T
+    dev = "cuda"
+    for name, (mode, cin, cout, k, pro) in SHAPES.items():
+        if a.only and a.only not in name:
+            continue
+        x = torch.randn(N, cin, device=dev).to(dt)
+        dy = torch.randn(N, cout, device=dev).to(dt)
+        w = (torch.randn(cout, k * cin, device=dev) / (k * cin) ** 0.5).to(dt)
+        y = torch.empty(N, cout, device=dev, dtype=dt)
+        dx = torch.empty(N, cin, device=dev, dtype=dt)
+        slabs = torch.empty(a.splits, cout, k * cin, device=dev)
+        bias = torch.zeros(cout, device=dev)
+        if mode == "fwd":
+            fn = lambda: ops.conv_fwd(x, w, y, T=T, cin=cin, cout=cout, ntaps=k, pad=(k - 1) // 2, prologue=pro,  # noqa
+                                      bias=bias)
+        elif mode == "dgrad":
+            fn = lambda: ops.conv_dgrad(dy, w, dx, T=T, cin=cout, cout=cin, ntaps=k, pad=(k - 1) // 2)  # noqa
+        else:
+            fn = lambda: ops.conv_wgrad(dy, x, slabs, T=T, r_dim=cout, c_dim=cin, ntaps=k, pad=(k - 1) // 2,  # noqa
+                                        q_prologue=pro, splits=a.splits)
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / a.iters
+        flops = 2.0 * N * cin * cout * k
+        print(f"{name:14s} {us:8.1f} us  {flops / us / 1e6:8.1f} TFLOP/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

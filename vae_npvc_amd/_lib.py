@@ -19,7 +19,7 @@ ABI_VERSION = 100
 
 VQX_F32, VQX_BF16 = 0, 1
 PRO_NONE, PRO_LRELU, PRO_RELU, PRO_SCALE_RELU = 0, 1, 2, 3
-EPI_BIAS, EPI_ROWBIAS, EPI_MASK, EPI_RES, EPI_GNADD, EPI_SPLIT, EPI_OUTF32 = (1 << i for i in range(7))
+EPI_BIAS, EPI_ROWBIAS, EPI_MASK, EPI_RES, EPI_GNADD, EPI_SPLIT, EPI_OUTF32, EPI_ACT, EPI_ACT2 = (1 << i for i in range(9))
 
 c_void_p, c_int32, c_int64, c_float, c_double = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
                                                  ctypes.c_float, ctypes.c_double)
@@ -35,6 +35,7 @@ class ConvArgs(ctypes.Structure):
         ("ldgn", c_int32), ("ldo2", c_int32), ("dtype", c_int32), ("prologue", c_int32),
         ("epilogue", c_int32), ("split_col", c_int32), ("out2_accumulate", c_int32),
         ("pro_scale", c_float), ("mask_slope", c_float), ("mask_scale", c_float),
+        ("y2", c_void_p), ("ldy2", c_int32), ("epi_act", c_int32),
     ]
 
 
@@ -87,6 +88,8 @@ _SIGS = {
     "vqx_linear_bwd_f32": [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p],
     "vqx_grad_sq_norm": [c_void_p, c_int64, c_void_p, c_void_p, c_void_p],
     "vqx_adam_hyper": [c_void_p, c_double, c_double, c_int32, c_double, c_double, c_double, c_void_p, c_void_p],
+    "vqx_scale_act_2d": [c_void_p, c_int32, c_int32, c_void_p, c_int32, c_int32, c_int64, c_int32, c_float, c_int32,
+                         c_void_p],
     "vqx_convert_2d": [c_void_p, c_int32, c_int32, c_void_p, c_int32, c_int32, c_int64, c_int32, c_void_p],
     "vqx_adam_step": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_float, c_void_p],
 }

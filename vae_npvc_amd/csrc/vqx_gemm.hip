@@ -218,23 +218,49 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
     }
   }
 
-  uint4 ra[4], rb[4];
+  uint4 ra0[4], rb0[4], ra1[4], rb1[4];
 
-  auto load_tile = [&](int kt) {
+  // One buffer descriptor per operand for the whole kernel.  Its base sits
+  // `lo` bytes before the operand (the largest negative im2col shift), so
+  // every in-range offset is non-negative; per K-tile only a scalar byte
+  // shift `ks` is added to each lane's offset (an out-of-range sentinel stays
+  // out of range).
+  int64_t a_lo = 0, b_lo = 0;
+  if constexpr (MODE != MODE_WGRAD) a_lo = (int64_t)P.pad * P.lda * ES;
+  if constexpr (MODE == MODE_WGRAD) b_lo = (int64_t)(P.ntaps - 1) * P.ldb * ES;
+  const __amdgpu_buffer_rsrc_t rsA = rsrc_at(P.a, -a_lo, P.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsB = rsrc_at(P.b, -b_lo, P.b_bytes);
+  if constexpr (MODE != MODE_WGRAD) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) aoff[i] += (unsigned)a_lo;  // rebase to the descriptor
+  }  // WGRAD: boff already carries the (ntaps-1)-row margin b_lo
+  // incremental (tap, channel) position of the next K-tile to load (FWD/DGRAD fast path)
+  int ld_tap = 0, ld_c0 = 0;
+
+  auto load_tile = [&](int kt, uint4 (&ra)[4], uint4 (&rb)[4]) {
     const int64_t k0 = kbeg + (int64_t)kt * BK;
     if constexpr (MODE != MODE_WGRAD) {
       if constexpr (!GEN) {
-        const int tap = (int)k0 / P.kcin;
-        const int ci0 = (int)k0 - tap * P.kcin;
-        const __amdgpu_buffer_rsrc_t ra_r =
-            rsrc_at(P.a, ((int64_t)(tap - P.pad) * P.lda + ci0) * ES, P.a_bytes);
+        const int tap = ld_tap, c0 = ld_c0;  // k0 == tap*kcin + c0
+        ld_c0 += BK;
+        if (ld_c0 >= P.kcin) { ld_c0 = 0; ld_tap += 1; }
+        const unsigned ksa = (unsigned)(((tap - P.pad) * P.lda + c0) * ES);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const unsigned off = ((amask[i] >> tap) & 1) ? aoff[i] : kOOB;
-          ra[i] = pro_chunk<T, PRO>(bload(ra_r, off), P.pro_scale);
+          const unsigned off = ((amask[i] >> tap) & 1) ? aoff[i] + ksa : kOOB;
+          ra[i] = bload(rsA, off);
+        }
+        if constexpr (MODE == MODE_FWD) {
+          const unsigned ksb = (unsigned)(k0 * ES);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) rb[i] = bload(rsB, boff[i] + ksb);
+        } else {
+          // forward weight We[co][j][ci] read as rows k = (j, co), taps flipped
+          const unsigned ksb = (unsigned)(((int64_t)c0 * P.ntaps * P.cdim + (int64_t)(P.ntaps - 1 - tap) * P.cdim) * ES);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) rb[i] = bload(rsB, boff[i] + ksb);
         }
       } else {
-        const __amdgpu_buffer_rsrc_t ra_r = rsrc_at(P.a, 0, P.a_bytes);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int c = tid + kThreads * i;
@@ -242,31 +268,16 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
           const int tap = tap_of(k, P.kcin);
           const int ci = k - tap * P.kcin;
           const bool ok = k < P.K && ((amask[i] >> tap) & 1);
-          const unsigned off = ok ? aoff[i] + (unsigned)((((tap - P.pad) * P.lda) + ci) * ES) : kOOB;
-          ra[i] = pro_chunk<T, PRO>(bload(ra_r, off), P.pro_scale);
+          ra[i] = bload(rsA, ok ? aoff[i] + (unsigned)((((tap - P.pad) * P.lda) + ci) * ES) : kOOB);
         }
-      }
-      if constexpr (MODE == MODE_FWD) {
-        const __amdgpu_buffer_rsrc_t rb_r = rsrc_at(P.b, k0 * ES, P.b_bytes);
+        if constexpr (MODE == MODE_FWD) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          unsigned off = boff[i];
-          if constexpr (GEN) {
+          for (int i = 0; i < 4; ++i) {
             const int c = tid + kThreads * i;
-            if ((int)k0 + (c & 7) * EPC >= P.K) off = kOOB;
+            const bool ok = (int)k0 + (c & 7) * EPC < P.K;
+            rb[i] = bload(rsB, ok ? boff[i] + (unsigned)(k0 * ES) : kOOB);
           }
-          rb[i] = bload(rb_r, off);
-        }
-      } else {
-        if constexpr (!GEN) {
-          const int j = (int)k0 / P.kcin;
-          const int co0 = (int)k0 - j * P.kcin;
-          const __amdgpu_buffer_rsrc_t rb_r =
-              rsrc_at(P.b, ((int64_t)co0 * P.ntaps * P.cdim + (int64_t)(P.ntaps - 1 - j) * P.cdim) * ES, P.b_bytes);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) rb[i] = bload(rb_r, boff[i]);
         } else {
-          const __amdgpu_buffer_rsrc_t rb_r = rsrc_at(P.b, 0, P.b_bytes);
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int c = tid + kThreads * i;
@@ -276,23 +287,23 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
             const int co = k - j * P.kcin;
             const int ci = n0 + cch * EPC;
             const bool ok = k < P.K && ci < P.Nc;
-            rb[i] = bload(rb_r, ok ? (unsigned)(((int64_t)co * P.ntaps * P.cdim + (P.ntaps - 1 - j) * P.cdim + ci) * ES)
-                                   : kOOB);
+            rb[i] = bload(rsB, ok ? (unsigned)(((int64_t)co * P.ntaps * P.cdim + (P.ntaps - 1 - j) * P.cdim + ci) * ES)
+                                  : kOOB);
           }
         }
       }
     } else {
-      const __amdgpu_buffer_rsrc_t ra_r = rsrc_at(P.a, k0 * P.lda * ES, P.a_bytes);
-      const __amdgpu_buffer_rsrc_t rb_r = rsrc_at(P.b, (k0 - (P.ntaps - 1)) * P.ldb * ES, P.b_bytes);
+      const unsigned ksa = (unsigned)(k0 * P.lda * ES);
+      const unsigned ksb = (unsigned)(k0 * P.ldb * ES);
       const int t0 = (int)((int)k0 % P.T);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        unsigned offa = aoff[i];
+        unsigned offa = aoff[i] + ksa;
         if constexpr (GEN) {
           const int c = tid + kThreads * i;
           if (k0 + c / CPR >= kend) offa = kOOB;
         }
-        ra[i] = bload(ra_r, offa);
+        ra[i] = bload(rsA, offa);
         int tt;
         if constexpr (!GEN) {
           tt = t0 + bsh[i];
@@ -302,22 +313,29 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
           tt = (int)(n % P.T) + (bsh[i] - c / CPR);
           if (n >= kend) tt = -1;
         }
-        const unsigned offb = (tt >= 0 && tt < P.T) ? boff[i] : kOOB;
-        rb[i] = pro_chunk<T, PRO>(bload(rb_r, offb), P.pro_scale);
+        rb[i] = bload(rsB, (tt >= 0 && tt < P.T) ? boff[i] + ksb : kOOB);
       }
     }
   };
 
-  auto store_tile = [&](int buf) {
+  // prologue (activation) is applied here, after the load has landed, so the
+  // loads of a tile stay in flight across the previous tile's MFMAs
+  auto store_tile = [&](int buf, const uint4 (&ra)[4], const uint4 (&rb)[4]) {
     char* la = smem + buf * 2 * TILE_BYTES;
     char* lb = la + TILE_BYTES;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int c = tid + kThreads * i;
-      if constexpr (MODE != MODE_WGRAD) *(uint4*)(la + kmaj_off(c >> 3, c & 7)) = ra[i];
-      else *(uint4*)(la + mnmaj_off<T>(c / CPR, c % CPR)) = ra[i];
-      if constexpr (MODE == MODE_FWD) *(uint4*)(lb + kmaj_off(c >> 3, c & 7)) = rb[i];
-      else *(uint4*)(lb + mnmaj_off<T>(c / CPR, c % CPR)) = rb[i];
+      if constexpr (MODE != MODE_WGRAD)
+        *(uint4*)(la + kmaj_off(c >> 3, c & 7)) = pro_chunk<T, PRO>(ra[i], P.pro_scale);
+      else
+        *(uint4*)(la + mnmaj_off<T>(c / CPR, c % CPR)) = ra[i];
+      if constexpr (MODE == MODE_FWD)
+        *(uint4*)(lb + kmaj_off(c >> 3, c & 7)) = rb[i];
+      else if constexpr (MODE == MODE_DGRAD)
+        *(uint4*)(lb + mnmaj_off<T>(c / CPR, c % CPR)) = rb[i];
+      else
+        *(uint4*)(lb + mnmaj_off<T>(c / CPR, c % CPR)) = pro_chunk<T, PRO>(rb[i], P.pro_scale);
     }
   };
 
@@ -400,17 +418,25 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
     }
   };
 
+  // Two register sets give every tile's loads two compute phases to land:
+  // tile t is issued during tile t-2's MFMAs and written to LDS after t-1's.
   if (nk > 0) {
-    load_tile(0);
-    store_tile(0);
+    load_tile(0, ra0, rb0);
+    store_tile(0, ra0, rb0);
+    if (nk > 1) load_tile(1, ra1, rb1);
     __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      const bool more = (kt + 1) < nk;
-      if (more) load_tile(kt + 1);
-      compute_tile(kt & 1);
-      if (more) store_tile((kt + 1) & 1);
+    int kt = 0;
+    for (; kt + 2 <= nk; kt += 2) {  // no early exit: keeps acc in place across the halves
+      if (kt + 2 < nk) load_tile(kt + 2, ra0, rb0);
+      compute_tile(0);
+      store_tile(1, ra1, rb1);
+      __syncthreads();
+      if (kt + 3 < nk) load_tile(kt + 3, ra1, rb1);
+      compute_tile(1);
+      if (kt + 2 < nk) store_tile(0, ra0, rb0);
       __syncthreads();
     }
+    if (kt < nk) compute_tile(0);  // odd tail, already in buffer 0
   }
 
   // ---------------- epilogue

@@ -714,6 +714,20 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   }
 }
 
+__global__ __launch_bounds__(256) void scale_act_2d_kernel(const void* __restrict__ src, int lds, int sdt,
+                                                           void* __restrict__ dst, int ldd, int ddt, int64_t rows,
+                                                           int cols, float scale, int act) {
+  const int64_t total = rows * cols;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / cols;
+    const int c = (int)(e - r * cols);
+    float v = scale * ld_dt(src, r * lds + c, sdt);
+    if (act == VQX_PRO_RELU) v = v > 0.f ? v : 0.f;
+    else if (act == VQX_PRO_LRELU) v = v > 0.f ? v : 0.2f * v;
+    st_dt(dst, r * ldd + c, v, ddt);
+  }
+}
+
 __global__ __launch_bounds__(256) void convert_2d_kernel(const void* __restrict__ src, int lds, int sdt,
                                                          void* __restrict__ dst, int ldd, int ddt, int64_t rows,
                                                          int cols) {
@@ -969,4 +983,14 @@ extern "C" int vqx_convert_2d(const void* src, int32_t ld_src, int32_t src_dtype
   hipLaunchKernelGGL(convert_2d_kernel, dim3(grid_for(rows * cols, 256, 8192)), dim3(256), 0, (hipStream_t)stream,
                      src, ld_src, src_dtype, dst, ld_dst, dst_dtype, rows, cols);
   return launch_status("vqx_convert_2d");
+}
+
+extern "C" int vqx_scale_act_2d(const void* src, int32_t ld_src, int32_t src_dtype, void* dst, int32_t ld_dst,
+                                int32_t dst_dtype, int64_t rows, int32_t cols, float scale, int32_t act,
+                                vqx_stream_t stream) {
+  if (rows <= 0 || cols <= 0) return 0;
+  if (!dst || !src) { set_error("vqx_scale_act_2d: null pointer"); return -1; }
+  hipLaunchKernelGGL(scale_act_2d_kernel, dim3(grid_for(rows * cols, 256, 8192)), dim3(256), 0, (hipStream_t)stream,
+                     src, ld_src, src_dtype, dst, ld_dst, dst_dtype, rows, cols, scale, act);
+  return launch_status("vqx_scale_act_2d");
 }

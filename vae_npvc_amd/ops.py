@@ -31,7 +31,8 @@ def _check_cuda(*ts):
 
 def conv_args(x, w, y, *, T, cin, cout, ntaps, pad, prologue=L.PRO_NONE, pro_scale=1.0, bias=None,
               rowbias=None, res=None, mask=None, mask_slope=0.0, mask_scale=1.0, gn_h=None, gn_mr=None,
-              gn_gamma=None, gn_beta=None, out2=None, split_col=0, out2_accumulate=False, out_f32=False):
+              gn_gamma=None, gn_beta=None, out2=None, split_col=0, out2_accumulate=False, out_f32=False,
+              act=None, y2=None):
     epi = 0
     if bias is not None:
         epi |= L.EPI_BIAS
@@ -47,6 +48,10 @@ def conv_args(x, w, y, *, T, cin, cout, ntaps, pad, prologue=L.PRO_NONE, pro_sca
         epi |= L.EPI_SPLIT
     if out_f32:
         epi |= L.EPI_OUTF32
+    if act is not None and y2 is None:
+        epi |= L.EPI_ACT
+    if y2 is not None:
+        epi |= L.EPI_ACT2
     a = L.ConvArgs()
     a.x, a.w, a.y = ptr(x), ptr(w), ptr(y)
     a.bias, a.rowbias, a.res, a.mask = ptr(bias), ptr(rowbias), ptr(res), ptr(mask)
@@ -61,6 +66,8 @@ def conv_args(x, w, y, *, T, cin, cout, ntaps, pad, prologue=L.PRO_NONE, pro_sca
     a.prologue, a.epilogue = prologue, epi
     a.split_col, a.out2_accumulate = split_col, int(bool(out2_accumulate))
     a.pro_scale, a.mask_slope, a.mask_scale = pro_scale, mask_slope, mask_scale
+    a.y2, a.ldy2 = ptr(y2), (y2.stride(0) if y2 is not None else 0)
+    a.epi_act = act if act is not None else 0
     return a
 
 
@@ -293,3 +300,12 @@ def zero_(t):
     """Zero a contiguous f32/bf16 device tensor with the native fill."""
     flat = t.view(1, -1)
     return convert_2d(None, flat)
+
+
+def scale_act_2d(src, dst, scale, act, rows=None, cols=None):
+    """dst = act(scale * src) (strided, dtype-converting)."""
+    rows = dst.shape[0] if rows is None else rows
+    cols = dst.shape[1] if cols is None else cols
+    call("vqx_scale_act_2d", ptr(src), src.stride(0), dt_code(src.dtype), ptr(dst), dst.stride(0), dt_code(dst.dtype),
+         rows, cols, scale, act, stream_ptr())
+    return dst
