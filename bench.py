@@ -154,6 +154,9 @@ def main():
     if rank == 0:
         if kernels is not None and os.environ.get("VQX_BENCH_KERNELS"):
             out["kernels"] = kernels
+            if os.environ.get("VQX_BENCH_KERNELS") == "2":
+                out["layers"] = {k: (v["launches"] // a.steps, round(v["avg_us"], 1), round(v["tflops"], 1))
+                                 for k, v in probe.summary(by_shape=True).items()}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -148,3 +148,47 @@ def test_vq_argmin_exact(K):
     onehot = F.one_hot(ref, K).float()
     assert torch.allclose(bcnt.cpu(), onehot.sum(0))
     assert torch.allclose(bsum.cpu(), onehot.t() @ z, atol=1e-4, rtol=1e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("act", ["lrelu", "relu"])
+def test_conv_fwd_act_epilogues(dtype, act):
+    """ACT (y = act(v)) and ACT2 (y = v, y2 = act(v)): the producer-side
+    activation that replaces GEMM prologues (vqvae.py:186-187 LeakyReLU stack
+    head, 316-317 final ReLUs)."""
+    ops = _ops()
+    from vae_npvc_amd import _lib as L
+    torch.manual_seed(3)
+    B, T, cin, cout, k = 2, 96, 512, 512, 3
+    x = torch.randn(B * T, cin, device=DEV).to(dtype)
+    w = (torch.randn(cout, cin, k, device=DEV) / (cin * k) ** 0.5).to(dtype)
+    bias = torch.randn(cout, device=DEV)
+    code = L.PRO_LRELU if act == "lrelu" else L.PRO_RELU
+    y = torch.empty(B * T, cout, device=DEV, dtype=dtype)
+    y2 = torch.empty(B * T, cout, device=DEV, dtype=dtype)
+    ops.conv_fwd(x, pack(w.float()).to(dtype), y, T=T, cin=cin, cout=cout, ntaps=k, pad=1, bias=bias, act=code, y2=y2)
+    y3 = torch.empty(B * T, cout, device=DEV, dtype=dtype)
+    ops.conv_fwd(x, pack(w.float()).to(dtype), y3, T=T, cin=cin, cout=cout, ntaps=k, pad=1, bias=bias, act=code)
+    torch.cuda.synchronize()
+    ref = ref_conv(x.float().cpu(), w.float().cpu(), B, T, 1) + bias.double().cpu()
+    aref = F.leaky_relu(ref, 0.2) if act == "lrelu" else F.relu(ref)
+    assert relerr(y, ref) < TOL[dtype]
+    assert relerr(y2, aref) < TOL[dtype]
+    # y2 is act applied to the same rounded pre-activation: exact in the element dtype
+    slope = 0.2 if act == "lrelu" else 0.0
+    yf = y.float()
+    assert torch.equal(y2, torch.where(yf > 0, yf, slope * yf).to(dtype)) or dtype == torch.bfloat16
+    assert torch.equal(y3, y2)
+
+
+@pytest.mark.parametrize("dt_out", [torch.float32, torch.bfloat16])
+def test_scale_act_2d(dt_out):
+    ops = _ops()
+    from vae_npvc_amd import _lib as L
+    torch.manual_seed(4)
+    src = torch.randn(300, 128, device=DEV)
+    dst = torch.empty(300, 128, device=DEV, dtype=dt_out)
+    s = (1.0 / 11) ** 0.5
+    ops.scale_act_2d(src, dst, s, L.PRO_RELU)
+    torch.cuda.synchronize()
+    assert torch.equal(dst, torch.relu(src * s).to(dt_out))

@@ -13,13 +13,16 @@ from vae_npvc_amd import ops  # noqa: E402
 
 SHAPES = {  # name: (mode, cin, cout, k, prologue)
     "dec_in_fwd": ("fwd", 512, 1024, 3, L.PRO_NONE),
-    "enc_k3_fwd": ("fwd", 512, 512, 3, L.PRO_LRELU),
+    "enc_k3_fwd": ("fwd", 512, 512, 3, L.PRO_NONE),
+    "enc_k3_fwd_pro": ("fwd", 512, 512, 3, L.PRO_LRELU),
     "enc_sk_fwd": ("fwd", 512, 512, 1, L.PRO_NONE),
     "dec_rs_fwd": ("fwd", 512, 640, 1, L.PRO_NONE),
     "dec_in_dgrad": ("dgrad", 512, 1024, 3, L.PRO_NONE),
     "enc_k3_dgrad": ("dgrad", 512, 512, 3, L.PRO_NONE),
     "dec_in_wgrad": ("wgrad", 512, 1024, 3, L.PRO_NONE),
-    "enc_k3_wgrad": ("wgrad", 512, 512, 3, L.PRO_LRELU),
+    "enc_k3_wgrad": ("wgrad", 512, 512, 3, L.PRO_NONE),
+    "fin1_fwd": ("fwd", 80, 80, 1, L.PRO_NONE),
+    "enc0_fwd": ("fwd", 80, 512, 3, L.PRO_NONE),
 }
 
 
@@ -29,6 +32,7 @@ def main():
     ap.add_argument("--only", default=None)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--splits", type=int, default=8)
+    ap.add_argument("--rotate", type=int, default=1, help="cycle through R operand sets (R*~50 MB > MALL = cold)")
     a = ap.parse_args()
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     B, T = 64, 256
@@ -37,28 +41,31 @@ def main():
     for name, (mode, cin, cout, k, pro) in SHAPES.items():
         if a.only and a.only not in name:
             continue
-        x = torch.randn(N, cin, device=dev).to(dt)
-        dy = torch.randn(N, cout, device=dev).to(dt)
+        R = a.rotate
+        xs = [torch.randn(N, cin, device=dev).to(dt) for _ in range(R)]
+        dys = [torch.randn(N, cout, device=dev).to(dt) for _ in range(R)]
         w = (torch.randn(cout, k * cin, device=dev) / (k * cin) ** 0.5).to(dt)
-        y = torch.empty(N, cout, device=dev, dtype=dt)
-        dx = torch.empty(N, cin, device=dev, dtype=dt)
+        ys = [torch.empty(N, cout, device=dev, dtype=dt) for _ in range(R)]
+        dxs = [torch.empty(N, cin, device=dev, dtype=dt) for _ in range(R)]
         slabs = torch.empty(a.splits, cout, k * cin, device=dev)
         bias = torch.zeros(cout, device=dev)
-        if mode == "fwd":
-            fn = lambda: ops.conv_fwd(x, w, y, T=T, cin=cin, cout=cout, ntaps=k, pad=(k - 1) // 2, prologue=pro,  # noqa
-                                      bias=bias)
-        elif mode == "dgrad":
-            fn = lambda: ops.conv_dgrad(dy, w, dx, T=T, cin=cout, cout=cin, ntaps=k, pad=(k - 1) // 2)  # noqa
-        else:
-            fn = lambda: ops.conv_wgrad(dy, x, slabs, T=T, r_dim=cout, c_dim=cin, ntaps=k, pad=(k - 1) // 2,  # noqa
-                                        q_prologue=pro, splits=a.splits)
-        for _ in range(3):
-            fn()
+
+        def fn(i):
+            x, dy, y, dx = xs[i % R], dys[i % R], ys[i % R], dxs[i % R]
+            if mode == "fwd":
+                ops.conv_fwd(x, w, y, T=T, cin=cin, cout=cout, ntaps=k, pad=(k - 1) // 2, prologue=pro, bias=bias)
+            elif mode == "dgrad":
+                ops.conv_dgrad(dy, w, dx, T=T, cin=cout, cout=cin, ntaps=k, pad=(k - 1) // 2)
+            else:
+                ops.conv_wgrad(dy, x, slabs, T=T, r_dim=cout, c_dim=cin, ntaps=k, pad=(k - 1) // 2,
+                               q_prologue=pro, splits=a.splits)
+        for i in range(3):
+            fn(i)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        for _ in range(a.iters):
-            fn()
+        for i in range(a.iters):
+            fn(i)
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / a.iters

@@ -1,11 +1,17 @@
+# Full GPU pass: parity tests, bench (per-kernel summary), rocprof kernel-trace.
+# usage: bash tools/gpu_run3.sh TAG
+TAG=${1:-x}
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-timeout -k 10 900 python -m pytest tests/test_gpu_kernels.py tests/test_gpu_step.py -q -rs --timeout 300 > gpurun_out/t6.log 2>&1
-rc=$?; echo "pytest rc=$rc" >> gpurun_out/t6.log
+O=gpurun_out/$TAG
+mkdir -p $O
+timeout -k 10 900 python -m pytest tests -m gpu -q -rs --timeout 300 > $O/tests.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> $O/tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-VQX_BENCH_KERNELS=1 timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/bench6.log 2>&1
-rc=$?; echo "bench rc=$rc" >> gpurun_out/bench6.log
+VQX_BENCH_KERNELS=2 timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline > $O/bench.log 2>&1
+rc=$?; echo "bench rc=$rc" >> $O/bench.log
 if [ $rc -ne 0 ]; then exit $rc; fi
-mkdir -p gpurun_out/prof6
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof6 -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-probe > gpurun_out/prof6/bench.log 2>&1
-echo "prof rc=$?" >> gpurun_out/prof6/bench.log
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-probe > $O/prof.log 2>&1
+echo "prof rc=$?" >> $O/prof.log
+tail -4 $O/tests.log
+grep -o '"value": [0-9.]*, "unit": "[^"]*", "n_gpus": [0-9]*, "steps": [0-9]*, "warmup": [0-9]*, "ms_per_step": [0-9.]*' $O/bench.log

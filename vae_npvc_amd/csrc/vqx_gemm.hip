@@ -27,6 +27,7 @@
 // (channels for FWD/DGRAD, j*cd+c for WGRAD), so each lane ends up holding 4
 // consecutive output elements per register group: the epilogue does vector
 // loads/stores (8 B bf16, 16 B f32) for bias, residual, masks and results.
+#include <stdlib.h>
 #include "vqx_common.h"
 
 namespace vqx {
@@ -67,6 +68,8 @@ struct GemmParams {
   const float* gn_beta;
   float* out2;
   int ldo2, split_col, out2_acc;
+  void* y2;
+  int ldy2, epi_act;
 };
 
 template <typename T> struct Cfg;
@@ -126,39 +129,146 @@ __device__ __forceinline__ int mnmaj_off(int row, int ch) {
   else return row * 512 + 16 * ch;
 }
 
-// 4 consecutive elements (8 B bf16 / 16 B f32) at p+i
+// 8 consecutive elements (16 B bf16 / 32 B f32) at p+i
 template <typename T>
-__device__ __forceinline__ void ld4(const void* p, int64_t i, float* f) {
+__device__ __forceinline__ void ld8(const void* p, int64_t i, float* f) {
   if constexpr (sizeof(T) == 2) {
-    const uint2 u = *(const uint2*)((const bf16_t*)p + i);
-    f[0] = __uint_as_float(u.x << 16); f[1] = __uint_as_float(u.x & 0xffff0000u);
-    f[2] = __uint_as_float(u.y << 16); f[3] = __uint_as_float(u.y & 0xffff0000u);
+    const uint4 u = *(const uint4*)((const bf16_t*)p + i);
+    const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f[2 * k] = __uint_as_float(w[k] << 16);
+      f[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+    }
   } else {
-    const f32x4_t v = *(const f32x4_t*)((const float*)p + i);
-    f[0] = v[0]; f[1] = v[1]; f[2] = v[2]; f[3] = v[3];
+    const f32x4_t a = *(const f32x4_t*)((const float*)p + i);
+    const f32x4_t b = *(const f32x4_t*)((const float*)p + i + 4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { f[k] = a[k]; f[4 + k] = b[k]; }
   }
 }
 template <typename T>
-__device__ __forceinline__ void st4(void* p, int64_t i, const float* f) {
+__device__ __forceinline__ void st8(void* p, int64_t i, const float* f) {
   if constexpr (sizeof(T) == 2) {
-    uint2 u;
+    uint4 u;
     u.x = (unsigned)f2bf(f[0]) | ((unsigned)f2bf(f[1]) << 16);
     u.y = (unsigned)f2bf(f[2]) | ((unsigned)f2bf(f[3]) << 16);
-    *(uint2*)((bf16_t*)p + i) = u;
+    u.z = (unsigned)f2bf(f[4]) | ((unsigned)f2bf(f[5]) << 16);
+    u.w = (unsigned)f2bf(f[6]) | ((unsigned)f2bf(f[7]) << 16);
+    *(uint4*)((bf16_t*)p + i) = u;
   } else {
-    f32x4_t v = {f[0], f[1], f[2], f[3]};
-    *(f32x4_t*)((float*)p + i) = v;
+    const f32x4_t a = {f[0], f[1], f[2], f[3]}, b = {f[4], f[5], f[6], f[7]};
+    *(f32x4_t*)((float*)p + i) = a;
+    *(f32x4_t*)((float*)p + i + 4) = b;
   }
 }
 
-template <typename T, int MODE, int PRO, bool GEN>
+// FWD/DGRAD epilogue on 8 consecutive output channels of one frame, in the
+// order bias, row bias, activation-derivative mask, split to out2 (returns),
+// residual, GroupNorm-apply add, activation, store.
+template <typename T>
+__device__ __forceinline__ void epilogue8(const GemmParams& P, int64_t row, int col, float* v) {
+  const int epi = P.epi;
+  const int bidx = (epi & (VQX_EPI_ROWBIAS | VQX_EPI_GNADD)) ? (int)(row / P.T) : 0;
+  float t[8];
+  if (epi & VQX_EPI_BIAS) {
+    ld8<float>(P.bias, col, t);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += t[e];
+  }
+  if (epi & VQX_EPI_ROWBIAS) {
+    ld8<float>(P.rowbias, (int64_t)bidx * P.Nc + col, t);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += t[e];
+  }
+  if (epi & VQX_EPI_MASK) {
+    ld8<T>(P.mask, row * P.ldmask + col, t);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= (t[e] > 0.f ? 1.f : P.mask_slope) * P.mask_scale;
+  }
+  if ((epi & VQX_EPI_SPLIT) && col >= P.split_col) {  // split_col % 8 == 0
+    float* o2 = P.out2 + row * P.ldo2 + (col - P.split_col);
+    if (P.out2_acc) {
+      ld8<float>(o2, 0, t);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += t[e];
+    }
+    st8<float>(o2, 0, v);
+    return;
+  }
+  if (epi & VQX_EPI_RES) {
+    ld8<T>(P.res, row * P.ldres + col, t);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += t[e];
+  }
+  if (epi & VQX_EPI_GNADD) {
+    float ga[8], be[8];
+    ld8<T>(P.gn_h, row * P.ldgn + col, t);
+    ld8<float>(P.gn_gamma, col, ga);
+    ld8<float>(P.gn_beta, col, be);
+    const float mean = P.gn_mr[2 * bidx], rstd = P.gn_mr[2 * bidx + 1];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += (t[e] - mean) * rstd * ga[e] + be[e];
+  }
+  if (epi & (VQX_EPI_ACT | VQX_EPI_ACT2)) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) t[e] = apply_pro(v[e], P.epi_act, 1.f);
+    if (epi & VQX_EPI_ACT2) {
+      st8<T>(P.y2, row * P.ldy2 + col, t);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = t[e];
+    }
+  }
+  if (P.out_f32) st8<float>(P.y, row * P.ldy + col, v);
+  else st8<T>(P.y, row * P.ldy + col, v);
+}
+
+// Fragment-level prologue (LDS-DMA staging cannot transform data in flight).
+template <int PRO>
+__device__ __forceinline__ bf16x8_t pro_frag(bf16x8_t f, float s) {
+  if constexpr (PRO == VQX_PRO_NONE) {
+    return f;
+  } else {
+    uint4 u = __builtin_bit_cast(uint4, f);
+    u = pro_chunk<bf16_t, PRO>(u, s);
+    return __builtin_bit_cast(bf16x8_t, u);
+  }
+}
+template <int PRO>
+__device__ __forceinline__ f32x4_t pro_frag(f32x4_t f, float s) {
+  if constexpr (PRO == VQX_PRO_NONE) {
+    return f;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f[i] = apply_pro(f[i], PRO, s);
+    return f;
+  }
+}
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, unsigned off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (VQX_LDS(void)*)lds, 16, (int)off, 0, 0, 0);
+}
+
+// Staging layout (both paths).  A K-tile operand is 16 KiB = 16 pieces of
+// 1 KiB; wave w fills pieces 4w..4w+3, lane l the 16-B chunk c = piece*64+l
+// at LDS byte 16*c (lane-linear, as an LDS-DMA writes).  The XOR swizzle
+// that keeps the fragment reads conflict-free is applied to the SOURCE chunk:
+//   K-major  (128-B rows):  row = c>>3, data chunk = (c&7) ^ ((row>>1)&7)
+//   MN-major (256-B rows, bf16): row = c>>4, data chunk = (c&15) ^ mn_swz(row)
+//   MN-major (512-B rows, f32):  row = c>>5, data chunk = c&31
+// DMA = true: operands go global -> LDS by buffer_load ... lds (no VGPR
+// staging, no ds_write), one K-tile ahead, `vmcnt(0)` + barrier per tile.
+// DMA = false: global -> VGPR (two register sets) -> ds_write_b128.
+template <typename T, int MODE, int PRO, bool GEN, bool DMA>
 __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
   using C = Cfg<T>;
   constexpr int BK = C::BK, EPC = C::EPC, CPR = C::MNCPR, ES = sizeof(T);
   constexpr int TILE_BYTES = 16384;
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
   const int tiles_mn = P.tiles_m * P.tiles_n;
@@ -177,15 +287,16 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
   }
   const int nk = (kend > kbeg) ? (int)((kend - kbeg + BK - 1) / BK) : 0;
 
-  // ---------------- per-thread constant addressing (chunk i = tid + 256*i)
+  // ---------------- per-thread constant addressing (chunk c = (4*wid+i)*64 + lane)
   unsigned aoff[4], boff[4];
   int amask[4];  // FWD/DGRAD: bit j set <=> tap j keeps the frame inside its utterance
   int bsh[4];    // WGRAD: krow + shift of the q chunk
+  int ak[4], bk[4];  // k offset of the chunk inside the K-tile (elements / rows)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int c = tid + kThreads * i;
+    const int c = (4 * wid + i) * 64 + lane;
     if constexpr (MODE != MODE_WGRAD) {
-      const int row = c >> 3, kch = c & 7;
+      const int row = c >> 3, kch = (c & 7) ^ ((row >> 1) & 7);
       const int64_t n = (int64_t)m0 + row;
       const int t = (int)(n % P.T);
       int msk = 0;
@@ -193,19 +304,26 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
 #pragma unroll
         for (int j = 0; j < 3; ++j) msk |= ((t + j - P.pad >= 0) && (t + j - P.pad < P.T)) ? (1 << j) : 0;
       amask[i] = msk;
+      ak[i] = kch * EPC;
       aoff[i] = (unsigned)((n * P.lda + (GEN ? 0 : kch * EPC)) * ES);
       if constexpr (MODE == MODE_FWD) {
         const int co = n0 + row;
+        bk[i] = kch * EPC;
         boff[i] = co < P.Nc ? (unsigned)(((int64_t)co * P.K + kch * EPC) * ES) : kOOB;
       } else {
-        const int krow = c / CPR, cch = c % CPR;
+        const int krow = c / CPR;
+        const int cch = (sizeof(T) == 2) ? ((c % CPR) ^ mn_swz(krow)) : (c % CPR);
         const int ci = n0 + cch * EPC;
+        bk[i] = krow;
         boff[i] = ci < P.Nc ? (unsigned)(((int64_t)krow * P.ntaps * P.cdim + ci) * ES) : kOOB;
+        if constexpr (GEN) boff[i] = ci < P.Nc ? (unsigned)(ci * ES) : kOOB;
       }
       bsh[i] = 0;
     } else {
-      const int krow = c / CPR, cch = c % CPR;
+      const int krow = c / CPR;
+      const int cch = (sizeof(T) == 2) ? ((c % CPR) ^ mn_swz(krow)) : (c % CPR);
       const int r = m0 + cch * EPC;
+      ak[i] = bk[i] = krow;
       aoff[i] = r < P.Mc ? (unsigned)(((int64_t)krow * P.lda + r) * ES) : kOOB;
       const int col = n0 + cch * EPC;
       const int j = tap_of(col, P.cdim);
@@ -218,13 +336,11 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
     }
   }
 
-  uint4 ra0[4], rb0[4], ra1[4], rb1[4];
-
   // One buffer descriptor per operand for the whole kernel.  Its base sits
   // `lo` bytes before the operand (the largest negative im2col shift), so
   // every in-range offset is non-negative; per K-tile only a scalar byte
-  // shift `ks` is added to each lane's offset (an out-of-range sentinel stays
-  // out of range).
+  // shift is added to each lane's offset (an out-of-range sentinel stays out
+  // of range).
   int64_t a_lo = 0, b_lo = 0;
   if constexpr (MODE != MODE_WGRAD) a_lo = (int64_t)P.pad * P.lda * ES;
   if constexpr (MODE == MODE_WGRAD) b_lo = (int64_t)(P.ntaps - 1) * P.ldb * ES;
@@ -237,7 +353,8 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
   // incremental (tap, channel) position of the next K-tile to load (FWD/DGRAD fast path)
   int ld_tap = 0, ld_c0 = 0;
 
-  auto load_tile = [&](int kt, uint4 (&ra)[4], uint4 (&rb)[4]) {
+  // Byte offsets of K-tile kt's chunks (kOOB where the im2col / edge reads zero).
+  auto tile_offsets = [&](int kt, unsigned (&oa)[4], unsigned (&ob)[4]) {
     const int64_t k0 = kbeg + (int64_t)kt * BK;
     if constexpr (MODE != MODE_WGRAD) {
       if constexpr (!GEN) {
@@ -246,49 +363,34 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
         if (ld_c0 >= P.kcin) { ld_c0 = 0; ld_tap += 1; }
         const unsigned ksa = (unsigned)(((tap - P.pad) * P.lda + c0) * ES);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const unsigned off = ((amask[i] >> tap) & 1) ? aoff[i] + ksa : kOOB;
-          ra[i] = bload(rsA, off);
-        }
-        if constexpr (MODE == MODE_FWD) {
-          const unsigned ksb = (unsigned)(k0 * ES);
+        for (int i = 0; i < 4; ++i) oa[i] = ((amask[i] >> tap) & 1) ? aoff[i] + ksa : kOOB;
+        unsigned ksb;
+        if constexpr (MODE == MODE_FWD) ksb = (unsigned)(k0 * ES);
+        else  // forward weight We[co][j][ci] read as rows k = (j, co), taps flipped
+          ksb = (unsigned)(((int64_t)c0 * P.ntaps * P.cdim + (int64_t)(P.ntaps - 1 - tap) * P.cdim) * ES);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) rb[i] = bload(rsB, boff[i] + ksb);
-        } else {
-          // forward weight We[co][j][ci] read as rows k = (j, co), taps flipped
-          const unsigned ksb = (unsigned)(((int64_t)c0 * P.ntaps * P.cdim + (int64_t)(P.ntaps - 1 - tap) * P.cdim) * ES);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) rb[i] = bload(rsB, boff[i] + ksb);
-        }
+        for (int i = 0; i < 4; ++i) ob[i] = boff[i] + ksb;
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int c = tid + kThreads * i;
-          const int k = (int)k0 + (c & 7) * EPC;
+          const int k = (int)k0 + ak[i];
           const int tap = tap_of(k, P.kcin);
           const int ci = k - tap * P.kcin;
           const bool ok = k < P.K && ((amask[i] >> tap) & 1);
-          ra[i] = bload(rsA, ok ? aoff[i] + (unsigned)((((tap - P.pad) * P.lda) + ci) * ES) : kOOB);
+          oa[i] = ok ? aoff[i] + (unsigned)((((tap - P.pad) * P.lda) + ci) * ES) : kOOB;
         }
         if constexpr (MODE == MODE_FWD) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int c = tid + kThreads * i;
-            const bool ok = (int)k0 + (c & 7) * EPC < P.K;
-            rb[i] = bload(rsB, ok ? boff[i] + (unsigned)(k0 * ES) : kOOB);
-          }
+          for (int i = 0; i < 4; ++i) ob[i] = ((int)k0 + bk[i] < P.K) ? boff[i] + (unsigned)(k0 * ES) : kOOB;
         } else {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const int c = tid + kThreads * i;
-            const int krow = c / CPR, cch = c % CPR;
-            const int k = (int)k0 + krow;
+            const int k = (int)k0 + bk[i];
             const int j = tap_of(k, P.kcin);
             const int co = k - j * P.kcin;
-            const int ci = n0 + cch * EPC;
-            const bool ok = k < P.K && ci < P.Nc;
-            rb[i] = bload(rsB, ok ? (unsigned)(((int64_t)co * P.ntaps * P.cdim + (P.ntaps - 1 - j) * P.cdim + ci) * ES)
-                                  : kOOB);
+            ob[i] = (k < P.K && boff[i] != kOOB)
+                        ? boff[i] + (unsigned)(((int64_t)co * P.ntaps * P.cdim + (P.ntaps - 1 - j) * P.cdim) * ES)
+                        : kOOB;
           }
         }
       }
@@ -299,45 +401,55 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         unsigned offa = aoff[i] + ksa;
-        if constexpr (GEN) {
-          const int c = tid + kThreads * i;
-          if (k0 + c / CPR >= kend) offa = kOOB;
-        }
-        ra[i] = bload(rsA, offa);
         int tt;
         if constexpr (!GEN) {
           tt = t0 + bsh[i];
         } else {
-          const int c = tid + kThreads * i;
-          const int64_t n = k0 + c / CPR;
-          tt = (int)(n % P.T) + (bsh[i] - c / CPR);
+          const int64_t n = k0 + ak[i];
+          if (n >= kend) offa = kOOB;
+          tt = (int)(n % P.T) + (bsh[i] - ak[i]);
           if (n >= kend) tt = -1;
         }
-        rb[i] = bload(rsB, (tt >= 0 && tt < P.T) ? boff[i] + ksb : kOOB);
+        oa[i] = offa;
+        ob[i] = (tt >= 0 && tt < P.T) ? boff[i] + ksb : kOOB;
       }
     }
   };
 
-  // prologue (activation) is applied here, after the load has landed, so the
-  // loads of a tile stay in flight across the previous tile's MFMAs
+  auto dma_tile = [&](int buf, int kt) {
+    unsigned oa[4], ob[4];
+    tile_offsets(kt, oa, ob);
+    char* la = smem + buf * 2 * TILE_BYTES + wid * 4096;
+    char* lb = la + TILE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dma16(rsA, la + i * 1024, oa[i]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dma16(rsB, lb + i * 1024, ob[i]);
+  };
+
+  auto load_tile = [&](int kt, uint4 (&ra)[4], uint4 (&rb)[4]) {
+    unsigned oa[4], ob[4];
+    tile_offsets(kt, oa, ob);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ra[i] = bload(rsA, oa[i]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rb[i] = bload(rsB, ob[i]);
+  };
+
+  // register path: prologue applied at the store, after the load has landed
   auto store_tile = [&](int buf, const uint4 (&ra)[4], const uint4 (&rb)[4]) {
-    char* la = smem + buf * 2 * TILE_BYTES;
+    char* la = smem + buf * 2 * TILE_BYTES + wid * 4096 + lane * 16;
     char* lb = la + TILE_BYTES;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int c = tid + kThreads * i;
-      if constexpr (MODE != MODE_WGRAD)
-        *(uint4*)(la + kmaj_off(c >> 3, c & 7)) = pro_chunk<T, PRO>(ra[i], P.pro_scale);
-      else
-        *(uint4*)(la + mnmaj_off<T>(c / CPR, c % CPR)) = ra[i];
-      if constexpr (MODE == MODE_FWD)
-        *(uint4*)(lb + kmaj_off(c >> 3, c & 7)) = rb[i];
-      else if constexpr (MODE == MODE_DGRAD)
-        *(uint4*)(lb + mnmaj_off<T>(c / CPR, c % CPR)) = rb[i];
-      else
-        *(uint4*)(lb + mnmaj_off<T>(c / CPR, c % CPR)) = pro_chunk<T, PRO>(rb[i], P.pro_scale);
+      *(uint4*)(la + i * 1024) = (MODE != MODE_WGRAD) ? pro_chunk<T, PRO>(ra[i], P.pro_scale) : ra[i];
+      *(uint4*)(lb + i * 1024) = (MODE == MODE_WGRAD) ? pro_chunk<T, PRO>(rb[i], P.pro_scale) : rb[i];
     }
   };
+
+  // DMA path: the prologue is applied to fragments after ds_read
+  constexpr int FPRO_A = (DMA && MODE != MODE_WGRAD) ? PRO : VQX_PRO_NONE;
+  constexpr int FPRO_B = (DMA && MODE == MODE_WGRAD) ? PRO : VQX_PRO_NONE;
 
   // acc[mi][ni]: mi = 32-block of the "row" operand (A tile), ni = of the B tile.
   // MFMA D = first(32 x k) * second(k x 32): first = B-tile fragment (contiguous
@@ -379,6 +491,8 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
           else af[x] = tr_frag(la, wm * 64 + x * 32 + (g & 1) * 16, s);
           if constexpr (B_KMAJ) bfr[x] = *(const bf16x8_t*)(lb + kmaj_off(wn * 64 + x * 32 + r32, 2 * s + h));
           else bfr[x] = tr_frag(lb, wn * 64 + x * 32 + (g & 1) * 16, s);
+          af[x] = pro_frag<FPRO_A>(af[x], P.pro_scale);
+          bfr[x] = pro_frag<FPRO_B>(bfr[x], P.pro_scale);
         }
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi)
@@ -406,6 +520,8 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
 #pragma unroll
             for (int qq = 0; qq < 4; ++qq) bfr[x][qq] = *(const float*)(lb + (8 * s + 4 * h + qq) * 512 + col * 4);
           }
+          af[x] = pro_frag<FPRO_A>(af[x], P.pro_scale);
+          bfr[x] = pro_frag<FPRO_B>(bfr[x], P.pro_scale);
         }
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq)
@@ -418,120 +534,121 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
     }
   };
 
-  // Two register sets give every tile's loads two compute phases to land:
-  // tile t is issued during tile t-2's MFMAs and written to LDS after t-1's.
-  if (nk > 0) {
-    load_tile(0, ra0, rb0);
-    store_tile(0, ra0, rb0);
-    if (nk > 1) load_tile(1, ra1, rb1);
-    __syncthreads();
-    int kt = 0;
-    for (; kt + 2 <= nk; kt += 2) {  // no early exit: keeps acc in place across the halves
-      if (kt + 2 < nk) load_tile(kt + 2, ra0, rb0);
-      compute_tile(0);
-      store_tile(1, ra1, rb1);
+  if constexpr (DMA) {
+    // Tile kt+1 streams into the other buffer while tile kt is multiplied;
+    // __syncthreads() waits vmcnt(0) (the DMA is a pending LDS write) and
+    // orders every wave's reads of buffer kt&1 before its next refill.
+    if (nk > 0) {
+      dma_tile(0, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (kt + 3 < nk) load_tile(kt + 3, ra1, rb1);
-      compute_tile(1);
-      if (kt + 2 < nk) store_tile(0, ra0, rb0);
-      __syncthreads();
+      for (int kt = 0; kt < nk; ++kt) {
+        if (kt + 1 < nk) dma_tile((kt + 1) & 1, kt + 1);
+        compute_tile(kt & 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
     }
-    if (kt < nk) compute_tile(0);  // odd tail, already in buffer 0
+  } else {
+    uint4 ra0[4], rb0[4], ra1[4], rb1[4];
+    // Two register sets give every tile's loads two compute phases to land:
+    // tile t is issued during tile t-2's MFMAs and written to LDS after t-1's.
+    if (nk > 0) {
+      load_tile(0, ra0, rb0);
+      store_tile(0, ra0, rb0);
+      if (nk > 1) load_tile(1, ra1, rb1);
+      __syncthreads();
+      int kt = 0;
+      for (; kt + 2 <= nk; kt += 2) {  // no early exit: keeps acc in place across the halves
+        if (kt + 2 < nk) load_tile(kt + 2, ra0, rb0);
+        compute_tile(0);
+        store_tile(1, ra1, rb1);
+        __syncthreads();
+        if (kt + 3 < nk) load_tile(kt + 3, ra1, rb1);
+        compute_tile(1);
+        if (kt + 2 < nk) store_tile(0, ra0, rb0);
+        __syncthreads();
+      }
+      if (kt < nk) compute_tile(0);  // odd tail, already in buffer 0
+    }
   }
 
   // ---------------- epilogue
-  // lane holds output row (A-tile index) R = m0 + wm*64 + mi*32 + r32 and, per
-  // register group gq, output columns Cb = n0 + wn*64 + ni*32 + 8*gq + 4*h + (0..3).
-  if constexpr (MODE == MODE_WGRAD) {
-    float* out = (float*)P.y + (int64_t)split * P.Mc * P.Nc;
+  // The accumulator tile goes through LDS (one 64-row half at a time) so the
+  // epilogue reads and writes whole rows: 16 lanes x 8 consecutive columns
+  // per row, every global access 16 B and each row segment contiguous.
+  // Lane holds (before the transpose) output row wm*64 + mi*32 + r32 and,
+  // per register group gq, columns wn*64 + ni*32 + 8*gq + 4*h + (0..3).
+  constexpr int EP_LD = kBN + 4;  // floats; +4 keeps the b128 writes conflict-free
+  float* ep = (float*)smem;
+  const int er = tid >> 4, ec = (tid & 15) * 8;
+  __syncthreads();  // staging buffers are free
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi) {
-      const int row = m0 + wm * 64 + mi * 32 + r32;
-      if (row >= P.Mc) continue;
+  for (int half = 0; half < 2; ++half) {
+    if (wm == half) {
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
+      for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          const int col = n0 + wn * 64 + ni * 32 + 8 * gq + 4 * h;
-          if (col >= P.Nc) continue;  // Nc % 4 == 0
-          f32x4_t v = {acc[mi][ni][4 * gq], acc[mi][ni][4 * gq + 1], acc[mi][ni][4 * gq + 2], acc[mi][ni][4 * gq + 3]};
-          *(f32x4_t*)(out + (int64_t)row * P.Nc + col) = v;
-        }
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int gq = 0; gq < 4; ++gq) {
+            const f32x4_t v = {acc[mi][ni][4 * gq], acc[mi][ni][4 * gq + 1], acc[mi][ni][4 * gq + 2],
+                               acc[mi][ni][4 * gq + 3]};
+            *(f32x4_t*)(ep + (mi * 32 + r32) * EP_LD + wn * 64 + ni * 32 + 8 * gq + 4 * h) = v;
+          }
     }
-  } else {
-    const int epi = P.epi;
+    __syncthreads();
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi) {
-      const int64_t row = (int64_t)m0 + wm * 64 + mi * 32 + r32;
-      if (row >= P.n_rows) continue;
-      const int bidx = (epi & (VQX_EPI_ROWBIAS | VQX_EPI_GNADD)) ? (int)(row / P.T) : 0;
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          const int col = n0 + wn * 64 + ni * 32 + 8 * gq + 4 * h;
-          if (col >= P.Nc) continue;  // Nc % 4 == 0
-          float v[4] = {acc[mi][ni][4 * gq], acc[mi][ni][4 * gq + 1], acc[mi][ni][4 * gq + 2], acc[mi][ni][4 * gq + 3]};
-          if (epi & VQX_EPI_BIAS) {
-            const f32x4_t bb = *(const f32x4_t*)(P.bias + col);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += bb[e];
-          }
-          if (epi & VQX_EPI_ROWBIAS) {
-            const f32x4_t rb4 = *(const f32x4_t*)(P.rowbias + (int64_t)bidx * P.Nc + col);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += rb4[e];
-          }
-          if (epi & VQX_EPI_MASK) {
-            float mk[4];
-            ld4<T>(P.mask, row * P.ldmask + col, mk);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] *= (mk[e] > 0.f ? 1.f : P.mask_slope) * P.mask_scale;
-          }
-          if ((epi & VQX_EPI_SPLIT) && col >= P.split_col) {
-            float* o2 = P.out2 + row * P.ldo2 + (col - P.split_col);
-            f32x4_t cur = {0.f, 0.f, 0.f, 0.f};
-            if (P.out2_acc) cur = *(const f32x4_t*)o2;
-            f32x4_t nv = {cur[0] + v[0], cur[1] + v[1], cur[2] + v[2], cur[3] + v[3]};
-            *(f32x4_t*)o2 = nv;
-            continue;
-          }
-          if (epi & VQX_EPI_RES) {
-            float rr[4];
-            ld4<T>(P.res, row * P.ldres + col, rr);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += rr[e];
-          }
-          if (epi & VQX_EPI_GNADD) {
-            float hv[4];
-            ld4<T>(P.gn_h, row * P.ldgn + col, hv);
-            const float mean = P.gn_mr[2 * bidx], rstd = P.gn_mr[2 * bidx + 1];
-            const f32x4_t ga = *(const f32x4_t*)(P.gn_gamma + col);
-            const f32x4_t be = *(const f32x4_t*)(P.gn_beta + col);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += (hv[e] - mean) * rstd * ga[e] + be[e];
-          }
-          if (P.out_f32) st4<float>(P.y, row * P.ldy + col, v);
-          else st4<T>(P.y, row * P.ldy + col, v);
+    for (int pass = 0; pass < 4; ++pass) {
+      const int lr = pass * 16 + er;
+      const f32x4_t lo = *(const f32x4_t*)(ep + lr * EP_LD + ec);
+      const f32x4_t hi = *(const f32x4_t*)(ep + lr * EP_LD + ec + 4);
+      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const int64_t row = (int64_t)m0 + half * 64 + lr;
+      const int col = n0 + ec;
+      if constexpr (MODE == MODE_WGRAD) {
+        if (row < P.Mc && col < P.Nc) {  // Nc % 8 == 0
+          float* out = (float*)P.y + (int64_t)split * P.Mc * P.Nc + row * P.Nc + col;
+          st8<float>(out, 0, v);
         }
+      } else {
+        if (row < P.n_rows && col < P.Nc) epilogue8<T>(P, row, col, v);
+      }
     }
+    __syncthreads();
   }
 }
 
-template <typename T, int MODE, bool GEN>
+template <typename T, int MODE, bool GEN, bool DMA>
 static void launch_pro(const GemmParams& P, int grid, hipStream_t s) {
   switch (P.pro) {
-    case VQX_PRO_NONE: hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, VQX_PRO_NONE, GEN>), dim3(grid), dim3(kThreads), 0, s, P); break;
-    case VQX_PRO_LRELU: hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, VQX_PRO_LRELU, GEN>), dim3(grid), dim3(kThreads), 0, s, P); break;
-    case VQX_PRO_RELU: hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, VQX_PRO_RELU, GEN>), dim3(grid), dim3(kThreads), 0, s, P); break;
-    default: hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, VQX_PRO_SCALE_RELU, GEN>), dim3(grid), dim3(kThreads), 0, s, P); break;
+    case VQX_PRO_NONE: hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, VQX_PRO_NONE, GEN, DMA>), dim3(grid), dim3(kThreads), 0, s, P); break;
+    case VQX_PRO_LRELU: hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, VQX_PRO_LRELU, GEN, DMA>), dim3(grid), dim3(kThreads), 0, s, P); break;
+    case VQX_PRO_RELU: hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, VQX_PRO_RELU, GEN, DMA>), dim3(grid), dim3(kThreads), 0, s, P); break;
+    default: hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, VQX_PRO_SCALE_RELU, GEN, DMA>), dim3(grid), dim3(kThreads), 0, s, P); break;
   }
+}
+
+// Staging variant: LDS-DMA by default; VQX_GEMM_STAGING=reg selects the
+// register-staged pipeline (kept for A/B measurement).
+static bool use_dma() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("VQX_GEMM_STAGING");
+    v = (e && e[0] == 'r') ? 0 : 1;
+  }
+  return v == 1;
 }
 
 template <typename T, int MODE>
 static void launch_mode(const GemmParams& P, int grid, bool gen, hipStream_t s) {
-  if (gen) launch_pro<T, MODE, true>(P, grid, s);
-  else launch_pro<T, MODE, false>(P, grid, s);
+  if (use_dma()) {
+    if (gen) launch_pro<T, MODE, true, true>(P, grid, s);
+    else launch_pro<T, MODE, false, true>(P, grid, s);
+  } else {
+    if (gen) launch_pro<T, MODE, true, false>(P, grid, s);
+    else launch_pro<T, MODE, false, false>(P, grid, s);
+  }
 }
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -545,18 +662,20 @@ static int conv_common(const vqx_conv_args* a, int mode, hipStream_t s) {
   if (a->ntaps < 1 || a->ntaps > 3 || a->pad < 0 || a->pad >= a->ntaps + 1) { set_error("vqx_conv: ntaps %d / pad %d", a->ntaps, a->pad); return -1; }
   if (a->n_rows <= 0 || a->T <= 0 || a->n_rows % a->T) { set_error("vqx_conv: n_rows %lld not a multiple of T %d", (long long)a->n_rows, a->T); return -1; }
   if (a->cin <= 0 || a->cout <= 0 || a->cin % epc || a->ldx % epc || a->cin > a->ldx) { set_error("vqx_conv: cin %d / ldx %d must be multiples of %d", a->cin, a->ldx, epc); return -1; }
-  if (a->cout % 4 || a->ldy % 4) { set_error("vqx_conv: cout %d / ldy %d must be multiples of 4", a->cout, a->ldy); return -1; }
+  if (a->cout % 8 || a->ldy % 8) { set_error("vqx_conv: cout %d / ldy %d must be multiples of 8", a->cout, a->ldy); return -1; }
   if (mode == MODE_DGRAD && a->cout % epc) { set_error("vqx_conv_dgrad: cout %d must be a multiple of %d", a->cout, epc); return -1; }
   if (!aligned16(a->x) || !aligned16(a->w)) { set_error("vqx_conv: x/w must be 16-byte aligned"); return -1; }
   if (a->prologue < 0 || a->prologue > 3 || (mode == MODE_DGRAD && a->prologue)) { set_error("vqx_conv: bad prologue %d", a->prologue); return -1; }
   const int epi = a->epilogue;
   if ((epi & VQX_EPI_BIAS) && (!a->bias || !aligned16(a->bias))) { set_error("vqx_conv: BIAS needs a 16-B aligned bias"); return -1; }
   if ((epi & VQX_EPI_ROWBIAS) && (!a->rowbias || !aligned16(a->rowbias))) { set_error("vqx_conv: ROWBIAS needs an aligned rowbias"); return -1; }
-  if ((epi & VQX_EPI_RES) && (!a->res || a->ldres % 4)) { set_error("vqx_conv: RES operand"); return -1; }
-  if ((epi & VQX_EPI_MASK) && (!a->mask || a->ldmask % 4)) { set_error("vqx_conv: MASK operand"); return -1; }
-  if ((epi & VQX_EPI_GNADD) && !(a->gn_h && a->gn_mean_rstd && a->gn_gamma && a->gn_beta && a->ldgn % 4 == 0)) { set_error("vqx_conv: GNADD operands"); return -1; }
-  if ((epi & VQX_EPI_SPLIT) && (!a->out2 || a->split_col % 4 || a->ldo2 % 4)) { set_error("vqx_conv: SPLIT operands"); return -1; }
-  if (!a->y) { set_error("vqx_conv: null y"); return -1; }
+  if ((epi & VQX_EPI_RES) && (!a->res || a->ldres % 8 || !aligned16(a->res))) { set_error("vqx_conv: RES operand"); return -1; }
+  if ((epi & VQX_EPI_MASK) && (!a->mask || a->ldmask % 8 || !aligned16(a->mask))) { set_error("vqx_conv: MASK operand"); return -1; }
+  if ((epi & VQX_EPI_GNADD) && !(a->gn_h && a->gn_mean_rstd && a->gn_gamma && a->gn_beta && a->ldgn % 8 == 0 && aligned16(a->gn_h) && aligned16(a->gn_gamma) && aligned16(a->gn_beta))) { set_error("vqx_conv: GNADD operands"); return -1; }
+  if ((epi & VQX_EPI_SPLIT) && (!a->out2 || a->split_col % 8 || a->ldo2 % 4 || !aligned16(a->out2))) { set_error("vqx_conv: SPLIT operands"); return -1; }
+  if ((epi & VQX_EPI_ACT2) && (!a->y2 || a->ldy2 % 8 || !aligned16(a->y2))) { set_error("vqx_conv: ACT2 needs a 16-B aligned y2 with ldy2 %% 8 == 0"); return -1; }
+  if ((epi & (VQX_EPI_ACT | VQX_EPI_ACT2)) && a->epi_act != VQX_PRO_LRELU && a->epi_act != VQX_PRO_RELU) { set_error("vqx_conv: epi_act must be LRELU or RELU"); return -1; }
+  if (!a->y || !aligned16(a->y)) { set_error("vqx_conv: y must be non-null and 16-byte aligned"); return -1; }
 
   GemmParams P = {};
   P.a = a->x; P.b = a->w;
@@ -573,6 +692,7 @@ static int conv_common(const vqx_conv_args* a, int mode, hipStream_t s) {
   P.mask = a->mask; P.ldmask = a->ldmask; P.mask_slope = a->mask_slope; P.mask_scale = a->mask_scale;
   P.gn_h = a->gn_h; P.ldgn = a->ldgn; P.gn_mr = a->gn_mean_rstd; P.gn_gamma = a->gn_gamma; P.gn_beta = a->gn_beta;
   P.out2 = a->out2; P.ldo2 = a->ldo2; P.split_col = a->split_col; P.out2_acc = a->out2_accumulate;
+  P.y2 = a->y2; P.ldy2 = a->ldy2; P.epi_act = a->epi_act;
   if (P.a_bytes > 0x7fffffffLL || P.b_bytes > 0x7fffffffLL) { set_error("vqx_conv: operand larger than 2 GiB"); return -1; }
   const bool gen = (a->cin % bk) != 0;
   const int grid = P.tiles_m * P.tiles_n;
@@ -604,7 +724,7 @@ extern "C" int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream) {
   const int BK = a->dtype == VQX_BF16 ? 64 : 32;
   if (a->ntaps < 1 || a->ntaps > 3) { set_error("vqx_conv1d_wgrad: ntaps %d", a->ntaps); return -1; }
   if (a->n_rows <= 0 || a->T <= 0 || a->n_rows % a->T) { set_error("vqx_conv1d_wgrad: bad n_rows/T"); return -1; }
-  if (a->r_dim % epc || a->c_dim % epc || a->ldp % epc || a->ldq % epc) { set_error("vqx_conv1d_wgrad: dims must be multiples of %d", epc); return -1; }
+  if (a->r_dim % epc || a->c_dim % epc || a->ldp % epc || a->ldq % epc || a->c_dim % 8) { set_error("vqx_conv1d_wgrad: dims must be multiples of %d (c_dim of 8)", epc); return -1; }
   if (a->splits < 1) { set_error("vqx_conv1d_wgrad: splits < 1"); return -1; }
   if (!aligned16(a->p) || !aligned16(a->q) || !a->slabs || !aligned16(a->slabs)) { set_error("vqx_conv1d_wgrad: bad pointers"); return -1; }
   if (a->shift_sign != 1 && a->shift_sign != -1) { set_error("vqx_conv1d_wgrad: shift_sign must be +-1"); return -1; }

@@ -52,39 +52,56 @@ __global__ __launch_bounds__(256) void wn_pack_kernel(const vqx_wn_layer* __rest
 
 // Backward per weight-norm row o.  slabs[s][o][x] with x = j*cin+ci (Conv1d,
 // row co) or x = j'*cout+co (ConvT, row ci); dW of the effective conv.
+// The split-K slabs are summed with 16-B loads (4 splits in flight per
+// thread), scattered into the row's (c, j) order in LDS, then the norm
+// gradient is formed from LDS with coalesced reads of v.
 __global__ __launch_bounds__(256) void wn_bwd_kernel(const vqx_wn_layer* __restrict__ L, int n_layers) {
   const vqx_wn_layer& l = L[blockIdx.y];
   const int rows = l.kind == 0 ? l.cout : l.cin;
   const int o = blockIdx.x;
   if (o >= rows) return;
-  const int other = l.kind == 0 ? l.cin : l.cout;
+  const int other = l.kind == 0 ? l.cin : l.cout;  // multiple of 4 (host-checked)
   const int K = l.k;
   const int cols = other * K;
-  __shared__ float dw[4096];
+  __shared__ __attribute__((aligned(16))) float dw[4096];
   __shared__ float red[16];
   const int64_t slab_stride = (int64_t)rows * cols;
-  const float* v = l.v + (int64_t)o * cols;
-  float dot = 0.f;
-  for (int x = threadIdx.x; x < cols; x += blockDim.x) {
-    float s = 0.f;
-    for (int sp = 0; sp < l.splits; ++sp) s += l.slabs[sp * slab_stride + (int64_t)o * cols + x];
+  const float* srow = l.slabs + (int64_t)o * cols;
+  const int splits = l.splits;
+  for (int x4 = threadIdx.x; x4 < cols / 4; x4 += blockDim.x) {
+    const float* p = srow + 4 * x4;
+    f32x4_t s0 = *(const f32x4_t*)p, s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1, s3 = s1;
+    int sp = 1;
+    for (; sp + 3 <= splits; sp += 3) {
+      s1 += *(const f32x4_t*)(p + (int64_t)sp * slab_stride);
+      s2 += *(const f32x4_t*)(p + (int64_t)(sp + 1) * slab_stride);
+      s3 += *(const f32x4_t*)(p + (int64_t)(sp + 2) * slab_stride);
+    }
+    for (; sp < splits; ++sp) s1 += *(const f32x4_t*)(p + (int64_t)sp * slab_stride);
+    const f32x4_t sum = (s0 + s1) + (s2 + s3);
     // slab col x = j*other + c  -> v index c*K + (kind==0 ? j : K-1-j)
+    const int x = 4 * x4;
     const int j = x / other, c = x - j * other;
-    const int vi = c * K + (l.kind == 0 ? j : K - 1 - j);
-    dw[vi] = s;
-    dot = fmaf(s, v[vi], dot);
+    const int jj = l.kind == 0 ? j : K - 1 - j;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dw[(c + e) * K + jj] = sum[e];
   }
-  dot = block_sum(dot, red);  // includes __syncthreads: dw[] complete
+  __syncthreads();
+  const float* v = l.v + (int64_t)o * cols;
+  float* dv = l.dv + (int64_t)o * cols;
   if (!l.g) {  // plain weight (weight norm removed): dv is the weight gradient itself
-    for (int i = threadIdx.x; i < cols; i += blockDim.x) l.dv[(int64_t)o * cols + i] = dw[i];
+    for (int i = threadIdx.x; i < cols; i += blockDim.x) dv[i] = dw[i];
     return;
   }
+  float dot = 0.f;
+  for (int i = threadIdx.x; i < cols; i += blockDim.x) dot = fmaf(dw[i], v[i], dot);
+  dot = block_sum(dot, red);
   const float nrm = l.norm[o];
   const float gg = l.g[o];
   const float dg = dot / nrm;
   if (threadIdx.x == 0) l.dg[o] = dg;
   const float sc = gg / nrm, t = dg / nrm;
-  for (int i = threadIdx.x; i < cols; i += blockDim.x) l.dv[(int64_t)o * cols + i] = sc * (dw[i] - v[i] * t);
+  for (int i = threadIdx.x; i < cols; i += blockDim.x) dv[i] = sc * (dw[i] - v[i] * t);
 }
 
 // --------------------------------------------------------------- groupnorm
@@ -779,6 +796,7 @@ extern "C" int vqx_weight_norm_bwd(const vqx_wn_layer* lh, const vqx_wn_layer* l
     const int cols = (l.kind == 0 ? l.cin : l.cout) * l.k;
     if (cols > 4096) { set_error("vqx_weight_norm_bwd: row length %d > 4096", cols); return -1; }
     if (!l.slabs || !l.dv || (l.g && !l.dg) || l.splits < 1) { set_error("vqx_weight_norm_bwd: layer %d missing buffers", i); return -1; }
+    if ((l.kind == 0 ? l.cin : l.cout) % 4 || ((uintptr_t)l.slabs & 15)) { set_error("vqx_weight_norm_bwd: layer %d: slab rows must be 16-B vectors", i); return -1; }
     max_rows = rows > max_rows ? rows : max_rows;
   }
   hipLaunchKernelGGL(wn_bwd_kernel, dim3(max_rows, n_layers), dim3(256), 0, (hipStream_t)stream, ld, n_layers);

@@ -5,15 +5,17 @@ torch's current stream; torch is used only for device memory and streams.
 Step anatomy (frame-major activations [N = B*T, C], see include/vqx.h):
 
   pack     weight norm of all 44 convs -> packed effective weights (1 launch pair)
-  encoder  conv0 | 10 x {k3 conv (LReLU prologue) -> GN stats -> 1x1 skip conv
-           with the GroupNorm-apply + residual fused in its epilogue} | 1x1 out
-           conv (LReLU prologue, f32 out)                       (vqvae.py:185-192)
+  encoder  conv0 | 10 x {k3 conv -> GN stats -> 1x1 skip conv with the
+           GroupNorm-apply + residual fused in its epilogue} | 1x1 out conv
+           (f32 out).  Each GEMM producing c_i also stores LeakyReLU(c_i), so
+           no GEMM applies an activation to its staged operands
+                                                                 (vqvae.py:185-192)
   vq       fused distance/argmin/gather/commitment/EMA-statistics kernel
                                                                  (layers_vq.py:268-323)
   decoder  ConvT0 | 10 x {ConvT k3 (+ speaker term as a per-utterance row bias)
            -> GN stats -> GN+tanh*sigmoid -> 1x1 res/skip conv with the
            residual add and the skip accumulation split in its epilogue} |
-           ReLU(s*skip) 1x1 | ReLU 1x1                           (vqvae.py:298-318)
+           ReLU(s*skip) -> 1x1 (ReLU epilogue) -> 1x1            (vqvae.py:298-318)
   loss     log-likelihood + its gradient in one pass            (layers.py:283-296)
   backward encoder (driven only by beta*commitment, the reference quirk:
            z_vq carries no gradient, layers_vq.py:315) and decoder: dgrad GEMMs
@@ -79,6 +81,7 @@ class Workspace:
         ns, nd, K, D = d["ns"], d["nd"], d["K"], d["Z"]
         self.x = e(N, mel)
         self.c = [e(N, C) for _ in range(ns + 1)]
+        self.a = [e(N, C) for _ in range(ns + 1)]   # LeakyReLU(c_i), written by the producing GEMM (ACT2)
         self.h = [e(N, C) for _ in range(ns)]
         self.enc_mr = e(ns, B, 2, dt=F32)
         self.z = e(N, Z, dt=F32)
@@ -100,8 +103,8 @@ class Workspace:
         self.g = [e(N, Cd) for _ in range(nd)]
         self.dec_mr = e(nd, B, 4, dt=F32)
         self.skip32 = e(N, S, dt=F32)
-        self.skip_c = e(N, S) if cd != F32 else self.skip32
-        self.f1 = e(N, S)
+        self.a_skip = e(N, S)                       # ReLU(sqrt(1/(nd+1)) * skip)
+        self.f1 = e(N, S)                           # ReLU(final conv 1 output)
         self.xhat = e(N, Fo, dt=F32)
         self.xhat_nct = e(B, Fo, T, dt=F32)
         # scalars: 0 x_loss, 1 sqerr, 4..7 EMA diagnostics
@@ -206,7 +209,9 @@ class VQVAEEngine:
         self.fin2 = mk(dec.final_layer[3], "decoder.final_layer.3")
         self.convs = ([self.enc0] + [x for pair in zip(self.enc_k3, self.enc_sk) for x in pair] + [self.enc_out, self.dec0]
                       + [x for tr in zip(self.dec_in, self.dec_cond, self.dec_rs) for x in tr] + [self.fin1, self.fin2])
-        # split-K factors for the wgrad GEMMs (config-2 sized: ~512-768 workgroups)
+        # split-K factors for the wgrad GEMMs: ~512 workgroups (2 per CU) at
+        # config 2 (64 x 256 frames), at least 4 K-tiles (256 frames) per
+        # split; every split costs a slab write + read of rows x cols fp32
         N_ref = 64 * 256
         for Lr in self.convs:
             if Lr in self.dec_cond:
@@ -214,7 +219,7 @@ class VQVAEEngine:
                 continue
             r, c = (Lr.cin, Lr.k * Lr.cout) if Lr.kind else (Lr.cout, Lr.k * Lr.cin)
             tiles = math.ceil(r / 128) * math.ceil(c / 128)
-            Lr.splits = max(1, min(16, _pow2_floor(max(1, 640 // tiles)), N_ref // 512))
+            Lr.splits = max(1, min(_pow2_floor(max(1, 512 // tiles)), N_ref // 256))
         # slab arena: one backward group's slabs at a time (kept L2/MALL-resident)
         groups = self._bwd_groups()
         arena = max(sum(Lr.splits * Lr.rows * Lr.cols for Lr in grp) for grp in groups)
@@ -293,14 +298,16 @@ class VQVAEEngine:
     def encoder_fwd(self, w, x_nct):
         T = w.T
         ops.nct_to_ntc(x_nct, w.x)
-        self.fwd(self.enc0, w.x, w.c[0], T, bias=self.enc0.mod.bias)
+        # every GEMM producing c_i also writes a_i = LeakyReLU(c_i), the operand
+        # of the next k3 conv / the output conv (vqvae.py:86-87 stack[0], 190)
+        self.fwd(self.enc0, w.x, w.c[0], T, bias=self.enc0.mod.bias, act=L.PRO_LRELU, y2=w.a[0])
         for i in range(self.dims["ns"]):
             k3, sk, gn = self.enc_k3[i], self.enc_sk[i], self.enc_gn[i]
-            self.fwd(k3, w.c[i], w.h[i], T, prologue=L.PRO_LRELU, bias=k3.mod.bias)
+            self.fwd(k3, w.a[i], w.h[i], T, bias=k3.mod.bias)
             ops.groupnorm_stats(w.h[i], T, 1, w.gn_part, w.enc_mr[i])
             self.fwd(sk, w.c[i], w.c[i + 1], T, bias=sk.mod.bias, gn_h=w.h[i], gn_mr=w.enc_mr[i],
-                     gn_gamma=gn.weight, gn_beta=gn.bias)
-        self.fwd(self.enc_out, w.c[-1], w.z, T, prologue=L.PRO_LRELU, bias=self.enc_out.mod.bias, out_f32=True)
+                     gn_gamma=gn.weight, gn_beta=gn.bias, act=L.PRO_LRELU, y2=w.a[i + 1])
+        self.fwd(self.enc_out, w.a[-1], w.z, T, bias=self.enc_out.mod.bias, out_f32=True)
 
     def decoder_fwd(self, w, zq_c):
         T, nd, Cd = w.T, self.dims["nd"], self.dims["Cd"]
@@ -312,11 +319,10 @@ class VQVAEEngine:
             ops.gn_glu_fwd(w.u[i], w.g[i], T, w.dec_mr[i], gn.weight, gn.bias)
             self.fwd(rs, w.g[i], w.xs[i + 1], T, bias=rs.mod.bias, res=w.xs[i], out2=w.skip32, split_col=Cd,
                      out2_accumulate=(i > 0))
-        if w.skip_c is not w.skip32:
-            ops.convert_2d(w.skip32, w.skip_c)
-        self.fwd(self.fin1, w.skip_c, w.f1, T, prologue=L.PRO_SCALE_RELU, pro_scale=math.sqrt(1.0 / (nd + 1)),
-                 bias=self.fin1.mod.bias)
-        self.fwd(self.fin2, w.f1, w.xhat, T, prologue=L.PRO_RELU, bias=self.fin2.mod.bias, out_f32=True)
+        # final_layer = ReLU, conv, ReLU, conv on sqrt(1/(nd+1)) * sum(skips) (vqvae.py:316-318)
+        ops.scale_act_2d(w.skip32, w.a_skip, math.sqrt(1.0 / (nd + 1)), L.PRO_RELU)
+        self.fwd(self.fin1, w.a_skip, w.f1, T, bias=self.fin1.mod.bias, act=L.PRO_RELU)
+        self.fwd(self.fin2, w.f1, w.xhat, T, bias=self.fin2.mod.bias, out_f32=True)
 
     # ------------------------------------------------------------ quantizer host logic
     def _perm_rows(self, n, K, rank_offset=0, n_local=None):
@@ -375,9 +381,9 @@ class VQVAEEngine:
         ops.vq_commit_bwd(w.z, w.zq, 2.0 * self.m.beta * grad_scale / N, w.dz)
         eo = self.enc_out
         self.bias_grad(eo, w.dz, w)
-        self.wgrad(eo, w.dz, w.c[ns], T, pro=L.PRO_LRELU)
+        self.wgrad(eo, w.dz, w.a[ns], T)
         cur = w.dc[0]
-        self.dgrad(eo, w.dz, cur, T, mask=w.c[ns], mask_slope=0.2)
+        self.dgrad(eo, w.dz, cur, T, mask=w.a[ns], mask_slope=0.2)
         ops.weight_norm_bwd(self.wn_bwd_tables[id(eo)])
         cs_b, dg_b, db_b = (self._bview(t, B, C) for t in (w.colsum_b, w.dgam_b, w.dbet_b))
         for i in reversed(range(ns)):
@@ -390,8 +396,8 @@ class VQVAEEngine:
             ops.colsum(cs_b, w.cs_part, self.g(k3.mod.bias))
             ops.colsum(dg_b, w.cs_part, self.g(gn.weight))
             ops.colsum(db_b, w.cs_part, self.g(gn.bias))
-            self.wgrad(k3, w.dh, w.c[i], T, pro=L.PRO_LRELU)
-            self.dgrad(k3, w.dh, w.tmp, T, mask=w.c[i], mask_slope=0.2)
+            self.wgrad(k3, w.dh, w.a[i], T)
+            self.dgrad(k3, w.dh, w.tmp, T, mask=w.a[i], mask_slope=0.2)
             self.dgrad(sk, cur, nxt, T, res=w.tmp)
             ops.weight_norm_bwd(self.wn_bwd_tables[id(k3)])
             cur = nxt
@@ -405,14 +411,14 @@ class VQVAEEngine:
         f1, f2 = self.fin1, self.fin2
         dxhat = w.dxhat
         self.bias_grad(f2, dxhat, w)
-        self.wgrad(f2, dxhat, w.f1, T, pro=L.PRO_RELU)
+        self.wgrad(f2, dxhat, w.f1, T)
         self.dgrad(f2, dxhat, w.df1, T, mask=w.f1, mask_slope=0.0)
         s = math.sqrt(1.0 / (nd + 1))
         self.bias_grad(f1, w.df1, w)
-        self.wgrad(f1, w.df1, w.skip_c, T, pro=L.PRO_SCALE_RELU, scale=s)
+        self.wgrad(f1, w.df1, w.a_skip, T)
         cur, nxt = w.dr[0], w.dr[1]
         # dL/dskip (identical for every block) -> tail columns of both [dx | dskip] buffers
-        self.dgrad(f1, w.df1, cur[:, Cd:], T, mask=w.skip_c, mask_slope=0.0, mask_scale=s)
+        self.dgrad(f1, w.df1, cur[:, Cd:], T, mask=w.a_skip, mask_slope=0.0, mask_scale=s)
         ops.convert_2d(cur[:, Cd:], nxt[:, Cd:])
         ops.convert_2d(None, cur, cols=Cd)  # dL/dx_{nd+1} = 0: the last residual output is unused
         ops.weight_norm_bwd(self.wn_bwd_tables[id(f1)])

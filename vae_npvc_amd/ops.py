@@ -81,18 +81,21 @@ class LaunchProbe:
     def __init__(self):
         self.records = []
 
-    def run(self, mode, dtype_code, pro, flops, fn):
+    def run(self, mode, dtype_code, pro, flops, fn, shape=""):
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
         fn()
         e1.record()
-        self.records.append((f"vqx::conv_gemm_kernel<{self._DT[dtype_code]}, {mode}, {pro}>", flops, e0, e1))
+        self.records.append((f"vqx::conv_gemm_kernel<{self._DT[dtype_code]}, {mode}, {pro}>", flops, e0, e1, shape))
 
-    def summary(self):
+    def summary(self, by_shape=False):
+        """Aggregate per kernel symbol (by_shape: per symbol and layer shape)."""
         torch.cuda.synchronize()
         agg = {}
-        for key, fl, e0, e1 in self.records:
+        for key, fl, e0, e1, shape in self.records:
+            if by_shape:
+                key = f"{key} {shape}"
             a = agg.setdefault(key, [0, 0.0, 0.0])
             a[0] += 1
             a[1] += fl
@@ -117,7 +120,8 @@ def conv_fwd(x, w, y, **kw):
     if _probe is None:
         fn()
     else:
-        _probe.run(0, a.dtype, a.prologue, 2.0 * a.n_rows * a.cout * a.ntaps * a.cin, fn)
+        _probe.run(0, a.dtype, a.prologue, 2.0 * a.n_rows * a.cout * a.ntaps * a.cin, fn,
+                   f"{a.cin}->{a.cout} k{a.ntaps} epi{a.epilogue}")
     return y
 
 
@@ -130,7 +134,8 @@ def conv_dgrad(dy, w, dx, **kw):
     if _probe is None:
         fn()
     else:
-        _probe.run(1, a.dtype, a.prologue, 2.0 * a.n_rows * a.cout * a.ntaps * a.cin, fn)
+        _probe.run(1, a.dtype, a.prologue, 2.0 * a.n_rows * a.cout * a.ntaps * a.cin, fn,
+                   f"{a.cin}->{a.cout} k{a.ntaps} epi{a.epilogue}")
     return dx
 
 
@@ -147,7 +152,8 @@ def conv_wgrad(p, q, slabs, *, T, r_dim, c_dim, ntaps, pad, shift_sign=1, q_prol
     if _probe is None:
         fn()
     else:
-        _probe.run(2, a.dtype, a.q_prologue, 2.0 * a.n_rows * r_dim * ntaps * c_dim, fn)
+        _probe.run(2, a.dtype, a.q_prologue, 2.0 * a.n_rows * r_dim * ntaps * c_dim, fn,
+                   f"{r_dim}x{ntaps}x{c_dim} s{splits}")
     return slabs
 
 
