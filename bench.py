@@ -67,6 +67,21 @@ def cpu_baseline(cfg, steps):
                       f"torch-CPU {torch.__version__}, s/step={dt:.2f}"}
 
 
+def committed_traffic(symbol):
+    """HBM bytes per launch of `symbol` from the newest committed PMC summary
+    (profiles/rNN/hbm.json, written by tools/pmc_hbm.py from rocprofv3
+    FETCH_SIZE/WRITE_SIZE passes with the gfx950 corrections), or None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "hbm.json")), reverse=True):
+        try:
+            k = json.load(open(path))["kernels"].get(symbol)
+        except (OSError, ValueError, KeyError):
+            continue
+        if k:
+            return round(k["hbm_bytes_per_launch"]), os.path.relpath(path, ROOT)
+    return None, None
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -131,8 +146,10 @@ def main():
         name, s = dom
         peak = PEAK_BF16 if a.dtype == "bf16" else PEAK_F32
         ach = s["flops"] / s["seconds"]
+        traffic, tsrc = committed_traffic(name)
         roof = {"bound": "mfma", "kernel": name, "achieved": round(ach / 1e12, 2), "peak": peak / 1e12,
-                "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": None,
+                "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+                "traffic_source": tsrc,
                 "launches_per_step": s["launches"] / a.steps, "avg_launch_us": round(s["avg_us"], 2),
                 "flops_per_launch": s["flops"] / s["launches"]}
 

@@ -304,7 +304,17 @@ int vqx_convert_2d(const void* src, int32_t ld_src, int32_t src_dtype, void* dst
 
 /* Thread-local description of the last failure. */
 const char* vqx_last_error(void);
-/* ABI version (major*100 + minor). */
+/* Launch probe (measurement only; not reentrant while enabled).  While on,
+ * each conv GEMM launch records a start/stop event pair stamped on its own
+ * dispatch (hipExtLaunchKernelGGL); after the stream is synchronised,
+ * vqx_probe_read returns per launch {dtype, mode, prologue, gen, dma}, the
+ * algorithmic FLOPs and the kernel duration in ms.  Enabling clears the log. */
+int vqx_probe_enable(int32_t on);
+int vqx_probe_count(int64_t* n);
+int vqx_probe_read(int64_t i, int32_t* info5, double* flops, float* ms);
+
+/* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
+#define VQX_ABI_VERSION 102
 int vqx_version(void);
 
 #ifdef __cplusplus

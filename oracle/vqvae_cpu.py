@@ -216,10 +216,19 @@ class OracleVQVAE:
             z = z + torch.randn_like(z) * std
         return z
 
+    # Data-parallel hooks (tests/test_ddp_gloo.py): identity in one process.
+    # reduce_sum all-reduces the EMA statistics; pick_rows draws the
+    # dead-code / init rows z[randperm(N)[:K]] from the GLOBAL batch.
+    def reduce_sum(self, t):
+        return t
+
+    def pick_rows(self, zt):
+        return zt[torch.randperm(zt.shape[0])][: self.K]
+
     def init_emb(self, z):  # layers_vq.py:192-201
         self.emb_init = not self.emb_init
         _z = self._tile(z)
-        self.embeddings = _z[torch.randperm(_z.shape[0])][: self.K]
+        self.embeddings = self.pick_rows(_z)
         self.emb_sum = self.embeddings.clone()
         self.emb_elem = torch.ones(self.K)
 
@@ -228,10 +237,10 @@ class OracleVQVAE:
         with torch.no_grad():
             onehot = torch.zeros(K, z.shape[0])
             onehot.scatter_(0, idx.view(1, z.shape[0]), 1)
-            s = torch.matmul(onehot, z)
-            n = onehot.sum(dim=-1)
+            s = self.reduce_sum(torch.matmul(onehot, z))
+            n = self.reduce_sum(onehot.sum(dim=-1))
             _z = self._tile(z)
-            rand = _z[torch.randperm(_z.shape[0])][:K]
+            rand = self.pick_rows(_z)
             old = self.embeddings.clone()
             self.emb_sum = mu * self.emb_sum + (1.0 - mu) * s
             self.emb_elem = mu * self.emb_elem + (1.0 - mu) * n
@@ -324,6 +333,7 @@ class OracleTrainer:
             self.scheduler = torch.optim.lr_scheduler.StepLR(optimizer=self.optimizer, **lp)
         self.iteration = 0
         self.grads = None
+        self.grad_hook = None
 
     def train_step(self, batch, keep_grads=False):
         for p in self.model.params.values():
@@ -331,6 +341,8 @@ class OracleTrainer:
         x, y = batch
         xhat, loss, detail = self.model.forward(x, y)
         loss.backward()
+        if self.grad_hook is not None:  # data parallel: gradient all-reduce (mean)
+            self.grad_hook(list(self.model.params.values()))
         if keep_grads:
             self.grads = OrderedDict((k, v.grad.detach().clone()) for k, v in self.model.params.items())
         if self.max_grad_norm > 0:

@@ -27,7 +27,11 @@
 // (channels for FWD/DGRAD, j*cd+c for WGRAD), so each lane ends up holding 4
 // consecutive output elements per register group: the epilogue does vector
 // loads/stores (8 B bf16, 16 B f32) for bias, residual, masks and results.
+#include <hip/hip_ext.h>
 #include <stdlib.h>
+
+#include <vector>
+
 #include "vqx_common.h"
 
 namespace vqx {
@@ -619,13 +623,55 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
   }
 }
 
+// ---------------- launch probe (bench.py's roofline leg)
+// While enabled, every conv GEMM is launched with hipExtLaunchKernelGGL and a
+// start/stop event pair that the runtime stamps on the kernel's own dispatch
+// packet, so the measured duration is the kernel's (no extra queue packets
+// between kernels).  Events come from a pool reused across probe sessions.
+struct ProbeRec {
+  hipEvent_t start, stop;
+  int info[5];  // dtype, mode, prologue, gen, dma
+  double flops;
+};
+static bool g_probe_on = false;
+static std::vector<ProbeRec> g_probe;
+static std::vector<std::pair<hipEvent_t, hipEvent_t>> g_event_pool;
+static size_t g_probe_used = 0;
+
+template <typename K>
+static void launch_gemm(K kernel, int grid, hipStream_t s, const GemmParams& P, const int info[5], double flops) {
+  if (!g_probe_on) {
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), 0, s, P);
+    return;
+  }
+  if (g_probe_used == g_event_pool.size()) {
+    hipEvent_t a, b;
+    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
+      hipLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), 0, s, P);
+      return;
+    }
+    g_event_pool.emplace_back(a, b);
+  }
+  auto ev = g_event_pool[g_probe_used++];
+  ProbeRec r;
+  r.start = ev.first;
+  r.stop = ev.second;
+  for (int i = 0; i < 5; ++i) r.info[i] = info[i];
+  r.flops = flops;
+  g_probe.push_back(r);
+  hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), 0, s, ev.first, ev.second, 0, P);
+}
+
 template <typename T, int MODE, bool GEN, bool DMA>
 static void launch_pro(const GemmParams& P, int grid, hipStream_t s) {
+  const double flops = MODE == MODE_WGRAD ? 2.0 * (double)P.n_rows * P.Mc * P.Nc
+                                          : 2.0 * (double)P.n_rows * P.Nc * P.K;
+  const int info[5] = {sizeof(T) == 2 ? VQX_BF16 : VQX_F32, MODE, P.pro, GEN ? 1 : 0, DMA ? 1 : 0};
   switch (P.pro) {
-    case VQX_PRO_NONE: hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, VQX_PRO_NONE, GEN, DMA>), dim3(grid), dim3(kThreads), 0, s, P); break;
-    case VQX_PRO_LRELU: hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, VQX_PRO_LRELU, GEN, DMA>), dim3(grid), dim3(kThreads), 0, s, P); break;
-    case VQX_PRO_RELU: hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, VQX_PRO_RELU, GEN, DMA>), dim3(grid), dim3(kThreads), 0, s, P); break;
-    default: hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, VQX_PRO_SCALE_RELU, GEN, DMA>), dim3(grid), dim3(kThreads), 0, s, P); break;
+    case VQX_PRO_NONE: launch_gemm(conv_gemm_kernel<T, MODE, VQX_PRO_NONE, GEN, DMA>, grid, s, P, info, flops); break;
+    case VQX_PRO_LRELU: launch_gemm(conv_gemm_kernel<T, MODE, VQX_PRO_LRELU, GEN, DMA>, grid, s, P, info, flops); break;
+    case VQX_PRO_RELU: launch_gemm(conv_gemm_kernel<T, MODE, VQX_PRO_RELU, GEN, DMA>, grid, s, P, info, flops); break;
+    default: launch_gemm(conv_gemm_kernel<T, MODE, VQX_PRO_SCALE_RELU, GEN, DMA>, grid, s, P, info, flops); break;
   }
 }
 
@@ -746,4 +792,29 @@ extern "C" int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream) {
   if (a->dtype == VQX_BF16) launch_mode<bf16_t, MODE_WGRAD>(P, grid, gen, s);
   else launch_mode<float, MODE_WGRAD>(P, grid, gen, s);
   return launch_status("vqx_conv1d_wgrad");
+}
+
+extern "C" int vqx_probe_enable(int32_t on) {
+  if (on) {
+    g_probe.clear();
+    g_probe_used = 0;
+  }
+  g_probe_on = on != 0;
+  return 0;
+}
+
+extern "C" int vqx_probe_count(int64_t* n) {
+  if (!n) { set_error("vqx_probe_count: null"); return -1; }
+  *n = (int64_t)g_probe.size();
+  return 0;
+}
+
+extern "C" int vqx_probe_read(int64_t i, int32_t* info5, double* flops, float* ms) {
+  if (i < 0 || i >= (int64_t)g_probe.size() || !info5 || !flops || !ms) { set_error("vqx_probe_read: bad index %lld", (long long)i); return -1; }
+  const ProbeRec& r = g_probe[i];
+  for (int k = 0; k < 5; ++k) info5[k] = r.info[k];
+  *flops = r.flops;
+  const hipError_t e = hipEventElapsedTime(ms, r.start, r.stop);
+  if (e != hipSuccess) { set_error("vqx_probe_read: %s", hipGetErrorString(e)); return -1; }
+  return 0;
 }

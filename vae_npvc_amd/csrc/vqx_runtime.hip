@@ -24,4 +24,4 @@ int launch_status(const char* what) {
 }  // namespace vqx
 
 extern "C" const char* vqx_last_error(void) { return vqx::g_err; }
-extern "C" int vqx_version(void) { return 100; }
+extern "C" int vqx_version(void) { return VQX_ABI_VERSION; }

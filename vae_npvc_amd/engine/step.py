@@ -330,8 +330,8 @@ class VQVAEEngine:
         mapped to local row ids (-1 = row owned by another rank)."""
         perm = torch.randperm(n)[:K]
         if n_local is not None:
-            loc = perm - rank_offset
-            perm = torch.where((loc >= 0) & (loc < n_local), loc, torch.full_like(loc, -1))
+            from ..parallel.ddp import owned_rows
+            perm = owned_rows(perm, rank_offset, n_local)
         return perm.pin_memory().to(self.device, non_blocking=True)
 
     def _tile_rows(self, w):
@@ -458,7 +458,7 @@ class VQVAEEngine:
         if q.initialized:
             return False
         K = self.dims["K"]
-        if w.N < K:
+        if w.N * self.world < K:  # N_global < K: noisy tiling (local rows; DESIGN.md "multi-GPU")
             rows = self._tile_rows(w)
             q.embeddings.copy_(rows)
         else:

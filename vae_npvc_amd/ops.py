@@ -72,34 +72,49 @@ def conv_args(x, w, y, *, T, cin, cout, ntaps, pad, prologue=L.PRO_NONE, pro_sca
 
 
 class LaunchProbe:
-    """Per-launch HIP-event timing of the conv GEMM kernels (bench.py's roofline
-    leg).  Records (kernel symbol, algorithmic FLOPs, start, end) per launch on
-    torch's current stream, i.e. the stream the kernels run on."""
+    """Per-launch timing of the conv GEMM kernels (bench.py's roofline leg).
+    libvqx launches each GEMM with hipExtLaunchKernelGGL and a start/stop
+    event pair stamped on the kernel's own dispatch (vqx_probe_*), on the
+    stream the kernel runs on; this class only labels and aggregates."""
 
     _DT = {L.VQX_F32: "float", L.VQX_BF16: "unsigned short"}
 
     def __init__(self):
-        self.records = []
+        self.shapes = []
 
-    def run(self, mode, dtype_code, pro, flops, fn, shape=""):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        fn()
-        e1.record()
-        self.records.append((f"vqx::conv_gemm_kernel<{self._DT[dtype_code]}, {mode}, {pro}>", flops, e0, e1, shape))
+    def start(self):
+        self.shapes = []
+        call("vqx_probe_enable", 1)
+
+    def stop(self):
+        call("vqx_probe_enable", 0)
+
+    def records(self):
+        """[(rocprof symbol, flops, seconds, shape label)] after a device sync."""
+        torch.cuda.synchronize()
+        n = ctypes.c_int64()
+        call("vqx_probe_count", ctypes.byref(n))
+        info = (ctypes.c_int32 * 5)()
+        fl, ms = ctypes.c_double(), ctypes.c_float()
+        out = []
+        for i in range(n.value):
+            call("vqx_probe_read", i, info, ctypes.byref(fl), ctypes.byref(ms))
+            dt, mode, pro, gen, dma = list(info)
+            sym = (f"vqx::conv_gemm_kernel<{self._DT[dt]}, {mode}, {pro}, {'true' if gen else 'false'}, "
+                   f"{'true' if dma else 'false'}>")
+            out.append((sym, fl.value, ms.value * 1e-3, self.shapes[i] if i < len(self.shapes) else ""))
+        return out
 
     def summary(self, by_shape=False):
         """Aggregate per kernel symbol (by_shape: per symbol and layer shape)."""
-        torch.cuda.synchronize()
         agg = {}
-        for key, fl, e0, e1, shape in self.records:
+        for key, fl, sec, shape in self.records():
             if by_shape:
                 key = f"{key} {shape}"
             a = agg.setdefault(key, [0, 0.0, 0.0])
             a[0] += 1
             a[1] += fl
-            a[2] += e0.elapsed_time(e1) * 1e-3
+            a[2] += sec
         return {k: {"launches": n, "flops": f, "seconds": t, "avg_us": 1e6 * t / n, "tflops": f / t / 1e12}
                 for k, (n, f, t) in agg.items()}
 
@@ -108,20 +123,22 @@ _probe = None
 
 
 def set_probe(p):
+    """Install (p.start()) or remove (None) the GEMM launch probe."""
     global _probe
+    if _probe is not None and p is None:
+        _probe.stop()
     _probe = p
+    if p is not None:
+        p.start()
 
 
 def conv_fwd(x, w, y, **kw):
     """y = epi(conv(pro(x), w)); x [N, cin], w packed [cout, ntaps*cin], y [N, cout]."""
     _check_cuda(x, w, y)
     a = conv_args(x, w, y, **kw)
-    fn = lambda: call("vqx_conv1d_fwd", ctypes.byref(a), stream_ptr())  # noqa: E731
-    if _probe is None:
-        fn()
-    else:
-        _probe.run(0, a.dtype, a.prologue, 2.0 * a.n_rows * a.cout * a.ntaps * a.cin, fn,
-                   f"{a.cin}->{a.cout} k{a.ntaps} epi{a.epilogue}")
+    if _probe is not None:
+        _probe.shapes.append(f"{a.cin}->{a.cout} k{a.ntaps} epi{a.epilogue}")
+    call("vqx_conv1d_fwd", ctypes.byref(a), stream_ptr())
     return y
 
 
@@ -130,12 +147,9 @@ def conv_dgrad(dy, w, dx, **kw):
     Pass cin=cout_f, cout=cin_f."""
     _check_cuda(dy, w, dx)
     a = conv_args(dy, w, dx, **kw)
-    fn = lambda: call("vqx_conv1d_dgrad", ctypes.byref(a), stream_ptr())  # noqa: E731
-    if _probe is None:
-        fn()
-    else:
-        _probe.run(1, a.dtype, a.prologue, 2.0 * a.n_rows * a.cout * a.ntaps * a.cin, fn,
-                   f"{a.cin}->{a.cout} k{a.ntaps} epi{a.epilogue}")
+    if _probe is not None:
+        _probe.shapes.append(f"{a.cin}->{a.cout} k{a.ntaps} epi{a.epilogue}")
+    call("vqx_conv1d_dgrad", ctypes.byref(a), stream_ptr())
     return dx
 
 
@@ -148,12 +162,9 @@ def conv_wgrad(p, q, slabs, *, T, r_dim, c_dim, ntaps, pad, shift_sign=1, q_prol
     a.n_rows, a.T, a.r_dim, a.c_dim, a.ntaps, a.pad, a.shift_sign = p.shape[0], T, r_dim, c_dim, ntaps, pad, shift_sign
     a.ldp, a.ldq = p.stride(0), q.stride(0)
     a.dtype, a.q_prologue, a.splits, a.pro_scale = dt_code(p.dtype), q_prologue, splits, pro_scale
-    fn = lambda: call("vqx_conv1d_wgrad", ctypes.byref(a), stream_ptr())  # noqa: E731
-    if _probe is None:
-        fn()
-    else:
-        _probe.run(2, a.dtype, a.q_prologue, 2.0 * a.n_rows * r_dim * ntaps * c_dim, fn,
-                   f"{r_dim}x{ntaps}x{c_dim} s{splits}")
+    if _probe is not None:
+        _probe.shapes.append(f"{r_dim}x{ntaps}x{c_dim} s{splits}")
+    call("vqx_conv1d_wgrad", ctypes.byref(a), stream_ptr())
     return slabs
 
 

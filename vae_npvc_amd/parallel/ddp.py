@@ -21,6 +21,14 @@ import torch.distributed as dist
 BUCKET_BYTES = 64 << 20  # ~16M fp32 gradients per all-reduce (per-link ring ≈ 0.5 ms at 8 GPUs)
 
 
+def owned_rows(perm, rank_offset, n_local):
+    """Map global row ids (a randperm of the global batch's frames) to this
+    rank's local rows; rows another rank owns become -1 (gathered as zeros),
+    so a SUM all-reduce of the per-rank gathers assembles z_global[perm]."""
+    loc = perm - rank_offset
+    return torch.where((loc >= 0) & (loc < n_local), loc, torch.full_like(loc, -1))
+
+
 class Comm:
     def __init__(self, group=None, bucket_bytes=BUCKET_BYTES):
         self.group = group
