@@ -51,10 +51,15 @@ enum {
                                '+=' when out2_accumulate)                      */
   VQX_EPI_OUTF32 = 1 << 6,  /* y stored as f32 instead of `dtype`              */
   VQX_EPI_ACT = 1 << 7,     /* y = act(v), act = epi_act (VQX_PRO_LRELU/RELU)  */
-  VQX_EPI_ACT2 = 1 << 8     /* also y2[n][c] = act(v) (dtype): the producer writes
+  VQX_EPI_ACT2 = 1 << 8,    /* also y2[n][c] = act(v) (dtype): the producer writes
                                the pre-activated copy its consumers read, so no
                                GEMM applies an activation while staging        */
+  VQX_EPI_COLSUM = 1 << 9   /* colsum_part[tile][c] = sum over the 128-frame row
+                               tile of the stored fp32 value (before rounding):
+                               the bias gradient of the layer y feeds, reduced
+                               later by a VQX_WN_COLREDUCE table entry          */
 };
+#define VQX_CONV_TILE_ROWS 128   /* frames per GEMM row tile (COLSUM partial rows) */
 
 /*
  * Stride-1 Conv1d / ConvTranspose1d as an implicit-im2col GEMM on MFMA.
@@ -92,6 +97,7 @@ typedef struct vqx_conv_args {
   float pro_scale, mask_slope, mask_scale;
   void* y2;                  /* ACT2 destination [N][ldy2]                     */
   int32_t ldy2, epi_act;
+  float* colsum_part;        /* COLSUM destination [ceil(N/128)][cout]         */
 } vqx_conv_args;
 
 int vqx_conv1d_fwd(const vqx_conv_args* a, vqx_stream_t stream);
@@ -126,6 +132,9 @@ int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream);
  * (effective tap j' = k-1-j).  Descriptors are batched: one launch packs
  * every layer of the model.
  */
+#define VQX_WN_COLREDUCE 2  /* table entry kind: dv[c] = sum_{r < cin} v[r*cout + c] (bias /
+                               GroupNorm-affine gradients from per-tile or per-utterance
+                               partials, reduced in the same backward launch)        */
 typedef struct vqx_wn_layer {
   const float* v;       /* [rows][cols] */
   const float* g;       /* [rows]       */
@@ -264,6 +273,26 @@ int vqx_embedding_bwd(const float* dout, const int64_t* ids, int32_t B, int32_t 
  * out[b][o] = sum_i W[o][i] * c[b][i] + bias[o]   (f32, W from weight norm
  * in f32).  And its backward:  dW[o][i] += sum_b dout[b][o] * c[b][i],
  * dc[b][i] += sum_o dout[b][o] * W[o][i]. */
+/* All ResSkip blocks' speaker-conditioning linears in one launch (conv_cond on
+ * the time-constant embedding, layers.py:218-236; table on the device).
+ * fwd: out_l[b][o] = W_l[o][:] . c[b][:] + bias_l[o].
+ * bwd: dW_l = dout_l^T c, dbias_l = colsum(dout_l) (both overwritten) and
+ *      dc[b][i] = sum_l sum_o dout_l[b][o] W_l[o][i] (overwritten; NULL skips),
+ *      reduced deterministically from split-K partials
+ *      [n * ceil(O/64)][B][I] f32 (caller workspace). */
+typedef struct vqx_linear_layer {
+  const float* W;      /* [O][I] */
+  const float* bias;   /* [O] or NULL */
+  float* out;          /* fwd [B][O] */
+  const float* dout;   /* bwd [B][O] */
+  float* dW;           /* bwd [O][I] */
+  float* dbias;        /* bwd [O] or NULL */
+} vqx_linear_layer;
+int vqx_linear_batched_fwd(const vqx_linear_layer* table_dev, int32_t n, const float* c, int32_t B,
+                           int32_t I, int32_t O, vqx_stream_t stream);
+int vqx_linear_batched_bwd(const vqx_linear_layer* table_dev, int32_t n, const float* c, int32_t B,
+                           int32_t I, int32_t O, float* dc, float* partials, vqx_stream_t stream);
+
 int vqx_linear_f32(const float* c, const float* W, const float* bias, int32_t B, int32_t I,
                    int32_t O, float* out, vqx_stream_t stream);
 int vqx_linear_bwd_f32(const float* dout, const float* c, const float* W, int32_t B, int32_t I,
@@ -304,6 +333,11 @@ int vqx_convert_2d(const void* src, int32_t ld_src, int32_t src_dtype, void* dst
 
 /* Thread-local description of the last failure. */
 const char* vqx_last_error(void);
+/* Conv GEMM tile height: 0 = automatic (currently 128 rows), 1 = 128 rows
+ * (2 workgroups of 4 waves per CU), 2 = 256 rows (1 workgroup of 8 waves per
+ * CU).  Process-wide; the default comes from env VQX_GEMM_SUB. */
+int vqx_set_gemm_tile(int32_t policy);
+
 /* Launch probe (measurement only; not reentrant while enabled).  While on,
  * each conv GEMM launch records a start/stop event pair stamped on its own
  * dispatch (hipExtLaunchKernelGGL); after the stream is synchronised,
@@ -314,7 +348,7 @@ int vqx_probe_count(int64_t* n);
 int vqx_probe_read(int64_t i, int32_t* info5, double* flops, float* ms);
 
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
-#define VQX_ABI_VERSION 102
+#define VQX_ABI_VERSION 105
 int vqx_version(void);
 
 #ifdef __cplusplus

@@ -15,6 +15,15 @@ def _ops():
     return ops
 
 
+@pytest.fixture(params=[1, 2], ids=["tile128", "tile256"])
+def tile(request):
+    """Run a GEMM test with the 128-row and with the 256-row (8-wave) tile."""
+    from vae_npvc_amd import _lib as L
+    L.call("vqx_set_gemm_tile", request.param)
+    yield request.param
+    L.call("vqx_set_gemm_tile", 0)
+
+
 def ref_conv(x_ntc, w, B, T, pad, pro=None):
     x = x_ntc.double().view(B, T, -1).permute(0, 2, 1)
     if pro == "lrelu":
@@ -41,7 +50,7 @@ def relerr(a, b):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("cin,cout,k,pro", [(80, 512, 3, None), (512, 512, 3, "lrelu"), (512, 128, 1, "lrelu"),
                                             (128, 80, 1, "relu"), (512, 640, 1, None), (512, 1024, 3, None)])
-def test_conv_fwd(dtype, cin, cout, k, pro):
+def test_conv_fwd(dtype, cin, cout, k, pro, tile):
     ops = _ops()
     from vae_npvc_amd import _lib as L
     torch.manual_seed(0)
@@ -61,7 +70,7 @@ def test_conv_fwd(dtype, cin, cout, k, pro):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("cin,cout,k", [(512, 512, 3), (512, 128, 1), (128, 80, 1), (512, 1024, 3), (80, 512, 3)])
-def test_conv_dgrad_wgrad(dtype, cin, cout, k):
+def test_conv_dgrad_wgrad(dtype, cin, cout, k, tile):
     ops = _ops()
     torch.manual_seed(1)
     B, T = 2, 128
@@ -89,7 +98,7 @@ def test_conv_dgrad_wgrad(dtype, cin, cout, k):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_convtranspose_via_weight_norm_pack(dtype):
+def test_convtranspose_via_weight_norm_pack(dtype, tile):
     """ConvTranspose1d(cin->cout, k3, p1) through the weight-norm pack kernel
     (dim 0 = in-channels) and the conv GEMM, fwd + wgrad(sign -1)."""
     ops = _ops()
@@ -152,7 +161,7 @@ def test_vq_argmin_exact(K):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("act", ["lrelu", "relu"])
-def test_conv_fwd_act_epilogues(dtype, act):
+def test_conv_fwd_act_epilogues(dtype, act, tile):
     """ACT (y = act(v)) and ACT2 (y = v, y2 = act(v)): the producer-side
     activation that replaces GEMM prologues (vqvae.py:186-187 LeakyReLU stack
     head, 316-317 final ReLUs)."""
@@ -192,3 +201,59 @@ def test_scale_act_2d(dt_out):
     ops.scale_act_2d(src, dst, s, L.PRO_RELU)
     torch.cuda.synchronize()
     assert torch.equal(dst, torch.relu(src * s).to(dt_out))
+
+
+@pytest.mark.parametrize("n_utt,T", [(3, 128), (1, 384), (5, 64)])
+def test_dgrad_colsum_partials(n_utt, T, tile):
+    """COLSUM epilogue: per-128-frame-group column sums of the stored fp32
+    output (the bias gradient of the next layer down), ragged row counts."""
+    ops = _ops()
+    torch.manual_seed(5)
+    cin, cout, k = 512, 256, 3
+    N = n_utt * T
+    dy = torch.randn(N, cout, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(cout, k * cin, device=DEV) / (k * cin) ** 0.5).to(torch.bfloat16)
+    res = torch.randn(N, cin, device=DEV).to(torch.bfloat16)  # RES is read in the compute dtype
+    dx = torch.empty(N, cin, device=DEV)
+    groups = (N + 127) // 128
+    part = torch.full((groups, cin), float("nan"), device=DEV)
+    ops.conv_dgrad(dy, w, dx, T=T, cin=cout, cout=cin, ntaps=k, pad=1, res=res, out_f32=True, colsum=part)
+    torch.cuda.synchronize()
+    pad = torch.zeros(groups * 128 - N, cin, device=DEV)
+    want = torch.cat([dx, pad]).view(groups, 128, cin).sum(1)
+    assert torch.isfinite(part).all()
+    assert relerr(part, want) < 1e-5
+
+
+def test_linear_batched_and_colreduce():
+    """Batched speaker-conditioning linears (fwd, dW, dbias, dc) and the
+    weight-norm backward's column-reduce entries."""
+    from vae_npvc_amd import _lib as L
+    ops = _ops()
+    torch.manual_seed(6)
+    n, B, I, O = 4, 16, 128, 1024
+    c = torch.randn(B, I, device=DEV)
+    Ws = [torch.randn(O, I, device=DEV) / I ** 0.5 for _ in range(n)]
+    bs = [torch.randn(O, device=DEV) for _ in range(n)]
+    outs = [torch.empty(B, O, device=DEV) for _ in range(n)]
+    douts = [torch.randn(B, O, device=DEV) for _ in range(n)]
+    dWs = [torch.empty(O, I, device=DEV) for _ in range(n)]
+    dbs = [torch.empty(O, device=DEV) for _ in range(n)]
+    tab = ops.linear_table([dict(W=Ws[i], bias=bs[i], out=outs[i], dout=douts[i], dW=dWs[i], dbias=dbs[i])
+                            for i in range(n)])
+    dc = torch.empty(B, I, device=DEV)
+    ops.linear_batched_fwd(tab, c, B, I, O)
+    ops.linear_batched_bwd(tab, c, B, I, O, dc)
+    src = torch.randn(70, 300, device=DEV)
+    dst = torch.empty(300, device=DEV)
+    ops.weight_norm_bwd(ops.wn_table([ops.colreduce_entry(src, dst)]))
+    torch.cuda.synchronize()
+    cd = c.double()
+    for i in range(n):
+        assert relerr(outs[i], cd @ Ws[i].double().t() + bs[i].double()) < 1e-6
+        assert relerr(dWs[i], douts[i].double().t() @ cd) < 1e-6
+        assert relerr(dbs[i], douts[i].double().sum(0)) < 1e-6
+    want_dc = sum(douts[i].double() @ Ws[i].double() for i in range(n))
+    assert relerr(dc, want_dc) < 1e-6
+    assert relerr(dst, src.double().sum(0)) < 1e-6
+    assert L.WN_COLREDUCE == 2

@@ -15,3 +15,4 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-fo
 echo "prof rc=$?" >> $O/prof.log
 tail -4 $O/tests.log
 grep -o '"value": [0-9.]*, "unit": "[^"]*", "n_gpus": [0-9]*, "steps": [0-9]*, "warmup": [0-9]*, "ms_per_step": [0-9.]*' $O/bench.log
+python3 tools/prof_summary.py $O/prof 7 25 > $O/prof_summary.txt

@@ -15,11 +15,13 @@ from pathlib import Path
 import torch  # noqa: F401  (loads the HIP runtime first; see module docstring)
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libvqx.so"
-ABI_VERSION = 102  # include/vqx.h VQX_ABI_VERSION
+ABI_VERSION = 105  # include/vqx.h VQX_ABI_VERSION
 
 VQX_F32, VQX_BF16 = 0, 1
 PRO_NONE, PRO_LRELU, PRO_RELU, PRO_SCALE_RELU = 0, 1, 2, 3
-EPI_BIAS, EPI_ROWBIAS, EPI_MASK, EPI_RES, EPI_GNADD, EPI_SPLIT, EPI_OUTF32, EPI_ACT, EPI_ACT2 = (1 << i for i in range(9))
+EPI_BIAS, EPI_ROWBIAS, EPI_MASK, EPI_RES, EPI_GNADD, EPI_SPLIT, EPI_OUTF32, EPI_ACT, EPI_ACT2, EPI_COLSUM = (
+    1 << i for i in range(10))
+CONV_TILE_ROWS = 128
 
 c_void_p, c_int32, c_int64, c_float, c_double = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
                                                  ctypes.c_float, ctypes.c_double)
@@ -35,7 +37,7 @@ class ConvArgs(ctypes.Structure):
         ("ldgn", c_int32), ("ldo2", c_int32), ("dtype", c_int32), ("prologue", c_int32),
         ("epilogue", c_int32), ("split_col", c_int32), ("out2_accumulate", c_int32),
         ("pro_scale", c_float), ("mask_slope", c_float), ("mask_scale", c_float),
-        ("y2", c_void_p), ("ldy2", c_int32), ("epi_act", c_int32),
+        ("y2", c_void_p), ("ldy2", c_int32), ("epi_act", c_int32), ("colsum_part", c_void_p),
     ]
 
 
@@ -55,6 +57,13 @@ class WNLayer(ctypes.Structure):
         ("k", c_int32), ("splits", c_int32), ("dtype", c_int32),
     ]
 
+
+class LinearLayer(ctypes.Structure):
+    _fields_ = [("W", c_void_p), ("bias", c_void_p), ("out", c_void_p), ("dout", c_void_p), ("dW", c_void_p),
+                ("dbias", c_void_p)]
+
+
+WN_COLREDUCE = 2
 
 # name -> argtypes (restype is int for every entry point except the two below)
 _SIGS = {
@@ -88,6 +97,9 @@ _SIGS = {
     "vqx_linear_bwd_f32": [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p],
     "vqx_grad_sq_norm": [c_void_p, c_int64, c_void_p, c_void_p, c_void_p],
     "vqx_adam_hyper": [c_void_p, c_double, c_double, c_int32, c_double, c_double, c_double, c_void_p, c_void_p],
+    "vqx_linear_batched_fwd": [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p],
+    "vqx_linear_batched_bwd": [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p],
+    "vqx_set_gemm_tile": [c_int32],
     "vqx_probe_enable": [c_int32],
     "vqx_probe_count": [ctypes.POINTER(c_int64)],
     "vqx_probe_read": [c_int64, ctypes.POINTER(c_int32), ctypes.POINTER(c_double), ctypes.POINTER(c_float)],

@@ -36,7 +36,7 @@
 
 namespace vqx {
 
-constexpr int kBM = 128, kBN = 128, kThreads = 256;
+constexpr int kBN = 128;  // tile width; the height is 128*SUB (conv_gemm_kernel)
 constexpr unsigned kOOB = 0x80000000u;  // buffer offset that is always out of range -> loads 0
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 
@@ -74,6 +74,7 @@ struct GemmParams {
   int ldo2, split_col, out2_acc;
   void* y2;
   int ldy2, epi_act;
+  float* colsum_part;
 };
 
 template <typename T> struct Cfg;
@@ -198,6 +199,8 @@ __device__ __forceinline__ void epilogue8(const GemmParams& P, int64_t row, int 
       for (int e = 0; e < 8; ++e) v[e] += t[e];
     }
     st8<float>(o2, 0, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = 0.f;  // not part of y: no column-sum contribution
     return;
   }
   if (epi & VQX_EPI_RES) {
@@ -254,22 +257,31 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, unsig
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (VQX_LDS(void)*)lds, 16, (int)off, 0, 0, 0);
 }
 
-// Staging layout (both paths).  A K-tile operand is 16 KiB = 16 pieces of
-// 1 KiB; wave w fills pieces 4w..4w+3, lane l the 16-B chunk c = piece*64+l
-// at LDS byte 16*c (lane-linear, as an LDS-DMA writes).  The XOR swizzle
-// that keeps the fragment reads conflict-free is applied to the SOURCE chunk:
+// Staging layout (both paths).  The block tile is BM x 128 with BM = 128*SUB
+// (SUB = 1: 4 waves, 2 workgroups per CU; SUB = 2: 8 waves, 1 per CU, 25%
+// fewer operand bytes per FLOP).  Waves form a (2*SUB) x 2 grid of 64x64
+// wave tiles.  A K-tile operand is made of 16-KiB sub-tiles (A: SUB of them,
+// B: one), each 16 pieces of 1 KiB; wave w fills A pieces 4w..4w+3 and B
+// pieces (4/SUB)w.., lane l the 16-B chunk c = piece*64+l at LDS byte 16*c
+// (lane-linear, as an LDS-DMA writes).  The XOR swizzle that keeps the
+// fragment reads conflict-free is applied to the SOURCE chunk:
 //   K-major  (128-B rows):  row = c>>3, data chunk = (c&7) ^ ((row>>1)&7)
 //   MN-major (256-B rows, bf16): row = c>>4, data chunk = (c&15) ^ mn_swz(row)
 //   MN-major (512-B rows, f32):  row = c>>5, data chunk = c&31
+// (an MN-major A tile is SUB such sub-tiles side by side, 128 columns each).
 // DMA = true: operands go global -> LDS by buffer_load ... lds (no VGPR
 // staging, no ds_write), one K-tile ahead, `vmcnt(0)` + barrier per tile.
 // DMA = false: global -> VGPR (two register sets) -> ds_write_b128.
-template <typename T, int MODE, int PRO, bool GEN, bool DMA>
-__global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
+template <typename T, int MODE, int PRO, bool GEN, bool DMA, int SUB>
+__global__ __launch_bounds__(256 * SUB, SUB == 1 ? 2 : 1) void conv_gemm_kernel(GemmParams P) {
   using C = Cfg<T>;
   constexpr int BK = C::BK, EPC = C::EPC, CPR = C::MNCPR, ES = sizeof(T);
-  constexpr int TILE_BYTES = 16384;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
+  constexpr int BM = 128 * SUB, NB = 4 / SUB;  // NB: B chunks per thread
+  constexpr int A_BYTES = 16384 * SUB, STAGE = A_BYTES + 16384;
+  // LDS-DMA ring depth: 2 for the 2-workgroups-per-CU tile, 3 (two K-tiles in
+  // flight across each barrier) for the 1-workgroup-per-CU 256-row tile
+  constexpr int NST = (DMA && SUB == 2) ? 3 : 2;
+  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -279,7 +291,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
   const int split = lin / tiles_mn;
   const int tmn = lin - split * tiles_mn;
   const int tm = tmn / P.tiles_n, tn = tmn - tm * P.tiles_n;
-  const int m0 = tm * kBM, n0 = tn * kBN;
+  const int m0 = tm * BM, n0 = tn * kBN;
 
   int64_t kbeg = 0, kend;
   if constexpr (MODE == MODE_WGRAD) {
@@ -291,14 +303,15 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
   }
   const int nk = (kend > kbeg) ? (int)((kend - kbeg + BK - 1) / BK) : 0;
 
-  // ---------------- per-thread constant addressing (chunk c = (4*wid+i)*64 + lane)
-  unsigned aoff[4], boff[4];
-  int amask[4];  // FWD/DGRAD: bit j set <=> tap j keeps the frame inside its utterance
-  int bsh[4];    // WGRAD: krow + shift of the q chunk
-  int ak[4], bk[4];  // k offset of the chunk inside the K-tile (elements / rows)
+  // ---------------- per-thread constant addressing
+  unsigned aoff[4], boff[NB];
+  int amask[4];      // FWD/DGRAD: bit j set <=> tap j keeps the frame inside its utterance
+  int bsh[NB];       // WGRAD: krow + shift of the q chunk
+  int ak[4], bk[NB];  // k offset of the chunk inside the K-tile (elements / rows)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int c = (4 * wid + i) * 64 + lane;
+    amask[i] = 0;
     if constexpr (MODE != MODE_WGRAD) {
       const int row = c >> 3, kch = (c & 7) ^ ((row >> 1) & 7);
       const int64_t n = (int64_t)m0 + row;
@@ -310,33 +323,42 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
       amask[i] = msk;
       ak[i] = kch * EPC;
       aoff[i] = (unsigned)((n * P.lda + (GEN ? 0 : kch * EPC)) * ES);
-      if constexpr (MODE == MODE_FWD) {
-        const int co = n0 + row;
-        bk[i] = kch * EPC;
-        boff[i] = co < P.Nc ? (unsigned)(((int64_t)co * P.K + kch * EPC) * ES) : kOOB;
-      } else {
-        const int krow = c / CPR;
-        const int cch = (sizeof(T) == 2) ? ((c % CPR) ^ mn_swz(krow)) : (c % CPR);
-        const int ci = n0 + cch * EPC;
-        bk[i] = krow;
-        boff[i] = ci < P.Nc ? (unsigned)(((int64_t)krow * P.ntaps * P.cdim + ci) * ES) : kOOB;
-        if constexpr (GEN) boff[i] = ci < P.Nc ? (unsigned)(ci * ES) : kOOB;
-      }
-      bsh[i] = 0;
+    } else {
+      const int sub = c >> 10, cc = c & 1023;
+      const int krow = cc / CPR;
+      const int cch = (sizeof(T) == 2) ? ((cc % CPR) ^ mn_swz(krow)) : (cc % CPR);
+      const int r = m0 + sub * 128 + cch * EPC;
+      ak[i] = krow;
+      aoff[i] = r < P.Mc ? (unsigned)(((int64_t)krow * P.lda + r) * ES) : kOOB;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int c = (NB * wid + i) * 64 + lane;
+    bsh[i] = 0;
+    if constexpr (MODE == MODE_FWD) {
+      const int row = c >> 3, kch = (c & 7) ^ ((row >> 1) & 7);
+      const int co = n0 + row;
+      bk[i] = kch * EPC;
+      boff[i] = co < P.Nc ? (unsigned)(((int64_t)co * P.K + kch * EPC) * ES) : kOOB;
+    } else if constexpr (MODE == MODE_DGRAD) {
+      const int krow = c / CPR;
+      const int cch = (sizeof(T) == 2) ? ((c % CPR) ^ mn_swz(krow)) : (c % CPR);
+      const int ci = n0 + cch * EPC;
+      bk[i] = krow;
+      boff[i] = ci < P.Nc ? (unsigned)(((int64_t)krow * P.ntaps * P.cdim + ci) * ES) : kOOB;
+      if constexpr (GEN) boff[i] = ci < P.Nc ? (unsigned)(ci * ES) : kOOB;
     } else {
       const int krow = c / CPR;
       const int cch = (sizeof(T) == 2) ? ((c % CPR) ^ mn_swz(krow)) : (c % CPR);
-      const int r = m0 + cch * EPC;
-      ak[i] = bk[i] = krow;
-      aoff[i] = r < P.Mc ? (unsigned)(((int64_t)krow * P.lda + r) * ES) : kOOB;
       const int col = n0 + cch * EPC;
       const int j = tap_of(col, P.cdim);
       const int cc = col - j * P.cdim;
       const int sh = P.sign * (j - P.pad);
+      bk[i] = krow;
       bsh[i] = krow + sh;
       // the q descriptor base sits (ntaps-1) rows before the tile so shifted offsets stay >= 0
       boff[i] = col < P.Nc ? (unsigned)(((int64_t)(krow + sh + P.ntaps - 1) * P.ldb + cc) * ES) : kOOB;
-      amask[i] = 0;
     }
   }
 
@@ -358,7 +380,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
   int ld_tap = 0, ld_c0 = 0;
 
   // Byte offsets of K-tile kt's chunks (kOOB where the im2col / edge reads zero).
-  auto tile_offsets = [&](int kt, unsigned (&oa)[4], unsigned (&ob)[4]) {
+  auto tile_offsets = [&](int kt, unsigned (&oa)[4], unsigned (&ob)[NB]) {
     const int64_t k0 = kbeg + (int64_t)kt * BK;
     if constexpr (MODE != MODE_WGRAD) {
       if constexpr (!GEN) {
@@ -373,7 +395,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
         else  // forward weight We[co][j][ci] read as rows k = (j, co), taps flipped
           ksb = (unsigned)(((int64_t)c0 * P.ntaps * P.cdim + (int64_t)(P.ntaps - 1 - tap) * P.cdim) * ES);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ob[i] = boff[i] + ksb;
+        for (int i = 0; i < NB; ++i) ob[i] = boff[i] + ksb;
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -385,10 +407,10 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
         }
         if constexpr (MODE == MODE_FWD) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) ob[i] = ((int)k0 + bk[i] < P.K) ? boff[i] + (unsigned)(k0 * ES) : kOOB;
+          for (int i = 0; i < NB; ++i) ob[i] = ((int)k0 + bk[i] < P.K) ? boff[i] + (unsigned)(k0 * ES) : kOOB;
         } else {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
+          for (int i = 0; i < NB; ++i) {
             const int k = (int)k0 + bk[i];
             const int j = tap_of(k, P.kcin);
             const int co = k - j * P.kcin;
@@ -405,50 +427,56 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         unsigned offa = aoff[i] + ksa;
+        if constexpr (GEN) {
+          if (k0 + ak[i] >= kend) offa = kOOB;
+        }
+        oa[i] = offa;
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
         int tt;
         if constexpr (!GEN) {
           tt = t0 + bsh[i];
         } else {
-          const int64_t n = k0 + ak[i];
-          if (n >= kend) offa = kOOB;
-          tt = (int)(n % P.T) + (bsh[i] - ak[i]);
+          const int64_t n = k0 + bk[i];
+          tt = (int)(n % P.T) + (bsh[i] - bk[i]);
           if (n >= kend) tt = -1;
         }
-        oa[i] = offa;
         ob[i] = (tt >= 0 && tt < P.T) ? boff[i] + ksb : kOOB;
       }
     }
   };
 
   auto dma_tile = [&](int buf, int kt) {
-    unsigned oa[4], ob[4];
+    unsigned oa[4], ob[NB];
     tile_offsets(kt, oa, ob);
-    char* la = smem + buf * 2 * TILE_BYTES + wid * 4096;
-    char* lb = la + TILE_BYTES;
+    char* la = smem + buf * STAGE + wid * 4096;
+    char* lb = smem + buf * STAGE + A_BYTES + wid * (NB * 1024);
 #pragma unroll
     for (int i = 0; i < 4; ++i) dma16(rsA, la + i * 1024, oa[i]);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dma16(rsB, lb + i * 1024, ob[i]);
+    for (int i = 0; i < NB; ++i) dma16(rsB, lb + i * 1024, ob[i]);
   };
 
-  auto load_tile = [&](int kt, uint4 (&ra)[4], uint4 (&rb)[4]) {
-    unsigned oa[4], ob[4];
+  auto load_tile = [&](int kt, uint4 (&ra)[4], uint4 (&rb)[NB]) {
+    unsigned oa[4], ob[NB];
     tile_offsets(kt, oa, ob);
 #pragma unroll
     for (int i = 0; i < 4; ++i) ra[i] = bload(rsA, oa[i]);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) rb[i] = bload(rsB, ob[i]);
+    for (int i = 0; i < NB; ++i) rb[i] = bload(rsB, ob[i]);
   };
 
   // register path: prologue applied at the store, after the load has landed
-  auto store_tile = [&](int buf, const uint4 (&ra)[4], const uint4 (&rb)[4]) {
-    char* la = smem + buf * 2 * TILE_BYTES + wid * 4096 + lane * 16;
-    char* lb = la + TILE_BYTES;
+  auto store_tile = [&](int buf, const uint4 (&ra)[4], const uint4 (&rb)[NB]) {
+    char* la = smem + buf * STAGE + wid * 4096 + lane * 16;
+    char* lb = smem + buf * STAGE + A_BYTES + wid * (NB * 1024) + lane * 16;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 4; ++i)
       *(uint4*)(la + i * 1024) = (MODE != MODE_WGRAD) ? pro_chunk<T, PRO>(ra[i], P.pro_scale) : ra[i];
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
       *(uint4*)(lb + i * 1024) = (MODE == MODE_WGRAD) ? pro_chunk<T, PRO>(rb[i], P.pro_scale) : rb[i];
-    }
   };
 
   // DMA path: the prologue is applied to fragments after ds_read
@@ -469,8 +497,11 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
   const int r32 = lane & 31, h = lane >> 5;
 
   auto compute_tile = [&](int buf) {
-    const char* la = smem + buf * 2 * TILE_BYTES;
-    const char* lb = la + TILE_BYTES;
+    const char* la = smem + buf * STAGE;
+    const char* lb = la + A_BYTES;
+    // MN-major A: this wave's 64 columns live in sub-tile wm>>1 at column (wm&1)*64
+    const char* la_sub = la + (wm >> 1) * 16384;
+    const int acol = (wm & 1) * 64;
     constexpr bool A_KMAJ = (MODE != MODE_WGRAD);
     constexpr bool B_KMAJ = (MODE == MODE_FWD);
     if constexpr (sizeof(T) == 2) {
@@ -486,23 +517,31 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
         const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         return __builtin_bit_cast(bf16x8_t, v);
       };
+      // all 16 fragments of the K-tile are read up front (64 VGPRs), so each
+      // MFMA waits only for its own operands (counted lgkmcnt), not for a
+      // drain of the LDS queue before every k-step
+      bf16x8_t af[4][2], bfr[4][2];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        bf16x8_t af[2], bfr[2];
+      for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int x = 0; x < 2; ++x) {
-          if constexpr (A_KMAJ) af[x] = *(const bf16x8_t*)(la + kmaj_off(wm * 64 + x * 32 + r32, 2 * s + h));
-          else af[x] = tr_frag(la, wm * 64 + x * 32 + (g & 1) * 16, s);
-          if constexpr (B_KMAJ) bfr[x] = *(const bf16x8_t*)(lb + kmaj_off(wn * 64 + x * 32 + r32, 2 * s + h));
-          else bfr[x] = tr_frag(lb, wn * 64 + x * 32 + (g & 1) * 16, s);
-          af[x] = pro_frag<FPRO_A>(af[x], P.pro_scale);
-          bfr[x] = pro_frag<FPRO_B>(bfr[x], P.pro_scale);
+          if constexpr (A_KMAJ) af[s][x] = *(const bf16x8_t*)(la + kmaj_off(wm * 64 + x * 32 + r32, 2 * s + h));
+          else af[s][x] = tr_frag(la_sub, acol + x * 32 + (g & 1) * 16, s);
+          if constexpr (B_KMAJ) bfr[s][x] = *(const bf16x8_t*)(lb + kmaj_off(wn * 64 + x * 32 + r32, 2 * s + h));
+          else bfr[s][x] = tr_frag(lb, wn * 64 + x * 32 + (g & 1) * 16, s);
+        }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+          af[s][x] = pro_frag<FPRO_A>(af[s][x], P.pro_scale);
+          bfr[s][x] = pro_frag<FPRO_B>(bfr[s][x], P.pro_scale);
         }
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
           for (int ni = 0; ni < 2; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[ni], af[mi], acc[mi][ni], 0, 0, 0);
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[s][ni], af[s][mi], acc[mi][ni], 0, 0, 0);
       }
     } else {
 #pragma unroll
@@ -513,9 +552,9 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
           if constexpr (A_KMAJ) {
             af[x] = *(const f32x4_t*)(la + kmaj_off(wm * 64 + x * 32 + r32, 2 * s + h));
           } else {
-            const int col = wm * 64 + x * 32 + r32;
+            const int col = acol + x * 32 + r32;
 #pragma unroll
-            for (int qq = 0; qq < 4; ++qq) af[x][qq] = *(const float*)(la + (8 * s + 4 * h + qq) * 512 + col * 4);
+            for (int qq = 0; qq < 4; ++qq) af[x][qq] = *(const float*)(la_sub + (8 * s + 4 * h + qq) * 512 + col * 4);
           }
           if constexpr (B_KMAJ) {
             bfr[x] = *(const f32x4_t*)(lb + kmaj_off(wn * 64 + x * 32 + r32, 2 * s + h));
@@ -538,7 +577,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
     }
   };
 
-  if constexpr (DMA) {
+  if constexpr (DMA && NST == 2) {
     // Tile kt+1 streams into the other buffer while tile kt is multiplied;
     // __syncthreads() waits vmcnt(0) (the DMA is a pending LDS write) and
     // orders every wave's reads of buffer kt&1 before its next refill.
@@ -553,8 +592,36 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
         __syncthreads();
       }
     }
+  } else if constexpr (DMA) {
+    // Three-buffer ring: tiles kt+1 and kt+2 are in flight while tile kt is
+    // multiplied.  A counted vmcnt (this wave's DMA pieces of one tile) retires
+    // tile kt+1 only, and a raw s_barrier (no __syncthreads: its fence would
+    // drain every DMA) publishes it and frees buffer kt%3 for tile kt+3.
+    constexpr int NP = 4 + NB;  // DMA pieces per wave per tile
+    if (nk > 0) {
+      dma_tile(0, 0);
+      if (nk > 1) {
+        dma_tile(1, 1);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NP) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      int buf = 0;
+      for (int kt = 0; kt < nk; ++kt) {
+        const int nbuf = buf == 2 ? 0 : buf + 1;
+        const int fbuf = nbuf == 2 ? 0 : nbuf + 1;  // (kt + 2) % 3
+        if (kt + 2 < nk) dma_tile(fbuf, kt + 2);
+        compute_tile(buf);
+        if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NP) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        buf = nbuf;
+      }
+    }
   } else {
-    uint4 ra0[4], rb0[4], ra1[4], rb1[4];
+    uint4 ra0[4], rb0[NB], ra1[4], rb1[NB];
     // Two register sets give every tile's loads two compute phases to land:
     // tile t is issued during tile t-2's MFMAs and written to LDS after t-1's.
     if (nk > 0) {
@@ -578,18 +645,21 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
   }
 
   // ---------------- epilogue
-  // The accumulator tile goes through LDS (one 64-row half at a time) so the
+  // The accumulator tile goes through LDS one 64-row slab at a time so the
   // epilogue reads and writes whole rows: 16 lanes x 8 consecutive columns
   // per row, every global access 16 B and each row segment contiguous.
   // Lane holds (before the transpose) output row wm*64 + mi*32 + r32 and,
   // per register group gq, columns wn*64 + ni*32 + 8*gq + 4*h + (0..3).
   constexpr int EP_LD = kBN + 4;  // floats; +4 keeps the b128 writes conflict-free
-  float* ep = (float*)smem;
+  constexpr int EROWS = 16 * SUB;  // rows per pass
+  float* ep = (float*)smem;                 // [64][EP_LD]
+  float* csr = (float*)(smem + 36864);      // COLSUM reduction [EROWS][kBN]
   const int er = tid >> 4, ec = (tid & 15) * 8;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // COLSUM accumulators
   __syncthreads();  // staging buffers are free
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    if (wm == half) {
+  for (int slab = 0; slab < 2 * SUB; ++slab) {
+    if (wm == slab) {
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -603,12 +673,12 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
     }
     __syncthreads();
 #pragma unroll
-    for (int pass = 0; pass < 4; ++pass) {
-      const int lr = pass * 16 + er;
+    for (int pass = 0; pass < 64 / EROWS; ++pass) {
+      const int lr = pass * EROWS + er;
       const f32x4_t lo = *(const f32x4_t*)(ep + lr * EP_LD + ec);
       const f32x4_t hi = *(const f32x4_t*)(ep + lr * EP_LD + ec + 4);
       float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      const int64_t row = (int64_t)m0 + half * 64 + lr;
+      const int64_t row = (int64_t)m0 + slab * 64 + lr;
       const int col = n0 + ec;
       if constexpr (MODE == MODE_WGRAD) {
         if (row < P.Mc && col < P.Nc) {  // Nc % 8 == 0
@@ -616,10 +686,34 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(GemmParams P) {
           st8<float>(out, 0, v);
         }
       } else {
-        if (row < P.n_rows && col < P.Nc) epilogue8<T>(P, row, col, v);
+        if (row < P.n_rows && col < P.Nc) {
+          epilogue8<T>(P, row, col, v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) cs[e] += v[e];
+        }
       }
     }
     __syncthreads();
+    if constexpr (MODE != MODE_WGRAD) {
+      // per-128-row-group column sums of the stored values (bias gradient of
+      // the layer this output feeds), reduced over the EROWS row lanes in LDS
+      if ((P.epi & VQX_EPI_COLSUM) && (slab & 1)) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          csr[er * kBN + ec + e] = cs[e];
+          cs[e] = 0.f;
+        }
+        __syncthreads();
+        const int64_t grp_row = (int64_t)m0 + (slab >> 1) * 128;
+        if (tid < kBN && n0 + tid < P.Nc && grp_row < P.n_rows) {
+          float t = 0.f;
+#pragma unroll
+          for (int r = 0; r < EROWS; ++r) t += csr[r * kBN + tid];
+          P.colsum_part[(grp_row / 128) * P.Nc + n0 + tid] = t;
+        }
+        __syncthreads();
+      }
+    }
   }
 }
 
@@ -639,15 +733,16 @@ static std::vector<std::pair<hipEvent_t, hipEvent_t>> g_event_pool;
 static size_t g_probe_used = 0;
 
 template <typename K>
-static void launch_gemm(K kernel, int grid, hipStream_t s, const GemmParams& P, const int info[5], double flops) {
+static void launch_gemm(K kernel, int grid, int threads, hipStream_t s, const GemmParams& P, const int info[5],
+                        double flops) {
   if (!g_probe_on) {
-    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), 0, s, P);
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(threads), 0, s, P);
     return;
   }
   if (g_probe_used == g_event_pool.size()) {
     hipEvent_t a, b;
     if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
-      hipLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), 0, s, P);
+      hipLaunchKernelGGL(kernel, dim3(grid), dim3(threads), 0, s, P);
       return;
     }
     g_event_pool.emplace_back(a, b);
@@ -659,24 +754,25 @@ static void launch_gemm(K kernel, int grid, hipStream_t s, const GemmParams& P, 
   for (int i = 0; i < 5; ++i) r.info[i] = info[i];
   r.flops = flops;
   g_probe.push_back(r);
-  hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), 0, s, ev.first, ev.second, 0, P);
+  hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(threads), 0, s, ev.first, ev.second, 0, P);
 }
 
-template <typename T, int MODE, bool GEN, bool DMA>
+template <typename T, int MODE, bool GEN, bool DMA, int SUB>
 static void launch_pro(const GemmParams& P, int grid, hipStream_t s) {
   const double flops = MODE == MODE_WGRAD ? 2.0 * (double)P.n_rows * P.Mc * P.Nc
                                           : 2.0 * (double)P.n_rows * P.Nc * P.K;
-  const int info[5] = {sizeof(T) == 2 ? VQX_BF16 : VQX_F32, MODE, P.pro, GEN ? 1 : 0, DMA ? 1 : 0};
+  const int info[5] = {sizeof(T) == 2 ? VQX_BF16 : VQX_F32, MODE, P.pro, GEN ? 1 : 0, (DMA ? 1 : 0) | (SUB == 2 ? 2 : 0)};
+  const int nt = 256 * SUB;
   switch (P.pro) {
-    case VQX_PRO_NONE: launch_gemm(conv_gemm_kernel<T, MODE, VQX_PRO_NONE, GEN, DMA>, grid, s, P, info, flops); break;
-    case VQX_PRO_LRELU: launch_gemm(conv_gemm_kernel<T, MODE, VQX_PRO_LRELU, GEN, DMA>, grid, s, P, info, flops); break;
-    case VQX_PRO_RELU: launch_gemm(conv_gemm_kernel<T, MODE, VQX_PRO_RELU, GEN, DMA>, grid, s, P, info, flops); break;
-    default: launch_gemm(conv_gemm_kernel<T, MODE, VQX_PRO_SCALE_RELU, GEN, DMA>, grid, s, P, info, flops); break;
+    case VQX_PRO_NONE: launch_gemm(conv_gemm_kernel<T, MODE, VQX_PRO_NONE, GEN, DMA, SUB>, grid, nt, s, P, info, flops); break;
+    case VQX_PRO_LRELU: launch_gemm(conv_gemm_kernel<T, MODE, VQX_PRO_LRELU, GEN, DMA, SUB>, grid, nt, s, P, info, flops); break;
+    case VQX_PRO_RELU: launch_gemm(conv_gemm_kernel<T, MODE, VQX_PRO_RELU, GEN, DMA, SUB>, grid, nt, s, P, info, flops); break;
+    default: launch_gemm(conv_gemm_kernel<T, MODE, VQX_PRO_SCALE_RELU, GEN, DMA, SUB>, grid, nt, s, P, info, flops); break;
   }
 }
 
 // Staging variant: LDS-DMA by default; VQX_GEMM_STAGING=reg selects the
-// register-staged pipeline (kept for A/B measurement).
+// register-staged pipeline (kept for A/B measurement, 128-row tiles only).
 static bool use_dma() {
   static int v = -1;
   if (v < 0) {
@@ -686,14 +782,38 @@ static bool use_dma() {
   return v == 1;
 }
 
+// Tile height: 128 rows (SUB = 1, two 4-wave workgroups per CU).  The
+// 256-row tile (SUB = 2, one 8-wave workgroup per CU, 25% fewer operand
+// bytes per FLOP) measured equal or up to 12% slower on every config-2 layer
+// (profiles/r01), so the automatic policy keeps 128; vqx_set_gemm_tile(2) /
+// VQX_GEMM_SUB=2 selects it for A/B runs.
+static int g_tile_policy = -1;  // 0 auto, 1 / 2 forced (vqx_set_gemm_tile)
+static int pick_sub(int64_t tiles256) {
+  if (g_tile_policy < 0) {
+    const char* e = getenv("VQX_GEMM_SUB");
+    g_tile_policy = (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
+  }
+  if (g_tile_policy) return g_tile_policy;
+  (void)tiles256;
+  return 1;
+}
+
 template <typename T, int MODE>
-static void launch_mode(const GemmParams& P, int grid, bool gen, hipStream_t s) {
-  if (use_dma()) {
-    if (gen) launch_pro<T, MODE, true, true>(P, grid, s);
-    else launch_pro<T, MODE, false, true>(P, grid, s);
+static void launch_mode(GemmParams& P, int64_t rows, int extra_mult, bool gen, hipStream_t s) {
+  // rows: extent of the tile-M dimension; extra_mult: split-K factor (WGRAD)
+  const int64_t t256 = ((rows + 255) / 256) * P.tiles_n * extra_mult;
+  const int sub = use_dma() ? pick_sub(t256) : 1;
+  P.tiles_m = (int)((rows + 128 * sub - 1) / (128 * sub));
+  const int grid = P.tiles_m * P.tiles_n * extra_mult;
+  if (!use_dma()) {
+    if (gen) launch_pro<T, MODE, true, false, 1>(P, grid, s);
+    else launch_pro<T, MODE, false, false, 1>(P, grid, s);
+  } else if (sub == 2) {
+    if (gen) launch_pro<T, MODE, true, true, 2>(P, grid, s);
+    else launch_pro<T, MODE, false, true, 2>(P, grid, s);
   } else {
-    if (gen) launch_pro<T, MODE, true, false>(P, grid, s);
-    else launch_pro<T, MODE, false, false>(P, grid, s);
+    if (gen) launch_pro<T, MODE, true, true, 1>(P, grid, s);
+    else launch_pro<T, MODE, false, true, 1>(P, grid, s);
   }
 }
 
@@ -721,6 +841,7 @@ static int conv_common(const vqx_conv_args* a, int mode, hipStream_t s) {
   if ((epi & VQX_EPI_SPLIT) && (!a->out2 || a->split_col % 8 || a->ldo2 % 4 || !aligned16(a->out2))) { set_error("vqx_conv: SPLIT operands"); return -1; }
   if ((epi & VQX_EPI_ACT2) && (!a->y2 || a->ldy2 % 8 || !aligned16(a->y2))) { set_error("vqx_conv: ACT2 needs a 16-B aligned y2 with ldy2 %% 8 == 0"); return -1; }
   if ((epi & (VQX_EPI_ACT | VQX_EPI_ACT2)) && a->epi_act != VQX_PRO_LRELU && a->epi_act != VQX_PRO_RELU) { set_error("vqx_conv: epi_act must be LRELU or RELU"); return -1; }
+  if ((epi & VQX_EPI_COLSUM) && !a->colsum_part) { set_error("vqx_conv: COLSUM needs colsum_part [ceil(n_rows/128)][cout]"); return -1; }
   if (!a->y || !aligned16(a->y)) { set_error("vqx_conv: y must be non-null and 16-byte aligned"); return -1; }
 
   GemmParams P = {};
@@ -732,20 +853,22 @@ static int conv_common(const vqx_conv_args* a, int mode, hipStream_t s) {
   P.ntaps = a->ntaps; P.pad = a->pad; P.sign = 1;
   P.cdim = a->cout;
   P.pro = a->prologue; P.pro_scale = a->pro_scale;
-  P.tiles_m = (int)((a->n_rows + kBM - 1) / kBM); P.tiles_n = (a->cout + kBN - 1) / kBN; P.splits = 1;
+  P.tiles_n = (a->cout + kBN - 1) / kBN; P.splits = 1;  // tiles_m: launch_mode (tile height)
   P.y = a->y; P.ldy = a->ldy; P.epi = epi; P.out_f32 = (epi & VQX_EPI_OUTF32) ? 1 : 0;
   P.bias = a->bias; P.rowbias = a->rowbias; P.res = a->res; P.ldres = a->ldres;
   P.mask = a->mask; P.ldmask = a->ldmask; P.mask_slope = a->mask_slope; P.mask_scale = a->mask_scale;
   P.gn_h = a->gn_h; P.ldgn = a->ldgn; P.gn_mr = a->gn_mean_rstd; P.gn_gamma = a->gn_gamma; P.gn_beta = a->gn_beta;
   P.out2 = a->out2; P.ldo2 = a->ldo2; P.split_col = a->split_col; P.out2_acc = a->out2_accumulate;
   P.y2 = a->y2; P.ldy2 = a->ldy2; P.epi_act = a->epi_act;
+  P.colsum_part = a->colsum_part;
   if (P.a_bytes > 0x7fffffffLL || P.b_bytes > 0x7fffffffLL) { set_error("vqx_conv: operand larger than 2 GiB"); return -1; }
   const bool gen = (a->cin % bk) != 0;
-  const int grid = P.tiles_m * P.tiles_n;
   if (a->dtype == VQX_BF16) {
-    if (mode == MODE_FWD) launch_mode<bf16_t, MODE_FWD>(P, grid, gen, s); else launch_mode<bf16_t, MODE_DGRAD>(P, grid, gen, s);
+    if (mode == MODE_FWD) launch_mode<bf16_t, MODE_FWD>(P, a->n_rows, 1, gen, s);
+    else launch_mode<bf16_t, MODE_DGRAD>(P, a->n_rows, 1, gen, s);
   } else {
-    if (mode == MODE_FWD) launch_mode<float, MODE_FWD>(P, grid, gen, s); else launch_mode<float, MODE_DGRAD>(P, grid, gen, s);
+    if (mode == MODE_FWD) launch_mode<float, MODE_FWD>(P, a->n_rows, 1, gen, s);
+    else launch_mode<float, MODE_DGRAD>(P, a->n_rows, 1, gen, s);
   }
   return launch_status(mode == MODE_FWD ? "vqx_conv1d_fwd" : "vqx_conv1d_dgrad");
 }
@@ -781,17 +904,22 @@ extern "C" int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream) {
   if (P.a_bytes > 0x7fffffffLL || P.b_bytes > 0x7fffffffLL) { set_error("vqx_conv1d_wgrad: operand larger than 2 GiB"); return -1; }
   P.Mc = a->r_dim; P.Nc = a->ntaps * a->c_dim; P.ntaps = a->ntaps; P.pad = a->pad; P.sign = a->shift_sign;
   P.cdim = a->c_dim; P.pro = a->q_prologue; P.pro_scale = a->pro_scale;
-  P.tiles_m = (P.Mc + kBM - 1) / kBM; P.tiles_n = (P.Nc + kBN - 1) / kBN; P.splits = a->splits;
+  P.tiles_n = (P.Nc + kBN - 1) / kBN; P.splits = a->splits;  // tiles_m: launch_mode
   int64_t kps = (a->n_rows + a->splits - 1) / a->splits;
   kps = (kps + BK - 1) / BK * BK;
   P.k_per_split = kps;
   P.y = a->slabs;
   const bool gen = (a->T % BK) != 0 || (a->n_rows % BK) != 0;
-  const int grid = P.tiles_m * P.tiles_n * P.splits;
   hipStream_t s = (hipStream_t)stream;
-  if (a->dtype == VQX_BF16) launch_mode<bf16_t, MODE_WGRAD>(P, grid, gen, s);
-  else launch_mode<float, MODE_WGRAD>(P, grid, gen, s);
+  if (a->dtype == VQX_BF16) launch_mode<bf16_t, MODE_WGRAD>(P, P.Mc, P.splits, gen, s);
+  else launch_mode<float, MODE_WGRAD>(P, P.Mc, P.splits, gen, s);
   return launch_status("vqx_conv1d_wgrad");
+}
+
+extern "C" int vqx_set_gemm_tile(int32_t policy) {
+  if (policy < 0 || policy > 2) { set_error("vqx_set_gemm_tile: policy %d not in {0, 1, 2}", policy); return -1; }
+  g_tile_policy = policy;
+  return 0;
 }
 
 extern "C" int vqx_probe_enable(int32_t on) {

@@ -57,6 +57,22 @@ __global__ __launch_bounds__(256) void wn_pack_kernel(const vqx_wn_layer* __rest
 // gradient is formed from LDS with coalesced reads of v.
 __global__ __launch_bounds__(256) void wn_bwd_kernel(const vqx_wn_layer* __restrict__ L, int n_layers) {
   const vqx_wn_layer& l = L[blockIdx.y];
+  if (l.kind == VQX_WN_COLREDUCE) {  // dv[c] = sum_r v[r][c]: bias / affine gradients from partials
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= l.cout) return;
+    const float* p = l.v + c;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int r = 0;
+    for (; r + 4 <= l.cin; r += 4) {
+      a0 += p[(int64_t)r * l.cout];
+      a1 += p[(int64_t)(r + 1) * l.cout];
+      a2 += p[(int64_t)(r + 2) * l.cout];
+      a3 += p[(int64_t)(r + 3) * l.cout];
+    }
+    for (; r < l.cin; ++r) a0 += p[(int64_t)r * l.cout];
+    l.dv[c] = (a0 + a1) + (a2 + a3);
+    return;
+  }
   const int rows = l.kind == 0 ? l.cout : l.cin;
   const int o = blockIdx.x;
   if (o >= rows) return;
@@ -668,6 +684,155 @@ __global__ __launch_bounds__(256) void linear_bwd_x_kernel(const float* __restri
   }
 }
 
+// Batched speaker-conditioning linears (all ResSkip blocks per launch) as
+// small LDS-tiled fp32 GEMMs: 64x64 output tiles, 256 threads x 16 outputs,
+// K in chunks of 64.  Grid z carries (layer, tile of the third dimension).
+constexpr int kLT = 64;
+
+// out_l[b][o] = sum_i c[b][i] W_l[o][i] + bias_l[o].  grid (ceil(O/64), n, ceil(B/64))
+__global__ __launch_bounds__(256) void linear_batched_fwd_kernel(const vqx_linear_layer* __restrict__ L,
+                                                                 const float* __restrict__ c, int B, int I, int O) {
+  const vqx_linear_layer& l = L[blockIdx.y];
+  const int o0 = blockIdx.x * kLT, b0 = blockIdx.z * kLT;
+  __shared__ float cs[kLT][kLT + 1];   // [b][i]
+  __shared__ __attribute__((aligned(16))) float wt[kLT][kLT + 4];  // [i][o]
+  const int t = threadIdx.x, tb = t >> 2, to = (t & 3) * 16;
+  float acc[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+  for (int i0 = 0; i0 < I; i0 += kLT) {
+    for (int e = t; e < kLT * kLT; e += 256) {
+      const int r = e >> 6, q = e & 63;  // r: b or o row, q: i column (coalesced)
+      cs[r][q] = (b0 + r < B && i0 + q < I) ? c[(int64_t)(b0 + r) * I + i0 + q] : 0.f;
+      wt[q][r] = (o0 + r < O && i0 + q < I) ? l.W[(int64_t)(o0 + r) * I + i0 + q] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int i = 0; i < kLT; ++i) {
+      const float x = cs[tb][i];
+#pragma unroll
+      for (int j = 0; j < 16; j += 4) {
+        const f32x4_t w = *(const f32x4_t*)&wt[i][to + j];
+        acc[j] = fmaf(x, w[0], acc[j]);
+        acc[j + 1] = fmaf(x, w[1], acc[j + 1]);
+        acc[j + 2] = fmaf(x, w[2], acc[j + 2]);
+        acc[j + 3] = fmaf(x, w[3], acc[j + 3]);
+      }
+    }
+    __syncthreads();
+  }
+  const int b = b0 + tb;
+  if (b >= B) return;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int o = o0 + to + j;
+    if (o < O) l.out[(int64_t)b * O + o] = acc[j] + (l.bias ? l.bias[o] : 0.f);
+  }
+}
+
+// dW_l[o][i] = sum_b dout_l[b][o] c[b][i]; dbias_l[o] = sum_b dout_l[b][o].
+// grid (ceil(O/64), n, ceil(I/64)); the i-tile-0 blocks also write dbias.
+__global__ __launch_bounds__(256) void linear_batched_bwd_w_kernel(const vqx_linear_layer* __restrict__ L,
+                                                                   const float* __restrict__ c, int B, int I, int O) {
+  const vqx_linear_layer& l = L[blockIdx.y];
+  const int o0 = blockIdx.x * kLT, i0 = blockIdx.z * kLT;
+  __shared__ float ds[kLT][kLT + 1];   // [b][o]
+  __shared__ __attribute__((aligned(16))) float cs[kLT][kLT + 4];  // [b][i]
+  const int t = threadIdx.x, to = t >> 2, ti = (t & 3) * 16;
+  float acc[16], db = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+  for (int b0 = 0; b0 < B; b0 += kLT) {
+    for (int e = t; e < kLT * kLT; e += 256) {
+      const int r = e >> 6, q = e & 63;
+      ds[r][q] = (b0 + r < B && o0 + q < O) ? l.dout[(int64_t)(b0 + r) * O + o0 + q] : 0.f;
+      cs[r][q] = (b0 + r < B && i0 + q < I) ? c[(int64_t)(b0 + r) * I + i0 + q] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int b = 0; b < kLT; ++b) {
+      const float d = ds[b][to];
+      db += d;
+#pragma unroll
+      for (int j = 0; j < 16; j += 4) {
+        const f32x4_t x = *(const f32x4_t*)&cs[b][ti + j];
+        acc[j] = fmaf(d, x[0], acc[j]);
+        acc[j + 1] = fmaf(d, x[1], acc[j + 1]);
+        acc[j + 2] = fmaf(d, x[2], acc[j + 2]);
+        acc[j + 3] = fmaf(d, x[3], acc[j + 3]);
+      }
+    }
+    __syncthreads();
+  }
+  const int o = o0 + to;
+  if (o >= O) return;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int i = i0 + ti + j;
+    if (i < I) l.dW[(int64_t)o * I + i] = acc[j];
+  }
+  if (blockIdx.z == 0 && (t & 3) == 0 && l.dbias) l.dbias[o] = db;
+}
+
+// Split-K partial of dc[b][i] = sum_l sum_o dout_l[b][o] W_l[o][i] over one
+// 64-wide o chunk of one layer.  grid (ceil(O/64), n, ceil(B/64)*ceil(I/64));
+// part[(l*nO + oc)][b][i].
+__global__ __launch_bounds__(256) void linear_batched_bwd_x_kernel(const vqx_linear_layer* __restrict__ L, int B,
+                                                                   int I, int O, float* __restrict__ part) {
+  const vqx_linear_layer& l = L[blockIdx.y];
+  const int nI = (I + kLT - 1) / kLT;
+  const int o0 = blockIdx.x * kLT, b0 = (blockIdx.z / nI) * kLT, i0 = (blockIdx.z % nI) * kLT;
+  __shared__ float ds[kLT][kLT + 1];   // [b][o]
+  __shared__ __attribute__((aligned(16))) float ws[kLT][kLT + 4];  // [o][i]
+  const int t = threadIdx.x, tb = t >> 2, ti = (t & 3) * 16;
+  for (int e = t; e < kLT * kLT; e += 256) {
+    const int r = e >> 6, q = e & 63;
+    ds[r][q] = (b0 + r < B && o0 + q < O) ? l.dout[(int64_t)(b0 + r) * O + o0 + q] : 0.f;
+    ws[r][q] = (o0 + r < O && i0 + q < I) ? l.W[(int64_t)(o0 + r) * I + i0 + q] : 0.f;
+  }
+  __syncthreads();
+  float acc[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+#pragma unroll 8
+  for (int o = 0; o < kLT; ++o) {
+    const float d = ds[tb][o];
+#pragma unroll
+    for (int j = 0; j < 16; j += 4) {
+      const f32x4_t w = *(const f32x4_t*)&ws[o][ti + j];
+      acc[j] = fmaf(d, w[0], acc[j]);
+      acc[j + 1] = fmaf(d, w[1], acc[j + 1]);
+      acc[j + 2] = fmaf(d, w[2], acc[j + 2]);
+      acc[j + 3] = fmaf(d, w[3], acc[j + 3]);
+    }
+  }
+  const int b = b0 + tb;
+  if (b >= B) return;
+  float* out = part + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * B * I;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int i = i0 + ti + j;
+    if (i < I) out[(int64_t)b * I + i] = acc[j];
+  }
+}
+
+// dc[e] = sum_p part[p][e] in a fixed order (deterministic)
+__global__ __launch_bounds__(256) void sum_slices_kernel(const float* __restrict__ part, int np, int64_t n,
+                                                         float* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int p = 0;
+  for (; p + 4 <= np; p += 4) {
+    a0 += part[(int64_t)p * n + e];
+    a1 += part[(int64_t)(p + 1) * n + e];
+    a2 += part[(int64_t)(p + 2) * n + e];
+    a3 += part[(int64_t)(p + 3) * n + e];
+  }
+  for (; p < np; ++p) a0 += part[(int64_t)p * n + e];
+  out[e] = (a0 + a1) + (a2 + a3);
+}
+
 // --------------------------------------------------------------- optimizer
 constexpr int kNormBlocks = 1024;
 
@@ -792,6 +957,13 @@ extern "C" int vqx_weight_norm_bwd(const vqx_wn_layer* lh, const vqx_wn_layer* l
   int max_rows = 1;
   for (int i = 0; i < n_layers; ++i) {
     const vqx_wn_layer& l = lh[i];
+    if (l.kind == VQX_WN_COLREDUCE) {
+      if (!l.v || !l.dv || l.cin < 1 || l.cout < 1) { set_error("vqx_weight_norm_bwd: column-reduce entry %d", i); return -1; }
+      const int blocks = (l.cout + 255) / 256;
+      max_rows = blocks > max_rows ? blocks : max_rows;
+      continue;
+    }
+    if (l.kind != 0 && l.kind != 1) { set_error("vqx_weight_norm_bwd: layer %d bad kind", i); return -1; }
     const int rows = l.kind == 0 ? l.cout : l.cin;
     const int cols = (l.kind == 0 ? l.cin : l.cout) * l.k;
     if (cols > 4096) { set_error("vqx_weight_norm_bwd: row length %d > 4096", cols); return -1; }
@@ -1011,4 +1183,29 @@ extern "C" int vqx_scale_act_2d(const void* src, int32_t ld_src, int32_t src_dty
   hipLaunchKernelGGL(scale_act_2d_kernel, dim3(grid_for(rows * cols, 256, 8192)), dim3(256), 0, (hipStream_t)stream,
                      src, ld_src, src_dtype, dst, ld_dst, dst_dtype, rows, cols, scale, act);
   return launch_status("vqx_scale_act_2d");
+}
+
+extern "C" int vqx_linear_batched_fwd(const vqx_linear_layer* table_dev, int32_t n, const float* c, int32_t B,
+                                      int32_t I, int32_t O, vqx_stream_t stream) {
+  if (!table_dev || n < 1 || !c || B < 1 || I < 1 || O < 1) { set_error("vqx_linear_batched_fwd: bad arguments"); return -1; }
+  hipLaunchKernelGGL(linear_batched_fwd_kernel, dim3((O + kLT - 1) / kLT, n, (B + kLT - 1) / kLT), dim3(256), 0,
+                     (hipStream_t)stream, table_dev, c, B, I, O);
+  return launch_status("vqx_linear_batched_fwd");
+}
+
+extern "C" int vqx_linear_batched_bwd(const vqx_linear_layer* table_dev, int32_t n, const float* c, int32_t B,
+                                      int32_t I, int32_t O, float* dc, float* partials, vqx_stream_t stream) {
+  if (!table_dev || n < 1 || !c || B < 1 || I < 1 || O < 1) { set_error("vqx_linear_batched_bwd: bad arguments"); return -1; }
+  if (dc && !partials) { set_error("vqx_linear_batched_bwd: dc needs partials [n*ceil(O/64)][B][I]"); return -1; }
+  hipStream_t s = (hipStream_t)stream;
+  const int nO = (O + kLT - 1) / kLT;
+  hipLaunchKernelGGL(linear_batched_bwd_w_kernel, dim3(nO, n, (I + kLT - 1) / kLT), dim3(256), 0, s,
+                     table_dev, c, B, I, O);
+  if (dc) {
+    hipLaunchKernelGGL(linear_batched_bwd_x_kernel, dim3(nO, n, ((B + kLT - 1) / kLT) * ((I + kLT - 1) / kLT)),
+                       dim3(256), 0, s, table_dev, B, I, O, partials);
+    const int64_t ne = (int64_t)B * I;
+    hipLaunchKernelGGL(sum_slices_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, s, partials, n * nO, ne, dc);
+  }
+  return launch_status("vqx_linear_batched_bwd");
 }

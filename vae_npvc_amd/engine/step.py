@@ -128,6 +128,20 @@ class Workspace:
         self.tmp = e(N, C)
         self.dyemb = e(B, d["ydim"], dt=F32)
         self.cs_part = e(64 * max(C, 2 * Cd, Cd + S, mel, 1024), dt=F32)
+        # bias-gradient partials: GEMM COLSUM epilogues write [row tile][C]
+        # sums of the gradient they produce; the group's weight-norm backward
+        # launch reduces them (VQX_WN_COLREDUCE entries)
+        tm = (N + L.CONV_TILE_ROWS - 1) // L.CONV_TILE_ROWS
+        self.cs_enc = [e(tm, C, dt=F32) for _ in range(2)]   # dL/dc_i (ping-pong)
+        self.cs_dec = [e(tm, Cd, dt=F32) for _ in range(2)]  # dL/dx_i (ping-pong)
+        self.cs_skip = e(tm, S, dt=F32)                      # dL/dskip
+        self.cs_f1 = e(tm, S, dt=F32)                        # dL/d(final conv 1 output)
+        # per-utterance column sums of du per decoder block: conv_in and
+        # conv_cond bias gradients, and dout of the batched conditioning backward
+        self.cs_all = e(nd, B, 2 * Cd, dt=F32)
+        O = 2 * Cd
+        self.lin_part = e(nd * ((O + 63) // 64) * B * d["ydim"], dt=F32)  # split-K partials of d(embedding)
+        eng._build_bwd_tables(self)
 
 
 class VQVAEEngine:
@@ -231,14 +245,13 @@ class VQVAEEngine:
                 Lr.slab = self.arena[off:off + n].view(Lr.splits, Lr.rows, Lr.cols)
                 off += n
         self.wn_fwd_table = ops.wn_table([self._wn_entry(Lr, bwd=False) for Lr in self.convs])
-        self.wn_bwd_tables = {id(grp[0]): ops.wn_table([self._wn_entry(Lr, bwd=True) for Lr in grp]) for grp in groups}
         self.groups = groups
 
     def _bwd_groups(self):
         ns, nd = self.dims["ns"], self.dims["nd"]
         gr = [[self.fin1, self.fin2]]
-        gr += [[self.dec_in[i], self.dec_cond[i], self.dec_rs[i]] for i in range(nd)]
-        gr += [[self.dec0], [self.enc_out]]
+        gr += [[self.dec_in[i], self.dec_rs[i]] for i in range(nd)]
+        gr += [list(self.dec_cond), [self.dec0], [self.enc_out]]
         gr += [[self.enc_k3[i], self.enc_sk[i]] for i in range(ns)]
         gr += [[self.enc0]]
         return gr
@@ -256,7 +269,45 @@ class VQVAEEngine:
     def refresh_tables(self):
         """Rebuild descriptor tables (after remove_weight_norm or a re-flatten)."""
         self.wn_fwd_table = ops.wn_table([self._wn_entry(Lr, bwd=False) for Lr in self.convs])
-        self.wn_bwd_tables = {id(g[0]): ops.wn_table([self._wn_entry(Lr, bwd=True) for Lr in g]) for g in self.groups}
+        for (_, _, train), w in self._ws.items():
+            if train:
+                self._build_bwd_tables(w)
+
+    def _build_bwd_tables(self, w):
+        """Per-workspace backward tables: each group's weight-norm backward plus
+        the column reductions of the bias / GroupNorm-affine partials that are
+        final when the group's GEMMs are done (one launch per group)."""
+        ns, nd, B = self.dims["ns"], self.dims["nd"], w.B
+        C, Cd, S = self.dims["C"], self.dims["Cd"], self.dims["S"]
+        g = self.g
+        cr = ops.colreduce_entry
+        cs_enc_b = self._bview(w.colsum_b, B, C)
+        dg_enc_b, db_enc_b = self._bview(w.dgam_b, B, C), self._bview(w.dbet_b, B, C)
+        dg_dec_b, db_dec_b = self._bview(w.dgam_b, B, 2 * Cd), self._bview(w.dbet_b, B, 2 * Cd)
+        t = {}
+        f1 = self.fin1
+        t["fin"] = [self._wn_entry(f1, True), self._wn_entry(self.fin2, True),
+                    cr(w.cs_f1, g(f1.mod.bias))]
+        for i in range(nd):
+            ci, rs, gn, cond = self.dec_in[i], self.dec_rs[i], self.dec_gn[i], self.dec_cond[i]
+            rb = g(rs.mod.bias)
+            t[("dec", i)] = [self._wn_entry(ci, True), self._wn_entry(rs, True),
+                             cr(w.cs_dec[(nd - 1 - i) % 2], rb[:Cd]), cr(w.cs_skip, rb[Cd:]),
+                             cr(w.cs_all[i], g(ci.mod.bias)), cr(dg_dec_b, g(gn.weight)), cr(db_dec_b, g(gn.bias))]
+        t["cond"] = [self._wn_entry(Lr, True) for Lr in self.dec_cond]
+        t["dec0"] = [self._wn_entry(self.dec0, True), cr(w.cs_dec[nd % 2], g(self.dec0.mod.bias))]
+        t["enc_out"] = [self._wn_entry(self.enc_out, True)]
+        for i in range(ns):
+            k3, sk, gn = self.enc_k3[i], self.enc_sk[i], self.enc_gn[i]
+            t[("enc", i)] = [self._wn_entry(k3, True), self._wn_entry(sk, True),
+                             cr(w.cs_enc[(ns - 1 - i) % 2], g(sk.mod.bias)),
+                             cr(cs_enc_b, g(k3.mod.bias)), cr(dg_enc_b, g(gn.weight)), cr(db_enc_b, g(gn.bias))]
+        t["enc0"] = [self._wn_entry(self.enc0, True), cr(w.cs_enc[ns % 2], g(self.enc0.mod.bias))]
+        w.bwd_tables = {k: ops.wn_table(v) for k, v in t.items()}
+        # all ResSkip blocks' conditioning linears, forward and backward, one table
+        w.cond_table = ops.linear_table([dict(W=Lr.wp, bias=Lr.mod.bias, out=w.condbias[i], dout=w.cs_all[i],
+                                              dW=Lr.slab.view(Lr.rows, Lr.cols), dbias=g(Lr.mod.bias))
+                                         for i, Lr in enumerate(self.dec_cond)])
 
     def ws(self, B, T, train=True):
         key = (B, T, train)
@@ -292,8 +343,12 @@ class VQVAEEngine:
 
     def embed_and_cond(self, w, y):
         ops.embedding_fwd(self.m.embeds._embedding.weight, y.reshape(-1), w.yemb)
-        for i, Lr in enumerate(self.dec_cond):
-            ops.linear_f32(w.yemb, Lr.wp, Lr.mod.bias, w.condbias[i])
+        if getattr(w, "cond_table", None) is not None:
+            Lr = self.dec_cond[0]
+            ops.linear_batched_fwd(w.cond_table, w.yemb, w.B, Lr.cin, Lr.cout)
+        else:
+            for i, Lr in enumerate(self.dec_cond):
+                ops.linear_f32(w.yemb, Lr.wp, Lr.mod.bias, w.condbias[i])
 
     def encoder_fwd(self, w, x_nct):
         T = w.T
@@ -380,73 +435,70 @@ class VQVAEEngine:
         B = w.B
         ops.vq_commit_bwd(w.z, w.zq, 2.0 * self.m.beta * grad_scale / N, w.dz)
         eo = self.enc_out
+        tb = w.bwd_tables
         self.bias_grad(eo, w.dz, w)
         self.wgrad(eo, w.dz, w.a[ns], T)
         cur = w.dc[0]
-        self.dgrad(eo, w.dz, cur, T, mask=w.a[ns], mask_slope=0.2)
-        ops.weight_norm_bwd(self.wn_bwd_tables[id(eo)])
+        # every dL/dc_i producer also writes its bias-gradient partials (COLSUM)
+        self.dgrad(eo, w.dz, cur, T, mask=w.a[ns], mask_slope=0.2, colsum=w.cs_enc[0])
+        ops.weight_norm_bwd(tb["enc_out"])
         cs_b, dg_b, db_b = (self._bview(t, B, C) for t in (w.colsum_b, w.dgam_b, w.dbet_b))
         for i in reversed(range(ns)):
             k3, sk, gn = self.enc_k3[i], self.enc_sk[i], self.enc_gn[i]
-            nxt = w.dc[(ns - i) % 2]
+            j = (ns - i) % 2
+            nxt = w.dc[j]
             # cur = dL/dc_{i+1}, the gradient w.r.t. block i's output GN(h_i) + skip(c_i)
-            self.bias_grad(sk, cur, w)
             self.wgrad(sk, cur, w.c[i], T)
             ops.gn_bwd(cur, w.h[i], w.dh, T, 1, False, w.enc_mr[i], gn.weight, gn.bias, w.gnb_part, cs_b, dg_b, db_b)
-            ops.colsum(cs_b, w.cs_part, self.g(k3.mod.bias))
-            ops.colsum(dg_b, w.cs_part, self.g(gn.weight))
-            ops.colsum(db_b, w.cs_part, self.g(gn.bias))
             self.wgrad(k3, w.dh, w.a[i], T)
             self.dgrad(k3, w.dh, w.tmp, T, mask=w.a[i], mask_slope=0.2)
-            self.dgrad(sk, cur, nxt, T, res=w.tmp)
-            ops.weight_norm_bwd(self.wn_bwd_tables[id(k3)])
+            self.dgrad(sk, cur, nxt, T, res=w.tmp, colsum=w.cs_enc[j])
+            # weight norms of k3/sk + biases of sk (cur partials), k3 and the GN affine
+            ops.weight_norm_bwd(tb[("enc", i)])
             cur = nxt
         # cur = dL/dc_0 (conv0 output); conv0's input (the mel batch) needs no gradient
-        self.bias_grad(self.enc0, cur, w)
         self.wgrad(self.enc0, cur, w.x, T)
-        ops.weight_norm_bwd(self.wn_bwd_tables[id(self.enc0)])
+        ops.weight_norm_bwd(tb["enc0"])
 
     def decoder_bwd(self, w):
         T, nd, Cd, B = w.T, self.dims["nd"], self.dims["Cd"], w.B
         f1, f2 = self.fin1, self.fin2
         dxhat = w.dxhat
+        tb = w.bwd_tables
         self.bias_grad(f2, dxhat, w)
         self.wgrad(f2, dxhat, w.f1, T)
-        self.dgrad(f2, dxhat, w.df1, T, mask=w.f1, mask_slope=0.0)
+        self.dgrad(f2, dxhat, w.df1, T, mask=w.f1, mask_slope=0.0, colsum=w.cs_f1)
         s = math.sqrt(1.0 / (nd + 1))
-        self.bias_grad(f1, w.df1, w)
         self.wgrad(f1, w.df1, w.a_skip, T)
         cur, nxt = w.dr[0], w.dr[1]
         # dL/dskip (identical for every block) -> tail columns of both [dx | dskip] buffers
-        self.dgrad(f1, w.df1, cur[:, Cd:], T, mask=w.a_skip, mask_slope=0.0, mask_scale=s)
+        self.dgrad(f1, w.df1, cur[:, Cd:], T, mask=w.a_skip, mask_slope=0.0, mask_scale=s, colsum=w.cs_skip)
         ops.convert_2d(cur[:, Cd:], nxt[:, Cd:])
         ops.convert_2d(None, cur, cols=Cd)  # dL/dx_{nd+1} = 0: the last residual output is unused
-        ops.weight_norm_bwd(self.wn_bwd_tables[id(f1)])
-        ops.zero_(w.dyemb)
+        ops.zero_(w.cs_dec[0])  # ... and so are its bias-gradient partials (read by block nd-1)
+        ops.weight_norm_bwd(tb["fin"])
         C2 = 2 * Cd
-        cs_b, dg_b, db_b = (self._bview(t, B, C2) for t in (w.colsum_b, w.dgam_b, w.dbet_b))
+        dg_b, db_b = (self._bview(t, B, C2) for t in (w.dgam_b, w.dbet_b))
         for i in reversed(range(nd)):
-            ci, cond, gn, rs = self.dec_in[i], self.dec_cond[i], self.dec_gn[i], self.dec_rs[i]
+            ci, gn, rs = self.dec_in[i], self.dec_gn[i], self.dec_rs[i]
+            j = (nd - 1 - i) % 2
             # cur = [dL/dx_{i+1} | dL/dskip]
-            self.bias_grad(rs, cur, w)
             self.wgrad(rs, cur, w.g[i], T)
             self.dgrad(rs, cur, w.dg, T)
-            ops.gn_bwd(w.dg, w.u[i], w.du, T, 2, True, w.dec_mr[i], gn.weight, gn.bias, w.gnb_part, cs_b, dg_b,
-                       db_b)
-            ops.colsum(cs_b, w.cs_part, self.g(ci.mod.bias))
-            ops.colsum(cs_b, w.cs_part, self.g(cond.mod.bias))
-            ops.colsum(dg_b, w.cs_part, self.g(gn.weight))
-            ops.colsum(db_b, w.cs_part, self.g(gn.bias))
-            ops.zero_(cond.slab)
-            ops.linear_bwd_f32(cs_b, w.yemb, cond.wp, dW=cond.slab.view(cond.rows, cond.cols), dc=w.dyemb)
+            ops.gn_bwd(w.dg, w.u[i], w.du, T, 2, True, w.dec_mr[i], gn.weight, gn.bias, w.gnb_part, w.cs_all[i],
+                       dg_b, db_b)
             self.wgrad(ci, w.du, w.xs[i], T)
-            self.dgrad(ci, w.du, nxt[:, :Cd], T, res=cur[:, :Cd])
-            ops.weight_norm_bwd(self.wn_bwd_tables[id(ci)])
+            self.dgrad(ci, w.du, nxt[:, :Cd], T, res=cur[:, :Cd], colsum=w.cs_dec[1 - j])
+            # weight norms of conv_in/res_skip + biases of res_skip, conv_in and the GN affine
+            ops.weight_norm_bwd(tb[("dec", i)])
             cur, nxt = nxt, cur
+        # speaker conditioning of all blocks at once: dW, bias and d(embedding)
+        cond = self.dec_cond[0]
+        ops.linear_batched_bwd(w.cond_table, w.yemb, B, cond.cin, cond.cout, w.dyemb, w.lin_part)
+        ops.weight_norm_bwd(tb["cond"])
         dx1 = cur[:, :Cd]  # dL/dx_1, the ConvT0 output; z_vq itself receives no gradient
-        self.bias_grad(self.dec0, dx1, w)
         self.wgrad(self.dec0, dx1, w.zq_in, T)
-        ops.weight_norm_bwd(self.wn_bwd_tables[id(self.dec0)])
+        ops.weight_norm_bwd(tb["dec0"])
         emb_g = self.g(self.m.embeds._embedding.weight)
         ops.zero_(emb_g)
         ops.embedding_bwd(w.dyemb, w.y_dev, emb_g)

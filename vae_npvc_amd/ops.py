@@ -32,7 +32,7 @@ def _check_cuda(*ts):
 def conv_args(x, w, y, *, T, cin, cout, ntaps, pad, prologue=L.PRO_NONE, pro_scale=1.0, bias=None,
               rowbias=None, res=None, mask=None, mask_slope=0.0, mask_scale=1.0, gn_h=None, gn_mr=None,
               gn_gamma=None, gn_beta=None, out2=None, split_col=0, out2_accumulate=False, out_f32=False,
-              act=None, y2=None):
+              act=None, y2=None, colsum=None):
     epi = 0
     if bias is not None:
         epi |= L.EPI_BIAS
@@ -52,6 +52,8 @@ def conv_args(x, w, y, *, T, cin, cout, ntaps, pad, prologue=L.PRO_NONE, pro_sca
         epi |= L.EPI_ACT
     if y2 is not None:
         epi |= L.EPI_ACT2
+    if colsum is not None:
+        epi |= L.EPI_COLSUM
     a = L.ConvArgs()
     a.x, a.w, a.y = ptr(x), ptr(w), ptr(y)
     a.bias, a.rowbias, a.res, a.mask = ptr(bias), ptr(rowbias), ptr(res), ptr(mask)
@@ -68,6 +70,7 @@ def conv_args(x, w, y, *, T, cin, cout, ntaps, pad, prologue=L.PRO_NONE, pro_sca
     a.pro_scale, a.mask_slope, a.mask_scale = pro_scale, mask_slope, mask_scale
     a.y2, a.ldy2 = ptr(y2), (y2.stride(0) if y2 is not None else 0)
     a.epi_act = act if act is not None else 0
+    a.colsum_part = ptr(colsum)
     return a
 
 
@@ -99,9 +102,9 @@ class LaunchProbe:
         out = []
         for i in range(n.value):
             call("vqx_probe_read", i, info, ctypes.byref(fl), ctypes.byref(ms))
-            dt, mode, pro, gen, dma = list(info)
+            dt, mode, pro, gen, stg = list(info)  # stg: bit 0 LDS-DMA staging, bit 1 256-row tile
             sym = (f"vqx::conv_gemm_kernel<{self._DT[dt]}, {mode}, {pro}, {'true' if gen else 'false'}, "
-                   f"{'true' if dma else 'false'}>")
+                   f"{'true' if stg & 1 else 'false'}, {2 if stg & 2 else 1}>")
             out.append((sym, fl.value, ms.value * 1e-3, self.shapes[i] if i < len(self.shapes) else ""))
         return out
 
@@ -180,6 +183,35 @@ def wn_table(layers):
     raw = bytes(arr)
     dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to("cuda")
     return arr, dev
+
+
+def colreduce_entry(src, dst):
+    """VQX_WN_COLREDUCE table entry: dst[c] = sum_r src[r][c] (src contiguous f32 [R][C])."""
+    R, C = src.shape
+    return dict(kind=L.WN_COLREDUCE, v=src, dv=dst, cin=R, cout=C, k=1, dtype=L.VQX_F32, splits=1)
+
+
+def linear_table(layers):
+    """Device table of vqx_linear_layer (host ctypes copy kept alive alongside)."""
+    arr = (L.LinearLayer * len(layers))()
+    for i, d in enumerate(layers):
+        for k in ("W", "bias", "out", "dout", "dW", "dbias"):
+            setattr(arr[i], k, ptr(d.get(k)))
+    dev = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to("cuda")
+    return arr, dev
+
+
+def linear_batched_fwd(table, c, B, I, O):
+    arr, dev = table
+    call("vqx_linear_batched_fwd", dev.data_ptr(), len(arr), ptr(c), B, I, O, stream_ptr())
+
+
+def linear_batched_bwd(table, c, B, I, O, dc, partials=None):
+    """partials: f32 workspace of >= len(table) * ceil(O/64) * B * I (allocated if None)."""
+    arr, dev = table
+    if dc is not None and partials is None:
+        partials = torch.empty(len(arr) * ((O + 63) // 64) * B * I, device=c.device, dtype=torch.float32)
+    call("vqx_linear_batched_bwd", dev.data_ptr(), len(arr), ptr(c), B, I, O, ptr(dc), ptr(partials), stream_ptr())
 
 
 def weight_norm_fwd(table):
