@@ -21,6 +21,8 @@ SHAPES = {  # name: (mode, cin, cout, k, prologue)
     "enc_k3_dgrad": ("dgrad", 512, 512, 3, L.PRO_NONE),
     "dec_in_wgrad": ("wgrad", 512, 1024, 3, L.PRO_NONE),
     "enc_k3_wgrad": ("wgrad", 512, 512, 3, L.PRO_NONE),
+    "dec_rs_wgrad": ("wgrad", 512, 640, 1, L.PRO_NONE),
+    "enc_sk_wgrad": ("wgrad", 512, 512, 1, L.PRO_NONE),
     "fin1_fwd": ("fwd", 80, 80, 1, L.PRO_NONE),
     "enc0_fwd": ("fwd", 80, 512, 3, L.PRO_NONE),
 }
@@ -33,21 +35,28 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--splits", type=int, default=8)
     ap.add_argument("--rotate", type=int, default=1, help="cycle through R operand sets (R*~50 MB > MALL = cold)")
+    ap.add_argument("--sweep-splits", default=None, help="comma list: time every wgrad shape at each split count")
     a = ap.parse_args()
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     B, T = 64, 256
     N = B * T
     dev = "cuda"
+    jobs = []
     for name, (mode, cin, cout, k, pro) in SHAPES.items():
         if a.only and a.only not in name:
             continue
+        if a.sweep_splits and mode == "wgrad":
+            jobs += [(f"{name} s{sp}", mode, cin, cout, k, pro, int(sp)) for sp in a.sweep_splits.split(",")]
+        elif not a.sweep_splits:
+            jobs.append((name, mode, cin, cout, k, pro, a.splits))
+    for name, mode, cin, cout, k, pro, splits in jobs:
         R = a.rotate
         xs = [torch.randn(N, cin, device=dev).to(dt) for _ in range(R)]
         dys = [torch.randn(N, cout, device=dev).to(dt) for _ in range(R)]
         w = (torch.randn(cout, k * cin, device=dev) / (k * cin) ** 0.5).to(dt)
         ys = [torch.empty(N, cout, device=dev, dtype=dt) for _ in range(R)]
         dxs = [torch.empty(N, cin, device=dev, dtype=dt) for _ in range(R)]
-        slabs = torch.empty(a.splits, cout, k * cin, device=dev)
+        slabs = torch.empty(splits, cout, k * cin, device=dev)
         bias = torch.zeros(cout, device=dev)
 
         def fn(i):
@@ -58,7 +67,7 @@ def main():
                 ops.conv_dgrad(dy, w, dx, T=T, cin=cout, cout=cin, ntaps=k, pad=(k - 1) // 2)
             else:
                 ops.conv_wgrad(dy, x, slabs, T=T, r_dim=cout, c_dim=cin, ntaps=k, pad=(k - 1) // 2,
-                               q_prologue=pro, splits=a.splits)
+                               q_prologue=pro, splits=splits)
         for i in range(3):
             fn(i)
         torch.cuda.synchronize()

@@ -39,13 +39,6 @@ from .. import ops
 F32 = torch.float32
 
 
-def _pow2_floor(x):
-    p = 1
-    while p * 2 <= x:
-        p *= 2
-    return p
-
-
 @dataclass
 class ConvLayer:
     mod: object          # WNConv1d
@@ -223,9 +216,11 @@ class VQVAEEngine:
         self.fin2 = mk(dec.final_layer[3], "decoder.final_layer.3")
         self.convs = ([self.enc0] + [x for pair in zip(self.enc_k3, self.enc_sk) for x in pair] + [self.enc_out, self.dec0]
                       + [x for tr in zip(self.dec_in, self.dec_cond, self.dec_rs) for x in tr] + [self.fin1, self.fin2])
-        # split-K factors for the wgrad GEMMs: ~512 workgroups (2 per CU) at
-        # config 2 (64 x 256 frames), at least 4 K-tiles (256 frames) per
-        # split; every split costs a slab write + read of rows x cols fp32
+        # split-K factors for the wgrad GEMMs: one full round of ~480-512
+        # workgroups (2 per CU) at config 2 (64 x 256 frames), at least 4
+        # K-tiles (256 frames) per split.  Measured sweep (tools/gemm_bench.py
+        # --sweep-splits): dec_in best at 5, enc k3 at 10, res/skip at 24,
+        # enc skip at 32 -- exactly floor(512 / tiles).
         N_ref = 64 * 256
         for Lr in self.convs:
             if Lr in self.dec_cond:
@@ -233,7 +228,7 @@ class VQVAEEngine:
                 continue
             r, c = (Lr.cin, Lr.k * Lr.cout) if Lr.kind else (Lr.cout, Lr.k * Lr.cin)
             tiles = math.ceil(r / 128) * math.ceil(c / 128)
-            Lr.splits = max(1, min(_pow2_floor(max(1, 512 // tiles)), N_ref // 256))
+            Lr.splits = max(1, min(512 // tiles, N_ref // 256))
         # slab arena: one backward group's slabs at a time (kept L2/MALL-resident)
         groups = self._bwd_groups()
         arena = max(sum(Lr.splits * Lr.rows * Lr.cols for Lr in grp) for grp in groups)
