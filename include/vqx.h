@@ -54,10 +54,20 @@ enum {
   VQX_EPI_ACT2 = 1 << 8,    /* also y2[n][c] = act(v) (dtype): the producer writes
                                the pre-activated copy its consumers read, so no
                                GEMM applies an activation while staging        */
-  VQX_EPI_COLSUM = 1 << 9   /* colsum_part[tile][c] = sum over the 128-frame row
+  VQX_EPI_COLSUM = 1 << 9,  /* colsum_part[tile][c] = sum over the 128-frame row
                                tile of the stored fp32 value (before rounding):
                                the bias gradient of the layer y feeds, reduced
                                later by a VQX_WN_COLREDUCE table entry          */
+  VQX_EPI_GNSTATS = 1 << 10, /* y is a GroupNorm input: stat_part[g128][tn][4] =
+                               (count, mean, M2, 0) of the stored fp32 values of
+                               each 128-frame x 128-channel tile; combined by
+                               vqx_gn_finalize_tiles.  Needs T % 128 == 0 and
+                               cout/gn_groups % 128 == 0                        */
+  VQX_EPI_GNBWD = 1 << 11   /* y is the gradient dy of a GroupNorm output (GLU-
+                               gated when gn_glu): stat_part[g128][tn][4] = per
+                               tile (sum g*dh, sum g*dh*xhat) for group a (and b)
+                               with u = gn_h [N][ldgn], the forward mean/rstd,
+                               gamma, beta; consumed by vqx_gn_bwd(nparts > 0)  */
 };
 #define VQX_CONV_TILE_ROWS 128   /* frames per GEMM row tile (COLSUM partial rows) */
 
@@ -98,6 +108,8 @@ typedef struct vqx_conv_args {
   void* y2;                  /* ACT2 destination [N][ldy2]                     */
   int32_t ldy2, epi_act;
   float* colsum_part;        /* COLSUM destination [ceil(N/128)][cout]         */
+  float* stat_part;          /* GNSTATS / GNBWD destination [N/128][ceil(cout/128)][4] */
+  int32_t gn_groups, gn_glu;
 } vqx_conv_args;
 
 int vqx_conv1d_fwd(const vqx_conv_args* a, vqx_stream_t stream);
@@ -186,8 +198,16 @@ int vqx_gn_glu_fwd(const void* u, int32_t ldu, void* g, int32_t ldg, int32_t dty
 int vqx_gn_bwd(const void* dy, int32_t lddy, const void* u, int32_t ldu, void* du, int32_t lddu,
                int32_t dtype, int64_t n_rows, int32_t T, int32_t C, int32_t G, int32_t glu,
                const float* mean_rstd, const float* gamma, const float* beta,
-               float* partials /* >= B*64*G */, float* colsum_b /* [B][C] */,
-               float* dgamma_b /* [B][C] */, float* dbeta_b /* [B][C] */, vqx_stream_t stream);
+               float* partials /* nparts == 0: workspace >= B*64*G */,
+               int32_t nparts /* 0: reduce here; > 0: partials hold the producing GEMM's
+                                 VQX_EPI_GNBWD tiles, nparts per utterance */,
+               float* colsum_b /* [B][C] */, float* dgamma_b /* [B][C] */, float* dbeta_b /* [B][C] */,
+               vqx_stream_t stream);
+
+/* GroupNorm statistics from a GEMM's VQX_EPI_GNSTATS tiles (see there):
+ * mean_rstd[B][G][2], combined per (utterance, group) in double. */
+int vqx_gn_finalize_tiles(const float* parts, int64_t n_rows, int32_t T, int32_t C, int32_t G, float eps,
+                          float* mean_rstd, vqx_stream_t stream);
 
 /*
  * Sum over rows: out[c] (+)= sum_n x[n][c] (f32 accumulation, deterministic
@@ -348,7 +368,7 @@ int vqx_probe_count(int64_t* n);
 int vqx_probe_read(int64_t i, int32_t* info5, double* flops, float* ms);
 
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
-#define VQX_ABI_VERSION 105
+#define VQX_ABI_VERSION 106
 int vqx_version(void);
 
 #ifdef __cplusplus

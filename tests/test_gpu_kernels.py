@@ -257,3 +257,63 @@ def test_linear_batched_and_colreduce():
     assert relerr(dc, want_dc) < 1e-6
     assert relerr(dst, src.double().sum(0)) < 1e-6
     assert L.WN_COLREDUCE == 2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("G,cout", [(1, 512), (2, 1024)])
+def test_gnstats_epilogue_matches_standalone(dtype, G, cout, tile):
+    """GEMM-epilogue GroupNorm statistics (tiles + finalize) = the standalone
+    two-pass statistics kernel (nn.GroupNorm, layers.py:154,201)."""
+    ops = _ops()
+    torch.manual_seed(7)
+    B, T, cin = 3, 256, 512
+    x = torch.randn(B * T, cin, device=DEV).to(dtype)
+    w = (torch.randn(cout, 3 * cin, device=DEV) / (3 * cin) ** 0.5).to(dtype)
+    bias = torch.randn(cout, device=DEV)
+    y = torch.empty(B * T, cout, device=DEV, dtype=dtype)
+    tiles = torch.empty(B * T // 128 * (cout // 128) * 4, device=DEV)
+    mr_fused = torch.empty(B, G, 2, device=DEV)
+    ops.conv_fwd(x, w, y, T=T, cin=cin, cout=cout, ntaps=3, pad=1, bias=bias, gn_stats=tiles, gn_groups=G)
+    ops.gn_finalize_tiles(tiles, B * T, T, cout, G, mr_fused)
+    mr_ref = torch.empty(B, G, 2, device=DEV)
+    ops.groupnorm_stats(y, T, G, torch.empty(B * G * 24, device=DEV), mr_ref)
+    yy = y.double().view(B, T, G, cout // G)
+    mean = yy.mean(dim=(1, 3))
+    rstd = 1.0 / torch.sqrt(yy.var(dim=(1, 3), unbiased=False) + 1e-5)
+    torch.cuda.synchronize()
+    # fused stats come from the fp32 values before rounding to `dtype`
+    tol = 1e-5 if dtype == torch.float32 else 5e-3
+    assert relerr(mr_fused[..., 0], mean) < tol and relerr(mr_fused[..., 1], rstd) < tol
+    assert relerr(mr_fused, mr_ref) < tol
+
+
+@pytest.mark.parametrize("glu", [False, True])
+def test_gnbwd_epilogue_matches_standalone(glu, tile):
+    """GEMM-epilogue GroupNorm-backward sums feeding vqx_gn_bwd(nparts>0) give
+    the same du / per-utterance sums as the standalone two-pass backward."""
+    ops = _ops()
+    torch.manual_seed(8)
+    dt = torch.bfloat16
+    B, T, cin = 2, 256, 512
+    C = 1024 if glu else 512           # GN channels
+    cout = C // 2 if glu else C        # dgrad output = dL/d(GN output) (or dL/dg for GLU)
+    G = 2 if glu else 1
+    dy = torch.randn(B * T, cin, device=DEV).to(dt)
+    w = (torch.randn(cin, cout, device=DEV) / cout ** 0.5).to(dt)   # 1x1 conv cout->cin, dgrad gives [N, cout]
+    u = torch.randn(B * T, C, device=DEV).to(dt)
+    mr = torch.empty(B, G, 2, device=DEV)
+    ops.groupnorm_stats(u, T, G, torch.empty(B * G * 24, device=DEV), mr)
+    gamma, beta = torch.randn(C, device=DEV), torch.randn(C, device=DEV)
+    g_out = torch.empty(B * T, cout, device=DEV, dtype=dt)
+    parts = torch.empty(B * T // 128 * (cout // 128) * 4, device=DEV)
+    ops.conv_dgrad(dy, w, g_out, T=T, cin=cin, cout=cout, ntaps=1, pad=0, gn_bwd=parts, gn_h=u, gn_mr=mr,
+                   gn_gamma=gamma, gn_beta=beta, gn_groups=G, gn_glu=glu)
+    outs = []
+    for nparts, pt in ((0, torch.empty(B * 64 * 2, device=DEV)), ((T // 128) * (cout // 128), parts)):
+        du = torch.empty(B * T, C, device=DEV, dtype=dt)
+        cs, dgm, dbt = (torch.empty(B, C, device=DEV) for _ in range(3))
+        ops.gn_bwd(g_out, u, du, T, G, glu, mr, gamma, beta, pt, cs, dgm, dbt, nparts=nparts)
+        outs.append((du, cs, dgm, dbt))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert relerr(a, b) < 2e-2, relerr(a, b)

@@ -15,12 +15,12 @@ from pathlib import Path
 import torch  # noqa: F401  (loads the HIP runtime first; see module docstring)
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libvqx.so"
-ABI_VERSION = 105  # include/vqx.h VQX_ABI_VERSION
+ABI_VERSION = 106  # include/vqx.h VQX_ABI_VERSION
 
 VQX_F32, VQX_BF16 = 0, 1
 PRO_NONE, PRO_LRELU, PRO_RELU, PRO_SCALE_RELU = 0, 1, 2, 3
-EPI_BIAS, EPI_ROWBIAS, EPI_MASK, EPI_RES, EPI_GNADD, EPI_SPLIT, EPI_OUTF32, EPI_ACT, EPI_ACT2, EPI_COLSUM = (
-    1 << i for i in range(10))
+(EPI_BIAS, EPI_ROWBIAS, EPI_MASK, EPI_RES, EPI_GNADD, EPI_SPLIT, EPI_OUTF32, EPI_ACT, EPI_ACT2, EPI_COLSUM, EPI_GNSTATS,
+ EPI_GNBWD) = (1 << i for i in range(12))
 CONV_TILE_ROWS = 128
 
 c_void_p, c_int32, c_int64, c_float, c_double = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
@@ -38,6 +38,7 @@ class ConvArgs(ctypes.Structure):
         ("epilogue", c_int32), ("split_col", c_int32), ("out2_accumulate", c_int32),
         ("pro_scale", c_float), ("mask_slope", c_float), ("mask_scale", c_float),
         ("y2", c_void_p), ("ldy2", c_int32), ("epi_act", c_int32), ("colsum_part", c_void_p),
+        ("stat_part", c_void_p), ("gn_groups", c_int32), ("gn_glu", c_int32),
     ]
 
 
@@ -77,8 +78,9 @@ _SIGS = {
     "vqx_gn_glu_fwd": [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int64, c_int32, c_int32, c_void_p,
                        c_void_p, c_void_p, c_void_p],
     "vqx_gn_bwd": [c_void_p, c_int32, c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int64, c_int32, c_int32,
-                   c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                   c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p,
                    c_void_p],
+    "vqx_gn_finalize_tiles": [c_void_p, c_int64, c_int32, c_int32, c_int32, c_float, c_void_p, c_void_p],
     "vqx_colsum": [c_void_p, c_int32, c_int32, c_int64, c_int32, c_void_p, c_void_p, c_int32, c_void_p],
     "vqx_nct_to_ntc": [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_int32, c_int32, c_void_p],
     "vqx_ntc_to_nct": [c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p],

@@ -40,6 +40,20 @@ __device__ __forceinline__ void st_dt(void* p, int64_t i, float v, int dt) {
   if (dt == VQX_BF16) ((bf16_t*)p)[i] = f2bf(v); else ((float*)p)[i] = v;
 }
 
+__device__ __forceinline__ float fsigmoid(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float ftanh(float x) { return 2.f / (1.f + __expf(-2.f * x)) - 1.f; }
+
+// Chan et al. parallel merge of (count, mean, M2) moments: a <- a (+) b.
+__device__ __forceinline__ void moments_merge(float& na, float& ma, float& qa, float nb, float mb, float qb) {
+  const float n = na + nb;
+  if (nb == 0.f) return;
+  const float d = mb - ma;
+  const float f = nb / n;
+  ma = fmaf(d, f, ma);
+  qa = qa + qb + d * d * na * f;
+  na = n;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -75,6 +75,8 @@ struct GemmParams {
   void* y2;
   int ldy2, epi_act;
   float* colsum_part;
+  float* stat_part;  // GNSTATS / GNBWD per-(128-row group, column tile) partials
+  int gn_groups, gn_glu;
 };
 
 template <typename T> struct Cfg;
@@ -229,6 +231,49 @@ __device__ __forceinline__ void epilogue8(const GemmParams& P, int64_t row, int 
   }
   if (P.out_f32) st8<float>(P.y, row * P.ldy + col, v);
   else st8<T>(P.y, row * P.ldy + col, v);
+}
+
+// GNBWD: GroupNorm-backward sums of this output (the GN input's gradient dy)
+// for 8 consecutive channels of one frame: s[0..1] = (sum g*dh, sum g*dh*xhat)
+// of group a, s[2..3] of group b (GLU: u = [a | b], dh through
+// tanh(h_a)*sigmoid(h_b), layers.py:240-242).  u, mean/rstd, gamma, beta are
+// the forward GroupNorm's (gn_h, gn_mr, gn_gamma, gn_beta).
+template <typename T>
+__device__ __forceinline__ void gnbwd8(const GemmParams& P, int64_t row, int col, const float* dy, float* s) {
+  const int b = (int)(row / P.T);
+  float ua[8], ga[8];
+  ld8<T>(P.gn_h, row * P.ldgn + col, ua);
+  ld8<float>(P.gn_gamma, col, ga);
+  if (!P.gn_glu) {
+    const int grp = P.gn_groups == 1 ? 0 : col / (P.Nc / P.gn_groups);
+    const float m = P.gn_mr[(b * P.gn_groups + grp) * 2], r = P.gn_mr[(b * P.gn_groups + grp) * 2 + 1];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float g = ga[e] * dy[e];
+      s[0] += g;
+      s[1] = fmaf(g, (ua[e] - m) * r, s[1]);
+    }
+    return;
+  }
+  const int half = P.Nc;
+  float ub[8], gb[8], ba[8], bb[8];
+  ld8<T>(P.gn_h, row * P.ldgn + col + half, ub);
+  ld8<float>(P.gn_gamma, col + half, gb);
+  ld8<float>(P.gn_beta, col, ba);
+  ld8<float>(P.gn_beta, col + half, bb);
+  const float ma = P.gn_mr[b * 4], ra = P.gn_mr[b * 4 + 1], mb = P.gn_mr[b * 4 + 2], rb = P.gn_mr[b * 4 + 3];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float xa = (ua[e] - ma) * ra, xb = (ub[e] - mb) * rb;
+    const float ta = ftanh(xa * ga[e] + ba[e]);
+    const float sb = fsigmoid(xb * gb[e] + bb[e]);
+    const float dga = ga[e] * (dy[e] * sb * (1.f - ta * ta));
+    const float dgb = gb[e] * (dy[e] * ta * (sb * (1.f - sb)));
+    s[0] += dga;
+    s[1] = fmaf(dga, xa, s[1]);
+    s[2] += dgb;
+    s[3] = fmaf(dgb, xb, s[3]);
+  }
 }
 
 // Fragment-level prologue (LDS-DMA staging cannot transform data in flight).
@@ -656,6 +701,8 @@ __global__ __launch_bounds__(256 * SUB, SUB == 1 ? 2 : 1) void conv_gemm_kernel(
   float* csr = (float*)(smem + 36864);      // COLSUM reduction [EROWS][kBN]
   const int er = tid >> 4, ec = (tid & 15) * 8;
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // COLSUM accumulators
+  float mn = 0.f, mm = 0.f, mq = 0.f;                       // GNSTATS running (count, mean, M2)
+  float gs[4] = {0.f, 0.f, 0.f, 0.f};                       // GNBWD sums
   __syncthreads();  // staging buffers are free
 #pragma unroll
   for (int slab = 0; slab < 2 * SUB; ++slab) {
@@ -690,11 +737,58 @@ __global__ __launch_bounds__(256 * SUB, SUB == 1 ? 2 : 1) void conv_gemm_kernel(
           epilogue8<T>(P, row, col, v);
 #pragma unroll
           for (int e = 0; e < 8; ++e) cs[e] += v[e];
+          if (P.epi & VQX_EPI_GNSTATS) {  // two-pass moments of the 8 values, merged
+            float m8 = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) m8 += v[e];
+            m8 *= 0.125f;
+            float q8 = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) q8 = fmaf(v[e] - m8, v[e] - m8, q8);
+            moments_merge(mn, mm, mq, 8.f, m8, q8);
+          }
+          if (P.epi & VQX_EPI_GNBWD) gnbwd8<T>(P, row, col, v, gs);
         }
       }
     }
     __syncthreads();
     if constexpr (MODE != MODE_WGRAD) {
+      // per-(128-row group, column tile) GroupNorm partials
+      if ((P.epi & (VQX_EPI_GNSTATS | VQX_EPI_GNBWD)) && (slab & 1)) {
+        const int64_t grp_row = (int64_t)m0 + (slab >> 1) * 128;
+        float* out = P.stat_part + ((grp_row / 128) * P.tiles_n + tn) * 4;
+        if (P.epi & VQX_EPI_GNSTATS) {
+          // merge the 64 lanes of each wave, then the waves (deterministic order)
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) {
+            const float n2 = __shfl_xor(mn, o, 64), m2 = __shfl_xor(mm, o, 64), q2 = __shfl_xor(mq, o, 64);
+            if ((lane & o) == 0) moments_merge(mn, mm, mq, n2, m2, q2);
+            else { float a = n2, b = m2, c = q2; moments_merge(a, b, c, mn, mm, mq); mn = a; mm = b; mq = c; }
+          }
+          if (lane == 0) { csr[3 * wid] = mn; csr[3 * wid + 1] = mm; csr[3 * wid + 2] = mq; }
+          __syncthreads();
+          if (tid == 0 && grp_row < P.n_rows) {
+            float a = csr[0], b = csr[1], c = csr[2];
+            for (int w = 1; w < 4 * SUB; ++w) moments_merge(a, b, c, csr[3 * w], csr[3 * w + 1], csr[3 * w + 2]);
+            out[0] = a; out[1] = b; out[2] = c; out[3] = 0.f;
+          }
+          mn = mm = mq = 0.f;
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            float x = wave_sum(gs[k]);
+            if (lane == 0) csr[4 * wid + k] = x;
+            gs[k] = 0.f;
+          }
+          __syncthreads();
+          if (tid < 4 && grp_row < P.n_rows) {
+            float x = 0.f;
+            for (int w = 0; w < 4 * SUB; ++w) x += csr[4 * w + tid];
+            out[tid] = x;
+          }
+        }
+        __syncthreads();
+      }
       // per-128-row-group column sums of the stored values (bias gradient of
       // the layer this output feeds), reduced over the EROWS row lanes in LDS
       if ((P.epi & VQX_EPI_COLSUM) && (slab & 1)) {
@@ -841,6 +935,17 @@ static int conv_common(const vqx_conv_args* a, int mode, hipStream_t s) {
   if ((epi & VQX_EPI_SPLIT) && (!a->out2 || a->split_col % 8 || a->ldo2 % 4 || !aligned16(a->out2))) { set_error("vqx_conv: SPLIT operands"); return -1; }
   if ((epi & VQX_EPI_ACT2) && (!a->y2 || a->ldy2 % 8 || !aligned16(a->y2))) { set_error("vqx_conv: ACT2 needs a 16-B aligned y2 with ldy2 %% 8 == 0"); return -1; }
   if ((epi & (VQX_EPI_ACT | VQX_EPI_ACT2)) && a->epi_act != VQX_PRO_LRELU && a->epi_act != VQX_PRO_RELU) { set_error("vqx_conv: epi_act must be LRELU or RELU"); return -1; }
+  if (epi & (VQX_EPI_GNSTATS | VQX_EPI_GNBWD)) {
+    const int G = a->gn_groups;
+    if ((epi & VQX_EPI_GNSTATS) && (epi & VQX_EPI_GNBWD)) { set_error("vqx_conv: GNSTATS and GNBWD are exclusive"); return -1; }
+    if (!a->stat_part || a->T % 128 || G < 1 || (epi & VQX_EPI_GNADD)) { set_error("vqx_conv: GN partials need stat_part, T %% 128 == 0, no GNADD"); return -1; }
+    if ((epi & VQX_EPI_GNSTATS) && (a->cout % G || (a->cout / G) % 128)) { set_error("vqx_conv: GNSTATS needs cout/G %% 128 == 0"); return -1; }
+    if (epi & VQX_EPI_GNBWD) {
+      if (!(a->gn_h && a->gn_mean_rstd && a->gn_gamma && aligned16(a->gn_h) && aligned16(a->gn_gamma) && a->ldgn % 8 == 0)) { set_error("vqx_conv: GNBWD operands"); return -1; }
+      if (a->gn_glu && (G != 2 || !a->gn_beta || !aligned16(a->gn_beta))) { set_error("vqx_conv: GNBWD glu needs G=2 and beta"); return -1; }
+      if (!a->gn_glu && (a->cout % G || (a->cout / G) % 128)) { set_error("vqx_conv: GNBWD needs cout/G %% 128 == 0"); return -1; }
+    }
+  }
   if ((epi & VQX_EPI_COLSUM) && !a->colsum_part) { set_error("vqx_conv: COLSUM needs colsum_part [ceil(n_rows/128)][cout]"); return -1; }
   if (!a->y || !aligned16(a->y)) { set_error("vqx_conv: y must be non-null and 16-byte aligned"); return -1; }
 
@@ -861,6 +966,7 @@ static int conv_common(const vqx_conv_args* a, int mode, hipStream_t s) {
   P.out2 = a->out2; P.ldo2 = a->ldo2; P.split_col = a->split_col; P.out2_acc = a->out2_accumulate;
   P.y2 = a->y2; P.ldy2 = a->ldy2; P.epi_act = a->epi_act;
   P.colsum_part = a->colsum_part;
+  P.stat_part = a->stat_part; P.gn_groups = a->gn_groups; P.gn_glu = a->gn_glu;
   if (P.a_bytes > 0x7fffffffLL || P.b_bytes > 0x7fffffffLL) { set_error("vqx_conv: operand larger than 2 GiB"); return -1; }
   const bool gen = (a->cin % bk) != 0;
   if (a->dtype == VQX_BF16) {

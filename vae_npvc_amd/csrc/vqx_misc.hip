@@ -178,9 +178,30 @@ __global__ void gn_finalize_kernel(const float* __restrict__ part, int nbg, floa
   mr[2 * bg + 1] = 1.0f / sqrtf(var + eps);
 }
 
-// fast sigmoid / tanh on v_exp_f32 (|rel err| ~1e-7, far inside the parity tolerance)
-__device__ __forceinline__ float fsigmoid(float x) { return 1.f / (1.f + __expf(-x)); }
-__device__ __forceinline__ float ftanh(float x) { return 2.f / (1.f + __expf(-2.f * x)) - 1.f; }
+// Combine the GEMM GNSTATS tiles [N/128][ntn][4] = (count, mean, M2, -) of
+// utterance b's row groups and group g's column tiles (double, fixed order).
+__global__ void gn_finalize_tiles_kernel(const float* __restrict__ part, int B, int G, int rg_per_utt, int ntn,
+                                         int tn_per_group, float eps, float* __restrict__ mr) {
+  const int bg = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bg >= B * G) return;
+  const int b = bg / G, g = bg - b * G;
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  for (int r = 0; r < rg_per_utt; ++r)
+    for (int t = 0; t < tn_per_group; ++t) {
+      const float* o = part + ((int64_t)(b * rg_per_utt + r) * ntn + g * tn_per_group + t) * 4;
+      const double nb = o[0];
+      if (nb == 0.0) continue;
+      const double d = (double)o[1] - mean;
+      const double nn = n + nb;
+      mean += d * nb / nn;
+      m2 += (double)o[2] + d * d * n * nb / nn;
+      n = nn;
+    }
+  const float var = n > 0.0 ? (float)(m2 / n) : 0.f;
+  mr[2 * bg] = (float)mean;
+  mr[2 * bg + 1] = 1.0f / sqrtf(var + eps);
+}
+
 
 // ---- 16-byte chunk helpers (8 bf16 or 4 f32 per chunk) -------------------
 template <typename T> struct Vec;
@@ -346,9 +367,9 @@ __global__ __launch_bounds__(256) void gn_bwd_apply_vec_kernel(const T* __restri
                                                                const float* __restrict__ mr,
                                                                const float* __restrict__ gamma,
                                                                const float* __restrict__ beta,
-                                                               const float* __restrict__ part,
-                                                               float* __restrict__ colsum_b, float* __restrict__ dgamma_b,
-                                                               float* __restrict__ dbeta_b) {
+                                                               const float* __restrict__ part, int nparts,
+                                                               int pstride, float* __restrict__ colsum_b,
+                                                               float* __restrict__ dgamma_b, float* __restrict__ dbeta_b) {
   constexpr int V = Vec<T>::N;
   const int b = blockIdx.y;
   const int ch = blockIdx.x * 8 + (threadIdx.x & 7), rg = threadIdx.x >> 3;
@@ -362,8 +383,8 @@ __global__ __launch_bounds__(256) void gn_bwd_apply_vec_kernel(const T* __restri
     const int cg = C / G;
     const float M = (float)T_ * (float)cg;
     float S1a = 0.f, S2a = 0.f, S1b = 0.f, S2b = 0.f;
-    for (int q = 0; q < kGnBwdParts; ++q) {
-      const float* o = part + ((int64_t)b * kGnBwdParts + q) * G * 2;
+    for (int q = 0; q < nparts; ++q) {
+      const float* o = part + ((int64_t)b * nparts + q) * pstride;
       S1a += o[0];
       S2a += o[1];
       if (glu) { S1b += o[2]; S2b += o[3]; }
@@ -1017,7 +1038,8 @@ extern "C" int vqx_gn_glu_fwd(const void* u, int32_t ldu, void* g, int32_t ldg, 
 extern "C" int vqx_gn_bwd(const void* dy, int32_t lddy, const void* u, int32_t ldu, void* du, int32_t lddu,
                           int32_t dtype, int64_t n_rows, int32_t T, int32_t C, int32_t G, int32_t glu,
                           const float* mean_rstd, const float* gamma, const float* beta, float* partials,
-                          float* colsum_p, float* dgamma_p, float* dbeta_p, vqx_stream_t stream) {
+                          int32_t nparts, float* colsum_p, float* dgamma_p, float* dbeta_p, vqx_stream_t stream) {
+  if (nparts < 0) { set_error("vqx_gn_bwd: nparts < 0"); return -1; }
   if (glu && G != 2) { set_error("vqx_gn_bwd: glu requires G=2"); return -1; }
   if (!glu && G != 1) { set_error("vqx_gn_bwd: non-glu path supports G=1"); return -1; }
   if (C % G || n_rows % T) { set_error("vqx_gn_bwd: bad shape"); return -1; }
@@ -1031,12 +1053,16 @@ extern "C" int vqx_gn_bwd(const void* dy, int32_t lddy, const void* u, int32_t l
     return -1;
   }
   hipStream_t s = (hipStream_t)stream;
+  // nparts == 0: reduce here (kGnBwdParts row parts per utterance, G*2 floats
+  // each); nparts > 0: the producing GEMM's GNBWD epilogue already wrote
+  // nparts tiles per utterance (4 floats each)
+  const int np = nparts ? nparts : kGnBwdParts, ps = nparts ? 4 : G * 2;
   if (dtype == VQX_BF16) {
-    hipLaunchKernelGGL(gn_bwd_reduce_vec_kernel<bf16_t>, dim3(kGnBwdParts, B), dim3(256), 0, s, (const bf16_t*)dy, lddy, (const bf16_t*)u, ldu, T, C, G, glu, cpr, mean_rstd, gamma, beta, partials);
-    hipLaunchKernelGGL(gn_bwd_apply_vec_kernel<bf16_t>, dim3((cpr + 7) / 8, B), dim3(256), 0, s, (const bf16_t*)dy, lddy, (const bf16_t*)u, ldu, (bf16_t*)du, lddu, T, C, G, glu, cpr, mean_rstd, gamma, beta, partials, colsum_p, dgamma_p, dbeta_p);
+    if (!nparts) hipLaunchKernelGGL(gn_bwd_reduce_vec_kernel<bf16_t>, dim3(kGnBwdParts, B), dim3(256), 0, s, (const bf16_t*)dy, lddy, (const bf16_t*)u, ldu, T, C, G, glu, cpr, mean_rstd, gamma, beta, partials);
+    hipLaunchKernelGGL(gn_bwd_apply_vec_kernel<bf16_t>, dim3((cpr + 7) / 8, B), dim3(256), 0, s, (const bf16_t*)dy, lddy, (const bf16_t*)u, ldu, (bf16_t*)du, lddu, T, C, G, glu, cpr, mean_rstd, gamma, beta, partials, np, ps, colsum_p, dgamma_p, dbeta_p);
   } else {
-    hipLaunchKernelGGL(gn_bwd_reduce_vec_kernel<float>, dim3(kGnBwdParts, B), dim3(256), 0, s, (const float*)dy, lddy, (const float*)u, ldu, T, C, G, glu, cpr, mean_rstd, gamma, beta, partials);
-    hipLaunchKernelGGL(gn_bwd_apply_vec_kernel<float>, dim3((cpr + 7) / 8, B), dim3(256), 0, s, (const float*)dy, lddy, (const float*)u, ldu, (float*)du, lddu, T, C, G, glu, cpr, mean_rstd, gamma, beta, partials, colsum_p, dgamma_p, dbeta_p);
+    if (!nparts) hipLaunchKernelGGL(gn_bwd_reduce_vec_kernel<float>, dim3(kGnBwdParts, B), dim3(256), 0, s, (const float*)dy, lddy, (const float*)u, ldu, T, C, G, glu, cpr, mean_rstd, gamma, beta, partials);
+    hipLaunchKernelGGL(gn_bwd_apply_vec_kernel<float>, dim3((cpr + 7) / 8, B), dim3(256), 0, s, (const float*)dy, lddy, (const float*)u, ldu, (float*)du, lddu, T, C, G, glu, cpr, mean_rstd, gamma, beta, partials, np, ps, colsum_p, dgamma_p, dbeta_p);
   }
   return launch_status("vqx_gn_bwd");
 }
@@ -1208,4 +1234,16 @@ extern "C" int vqx_linear_batched_bwd(const vqx_linear_layer* table_dev, int32_t
     hipLaunchKernelGGL(sum_slices_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, s, partials, n * nO, ne, dc);
   }
   return launch_status("vqx_linear_batched_bwd");
+}
+
+extern "C" int vqx_gn_finalize_tiles(const float* parts, int64_t n_rows, int32_t T, int32_t C, int32_t G, float eps,
+                                     float* mean_rstd, vqx_stream_t stream) {
+  if (!parts || !mean_rstd || T % 128 || n_rows % T || G < 1 || C % G || (C / G) % 128) {
+    set_error("vqx_gn_finalize_tiles: needs T %% 128 == 0 and C/G %% 128 == 0");
+    return -1;
+  }
+  const int B = (int)(n_rows / T);
+  hipLaunchKernelGGL(gn_finalize_tiles_kernel, dim3((B * G + 127) / 128), dim3(128), 0, (hipStream_t)stream, parts, B,
+                     G, T / 128, C / 128, (C / G) / 128, eps, mean_rstd);
+  return launch_status("vqx_gn_finalize_tiles");
 }

@@ -28,6 +28,7 @@ model parameters are views into them, so `model.state_dict()` stays the
 reference's and the optimizer touches one contiguous buffer.
 """
 import math
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -102,6 +103,12 @@ class Workspace:
         self.xhat_nct = e(B, Fo, T, dt=F32)
         # scalars: 0 x_loss, 1 sqerr, 4..7 EMA diagnostics
         self.stats = torch.zeros(8, device=dev, dtype=F32)
+        # GroupNorm partials written by GEMM epilogues (GNSTATS / GNBWD tiles:
+        # [N/128][column tile][4]) when T and the group widths are multiples of 128
+        self.fuse_gn = (T % 128 == 0 and C % 128 == 0 and Cd % 128 == 0
+                        and os.environ.get("VQX_FUSE_GN", "1") != "0")
+        self.gn_rg = N // 128 if self.fuse_gn else 0
+        self.gst = e(max(1, self.gn_rg) * ((max(C, 2 * Cd) + 127) // 128) * 4, dt=F32)
         self.loss_part = e(1024, dt=F32)
         self.gn_part = e(B * 2 * 8 * 3, dt=F32)
         if not train:
@@ -111,7 +118,7 @@ class Workspace:
         self.dr = [e(N, Cd + S) for _ in range(2)]
         self.dg = e(N, Cd)
         self.du = e(N, 2 * Cd)
-        self.gnb_part = e(B * 64 * 2, dt=F32)
+        self.gnb_part = e(max(B * 64 * 2, max(1, self.gn_rg) * ((max(C, Cd) + 127) // 128) * 4), dt=F32)
         self.colsum_b = e(B * 2 * max(Cd, C), dt=F32)   # per-utterance column sums of du
         self.dgam_b = e(B * 2 * max(Cd, C), dt=F32)
         self.dbet_b = e(B * 2 * max(Cd, C), dt=F32)
@@ -353,8 +360,12 @@ class VQVAEEngine:
         self.fwd(self.enc0, w.x, w.c[0], T, bias=self.enc0.mod.bias, act=L.PRO_LRELU, y2=w.a[0])
         for i in range(self.dims["ns"]):
             k3, sk, gn = self.enc_k3[i], self.enc_sk[i], self.enc_gn[i]
-            self.fwd(k3, w.a[i], w.h[i], T, bias=k3.mod.bias)
-            ops.groupnorm_stats(w.h[i], T, 1, w.gn_part, w.enc_mr[i])
+            if w.fuse_gn:  # statistics of h_i from the k3 GEMM's epilogue tiles
+                self.fwd(k3, w.a[i], w.h[i], T, bias=k3.mod.bias, gn_stats=w.gst, gn_groups=1)
+                ops.gn_finalize_tiles(w.gst, w.N, T, k3.cout, 1, w.enc_mr[i])
+            else:
+                self.fwd(k3, w.a[i], w.h[i], T, bias=k3.mod.bias)
+                ops.groupnorm_stats(w.h[i], T, 1, w.gn_part, w.enc_mr[i])
             self.fwd(sk, w.c[i], w.c[i + 1], T, bias=sk.mod.bias, gn_h=w.h[i], gn_mr=w.enc_mr[i],
                      gn_gamma=gn.weight, gn_beta=gn.bias, act=L.PRO_LRELU, y2=w.a[i + 1])
         self.fwd(self.enc_out, w.a[-1], w.z, T, bias=self.enc_out.mod.bias, out_f32=True)
@@ -364,8 +375,12 @@ class VQVAEEngine:
         self.fwd(self.dec0, zq_c, w.xs[0], T, bias=self.dec0.mod.bias)
         for i in range(nd):
             ci, gn, rs = self.dec_in[i], self.dec_gn[i], self.dec_rs[i]
-            self.fwd(ci, w.xs[i], w.u[i], T, bias=ci.mod.bias, rowbias=w.condbias[i])
-            ops.groupnorm_stats(w.u[i], T, 2, w.gn_part, w.dec_mr[i])
+            if w.fuse_gn:
+                self.fwd(ci, w.xs[i], w.u[i], T, bias=ci.mod.bias, rowbias=w.condbias[i], gn_stats=w.gst, gn_groups=2)
+                ops.gn_finalize_tiles(w.gst, w.N, T, ci.cout, 2, w.dec_mr[i])
+            else:
+                self.fwd(ci, w.xs[i], w.u[i], T, bias=ci.mod.bias, rowbias=w.condbias[i])
+                ops.groupnorm_stats(w.u[i], T, 2, w.gn_part, w.dec_mr[i])
             ops.gn_glu_fwd(w.u[i], w.g[i], T, w.dec_mr[i], gn.weight, gn.bias)
             self.fwd(rs, w.g[i], w.xs[i + 1], T, bias=rs.mod.bias, res=w.xs[i], out2=w.skip32, split_col=Cd,
                      out2_accumulate=(i > 0))
@@ -419,6 +434,19 @@ class VQVAEEngine:
         return src
 
     # ------------------------------------------------------------ backward
+    def _gnb(self, w, i):
+        """GNBWD epilogue arguments: the GEMM producing dL/d(GN_i output) also
+        writes block i's GroupNorm-backward sums (encoder, G=1)."""
+        if not w.fuse_gn:
+            return {}
+        gn = self.enc_gn[i]
+        return dict(gn_bwd=w.gnb_part, gn_h=w.h[i], gn_mr=w.enc_mr[i], gn_gamma=gn.weight, gn_beta=gn.bias,
+                    gn_groups=1)
+
+    def _gnb_parts(self, w, cols):
+        """GNBWD tiles per utterance (0 = vqx_gn_bwd reduces itself)."""
+        return (w.T // 128) * ((cols + 127) // 128) if w.fuse_gn else 0
+
     def _bview(self, buf, B, C):
         return buf.view(-1)[: B * C].view(B, C)
 
@@ -435,7 +463,8 @@ class VQVAEEngine:
         self.wgrad(eo, w.dz, w.a[ns], T)
         cur = w.dc[0]
         # every dL/dc_i producer also writes its bias-gradient partials (COLSUM)
-        self.dgrad(eo, w.dz, cur, T, mask=w.a[ns], mask_slope=0.2, colsum=w.cs_enc[0])
+        # and, for the block below, the GroupNorm-backward sums (GNBWD)
+        self.dgrad(eo, w.dz, cur, T, mask=w.a[ns], mask_slope=0.2, colsum=w.cs_enc[0], **self._gnb(w, ns - 1))
         ops.weight_norm_bwd(tb["enc_out"])
         cs_b, dg_b, db_b = (self._bview(t, B, C) for t in (w.colsum_b, w.dgam_b, w.dbet_b))
         for i in reversed(range(ns)):
@@ -444,10 +473,11 @@ class VQVAEEngine:
             nxt = w.dc[j]
             # cur = dL/dc_{i+1}, the gradient w.r.t. block i's output GN(h_i) + skip(c_i)
             self.wgrad(sk, cur, w.c[i], T)
-            ops.gn_bwd(cur, w.h[i], w.dh, T, 1, False, w.enc_mr[i], gn.weight, gn.bias, w.gnb_part, cs_b, dg_b, db_b)
+            ops.gn_bwd(cur, w.h[i], w.dh, T, 1, False, w.enc_mr[i], gn.weight, gn.bias, w.gnb_part, cs_b, dg_b, db_b,
+                       nparts=self._gnb_parts(w, C))
             self.wgrad(k3, w.dh, w.a[i], T)
             self.dgrad(k3, w.dh, w.tmp, T, mask=w.a[i], mask_slope=0.2)
-            self.dgrad(sk, cur, nxt, T, res=w.tmp, colsum=w.cs_enc[j])
+            self.dgrad(sk, cur, nxt, T, res=w.tmp, colsum=w.cs_enc[j], **(self._gnb(w, i - 1) if i > 0 else {}))
             # weight norms of k3/sk + biases of sk (cur partials), k3 and the GN affine
             ops.weight_norm_bwd(tb[("enc", i)])
             cur = nxt
@@ -479,9 +509,13 @@ class VQVAEEngine:
             j = (nd - 1 - i) % 2
             # cur = [dL/dx_{i+1} | dL/dskip]
             self.wgrad(rs, cur, w.g[i], T)
-            self.dgrad(rs, cur, w.dg, T)
+            if w.fuse_gn:  # GLU + GroupNorm backward sums from the res/skip dgrad's epilogue
+                self.dgrad(rs, cur, w.dg, T, gn_bwd=w.gnb_part, gn_h=w.u[i], gn_mr=w.dec_mr[i], gn_gamma=gn.weight,
+                           gn_beta=gn.bias, gn_groups=2, gn_glu=True)
+            else:
+                self.dgrad(rs, cur, w.dg, T)
             ops.gn_bwd(w.dg, w.u[i], w.du, T, 2, True, w.dec_mr[i], gn.weight, gn.bias, w.gnb_part, w.cs_all[i],
-                       dg_b, db_b)
+                       dg_b, db_b, nparts=self._gnb_parts(w, Cd))
             self.wgrad(ci, w.du, w.xs[i], T)
             self.dgrad(ci, w.du, nxt[:, :Cd], T, res=cur[:, :Cd], colsum=w.cs_dec[1 - j])
             # weight norms of conv_in/res_skip + biases of res_skip, conv_in and the GN affine

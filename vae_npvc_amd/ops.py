@@ -32,7 +32,7 @@ def _check_cuda(*ts):
 def conv_args(x, w, y, *, T, cin, cout, ntaps, pad, prologue=L.PRO_NONE, pro_scale=1.0, bias=None,
               rowbias=None, res=None, mask=None, mask_slope=0.0, mask_scale=1.0, gn_h=None, gn_mr=None,
               gn_gamma=None, gn_beta=None, out2=None, split_col=0, out2_accumulate=False, out_f32=False,
-              act=None, y2=None, colsum=None):
+              act=None, y2=None, colsum=None, gn_stats=None, gn_bwd=None, gn_groups=1, gn_glu=False):
     epi = 0
     if bias is not None:
         epi |= L.EPI_BIAS
@@ -42,7 +42,7 @@ def conv_args(x, w, y, *, T, cin, cout, ntaps, pad, prologue=L.PRO_NONE, pro_sca
         epi |= L.EPI_MASK
     if res is not None:
         epi |= L.EPI_RES
-    if gn_h is not None:
+    if gn_h is not None and gn_bwd is None:  # GNBWD reads gn_* as the forward GN's operands
         epi |= L.EPI_GNADD
     if out2 is not None:
         epi |= L.EPI_SPLIT
@@ -54,6 +54,10 @@ def conv_args(x, w, y, *, T, cin, cout, ntaps, pad, prologue=L.PRO_NONE, pro_sca
         epi |= L.EPI_ACT2
     if colsum is not None:
         epi |= L.EPI_COLSUM
+    if gn_stats is not None:
+        epi |= L.EPI_GNSTATS
+    if gn_bwd is not None:
+        epi |= L.EPI_GNBWD
     a = L.ConvArgs()
     a.x, a.w, a.y = ptr(x), ptr(w), ptr(y)
     a.bias, a.rowbias, a.res, a.mask = ptr(bias), ptr(rowbias), ptr(res), ptr(mask)
@@ -71,6 +75,8 @@ def conv_args(x, w, y, *, T, cin, cout, ntaps, pad, prologue=L.PRO_NONE, pro_sca
     a.y2, a.ldy2 = ptr(y2), (y2.stride(0) if y2 is not None else 0)
     a.epi_act = act if act is not None else 0
     a.colsum_part = ptr(colsum)
+    a.stat_part = ptr(gn_stats if gn_stats is not None else gn_bwd)
+    a.gn_groups, a.gn_glu = gn_groups, int(gn_glu)
     return a
 
 
@@ -236,11 +242,18 @@ def gn_glu_fwd(u, g, T, mean_rstd, gamma, beta):
     return g
 
 
-def gn_bwd(dy, u, du, T, G, glu, mean_rstd, gamma, beta, partials, colsum_b=None, dgamma_b=None, dbeta_b=None):
+def gn_bwd(dy, u, du, T, G, glu, mean_rstd, gamma, beta, partials, colsum_b=None, dgamma_b=None, dbeta_b=None,
+           nparts=0):
+    """nparts > 0: `partials` already holds the producing GEMM's GNBWD tiles (nparts per utterance)."""
     call("vqx_gn_bwd", ptr(dy), dy.stride(0), ptr(u), u.stride(0), ptr(du), du.stride(0), dt_code(u.dtype),
-         u.shape[0], T, u.shape[1], G, int(glu), ptr(mean_rstd), ptr(gamma), ptr(beta), ptr(partials),
+         u.shape[0], T, u.shape[1], G, int(glu), ptr(mean_rstd), ptr(gamma), ptr(beta), ptr(partials), nparts,
          ptr(colsum_b), ptr(dgamma_b), ptr(dbeta_b), stream_ptr())
     return du
+
+
+def gn_finalize_tiles(parts, n_rows, T, C, G, mean_rstd, eps=1e-5):
+    call("vqx_gn_finalize_tiles", ptr(parts), n_rows, T, C, G, eps, ptr(mean_rstd), stream_ptr())
+    return mean_rstd
 
 
 def colsum(x, partials, out, accumulate=False, C=None):
