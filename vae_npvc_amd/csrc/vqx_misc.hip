@@ -14,39 +14,88 @@ constexpr float kLog2Pi = 1.8378770664093453f;  // log(2*pi), layers.py:8
 // but 0.  Conv1d: v[cout][cin][k], row o = co.  ConvT: v[cin][cout][k], row
 // o = ci, effective tap j' = k-1-j.  Packed effective weight:
 // wp[co][j*cin + ci].
+// Row norms of the ConvTranspose layers (rows = cin, contiguous cout*k):
+// one wave per row, 4 rows per block.  Conv1d layers get theirs in the pack.
 __global__ __launch_bounds__(256) void wn_norm_kernel(const vqx_wn_layer* __restrict__ L, int n_layers) {
   const vqx_wn_layer& l = L[blockIdx.y];
-  const int rows = l.kind == 0 ? l.cout : l.cin;
-  const int cols = (l.kind == 0 ? l.cin : l.cout) * l.k;
-  const int o = blockIdx.x;
-  if (o >= rows) return;
-  __shared__ float red[16];
+  if (l.kind != 1 || !l.g) return;
+  const int o = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (o >= l.cin) return;
+  const int cols = l.cout * l.k;
   const float* v = l.v + (int64_t)o * cols;
   float s = 0.f;
-  for (int i = threadIdx.x; i < cols; i += blockDim.x) s = fmaf(v[i], v[i], s);
-  s = block_sum(s, red);
-  if (threadIdx.x == 0) l.norm[o] = sqrtf(s);
+  if ((cols & 3) == 0 && (((uintptr_t)v) & 15) == 0) {
+    for (int i = lane * 4; i < cols; i += 256) {
+      const f32x4_t x = *(const f32x4_t*)(v + i);
+      s = fmaf(x[0], x[0], fmaf(x[1], x[1], fmaf(x[2], x[2], fmaf(x[3], x[3], s))));
+    }
+  } else {
+    for (int i = lane; i < cols; i += 64) s = fmaf(v[i], v[i], s);
+  }
+  s = wave_sum(s);
+  if (lane == 0) l.norm[o] = sqrtf(s);
 }
 
+// Pack w = g*v/||v|| into the effective-conv layout wp[co][j][ci].
+// kind 0 (Conv1d, v[co][ci][j]): block = one row co: the row is read
+//   contiguously into LDS, its norm reduced there (and saved), then written
+//   transposed [j][ci] with coalesced stores.
+// kind 1 (ConvT, v[ci][co][K-1-j]): block = a 64 ci x 64 co tile, read row
+//   segments (64*K contiguous floats per ci) into LDS, write wp[co][j][ci0..]
+//   rows of 64 consecutive ci.
+constexpr int kWnRow = 4096;
 __global__ __launch_bounds__(256) void wn_pack_kernel(const vqx_wn_layer* __restrict__ L, int n_layers) {
   const vqx_wn_layer& l = L[blockIdx.y];
-  const int64_t total = (int64_t)l.cout * l.cin * l.k;
   const int K = l.k, cin = l.cin, cout = l.cout;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    // e indexes wp[co][j][ci]
-    const int ci = (int)(e % cin);
-    const int64_t r = e / cin;
-    const int j = (int)(r % K);
-    const int co = (int)(r / K);
-    float w;
-    if (l.kind == 0) {
-      const float sc = l.g ? l.g[co] / l.norm[co] : 1.f;
-      w = l.v[((int64_t)co * cin + ci) * K + j] * sc;
-    } else {
-      const float sc = l.g ? l.g[ci] / l.norm[ci] : 1.f;
-      w = l.v[((int64_t)ci * cout + co) * K + (K - 1 - j)] * sc;
+  __shared__ float buf[kWnRow + 64];
+  __shared__ float red[16];
+  if (l.kind == 0) {
+    const int co = blockIdx.x;
+    if (co >= cout) return;
+    const int cols = cin * K;
+    const float* v = l.v + (int64_t)co * cols;
+    float s = 0.f;
+    for (int i = threadIdx.x; i < cols; i += 256) {
+      const float x = v[i];
+      buf[i] = x;
+      s = fmaf(x, x, s);
     }
-    st_dt(l.w_packed, e, w, l.dtype);
+    s = block_sum(s, red);  // includes the barriers that publish buf
+    float sc = 1.f;
+    if (l.g) {
+      const float nrm = sqrtf(s);
+      if (threadIdx.x == 0) l.norm[co] = nrm;
+      sc = l.g[co] / nrm;
+    }
+    for (int e = threadIdx.x; e < cols; e += 256) {  // e = j*cin + ci
+      const int j = e / cin, ci = e - j * cin;
+      st_dt(l.w_packed, (int64_t)co * cols + e, buf[ci * K + j] * sc, l.dtype);
+    }
+    return;
+  }
+  // kind 1: tile of 64 ci x 16 co (x K taps) = 64 x 16K floats <= 64 x 48 in LDS
+  constexpr int TCO = 16;
+  const int ntc = (cout + TCO - 1) / TCO;
+  const int ci0 = (blockIdx.x / ntc) * 64, co0 = (blockIdx.x % ntc) * TCO;
+  if (ci0 >= cin || K > 3) return;
+  const int wseg = TCO * K;  // floats per ci row segment (contiguous in v)
+  for (int e = threadIdx.x; e < 64 * wseg; e += 256) {
+    const int r = e / wseg, q = e - r * wseg;  // r: ci offset, q = co_local*K + tap
+    const int ci = ci0 + r, co = co0 + q / K;
+    float x = 0.f;
+    if (ci < cin && co < cout) {
+      x = l.v[((int64_t)ci * cout + co0) * K + q];
+      if (l.g) x *= l.g[ci] / l.norm[ci];
+    }
+    buf[q * 65 + r] = x;  // [co_local*K + tap][ci] (+1 pad)
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < TCO * K * 64; e += 256) {  // e = (co_local*K + j)*64 + ci_local
+    const int cj = e >> 6, r = e & 63;
+    const int cl = cj / K, j = cj - cl * K;
+    const int co = co0 + cl, ci = ci0 + r;
+    if (co < cout && ci < cin)
+      st_dt(l.w_packed, ((int64_t)co * K + j) * cin + ci, buf[(cl * K + (K - 1 - j)) * 65 + r], l.dtype);
   }
 }
 
@@ -966,9 +1015,19 @@ extern "C" int vqx_weight_norm_fwd(const vqx_wn_layer* lh, const vqx_wn_layer* l
     const int64_t el = (int64_t)l.cout * l.cin * l.k;
     max_el = el > max_el ? el : max_el;
   }
+  // kind 0: one block per row; kind 1: 64 ci x 16 co tiles (after the row norms)
+  int max_units = 1, max_t_rows = 1;
+  for (int i = 0; i < n_layers; ++i) {
+    const vqx_wn_layer& l = lh[i];
+    if ((l.kind == 0 ? l.cin : l.cout) * l.k > kWnRow || l.k > 3) { set_error("vqx_weight_norm_fwd: layer %d row too long", i); return -1; }
+    const int units = l.kind == 0 ? l.cout : ((l.cin + 63) / 64) * ((l.cout + 15) / 16);
+    max_units = units > max_units ? units : max_units;
+    if (l.kind == 1) max_t_rows = l.cin > max_t_rows ? l.cin : max_t_rows;
+  }
+  (void)max_el;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(wn_norm_kernel, dim3(max_rows, n_layers), dim3(256), 0, s, ld, n_layers);
-  hipLaunchKernelGGL(wn_pack_kernel, dim3(grid_for(max_el, 256, 2048), n_layers), dim3(256), 0, s, ld, n_layers);
+  hipLaunchKernelGGL(wn_norm_kernel, dim3((max_t_rows + 3) / 4, n_layers), dim3(256), 0, s, ld, n_layers);
+  hipLaunchKernelGGL(wn_pack_kernel, dim3(max_units, n_layers), dim3(256), 0, s, ld, n_layers);
   return launch_status("vqx_weight_norm_fwd");
 }
 
