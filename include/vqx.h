@@ -361,14 +361,17 @@ int vqx_set_gemm_tile(int32_t policy);
 /* Launch probe (measurement only; not reentrant while enabled).  While on,
  * each conv GEMM launch records a start/stop event pair stamped on its own
  * dispatch (hipExtLaunchKernelGGL); after the stream is synchronised,
- * vqx_probe_read returns per launch {dtype, mode, prologue, gen, dma}, the
- * algorithmic FLOPs and the kernel duration in ms.  Enabling clears the log. */
+ * vqx_probe_read returns per launch {dtype, mode, prologue, gen, staging},
+ * the algorithmic FLOPs and the kernel duration in ms.  enable(0/1) pauses /
+ * resumes recording (an event-stamped dispatch costs a few us of queue time,
+ * so callers sample); clear() empties the log. */
 int vqx_probe_enable(int32_t on);
+int vqx_probe_clear(void);
 int vqx_probe_count(int64_t* n);
 int vqx_probe_read(int64_t i, int32_t* info5, double* flops, float* ms);
 
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
-#define VQX_ABI_VERSION 106
+#define VQX_ABI_VERSION 107
 int vqx_version(void);
 
 #ifdef __cplusplus

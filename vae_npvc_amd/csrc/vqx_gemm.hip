@@ -1029,11 +1029,13 @@ extern "C" int vqx_set_gemm_tile(int32_t policy) {
 }
 
 extern "C" int vqx_probe_enable(int32_t on) {
-  if (on) {
-    g_probe.clear();
-    g_probe_used = 0;
-  }
-  g_probe_on = on != 0;
+  g_probe_on = on != 0;  // pause / resume; the log is kept
+  return 0;
+}
+
+extern "C" int vqx_probe_clear(void) {
+  g_probe.clear();
+  g_probe_used = 0;
   return 0;
 }
 

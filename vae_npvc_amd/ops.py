@@ -91,8 +91,12 @@ class LaunchProbe:
     def __init__(self):
         self.shapes = []
 
-    def start(self):
+    def clear(self):
         self.shapes = []
+        call("vqx_probe_clear")
+
+    def start(self):
+        """Resume recording (the log is kept; clear() empties it)."""
         call("vqx_probe_enable", 1)
 
     def stop(self):
