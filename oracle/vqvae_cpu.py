@@ -10,11 +10,12 @@ Pinned against golden vectors produced by importing the reference itself in
 the survey container (tests/golden/make_golden.py -> tests/golden/*.npz);
 tests/test_oracle_golden.py checks this restatement against them.
 
-Scope (SURVEY §8a): the single-stage Encoder/Decoder of
+Scope (SURVEY §8a, §8f row 1): the single-stage Encoder/Decoder of
 egs/vcc20/vae1/conf/train_pytorch_vqvae.yaml and
 egs/aishell3/vc2/conf/train_pytorch_vqvae.yaml (one resolution stage, k=3,
-stack_layers 1, no dilation), EMAVectorQuantizer, Jitter, log_loss and
-Trainer.train_step (Adam, clip_grad_norm_, StepLR).  Every function cites the
+stack_layers 1, no dilation), EMAVectorQuantizer (use_ema: true) and the
+straight-through VectorQuantizer (use_ema: false, embed_norm on/off), Jitter,
+log_loss and Trainer.train_step (Adam, clip_grad_norm_, StepLR).  Every function cites the
 reference file:line it restates (paths relative to the reference root).
 """
 import math
@@ -71,12 +72,16 @@ def layer_specs(cfg):
         conv(f"decoder.layers.{i}.res_skip_layers", Cd, Cd + skip, 1)
     conv("decoder.final_layer.1", skip, skip, 1)
     conv("decoder.final_layer.3", skip, fin, 1)
+    if not cfg.get("use_ema", False):  # VectorQuantizer's codebook is a parameter (layers_vq.py:18)
+        spec.append(("quantizer.embeddings", (cfg.get("z_num", 512), cfg.get("z_dim", 128))))
     spec.append(("embeds._embedding.weight", (cfg.get("y_num", 10), cfg.get("y_dim", 128))))
     return spec
 
 
 def buffer_specs(cfg):
     K, D = cfg.get("z_num", 512), cfg.get("z_dim", 128)
+    if not cfg.get("use_ema", False):
+        return []
     return [("quantizer.emb_init", ()), ("quantizer.emb_sum", (K, D)), ("quantizer.emb_elem", (K,)),
             ("quantizer.embeddings", (K, D))]
 
@@ -105,11 +110,13 @@ def seeded_state_dict(cfg, seed):
             sd[name] = torch.from_numpy((1.0 + 0.1 * rng.standard_normal(shape)).astype(np.float32))
         elif name.endswith(".bias"):
             sd[name] = torch.from_numpy(rng.uniform(-0.05, 0.05, size=shape).astype(np.float32))
-        elif name == "embeds._embedding.weight":
+        elif name in ("embeds._embedding.weight", "quantizer.embeddings"):
             sd[name] = torch.from_numpy(rng.standard_normal(shape).astype(np.float32))
         else:
             raise KeyError(name)
     K, D = cfg.get("z_num", 512), cfg.get("z_dim", 128)
+    if not cfg.get("use_ema", False):
+        return sd
     sd["quantizer.emb_init"] = torch.tensor(False)
     sd["quantizer.emb_sum"] = torch.zeros(K, D)
     sd["quantizer.emb_elem"] = torch.ones(K)
@@ -130,8 +137,9 @@ def seeded_batch(cfg, B, T, seed):
 # ----------------------------------------------------------------- the model
 class OracleVQVAE:
     """Functional restatement of vae_npvc.model.vqvae.Model with the EMA
-    quantizer (use_ema: true).  Parameters are CPU fp32 leaf tensors keyed by
-    the reference state_dict names."""
+    quantizer (use_ema: true) or the straight-through VectorQuantizer
+    (use_ema: false).  Parameters are CPU fp32 leaf tensors keyed by the
+    reference state_dict names."""
 
     def __init__(self, cfg, state_dict):
         self.cfg = cfg
@@ -140,10 +148,13 @@ class OracleVQVAE:
             t = state_dict[name].detach().clone().float().contiguous()
             assert tuple(t.shape) == tuple(shape), (name, t.shape, shape)
             self.params[name] = t.requires_grad_(True)
-        self.emb_init = bool(state_dict["quantizer.emb_init"])
-        self.emb_sum = state_dict["quantizer.emb_sum"].clone().float()
-        self.emb_elem = state_dict["quantizer.emb_elem"].clone().float()
-        self.embeddings = state_dict["quantizer.embeddings"].clone().float()
+        self.use_ema = cfg.get("use_ema", False)
+        self.normalize = cfg.get("embed_norm", True)  # vqvae.py:30
+        if self.use_ema:
+            self.emb_init = bool(state_dict["quantizer.emb_init"])
+            self.emb_sum = state_dict["quantizer.emb_sum"].clone().float()
+            self.emb_elem = state_dict["quantizer.emb_elem"].clone().float()
+            self.embeddings = state_dict["quantizer.embeddings"].clone().float()
         self.mu = cfg.get("mu", 0.9)
         self.beta = cfg.get("beta", 0.01)
         self.jitter_p = cfg.get("jitter_p", 0.0)
@@ -156,6 +167,8 @@ class OracleVQVAE:
 
     def state_dict(self):
         sd = OrderedDict((k, v.detach().clone()) for k, v in self.params.items())
+        if not self.use_ema:
+            return sd
         sd["quantizer.emb_init"] = torch.tensor(self.emb_init)
         sd["quantizer.emb_sum"] = self.emb_sum.clone()
         sd["quantizer.emb_elem"] = self.emb_elem.clone()
@@ -272,16 +285,53 @@ class OracleVQVAE:
         zq = zq.view(B, T, D).transpose(1, 2).contiguous()
         return zq, 0.0, enc_loss, detail
 
-    def encode(self, x):  # vqvae.py:45-52 / layers_vq.py:236-252
+    # ---- VectorQuantizer (layers_vq.py:9-163), reduction 'frame_mean', target_norm 1.0
+    def _plain_codebook(self, in_place):
+        E = self.params["quantizer.embeddings"]
+        if not self.normalize:
+            return E
+        if in_place:  # embed_norm() (layers_vq.py:28-33), called by every forward
+            with torch.no_grad():
+                E.mul_(1.0 / E.norm(dim=1, keepdim=True))
+        return 1.0 * E / E.norm(dim=1, keepdim=True)
+
+    def quantize_plain(self, z):  # layers_vq.py:79-150
+        B, D, T = z.shape
+        zf = z.transpose(1, 2).contiguous().view(-1, D)
+        z_norm = 1.0 * zf / zf.norm(dim=1, keepdim=True) if self.normalize else zf
+        emb = self._plain_codebook(in_place=True)
+        dist = self.distances(z_norm, emb)
+        idx = torch.argmin(dist, dim=1)
+        z_vq = emb.index_select(dim=0, index=idx)
+        self.last["idx"] = idx.detach().clone()
+        counts = torch.bincount(idx, minlength=self.K).float()
+        avg_probs = counts / idx.numel()
+        perplexity = torch.exp(-torch.sum(avg_probs * torch.log(avg_probs + 1e-10)))
+        z_qut_loss = F.mse_loss(z_vq, z_norm.detach(), reduction="none")
+        z_enc_loss = F.mse_loss(z_vq.detach(), z_norm, reduction="none")
+        if self.normalize:
+            z_enc_loss = z_enc_loss + F.mse_loss(z_norm, zf, reduction="none")
+        z_qut_loss = z_qut_loss.sum() / (B * T)
+        z_enc_loss = z_enc_loss.sum() / (B * T)
+        z_vq = z_norm + (z_vq - z_norm).detach()
+        z_vq = z_vq.view(B, T, D).transpose(1, 2).contiguous()
+        return z_vq, z_qut_loss, z_enc_loss, {"entropy": perplexity.item()}
+
+    def encode(self, x):  # vqvae.py:45-52 / layers_vq.py:236-252 (EMA), 36-58 (plain)
         z = self.encoder(x)
         B, D, T = z.shape
         zf = z.transpose(1, 2).contiguous().view(-1, D)
-        return torch.argmin(self.distances(zf, self.embeddings), dim=1).view(B, T)
+        if self.use_ema:
+            return torch.argmin(self.distances(zf, self.embeddings), dim=1).view(B, T)
+        if self.normalize:
+            zf = 1.0 * zf / zf.norm(dim=1, keepdim=True)
+        return torch.argmin(self.distances(zf, self._plain_codebook(in_place=False)), dim=1).view(B, T)
 
-    def decode(self, z_idx, y_idx):  # vqvae.py:55-60 / layers_vq.py:255-265
+    def decode(self, z_idx, y_idx):  # vqvae.py:55-60 / layers_vq.py:255-265 (EMA), 61-76 (plain)
         y = F.embedding(y_idx, self.params["embeds._embedding.weight"]).transpose(1, 2).contiguous()
         B, T = z_idx.shape
-        zq = self.embeddings.index_select(0, z_idx.flatten()).view(B, T, -1).transpose(1, 2).contiguous()
+        E = self.embeddings if self.use_ema else self._plain_codebook(in_place=False)
+        zq = E.index_select(0, z_idx.flatten()).view(B, T, -1).transpose(1, 2).contiguous()
         return self.decoder(zq, y)
 
     def jitter(self, zq):  # layers_vq.py:353-379 (replaces with probability 1-p: the reference's quirk)
@@ -306,7 +356,7 @@ class OracleVQVAE:
         y = F.embedding(y_idx, self.params["embeds._embedding.weight"]).transpose(1, 2).contiguous()
         z = self.encoder(x)
         self.last["z"] = z
-        zq, zq_loss, enc_loss, detail = self.quantize(z)
+        zq, zq_loss, enc_loss, detail = self.quantize(z) if self.use_ema else self.quantize_plain(z)
         zq = self.jitter(zq)
         xhat = self.decoder(zq, y)
         B, D, T = x.shape

@@ -16,6 +16,9 @@ stored):
   * vq_tile.npz/.json     the N < K tiling path (layers_vq.py:183-190)
   * jitter.json           Jitter.forward neighbour map (layers_vq.py:353-379)
   * full_step.npz/.json   2 steps at the config-2 size B=64 x T=256
+  * step_<cfg>_plain*     3 steps with the straight-through VectorQuantizer
+                          (use_ema: false; embed_norm true / false; aishell3
+                          with jitter_p 0.12), SURVEY §8f row 1
 Weights/inputs come from numpy PCG64 seeds (oracle/vqvae_cpu.py), so the GPU
 box regenerates them bit-identically without receiving any weights.
 """
@@ -44,7 +47,19 @@ CFGS = {
 }
 
 
+VARIANTS = {  # derived configs: base recipe + overrides
+    "vcc20_plain": ("vcc20", {"use_ema": False}),
+    "vcc20_plain_nonorm": ("vcc20", {"use_ema": False, "embed_norm": False}),
+    "aishell3_plain": ("aishell3", {"use_ema": False}),
+}
+
+
 def load_cfg(name):
+    if name in VARIANTS:
+        base, over = VARIANTS[name]
+        cfg = yaml.safe_load(open(CFGS[base]))
+        cfg.update(over)
+        return cfg
     return yaml.safe_load(open(CFGS[name]))
 
 
@@ -98,7 +113,8 @@ def step_fixture(name, B, T, steps, wseed, bseed, tseed, nseed, out_prefix, keep
     cfg = load_cfg(name)
     sd = seeded_state_dict(cfg, wseed)
     model = ref_model(cfg, sd)
-    rec = Recorder(model.quantizer)
+    ema = cfg.get("use_ema", False)
+    rec = Recorder(model.quantizer) if ema else None
     opt = torch.optim.Adam(model.parameters(), lr=cfg.get("learning_rate", 1e-3), betas=(0.5, 0.999),
                            weight_decay=0.0)
     sched = torch.optim.lr_scheduler.StepLR(optimizer=opt, **cfg["lr_param"]) if cfg.get("lr_scheduler") else None
@@ -115,13 +131,15 @@ def step_fixture(name, B, T, steps, wseed, bseed, tseed, nseed, out_prefix, keep
         if s == 0:
             meta["grads"] = {k: summarize(g) for k, g in grads.items()}
             arrays["xhat0_slice"] = xhat[:, :, :16].numpy().astype(np.float32)
+        q = model.quantizer
+        meta[f"embeddings{s}"] = summarize(q.embeddings)
+        if not ema:
+            continue
         c = rec.calls[-1]
         if keep_idx:
             arrays[f"idx{s}"] = c["idx"].numpy().astype(np.int16)
             arrays[f"gap{s}"] = c["gap"].numpy().astype(np.float32)
-        q = model.quantizer
         arrays[f"emb_elem{s}"] = q.emb_elem.detach().numpy().astype(np.float32)
-        meta[f"embeddings{s}"] = summarize(q.embeddings)
         meta[f"emb_sum{s}"] = summarize(q.emb_sum)
     meta["params_after"] = {k: summarize(p, 8) for k, p in model.named_parameters()}
     np.savez_compressed(HERE / f"{out_prefix}.npz", **arrays)
@@ -218,11 +236,19 @@ def structure_fixture():
 
 if __name__ == "__main__":
     torch.set_num_threads(os.cpu_count() or 8)
+    if "--only-plain" in sys.argv:  # just the §8f row-1 fixtures
+        for i, name in enumerate(VARIANTS):
+            step_fixture(name, B=4, T=128, steps=3, wseed=1101 + i, bseed=2101 + i, tseed=3101 + i,
+                         nseed=4101 + i, out_prefix=f"step_{name}")
+        sys.exit(0)
     structure_fixture()
     jitter_fixture()
     step_fixture("vcc20", B=4, T=128, steps=3, wseed=1001, bseed=2001, tseed=3001, nseed=4001, out_prefix="step_vcc20")
     step_fixture("aishell3", B=4, T=128, steps=3, wseed=1002, bseed=2002, tseed=3002, nseed=4002,
                  out_prefix="step_aishell3")
+    for i, name in enumerate(VARIANTS):
+        step_fixture(name, B=4, T=128, steps=3, wseed=1101 + i, bseed=2101 + i, tseed=3101 + i, nseed=4101 + i,
+                     out_prefix=f"step_{name}")
     for K in (128, 512, 1024):
         vq_fixture(K, 64, 256, 5000 + K, f"vq_K{K}")
     vq_tile_fixture(6001, "vq_tile")

@@ -69,6 +69,43 @@ def test_oracle_train_steps_match_reference(prefix):
         assert close(float(p.detach().double().norm()), meta["params_after"][k]["norm"], 1e-4), k
 
 
+PLAIN = {"vcc20_plain": ("vcc20", {"use_ema": False}),
+         "vcc20_plain_nonorm": ("vcc20", {"use_ema": False, "embed_norm": False}),
+         "aishell3_plain": ("aishell3", {"use_ema": False})}
+
+
+def plain_cfg(name):
+    base, over = PLAIN[name]
+    return dict(cfg_of(base), **over)
+
+
+@pytest.mark.parametrize("name", list(PLAIN))
+def test_oracle_plain_vq_steps_match_reference(name):
+    """Straight-through VectorQuantizer (use_ema: false):
+    losses, perplexity, step-0 gradients (incl. the codebook parameter) and
+    parameters after 3 Adam steps vs the reference run."""
+    meta, arr = load_fixture(f"step_{name}")
+    cfg = plain_cfg(name)
+    torch.set_num_threads(4)
+    tr = OracleTrainer(cfg, seeded_state_dict(cfg, meta["wseed"]))
+    torch.manual_seed(meta["tseed"])
+    np.random.seed(meta["nseed"])
+    for s in range(meta["steps"]):
+        batch = seeded_batch(cfg, meta["B"], meta["T"], meta["bseed"] + s)
+        _, detail = tr.train_step(batch, keep_grads=(s == 0))
+        ref = meta["detail"][s]
+        assert set(detail) == set(ref)
+        for k, v in ref.items():
+            assert close(detail[k], v, 1e-4), (s, k, detail[k], v)
+        if s == 0:
+            np.testing.assert_allclose(tr.last_xhat[:, :, :16].numpy(), arr["xhat0_slice"], rtol=1e-3, atol=1e-3)
+            for k, g in tr.grads.items():
+                gn = float(g.double().norm())
+                assert close(gn, meta["grads"][k]["norm"], 2e-3) or abs(gn - meta["grads"][k]["norm"]) < 1e-8, k
+    for k, p in tr.model.params.items():
+        assert close(float(p.detach().double().norm()), meta["params_after"][k]["norm"], 1e-4), k
+
+
 @pytest.mark.parametrize("K", [128, 512, 1024])
 def test_oracle_vq_matches_reference(K):
     from oracle.vqvae_cpu import OracleVQVAE
