@@ -339,6 +339,33 @@ int vqx_adam_hyper(int64_t* step, double lr0, double gamma, int32_t step_size, d
 int vqx_adam_step(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper,
                   const float* sumsq, float max_norm, vqx_stream_t stream);
 
+/*
+ * Straight-through VectorQuantizer (use_ema: false; layers_vq.py:9-163,
+ * reduction 'frame_mean', target_norm 1.0, z_dim 128).
+ * vqx_vq_normalize (embed_norm: true): the codebook parameter E [K][D] is
+ *   renormalised in place (embed_norm(), :28-33) and emb_norm = E/||E||
+ *   (:99), e_len = ||E|| after that step; z_norm = z/||z|| (:97), z_len =
+ *   ||z||; normloss_out = sum (z_norm - z)^2 (:125-126; partials >= N/4+1).
+ *   Then vqx_vq_forward(z_norm, emb_norm, ..., bsum, bcnt) gives idx, z_q,
+ *   the commitment sum and the per-code sums/counts the backward uses.
+ * vqx_vq_perplexity: exp(-sum p log(p + 1e-10)), p = counts/N (:112-114).
+ * vqx_vq_plain_bwd: gradients of x_loss + z_qut + beta*z_enc (scale =
+ *   2/(B*T)): dz [N][D] (dtype) from the decoder's straight-through gradient
+ *   dzq (zeroed on frames the Jitter replaced: src_t[t] != t; NULL = no
+ *   jitter) plus the commitment / normalisation terms through z/||z||, and
+ *   the codebook-parameter gradient dE [K][D] f32 (overwritten) through
+ *   E/||E|| (or directly when normalize = 0, emb = E).
+ */
+int vqx_vq_normalize(const float* z, int64_t n_rows, int32_t D, float* E, int32_t K, float* z_norm,
+                     float* z_len, float* emb_norm, float* e_len, float* partials, float* normloss_out,
+                     vqx_stream_t stream);
+int vqx_vq_perplexity(const float* counts, int32_t K, int64_t n_rows, float* out, vqx_stream_t stream);
+int vqx_vq_plain_bwd(const float* z, const float* z_norm, const float* z_len, const float* zq,
+                     const void* dzq, const int32_t* src_t, int32_t T, int64_t n_rows, int32_t D,
+                     int32_t normalize, float beta, float scale, void* dz, int32_t dtype, const float* bsum,
+                     const float* bcnt, const float* emb, const float* e_len, int32_t K, float* dE,
+                     vqx_stream_t stream);
+
 /* dst[r][c] = act(scale * src[r][c]) with dtype conversion (act = VQX_PRO_*;
  * the decoder's ReLU(sqrt(1/11) * skip) operand, vqvae.py:316-317). */
 int vqx_scale_act_2d(const void* src, int32_t ld_src, int32_t src_dtype, void* dst, int32_t ld_dst,
@@ -371,7 +398,7 @@ int vqx_probe_count(int64_t* n);
 int vqx_probe_read(int64_t i, int32_t* info5, double* flops, float* ms);
 
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
-#define VQX_ABI_VERSION 107
+#define VQX_ABI_VERSION 108
 int vqx_version(void);
 
 #ifdef __cplusplus

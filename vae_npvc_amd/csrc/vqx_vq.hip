@@ -379,3 +379,180 @@ extern "C" int vqx_vq_commit_bwd(const float* z, const float* zq, int64_t count,
                        (float*)dz);
   return launch_status("vqx_vq_commit_bwd");
 }
+
+// ===================================================================
+// Straight-through VectorQuantizer (use_ema: false; layers_vq.py:9-163,
+// reduction 'frame_mean', target_norm 1.0).  One wave per 128-wide row.
+// ===================================================================
+namespace {
+
+__device__ __forceinline__ float wave_sum64(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Blocks [0, ceil(K/4)) renormalise the codebook rows, the rest the frames.
+//   codebook (embed_norm, layers_vq.py:28-33, then :99): E *= 1/||E|| in
+//     place, embn = (1.0*E)/||E||, e_len = ||E|| (after the in-place step);
+//   frames (:97): z_norm = (1.0*z)/||z||, z_len = ||z||, and the per-block
+//     sum of (z_norm - z)^2 (normalisation loss, :125-126).
+__global__ __launch_bounds__(256) void vq_normalize_kernel(const float* __restrict__ z, int64_t N, float* __restrict__ E,
+                                                           int K, float* __restrict__ zn, float* __restrict__ zlen,
+                                                           float* __restrict__ embn, float* __restrict__ elen,
+                                                           float* __restrict__ part) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int kb = (K + 3) / 4;
+  __shared__ float red[4];
+  if ((int)blockIdx.x < kb) {
+    const int k = blockIdx.x * 4 + w;
+    if (k >= K) return;
+    float2 e = *(const float2*)(E + (int64_t)k * 128 + 2 * lane);
+    const float n1 = sqrtf(wave_sum64(e.x * e.x + e.y * e.y));
+    const float f = 1.0f / n1;
+    e.x *= f;
+    e.y *= f;
+    *(float2*)(E + (int64_t)k * 128 + 2 * lane) = e;
+    const float n2 = sqrtf(wave_sum64(e.x * e.x + e.y * e.y));
+    *(float2*)(embn + (int64_t)k * 128 + 2 * lane) = make_float2(e.x / n2, e.y / n2);
+    if (lane == 0) elen[k] = n2;
+    return;
+  }
+  const int64_t n = (int64_t)(blockIdx.x - kb) * 4 + w;
+  float l = 0.f;
+  if (n < N) {
+    const float2 v = *(const float2*)(z + n * 128 + 2 * lane);
+    const float nz = sqrtf(wave_sum64(v.x * v.x + v.y * v.y));
+    const float2 u = make_float2(v.x / nz, v.y / nz);
+    *(float2*)(zn + n * 128 + 2 * lane) = u;
+    if (lane == 0) zlen[n] = nz;
+    l = wave_sum64((u.x - v.x) * (u.x - v.x) + (u.y - v.y) * (u.y - v.y));
+  }
+  if (lane == 0) red[w] = l;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x - kb] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// perplexity exp(-sum p log(p + 1e-10)), p = counts / N (layers_vq.py:112-114)
+__global__ __launch_bounds__(256) void vq_perplexity_kernel(const float* __restrict__ cnt, int K, float inv_n,
+                                                            float* __restrict__ out) {
+  __shared__ float red[16];
+  float h = 0.f;
+  for (int k = threadIdx.x; k < K; k += 256) {
+    const float p = cnt[k] * inv_n;
+    h += p * logf(p + 1e-10f);
+  }
+  h = vqx::block_sum(h, red);
+  if (threadIdx.x == 0) *out = expf(-h);
+}
+
+// Backward of  loss = x_loss + z_qut + beta * z_enc  through the quantizer.
+// frames n: dzn = st(dzq_n) + beta*s*(zn - zq) [+ beta*s*(zn - z)]; with
+//   normalisation dz = (dzn - zn (zn.dzn)) / ||z|| - beta*s*(zn - z), else
+//   dz = dzn.  st(): the straight-through gradient from the decoder, zero on
+//   frames the Jitter replaced (its copy comes from a detached tensor,
+//   layers_vq.py:356,377).
+// codes k: d = s*(cnt_k*emb_k - bsum_k) (= sum over the code's frames of
+//   2(zq - zn)/(B*T), z_qut), then dE = (d - emb (emb.d)) / e_len through
+//   emb = E/||E||, or dE = d without normalisation.
+template <typename T>
+__global__ __launch_bounds__(256) void vq_plain_bwd_kernel(const float* __restrict__ z, const float* __restrict__ zn,
+                                                           const float* __restrict__ zlen, const float* __restrict__ zq,
+                                                           const T* __restrict__ dzq, const int* __restrict__ src_t,
+                                                           int Tn, int64_t N, int normalize, float beta, float s,
+                                                           T* __restrict__ dz, const float* __restrict__ bsum,
+                                                           const float* __restrict__ bcnt,
+                                                           const float* __restrict__ emb, const float* __restrict__ elen,
+                                                           int K, float* __restrict__ dE) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int kb = (K + 3) / 4;
+  if ((int)blockIdx.x < kb) {
+    const int k = blockIdx.x * 4 + w;
+    if (k >= K) return;
+    const float2 e = *(const float2*)(emb + (int64_t)k * 128 + 2 * lane);
+    const float2 b = *(const float2*)(bsum + (int64_t)k * 128 + 2 * lane);
+    const float c = bcnt[k];
+    float2 d = make_float2(s * (c * e.x - b.x), s * (c * e.y - b.y));
+    if (normalize) {
+      const float dot = wave_sum64(e.x * d.x + e.y * d.y);
+      const float il = 1.0f / elen[k];
+      d = make_float2((d.x - e.x * dot) * il, (d.y - e.y * dot) * il);
+    }
+    *(float2*)(dE + (int64_t)k * 128 + 2 * lane) = d;
+    return;
+  }
+  const int64_t n = (int64_t)(blockIdx.x - kb) * 4 + w;
+  if (n >= N) return;
+  const int64_t o = n * 128 + 2 * lane;
+  const float2 u = *(const float2*)(zn + o);
+  const float2 q = *(const float2*)(zq + o);
+  float g0 = 0.f, g1 = 0.f;
+  const int t = (int)(n % Tn);
+  if (dzq && (!src_t || src_t[t] == t)) {
+    g0 = Elem<T>::ld(dzq, o);
+    g1 = Elem<T>::ld(dzq, o + 1);
+  }
+  const float bs = beta * s;
+  float d0 = g0 + bs * (u.x - q.x), d1 = g1 + bs * (u.y - q.y);
+  if (normalize) {
+    const float2 v = *(const float2*)(z + o);
+    d0 += bs * (u.x - v.x);
+    d1 += bs * (u.y - v.y);
+    const float dot = wave_sum64(u.x * d0 + u.y * d1);
+    const float il = 1.0f / zlen[n];
+    d0 = (d0 - u.x * dot) * il - bs * (u.x - v.x);
+    d1 = (d1 - u.y * dot) * il - bs * (u.y - v.y);
+  }
+  Elem<T>::st(dz, o, d0);
+  Elem<T>::st(dz, o + 1, d1);
+}
+
+}  // namespace
+
+extern "C" int vqx_vq_normalize(const float* z, int64_t n_rows, int32_t D, float* E, int32_t K, float* z_norm,
+                                float* z_len, float* emb_norm, float* e_len, float* partials, float* normloss_out,
+                                vqx_stream_t stream) {
+  if (D != 128) { set_error("vqx_vq_normalize: z_dim must be 128"); return -1; }
+  if (!z || !E || !z_norm || !z_len || !emb_norm || !e_len || !partials || n_rows < 1 || K < 1) {
+    set_error("vqx_vq_normalize: bad arguments");
+    return -1;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int kb = (K + 3) / 4;
+  const int64_t zb = (n_rows + 3) / 4;
+  hipLaunchKernelGGL(vq_normalize_kernel, dim3((unsigned)(kb + zb)), dim3(256), 0, s, z, n_rows, E, K, z_norm, z_len,
+                     emb_norm, e_len, partials);
+  if (normloss_out) hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(1024), 0, s, partials, (int)zb, 1.0f, normloss_out);
+  return launch_status("vqx_vq_normalize");
+}
+
+extern "C" int vqx_vq_perplexity(const float* counts, int32_t K, int64_t n_rows, float* out, vqx_stream_t stream) {
+  if (!counts || !out || K < 1 || n_rows < 1) { set_error("vqx_vq_perplexity: bad arguments"); return -1; }
+  hipLaunchKernelGGL(vq_perplexity_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, counts, K, 1.0f / (float)n_rows, out);
+  return launch_status("vqx_vq_perplexity");
+}
+
+extern "C" int vqx_vq_plain_bwd(const float* z, const float* z_norm, const float* z_len, const float* zq,
+                                const void* dzq, const int32_t* src_t, int32_t T, int64_t n_rows, int32_t D,
+                                int32_t normalize, float beta, float scale, void* dz, int32_t dtype, const float* bsum,
+                                const float* bcnt, const float* emb, const float* e_len, int32_t K, float* dE,
+                                vqx_stream_t stream) {
+  if (D != 128) { set_error("vqx_vq_plain_bwd: z_dim must be 128"); return -1; }
+  if (!z_norm || !zq || !dz || !bsum || !bcnt || !emb || !dE || T < 1 || n_rows < 1 || K < 1 ||
+      (normalize && (!z || !z_len || !e_len))) {
+    set_error("vqx_vq_plain_bwd: bad arguments");
+    return -1;
+  }
+  const int kb = (K + 3) / 4;
+  const int64_t zb = (n_rows + 3) / 4;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == VQX_BF16)
+    hipLaunchKernelGGL(vq_plain_bwd_kernel<bf16_t>, dim3((unsigned)(kb + zb)), dim3(256), 0, s, z, z_norm, z_len, zq,
+                       (const bf16_t*)dzq, src_t, T, n_rows, normalize, beta, scale, (bf16_t*)dz, bsum, bcnt, emb, e_len,
+                       K, dE);
+  else
+    hipLaunchKernelGGL(vq_plain_bwd_kernel<float>, dim3((unsigned)(kb + zb)), dim3(256), 0, s, z, z_norm, z_len, zq,
+                       (const float*)dzq, src_t, T, n_rows, normalize, beta, scale, (float*)dz, bsum, bcnt, emb, e_len,
+                       K, dE);
+  return launch_status("vqx_vq_plain_bwd");
+}

@@ -84,6 +84,13 @@ class Workspace:
         self.zq_c = e(N, Z)
         self.zq_j = e(N, Z) if d["jitter_p"] > 0 else None
         self.src_t = torch.empty(T, device=dev, dtype=torch.int32)
+        self.jittered = False
+        if eng.plain:  # straight-through quantizer: normalised frames / codebook and their norms
+            self.z_norm = e(N, Z, dt=F32)
+            self.z_len = e(N, dt=F32)
+            self.embn = e(K, Z, dt=F32)
+            self.e_len = e(K, dt=F32)
+            self.pv_part = e(N // 4 + 8, dt=F32)
         self.vq_part = e((N + 63) // 64, dt=F32)
         # EMA statistics bundle (all-reduced as one buffer in data parallel)
         self.ema = e(K * D + K + K * D, dt=F32)
@@ -123,6 +130,7 @@ class Workspace:
         self.dgam_b = e(B * 2 * max(Cd, C), dt=F32)
         self.dbet_b = e(B * 2 * max(Cd, C), dt=F32)
         self.dz = e(N, Z)
+        self.dzq = e(N, Z) if eng.plain else None  # decoder gradient w.r.t. its (jittered) input
         self.dc = [e(N, C) for _ in range(2)]
         self.dh = e(N, C)
         self.tmp = e(N, C)
@@ -156,6 +164,9 @@ class VQVAEEngine:
                              F=dec.final_ch, cond=dec.cond_ch, nd=dec.n_stacks, K=model.quantizer.z_num,
                              ydim=model.embeds._embedding.weight.shape[1], jitter_p=model.jitter.probability)
         assert d["Z"] == 128 and model.quantizer.z_dim == 128, "the fused VQ kernel is built for z_dim = 128"
+        # straight-through VectorQuantizer (use_ema: false)
+        self.plain = not model.use_ema
+        self.vq_normalize = bool(getattr(model.quantizer, "normalize", False)) if self.plain else False
         self._flatten()
         self._build_layers()
         self._ws = {}
@@ -456,7 +467,8 @@ class VQVAEEngine:
         reduction='frame_mean', layers_vq.py:292,315)."""
         T, N, ns, C = w.T, w.N, self.dims["ns"], self.dims["C"]
         B = w.B
-        ops.vq_commit_bwd(w.z, w.zq, 2.0 * self.m.beta * grad_scale / N, w.dz)
+        if not self.plain:  # EMA: the commitment term is the encoder's only gradient
+            ops.vq_commit_bwd(w.z, w.zq, 2.0 * self.m.beta * grad_scale / N, w.dz)
         eo = self.enc_out
         tb = w.bwd_tables
         self.bias_grad(eo, w.dz, w)
@@ -525,8 +537,10 @@ class VQVAEEngine:
         cond = self.dec_cond[0]
         ops.linear_batched_bwd(w.cond_table, w.yemb, B, cond.cin, cond.cout, w.dyemb, w.lin_part)
         ops.weight_norm_bwd(tb["cond"])
-        dx1 = cur[:, :Cd]  # dL/dx_1, the ConvT0 output; z_vq itself receives no gradient
+        dx1 = cur[:, :Cd]  # dL/dx_1, the ConvT0 output
         self.wgrad(self.dec0, dx1, w.zq_in, T)
+        if self.plain:  # straight-through VQ: the decoder input's gradient reaches the encoder
+            self.dgrad(self.dec0, dx1, w.dzq, T)
         ops.weight_norm_bwd(tb["dec0"])
         emb_g = self.g(self.m.embeds._embedding.weight)
         ops.zero_(emb_g)
@@ -552,7 +566,32 @@ class VQVAEEngine:
         q.mark_initialized()
         return True
 
+    def vq_plain_forward(self, w):
+        """VectorQuantizer.forward (layers_vq.py:79-150): renormalise the
+        codebook parameter in place and the frames, nearest code, per-code
+        sums / counts (for the codebook gradient) and the perplexity."""
+        q = self.m.quantizer
+        ops.zero_(w.ema)
+        if self.vq_normalize:
+            ops.vq_normalize(w.z, q.embeddings.data, w.z_norm, w.z_len, w.embn, w.e_len, w.pv_part, w.stats[2:3])
+            zin, emb = w.z_norm, w.embn
+        else:
+            zin, emb = w.z, q.embeddings.data
+        ops.vq_forward(zin, emb, w.idx, w.zq, w.zq_c, w.stats[1:2], w.vq_part, w.bsum, w.bcnt)
+        ops.vq_perplexity(w.bcnt, w.N, w.stats[4:5])
+
+    def vq_plain_backward(self, w):
+        """Straight-through + codebook + commitment (+ normalisation) gradients."""
+        q = self.m.quantizer
+        zin = w.z_norm if self.vq_normalize else w.z
+        emb = w.embn if self.vq_normalize else q.embeddings.data
+        ops.vq_plain_bwd(w.z, zin, w.z_len if self.vq_normalize else None, w.zq, w.dzq,
+                         w.src_t if w.jittered else None, w.T, self.vq_normalize, float(self.m.beta), 2.0 / w.N,
+                         w.dz, w.bsum, w.bcnt, emb, w.e_len if self.vq_normalize else None, self.g(q.embeddings))
+
     def vq_forward_train(self, w):
+        if self.plain:
+            return self.vq_plain_forward(w)
         q = self.m.quantizer
         K = self.dims["K"]
         self.vq_init_if_needed(w)
@@ -568,6 +607,8 @@ class VQVAEEngine:
             self._ema_work = self.comm.all_reduce_sum(w.ema, async_op=True)
 
     def vq_ema_update(self, w):
+        if self.plain:  # the straight-through codebook is a parameter updated by Adam
+            return
         q = self.m.quantizer
         if getattr(self, "_ema_work", None) is not None:
             self._ema_work.wait()
@@ -590,16 +631,29 @@ class VQVAEEngine:
         self.encoder_fwd(w, x)
         self.vq_forward_train(w)
         w.zq_in = w.zq_c
+        w.jittered = False
         if self.dims["jitter_p"] > 0 and self.m.jitter.training:
             src = torch.from_numpy(self.jitter_map(T)).pin_memory()
             w.src_t.copy_(src, non_blocking=True)
             ops.time_gather(w.zq_c, w.zq_j, B, T, w.src_t)
             w.zq_in = w.zq_j
+            w.jittered = True
         self.decoder_fwd(w, w.zq_in)
         ops.logloss_fwd_bwd(x, w.xhat, 1.0 / (B * T), w.dxhat, w.stats[0:1], w.loss_part)
         return w
 
     def backward(self, w, grad_loss=None):
+        if self.plain:
+            # straight-through: the encoder's gradient comes through the decoder
+            self.decoder_bwd(w)
+            self.vq_plain_backward(w)
+            if self.world > 1:
+                self.comm.grads_ready(self.flat_g, self.enc_end, self.n_params)
+            self.encoder_bwd(w)
+            if self.world > 1:
+                self.comm.grads_ready(self.flat_g, 0, self.enc_end)
+                self.comm.finish()
+            return
         self.encoder_bwd(w)
         if self.world > 1:
             self.comm.grads_ready(self.flat_g, 0, self.enc_end)
@@ -640,10 +694,26 @@ class VQVAEEngine:
         self.vq_ema_update(w)
         return w
 
+    def total_loss(self, w):
+        """(total, VQ loss) device scalars of the step's loss (vqvae.py:83)."""
+        n = w.N
+        xl = w.stats[0:1]
+        if self.plain:
+            qut = w.stats[1:2] / n
+            enc = (w.stats[1:2] + w.stats[2:3]) / n
+            return (xl + qut) + self.m.beta * enc, enc
+        vq = w.stats[1:2] / n
+        return xl + self.m.beta * vq, vq
+
     def loss_detail(self, w, stats_host):
-        """The reference's loss dict (vqvae.py:85-87, layers_vq.py:228-233)."""
+        """The reference's loss dict (vqvae.py:85-87, layers_vq.py:228-233 / 112-116)."""
         s = stats_host.tolist()
         n = w.N
+        if self.plain:
+            f = np.float32
+            qut, enc, xl = f(s[1]) / f(n), (f(s[1]) + f(s[2])) / f(n), f(s[0])
+            return {"Total": float((xl + qut) + f(self.m.beta) * enc), "VQ loss": float(enc), "X like": float(xl),
+                    "entropy": s[4]}
         vq = s[1] / n
         xl = s[0]
         d = {"Total": float(np.float32(xl) + np.float32(self.m.beta) * np.float32(vq)), "VQ loss": vq, "X like": xl}
@@ -660,7 +730,10 @@ class VQVAEEngine:
         self.embed_and_cond(w, w.y_dev)
         self.encoder_fwd(w, x)
         q = self.m.quantizer
-        ops.vq_forward(w.z, q.embeddings, w.idx, w.zq, w.zq_c, w.stats[1:2], w.vq_part, None, None)
+        if self.plain:  # VectorQuantizer.forward renormalises in eval too (layers_vq.py:95-101)
+            self.vq_plain_forward(w)
+        else:
+            ops.vq_forward(w.z, q.embeddings, w.idx, w.zq, w.zq_c, w.stats[1:2], w.vq_part, None, None)
         w.zq_in = w.zq_c
         self.decoder_fwd(w, w.zq_c)
         ops.logloss_fwd_bwd(x, w.xhat, 1.0 / (B * T), None, w.stats[0:1], w.loss_part)
@@ -674,6 +747,8 @@ class VQVAEEngine:
         self.pack_weights()
         self.encoder_fwd(w, x)
         q = self.m.quantizer
+        if self.plain:
+            return q.encode(w.z.view(B, T, -1), time_last=False)
         ops.vq_forward(w.z, q.embeddings, w.idx, None, None, None, w.vq_part, None, None)
         return w.idx.view(B, T).clone()
 
@@ -685,7 +760,7 @@ class VQVAEEngine:
         self.pack_weights()
         self.embed_and_cond(w, w.y_dev)
         q = self.m.quantizer
-        ops.gather_rows(q.embeddings, z_idx.reshape(-1).contiguous(), w.zq)
+        ops.gather_rows(q._codebook() if self.plain else q.embeddings, z_idx.reshape(-1).contiguous(), w.zq)
         ops.convert_2d(w.zq, w.zq_c)
         self.decoder_fwd(w, w.zq_c)
         ops.ntc_to_nct(w.xhat, w.xhat_nct)

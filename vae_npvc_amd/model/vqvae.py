@@ -17,7 +17,7 @@ import torch.nn as nn
 
 from ..engine.step import VQVAEEngine
 from .layers import Conditions, ResidualBlock, ResSkipBlock, WNConv1d
-from .layers_vq import EMAVectorQuantizer, Jitter
+from .layers_vq import EMAVectorQuantizer, Jitter, VectorQuantizer
 
 
 def _single(lst, what):
@@ -78,9 +78,7 @@ class _StepFunction(torch.autograd.Function):
     def forward(ctx, engine, x, y, *params):
         w = engine.forward_train(x, y)
         ctx.engine, ctx.w = engine, w
-        loss = w.stats[0:1].clone()  # x_loss; beta * z_enc_loss is added below
-        vq = w.stats[1:2] / w.N
-        total = loss + engine.m.beta * vq
+        total, vq = engine.total_loss(w)
         stats = w.stats.clone()
         ctx.mark_non_differentiable(vq, stats)
         return total.view(()), vq.view(()), stats
@@ -104,11 +102,12 @@ class Model(nn.Module):
         self.encoder = Encoder(**arch["encoder"])
         self.decoder = Decoder(**arch["decoder"])
         self.use_ema = arch.get("use_ema", False)
-        if not self.use_ema:
-            raise NotImplementedError("use_ema: false (plain VectorQuantizer) is SURVEY §8f 'next' #1; "
-                                      "the baseline recipes use the EMA quantizer")
-        self.quantizer = EMAVectorQuantizer(arch.get("z_num", 512), arch.get("z_dim", 128), arch.get("mu", 0.9),
-                                            reduction="frame_mean")
+        if self.use_ema:
+            self.quantizer = EMAVectorQuantizer(arch.get("z_num", 512), arch.get("z_dim", 128), arch.get("mu", 0.9),
+                                                reduction="frame_mean")
+        else:  # straight-through codebook, L2-normalised by default (vqvae.py:26-32)
+            self.quantizer = VectorQuantizer(arch.get("z_num", 512), arch.get("z_dim", 128),
+                                             normalize=arch.get("embed_norm", True), reduction="frame_mean")
         self.embeds = Conditions(arch.get("y_num", 10), arch.get("y_dim", 128))
         self.jitter = Jitter(probability=arch.get("jitter_p", 0.0))
         self.beta = arch.get("beta", 0.01)
@@ -142,12 +141,11 @@ class Model(nn.Module):
             detail = eng.loss_detail(w, stats.cpu())
             return xhat, total, detail
         w = eng.forward_eval(x, y_idx)
-        stats = w.stats.cpu()
-        n = w.N
-        vq = stats[1].item() / n
-        xl = stats[0].item()
-        total = torch.tensor(xl + self.beta * vq, device=x.device)
-        return w.xhat_nct.clone(), total, {"Total": float(total), "VQ loss": vq, "X like": xl}
+        d = eng.loss_detail(w, w.stats.cpu())
+        detail = {k: d[k] for k in ("Total", "VQ loss", "X like")}
+        if "entropy" in d and eng.plain:  # VectorQuantizer reports perplexity in eval too
+            detail["entropy"] = d["entropy"]
+        return w.xhat_nct.clone(), torch.tensor(d["Total"], device=x.device), detail
 
     def encode(self, input):
         x = input[0] if isinstance(input, (list, tuple)) else input

@@ -375,3 +375,19 @@ def scale_act_2d(src, dst, scale, act, rows=None, cols=None):
     call("vqx_scale_act_2d", ptr(src), src.stride(0), dt_code(src.dtype), ptr(dst), dst.stride(0), dt_code(dst.dtype),
          rows, cols, scale, act, stream_ptr())
     return dst
+
+
+def vq_normalize(z, E, z_norm, z_len, emb_norm, e_len, partials, normloss_out=None):
+    """embed_norm() in place on E, emb_norm = E/||E||, z_norm = z/||z|| (+ sum (z_norm - z)^2)."""
+    call("vqx_vq_normalize", ptr(z), z.shape[0], z.shape[1], ptr(E), E.shape[0], ptr(z_norm), ptr(z_len),
+         ptr(emb_norm), ptr(e_len), ptr(partials), ptr(normloss_out), stream_ptr())
+
+
+def vq_perplexity(counts, n_rows, out):
+    call("vqx_vq_perplexity", ptr(counts), counts.shape[0], n_rows, ptr(out), stream_ptr())
+
+
+def vq_plain_bwd(z, z_norm, z_len, zq, dzq, src_t, T, normalize, beta, scale, dz, bsum, bcnt, emb, e_len, dE):
+    call("vqx_vq_plain_bwd", ptr(z), ptr(z_norm), ptr(z_len), ptr(zq), ptr(dzq), ptr(src_t), T, zq.shape[0],
+         zq.shape[1], int(normalize), beta, scale, ptr(dz), dt_code(dz.dtype), ptr(bsum), ptr(bcnt), ptr(emb),
+         ptr(e_len), emb.shape[0], ptr(dE), stream_ptr())
