@@ -5,7 +5,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/$TAG
 mkdir -p $O
-timeout -k 10 900 python -m pytest tests -m gpu -q -rs --timeout 300 > $O/tests.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rs --timeout 300 --timeout-method thread > $O/tests.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> $O/tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 VQX_BENCH_KERNELS=2 timeout -k 10 400 python bench.py > $O/bench.log 2>&1
