@@ -380,9 +380,9 @@ int vqx_convert_2d(const void* src, int32_t ld_src, int32_t src_dtype, void* dst
 
 /* Thread-local description of the last failure. */
 const char* vqx_last_error(void);
-/* Conv GEMM tile height: 0 = automatic (currently 128 rows), 1 = 128 rows
- * (2 workgroups of 4 waves per CU), 2 = 256 rows (1 workgroup of 8 waves per
- * CU).  Process-wide; the default comes from env VQX_GEMM_SUB. */
+/* bf16 conv GEMM pipeline (K-tile depth BK x LDS-DMA ring depth): 0 =
+ * automatic (= 1), 1 = BK 64 x 2-deep, 2 = BK 32 x 4-deep (A/B only).
+ * Process-wide; the default comes from env VQX_GEMM_VARIANT. */
 int vqx_set_gemm_tile(int32_t policy);
 
 /* Launch probe (measurement only; not reentrant while enabled).  While on,

@@ -15,9 +15,10 @@ def _ops():
     return ops
 
 
-@pytest.fixture(params=[1, 2], ids=["tile128", "tile256"])
+@pytest.fixture(params=[1, 2], ids=["bk64x2", "bk32x4"])
 def tile(request):
-    """Run a GEMM test with the 128-row and with the 256-row (8-wave) tile."""
+    """Run a GEMM test with every bf16 pipeline variant (K-tile depth x ring
+    depth, vqx_gemm_inst.h); f32 has one pipeline."""
     from vae_npvc_amd import _lib as L
     L.call("vqx_set_gemm_tile", request.param)
     yield request.param

@@ -1,0 +1,7 @@
+# Build the GEMM lab binaries (one per lab mode) for gfx950, in parallel.
+cd "$(dirname "$0")"
+for m in 0 1 2; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=fast -I ../../include -DVQX_LAB_MODE=$m gemm_lab.hip -o gemm_lab_m$m &
+done
+wait
+ls -la gemm_lab_m*

@@ -16,8 +16,9 @@ PKG = HERE.parent
 ROOT = PKG.parent
 OUT_DIR = PKG / "lib"
 LIB = OUT_DIR / "libvqx.so"
-SOURCES = ["vqx_runtime.hip", "vqx_gemm.hip", "vqx_vq.hip", "vqx_misc.hip"]
-HEADERS = ["vqx_common.h", str(ROOT / "include" / "vqx.h")]
+SOURCES = ["vqx_runtime.hip", "vqx_gemm.hip", "vqx_gemm_fwd.hip", "vqx_gemm_dgrad.hip", "vqx_gemm_wgrad.hip",
+           "vqx_vq.hip", "vqx_misc.hip"]
+HEADERS = ["vqx_common.h", "vqx_gemm_kernel.h", "vqx_gemm_inst.h", str(ROOT / "include" / "vqx.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=fast",
@@ -42,7 +43,7 @@ def _compile(src: Path, obj: Path, force: bool):
     return obj, "built"
 
 
-def build(force: bool = False, jobs: int = 4, verbose: bool = True) -> Path:
+def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> Path:
     OUT_DIR.mkdir(exist_ok=True)
     objdir = OUT_DIR / "obj"
     objdir.mkdir(exist_ok=True)
@@ -65,7 +66,7 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = True) -> Path:
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
-    ap.add_argument("-j", type=int, default=4)
+    ap.add_argument("-j", type=int, default=8)
     a = ap.parse_args()
     build(force=a.force, jobs=a.j)
     sys.exit(0)

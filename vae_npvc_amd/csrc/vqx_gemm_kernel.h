@@ -1,0 +1,785 @@
+// Conv1d / ConvTranspose1d (stride 1) as implicit-im2col GEMMs on gfx950 MFMA.
+//
+// One kernel template covers the three products of a conv layer:
+//   FWD   Y[n][co]      = sum_{j,ci} pro(x[n+j-pad][ci]) * We[co][j][ci]
+//   DGRAD Y[n][ci]      = sum_{j,co} dy[n+j-pad][co]     * We[co][k-1-j][ci]
+//   WGRAD S[r][j*cd+c]  = sum_n      p[n][r]             * pro(q[n+s(j-pad)][c])
+// Frames (n = b*T + t) are the long GEMM dimension: 16,384 at config 2.
+//
+// Workgroup: 256 threads, 128x128 output tile, 4 waves in 2x2, each wave a
+// 64x64 sub-tile = 2x2 MFMA blocks of 32x32, two workgroups per CU.  bf16:
+// v_mfma_f32_32x32x16_bf16, BK = 32 or 64; f32 (parity mode):
+// v_mfma_f32_32x32x2_f32, BK = 32, an exact fp32 fmaf chain.
+//
+// Staging: LDS-DMA (buffer_load ... lds) through an NST-deep ring of K-tiles
+// (see conv_gemm_kernel).  Loads are raw buffer loads: an offset past the
+// descriptor's range returns zeros, which is how the im2col zero padding at
+// utterance edges, the ragged M/N edges and the K tail are produced without
+// branches.  When a K-tile lies inside one tap (cin % BK == 0: every large
+// layer) the tap shift and the channel offset are folded into a scalar byte
+// shift, so the per-chunk VALU work is one select.  K-contiguous operands
+// live K-major in LDS (ds_read_b128, XOR swizzle); K-strided operands
+// (weights in DGRAD, both operands in WGRAD) are stored as they lie in memory
+// and read with ds_read_b64_tr_b16 (bf16) or ds_read_b32 (f32).
+//
+// The MFMA's first operand is the one whose index is contiguous in the output
+// (channels for FWD/DGRAD, j*cd+c for WGRAD), so each lane ends up holding 4
+// consecutive output elements per register group: the epilogue does vector
+// loads/stores (8 B bf16, 16 B f32) for bias, residual, masks and results.
+#pragma once
+#include "vqx_common.h"
+
+// tools/gemm_lab.hip only: 1 = no operand DMA in the main loop, 2 = no MFMA
+#ifndef VQX_LAB_MODE
+#define VQX_LAB_MODE 0
+#endif
+
+namespace vqx {
+
+constexpr int kBN = 128;  // tile width (and height)
+constexpr unsigned kOOB = 0x80000000u;  // buffer offset that is always out of range -> loads 0
+enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
+
+struct GemmParams {
+  const void* a;   // FWD/DGRAD: activation [N][lda]   WGRAD: p [N][lda]
+  const void* b;   // FWD/DGRAD: packed We [cout_f][ntaps*cin_f]   WGRAD: q [N][ldb]
+  int64_t a_bytes, b_bytes;
+  int64_t n_rows;  // frames
+  int T, lda, ldb;
+  int kcin;        // FWD/DGRAD: channels per tap on the K side
+  int K;           // FWD/DGRAD: ntaps*kcin
+  int Mc, Nc;      // output dims: FWD/DGRAD rows = frames, cols = channels; WGRAD rows = r, cols = j*cd+c
+  int ntaps, pad, sign;
+  int cdim;        // DGRAD: cin of the forward layer (= Nc); WGRAD: c_dim
+  int pro;
+  float pro_scale;
+  int tiles_m, tiles_n, splits;
+  int64_t k_per_split;
+  // epilogue
+  void* y;
+  int ldy, epi, out_f32;
+  const float* bias;
+  const float* rowbias;
+  const void* res;
+  int ldres;
+  const void* mask;
+  int ldmask;
+  float mask_slope, mask_scale;
+  const void* gn_h;
+  int ldgn;
+  const float* gn_mr;
+  const float* gn_gamma;
+  const float* gn_beta;
+  float* out2;
+  int ldo2, split_col, out2_acc;
+  void* y2;
+  int ldy2, epi_act;
+  float* colsum_part;
+  float* stat_part;  // GNSTATS / GNBWD per-(128-row group, column tile) partials
+  int gn_groups, gn_glu;
+};
+
+template <typename T> struct Cfg;
+template <> struct Cfg<bf16_t> { static constexpr int EPC = 8, MNCPR = 16; };
+template <> struct Cfg<float> { static constexpr int EPC = 4, MNCPR = 32; };
+
+__device__ __forceinline__ float apply_pro(float v, int pro, float s) {
+  if (pro == VQX_PRO_LRELU) return v > 0.f ? v : 0.2f * v;
+  if (pro == VQX_PRO_RELU) return v > 0.f ? v : 0.f;
+  if (pro == VQX_PRO_SCALE_RELU) { v = v * s; return v > 0.f ? v : 0.f; }
+  return v;
+}
+
+template <typename T, int PRO>
+__device__ __forceinline__ uint4 pro_chunk(uint4 u, float s) {
+  if constexpr (PRO == VQX_PRO_NONE) {
+    return u;
+  } else if constexpr (sizeof(T) == 2) {
+    unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float lo = __uint_as_float(w[i] << 16), hi = __uint_as_float(w[i] & 0xffff0000u);
+      lo = apply_pro(lo, PRO, s);
+      hi = apply_pro(hi, PRO, s);
+      w[i] = (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  } else {
+    float f[4] = {__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f[i] = apply_pro(f[i], PRO, s);
+    return make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3]));
+  }
+}
+
+__device__ __forceinline__ int tap_of(int k, int c) { return (k >= c) + (k >= 2 * c); }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_at(const void* base, int64_t shift_bytes, int64_t total_bytes) {
+  int64_t rec = total_bytes - shift_bytes;
+  if (rec < 0) rec = 0;
+  if (rec > 0x7fffffff) rec = 0x7fffffff;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + shift_bytes), (short)0, (int)rec, 0x00020000);
+}
+
+__device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+// LDS byte offsets of a 16-B chunk.  K-major rows hold KCH chunks (128-B
+// rows: KCH = 8, 64-B rows: KCH = 4); the swizzle makes each 16-lane group of
+// a 32x32 fragment's ds_read_b128 (rows {0-3,12-15,20-27} / {4-11,16-19,28-31},
+// one chunk column) hit all 64 banks once.
+template <int KCH>
+__device__ __forceinline__ int kswz(int row) {
+  if constexpr (KCH == 8) return (row >> 1) & 7;
+  else return (row >> 2) & 3;
+}
+template <int KCH>
+__device__ __forceinline__ int kmaj_off(int row, int ch) { return row * (16 * KCH) + 16 * (ch ^ kswz<KCH>(row)); }
+__device__ __forceinline__ int mn_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+template <typename T>
+__device__ __forceinline__ int mnmaj_off(int row, int ch) {
+  if constexpr (sizeof(T) == 2) return row * 256 + 16 * (ch ^ mn_swz(row));
+  else return row * 512 + 16 * ch;
+}
+
+// 8 consecutive elements (16 B bf16 / 32 B f32) at p+i
+template <typename T>
+__device__ __forceinline__ void ld8(const void* p, int64_t i, float* f) {
+  if constexpr (sizeof(T) == 2) {
+    const uint4 u = *(const uint4*)((const bf16_t*)p + i);
+    const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f[2 * k] = __uint_as_float(w[k] << 16);
+      f[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+    }
+  } else {
+    const f32x4_t a = *(const f32x4_t*)((const float*)p + i);
+    const f32x4_t b = *(const f32x4_t*)((const float*)p + i + 4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { f[k] = a[k]; f[4 + k] = b[k]; }
+  }
+}
+template <typename T>
+__device__ __forceinline__ void st8(void* p, int64_t i, const float* f) {
+  if constexpr (sizeof(T) == 2) {
+    uint4 u;
+    u.x = (unsigned)f2bf(f[0]) | ((unsigned)f2bf(f[1]) << 16);
+    u.y = (unsigned)f2bf(f[2]) | ((unsigned)f2bf(f[3]) << 16);
+    u.z = (unsigned)f2bf(f[4]) | ((unsigned)f2bf(f[5]) << 16);
+    u.w = (unsigned)f2bf(f[6]) | ((unsigned)f2bf(f[7]) << 16);
+    *(uint4*)((bf16_t*)p + i) = u;
+  } else {
+    const f32x4_t a = {f[0], f[1], f[2], f[3]}, b = {f[4], f[5], f[6], f[7]};
+    *(f32x4_t*)((float*)p + i) = a;
+    *(f32x4_t*)((float*)p + i + 4) = b;
+  }
+}
+
+// FWD/DGRAD epilogue on 8 consecutive output channels of one frame, in the
+// order bias, row bias, activation-derivative mask, split to out2 (returns),
+// residual, GroupNorm-apply add, activation, store.
+template <typename T>
+__device__ __forceinline__ void epilogue8(const GemmParams& P, int64_t row, int col, float* v) {
+  const int epi = P.epi;
+  const int bidx = (epi & (VQX_EPI_ROWBIAS | VQX_EPI_GNADD)) ? (int)(row / P.T) : 0;
+  float t[8];
+  if (epi & VQX_EPI_BIAS) {
+    ld8<float>(P.bias, col, t);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += t[e];
+  }
+  if (epi & VQX_EPI_ROWBIAS) {
+    ld8<float>(P.rowbias, (int64_t)bidx * P.Nc + col, t);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += t[e];
+  }
+  if (epi & VQX_EPI_MASK) {
+    ld8<T>(P.mask, row * P.ldmask + col, t);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= (t[e] > 0.f ? 1.f : P.mask_slope) * P.mask_scale;
+  }
+  if ((epi & VQX_EPI_SPLIT) && col >= P.split_col) {  // split_col % 8 == 0
+    float* o2 = P.out2 + row * P.ldo2 + (col - P.split_col);
+    if (P.out2_acc) {
+      ld8<float>(o2, 0, t);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += t[e];
+    }
+    st8<float>(o2, 0, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = 0.f;  // not part of y: no column-sum contribution
+    return;
+  }
+  if (epi & VQX_EPI_RES) {
+    ld8<T>(P.res, row * P.ldres + col, t);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += t[e];
+  }
+  if (epi & VQX_EPI_GNADD) {
+    float ga[8], be[8];
+    ld8<T>(P.gn_h, row * P.ldgn + col, t);
+    ld8<float>(P.gn_gamma, col, ga);
+    ld8<float>(P.gn_beta, col, be);
+    const float mean = P.gn_mr[2 * bidx], rstd = P.gn_mr[2 * bidx + 1];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += (t[e] - mean) * rstd * ga[e] + be[e];
+  }
+  if (epi & (VQX_EPI_ACT | VQX_EPI_ACT2)) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) t[e] = apply_pro(v[e], P.epi_act, 1.f);
+    if (epi & VQX_EPI_ACT2) {
+      st8<T>(P.y2, row * P.ldy2 + col, t);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = t[e];
+    }
+  }
+  if (P.out_f32) st8<float>(P.y, row * P.ldy + col, v);
+  else st8<T>(P.y, row * P.ldy + col, v);
+}
+
+// GNBWD: GroupNorm-backward sums of this output (the GN input's gradient dy)
+// for 8 consecutive channels of one frame: s[0..1] = (sum g*dh, sum g*dh*xhat)
+// of group a, s[2..3] of group b (GLU: u = [a | b], dh through
+// tanh(h_a)*sigmoid(h_b), layers.py:240-242).  u, mean/rstd, gamma, beta are
+// the forward GroupNorm's (gn_h, gn_mr, gn_gamma, gn_beta).
+template <typename T>
+__device__ __forceinline__ void gnbwd8(const GemmParams& P, int64_t row, int col, const float* dy, float* s) {
+  const int b = (int)(row / P.T);
+  float ua[8], ga[8];
+  ld8<T>(P.gn_h, row * P.ldgn + col, ua);
+  ld8<float>(P.gn_gamma, col, ga);
+  if (!P.gn_glu) {
+    const int grp = P.gn_groups == 1 ? 0 : col / (P.Nc / P.gn_groups);
+    const float m = P.gn_mr[(b * P.gn_groups + grp) * 2], r = P.gn_mr[(b * P.gn_groups + grp) * 2 + 1];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float g = ga[e] * dy[e];
+      s[0] += g;
+      s[1] = fmaf(g, (ua[e] - m) * r, s[1]);
+    }
+    return;
+  }
+  const int half = P.Nc;
+  float ub[8], gb[8], ba[8], bb[8];
+  ld8<T>(P.gn_h, row * P.ldgn + col + half, ub);
+  ld8<float>(P.gn_gamma, col + half, gb);
+  ld8<float>(P.gn_beta, col, ba);
+  ld8<float>(P.gn_beta, col + half, bb);
+  const float ma = P.gn_mr[b * 4], ra = P.gn_mr[b * 4 + 1], mb = P.gn_mr[b * 4 + 2], rb = P.gn_mr[b * 4 + 3];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float xa = (ua[e] - ma) * ra, xb = (ub[e] - mb) * rb;
+    const float ta = ftanh(xa * ga[e] + ba[e]);
+    const float sb = fsigmoid(xb * gb[e] + bb[e]);
+    const float dga = ga[e] * (dy[e] * sb * (1.f - ta * ta));
+    const float dgb = gb[e] * (dy[e] * ta * (sb * (1.f - sb)));
+    s[0] += dga;
+    s[1] = fmaf(dga, xa, s[1]);
+    s[2] += dgb;
+    s[3] = fmaf(dgb, xb, s[3]);
+  }
+}
+
+// Fragment-level prologue (LDS-DMA staging cannot transform data in flight).
+template <int PRO>
+__device__ __forceinline__ bf16x8_t pro_frag(bf16x8_t f, float s) {
+  if constexpr (PRO == VQX_PRO_NONE) {
+    return f;
+  } else {
+    uint4 u = __builtin_bit_cast(uint4, f);
+    u = pro_chunk<bf16_t, PRO>(u, s);
+    return __builtin_bit_cast(bf16x8_t, u);
+  }
+}
+template <int PRO>
+__device__ __forceinline__ f32x4_t pro_frag(f32x4_t f, float s) {
+  if constexpr (PRO == VQX_PRO_NONE) {
+    return f;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f[i] = apply_pro(f[i], PRO, s);
+    return f;
+  }
+}
+
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, unsigned off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (VQX_LDS(void)*)lds, 16, (int)off, 0, 0, 0);
+}
+
+// vmcnt immediate from a small runtime count (0..8, 12, 16; anything else waits for all)
+__device__ __forceinline__ void wait_vm(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// Staging layout.  The block tile is 128 x 128 with 4 waves in a 2 x 2 grid
+// of 64 x 64 wave tiles.  A K-tile operand (A rows x BK, or BK x 128 B
+// columns) is 128*BK*sizeof(T) bytes = PIECES pieces of 1 KiB; wave w fills
+// pieces PW*w .. PW*w+PW-1 of each operand, lane l the 16-B chunk
+// c = piece*64+l at LDS byte 16*c (lane-linear, as an LDS-DMA writes).  The
+// XOR swizzle that keeps the fragment reads conflict-free is applied to the
+// SOURCE chunk:
+//   K-major,  RB-byte rows (RB = BK*sizeof(T)):  row = c / (RB/16),
+//             data chunk = (c % (RB/16)) ^ kswz(row)
+//   MN-major (256-B rows, bf16): row = c>>4, data chunk = (c&15) ^ mn_swz(row)
+//   MN-major (512-B rows, f32):  row = c>>5, data chunk = c&31
+// Operands go global -> LDS by buffer_load ... lds (no VGPR staging, no
+// ds_write) through an NST-deep ring: NST-1 K-tiles are in flight while one
+// is multiplied.  A counted vmcnt (this wave's pieces of the tiles still
+// allowed in flight) retires tile kt+1 only, and a raw s_barrier publishes it
+// and frees the buffer of tile kt for tile kt+NST.
+//   BK=64, NST=2: 64 KiB per workgroup (the round-1 pipeline);
+//   BK=32, NST=4: 64 KiB, three 16-KiB K-tiles in flight (bf16 default).
+// Two 4-wave workgroups per CU either way.
+template <typename T, int MODE, int PRO, bool GEN, int BK, int NST>
+__global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
+  using C = Cfg<T>;
+  constexpr int EPC = C::EPC, CPR = C::MNCPR, ES = sizeof(T);
+  constexpr int SUB = 1, BM = 128;
+  constexpr int RB = BK * ES;                 // K-major row bytes (64 or 128)
+  constexpr int KCH = RB / 16;                // 16-B chunks per K-major row
+  constexpr int OP_BYTES = 128 * BK * ES;     // one operand's K-tile
+  constexpr int PW = OP_BYTES / 1024 / 4;     // pieces per wave per operand
+  constexpr int A_BYTES = OP_BYTES, STAGE = 2 * OP_BYTES;
+  constexpr int NP = 2 * PW;                  // DMA pieces per wave per K-tile
+  static_assert(NST * STAGE >= 45056, "epilogue staging needs 44 KiB of LDS");
+  static_assert(BK % (16 / ES * 2) == 0 || ES == 4, "BK");
+  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int tiles_mn = P.tiles_m * P.tiles_n;
+  const int split = lin / tiles_mn;
+  const int tmn = lin - split * tiles_mn;
+  const int tm = tmn / P.tiles_n, tn = tmn - tm * P.tiles_n;
+  const int m0 = tm * BM, n0 = tn * kBN;
+
+  int64_t kbeg = 0, kend;
+  if constexpr (MODE == MODE_WGRAD) {
+    kbeg = (int64_t)split * P.k_per_split;
+    kend = kbeg + P.k_per_split;
+    if (kend > P.n_rows) kend = P.n_rows;
+  } else {
+    kend = P.K;
+  }
+  const int nk = (kend > kbeg) ? (int)((kend - kbeg + BK - 1) / BK) : 0;
+
+  // ---------------- per-thread constant addressing
+  unsigned aoff[PW], boff[PW];
+  int amask[PW];      // FWD/DGRAD: bit j set <=> tap j keeps the frame inside its utterance
+  int bsh[PW];        // WGRAD: krow + shift of the q chunk
+  int ak[PW], bk[PW];  // k offset of the chunk inside the K-tile (elements / rows)
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int c = (PW * wid + i) * 64 + lane;
+    amask[i] = 0;
+    if constexpr (MODE != MODE_WGRAD) {
+      const int row = c / KCH, kch = (c % KCH) ^ kswz<KCH>(row);
+      const int64_t n = (int64_t)m0 + row;
+      const int t = (int)(n % P.T);
+      int msk = 0;
+      if (n < P.n_rows)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) msk |= ((t + j - P.pad >= 0) && (t + j - P.pad < P.T)) ? (1 << j) : 0;
+      amask[i] = msk;
+      ak[i] = kch * EPC;
+      aoff[i] = (unsigned)((n * P.lda + (GEN ? 0 : kch * EPC)) * ES);
+    } else {
+      const int krow = c / CPR;
+      const int cch = (sizeof(T) == 2) ? ((c % CPR) ^ mn_swz(krow)) : (c % CPR);
+      const int r = m0 + cch * EPC;
+      ak[i] = krow;
+      aoff[i] = r < P.Mc ? (unsigned)(((int64_t)krow * P.lda + r) * ES) : kOOB;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int c = (PW * wid + i) * 64 + lane;
+    bsh[i] = 0;
+    if constexpr (MODE == MODE_FWD) {
+      const int row = c / KCH, kch = (c % KCH) ^ kswz<KCH>(row);
+      const int co = n0 + row;
+      bk[i] = kch * EPC;
+      boff[i] = co < P.Nc ? (unsigned)(((int64_t)co * P.K + kch * EPC) * ES) : kOOB;
+    } else if constexpr (MODE == MODE_DGRAD) {
+      const int krow = c / CPR;
+      const int cch = (sizeof(T) == 2) ? ((c % CPR) ^ mn_swz(krow)) : (c % CPR);
+      const int ci = n0 + cch * EPC;
+      bk[i] = krow;
+      boff[i] = ci < P.Nc ? (unsigned)(((int64_t)krow * P.ntaps * P.cdim + ci) * ES) : kOOB;
+      if constexpr (GEN) boff[i] = ci < P.Nc ? (unsigned)(ci * ES) : kOOB;
+    } else {
+      const int krow = c / CPR;
+      const int cch = (sizeof(T) == 2) ? ((c % CPR) ^ mn_swz(krow)) : (c % CPR);
+      const int col = n0 + cch * EPC;
+      const int j = tap_of(col, P.cdim);
+      const int cc = col - j * P.cdim;
+      const int sh = P.sign * (j - P.pad);
+      bk[i] = krow;
+      bsh[i] = krow + sh;
+      // the q descriptor base sits (ntaps-1) rows before the tile so shifted offsets stay >= 0
+      boff[i] = col < P.Nc ? (unsigned)(((int64_t)(krow + sh + P.ntaps - 1) * P.ldb + cc) * ES) : kOOB;
+    }
+  }
+
+  // One buffer descriptor per operand for the whole kernel.  Its base sits
+  // `lo` bytes before the operand (the largest negative im2col shift), so
+  // every in-range offset is non-negative; per K-tile only a scalar byte
+  // shift is added to each lane's offset (an out-of-range sentinel stays out
+  // of range).
+  int64_t a_lo = 0, b_lo = 0;
+  if constexpr (MODE != MODE_WGRAD) a_lo = (int64_t)P.pad * P.lda * ES;
+  if constexpr (MODE == MODE_WGRAD) b_lo = (int64_t)(P.ntaps - 1) * P.ldb * ES;
+  const __amdgpu_buffer_rsrc_t rsA = rsrc_at(P.a, -a_lo, P.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsB = rsrc_at(P.b, -b_lo, P.b_bytes);
+  if constexpr (MODE != MODE_WGRAD) {
+#pragma unroll
+    for (int i = 0; i < PW; ++i) aoff[i] += (unsigned)a_lo;  // rebase to the descriptor
+  }  // WGRAD: boff already carries the (ntaps-1)-row margin b_lo
+  // incremental (tap, channel) position of the next K-tile to load (FWD/DGRAD fast path)
+  int ld_tap = 0, ld_c0 = 0;
+
+  // Byte offsets of K-tile kt's chunks (kOOB where the im2col / edge reads zero).
+  auto tile_offsets = [&](int kt, unsigned (&oa)[PW], unsigned (&ob)[PW]) {
+    const int64_t k0 = kbeg + (int64_t)kt * BK;
+    if constexpr (MODE != MODE_WGRAD) {
+      if constexpr (!GEN) {
+        const int tap = ld_tap, c0 = ld_c0;  // k0 == tap*kcin + c0
+        ld_c0 += BK;
+        if (ld_c0 >= P.kcin) { ld_c0 = 0; ld_tap += 1; }
+        const unsigned ksa = (unsigned)(((tap - P.pad) * P.lda + c0) * ES);
+#pragma unroll
+        for (int i = 0; i < PW; ++i) oa[i] = ((amask[i] >> tap) & 1) ? aoff[i] + ksa : kOOB;
+        unsigned ksb;
+        if constexpr (MODE == MODE_FWD) ksb = (unsigned)(k0 * ES);
+        else  // forward weight We[co][j][ci] read as rows k = (j, co), taps flipped
+          ksb = (unsigned)(((int64_t)c0 * P.ntaps * P.cdim + (int64_t)(P.ntaps - 1 - tap) * P.cdim) * ES);
+#pragma unroll
+        for (int i = 0; i < PW; ++i) ob[i] = boff[i] + ksb;
+      } else {
+#pragma unroll
+        for (int i = 0; i < PW; ++i) {
+          const int k = (int)k0 + ak[i];
+          const int tap = tap_of(k, P.kcin);
+          const int ci = k - tap * P.kcin;
+          const bool ok = k < P.K && ((amask[i] >> tap) & 1);
+          oa[i] = ok ? aoff[i] + (unsigned)((((tap - P.pad) * P.lda) + ci) * ES) : kOOB;
+        }
+        if constexpr (MODE == MODE_FWD) {
+#pragma unroll
+          for (int i = 0; i < PW; ++i) ob[i] = ((int)k0 + bk[i] < P.K) ? boff[i] + (unsigned)(k0 * ES) : kOOB;
+        } else {
+#pragma unroll
+          for (int i = 0; i < PW; ++i) {
+            const int k = (int)k0 + bk[i];
+            const int j = tap_of(k, P.kcin);
+            const int co = k - j * P.kcin;
+            ob[i] = (k < P.K && boff[i] != kOOB)
+                        ? boff[i] + (unsigned)(((int64_t)co * P.ntaps * P.cdim + (P.ntaps - 1 - j) * P.cdim) * ES)
+                        : kOOB;
+          }
+        }
+      }
+    } else {
+      const unsigned ksa = (unsigned)(k0 * P.lda * ES);
+      const unsigned ksb = (unsigned)(k0 * P.ldb * ES);
+      const int t0 = (int)((int)k0 % P.T);
+#pragma unroll
+      for (int i = 0; i < PW; ++i) {
+        unsigned offa = aoff[i] + ksa;
+        if constexpr (GEN) {
+          if (k0 + ak[i] >= kend) offa = kOOB;
+        }
+        oa[i] = offa;
+      }
+#pragma unroll
+      for (int i = 0; i < PW; ++i) {
+        int tt;
+        if constexpr (!GEN) {
+          tt = t0 + bsh[i];
+        } else {
+          const int64_t n = k0 + bk[i];
+          tt = (int)(n % P.T) + (bsh[i] - bk[i]);
+          if (n >= kend) tt = -1;
+        }
+        ob[i] = (tt >= 0 && tt < P.T) ? boff[i] + ksb : kOOB;
+      }
+    }
+  };
+
+  auto dma_tile = [&](int buf, int kt) {
+    unsigned oa[PW], ob[PW];
+    tile_offsets(kt, oa, ob);
+    char* la = smem + buf * STAGE + wid * (PW * 1024);
+    char* lb = smem + buf * STAGE + A_BYTES + wid * (PW * 1024);
+#pragma unroll
+    for (int i = 0; i < PW; ++i) dma16(rsA, la + i * 1024, oa[i]);
+#pragma unroll
+    for (int i = 0; i < PW; ++i) dma16(rsB, lb + i * 1024, ob[i]);
+  };
+
+  // LDS-DMA cannot transform data in flight: the prologue is applied to fragments after ds_read
+  constexpr int FPRO_A = (MODE != MODE_WGRAD) ? PRO : VQX_PRO_NONE;
+  constexpr int FPRO_B = (MODE == MODE_WGRAD) ? PRO : VQX_PRO_NONE;
+
+  // acc[mi][ni]: mi = 32-block of the "row" operand (A tile), ni = of the B tile.
+  // MFMA D = first(32 x k) * second(k x 32): first = B-tile fragment (contiguous
+  // output index), second = A-tile fragment; D[row of first][col of second].
+  f32x16_t acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int r32 = lane & 31, h = lane >> 5;
+
+  auto compute_tile = [&](int buf) {
+    const char* la = smem + buf * STAGE;
+    const char* lb = la + A_BYTES;
+    const int acol = wm * 64;
+    constexpr bool A_KMAJ = (MODE != MODE_WGRAD);
+    constexpr bool B_KMAJ = (MODE == MODE_FWD);
+    if constexpr (sizeof(T) == 2) {
+      constexpr int KS = BK / 16;  // k-steps of v_mfma_f32_32x32x16_bf16
+      const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+      typedef short s16x8_t __attribute__((ext_vector_type(8)));
+      auto tr_frag = [&](const char* base, int colbase, int s) {
+        const int kb = 16 * s + (g >> 1) * 8;
+        const int ch = (colbase >> 3) + (p >> 1);
+        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (VQX_LDS(s16x4_t)*)(base + mnmaj_off<T>(kb + q, ch) + 8 * (p & 1)));
+        const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (VQX_LDS(s16x4_t)*)(base + mnmaj_off<T>(kb + 4 + q, ch) + 8 * (p & 1)));
+        const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(bf16x8_t, v);
+      };
+      bf16x8_t af[KS][2], bfr[KS][2];
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+          if constexpr (A_KMAJ) af[s][x] = *(const bf16x8_t*)(la + kmaj_off<KCH>(wm * 64 + x * 32 + r32, 2 * s + h));
+          else af[s][x] = tr_frag(la, acol + x * 32 + (g & 1) * 16, s);
+          if constexpr (B_KMAJ) bfr[s][x] = *(const bf16x8_t*)(lb + kmaj_off<KCH>(wn * 64 + x * 32 + r32, 2 * s + h));
+          else bfr[s][x] = tr_frag(lb, wn * 64 + x * 32 + (g & 1) * 16, s);
+        }
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+          af[s][x] = pro_frag<FPRO_A>(af[s][x], P.pro_scale);
+          bfr[s][x] = pro_frag<FPRO_B>(bfr[s][x], P.pro_scale);
+        }
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[s][ni], af[s][mi], acc[mi][ni], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < BK / 8; ++s) {
+        f32x4_t af[2], bfr[2];
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+          if constexpr (A_KMAJ) {
+            af[x] = *(const f32x4_t*)(la + kmaj_off<KCH>(wm * 64 + x * 32 + r32, 2 * s + h));
+          } else {
+            const int col = acol + x * 32 + r32;
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) af[x][qq] = *(const float*)(la + (8 * s + 4 * h + qq) * 512 + col * 4);
+          }
+          if constexpr (B_KMAJ) {
+            bfr[x] = *(const f32x4_t*)(lb + kmaj_off<KCH>(wn * 64 + x * 32 + r32, 2 * s + h));
+          } else {
+            const int col = wn * 64 + x * 32 + r32;
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) bfr[x][qq] = *(const float*)(lb + (8 * s + 4 * h + qq) * 512 + col * 4);
+          }
+          af[x] = pro_frag<FPRO_A>(af[x], P.pro_scale);
+          bfr[x] = pro_frag<FPRO_B>(bfr[x], P.pro_scale);
+        }
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
+          for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+              acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(bfr[ni][qq], af[mi][qq], acc[mi][ni], 0, 0, 0);
+      }
+    }
+  };
+
+  if (nk > 0) {
+    // prologue: tiles 0 .. NST-2 in flight, then wait for tile 0
+    const int pre = nk < NST - 1 ? nk : NST - 1;
+#pragma unroll
+    for (int t = 0; t < NST - 1; ++t)
+      if (t < pre) dma_tile(t, t);
+    wait_vm(NP * (pre - 1));
+    __builtin_amdgcn_s_barrier();
+    int buf = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      const int fbuf = (buf + NST - 1) % NST;  // buffer of tile kt+NST-1 == buffer of tile kt-1
+#if VQX_LAB_MODE != 1
+      if (kt + NST - 1 < nk) dma_tile(fbuf, kt + NST - 1);
+#endif
+#if VQX_LAB_MODE != 2
+      compute_tile(buf);
+#endif
+      // tile kt+1 must have landed; tiles kt+2 .. min(nk, kt+NST)-1 may stay in flight
+      int ahead = (kt + NST - 1 < nk ? kt + NST : nk) - (kt + 2);
+      if (ahead < 0) ahead = 0;
+      wait_vm(NP * ahead);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      buf = buf + 1 == NST ? 0 : buf + 1;
+    }
+  }
+
+  // ---------------- epilogue
+  // The accumulator tile goes through LDS one 64-row slab at a time so the
+  // epilogue reads and writes whole rows: 16 lanes x 8 consecutive columns
+  // per row, every global access 16 B and each row segment contiguous.
+  // Lane holds (before the transpose) output row wm*64 + mi*32 + r32 and,
+  // per register group gq, columns wn*64 + ni*32 + 8*gq + 4*h + (0..3).
+  constexpr int EP_LD = kBN + 4;  // floats; +4 keeps the b128 writes conflict-free
+  constexpr int EROWS = 16 * SUB;  // rows per pass
+  float* ep = (float*)smem;                 // [64][EP_LD]
+  float* csr = (float*)(smem + 36864);      // COLSUM reduction [EROWS][kBN]
+  const int er = tid >> 4, ec = (tid & 15) * 8;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // COLSUM accumulators
+  float mn = 0.f, mm = 0.f, mq = 0.f;                       // GNSTATS running (count, mean, M2)
+  float gs[4] = {0.f, 0.f, 0.f, 0.f};                       // GNBWD sums
+  __syncthreads();  // staging buffers are free
+#pragma unroll
+  for (int slab = 0; slab < 2 * SUB; ++slab) {
+    if (wm == slab) {
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int gq = 0; gq < 4; ++gq) {
+            const f32x4_t v = {acc[mi][ni][4 * gq], acc[mi][ni][4 * gq + 1], acc[mi][ni][4 * gq + 2],
+                               acc[mi][ni][4 * gq + 3]};
+            *(f32x4_t*)(ep + (mi * 32 + r32) * EP_LD + wn * 64 + ni * 32 + 8 * gq + 4 * h) = v;
+          }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int pass = 0; pass < 64 / EROWS; ++pass) {
+      const int lr = pass * EROWS + er;
+      const f32x4_t lo = *(const f32x4_t*)(ep + lr * EP_LD + ec);
+      const f32x4_t hi = *(const f32x4_t*)(ep + lr * EP_LD + ec + 4);
+      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const int64_t row = (int64_t)m0 + slab * 64 + lr;
+      const int col = n0 + ec;
+      if constexpr (MODE == MODE_WGRAD) {
+        if (row < P.Mc && col < P.Nc) {  // Nc % 8 == 0
+          float* out = (float*)P.y + (int64_t)split * P.Mc * P.Nc + row * P.Nc + col;
+          st8<float>(out, 0, v);
+        }
+      } else {
+        if (row < P.n_rows && col < P.Nc) {
+          epilogue8<T>(P, row, col, v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) cs[e] += v[e];
+          if (P.epi & VQX_EPI_GNSTATS) {  // two-pass moments of the 8 values, merged
+            float m8 = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) m8 += v[e];
+            m8 *= 0.125f;
+            float q8 = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) q8 = fmaf(v[e] - m8, v[e] - m8, q8);
+            moments_merge(mn, mm, mq, 8.f, m8, q8);
+          }
+          if (P.epi & VQX_EPI_GNBWD) gnbwd8<T>(P, row, col, v, gs);
+        }
+      }
+    }
+    __syncthreads();
+    if constexpr (MODE != MODE_WGRAD) {
+      // per-(128-row group, column tile) GroupNorm partials
+      if ((P.epi & (VQX_EPI_GNSTATS | VQX_EPI_GNBWD)) && (slab & 1)) {
+        const int64_t grp_row = (int64_t)m0 + (slab >> 1) * 128;
+        float* out = P.stat_part + ((grp_row / 128) * P.tiles_n + tn) * 4;
+        if (P.epi & VQX_EPI_GNSTATS) {
+          // merge the 64 lanes of each wave, then the waves (deterministic order)
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) {
+            const float n2 = __shfl_xor(mn, o, 64), m2 = __shfl_xor(mm, o, 64), q2 = __shfl_xor(mq, o, 64);
+            if ((lane & o) == 0) moments_merge(mn, mm, mq, n2, m2, q2);
+            else { float a = n2, b = m2, c = q2; moments_merge(a, b, c, mn, mm, mq); mn = a; mm = b; mq = c; }
+          }
+          if (lane == 0) { csr[3 * wid] = mn; csr[3 * wid + 1] = mm; csr[3 * wid + 2] = mq; }
+          __syncthreads();
+          if (tid == 0 && grp_row < P.n_rows) {
+            float a = csr[0], b = csr[1], c = csr[2];
+            for (int w = 1; w < 4 * SUB; ++w) moments_merge(a, b, c, csr[3 * w], csr[3 * w + 1], csr[3 * w + 2]);
+            out[0] = a; out[1] = b; out[2] = c; out[3] = 0.f;
+          }
+          mn = mm = mq = 0.f;
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            float x = wave_sum(gs[k]);
+            if (lane == 0) csr[4 * wid + k] = x;
+            gs[k] = 0.f;
+          }
+          __syncthreads();
+          if (tid < 4 && grp_row < P.n_rows) {
+            float x = 0.f;
+            for (int w = 0; w < 4 * SUB; ++w) x += csr[4 * w + tid];
+            out[tid] = x;
+          }
+        }
+        __syncthreads();
+      }
+      // per-128-row-group column sums of the stored values (bias gradient of
+      // the layer this output feeds), reduced over the EROWS row lanes in LDS
+      if ((P.epi & VQX_EPI_COLSUM) && (slab & 1)) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          csr[er * kBN + ec + e] = cs[e];
+          cs[e] = 0.f;
+        }
+        __syncthreads();
+        const int64_t grp_row = (int64_t)m0 + (slab >> 1) * 128;
+        if (tid < kBN && n0 + tid < P.Nc && grp_row < P.n_rows) {
+          float t = 0.f;
+#pragma unroll
+          for (int r = 0; r < EROWS; ++r) t += csr[r * kBN + tid];
+          P.colsum_part[(grp_row / 128) * P.Nc + n0 + tid] = t;
+        }
+        __syncthreads();
+      }
+    }
+  }
+}
+
+
+}  // namespace vqx

@@ -1,0 +1,6 @@
+// Instantiations of the conv GEMM for MODE_WGRAD (see vqx_gemm_inst.h).
+#include "vqx_gemm_inst.h"
+
+namespace vqx {
+template void launch_mode_dt<MODE_WGRAD>(const GemmParams&, int, bool, bool, int, hipStream_t);
+}  // namespace vqx
