@@ -322,13 +322,21 @@ class VQVAEEngine:
                                               dW=Lr.slab.view(Lr.rows, Lr.cols), dbias=g(Lr.mod.bias))
                                          for i, Lr in enumerate(self.dec_cond)])
 
+    MAX_EVAL_WS = 4  # inference over variable-length utterances keeps only the latest shapes
+
     def ws(self, B, T, train=True):
         key = (B, T, train)
         w = self._ws.get(key)
         if w is None:
             if train and (B, T, False) in self._ws:
                 del self._ws[(B, T, False)]
+            if not train:
+                evals = [k for k in self._ws if not k[2]]
+                for k in evals[: max(0, len(evals) - self.MAX_EVAL_WS + 1)]:
+                    del self._ws[k]
             w = self._ws[key] = Workspace(self, B, T, train)
+        elif not train:
+            self._ws[key] = self._ws.pop(key)  # most recently used last
         return w
 
     # ------------------------------------------------------------ conv helpers
