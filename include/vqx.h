@@ -339,6 +339,21 @@ int vqx_adam_hyper(int64_t* step, double lr0, double gamma, int32_t step_size, d
 int vqx_adam_step(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper,
                   const float* sumsq, float max_norm, vqx_stream_t stream);
 
+/* RAdam, optim_type: RAdam (replaces trainer/radam.py:5-78 RAdam.step, built
+ * by trainer/basic.py:30-34 with betas (0.5, 0.999), weight_decay 0).
+ * radam_hyper: increments t and writes hyper[9] = {lr_t, -ss*lr_t, rect, t,
+ *   b1, 1-b1, b2, 1-b2, eps}: N_max = 2/(1-b2)-1, N = N_max - 2t b2^t/(1-b2^t);
+ *   rect = N >= 5; ss = sqrt((1-b2^t)(N-4)/(N_max-4)(N-2)/N N_max/(N_max-2))
+ *   / (1-b1^t) when rect, else 1/(1-b1^t) (radam.py:49-59), all in double
+ *   like the Python floats, then rounded to f32; lr_t as adam_hyper (StepLR).
+ * radam_step: g' = coef*g (clip as adam_step); v = v*b2 + ((1-b2)*g')*g';
+ *   m = m*b1 + (1-b1)*g'; p += (-ss*lr) * (m / (sqrt(v) + eps)) when rect,
+ *   else p += (-ss*lr) * m (radam.py:41-42, 64-71). */
+int vqx_radam_hyper(int64_t* step, double lr0, double gamma, int32_t step_size, double beta1,
+                    double beta2, double eps, float* hyper, vqx_stream_t stream);
+int vqx_radam_step(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper,
+                   const float* sumsq, float max_norm, vqx_stream_t stream);
+
 /*
  * Straight-through VectorQuantizer (use_ema: false; layers_vq.py:9-163,
  * reduction 'frame_mean', target_norm 1.0, z_dim 128).
@@ -398,7 +413,7 @@ int vqx_probe_count(int64_t* n);
 int vqx_probe_read(int64_t i, int32_t* info5, double* flops, float* ms);
 
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
-#define VQX_ABI_VERSION 108
+#define VQX_ABI_VERSION 109
 int vqx_version(void);
 
 #ifdef __cplusplus

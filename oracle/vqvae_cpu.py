@@ -367,16 +367,62 @@ class OracleVQVAE:
         return xhat, loss, losses
 
 
+class ORAdam(torch.optim.Optimizer):
+    """RAdam.step (trainer/radam.py:15-78) in the same fp32 op order, on the
+    current torch signatures: v = v*b2 + (1-b2)*g*g, m = m*b1 + (1-b1)*g,
+    N_sma = N_max - 2 t b2^t / (1 - b2^t); N_sma >= 5: p += -(ss*lr) * m /
+    (sqrt(v) + eps) with the rectified step size ss (python doubles, :53-57),
+    else p += -(lr/(1 - b1^t)) * m (:58-59, 68-71).  weight_decay 0 only
+    (trainer/basic.py:31-34)."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0):
+        assert weight_decay == 0
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+
+    @torch.no_grad()
+    def step(self):
+        for group in self.param_groups:
+            beta1, beta2 = group["betas"]
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                grad = p.grad.float()
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = 0
+                    st["exp_avg"] = torch.zeros_like(p)
+                    st["exp_avg_sq"] = torch.zeros_like(p)
+                m, v = st["exp_avg"], st["exp_avg_sq"]
+                v.mul_(beta2).addcmul_(grad, grad, value=1 - beta2)
+                m.mul_(beta1).add_(grad, alpha=1 - beta1)
+                st["step"] += 1
+                t = st["step"]
+                beta2_t = beta2 ** t
+                n_max = 2 / (1 - beta2) - 1
+                n_sma = n_max - 2 * t * beta2_t / (1 - beta2_t)
+                if n_sma >= 5:
+                    ss = math.sqrt((1 - beta2_t) * (n_sma - 4) / (n_max - 4) * (n_sma - 2) / n_sma * n_max /
+                                   (n_max - 2)) / (1 - beta1 ** t)
+                    p.addcdiv_(m, v.sqrt().add_(group["eps"]), value=-ss * group["lr"])
+                else:
+                    ss = 1.0 / (1 - beta1 ** t)
+                    p.add_(m, alpha=-ss * group["lr"])
+
+
 class OracleTrainer:
     """Trainer.train_step (trainer/basic.py:55-79) on CPU: zero_grad, forward,
-    backward, clip_grad_norm_, Adam(betas=(0.5, 0.999), wd 0), StepLR."""
+    backward, clip_grad_norm_, Adam or RAdam (betas=(0.5, 0.999), wd 0,
+    trainer/basic.py:30-39), StepLR."""
 
     def __init__(self, cfg, state_dict):
         self.model = OracleVQVAE(cfg, state_dict)
         params = list(self.model.params.values())
         self.max_grad_norm = cfg.get("max_grad_norm", 5)
-        self.optimizer = torch.optim.Adam(params, lr=cfg.get("learning_rate", 1e-3), betas=(0.5, 0.999),
-                                          weight_decay=0.0)
+        if str(cfg.get("optim_type", "Adam")).upper() == "RADAM":
+            self.optimizer = ORAdam(params, lr=cfg.get("learning_rate", 1e-3), betas=(0.5, 0.999), weight_decay=0.0)
+        else:
+            self.optimizer = torch.optim.Adam(params, lr=cfg.get("learning_rate", 1e-3), betas=(0.5, 0.999),
+                                              weight_decay=0.0)
         self.scheduler = None
         if cfg.get("lr_scheduler", None) is not None:
             lp = cfg.get("lr_param", {"step_size": 100000, "gamma": 0.5, "last_epoch": -1})

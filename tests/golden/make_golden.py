@@ -19,6 +19,9 @@ stored):
   * step_<cfg>_plain*     3 steps with the straight-through VectorQuantizer
                           (use_ema: false; embed_norm true / false; aishell3
                           with jitter_p 0.12), SURVEY §8f row 1
+  * step_vcc20_radam      8 steps with optim_type RAdam (trainer/radam.py,
+                          SURVEY §8f row 4); RAdam switches to the adaptive
+                          update at step 6
 Weights/inputs come from numpy PCG64 seeds (oracle/vqvae_cpu.py), so the GPU
 box regenerates them bit-identically without receiving any weights.
 """
@@ -52,11 +55,13 @@ VARIANTS = {  # derived configs: base recipe + overrides
     "vcc20_plain_nonorm": ("vcc20", {"use_ema": False, "embed_norm": False}),
     "aishell3_plain": ("aishell3", {"use_ema": False}),
 }
+RADAM = {"vcc20_radam": ("vcc20", {"optim_type": "RAdam"})}
+VARIANTS_ALL = dict(VARIANTS, **RADAM)
 
 
 def load_cfg(name):
-    if name in VARIANTS:
-        base, over = VARIANTS[name]
+    if name in VARIANTS_ALL:
+        base, over = VARIANTS_ALL[name]
         cfg = yaml.safe_load(open(CFGS[base]))
         cfg.update(over)
         return cfg
@@ -115,8 +120,12 @@ def step_fixture(name, B, T, steps, wseed, bseed, tseed, nseed, out_prefix, keep
     model = ref_model(cfg, sd)
     ema = cfg.get("use_ema", False)
     rec = Recorder(model.quantizer) if ema else None
-    opt = torch.optim.Adam(model.parameters(), lr=cfg.get("learning_rate", 1e-3), betas=(0.5, 0.999),
-                           weight_decay=0.0)
+    if str(cfg.get("optim_type", "Adam")).upper() == "RADAM":  # trainer/basic.py:30-34
+        from vae_npvc.trainer.radam import RAdam
+        opt = RAdam(model.parameters(), lr=cfg.get("learning_rate", 1e-3), betas=(0.5, 0.999), weight_decay=0.0)
+    else:
+        opt = torch.optim.Adam(model.parameters(), lr=cfg.get("learning_rate", 1e-3), betas=(0.5, 0.999),
+                               weight_decay=0.0)
     sched = torch.optim.lr_scheduler.StepLR(optimizer=opt, **cfg["lr_param"]) if cfg.get("lr_scheduler") else None
     torch.manual_seed(tseed)
     np.random.seed(nseed)
@@ -236,6 +245,10 @@ def structure_fixture():
 
 if __name__ == "__main__":
     torch.set_num_threads(os.cpu_count() or 8)
+    if "--only-radam" in sys.argv:  # the §8f row-4 optimizer: 8 steps cross RAdam's N_sma >= 5 switch at step 6
+        step_fixture("vcc20_radam", B=4, T=128, steps=8, wseed=1201, bseed=2201, tseed=3201, nseed=4201,
+                     out_prefix="step_vcc20_radam")
+        sys.exit(0)
     if "--only-plain" in sys.argv:  # just the §8f row-1 fixtures
         for i, name in enumerate(VARIANTS):
             step_fixture(name, B=4, T=128, steps=3, wseed=1101 + i, bseed=2101 + i, tseed=3101 + i,
@@ -249,6 +262,8 @@ if __name__ == "__main__":
     for i, name in enumerate(VARIANTS):
         step_fixture(name, B=4, T=128, steps=3, wseed=1101 + i, bseed=2101 + i, tseed=3101 + i, nseed=4101 + i,
                      out_prefix=f"step_{name}")
+    step_fixture("vcc20_radam", B=4, T=128, steps=8, wseed=1201, bseed=2201, tseed=3201, nseed=4201,
+                 out_prefix="step_vcc20_radam")
     for K in (128, 512, 1024):
         vq_fixture(K, 64, 256, 5000 + K, f"vq_K{K}")
     vq_tile_fixture(6001, "vq_tile")

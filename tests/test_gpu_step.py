@@ -48,6 +48,39 @@ def test_fp32_train_steps_match_reference_golden(prefix):
         assert relclose(float(p.detach().double().norm()), meta["params_after"][n]["norm"], 1e-3), n
 
 
+def test_fp32_radam_steps_match_reference_golden(tmp_path):
+    """optim_type RAdam (trainer/radam.py): 8 fused steps
+    (the rectified update starts at step 6) vs the reference run: losses 1e-3
+    (1e-4 at step 0), parameters after 8 steps 1e-3; the optimizer state
+    round-trips through the reference RAdam's state_dict format."""
+    from oracle.vqvae_cpu import ORAdam, seeded_batch
+    meta, arr = load_fixture("step_vcc20_radam")
+    cfg = dict(cfg_of("vcc20", compute_dtype="fp32"), optim_type="RAdam")
+    tr = make_trainer(cfg, meta["wseed"])
+    torch.manual_seed(meta["tseed"])
+    np.random.seed(meta["nseed"])
+    for s in range(meta["steps"]):
+        x, y = seeded_batch(cfg, meta["B"], meta["T"], meta["bseed"] + s)
+        _, detail = tr.train_step((x.cuda(), y.cuda()))
+        detail = dict(detail)
+        for k, v in meta["detail"][s].items():
+            rt = 1e-3 if (k == "diff_emb" or s > 0) else 1e-4
+            assert relclose(detail[k], v, rt, 1e-6 if k == "diff_emb" else 0.0), (s, k, detail[k], v)
+    for n, p in tr.model.named_parameters():
+        assert relclose(float(p.detach().double().norm()), meta["params_after"][n]["norm"], 1e-3), n
+    sd = tr.optimizer.state_dict()
+    assert sd["state"][0]["step"] == meta["steps"] and isinstance(sd["state"][0]["step"], int)
+    ref_opt = ORAdam([torch.nn.Parameter(p.detach().cpu().clone()) for p in tr.model.parameters()], lr=1e-3,
+                     betas=(0.5, 0.999))
+    ref_opt.load_state_dict(sd)  # the reference RAdam accepts it
+    ckpt = tmp_path / "radam.pt"
+    tr.save_checkpoint(str(ckpt))
+    tr2 = make_trainer(cfg, meta["wseed"] + 1)
+    assert tr2.load_checkpoint(str(ckpt)) == meta["steps"]
+    assert int(tr2.engine.opt_step.item()) == meta["steps"]
+    assert torch.equal(tr2.engine.exp_avg, tr.engine.exp_avg)
+
+
 PLAIN = {"vcc20_plain": ("vcc20", {"use_ema": False}),
          "vcc20_plain_nonorm": ("vcc20", {"use_ema": False, "embed_norm": False}),
          "aishell3_plain": ("aishell3", {"use_ema": False})}

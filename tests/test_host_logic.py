@@ -53,12 +53,12 @@ def test_jitter_map_matches_reference_golden():
 
 
 def test_step_lr_bookkeeping_matches_torch():
-    """FusedAdamState reports the lr torch's Adam+StepLR would hold after `step`
+    """FusedOptimState reports the lr torch's Adam+StepLR would hold after `step`
     optimizer steps (trainer/basic.py:43-52 scheduler wiring)."""
-    from vae_npvc_amd.trainer.basic import FusedAdamState
+    from vae_npvc_amd.trainer.basic import FusedOptimState
     lr0, gamma, size = 1e-3, 0.5, 3
     eng = SimpleNamespace(lr0=lr0, sched_gamma=gamma, sched_step=size)
-    st = FusedAdamState(SimpleNamespace(engine=eng))
+    st = FusedOptimState(SimpleNamespace(engine=eng))
     p = torch.nn.Parameter(torch.zeros(1))
     opt = torch.optim.Adam([p], lr=lr0)
     sch = torch.optim.lr_scheduler.StepLR(opt, step_size=size, gamma=gamma)

@@ -37,10 +37,17 @@ def test_structure_matches_reference():
         assert n == st[name]["n_params"]
 
 
-@pytest.mark.parametrize("prefix", ["step_vcc20", "step_aishell3"])
+FIXTURE_CFG = {"step_vcc20": ("vcc20", {}), "step_aishell3": ("aishell3", {}),
+               "step_vcc20_radam": ("vcc20", {"optim_type": "RAdam"})}
+
+
+@pytest.mark.parametrize("prefix", list(FIXTURE_CFG))
 def test_oracle_train_steps_match_reference(prefix):
+    """Adam (3 steps) and RAdam (8 steps: the rectified update starts at step 6,
+    trainer/radam.py:53-59) against the reference run."""
     meta, arr = load_fixture(prefix)
-    cfg = cfg_of(meta["config"])
+    base, over = FIXTURE_CFG[prefix]
+    cfg = dict(cfg_of(base), **over)
     torch.set_num_threads(4)
     tr = OracleTrainer(cfg, seeded_state_dict(cfg, meta["wseed"]))
     torch.manual_seed(meta["tseed"])

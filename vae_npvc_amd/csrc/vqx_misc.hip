@@ -939,6 +939,56 @@ __global__ void adam_hyper_kernel(int64_t* __restrict__ step, double lr0, double
   hyper[7] = (float)eps;
 }
 
+// RAdam (trainer/radam.py:15-78): rectification decided once per step on the
+// device, in double like the reference's Python floats.
+__global__ void radam_hyper_kernel(int64_t* __restrict__ step, double lr0, double gamma, int step_size, double b1,
+                                   double b2, double eps, float* __restrict__ hyper) {
+  const int64_t t = step[0] + 1;
+  step[0] = t;
+  const double lr = lr0 * pow(gamma, (double)((t - 1) / step_size));
+  const double b2t = pow(b2, (double)t);
+  const double nmax = 2.0 / (1.0 - b2) - 1.0;
+  const double nsma = nmax - 2.0 * (double)t * b2t / (1.0 - b2t);
+  const bool rect = nsma >= 5.0;
+  const double ss = rect ? sqrt((1.0 - b2t) * (nsma - 4.0) / (nmax - 4.0) * (nsma - 2.0) / nsma * nmax / (nmax - 2.0)) /
+                               (1.0 - pow(b1, (double)t))
+                         : 1.0 / (1.0 - pow(b1, (double)t));
+  hyper[0] = (float)lr;
+  hyper[1] = (float)(-ss * lr);
+  hyper[2] = rect ? 1.f : 0.f;
+  hyper[3] = (float)t;
+  hyper[4] = (float)b1;
+  hyper[5] = (float)(1.0 - b1);
+  hyper[6] = (float)b2;
+  hyper[7] = (float)(1.0 - b2);
+  hyper[8] = (float)eps;
+}
+
+__global__ __launch_bounds__(256) void radam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                    const float* __restrict__ hyper, const float* __restrict__ sumsq,
+                                                    float max_norm) {
+  float coef = 1.f;
+  if (max_norm > 0.f && sumsq) {
+    const float tn = sqrtf(sumsq[0]);
+    coef = max_norm / (tn + 1e-6f);
+    coef = coef < 1.f ? coef : 1.f;
+  }
+  const float val = hyper[1];
+  const bool rect = hyper[2] != 0.f;
+  const float b1 = hyper[4], omb1 = hyper[5], b2 = hyper[6], omb2 = hyper[7], eps = hyper[8];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float gi = __fmul_rn(g[i], coef);
+    float vi = __fmul_rn(v[i], b2);
+    vi = __fadd_rn(vi, __fmul_rn(__fmul_rn(omb2, gi), gi));      // addcmul_(g, g, value=1-b2)
+    float mi = __fadd_rn(__fmul_rn(m[i], b1), __fmul_rn(omb1, gi));  // mul_(b1).add_(g, alpha=1-b1)
+    const float upd = rect ? __fdiv_rn(mi, __fadd_rn(__fsqrt_rn(vi), eps)) : mi;
+    p[i] = __fadd_rn(p[i], __fmul_rn(val, upd));
+    m[i] = mi;
+    v[i] = vi;
+  }
+}
+
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                    const float* __restrict__ hyper, const float* __restrict__ sumsq,
@@ -1249,6 +1299,24 @@ extern "C" int vqx_adam_step(float* p, const float* g, float* m, float* v, int64
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
                      hyper, sumsq, max_norm);
   return launch_status("vqx_adam_step");
+}
+
+extern "C" int vqx_radam_hyper(int64_t* step, double lr0, double gamma, int32_t step_size, double beta1,
+                               double beta2, double eps, float* hyper, vqx_stream_t stream) {
+  if (step_size < 1) { set_error("vqx_radam_hyper: step_size < 1"); return -1; }
+  if (!(beta2 > 0.0 && beta2 < 1.0) || !step || !hyper) { set_error("vqx_radam_hyper: bad arguments"); return -1; }
+  hipLaunchKernelGGL(radam_hyper_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step, lr0, gamma, step_size, beta1,
+                     beta2, eps, hyper);
+  return launch_status("vqx_radam_hyper");
+}
+
+extern "C" int vqx_radam_step(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper,
+                              const float* sumsq, float max_norm, vqx_stream_t stream) {
+  if (n <= 0) return 0;
+  if (!p || !g || !m || !v || !hyper) { set_error("vqx_radam_step: null pointer"); return -1; }
+  hipLaunchKernelGGL(radam_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
+                     hyper, sumsq, max_norm);
+  return launch_status("vqx_radam_step");
 }
 
 extern "C" int vqx_convert_2d(const void* src, int32_t ld_src, int32_t src_dtype, void* dst, int32_t ld_dst,

@@ -670,12 +670,19 @@ class VQVAEEngine:
             self.comm.grads_ready(self.flat_g, self.enc_end, self.n_params)
             self.comm.finish()
 
-    def init_optimizer(self, lr, betas=(0.5, 0.999), eps=1e-8, max_grad_norm=10.0, sched_step=None, sched_gamma=1.0):
+    def init_optimizer(self, lr, betas=(0.5, 0.999), eps=1e-8, max_grad_norm=10.0, sched_step=None, sched_gamma=1.0,
+                       kind="adam"):
+        """kind 'adam' (torch.optim.Adam, trainer/basic.py:36-39) or 'radam'
+        (trainer/radam.py RAdam, basic.py:30-34); both fused with the
+        global-norm clip and StepLR."""
+        if kind not in ("adam", "radam"):
+            raise ValueError(f"unknown optimizer {kind!r}")
+        self.opt_kind = kind
         dev = self.device
         self.exp_avg = torch.zeros(self.n_params, device=dev, dtype=F32)
         self.exp_avg_sq = torch.zeros(self.n_params, device=dev, dtype=F32)
         self.opt_step = torch.zeros(1, device=dev, dtype=torch.int64)
-        self.hyper = torch.zeros(8, device=dev, dtype=F32)
+        self.hyper = torch.zeros(16, device=dev, dtype=F32)
         self.sumsq = torch.zeros(1, device=dev, dtype=F32)
         self.norm_part = torch.zeros(1024, device=dev, dtype=F32)
         self.lr0, self.betas, self.eps, self.max_grad_norm = lr, betas, eps, max_grad_norm
@@ -686,10 +693,17 @@ class VQVAEEngine:
     def optimizer_step(self):
         if self.max_grad_norm > 0:
             ops.grad_sq_norm(self.flat_g, self.norm_part, self.sumsq)
+        sumsq = self.sumsq if self.max_grad_norm > 0 else None
+        if self.opt_kind == "radam":
+            ops.radam_hyper(self.opt_step, self.lr0, self.sched_gamma, self.sched_step, self.betas[0], self.betas[1],
+                            self.eps, self.hyper)
+            ops.radam_step(self.flat_p, self.flat_g, self.exp_avg, self.exp_avg_sq, self.hyper, sumsq,
+                           float(self.max_grad_norm))
+            return
         ops.adam_hyper(self.opt_step, self.lr0, self.sched_gamma, self.sched_step, self.betas[0], self.betas[1],
                        self.eps, self.hyper)
-        ops.adam_step(self.flat_p, self.flat_g, self.exp_avg, self.exp_avg_sq, self.hyper,
-                      self.sumsq if self.max_grad_norm > 0 else None, float(self.max_grad_norm))
+        ops.adam_step(self.flat_p, self.flat_g, self.exp_avg, self.exp_avg_sq, self.hyper, sumsq,
+                      float(self.max_grad_norm))
 
     def train_step(self, x, y):
         """One full training step (trainer/basic.py:55-79): forward, backward,

@@ -352,6 +352,15 @@ def adam_step(p, g, m, v, hyper, sumsq, max_norm):
          stream_ptr())
 
 
+def radam_hyper(step, lr0, gamma, step_size, beta1, beta2, eps, hyper):
+    call("vqx_radam_hyper", ptr(step), lr0, gamma, step_size, beta1, beta2, eps, ptr(hyper), stream_ptr())
+
+
+def radam_step(p, g, m, v, hyper, sumsq, max_norm):
+    call("vqx_radam_step", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), ptr(hyper), ptr(sumsq), max_norm,
+         stream_ptr())
+
+
 def convert_2d(src, dst, rows=None, cols=None):
     """dst[:rows, :cols] = src (dtype-converting, strided); src=None zero-fills."""
     rows = dst.shape[0] if rows is None else rows

@@ -3,10 +3,11 @@ reference's seam, vae_npvc/bin/train.py:33,49-51).  Same surface as
 vae_npvc/trainer/basic.py:10-121 — Trainer(config), train_step(input,
 iteration=None) -> (iteration, loss_detail), valid, valid_step,
 get_model_info, save_checkpoint, load_checkpoint — with the step fused on the
-MI355X: forward, backward, global-norm clip, Adam (betas (0.5, 0.999), wd 0)
-and StepLR run as HIP kernels with no host synchronisation; the optimizer
-state is saved in torch.optim.Adam's state_dict format so reference
-checkpoints ({'model', 'optimizer', 'iteration'}) load both ways.
+MI355X: forward, backward, global-norm clip, Adam or RAdam (betas
+(0.5, 0.999), wd 0, trainer/basic.py:30-39) and StepLR run as HIP kernels
+with no host synchronisation; the optimizer state is saved in the
+torch.optim.Adam / reference RAdam state_dict format so reference checkpoints
+({'model', 'optimizer', 'iteration'}) load both ways.
 
 Data parallel: when torch.distributed is initialised, each rank trains on its
 own shard (per-rank batch) and the engine all-reduces gradients and EMA
@@ -51,8 +52,10 @@ class LazyLossDetail(Mapping):
         return repr(self._get())
 
 
-class FusedAdamState:
-    """torch.optim.Adam-compatible state_dict view over the engine's flat moments."""
+class FusedOptimState:
+    """state_dict view over the engine's flat moments in the format of
+    torch.optim.Adam (optim_type Adam) or of the reference's RAdam
+    (trainer/radam.py:30-33: step as a Python int, no Adam-only group keys)."""
 
     def __init__(self, trainer):
         self.t = trainer
@@ -69,13 +72,15 @@ class FusedAdamState:
         for i, p in enumerate(e.params):
             n = p.numel()
             if step > 0:
-                state[i] = {"step": torch.tensor(float(step)),
+                state[i] = {"step": torch.tensor(float(step)) if e.opt_kind == "adam" else step,
                             "exp_avg": e.exp_avg[off:off + n].view_as(p).detach().cpu().clone(),
                             "exp_avg_sq": e.exp_avg_sq[off:off + n].view_as(p).detach().cpu().clone()}
             off += n
-        group = {"lr": self._lr_now(step + 1), "betas": tuple(e.betas), "eps": e.eps, "weight_decay": 0.0,
-                 "amsgrad": False, "maximize": False, "foreach": None, "capturable": False, "differentiable": False,
-                 "fused": None, "params": list(range(len(e.params)))}
+        group = {"lr": self._lr_now(step + 1), "betas": tuple(e.betas), "eps": e.eps, "weight_decay": 0.0}
+        if e.opt_kind == "adam":
+            group.update({"amsgrad": False, "maximize": False, "foreach": None, "capturable": False,
+                          "differentiable": False, "fused": None})
+        group["params"] = list(range(len(e.params)))
         if self.t.scheduler_cfg is not None:
             group["initial_lr"] = e.lr0
         return {"state": state, "param_groups": [group]}
@@ -102,9 +107,8 @@ class Trainer(object):
         model_type = config.get("model_type", "vae_npvc_amd.model.vqvae:Model").split(":")
         self.learning_rate = config.get("learning_rate", 1e-3)
         self.max_grad_norm = config.get("max_grad_norm", 5)
-        optim_type = config.get("optim_type", "Adam")
-        if optim_type.upper() != "ADAM":
-            raise NotImplementedError("optim_type RAdam is SURVEY §8f 'next' #4; the baseline recipes use Adam")
+        optim_type = str(config.get("optim_type", "Adam"))
+        self.optim_kind = "radam" if optim_type.upper() == "RADAM" else "adam"  # trainer/basic.py:30-39
         lr_sched = config.get("lr_scheduler", None)
         lr_param = config.get("lr_param", {"step_size": 100000, "gamma": 0.5, "last_epoch": -1})
         self.scheduler_cfg = lr_param if lr_sched is not None else None
@@ -127,8 +131,9 @@ class Trainer(object):
         self.engine.init_optimizer(self.learning_rate, betas=(0.5, 0.999), eps=1e-8,
                                    max_grad_norm=float(self.max_grad_norm),
                                    sched_step=sp.get("step_size") if self.scheduler_cfg else None,
-                                   sched_gamma=sp.get("gamma", 1.0) if self.scheduler_cfg else 1.0)
-        self.optimizer = FusedAdamState(self)
+                                   sched_gamma=sp.get("gamma", 1.0) if self.scheduler_cfg else 1.0,
+                                   kind=self.optim_kind)
+        self.optimizer = FusedOptimState(self)
         self.scheduler = None  # StepLR runs on the device inside the Adam kernel's hyper-parameter step
         self.iteration = 0
 
