@@ -395,15 +395,15 @@ int vqx_convert_2d(const void* src, int32_t ld_src, int32_t src_dtype, void* dst
 
 /* Thread-local description of the last failure. */
 const char* vqx_last_error(void);
-/* bf16 conv GEMM pipeline (K-tile depth BK x LDS-DMA ring depth): 0 =
- * automatic (= 1), 1 = BK 64 x 2-deep, 2 = BK 32 x 4-deep (A/B only).
- * Process-wide; the default comes from env VQX_GEMM_VARIANT. */
+/* bf16 conv GEMM pipeline selector, kept for ABI stability: 0 = automatic,
+ * 1 = BK 64 x 2-deep LDS-DMA ring (the only bf16 pipeline; BK 32 x 4-deep
+ * measured slower on every layer, profiles/r01/gemm_lab.txt). */
 int vqx_set_gemm_tile(int32_t policy);
 
 /* Launch probe (measurement only; not reentrant while enabled).  While on,
  * each conv GEMM launch records a start/stop event pair stamped on its own
  * dispatch (hipExtLaunchKernelGGL); after the stream is synchronised,
- * vqx_probe_read returns per launch {dtype, mode, prologue, gen, staging},
+ * vqx_probe_read returns per launch {dtype, mode, prologue, gen, epilogue kind},
  * the algorithmic FLOPs and the kernel duration in ms.  enable(0/1) pauses /
  * resumes recording (an event-stamped dispatch costs a few us of queue time,
  * so callers sample); clear() empties the log. */

@@ -15,7 +15,7 @@ def _ops():
     return ops
 
 
-@pytest.fixture(params=[1, 2], ids=["bk64x2", "bk32x4"])
+@pytest.fixture(params=[0, 1], ids=["auto", "bk64x2"])
 def tile(request):
     """Run a GEMM test with every bf16 pipeline variant (K-tile depth x ring
     depth, vqx_gemm_inst.h); f32 has one pipeline."""

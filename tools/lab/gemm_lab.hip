@@ -39,9 +39,12 @@ int main(int argc, char** argv) {
   struct Shape { const char* name; int mode, cin, cout, k; };
   const Shape shapes[] = {{"dec_in_fwd", MODE_FWD, 512, 1024, 3}, {"enc_k3_fwd", MODE_FWD, 512, 512, 3},
                           {"enc_sk_fwd", MODE_FWD, 512, 512, 1}, {"dec_in_dgrad", MODE_DGRAD, 1024, 512, 3},
-                          {"dec_in_wgrad", MODE_WGRAD, 512, 1024, 3}};
+                          {"dec_in_wgrad", MODE_WGRAD, 512, 1024, 3},
+                          {"k64", MODE_FWD, 64, 512, 1}, {"k128", MODE_FWD, 128, 512, 1},
+                          {"k256", MODE_FWD, 256, 512, 1}, {"k512", MODE_FWD, 512, 512, 1},
+                          {"k1024", MODE_FWD, 1024, 512, 1}, {"k1536", MODE_FWD, 1536, 512, 1}};
   void *x, *w, *y;
-  const size_t xb = (size_t)N * 1024 * 2, wb = (size_t)1024 * 3 * 1024 * 2, yb = (size_t)8 * 1024 * 3 * 1024 * 4;
+  const size_t xb = (size_t)N * 1536 * 2, wb = (size_t)1536 * 3 * 1024 * 2, yb = (size_t)8 * 1024 * 3 * 1024 * 4;
   CK(hipMalloc(&x, xb)); CK(hipMalloc(&w, wb)); CK(hipMalloc(&y, yb));
   std::vector<unsigned short> hx(xb / 2);
   for (size_t i = 0; i < hx.size(); ++i) hx[i] = 0x3f80 ^ (unsigned short)((i * 2654435761u) >> 20 & 0x807f);

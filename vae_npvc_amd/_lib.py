@@ -129,12 +129,13 @@ class VqxError(RuntimeError):
 _lib = None
 
 
-def load(path: os.PathLike = LIB_PATH):
-    """Load libvqx.so once; raise if it is absent (no CPU fallback exists)."""
+def load(path: os.PathLike = None):
+    """Load libvqx.so once (env VQX_LIB overrides the in-tree path, for A/B
+    builds); raise if it is absent (no CPU fallback exists)."""
     global _lib
     if _lib is not None:
         return _lib
-    path = Path(path)
+    path = Path(path or os.environ.get("VQX_LIB") or LIB_PATH)
     if not path.exists():
         raise VqxError(f"libvqx.so not found at {path}; build it with `python -m vae_npvc_amd.csrc.build` "
                        "(the HIP kernels are the only implementation of this path)")

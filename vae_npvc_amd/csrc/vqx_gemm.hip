@@ -10,8 +10,6 @@
 
 namespace vqx {
 
-static int gemm_bk(int variant) { return variant == 2 ? 32 : 64; }
-
 // ---------------- launch probe (bench.py's roofline leg)
 // While enabled, every conv GEMM is launched with hipExtLaunchKernelGGL and a
 // start/stop event pair that the runtime stamps on the kernel's own dispatch
@@ -19,7 +17,7 @@ static int gemm_bk(int variant) { return variant == 2 ? 32 : 64; }
 // between kernels).  Events come from a pool reused across probe sessions.
 struct ProbeRec {
   hipEvent_t start, stop;
-  int info[5];  // dtype, mode, prologue, gen, dma
+  int info[5];  // dtype, mode, prologue, gen, epilogue kind
   double flops;
 };
 static bool g_probe_on = false;
@@ -51,25 +49,13 @@ void gemm_launch(const void* fn, int grid, hipStream_t s, const GemmParams& P, c
   (void)hipExtLaunchKernel(fn, dim3(grid), dim3(256), args, 0, s, ev.first, ev.second, 0);
 }
 
-// Pipeline variant of the bf16 GEMMs (vqx_gemm_inst.h): 0 = automatic (1),
-// 1 or 2 forced (vqx_set_gemm_tile; default from env VQX_GEMM_VARIANT).
-static int g_tile_policy = -1;
-static int pick_variant() {
-  if (g_tile_policy < 0) {
-    const char* e = getenv("VQX_GEMM_VARIANT");
-    g_tile_policy = (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
-  }
-  return g_tile_policy ? g_tile_policy : 1;
-}
-
 static void launch_mode(GemmParams& P, int mode, int64_t rows, int extra_mult, bool bf16, bool gen, hipStream_t s) {
   // rows: extent of the tile-M dimension; extra_mult: split-K factor (WGRAD)
   P.tiles_m = (int)((rows + 127) / 128);
   const int grid = P.tiles_m * P.tiles_n * extra_mult;
-  const int variant = pick_variant();
-  if (mode == MODE_FWD) launch_mode_dt<MODE_FWD>(P, grid, bf16, gen, variant, s);
-  else if (mode == MODE_DGRAD) launch_mode_dt<MODE_DGRAD>(P, grid, bf16, gen, variant, s);
-  else launch_mode_dt<MODE_WGRAD>(P, grid, bf16, gen, variant, s);
+  if (mode == MODE_FWD) launch_mode_dt<MODE_FWD>(P, grid, bf16, gen, s);
+  else if (mode == MODE_DGRAD) launch_mode_dt<MODE_DGRAD>(P, grid, bf16, gen, s);
+  else launch_mode_dt<MODE_WGRAD>(P, grid, bf16, gen, s);
 }
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -128,7 +114,7 @@ static int conv_common(const vqx_conv_args* a, int mode, hipStream_t s) {
   P.colsum_part = a->colsum_part;
   P.stat_part = a->stat_part; P.gn_groups = a->gn_groups; P.gn_glu = a->gn_glu;
   if (P.a_bytes > 0x7fffffffLL || P.b_bytes > 0x7fffffffLL) { set_error("vqx_conv: operand larger than 2 GiB"); return -1; }
-  const bool gen = (a->cin % (a->dtype == VQX_BF16 ? gemm_bk(pick_variant()) : 32)) != 0;
+  const bool gen = (a->cin % (a->dtype == VQX_BF16 ? 64 : 32)) != 0;
   launch_mode(P, mode, a->n_rows, 1, a->dtype == VQX_BF16, gen, s);
   return launch_status(mode == MODE_FWD ? "vqx_conv1d_fwd" : "vqx_conv1d_dgrad");
 }
@@ -169,7 +155,7 @@ extern "C" int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream) {
   kps = (kps + kround - 1) / kround * kround;
   P.k_per_split = kps;
   P.y = a->slabs;
-  const int bkv = a->dtype == VQX_BF16 ? gemm_bk(pick_variant()) : 32;
+  const int bkv = a->dtype == VQX_BF16 ? 64 : 32;
   const bool gen = (a->T % bkv) != 0 || (a->n_rows % bkv) != 0;
   hipStream_t s = (hipStream_t)stream;
   launch_mode(P, MODE_WGRAD, P.Mc, P.splits, a->dtype == VQX_BF16, gen, s);
@@ -177,8 +163,8 @@ extern "C" int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream) {
 }
 
 extern "C" int vqx_set_gemm_tile(int32_t policy) {
-  if (policy < 0 || policy > 2) { set_error("vqx_set_gemm_tile: policy %d not in 0..2", policy); return -1; }
-  g_tile_policy = policy;
+  // one bf16 pipeline remains (BK 64, 2-deep ring); kept for ABI stability
+  if (policy < 0 || policy > 1) { set_error("vqx_set_gemm_tile: policy %d not in 0..1", policy); return -1; }
   return 0;
 }
 

@@ -2,5 +2,5 @@
 #include "vqx_gemm_inst.h"
 
 namespace vqx {
-template void launch_mode_dt<MODE_FWD>(const GemmParams&, int, bool, bool, int, hipStream_t);
+template void launch_mode_dt<MODE_FWD>(const GemmParams&, int, bool, bool, hipStream_t);
 }  // namespace vqx

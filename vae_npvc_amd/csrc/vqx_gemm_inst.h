@@ -1,10 +1,12 @@
 // Launch glue shared by the per-mode instantiation units (vqx_gemm_fwd.hip,
 // vqx_gemm_dgrad.hip, vqx_gemm_wgrad.hip), split so hipcc builds them in
-// parallel.  Pipeline variants of the bf16 GEMM (vqx_set_gemm_tile):
-//   1: BK = 64, 2-deep LDS-DMA ring (default)
-//   2: BK = 32, 4-deep ring (three K-tiles in flight; measured 5-30% slower on
-//      every config-2 layer, kept for A/B runs)
-// f32 (parity mode) always runs BK = 32, 2-deep.
+// parallel.  bf16 runs BK = 64 with a 2-deep LDS-DMA ring (BK = 32 with a
+// 4-deep ring measured 5-30% slower on every config-2 layer:
+// profiles/r01/gemm_lab.txt); f32 (parity mode) runs BK = 32, 2-deep.
+//
+// Instances: the bf16 fast path (no prologue, cin % 64 == 0) gets one kernel
+// per epilogue kind (EK_*); prologues, GEN tiles (cin % BK != 0) and f32 use
+// the generic EK_ALL kernel.  WGRAD's epilogue is the slab store (EK_NONE).
 #pragma once
 #include "vqx_gemm_kernel.h"
 
@@ -13,41 +15,66 @@ namespace vqx {
 // vqx_gemm.hip: plain launch, or the probe's event-stamped launch
 void gemm_launch(const void* fn, int grid, hipStream_t s, const GemmParams& P, const int info[5], double flops);
 
-template <typename T, int MODE, bool GEN, int BK, int NST>
-void launch_variant(const GemmParams& P, int grid, hipStream_t s, int variant) {
+// smallest epilogue kind whose feature mask covers `epi`
+inline int pick_ek(int epi) {
+  for (int ek = EK_NONE; ek < EK_ALL; ++ek)
+    if ((epi & ~ek_mask(ek)) == 0) return ek;
+  return EK_ALL;
+}
+
+template <typename T, int MODE, int PRO, bool GEN, int EK>
+void launch_one(const GemmParams& P, int grid, hipStream_t s) {
+  constexpr int BK = sizeof(T) == 2 ? 64 : 32;
   const double flops = MODE == MODE_WGRAD ? 2.0 * (double)P.n_rows * P.Mc * P.Nc
                                           : 2.0 * (double)P.n_rows * P.Nc * P.K;
-  const int info[5] = {sizeof(T) == 2 ? VQX_BF16 : VQX_F32, MODE, P.pro, GEN ? 1 : 0, variant};
-  const void* fn;
+  const int info[5] = {sizeof(T) == 2 ? VQX_BF16 : VQX_F32, MODE, P.pro, GEN ? 1 : 0, EK};
+  gemm_launch((const void*)conv_gemm_kernel<T, MODE, PRO, GEN, BK, 2, EK>, grid, s, P, info, flops);
+}
+
+template <typename T, int MODE, bool GEN, int EK>
+void launch_pro(const GemmParams& P, int grid, hipStream_t s) {
   if constexpr (MODE == MODE_DGRAD) {
-    fn = (const void*)conv_gemm_kernel<T, MODE, VQX_PRO_NONE, GEN, BK, NST>;
+    launch_one<T, MODE, VQX_PRO_NONE, GEN, EK>(P, grid, s);
   } else {
     switch (P.pro) {
-      case VQX_PRO_NONE: fn = (const void*)conv_gemm_kernel<T, MODE, VQX_PRO_NONE, GEN, BK, NST>; break;
-      case VQX_PRO_LRELU: fn = (const void*)conv_gemm_kernel<T, MODE, VQX_PRO_LRELU, GEN, BK, NST>; break;
-      case VQX_PRO_RELU: fn = (const void*)conv_gemm_kernel<T, MODE, VQX_PRO_RELU, GEN, BK, NST>; break;
-      default: fn = (const void*)conv_gemm_kernel<T, MODE, VQX_PRO_SCALE_RELU, GEN, BK, NST>; break;
+      case VQX_PRO_NONE: launch_one<T, MODE, VQX_PRO_NONE, GEN, EK>(P, grid, s); break;
+      case VQX_PRO_LRELU: launch_one<T, MODE, VQX_PRO_LRELU, GEN, EK>(P, grid, s); break;
+      case VQX_PRO_RELU: launch_one<T, MODE, VQX_PRO_RELU, GEN, EK>(P, grid, s); break;
+      default: launch_one<T, MODE, VQX_PRO_SCALE_RELU, GEN, EK>(P, grid, s); break;
     }
   }
-  gemm_launch(fn, grid, s, P, info, flops);
 }
 
 template <int MODE>
-void launch_mode_dt(const GemmParams& P, int grid, bool bf16, bool gen, int variant, hipStream_t s) {
+void launch_mode_dt(const GemmParams& P, int grid, bool bf16, bool gen, hipStream_t s) {
+  constexpr int EKW = MODE == MODE_WGRAD ? EK_NONE : EK_ALL;  // generic epilogue of this mode
   if (!bf16) {
-    if (gen) launch_variant<float, MODE, true, 32, 2>(P, grid, s, 0);
-    else launch_variant<float, MODE, false, 32, 2>(P, grid, s, 0);
+    if (gen) launch_pro<float, MODE, true, EKW>(P, grid, s);
+    else launch_pro<float, MODE, false, EKW>(P, grid, s);
     return;
   }
-#define VQX_V(BK, NST)                                                  \
-  if (gen) launch_variant<bf16_t, MODE, true, BK, NST>(P, grid, s, variant); \
-  else launch_variant<bf16_t, MODE, false, BK, NST>(P, grid, s, variant);
-  if (variant == 2) {
-    VQX_V(32, 4)
-  } else {
-    VQX_V(64, 2)
+  if (gen) {
+    launch_pro<bf16_t, MODE, true, EKW>(P, grid, s);
+    return;
   }
-#undef VQX_V
+  if constexpr (MODE == MODE_WGRAD) {
+    launch_pro<bf16_t, MODE, false, EK_NONE>(P, grid, s);
+  } else {
+    if (P.pro != VQX_PRO_NONE) {
+      launch_pro<bf16_t, MODE, false, EK_ALL>(P, grid, s);
+      return;
+    }
+    switch (pick_ek(P.epi)) {
+      case EK_NONE: launch_one<bf16_t, MODE, VQX_PRO_NONE, false, EK_NONE>(P, grid, s); break;
+      case EK_ELEM: launch_one<bf16_t, MODE, VQX_PRO_NONE, false, EK_ELEM>(P, grid, s); break;
+      case EK_GNADD: launch_one<bf16_t, MODE, VQX_PRO_NONE, false, EK_GNADD>(P, grid, s); break;
+      case EK_SPLIT: launch_one<bf16_t, MODE, VQX_PRO_NONE, false, EK_SPLIT>(P, grid, s); break;
+      case EK_COLSUM: launch_one<bf16_t, MODE, VQX_PRO_NONE, false, EK_COLSUM>(P, grid, s); break;
+      case EK_GNSTATS: launch_one<bf16_t, MODE, VQX_PRO_NONE, false, EK_GNSTATS>(P, grid, s); break;
+      case EK_GNBWD: launch_one<bf16_t, MODE, VQX_PRO_NONE, false, EK_GNBWD>(P, grid, s); break;
+      default: launch_one<bf16_t, MODE, VQX_PRO_NONE, false, EK_ALL>(P, grid, s); break;
+    }
+  }
 }
 
 }  // namespace vqx

@@ -34,6 +34,7 @@
 #define VQX_LAB_MODE 0
 #endif
 
+
 namespace vqx {
 
 constexpr int kBN = 128;  // tile width (and height)
@@ -179,12 +180,70 @@ __device__ __forceinline__ void st8(void* p, int64_t i, const float* f) {
   }
 }
 
+// Optional streaming (non-temporal) stores of the output tile.  They make the
+// producing GEMM 10-18% faster on the 1x1 layers in isolation
+// (profiles/r01/gemm_lab.txt) but the whole step 1.3% (outputs) / 2.9% (also
+// the WGRAD slabs) slower: the consumer then reads from HBM instead of the
+// Infinity Cache (profiles/r01/nt_store_ab.txt).  Off by default.
+#ifndef VQX_NT_Y
+#define VQX_NT_Y 0     // non-temporal FWD/DGRAD output stores
+#endif
+#ifndef VQX_NT_SLAB
+#define VQX_NT_SLAB 0  // non-temporal WGRAD slab stores
+#endif
+template <typename T, bool NT = true>
+__device__ __forceinline__ void st8_nt(void* p, int64_t i, const float* f) {
+  if constexpr (!NT) {
+    st8<T>(p, i, f);
+    return;
+  }
+  typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+  if constexpr (sizeof(T) == 2) {
+    const u32x4v u = {(unsigned)f2bf(f[0]) | ((unsigned)f2bf(f[1]) << 16),
+                      (unsigned)f2bf(f[2]) | ((unsigned)f2bf(f[3]) << 16),
+                      (unsigned)f2bf(f[4]) | ((unsigned)f2bf(f[5]) << 16),
+                      (unsigned)f2bf(f[6]) | ((unsigned)f2bf(f[7]) << 16)};
+    __builtin_nontemporal_store(u, (u32x4v*)((bf16_t*)p + i));
+  } else {
+    const f32x4_t a = {f[0], f[1], f[2], f[3]}, b = {f[4], f[5], f[6], f[7]};
+    __builtin_nontemporal_store(a, (f32x4_t*)((float*)p + i));
+    __builtin_nontemporal_store(b, (f32x4_t*)((float*)p + i + 4));
+  }
+}
+
+// Epilogue kinds: each conv_gemm_kernel instance compiles only the epilogue
+// features of its kind (the runtime flags are masked with it), so the common
+// launches do not carry the code of every fused epilogue (a 14k-instruction
+// kernel body measured ~2 us slower per launch than a specialised one).
+enum {
+  EK_NONE = 0,     // store only (OUTF32 allowed)
+  EK_ELEM = 1,     // BIAS | ROWBIAS | MASK | RES | ACT | ACT2 | OUTF32
+  EK_GNADD = 2,    // ELEM + GNADD
+  EK_SPLIT = 3,    // ELEM + SPLIT
+  EK_COLSUM = 4,   // ELEM + COLSUM
+  EK_GNSTATS = 5,  // ELEM + GNSTATS
+  EK_GNBWD = 6,    // ELEM + COLSUM + GNBWD
+  EK_ALL = 7       // every flag (generic path: prologues, GEN tiles, f32)
+};
+constexpr int kEpiElem = VQX_EPI_BIAS | VQX_EPI_ROWBIAS | VQX_EPI_MASK | VQX_EPI_RES | VQX_EPI_ACT | VQX_EPI_ACT2 |
+                         VQX_EPI_OUTF32;
+__host__ __device__ constexpr int ek_mask(int ek) {
+  return ek == EK_NONE ? VQX_EPI_OUTF32
+       : ek == EK_ELEM ? kEpiElem
+       : ek == EK_GNADD ? kEpiElem | VQX_EPI_GNADD
+       : ek == EK_SPLIT ? kEpiElem | VQX_EPI_SPLIT
+       : ek == EK_COLSUM ? kEpiElem | VQX_EPI_COLSUM
+       : ek == EK_GNSTATS ? kEpiElem | VQX_EPI_GNSTATS
+       : ek == EK_GNBWD ? kEpiElem | VQX_EPI_COLSUM | VQX_EPI_GNBWD
+       : ~0;
+}
+
 // FWD/DGRAD epilogue on 8 consecutive output channels of one frame, in the
 // order bias, row bias, activation-derivative mask, split to out2 (returns),
 // residual, GroupNorm-apply add, activation, store.
-template <typename T>
+template <typename T, int EMASK>
 __device__ __forceinline__ void epilogue8(const GemmParams& P, int64_t row, int col, float* v) {
-  const int epi = P.epi;
+  const int epi = P.epi & EMASK;
   const int bidx = (epi & (VQX_EPI_ROWBIAS | VQX_EPI_GNADD)) ? (int)(row / P.T) : 0;
   float t[8];
   if (epi & VQX_EPI_BIAS) {
@@ -238,8 +297,8 @@ __device__ __forceinline__ void epilogue8(const GemmParams& P, int64_t row, int 
       for (int e = 0; e < 8; ++e) v[e] = t[e];
     }
   }
-  if (P.out_f32) st8<float>(P.y, row * P.ldy + col, v);
-  else st8<T>(P.y, row * P.ldy + col, v);
+  if (P.out_f32) st8_nt<float, VQX_NT_Y>(P.y, row * P.ldy + col, v);
+  else st8_nt<T, VQX_NT_Y>(P.y, row * P.ldy + col, v);
 }
 
 // GNBWD: GroupNorm-backward sums of this output (the GN input's gradient dy)
@@ -349,8 +408,9 @@ __device__ __forceinline__ void wait_vm(int n) {
 //   BK=64, NST=2: 64 KiB per workgroup (the round-1 pipeline);
 //   BK=32, NST=4: 64 KiB, three 16-KiB K-tiles in flight (bf16 default).
 // Two 4-wave workgroups per CU either way.
-template <typename T, int MODE, int PRO, bool GEN, int BK, int NST>
+template <typename T, int MODE, int PRO, bool GEN, int BK, int NST, int EK>
 __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
+  constexpr int EMASK = ek_mask(EK);
   using C = Cfg<T>;
   constexpr int EPC = C::EPC, CPR = C::MNCPR, ES = sizeof(T);
   constexpr int SUB = 1, BM = 128;
@@ -659,6 +719,19 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
     }
   }
 
+#if VQX_LAB_MODE == 3  // lab only: no epilogue (the accumulators stay live)
+  if (P.n_rows < 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) t += acc[i][j][e];
+    ((float*)P.y)[tid] = t;
+  }
+  return;
+#endif
   // ---------------- epilogue
   // The accumulator tile goes through LDS one 64-row slab at a time so the
   // epilogue reads and writes whole rows: 16 lanes x 8 consecutive columns
@@ -700,14 +773,14 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
       if constexpr (MODE == MODE_WGRAD) {
         if (row < P.Mc && col < P.Nc) {  // Nc % 8 == 0
           float* out = (float*)P.y + (int64_t)split * P.Mc * P.Nc + row * P.Nc + col;
-          st8<float>(out, 0, v);
+          st8_nt<float, VQX_NT_SLAB>(out, 0, v);
         }
       } else {
         if (row < P.n_rows && col < P.Nc) {
-          epilogue8<T>(P, row, col, v);
+          epilogue8<T, EMASK>(P, row, col, v);
 #pragma unroll
           for (int e = 0; e < 8; ++e) cs[e] += v[e];
-          if (P.epi & VQX_EPI_GNSTATS) {  // two-pass moments of the 8 values, merged
+          if (P.epi & EMASK & VQX_EPI_GNSTATS) {  // two-pass moments of the 8 values, merged
             float m8 = 0.f;
 #pragma unroll
             for (int e = 0; e < 8; ++e) m8 += v[e];
@@ -717,17 +790,17 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
             for (int e = 0; e < 8; ++e) q8 = fmaf(v[e] - m8, v[e] - m8, q8);
             moments_merge(mn, mm, mq, 8.f, m8, q8);
           }
-          if (P.epi & VQX_EPI_GNBWD) gnbwd8<T>(P, row, col, v, gs);
+          if (P.epi & EMASK & VQX_EPI_GNBWD) gnbwd8<T>(P, row, col, v, gs);
         }
       }
     }
     __syncthreads();
     if constexpr (MODE != MODE_WGRAD) {
       // per-(128-row group, column tile) GroupNorm partials
-      if ((P.epi & (VQX_EPI_GNSTATS | VQX_EPI_GNBWD)) && (slab & 1)) {
+      if ((P.epi & EMASK & (VQX_EPI_GNSTATS | VQX_EPI_GNBWD)) && (slab & 1)) {
         const int64_t grp_row = (int64_t)m0 + (slab >> 1) * 128;
         float* out = P.stat_part + ((grp_row / 128) * P.tiles_n + tn) * 4;
-        if (P.epi & VQX_EPI_GNSTATS) {
+        if (P.epi & EMASK & VQX_EPI_GNSTATS) {
           // merge the 64 lanes of each wave, then the waves (deterministic order)
 #pragma unroll
           for (int o = 1; o < 64; o <<= 1) {
@@ -761,7 +834,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
       }
       // per-128-row-group column sums of the stored values (bias gradient of
       // the layer this output feeds), reduced over the EROWS row lanes in LDS
-      if ((P.epi & VQX_EPI_COLSUM) && (slab & 1)) {
+      if ((P.epi & EMASK & VQX_EPI_COLSUM) && (slab & 1)) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           csr[er * kBN + ec + e] = cs[e];

@@ -112,9 +112,9 @@ class LaunchProbe:
         out = []
         for i in range(n.value):
             call("vqx_probe_read", i, info, ctypes.byref(fl), ctypes.byref(ms))
-            dt, mode, pro, gen, stg = list(info)  # stg: bit 0 LDS-DMA staging, bit 1 256-row tile
-            sym = (f"vqx::conv_gemm_kernel<{self._DT[dt]}, {mode}, {pro}, {'true' if gen else 'false'}, "
-                   f"{'true' if stg & 1 else 'false'}, {2 if stg & 2 else 1}>")
+            dt, mode, pro, gen, ek = list(info)  # ek: epilogue kind (vqx_gemm_kernel.h EK_*)
+            bk = 64 if dt == L.VQX_BF16 else 32
+            sym = f"vqx::conv_gemm_kernel<{self._DT[dt]}, {mode}, {pro}, {'true' if gen else 'false'}, {bk}, 2, {ek}>"
             out.append((sym, fl.value, ms.value * 1e-3, self.shapes[i] if i < len(self.shapes) else ""))
         return out
 
