@@ -147,6 +147,19 @@ int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream);
 #define VQX_WN_COLREDUCE 2  /* table entry kind: dv[c] = sum_{r < cin} v[r*cout + c] (bias /
                                GroupNorm-affine gradients from per-tile or per-utterance
                                partials, reduced in the same backward launch)        */
+/* Resampling convs of the multi-resolution models (vqvae.py:144-156 /
+ * 243-263, vqvae2.py:197-226 / 297-319): kernel k = 2s, stride s, padding
+ * p = s/2 + s%2 (ConvT output_padding s%2).  With frames folded s at a time
+ * (x'[u] = x[s*u .. s*u+s-1], a reinterpretation of the frame-major [N][C]
+ * layout as [N/s][s*C]) the strided conv is a stride-1, 3-tap, pad-1 conv:
+ *   w_packed[r][m][q*C + c] = w[r][c][s*(m-1) + q + p]  (0 when outside [0,k))
+ * for rows r (kind 3: cout of v[cout][cin][k], C = cin; kind 4: cin of the
+ * ConvT's v[cin][cout][k], C = cout), m in 0..2, q in 0..s-1.  The strided
+ * Conv1d runs as vqx_conv1d_fwd on the folded input; the ConvTranspose1d
+ * (its adjoint) as vqx_conv1d_dgrad; both gradients follow the same way and
+ * the backward folds the 3-tap wgrad slabs [splits][r][3*s*C] back to v. */
+#define VQX_WN_RESAMPLE 3    /* strided Conv1d, v[cout][cin][k]          */
+#define VQX_WN_RESAMPLE_T 4  /* strided ConvTranspose1d, v[cin][cout][k] */
 typedef struct vqx_wn_layer {
   const float* v;       /* [rows][cols] */
   const float* g;       /* [rows]       */
@@ -156,6 +169,7 @@ typedef struct vqx_wn_layer {
   float* dg;            /* bwd: [rows] */
   const float* slabs;   /* bwd: wgrad slabs */
   int32_t kind, cout, cin, k, splits, dtype;
+  int32_t stride, pad;  /* kinds VQX_WN_RESAMPLE(_T) only */
 } vqx_wn_layer;
 
 /* `layers_host` sizes the launch; the kernels read the same table from the
@@ -413,7 +427,7 @@ int vqx_probe_count(int64_t* n);
 int vqx_probe_read(int64_t i, int32_t* info5, double* flops, float* ms);
 
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
-#define VQX_ABI_VERSION 109
+#define VQX_ABI_VERSION 110
 int vqx_version(void);
 
 #ifdef __cplusplus

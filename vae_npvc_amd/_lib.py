@@ -15,7 +15,7 @@ from pathlib import Path
 import torch  # noqa: F401  (loads the HIP runtime first; see module docstring)
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libvqx.so"
-ABI_VERSION = 109  # include/vqx.h VQX_ABI_VERSION
+ABI_VERSION = 110  # include/vqx.h VQX_ABI_VERSION
 
 VQX_F32, VQX_BF16 = 0, 1
 PRO_NONE, PRO_LRELU, PRO_RELU, PRO_SCALE_RELU = 0, 1, 2, 3
@@ -55,7 +55,7 @@ class WNLayer(ctypes.Structure):
     _fields_ = [
         ("v", c_void_p), ("g", c_void_p), ("w_packed", c_void_p), ("norm", c_void_p), ("dv", c_void_p),
         ("dg", c_void_p), ("slabs", c_void_p), ("kind", c_int32), ("cout", c_int32), ("cin", c_int32),
-        ("k", c_int32), ("splits", c_int32), ("dtype", c_int32),
+        ("k", c_int32), ("splits", c_int32), ("dtype", c_int32), ("stride", c_int32), ("pad", c_int32),
     ]
 
 
@@ -65,6 +65,7 @@ class LinearLayer(ctypes.Structure):
 
 
 WN_COLREDUCE = 2
+WN_RESAMPLE, WN_RESAMPLE_T = 3, 4  # strided Conv1d / ConvTranspose1d (include/vqx.h)
 
 # name -> argtypes (restype is int for every entry point except the two below)
 _SIGS = {

@@ -49,6 +49,35 @@ __global__ __launch_bounds__(256) void wn_pack_kernel(const vqx_wn_layer* __rest
   const int K = l.k, cin = l.cin, cout = l.cout;
   __shared__ float buf[kWnRow + 64];
   __shared__ float red[16];
+  if (l.kind == VQX_WN_RESAMPLE || l.kind == VQX_WN_RESAMPLE_T) {
+    // strided conv (include/vqx.h): row r of v, norm, then the folded 3-tap row
+    // w_packed[r][m][q*C + c] = w[r][c][S*(m-1) + q + pad]
+    const int rows = l.kind == VQX_WN_RESAMPLE ? cout : cin, C = l.kind == VQX_WN_RESAMPLE ? cin : cout;
+    const int r = blockIdx.x;
+    if (r >= rows) return;
+    const int cols = C * K;
+    const float* v = l.v + (int64_t)r * cols;
+    float s = 0.f;
+    for (int i = threadIdx.x; i < cols; i += 256) {
+      const float x = v[i];
+      buf[i] = x;
+      s = fmaf(x, x, s);
+    }
+    s = block_sum(s, red);
+    float sc = 1.f;
+    if (l.g) {
+      const float nrm = sqrtf(s);
+      if (threadIdx.x == 0) l.norm[r] = nrm;
+      sc = l.g[r] / nrm;
+    }
+    const int S = l.stride, SC = S * C, W = 3 * SC;
+    for (int e = threadIdx.x; e < W; e += 256) {
+      const int m = e / SC, rem = e - m * SC, q = rem / C, c = rem - q * C;
+      const int j = S * (m - 1) + q + l.pad;
+      st_dt(l.w_packed, (int64_t)r * W + e, (j >= 0 && j < K) ? buf[c * K + j] * sc : 0.f, l.dtype);
+    }
+    return;
+  }
   if (l.kind == 0) {
     const int co = blockIdx.x;
     if (co >= cout) return;
@@ -122,18 +151,22 @@ __global__ __launch_bounds__(256) void wn_bwd_kernel(const vqx_wn_layer* __restr
     l.dv[c] = (a0 + a1) + (a2 + a3);
     return;
   }
-  const int rows = l.kind == 0 ? l.cout : l.cin;
+  const bool rsm = l.kind == VQX_WN_RESAMPLE || l.kind == VQX_WN_RESAMPLE_T;
+  const bool row_is_cout = l.kind == 0 || l.kind == VQX_WN_RESAMPLE;
+  const int rows = row_is_cout ? l.cout : l.cin;
   const int o = blockIdx.x;
   if (o >= rows) return;
-  const int other = l.kind == 0 ? l.cin : l.cout;  // multiple of 4 (host-checked)
+  const int other = row_is_cout ? l.cin : l.cout;  // multiple of 4 (host-checked)
   const int K = l.k;
   const int cols = other * K;
+  const int S = l.stride, SC = S * other;
+  const int scols = rsm ? 3 * SC : cols;  // slab row: folded 3-tap row for the strided kinds
   __shared__ __attribute__((aligned(16))) float dw[4096];
   __shared__ float red[16];
-  const int64_t slab_stride = (int64_t)rows * cols;
-  const float* srow = l.slabs + (int64_t)o * cols;
+  const int64_t slab_stride = (int64_t)rows * scols;
+  const float* srow = l.slabs + (int64_t)o * scols;
   const int splits = l.splits;
-  for (int x4 = threadIdx.x; x4 < cols / 4; x4 += blockDim.x) {
+  for (int x4 = threadIdx.x; x4 < scols / 4; x4 += blockDim.x) {
     const float* p = srow + 4 * x4;
     f32x4_t s0 = *(const f32x4_t*)p, s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1, s3 = s1;
     int sp = 1;
@@ -144,8 +177,17 @@ __global__ __launch_bounds__(256) void wn_bwd_kernel(const vqx_wn_layer* __restr
     }
     for (; sp < splits; ++sp) s1 += *(const f32x4_t*)(p + (int64_t)sp * slab_stride);
     const f32x4_t sum = (s0 + s1) + (s2 + s3);
-    // slab col x = j*other + c  -> v index c*K + (kind==0 ? j : K-1-j)
     const int x = 4 * x4;
+    if (rsm) {  // slab col x = m*S*C + q*C + c -> v index c*K + S*(m-1) + q + pad (4 c's share m, q)
+      const int m = x / SC, rem = x - m * SC, q = rem / other, c = rem - q * other;
+      const int j = S * (m - 1) + q + l.pad;
+      if (j >= 0 && j < K) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dw[(c + e) * K + j] = sum[e];
+      }
+      continue;
+    }
+    // slab col x = j*other + c  -> v index c*K + (kind==0 ? j : K-1-j)
     const int j = x / other, c = x - j * other;
     const int jj = l.kind == 0 ? j : K - 1 - j;
 #pragma unroll
@@ -1059,8 +1101,9 @@ extern "C" int vqx_weight_norm_fwd(const vqx_wn_layer* lh, const vqx_wn_layer* l
   int64_t max_el = 1;
   for (int i = 0; i < n_layers; ++i) {
     const vqx_wn_layer& l = lh[i];
-    if (l.kind != 0 && l.kind != 1) { set_error("vqx_weight_norm_fwd: layer %d bad kind", i); return -1; }
-    const int rows = l.kind == 0 ? l.cout : l.cin;
+    if (l.kind != 0 && l.kind != 1 && l.kind != VQX_WN_RESAMPLE && l.kind != VQX_WN_RESAMPLE_T) { set_error("vqx_weight_norm_fwd: layer %d bad kind", i); return -1; }
+    if (l.kind >= VQX_WN_RESAMPLE && !(l.stride >= 1 && l.pad >= 0 && l.pad <= l.stride && l.k - 1 - l.pad < 2 * l.stride)) { set_error("vqx_weight_norm_fwd: layer %d: resampling conv needs 0 <= pad <= stride and k-1-pad < 2*stride", i); return -1; }
+    const int rows = (l.kind == 0 || l.kind == VQX_WN_RESAMPLE) ? l.cout : l.cin;
     max_rows = rows > max_rows ? rows : max_rows;
     const int64_t el = (int64_t)l.cout * l.cin * l.k;
     max_el = el > max_el ? el : max_el;
@@ -1069,8 +1112,10 @@ extern "C" int vqx_weight_norm_fwd(const vqx_wn_layer* lh, const vqx_wn_layer* l
   int max_units = 1, max_t_rows = 1;
   for (int i = 0; i < n_layers; ++i) {
     const vqx_wn_layer& l = lh[i];
-    if ((l.kind == 0 ? l.cin : l.cout) * l.k > kWnRow || l.k > 3) { set_error("vqx_weight_norm_fwd: layer %d row too long", i); return -1; }
-    const int units = l.kind == 0 ? l.cout : ((l.cin + 63) / 64) * ((l.cout + 15) / 16);
+    const bool rsm = l.kind >= VQX_WN_RESAMPLE;
+    const bool row_is_cout = l.kind == 0 || l.kind == VQX_WN_RESAMPLE;
+    if ((row_is_cout ? l.cin : l.cout) * l.k > kWnRow || (!rsm && l.k > 3)) { set_error("vqx_weight_norm_fwd: layer %d row too long", i); return -1; }
+    const int units = rsm ? (row_is_cout ? l.cout : l.cin) : l.kind == 0 ? l.cout : ((l.cin + 63) / 64) * ((l.cout + 15) / 16);
     max_units = units > max_units ? units : max_units;
     if (l.kind == 1) max_t_rows = l.cin > max_t_rows ? l.cin : max_t_rows;
   }
@@ -1093,12 +1138,14 @@ extern "C" int vqx_weight_norm_bwd(const vqx_wn_layer* lh, const vqx_wn_layer* l
       max_rows = blocks > max_rows ? blocks : max_rows;
       continue;
     }
-    if (l.kind != 0 && l.kind != 1) { set_error("vqx_weight_norm_bwd: layer %d bad kind", i); return -1; }
-    const int rows = l.kind == 0 ? l.cout : l.cin;
-    const int cols = (l.kind == 0 ? l.cin : l.cout) * l.k;
+    if (l.kind != 0 && l.kind != 1 && l.kind != VQX_WN_RESAMPLE && l.kind != VQX_WN_RESAMPLE_T) { set_error("vqx_weight_norm_bwd: layer %d bad kind", i); return -1; }
+    if (l.kind >= VQX_WN_RESAMPLE && !(l.stride >= 1 && l.pad >= 0 && l.pad <= l.stride && l.k - 1 - l.pad < 2 * l.stride)) { set_error("vqx_weight_norm_bwd: layer %d: bad resampling geometry", i); return -1; }
+    const bool row_is_cout = l.kind == 0 || l.kind == VQX_WN_RESAMPLE;
+    const int rows = row_is_cout ? l.cout : l.cin;
+    const int cols = (row_is_cout ? l.cin : l.cout) * l.k;
     if (cols > 4096) { set_error("vqx_weight_norm_bwd: row length %d > 4096", cols); return -1; }
     if (!l.slabs || !l.dv || (l.g && !l.dg) || l.splits < 1) { set_error("vqx_weight_norm_bwd: layer %d missing buffers", i); return -1; }
-    if ((l.kind == 0 ? l.cin : l.cout) % 4 || ((uintptr_t)l.slabs & 15)) { set_error("vqx_weight_norm_bwd: layer %d: slab rows must be 16-B vectors", i); return -1; }
+    if ((row_is_cout ? l.cin : l.cout) % 4 || ((uintptr_t)l.slabs & 15)) { set_error("vqx_weight_norm_bwd: layer %d: slab rows must be 16-B vectors", i); return -1; }
     max_rows = rows > max_rows ? rows : max_rows;
   }
   hipLaunchKernelGGL(wn_bwd_kernel, dim3(max_rows, n_layers), dim3(256), 0, (hipStream_t)stream, ld, n_layers);

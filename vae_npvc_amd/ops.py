@@ -190,6 +190,7 @@ def wn_table(layers):
             setattr(e, k, ptr(d.get(k)))
         e.kind, e.cout, e.cin, e.k = d["kind"], d["cout"], d["cin"], d["k"]
         e.splits, e.dtype = d.get("splits", 1), d["dtype"]
+        e.stride, e.pad = d.get("stride", 0), d.get("pad", 0)
     raw = bytes(arr)
     dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to("cuda")
     return arr, dev
