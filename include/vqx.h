@@ -409,9 +409,10 @@ int vqx_convert_2d(const void* src, int32_t ld_src, int32_t src_dtype, void* dst
 
 /* Thread-local description of the last failure. */
 const char* vqx_last_error(void);
-/* bf16 conv GEMM pipeline selector, kept for ABI stability: 0 = automatic,
- * 1 = BK 64 x 2-deep LDS-DMA ring (the only bf16 pipeline; BK 32 x 4-deep
- * measured slower on every layer, profiles/r01/gemm_lab.txt). */
+/* bf16 conv GEMM kernel policy (process-wide, for tests and A/B runs):
+ * 0 = automatic (3-tap, pad-1 FWD/DGRAD with T % 128 == 0 run the tap-reuse
+ * kernel, everything else the implicit-im2col kernel), 1 = implicit-im2col
+ * kernel only.  The environment variable VQX_TAP_REUSE=0 forces 1. */
 int vqx_set_gemm_tile(int32_t policy);
 
 /* Launch probe (measurement only; not reentrant while enabled).  While on,

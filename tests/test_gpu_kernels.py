@@ -15,10 +15,11 @@ def _ops():
     return ops
 
 
-@pytest.fixture(params=[0, 1], ids=["auto", "bk64x2"])
+@pytest.fixture(params=[0, 1], ids=["auto", "im2col"])
 def tile(request):
-    """Run a GEMM test with every bf16 pipeline variant (K-tile depth x ring
-    depth, vqx_gemm_inst.h); f32 has one pipeline."""
+    """Run a GEMM test under both kernel policies (vqx_set_gemm_tile): 0 lets
+    3-tap bf16 layers with T % 128 == 0 take the tap-reuse kernel, 1 keeps
+    every layer on the implicit-im2col kernel."""
     from vae_npvc_amd import _lib as L
     L.call("vqx_set_gemm_tile", request.param)
     yield request.param
@@ -318,3 +319,42 @@ def test_gnbwd_epilogue_matches_standalone(glu, tile):
     torch.cuda.synchronize()
     for a, b in zip(*outs):
         assert relerr(a, b) < 2e-2, relerr(a, b)
+
+
+@pytest.mark.parametrize("mode", ["fwd", "dgrad"])
+@pytest.mark.parametrize("n_utt,T,cin,cout", [(1, 128, 512, 512), (3, 128, 512, 1024), (2, 256, 1024, 512),
+                                               (1, 384, 128, 512), (2, 256, 512, 80)])
+def test_conv_tap_reuse_matches_im2col_and_fp64(mode, n_utt, T, cin, cout):
+    """The tap-reuse kernel (vqx_gemm_kernel.h conv_tr_kernel: one staged
+    130-frame window for all three taps, halo frames zeroed at utterance
+    edges) against the implicit-im2col kernel on the same bf16 operands and
+    against fp64 torch, with a bias + residual epilogue and fp32 output."""
+    ops = _ops()
+    from vae_npvc_amd import _lib as L
+    torch.manual_seed(7)
+    N = n_utt * T
+    k_in, k_out = (cin, cout) if mode == "fwd" else (cout, cin)  # GEMM K side / output channels
+    a = torch.randn(N, k_in, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(cout, cin, 3, device=DEV) / (cin * 3) ** 0.5).to(torch.bfloat16).float()
+    wp = pack(w).to(torch.bfloat16)
+    bias = torch.randn(k_out, device=DEV)
+    res = torch.randn(N, k_out, device=DEV).to(torch.bfloat16)
+    outs = []
+    for policy in (0, 1):
+        L.call("vqx_set_gemm_tile", policy)
+        y = torch.empty(N, k_out, device=DEV, dtype=torch.float32)
+        if mode == "fwd":
+            ops.conv_fwd(a, wp, y, T=T, cin=cin, cout=cout, ntaps=3, pad=1, bias=bias, res=res, out_f32=True)
+        else:
+            ops.conv_dgrad(a, wp, y, T=T, cin=cout, cout=cin, ntaps=3, pad=1, bias=bias, res=res, out_f32=True)
+        torch.cuda.synchronize()
+        outs.append(y)
+    L.call("vqx_set_gemm_tile", 0)
+    ad = a.double().cpu().view(n_utt, T, k_in).permute(0, 2, 1)
+    if mode == "fwd":
+        ref = F.conv1d(ad, w.double().cpu(), padding=1)
+    else:
+        ref = F.conv_transpose1d(ad, w.double().cpu(), padding=1)
+    ref = ref.permute(0, 2, 1).reshape(N, k_out) + bias.double().cpu() + res.double().cpu()
+    assert relerr(outs[0], outs[1]) < 1e-5  # same bf16 products, fp32 sums in another order
+    assert relerr(outs[0], ref) < 2e-5

@@ -49,6 +49,17 @@ void gemm_launch(const void* fn, int grid, hipStream_t s, const GemmParams& P, c
   (void)hipExtLaunchKernel(fn, dim3(grid), dim3(256), args, 0, s, ev.first, ev.second, 0);
 }
 
+// vqx_set_gemm_tile: 0 = automatic, 1 = implicit-im2col kernel only
+static int g_gemm_policy = 0;
+
+bool tap_reuse_enabled() {
+  static const bool env_on = [] {
+    const char* e = getenv("VQX_TAP_REUSE");
+    return !(e && e[0] == '0');
+  }();
+  return env_on && g_gemm_policy == 0;
+}
+
 static void launch_mode(GemmParams& P, int mode, int64_t rows, int extra_mult, bool bf16, bool gen, hipStream_t s) {
   // rows: extent of the tile-M dimension; extra_mult: split-K factor (WGRAD)
   P.tiles_m = (int)((rows + 127) / 128);
@@ -163,8 +174,8 @@ extern "C" int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream) {
 }
 
 extern "C" int vqx_set_gemm_tile(int32_t policy) {
-  // one bf16 pipeline remains (BK 64, 2-deep ring); kept for ABI stability
   if (policy < 0 || policy > 1) { set_error("vqx_set_gemm_tile: policy %d not in 0..1", policy); return -1; }
+  g_gemm_policy = policy;
   return 0;
 }
 

@@ -5,7 +5,7 @@
 // profiles/r01/gemm_lab.txt); f32 (parity mode) runs BK = 32, 2-deep.
 //
 // Instances: the bf16 fast path (no prologue, cin % 64 == 0) gets one kernel
-// per epilogue kind (EK_*); prologues, GEN tiles (cin % BK != 0) and f32 use
+// per epilogue kind (EK_*), and so does the tap-reuse kernel for 3-tap layers; prologues, GEN tiles (cin % BK != 0) and f32 use
 // the generic EK_ALL kernel.  WGRAD's epilogue is the slab store (EK_NONE).
 #pragma once
 #include "vqx_gemm_kernel.h"
@@ -14,6 +14,23 @@ namespace vqx {
 
 // vqx_gemm.hip: plain launch, or the probe's event-stamped launch
 void gemm_launch(const void* fn, int grid, hipStream_t s, const GemmParams& P, const int info[5], double flops);
+
+// vqx_gemm.hip: tap-reuse kernel switch (env VQX_TAP_REUSE=0 turns it off, for A/B runs)
+bool tap_reuse_enabled();
+
+// conv_tr_kernel applies: bf16, no prologue, 3 taps / pad 1, 32-channel K
+// slices, and every 128-frame tile inside one utterance
+inline bool tap_reuse_ok(const GemmParams& P, bool bf16, bool gen) {
+  return bf16 && !gen && P.pro == VQX_PRO_NONE && P.ntaps == 3 && P.pad == 1 && P.kcin % 32 == 0 &&
+         P.K == 3 * P.kcin && P.T % 128 == 0 && P.n_rows % 128 == 0 && tap_reuse_enabled();
+}
+
+template <int MODE, int EK>
+void launch_tr(const GemmParams& P, int grid, hipStream_t s) {
+  const double flops = 2.0 * (double)P.n_rows * P.Nc * P.K;
+  const int info[5] = {VQX_BF16, MODE, VQX_PRO_NONE, 2, EK};  // gen = 2: tap-reuse kernel
+  gemm_launch((const void*)conv_tr_kernel<MODE, EK>, grid, s, P, info, flops);
+}
 
 // smallest epilogue kind whose feature mask covers `epi`
 inline int pick_ek(int epi) {
@@ -62,6 +79,19 @@ void launch_mode_dt(const GemmParams& P, int grid, bool bf16, bool gen, hipStrea
   } else {
     if (P.pro != VQX_PRO_NONE) {
       launch_pro<bf16_t, MODE, false, EK_ALL>(P, grid, s);
+      return;
+    }
+    if (tap_reuse_ok(P, bf16, gen)) {
+      switch (pick_ek(P.epi)) {
+        case EK_NONE: launch_tr<MODE, EK_NONE>(P, grid, s); break;
+        case EK_ELEM: launch_tr<MODE, EK_ELEM>(P, grid, s); break;
+        case EK_GNADD: launch_tr<MODE, EK_GNADD>(P, grid, s); break;
+        case EK_SPLIT: launch_tr<MODE, EK_SPLIT>(P, grid, s); break;
+        case EK_COLSUM: launch_tr<MODE, EK_COLSUM>(P, grid, s); break;
+        case EK_GNSTATS: launch_tr<MODE, EK_GNSTATS>(P, grid, s); break;
+        case EK_GNBWD: launch_tr<MODE, EK_GNBWD>(P, grid, s); break;
+        default: launch_tr<MODE, EK_ALL>(P, grid, s); break;
+      }
       return;
     }
     switch (pick_ek(P.epi)) {

@@ -389,6 +389,138 @@ __device__ __forceinline__ void wait_vm(int n) {
   }
 }
 
+// Epilogue of a 128x128 output tile (shared by conv_gemm_kernel and
+// conv_tr_kernel).  The accumulator tile goes through LDS one 64-row slab at a
+// time so the epilogue reads and writes whole rows: 16 lanes x 8 consecutive
+// columns per row, every global access 16 B and each row segment contiguous.
+// Lane holds (before the transpose) output row wm*64 + mi*32 + r32 and, per
+// register group gq, columns wn*64 + ni*32 + 8*gq + 4*h + (0..3).  Needs
+// 44 KiB of `smem`; the caller's staging buffers must be free.
+template <typename T, int MODE, int EK>
+__device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&acc)[2][2], char* smem, int m0, int n0,
+                                              int tn, int split) {
+  constexpr int EMASK = ek_mask(EK);
+  constexpr int SUB = 1;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int r32 = lane & 31, h = lane >> 5;
+  constexpr int EP_LD = kBN + 4;  // floats; +4 keeps the b128 writes conflict-free
+  constexpr int EROWS = 16 * SUB;  // rows per pass
+  float* ep = (float*)smem;                 // [64][EP_LD]
+  float* csr = (float*)(smem + 36864);      // COLSUM reduction [EROWS][kBN]
+  const int er = tid >> 4, ec = (tid & 15) * 8;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // COLSUM accumulators
+  float mn = 0.f, mm = 0.f, mq = 0.f;                       // GNSTATS running (count, mean, M2)
+  float gs[4] = {0.f, 0.f, 0.f, 0.f};                       // GNBWD sums
+  __syncthreads();  // staging buffers are free
+#pragma unroll
+  for (int slab = 0; slab < 2 * SUB; ++slab) {
+    if (wm == slab) {
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int gq = 0; gq < 4; ++gq) {
+            const f32x4_t v = {acc[mi][ni][4 * gq], acc[mi][ni][4 * gq + 1], acc[mi][ni][4 * gq + 2],
+                               acc[mi][ni][4 * gq + 3]};
+            *(f32x4_t*)(ep + (mi * 32 + r32) * EP_LD + wn * 64 + ni * 32 + 8 * gq + 4 * h) = v;
+          }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int pass = 0; pass < 64 / EROWS; ++pass) {
+      const int lr = pass * EROWS + er;
+      const f32x4_t lo = *(const f32x4_t*)(ep + lr * EP_LD + ec);
+      const f32x4_t hi = *(const f32x4_t*)(ep + lr * EP_LD + ec + 4);
+      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const int64_t row = (int64_t)m0 + slab * 64 + lr;
+      const int col = n0 + ec;
+      if constexpr (MODE == MODE_WGRAD) {
+        if (row < P.Mc && col < P.Nc) {  // Nc % 8 == 0
+          float* out = (float*)P.y + (int64_t)split * P.Mc * P.Nc + row * P.Nc + col;
+          st8_nt<float, VQX_NT_SLAB>(out, 0, v);
+        }
+      } else {
+        if (row < P.n_rows && col < P.Nc) {
+          epilogue8<T, EMASK>(P, row, col, v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) cs[e] += v[e];
+          if (P.epi & EMASK & VQX_EPI_GNSTATS) {  // two-pass moments of the 8 values, merged
+            float m8 = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) m8 += v[e];
+            m8 *= 0.125f;
+            float q8 = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) q8 = fmaf(v[e] - m8, v[e] - m8, q8);
+            moments_merge(mn, mm, mq, 8.f, m8, q8);
+          }
+          if (P.epi & EMASK & VQX_EPI_GNBWD) gnbwd8<T>(P, row, col, v, gs);
+        }
+      }
+    }
+    __syncthreads();
+    if constexpr (MODE != MODE_WGRAD) {
+      // per-(128-row group, column tile) GroupNorm partials
+      if ((P.epi & EMASK & (VQX_EPI_GNSTATS | VQX_EPI_GNBWD)) && (slab & 1)) {
+        const int64_t grp_row = (int64_t)m0 + (slab >> 1) * 128;
+        float* out = P.stat_part + ((grp_row / 128) * P.tiles_n + tn) * 4;
+        if (P.epi & EMASK & VQX_EPI_GNSTATS) {
+          // merge the 64 lanes of each wave, then the waves (deterministic order)
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) {
+            const float n2 = __shfl_xor(mn, o, 64), m2 = __shfl_xor(mm, o, 64), q2 = __shfl_xor(mq, o, 64);
+            if ((lane & o) == 0) moments_merge(mn, mm, mq, n2, m2, q2);
+            else { float a = n2, b = m2, c = q2; moments_merge(a, b, c, mn, mm, mq); mn = a; mm = b; mq = c; }
+          }
+          if (lane == 0) { csr[3 * wid] = mn; csr[3 * wid + 1] = mm; csr[3 * wid + 2] = mq; }
+          __syncthreads();
+          if (tid == 0 && grp_row < P.n_rows) {
+            float a = csr[0], b = csr[1], c = csr[2];
+            for (int w = 1; w < 4 * SUB; ++w) moments_merge(a, b, c, csr[3 * w], csr[3 * w + 1], csr[3 * w + 2]);
+            out[0] = a; out[1] = b; out[2] = c; out[3] = 0.f;
+          }
+          mn = mm = mq = 0.f;
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            float x = wave_sum(gs[k]);
+            if (lane == 0) csr[4 * wid + k] = x;
+            gs[k] = 0.f;
+          }
+          __syncthreads();
+          if (tid < 4 && grp_row < P.n_rows) {
+            float x = 0.f;
+            for (int w = 0; w < 4 * SUB; ++w) x += csr[4 * w + tid];
+            out[tid] = x;
+          }
+        }
+        __syncthreads();
+      }
+      // per-128-row-group column sums of the stored values (bias gradient of
+      // the layer this output feeds), reduced over the EROWS row lanes in LDS
+      if ((P.epi & EMASK & VQX_EPI_COLSUM) && (slab & 1)) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          csr[er * kBN + ec + e] = cs[e];
+          cs[e] = 0.f;
+        }
+        __syncthreads();
+        const int64_t grp_row = (int64_t)m0 + (slab >> 1) * 128;
+        if (tid < kBN && n0 + tid < P.Nc && grp_row < P.n_rows) {
+          float t = 0.f;
+#pragma unroll
+          for (int r = 0; r < EROWS; ++r) t += csr[r * kBN + tid];
+          P.colsum_part[(grp_row / 128) * P.Nc + n0 + tid] = t;
+        }
+        __syncthreads();
+      }
+    }
+  }
+}
+
 // Staging layout.  The block tile is 128 x 128 with 4 waves in a 2 x 2 grid
 // of 64 x 64 wave tiles.  A K-tile operand (A rows x BK, or BK x 128 B
 // columns) is 128*BK*sizeof(T) bytes = PIECES pieces of 1 KiB; wave w fills
@@ -410,10 +542,9 @@ __device__ __forceinline__ void wait_vm(int n) {
 // Two 4-wave workgroups per CU either way.
 template <typename T, int MODE, int PRO, bool GEN, int BK, int NST, int EK>
 __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
-  constexpr int EMASK = ek_mask(EK);
   using C = Cfg<T>;
   constexpr int EPC = C::EPC, CPR = C::MNCPR, ES = sizeof(T);
-  constexpr int SUB = 1, BM = 128;
+  constexpr int BM = 128;
   constexpr int RB = BK * ES;                 // K-major row bytes (64 or 128)
   constexpr int KCH = RB / 16;                // 16-B chunks per K-major row
   constexpr int OP_BYTES = 128 * BK * ES;     // one operand's K-tile
@@ -732,127 +863,156 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
   }
   return;
 #endif
-  // ---------------- epilogue
-  // The accumulator tile goes through LDS one 64-row slab at a time so the
-  // epilogue reads and writes whole rows: 16 lanes x 8 consecutive columns
-  // per row, every global access 16 B and each row segment contiguous.
-  // Lane holds (before the transpose) output row wm*64 + mi*32 + r32 and,
-  // per register group gq, columns wn*64 + ni*32 + 8*gq + 4*h + (0..3).
-  constexpr int EP_LD = kBN + 4;  // floats; +4 keeps the b128 writes conflict-free
-  constexpr int EROWS = 16 * SUB;  // rows per pass
-  float* ep = (float*)smem;                 // [64][EP_LD]
-  float* csr = (float*)(smem + 36864);      // COLSUM reduction [EROWS][kBN]
-  const int er = tid >> 4, ec = (tid & 15) * 8;
-  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // COLSUM accumulators
-  float mn = 0.f, mm = 0.f, mq = 0.f;                       // GNSTATS running (count, mean, M2)
-  float gs[4] = {0.f, 0.f, 0.f, 0.f};                       // GNBWD sums
-  __syncthreads();  // staging buffers are free
-#pragma unroll
-  for (int slab = 0; slab < 2 * SUB; ++slab) {
-    if (wm == slab) {
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-          for (int gq = 0; gq < 4; ++gq) {
-            const f32x4_t v = {acc[mi][ni][4 * gq], acc[mi][ni][4 * gq + 1], acc[mi][ni][4 * gq + 2],
-                               acc[mi][ni][4 * gq + 3]};
-            *(f32x4_t*)(ep + (mi * 32 + r32) * EP_LD + wn * 64 + ni * 32 + 8 * gq + 4 * h) = v;
-          }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int pass = 0; pass < 64 / EROWS; ++pass) {
-      const int lr = pass * EROWS + er;
-      const f32x4_t lo = *(const f32x4_t*)(ep + lr * EP_LD + ec);
-      const f32x4_t hi = *(const f32x4_t*)(ep + lr * EP_LD + ec + 4);
-      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      const int64_t row = (int64_t)m0 + slab * 64 + lr;
-      const int col = n0 + ec;
-      if constexpr (MODE == MODE_WGRAD) {
-        if (row < P.Mc && col < P.Nc) {  // Nc % 8 == 0
-          float* out = (float*)P.y + (int64_t)split * P.Mc * P.Nc + row * P.Nc + col;
-          st8_nt<float, VQX_NT_SLAB>(out, 0, v);
-        }
-      } else {
-        if (row < P.n_rows && col < P.Nc) {
-          epilogue8<T, EMASK>(P, row, col, v);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) cs[e] += v[e];
-          if (P.epi & EMASK & VQX_EPI_GNSTATS) {  // two-pass moments of the 8 values, merged
-            float m8 = 0.f;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) m8 += v[e];
-            m8 *= 0.125f;
-            float q8 = 0.f;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) q8 = fmaf(v[e] - m8, v[e] - m8, q8);
-            moments_merge(mn, mm, mq, 8.f, m8, q8);
-          }
-          if (P.epi & EMASK & VQX_EPI_GNBWD) gnbwd8<T>(P, row, col, v, gs);
-        }
-      }
-    }
-    __syncthreads();
-    if constexpr (MODE != MODE_WGRAD) {
-      // per-(128-row group, column tile) GroupNorm partials
-      if ((P.epi & EMASK & (VQX_EPI_GNSTATS | VQX_EPI_GNBWD)) && (slab & 1)) {
-        const int64_t grp_row = (int64_t)m0 + (slab >> 1) * 128;
-        float* out = P.stat_part + ((grp_row / 128) * P.tiles_n + tn) * 4;
-        if (P.epi & EMASK & VQX_EPI_GNSTATS) {
-          // merge the 64 lanes of each wave, then the waves (deterministic order)
-#pragma unroll
-          for (int o = 1; o < 64; o <<= 1) {
-            const float n2 = __shfl_xor(mn, o, 64), m2 = __shfl_xor(mm, o, 64), q2 = __shfl_xor(mq, o, 64);
-            if ((lane & o) == 0) moments_merge(mn, mm, mq, n2, m2, q2);
-            else { float a = n2, b = m2, c = q2; moments_merge(a, b, c, mn, mm, mq); mn = a; mm = b; mq = c; }
-          }
-          if (lane == 0) { csr[3 * wid] = mn; csr[3 * wid + 1] = mm; csr[3 * wid + 2] = mq; }
-          __syncthreads();
-          if (tid == 0 && grp_row < P.n_rows) {
-            float a = csr[0], b = csr[1], c = csr[2];
-            for (int w = 1; w < 4 * SUB; ++w) moments_merge(a, b, c, csr[3 * w], csr[3 * w + 1], csr[3 * w + 2]);
-            out[0] = a; out[1] = b; out[2] = c; out[3] = 0.f;
-          }
-          mn = mm = mq = 0.f;
-        } else {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            float x = wave_sum(gs[k]);
-            if (lane == 0) csr[4 * wid + k] = x;
-            gs[k] = 0.f;
-          }
-          __syncthreads();
-          if (tid < 4 && grp_row < P.n_rows) {
-            float x = 0.f;
-            for (int w = 0; w < 4 * SUB; ++w) x += csr[4 * w + tid];
-            out[tid] = x;
-          }
-        }
-        __syncthreads();
-      }
-      // per-128-row-group column sums of the stored values (bias gradient of
-      // the layer this output feeds), reduced over the EROWS row lanes in LDS
-      if ((P.epi & EMASK & VQX_EPI_COLSUM) && (slab & 1)) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          csr[er * kBN + ec + e] = cs[e];
-          cs[e] = 0.f;
-        }
-        __syncthreads();
-        const int64_t grp_row = (int64_t)m0 + (slab >> 1) * 128;
-        if (tid < kBN && n0 + tid < P.Nc && grp_row < P.n_rows) {
-          float t = 0.f;
-#pragma unroll
-          for (int r = 0; r < EROWS; ++r) t += csr[r * kBN + tid];
-          P.colsum_part[(grp_row / 128) * P.Nc + n0 + tid] = t;
-        }
-        __syncthreads();
-      }
-    }
-  }
+  tile_epilogue<T, MODE, EK>(P, acc, smem, m0, n0, tn, split);
 }
 
+
+// ---------------------------------------------------------------------------
+// Tap-reuse conv GEMM: FWD / DGRAD of a 3-tap, pad-1 conv in bf16 when every
+// 128-frame tile lies inside one utterance (T % 128 == 0).
+//
+// The implicit-im2col kernel above walks K = (tap, channel) and stages the
+// activation tile once per tap, i.e. the same frames three times, shifted by
+// one row.  Its main loop is bound by the L2 -> LDS staging rate
+// (profiles/r01/gemm_lab.txt: operand staging alone takes 47 of 66 us on
+// dec_in FWD).  Here a stage holds 32 channels of the 130 frames
+// m0-1 .. m0+128 and the matching 32-channel slices of all three taps' weights
+// (33 KiB), and the three taps are multiplied out of it by reading the
+// activation fragments one or two rows further down: 1.5x the MFMA work per
+// stage for 1.03x the staged bytes of a 64-deep K-tile, i.e. 0.69x the staged
+// bytes per FLOP.
+//
+// Frame m0-1 (m0+128) is staged as zero when the tile starts (ends) an
+// utterance: those rows are read only by tap 0 of the first row (tap 2 of the
+// last row), which is exactly the im2col zero padding.  The row-shifted
+// fragment reads stay conflict-free because the K-major swizzle depends on
+// row % 16 only and a fragment's 16-lane groups cover 16 distinct residues.
+template <int MODE, int EK>
+__global__ __launch_bounds__(256, 2) void conv_tr_kernel(GemmParams P) {
+  using T = bf16_t;
+  constexpr int ES = 2, EPC = 8, BKC = 32, KCH = 4;  // 32 channels per stage: 64-B K-major rows
+  constexpr int A_PIECES = 9;                          // 130 rows x 64 B, rounded up to 1-KiB pieces
+  constexpr int A_BYTES = A_PIECES * 1024;
+  constexpr int TAP_BYTES = 128 * BKC * ES;            // one tap's weight slice: 8 KiB
+  constexpr int STAGE = A_BYTES + 3 * TAP_BYTES;       // 33 KiB
+  constexpr int NST = 2;
+  constexpr int PWB = 3 * TAP_BYTES / 1024 / 4;        // weight pieces per wave per stage (6)
+  static_assert(NST * STAGE >= 45056, "epilogue staging needs 44 KiB of LDS");
+  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = lin / P.tiles_n, tn = lin - tm * P.tiles_n;
+  const int m0 = tm * 128, n0 = tn * kBN;
+  const int nk = P.kcin / BKC;
+
+  // activation pieces of this wave: wid, wid+4 and (wave 0) 8; stage row sr holds frame m0-1+sr
+  unsigned aoff[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int piece = wid + 4 * i;
+    const int c = piece * 64 + lane;
+    const int row = c / KCH, kch = (c % KCH) ^ kswz<KCH>(row);
+    bool ok = piece < A_PIECES && row < 130;
+    if (row == 0 && m0 % P.T == 0) ok = false;
+    if (row == 129 && (m0 + 128) % P.T == 0) ok = false;
+    // the descriptor base sits one activation row before P.a, so frame m0-1+row is at (m0+row) rows
+    aoff[i] = ok ? (unsigned)((((int64_t)m0 + row) * P.lda + kch * EPC) * ES) : kOOB;
+  }
+  // weight pieces wid*6 .. wid*6+5 of the stage: piece pb is tap pb/8, 1-KiB slice pb%8 of it
+  unsigned boff[PWB];
+#pragma unroll
+  for (int i = 0; i < PWB; ++i) {
+    const int pb = wid * PWB + i;
+    const int tap = pb >> 3, c = (pb & 7) * 64 + lane;
+    if constexpr (MODE == MODE_FWD) {  // We[co][tap*kcin + ci], K-major rows of 32 channels
+      const int row = c / KCH, kch = (c % KCH) ^ kswz<KCH>(row);
+      const int co = n0 + row;
+      boff[i] = co < P.Nc ? (unsigned)(((int64_t)co * P.K + tap * P.kcin + kch * EPC) * ES) : kOOB;
+    } else {  // forward weight We[co][j][ci] read as rows co of tap j = 2 - tap (taps flipped)
+      const int krow = c / 16, cch = (c % 16) ^ mn_swz(krow);
+      const int ci = n0 + cch * EPC;
+      boff[i] = ci < P.Nc ? (unsigned)(((int64_t)krow * 3 * P.cdim + (2 - tap) * P.cdim + ci) * ES) : kOOB;
+    }
+  }
+  const __amdgpu_buffer_rsrc_t rsA = rsrc_at(P.a, -(int64_t)P.lda * ES, P.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsB = rsrc_at(P.b, 0, P.b_bytes);
+
+  auto dma_stage = [&](int buf, int kt) {
+    const int c0 = kt * BKC;
+    const unsigned ksa = (unsigned)(c0 * ES);
+    const unsigned ksb = MODE == MODE_FWD ? (unsigned)(c0 * ES) : (unsigned)((int64_t)c0 * 3 * P.cdim * ES);
+    char* st = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      if (wid + 4 * i < A_PIECES) dma16(rsA, st + (wid + 4 * i) * 1024, aoff[i] + ksa);
+#pragma unroll
+    for (int i = 0; i < PWB; ++i) dma16(rsB, st + A_BYTES + (wid * PWB + i) * 1024, boff[i] + ksb);
+  };
+
+  f32x16_t acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int r32 = lane & 31, h = lane >> 5;
+  const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+  typedef short s16x8_t __attribute__((ext_vector_type(8)));
+
+  auto compute_stage = [&](int buf) {
+    const char* la = smem + buf * STAGE;
+#pragma unroll
+    for (int tap = 0; tap < 3; ++tap) {
+      const char* lb = la + A_BYTES + tap * TAP_BYTES;
+      bf16x8_t af[2][2], bfr[2][2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+          af[s][x] = *(const bf16x8_t*)(la + kmaj_off<KCH>(wm * 64 + x * 32 + r32 + tap, 2 * s + h));
+          if constexpr (MODE == MODE_FWD) {
+            bfr[s][x] = *(const bf16x8_t*)(lb + kmaj_off<KCH>(wn * 64 + x * 32 + r32, 2 * s + h));
+          } else {
+            const int kb = 16 * s + (g >> 1) * 8;
+            const int ch = ((wn * 64 + x * 32 + (g & 1) * 16) >> 3) + (p >> 1);
+            const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (VQX_LDS(s16x4_t)*)(lb + mnmaj_off<T>(kb + q, ch) + 8 * (p & 1)));
+            const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (VQX_LDS(s16x4_t)*)(lb + mnmaj_off<T>(kb + 4 + q, ch) + 8 * (p & 1)));
+            const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            bfr[s][x] = __builtin_bit_cast(bf16x8_t, v);
+          }
+        }
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[s][ni], af[s][mi], acc[mi][ni], 0, 0, 0);
+    }
+  };
+
+  if (nk > 0) {
+    dma_stage(0, 0);
+    wait_vm(0);
+    __builtin_amdgcn_s_barrier();
+    int buf = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) dma_stage(buf ^ 1, kt + 1);
+      compute_stage(buf);
+      wait_vm(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      buf ^= 1;
+    }
+  }
+  tile_epilogue<T, MODE, EK>(P, acc, smem, m0, n0, tn, 0);
+}
 
 }  // namespace vqx

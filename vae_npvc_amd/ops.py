@@ -114,7 +114,10 @@ class LaunchProbe:
             call("vqx_probe_read", i, info, ctypes.byref(fl), ctypes.byref(ms))
             dt, mode, pro, gen, ek = list(info)  # ek: epilogue kind (vqx_gemm_kernel.h EK_*)
             bk = 64 if dt == L.VQX_BF16 else 32
-            sym = f"vqx::conv_gemm_kernel<{self._DT[dt]}, {mode}, {pro}, {'true' if gen else 'false'}, {bk}, 2, {ek}>"
+            if gen == 2:  # tap-reuse kernel (3-tap FWD/DGRAD, vqx_gemm_kernel.h conv_tr_kernel)
+                sym = f"vqx::conv_tr_kernel<{mode}, {ek}>"
+            else:
+                sym = f"vqx::conv_gemm_kernel<{self._DT[dt]}, {mode}, {pro}, {'true' if gen else 'false'}, {bk}, 2, {ek}>"
             out.append((sym, fl.value, ms.value * 1e-3, self.shapes[i] if i < len(self.shapes) else ""))
         return out
 
