@@ -407,6 +407,14 @@ int vqx_scale_act_2d(const void* src, int32_t ld_src, int32_t src_dtype, void* d
 int vqx_convert_2d(const void* src, int32_t ld_src, int32_t src_dtype, void* dst, int32_t ld_dst,
                    int32_t dst_dtype, int64_t rows, int32_t cols, vqx_stream_t stream);
 
+/* Output tiles (workgroups per split) of the weight-gradient kernel that
+ * vqx_conv1d_wgrad would launch for these arguments: 3-tap, pad-1 bf16
+ * layers with T % 64 == 0 and c_dim % 64 == 0 run the tap-reuse kernel
+ * (128 rows x 3 taps x 64 channels per tile), the rest 128 x 128 tiles.
+ * Callers size `splits` (and the slab buffer) from it to fill the GPU. */
+int vqx_wgrad_tiles(int64_t n_rows, int32_t T, int32_t r_dim, int32_t c_dim, int32_t ntaps, int32_t pad,
+                    int32_t dtype, int32_t q_prologue, int32_t* tiles);
+
 /* Thread-local description of the last failure. */
 const char* vqx_last_error(void);
 /* bf16 conv GEMM kernel policy (process-wide, for tests and A/B runs):
@@ -428,7 +436,7 @@ int vqx_probe_count(int64_t* n);
 int vqx_probe_read(int64_t i, int32_t* info5, double* flops, float* ms);
 
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
-#define VQX_ABI_VERSION 110
+#define VQX_ABI_VERSION 111
 int vqx_version(void);
 
 #ifdef __cplusplus

@@ -358,3 +358,39 @@ def test_conv_tap_reuse_matches_im2col_and_fp64(mode, n_utt, T, cin, cout):
     ref = ref.permute(0, 2, 1).reshape(N, k_out) + bias.double().cpu() + res.double().cpu()
     assert relerr(outs[0], outs[1]) < 1e-5  # same bf16 products, fp32 sums in another order
     assert relerr(outs[0], ref) < 2e-5
+
+
+@pytest.mark.parametrize("sign", [1, -1])
+@pytest.mark.parametrize("n_utt,T,r_dim,c_dim,splits", [(2, 128, 512, 512, 3), (3, 64, 80, 192, 2), (1, 256, 128, 64, 4),
+                                                         (2, 256, 1024, 512, 5), (4, 64, 256, 128, 16)])
+def test_wgrad_tap_reuse_matches_im2col_and_fp64(sign, n_utt, T, r_dim, c_dim, splits):
+    """The tap-reuse weight gradient (vqx_gemm_kernel.h wgrad_tr_kernel:
+    128 r x 3 taps x 64 c tiles, one staged 66-frame q window per K-tile)
+    against the implicit-im2col kernel and fp64, for both shift signs (Conv1d
+    and ConvTranspose1d), partial r tiles, empty splits and K-tiles that
+    start or end utterances."""
+    ops = _ops()
+    from vae_npvc_amd import _lib as L
+    torch.manual_seed(11)
+    N = n_utt * T
+    p = torch.randn(N, r_dim, device=DEV).to(torch.bfloat16)
+    q = torch.randn(N, c_dim, device=DEV).to(torch.bfloat16)
+    assert ops.wgrad_tiles(N, T, r_dim, c_dim, 3, 1, L.VQX_BF16) == -(-r_dim // 128) * (c_dim // 64)
+    outs = []
+    for policy in (0, 1):
+        L.call("vqx_set_gemm_tile", policy)
+        slabs = torch.full((splits, r_dim, 3 * c_dim), float("nan"), device=DEV)
+        ops.conv_wgrad(p, q, slabs, T=T, r_dim=r_dim, c_dim=c_dim, ntaps=3, pad=1, shift_sign=sign, splits=splits)
+        torch.cuda.synchronize()
+        outs.append(slabs.sum(0))
+    L.call("vqx_set_gemm_tile", 0)
+    pd = p.double().cpu().view(n_utt, T, r_dim)
+    qd = q.double().cpu().view(n_utt, T, c_dim)
+    ref = torch.zeros(r_dim, 3, c_dim, dtype=torch.float64)
+    for j in range(3):
+        sh = sign * (j - 1)
+        lo, hi = max(0, -sh), min(T, T - sh)
+        ref[:, j] = torch.einsum("btr,btc->rc", pd[:, lo:hi], qd[:, lo + sh:hi + sh])
+    ref = ref.reshape(r_dim, 3 * c_dim)
+    assert relerr(outs[0], outs[1]) < 1e-5
+    assert relerr(outs[0], ref) < 2e-5

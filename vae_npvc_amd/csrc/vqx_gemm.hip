@@ -168,9 +168,28 @@ extern "C" int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream) {
   P.y = a->slabs;
   const int bkv = a->dtype == VQX_BF16 ? 64 : 32;
   const bool gen = (a->T % bkv) != 0 || (a->n_rows % bkv) != 0;
+  if (!gen && wgrad_tr_ok(a->n_rows, a->T, a->c_dim, a->ntaps, a->pad, a->dtype == VQX_BF16, a->q_prologue)) {
+    P.tap_reuse = 1;
+    P.tiles_n = a->c_dim / 64;
+  }
   hipStream_t s = (hipStream_t)stream;
   launch_mode(P, MODE_WGRAD, P.Mc, P.splits, a->dtype == VQX_BF16, gen, s);
   return launch_status("vqx_conv1d_wgrad");
+}
+
+extern "C" int vqx_wgrad_tiles(int64_t n_rows, int32_t T, int32_t r_dim, int32_t c_dim, int32_t ntaps, int32_t pad,
+                               int32_t dtype, int32_t q_prologue, int32_t* tiles) {
+  if (!tiles || n_rows <= 0 || T <= 0 || r_dim <= 0 || c_dim <= 0 || ntaps < 1 || ntaps > 3) {
+    set_error("vqx_wgrad_tiles: bad arguments");
+    return -1;
+  }
+  const bool bf16 = dtype == VQX_BF16;
+  const int bkv = bf16 ? 64 : 32;
+  const bool gen = (T % bkv) != 0 || (n_rows % bkv) != 0;
+  const int tm = (r_dim + 127) / 128;
+  if (!gen && wgrad_tr_ok(n_rows, T, c_dim, ntaps, pad, bf16, q_prologue)) *tiles = tm * (c_dim / 64);
+  else *tiles = tm * ((ntaps * c_dim + kBN - 1) / kBN);
+  return 0;
 }
 
 extern "C" int vqx_set_gemm_tile(int32_t policy) {

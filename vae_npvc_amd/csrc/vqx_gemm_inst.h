@@ -25,6 +25,13 @@ inline bool tap_reuse_ok(const GemmParams& P, bool bf16, bool gen) {
          P.K == 3 * P.kcin && P.T % 128 == 0 && P.n_rows % 128 == 0 && tap_reuse_enabled();
 }
 
+// wgrad_tr_kernel applies: bf16, no prologue, 3 taps / pad 1, c_dim % 64 == 0,
+// 64-frame K-tiles inside one utterance
+inline bool wgrad_tr_ok(int64_t n_rows, int T, int c_dim, int ntaps, int pad, bool bf16, int pro) {
+  return bf16 && pro == VQX_PRO_NONE && ntaps == 3 && pad == 1 && c_dim % 64 == 0 && T % 64 == 0 &&
+         n_rows % 64 == 0 && tap_reuse_enabled();
+}
+
 template <int MODE, int EK>
 void launch_tr(const GemmParams& P, int grid, hipStream_t s) {
   const double flops = 2.0 * (double)P.n_rows * P.Nc * P.K;
@@ -75,6 +82,12 @@ void launch_mode_dt(const GemmParams& P, int grid, bool bf16, bool gen, hipStrea
     return;
   }
   if constexpr (MODE == MODE_WGRAD) {
+    if (P.tap_reuse) {
+      const double flops = 2.0 * (double)P.n_rows * P.Mc * P.Nc;
+      const int info[5] = {VQX_BF16, MODE_WGRAD, VQX_PRO_NONE, 2, EK_NONE};  // gen = 2: tap-reuse kernel
+      gemm_launch((const void*)wgrad_tr_kernel<EK_NONE>, grid, s, P, info, flops);
+      return;
+    }
     launch_pro<bf16_t, MODE, false, EK_NONE>(P, grid, s);
   } else {
     if (P.pro != VQX_PRO_NONE) {

@@ -78,6 +78,7 @@ struct GemmParams {
   float* colsum_part;
   float* stat_part;  // GNSTATS / GNBWD per-(128-row group, column tile) partials
   int gn_groups, gn_glu;
+  int tap_reuse;   // WGRAD: 1 = wgrad_tr_kernel tiling (tiles_n counts 64-channel blocks of c)
 };
 
 template <typename T> struct Cfg;
@@ -1013,6 +1014,185 @@ __global__ __launch_bounds__(256, 2) void conv_tr_kernel(GemmParams P) {
     }
   }
   tile_epilogue<T, MODE, EK>(P, acc, smem, m0, n0, tn, 0);
+}
+
+// ---------------------------------------------------------------------------
+// Tap-reuse weight gradient of a 3-tap, pad-1 conv (bf16, T % 64 == 0):
+//   S[r][j*cd + c] = sum_n p[n][r] * q[n + sign*(j-1)][c],  j = 0, 1, 2.
+// The implicit-im2col WGRAD tiles the output 128 x 128, so each of the three
+// taps' column blocks stages the same q frames again, one row shifted.  Here a
+// workgroup owns 128 rows r x (3 taps x 64 channels c): a stage holds 64
+// frames of p (16 KiB) and the 66 frames k0-1 .. k0+64 of q for its 64
+// channels (9 KiB), and the three taps read the q fragments 0, 1 or 2 rows
+// down.  24 MFMAs per wave per stage for 25 KiB staged: 2x the FLOPs per
+// staged byte of the 128 x 128 tile.  Split-K as before; each 64-frame K-tile
+// lies inside one utterance, so the halo frames are zero exactly when the
+// K-tile starts (ends) an utterance.
+//
+// LDS: p as 256-B rows (mn_swz, read with ds_read_b64_tr_b16 like the other
+// WGRAD), q as 128-B rows with the chunk XOR ((row >> 1) & 1) << 2: any four
+// consecutive rows land in four distinct 64-B bank groups, whatever the tap
+// shift.
+__device__ __forceinline__ int q_off128(int row, int ch) { return row * 128 + 16 * (ch ^ (((row >> 1) & 1) << 2)); }
+
+template <int EK>  // slab store only (EK_NONE); a template so every instantiation unit may include it
+__global__ __launch_bounds__(256, 2) void wgrad_tr_kernel(GemmParams P) {
+  using T = bf16_t;
+  constexpr int ES = 2, EPC = 8, BK = 64;
+  constexpr int A_BYTES = BK * 256;              // p: 64 frames x 128 r
+  constexpr int B_PIECES = 9;                    // q: 66 frames x 64 c (72-row capacity)
+  constexpr int B_BYTES = B_PIECES * 1024;
+  constexpr int STAGE = A_BYTES + B_BYTES;       // 25 KiB
+  constexpr int NST = 2;
+  constexpr int EP_LD = 64 + 4;                  // epilogue row pitch (floats)
+  constexpr int SMEM = NST * STAGE > 128 * EP_LD * 4 ? NST * STAGE : 128 * EP_LD * 4;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int tiles_mn = P.tiles_m * P.tiles_n;
+  const int split = lin / tiles_mn;
+  const int tmn = lin - split * tiles_mn;
+  const int tm = tmn / P.tiles_n, tn = tmn - tm * P.tiles_n;
+  const int r0 = tm * 128, c0 = tn * 64;
+  const int64_t kbeg = (int64_t)split * P.k_per_split;
+  int64_t kend = kbeg + P.k_per_split;
+  if (kend > P.n_rows) kend = P.n_rows;
+  const int nk = kend > kbeg ? (int)((kend - kbeg) / BK) : 0;
+
+  // p pieces wid*4 .. wid*4+3 (16 per stage)
+  unsigned aoff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = (wid * 4 + i) * 64 + lane;
+    const int krow = c / 16, cch = (c % 16) ^ mn_swz(krow);
+    const int r = r0 + cch * EPC;
+    aoff[i] = r < P.Mc ? (unsigned)(((int64_t)krow * P.lda + r) * ES) : kOOB;
+  }
+  // q pieces wid, wid+4 and (wave 0) 8; stage row sr holds frame k0-1+sr
+  unsigned boff[3];
+  int bedge[3];  // 1: the k0-1 halo row, 2: the k0+64 halo row
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int piece = wid + 4 * i;
+    const int c = piece * 64 + lane;
+    const int row = c / 8, ch = (c % 8) ^ (((row >> 1) & 1) << 2);
+    const int cc = c0 + ch * EPC;
+    bedge[i] = row == 0 ? 1 : (row == 65 ? 2 : 0);
+    // descriptor base one q row before P.b: frame k0-1+row sits at (k0+row) rows
+    boff[i] = (piece < B_PIECES && row < 66 && cc < P.cdim) ? (unsigned)(((int64_t)row * P.ldb + cc) * ES) : kOOB;
+  }
+  const __amdgpu_buffer_rsrc_t rsA = rsrc_at(P.a, 0, P.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsB = rsrc_at(P.b, -(int64_t)P.ldb * ES, P.b_bytes);
+
+  auto dma_stage = [&](int buf, int kt) {
+    const int64_t k0 = kbeg + (int64_t)kt * BK;
+    const int t0 = (int)(k0 % P.T);
+    const int edge = (t0 == 0 ? 1 : 0) | (t0 + BK == P.T ? 2 : 0);  // halo rows outside the utterance
+    const unsigned ksa = (unsigned)(k0 * P.lda * ES), ksb = (unsigned)(k0 * P.ldb * ES);
+    char* st = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dma16(rsA, st + (wid * 4 + i) * 1024, aoff[i] + ksa);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      if (wid + 4 * i < B_PIECES)
+        dma16(rsB, st + A_BYTES + (wid + 4 * i) * 1024, (bedge[i] & edge) ? kOOB : boff[i] + ksb);
+  };
+
+  f32x16_t acc[2][3];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int r32 = lane & 31, h = lane >> 5;
+  const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+  typedef short s16x8_t __attribute__((ext_vector_type(8)));
+  const int ro0 = 1 - P.sign, ro2 = 1 + P.sign;  // stage-row offset of taps 0 and 2 (tap 1: 1)
+
+  auto compute_stage = [&](int buf) {
+    const char* la = smem + buf * STAGE;
+    const char* lb = la + A_BYTES;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      bf16x8_t af[2], bfr[3];
+#pragma unroll
+      for (int x = 0; x < 2; ++x) {
+        const int kb = 16 * s + (g >> 1) * 8;
+        const int ch = ((wm * 64 + x * 32 + (g & 1) * 16) >> 3) + (p >> 1);
+        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (VQX_LDS(s16x4_t)*)(la + mnmaj_off<T>(kb + q, ch) + 8 * (p & 1)));
+        const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (VQX_LDS(s16x4_t)*)(la + mnmaj_off<T>(kb + 4 + q, ch) + 8 * (p & 1)));
+        const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[x] = __builtin_bit_cast(bf16x8_t, v);
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int ro = j == 0 ? ro0 : (j == 1 ? 1 : ro2);
+        const int kb = 16 * s + (g >> 1) * 8 + ro;
+        const int ch = ((wn * 32 + (g & 1) * 16) >> 3) + (p >> 1);
+        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (VQX_LDS(s16x4_t)*)(lb + q_off128(kb + q, ch) + 8 * (p & 1)));
+        const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (VQX_LDS(s16x4_t)*)(lb + q_off128(kb + 4 + q, ch) + 8 * (p & 1)));
+        const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfr[j] = __builtin_bit_cast(bf16x8_t, v);
+      }
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          acc[mi][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[mi], acc[mi][j], 0, 0, 0);
+    }
+  };
+
+  if (nk > 0) {
+    dma_stage(0, 0);
+    wait_vm(0);
+    __builtin_amdgcn_s_barrier();
+    int buf = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) dma_stage(buf ^ 1, kt + 1);
+      compute_stage(buf);
+      wait_vm(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      buf ^= 1;
+    }
+  }
+
+  // slab store, one tap at a time through LDS: rows of 64 channels, 8 lanes x 8 floats each
+  float* ep = (float*)smem;
+  float* slab = (float*)P.y + (int64_t)split * P.Mc * P.Nc;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    __syncthreads();
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const f32x4_t v = {acc[mi][j][4 * gq], acc[mi][j][4 * gq + 1], acc[mi][j][4 * gq + 2], acc[mi][j][4 * gq + 3]};
+        *(f32x4_t*)(ep + (wm * 64 + mi * 32 + r32) * EP_LD + wn * 32 + 8 * gq + 4 * h) = v;
+      }
+    __syncthreads();
+#pragma unroll
+    for (int pass = 0; pass < 4; ++pass) {
+      const int lr = pass * 32 + (tid >> 3), lc = (tid & 7) * 8;
+      const int r = r0 + lr, cc = c0 + lc;
+      if (r < P.Mc && cc < P.cdim) {
+        const f32x4_t lo = *(const f32x4_t*)(ep + lr * EP_LD + lc);
+        const f32x4_t hi = *(const f32x4_t*)(ep + lr * EP_LD + lc + 4);
+        float* o = slab + (int64_t)r * P.Nc + j * P.cdim + cc;
+        *(f32x4_t*)o = lo;
+        *(f32x4_t*)(o + 4) = hi;
+      }
+    }
+  }
 }
 
 }  // namespace vqx

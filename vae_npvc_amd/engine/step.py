@@ -237,15 +237,17 @@ class VQVAEEngine:
         # split-K factors for the wgrad GEMMs: one full round of ~480-512
         # workgroups (2 per CU) at config 2 (64 x 256 frames), at least 4
         # K-tiles (256 frames) per split.  Measured sweep (tools/gemm_bench.py
-        # --sweep-splits): dec_in best at 5, enc k3 at 10, res/skip at 24,
-        # enc skip at 32 -- exactly floor(512 / tiles).
-        N_ref = 64 * 256
+        # --sweep-splits) on 128 x 128 tiles: dec_in best at 5, enc k3 at 10,
+        # res/skip at 24, enc skip at 32 -- exactly floor(512 / tiles).  The
+        # tile count comes from the library (3-tap layers use the tap-reuse
+        # kernel's 128 x 192 tiles).
+        N_ref, T_ref = 64 * 256, 256
         for Lr in self.convs:
             if Lr in self.dec_cond:
                 Lr.splits = 1
                 continue
-            r, c = (Lr.cin, Lr.k * Lr.cout) if Lr.kind else (Lr.cout, Lr.k * Lr.cin)
-            tiles = math.ceil(r / 128) * math.ceil(c / 128)
+            r, c = (Lr.cin, Lr.cout) if Lr.kind else (Lr.cout, Lr.cin)
+            tiles = ops.wgrad_tiles(N_ref, T_ref, r, c, Lr.k, Lr.pad, self.dt)
             Lr.splits = max(1, min(512 // tiles, N_ref // 256))
         # slab arena: one backward group's slabs at a time (kept L2/MALL-resident)
         groups = self._bwd_groups()

@@ -114,7 +114,9 @@ class LaunchProbe:
             call("vqx_probe_read", i, info, ctypes.byref(fl), ctypes.byref(ms))
             dt, mode, pro, gen, ek = list(info)  # ek: epilogue kind (vqx_gemm_kernel.h EK_*)
             bk = 64 if dt == L.VQX_BF16 else 32
-            if gen == 2:  # tap-reuse kernel (3-tap FWD/DGRAD, vqx_gemm_kernel.h conv_tr_kernel)
+            if gen == 2 and mode == 2:  # tap-reuse weight gradient (vqx_gemm_kernel.h wgrad_tr_kernel)
+                sym = f"vqx::wgrad_tr_kernel<{ek}>"
+            elif gen == 2:  # tap-reuse kernel (3-tap FWD/DGRAD, vqx_gemm_kernel.h conv_tr_kernel)
                 sym = f"vqx::conv_tr_kernel<{mode}, {ek}>"
             else:
                 sym = f"vqx::conv_gemm_kernel<{self._DT[dt]}, {mode}, {pro}, {'true' if gen else 'false'}, {bk}, 2, {ek}>"
@@ -182,6 +184,13 @@ def conv_wgrad(p, q, slabs, *, T, r_dim, c_dim, ntaps, pad, shift_sign=1, q_prol
         _probe.shapes.append(f"{r_dim}x{ntaps}x{c_dim} s{splits}")
     call("vqx_conv1d_wgrad", ctypes.byref(a), stream_ptr())
     return slabs
+
+
+def wgrad_tiles(n_rows, T, r_dim, c_dim, ntaps, pad, dtype, q_prologue=L.PRO_NONE):
+    """Output tiles per split of the weight-gradient kernel conv_wgrad would launch."""
+    t = ctypes.c_int32()
+    call("vqx_wgrad_tiles", n_rows, T, r_dim, c_dim, ntaps, pad, dtype, q_prologue, ctypes.byref(t))
+    return t.value
 
 
 def wn_table(layers):
