@@ -394,3 +394,28 @@ def test_wgrad_tap_reuse_matches_im2col_and_fp64(sign, n_utt, T, r_dim, c_dim, s
     ref = ref.reshape(r_dim, 3 * c_dim)
     assert relerr(outs[0], outs[1]) < 1e-5
     assert relerr(outs[0], ref) < 2e-5
+
+
+@pytest.mark.parametrize("acc", [False, True])
+def test_split_epilogue_with_narrow_residual(acc, tile):
+    """res/skip output split (decoder res_skip layer, layers.py:244-249): the
+    GEMM's columns >= split_col go to the fp32 skip accumulator and only the
+    first split_col columns take the residual, whose buffer is exactly
+    split_col wide (no read past it on the split columns)."""
+    ops = _ops()
+    torch.manual_seed(5)
+    B, T, cin, C, S = 2, 128, 512, 512, 128
+    N = B * T
+    x = torch.randn(N, cin, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(C + S, cin, 1, device=DEV) / cin ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(C + S, device=DEV)
+    res = torch.randn(N, C, device=DEV).to(torch.bfloat16)  # exactly split_col wide
+    skip0 = torch.randn(N, S, device=DEV)
+    skip = skip0.clone()
+    y = torch.empty(N, C, device=DEV, dtype=torch.bfloat16)
+    ops.conv_fwd(x, pack(w.float()).to(torch.bfloat16), y, T=T, cin=cin, cout=C + S, ntaps=1, pad=0, bias=bias,
+                 res=res, out2=skip, split_col=C, out2_accumulate=acc)
+    torch.cuda.synchronize()
+    full = x.double().cpu() @ w.double().cpu()[:, :, 0].t() + bias.double().cpu()
+    assert relerr(y, full[:, :C] + res.double().cpu()) < 2e-2
+    assert relerr(skip, full[:, C:] + (skip0.double().cpu() if acc else 0)) < 2e-2
