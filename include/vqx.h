@@ -407,11 +407,12 @@ int vqx_scale_act_2d(const void* src, int32_t ld_src, int32_t src_dtype, void* d
 int vqx_convert_2d(const void* src, int32_t ld_src, int32_t src_dtype, void* dst, int32_t ld_dst,
                    int32_t dst_dtype, int64_t rows, int32_t cols, vqx_stream_t stream);
 
-/* Output tiles (workgroups per split) of the weight-gradient kernel that
- * vqx_conv1d_wgrad would launch for these arguments: 3-tap, pad-1 bf16
- * layers with T % 64 == 0 and c_dim % 64 == 0 run the tap-reuse kernel
- * (128 rows x 3 taps x 64 channels per tile), the rest 128 x 128 tiles.
- * Callers size `splits` (and the slab buffer) from it to fill the GPU. */
+/* Work units per split of the weight-gradient kernel that vqx_conv1d_wgrad
+ * would launch for these arguments, one unit = one 4-wave group (two per CU
+ * fill the GPU): 3-tap, pad-1 bf16 layers with T % 64 == 0 and
+ * c_dim % 64 == 0 run the tap-reuse kernel (128 rows x 3 taps x 64 channels
+ * per tile, two 4-wave K groups per tile), the rest one group per 128 x 128
+ * tile.  Callers size `splits` (and the slab buffer) from it. */
 int vqx_wgrad_tiles(int64_t n_rows, int32_t T, int32_t r_dim, int32_t c_dim, int32_t ntaps, int32_t pad,
                     int32_t dtype, int32_t q_prologue, int32_t* tiles);
 

@@ -25,16 +25,17 @@ static std::vector<ProbeRec> g_probe;
 static std::vector<std::pair<hipEvent_t, hipEvent_t>> g_event_pool;
 static size_t g_probe_used = 0;
 
-void gemm_launch(const void* fn, int grid, hipStream_t s, const GemmParams& P, const int info[5], double flops) {
+void gemm_launch(const void* fn, int grid, hipStream_t s, const GemmParams& P, const int info[5], double flops,
+                 int block) {
   void* args[] = {(void*)&P};
   if (!g_probe_on) {
-    (void)hipLaunchKernel(fn, dim3(grid), dim3(256), args, 0, s);
+    (void)hipLaunchKernel(fn, dim3(grid), dim3(block), args, 0, s);
     return;
   }
   if (g_probe_used == g_event_pool.size()) {
     hipEvent_t a, b;
     if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
-      (void)hipLaunchKernel(fn, dim3(grid), dim3(256), args, 0, s);
+      (void)hipLaunchKernel(fn, dim3(grid), dim3(block), args, 0, s);
       return;
     }
     g_event_pool.emplace_back(a, b);
@@ -46,7 +47,7 @@ void gemm_launch(const void* fn, int grid, hipStream_t s, const GemmParams& P, c
   for (int i = 0; i < 5; ++i) r.info[i] = info[i];
   r.flops = flops;
   g_probe.push_back(r);
-  (void)hipExtLaunchKernel(fn, dim3(grid), dim3(256), args, 0, s, ev.first, ev.second, 0);
+  (void)hipExtLaunchKernel(fn, dim3(grid), dim3(block), args, 0, s, ev.first, ev.second, 0);
 }
 
 // vqx_set_gemm_tile: 0 = automatic, 1 = implicit-im2col kernel only
@@ -58,6 +59,14 @@ bool tap_reuse_enabled() {
     return !(e && e[0] == '0');
   }();
   return env_on && g_gemm_policy == 0;
+}
+
+int wgrad_kgroups() {
+  static const int kg = [] {
+    const char* e = getenv("VQX_WGRAD_KG");  // 2 measured 0.5-1% slower end to end (profiles/r01)
+    return (e && e[0] == '2') ? 2 : 1;
+  }();
+  return kg;
 }
 
 static void launch_mode(GemmParams& P, int mode, int64_t rows, int extra_mult, bool bf16, bool gen, hipStream_t s) {
@@ -169,7 +178,7 @@ extern "C" int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream) {
   const int bkv = a->dtype == VQX_BF16 ? 64 : 32;
   const bool gen = (a->T % bkv) != 0 || (a->n_rows % bkv) != 0;
   if (!gen && wgrad_tr_ok(a->n_rows, a->T, a->c_dim, a->ntaps, a->pad, a->dtype == VQX_BF16, a->q_prologue)) {
-    P.tap_reuse = 1;
+    P.tap_reuse = wgrad_kgroups();
     P.tiles_n = a->c_dim / 64;
   }
   hipStream_t s = (hipStream_t)stream;
@@ -187,7 +196,7 @@ extern "C" int vqx_wgrad_tiles(int64_t n_rows, int32_t T, int32_t r_dim, int32_t
   const int bkv = bf16 ? 64 : 32;
   const bool gen = (T % bkv) != 0 || (n_rows % bkv) != 0;
   const int tm = (r_dim + 127) / 128;
-  if (!gen && wgrad_tr_ok(n_rows, T, c_dim, ntaps, pad, bf16, q_prologue)) *tiles = tm * (c_dim / 64);
+  if (!gen && wgrad_tr_ok(n_rows, T, c_dim, ntaps, pad, bf16, q_prologue)) *tiles = tm * (c_dim / 64) * wgrad_kgroups();
   else *tiles = tm * ((ntaps * c_dim + kBN - 1) / kBN);
   return 0;
 }

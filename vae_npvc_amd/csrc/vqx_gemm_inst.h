@@ -13,7 +13,8 @@
 namespace vqx {
 
 // vqx_gemm.hip: plain launch, or the probe's event-stamped launch
-void gemm_launch(const void* fn, int grid, hipStream_t s, const GemmParams& P, const int info[5], double flops);
+void gemm_launch(const void* fn, int grid, hipStream_t s, const GemmParams& P, const int info[5], double flops,
+                 int block = 256);
 
 // vqx_gemm.hip: tap-reuse kernel switch (env VQX_TAP_REUSE=0 turns it off, for A/B runs)
 bool tap_reuse_enabled();
@@ -27,6 +28,9 @@ inline bool tap_reuse_ok(const GemmParams& P, bool bf16, bool gen) {
 
 // wgrad_tr_kernel applies: bf16, no prologue, 3 taps / pad 1, c_dim % 64 == 0,
 // 64-frame K-tiles inside one utterance
+// K groups per tap-reuse WGRAD workgroup (default 1; env VQX_WGRAD_KG=2: two 4-wave groups)
+int wgrad_kgroups();
+
 inline bool wgrad_tr_ok(int64_t n_rows, int T, int c_dim, int ntaps, int pad, bool bf16, int pro) {
   return bf16 && pro == VQX_PRO_NONE && ntaps == 3 && pad == 1 && c_dim % 64 == 0 && T % 64 == 0 &&
          n_rows % 64 == 0 && tap_reuse_enabled();
@@ -84,8 +88,10 @@ void launch_mode_dt(const GemmParams& P, int grid, bool bf16, bool gen, hipStrea
   if constexpr (MODE == MODE_WGRAD) {
     if (P.tap_reuse) {
       const double flops = 2.0 * (double)P.n_rows * P.Mc * P.Nc;
-      const int info[5] = {VQX_BF16, MODE_WGRAD, VQX_PRO_NONE, 2, EK_NONE};  // gen = 2: tap-reuse kernel
-      gemm_launch((const void*)wgrad_tr_kernel<EK_NONE>, grid, s, P, info, flops);
+      // gen = 2: tap-reuse kernel; the prologue slot carries the K-group count
+      const int info[5] = {VQX_BF16, MODE_WGRAD, P.tap_reuse, 2, EK_NONE};
+      if (P.tap_reuse == 2) gemm_launch((const void*)wgrad_tr_kernel<EK_NONE, 2>, grid, s, P, info, flops, 512);
+      else gemm_launch((const void*)wgrad_tr_kernel<EK_NONE, 1>, grid, s, P, info, flops);
       return;
     }
     launch_pro<bf16_t, MODE, false, EK_NONE>(P, grid, s);

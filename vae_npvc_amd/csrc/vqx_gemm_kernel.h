@@ -1035,22 +1035,30 @@ __global__ __launch_bounds__(256, 2) void conv_tr_kernel(GemmParams P) {
 // shift.
 __device__ __forceinline__ int q_off128(int row, int ch) { return row * 128 + 16 * (ch ^ (((row >> 1) & 1) << 2)); }
 
-template <int EK>  // slab store only (EK_NONE); a template so every instantiation unit may include it
-__global__ __launch_bounds__(256, 2) void wgrad_tr_kernel(GemmParams P) {
+// KG = 2 splits K inside the workgroup as well: two 4-wave groups (8 waves,
+// one workgroup per CU) take alternate 64-frame K-tiles of the same output
+// tile, each through its own LDS ring, and are summed in LDS before the slab
+// store.  Same waves per CU as two 4-wave workgroups, half the slabs to write
+// and to reduce in the weight-norm backward.
+template <int EK, int KG>
+__global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void wgrad_tr_kernel(GemmParams P) {
   using T = bf16_t;
-  constexpr int ES = 2, EPC = 8, BK = 64;
+  constexpr int ES = 2, EPC = 8, BK = 64, NT = 256 * KG;
   constexpr int A_BYTES = BK * 256;              // p: 64 frames x 128 r
   constexpr int B_PIECES = 9;                    // q: 66 frames x 64 c (72-row capacity)
   constexpr int B_BYTES = B_PIECES * 1024;
   constexpr int STAGE = A_BYTES + B_BYTES;       // 25 KiB
   constexpr int NST = 2;
   constexpr int EP_LD = 64 + 4;                  // epilogue row pitch (floats)
-  constexpr int SMEM = NST * STAGE > 128 * EP_LD * 4 ? NST * STAGE : 128 * EP_LD * 4;
+  constexpr int RED_BYTES = KG > 1 ? 4 * 6 * 64 * 64 : 0;  // one group's accumulators
+  constexpr int SMEM0 = KG * NST * STAGE > 128 * EP_LD * 4 ? KG * NST * STAGE : 128 * EP_LD * 4;
+  constexpr int SMEM = SMEM0 > RED_BYTES ? SMEM0 : RED_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 1, wn = wid & 1;
+  const int grp = wid >> 2, wl = wid & 3;  // K group, wave within the group
+  const int wm = wl >> 1, wn = wl & 1;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
   const int tiles_mn = P.tiles_m * P.tiles_n;
   const int split = lin / tiles_mn;
@@ -1061,22 +1069,23 @@ __global__ __launch_bounds__(256, 2) void wgrad_tr_kernel(GemmParams P) {
   int64_t kend = kbeg + P.k_per_split;
   if (kend > P.n_rows) kend = P.n_rows;
   const int nk = kend > kbeg ? (int)((kend - kbeg) / BK) : 0;
+  const int nit = (nk + KG - 1) / KG;  // iterations per group; group g takes K-tiles g, g+KG, ...
 
-  // p pieces wid*4 .. wid*4+3 (16 per stage)
+  // p pieces wl*4 .. wl*4+3 (16 per stage)
   unsigned aoff[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int c = (wid * 4 + i) * 64 + lane;
+    const int c = (wl * 4 + i) * 64 + lane;
     const int krow = c / 16, cch = (c % 16) ^ mn_swz(krow);
     const int r = r0 + cch * EPC;
     aoff[i] = r < P.Mc ? (unsigned)(((int64_t)krow * P.lda + r) * ES) : kOOB;
   }
-  // q pieces wid, wid+4 and (wave 0) 8; stage row sr holds frame k0-1+sr
+  // q pieces wl, wl+4 and (wave 0 of the group) 8; stage row sr holds frame k0-1+sr
   unsigned boff[3];
   int bedge[3];  // 1: the k0-1 halo row, 2: the k0+64 halo row
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    const int piece = wid + 4 * i;
+    const int piece = wl + 4 * i;
     const int c = piece * 64 + lane;
     const int row = c / 8, ch = (c % 8) ^ (((row >> 1) & 1) << 2);
     const int cc = c0 + ch * EPC;
@@ -1086,19 +1095,20 @@ __global__ __launch_bounds__(256, 2) void wgrad_tr_kernel(GemmParams P) {
   }
   const __amdgpu_buffer_rsrc_t rsA = rsrc_at(P.a, 0, P.a_bytes);
   const __amdgpu_buffer_rsrc_t rsB = rsrc_at(P.b, -(int64_t)P.ldb * ES, P.b_bytes);
+  char* gsm = smem + grp * NST * STAGE;  // this group's ring
 
   auto dma_stage = [&](int buf, int kt) {
     const int64_t k0 = kbeg + (int64_t)kt * BK;
     const int t0 = (int)(k0 % P.T);
     const int edge = (t0 == 0 ? 1 : 0) | (t0 + BK == P.T ? 2 : 0);  // halo rows outside the utterance
     const unsigned ksa = (unsigned)(k0 * P.lda * ES), ksb = (unsigned)(k0 * P.ldb * ES);
-    char* st = smem + buf * STAGE;
+    char* st = gsm + buf * STAGE;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dma16(rsA, st + (wid * 4 + i) * 1024, aoff[i] + ksa);
+    for (int i = 0; i < 4; ++i) dma16(rsA, st + (wl * 4 + i) * 1024, aoff[i] + ksa);
 #pragma unroll
     for (int i = 0; i < 3; ++i)
-      if (wid + 4 * i < B_PIECES)
-        dma16(rsB, st + A_BYTES + (wid + 4 * i) * 1024, (bedge[i] & edge) ? kOOB : boff[i] + ksb);
+      if (wl + 4 * i < B_PIECES)
+        dma16(rsB, st + A_BYTES + (wl + 4 * i) * 1024, (bedge[i] & edge) ? kOOB : boff[i] + ksb);
   };
 
   f32x16_t acc[2][3];
@@ -1115,7 +1125,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_tr_kernel(GemmParams P) {
   const int ro0 = 1 - P.sign, ro2 = 1 + P.sign;  // stage-row offset of taps 0 and 2 (tap 1: 1)
 
   auto compute_stage = [&](int buf) {
-    const char* la = smem + buf * STAGE;
+    const char* la = gsm + buf * STAGE;
     const char* lb = la + A_BYTES;
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {
@@ -1151,18 +1161,50 @@ __global__ __launch_bounds__(256, 2) void wgrad_tr_kernel(GemmParams P) {
     }
   };
 
-  if (nk > 0) {
-    dma_stage(0, 0);
+  // every wave runs nit iterations and every barrier; a group's missing last
+  // K-tile (nk odd) is neither loaded nor multiplied
+  if (nit > 0) {
+    if (grp < nk) dma_stage(0, grp);
     wait_vm(0);
     __builtin_amdgcn_s_barrier();
     int buf = 0;
-    for (int kt = 0; kt < nk; ++kt) {
-      if (kt + 1 < nk) dma_stage(buf ^ 1, kt + 1);
-      compute_stage(buf);
+    for (int it = 0; it < nit; ++it) {
+      const int kt = it * KG + grp;
+      if (it + 1 < nit && kt + KG < nk) dma_stage(buf ^ 1, kt + KG);
+      if (kt < nk) compute_stage(buf);
       wait_vm(0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       buf ^= 1;
+    }
+  }
+
+  if constexpr (KG > 1) {  // group 1's accumulators -> LDS (lane-linear) -> added by group 0
+    float* red = (float*)smem;
+    __syncthreads();
+    if (grp == 1) {
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+          for (int gq = 0; gq < 4; ++gq) {
+            const f32x4_t v = {acc[mi][j][4 * gq], acc[mi][j][4 * gq + 1], acc[mi][j][4 * gq + 2], acc[mi][j][4 * gq + 3]};
+            *(f32x4_t*)(red + (((wl * 6 + mi * 3 + j) * 4 + gq) * 64 + lane) * 4) = v;
+          }
+    }
+    __syncthreads();
+    if (grp == 0) {
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+          for (int gq = 0; gq < 4; ++gq) {
+            const f32x4_t v = *(const f32x4_t*)(red + (((wl * 6 + mi * 3 + j) * 4 + gq) * 64 + lane) * 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[mi][j][4 * gq + e] += v[e];
+          }
     }
   }
 
@@ -1172,17 +1214,19 @@ __global__ __launch_bounds__(256, 2) void wgrad_tr_kernel(GemmParams P) {
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     __syncthreads();
+    if (grp == 0) {
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
+      for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        const f32x4_t v = {acc[mi][j][4 * gq], acc[mi][j][4 * gq + 1], acc[mi][j][4 * gq + 2], acc[mi][j][4 * gq + 3]};
-        *(f32x4_t*)(ep + (wm * 64 + mi * 32 + r32) * EP_LD + wn * 32 + 8 * gq + 4 * h) = v;
-      }
+        for (int gq = 0; gq < 4; ++gq) {
+          const f32x4_t v = {acc[mi][j][4 * gq], acc[mi][j][4 * gq + 1], acc[mi][j][4 * gq + 2], acc[mi][j][4 * gq + 3]};
+          *(f32x4_t*)(ep + (wm * 64 + mi * 32 + r32) * EP_LD + wn * 32 + 8 * gq + 4 * h) = v;
+        }
+    }
     __syncthreads();
 #pragma unroll
-    for (int pass = 0; pass < 4; ++pass) {
-      const int lr = pass * 32 + (tid >> 3), lc = (tid & 7) * 8;
+    for (int pass = 0; pass < 128 / (NT / 8); ++pass) {
+      const int lr = pass * (NT / 8) + (tid >> 3), lc = (tid & 7) * 8;
       const int r = r0 + lr, cc = c0 + lc;
       if (r < P.Mc && cc < P.cdim) {
         const f32x4_t lo = *(const f32x4_t*)(ep + lr * EP_LD + lc);
