@@ -40,8 +40,21 @@ __device__ __forceinline__ void st_dt(void* p, int64_t i, float v, int dt) {
   if (dt == VQX_BF16) ((bf16_t*)p)[i] = f2bf(v); else ((float*)p)[i] = v;
 }
 
-__device__ __forceinline__ float fsigmoid(float x) { return 1.f / (1.f + __expf(-x)); }
-__device__ __forceinline__ float ftanh(float x) { return 2.f / (1.f + __expf(-2.f * x)) - 1.f; }
+// GLU activations with the hardware reciprocal (v_rcp_f32, 1 ulp) instead of
+// IEEE division (a ~10-instruction scale/fixup sequence): the GroupNorm/GLU
+// kernels that call these per element are VALU-bound, not HBM-bound.
+#ifndef VQX_FAST_RCP
+#define VQX_FAST_RCP 1
+#endif
+__device__ __forceinline__ float frcp(float x) {
+#if VQX_FAST_RCP
+  return __builtin_amdgcn_rcpf(x);
+#else
+  return 1.f / x;
+#endif
+}
+__device__ __forceinline__ float fsigmoid(float x) { return frcp(1.f + __expf(-x)); }
+__device__ __forceinline__ float ftanh(float x) { return 2.f * frcp(1.f + __expf(-2.f * x)) - 1.f; }
 
 // Chan et al. parallel merge of (count, mean, M2) moments: a <- a (+) b.
 __device__ __forceinline__ void moments_merge(float& na, float& ma, float& qa, float nb, float mb, float qb) {
