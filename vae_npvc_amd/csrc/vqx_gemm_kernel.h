@@ -245,7 +245,7 @@ __host__ __device__ constexpr int ek_mask(int ek) {
 template <typename T, int EMASK>
 __device__ __forceinline__ void epilogue8(const GemmParams& P, int64_t row, int col, float* v) {
   const int epi = P.epi & EMASK;
-  const int bidx = (epi & (VQX_EPI_ROWBIAS | VQX_EPI_GNADD)) ? (int)(row / P.T) : 0;
+  const int bidx = (epi & (VQX_EPI_ROWBIAS | VQX_EPI_GNADD)) ? (int)row / P.T : 0;  // 32-bit: n_rows < 2^31 (host-checked)
   float t[8];
   if (epi & VQX_EPI_BIAS) {
     ld8<float>(P.bias, col, t);
@@ -309,7 +309,7 @@ __device__ __forceinline__ void epilogue8(const GemmParams& P, int64_t row, int 
 // the forward GroupNorm's (gn_h, gn_mr, gn_gamma, gn_beta).
 template <typename T>
 __device__ __forceinline__ void gnbwd8(const GemmParams& P, int64_t row, int col, const float* dy, float* s) {
-  const int b = (int)(row / P.T);
+  const int b = (int)row / P.T;
   float ua[8], ga[8];
   ld8<T>(P.gn_h, row * P.ldgn + col, ua);
   ld8<float>(P.gn_gamma, col, ga);
@@ -1099,7 +1099,7 @@ __global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void wgrad_tr_kernel(Gem
 
   auto dma_stage = [&](int buf, int kt) {
     const int64_t k0 = kbeg + (int64_t)kt * BK;
-    const int t0 = (int)(k0 % P.T);
+    const int t0 = (int)k0 % P.T;
     const int edge = (t0 == 0 ? 1 : 0) | (t0 + BK == P.T ? 2 : 0);  // halo rows outside the utterance
     const unsigned ksa = (unsigned)(k0 * P.lda * ES), ksb = (unsigned)(k0 * P.ldb * ES);
     char* st = gsm + buf * STAGE;

@@ -693,13 +693,13 @@ __global__ __launch_bounds__(256) void logloss_kernel(const float* __restrict__ 
   const int64_t total = (int64_t)B * T_ * C;
   float s = 0.f;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t n = e / C;
-    const int c = (int)(e - n * C);
-    const int b = (int)(n / T_), t = (int)(n - (int64_t)b * T_);
+    const int n = (int)e / C;  // 32-bit: total < 2^31 (host-checked)
+    const int c = (int)e - n * C;
+    const int b = (int)n / T_, t = (int)n - b * T_;
     const float xv = x[((int64_t)b * C + c) * T_ + t];
-    const float d = xh[n * ldxh + c] - xv;
+    const float d = xh[(int64_t)n * ldxh + c] - xv;
     s += 0.5f * (kLog2Pi + d * d);
-    if (dx) Elem<T>::st(dx, n * lddx + c, d * gscale);
+    if (dx) Elem<T>::st(dx, (int64_t)n * lddx + c, d * gscale);
   }
   s = block_sum(s, red);
   if (threadIdx.x == 0) part[blockIdx.x] = s;
@@ -719,9 +719,9 @@ __global__ void time_gather_kernel(const T* __restrict__ x, T* __restrict__ y, i
                                    const int* __restrict__ src) {
   const int64_t total = (int64_t)B * T_ * C;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t n = e / C;
-    const int c = (int)(e - n * C);
-    const int b = (int)(n / T_), t = (int)(n - (int64_t)b * T_);
+    const int n = (int)e / C;  // 32-bit: total < 2^31 (host-checked)
+    const int c = (int)e - n * C;
+    const int b = (int)n / T_, t = (int)n - b * T_;
     y[e] = x[((int64_t)b * T_ + src[t]) * C + c];
   }
 }
@@ -1280,6 +1280,7 @@ extern "C" int vqx_logloss_fwd_bwd(const float* x, const float* xhat, int32_t ld
                                    float grad_scale, void* dxhat, int32_t lddx, int32_t dtype, float* loss_out,
                                    float* partials, vqx_stream_t stream) {
   const int64_t total = (int64_t)B * C * T;
+  if (total <= 0 || total >= (1LL << 31)) { set_error("vqx_logloss_fwd_bwd: B*C*T must be in [1, 2^31)"); return -1; }
   const int grid = grid_for(total, 256, 1024);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == VQX_BF16)
@@ -1292,6 +1293,7 @@ extern "C" int vqx_logloss_fwd_bwd(const float* x, const float* xhat, int32_t ld
 
 extern "C" int vqx_time_gather(const void* x, void* y, int32_t B, int32_t T, int32_t C, const int32_t* src_t,
                                int32_t dtype, vqx_stream_t stream) {
+  if ((int64_t)B * T * C >= (1LL << 31)) { set_error("vqx_time_gather: B*T*C must be < 2^31"); return -1; }
   const int grid = grid_for((int64_t)B * T * C);
   if (dtype == VQX_BF16)
     hipLaunchKernelGGL(time_gather_kernel<bf16_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, (bf16_t*)y, B, T, C, src_t);
