@@ -23,6 +23,15 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return *reinterpret_cast<bf16_t*>(&b);
 }
 
+// two floats -> packed bf16 pair (lo in bits 0-15): one v_cvt_pk_bf16_f32
+// (round-to-nearest-even) instead of two conversions plus shift and or
+__device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2_t __attribute__((ext_vector_type(2)));
+  const f2_t v = {lo, hi};
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, b2_t));
+}
+
 template <typename T> struct Elem;
 template <> struct Elem<float> {
   __device__ static __forceinline__ float ld(const void* p, int64_t i) { return ((const float*)p)[i]; }
@@ -61,7 +70,7 @@ __device__ __forceinline__ void moments_merge(float& na, float& ma, float& qa, f
   const float n = na + nb;
   if (nb == 0.f) return;
   const float d = mb - ma;
-  const float f = nb / n;
+  const float f = nb * frcp(n);
   ma = fmaf(d, f, ma);
   qa = qa + qb + d * d * na * f;
   na = n;

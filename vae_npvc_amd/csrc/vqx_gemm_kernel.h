@@ -103,7 +103,7 @@ __device__ __forceinline__ uint4 pro_chunk(uint4 u, float s) {
       float lo = __uint_as_float(w[i] << 16), hi = __uint_as_float(w[i] & 0xffff0000u);
       lo = apply_pro(lo, PRO, s);
       hi = apply_pro(hi, PRO, s);
-      w[i] = (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+      w[i] = pack_bf16x2(lo, hi);
     }
     return make_uint4(w[0], w[1], w[2], w[3]);
   } else {
@@ -169,10 +169,10 @@ template <typename T>
 __device__ __forceinline__ void st8(void* p, int64_t i, const float* f) {
   if constexpr (sizeof(T) == 2) {
     uint4 u;
-    u.x = (unsigned)f2bf(f[0]) | ((unsigned)f2bf(f[1]) << 16);
-    u.y = (unsigned)f2bf(f[2]) | ((unsigned)f2bf(f[3]) << 16);
-    u.z = (unsigned)f2bf(f[4]) | ((unsigned)f2bf(f[5]) << 16);
-    u.w = (unsigned)f2bf(f[6]) | ((unsigned)f2bf(f[7]) << 16);
+    u.x = pack_bf16x2(f[0], f[1]);
+    u.y = pack_bf16x2(f[2], f[3]);
+    u.z = pack_bf16x2(f[4], f[5]);
+    u.w = pack_bf16x2(f[6], f[7]);
     *(uint4*)((bf16_t*)p + i) = u;
   } else {
     const f32x4_t a = {f[0], f[1], f[2], f[3]}, b = {f[4], f[5], f[6], f[7]};
@@ -200,10 +200,10 @@ __device__ __forceinline__ void st8_nt(void* p, int64_t i, const float* f) {
   }
   typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
   if constexpr (sizeof(T) == 2) {
-    const u32x4v u = {(unsigned)f2bf(f[0]) | ((unsigned)f2bf(f[1]) << 16),
-                      (unsigned)f2bf(f[2]) | ((unsigned)f2bf(f[3]) << 16),
-                      (unsigned)f2bf(f[4]) | ((unsigned)f2bf(f[5]) << 16),
-                      (unsigned)f2bf(f[6]) | ((unsigned)f2bf(f[7]) << 16)};
+    const u32x4v u = {pack_bf16x2(f[0], f[1]),
+                      pack_bf16x2(f[2], f[3]),
+                      pack_bf16x2(f[4], f[5]),
+                      pack_bf16x2(f[6], f[7])};
     __builtin_nontemporal_store(u, (u32x4v*)((bf16_t*)p + i));
   } else {
     const f32x4_t a = {f[0], f[1], f[2], f[3]}, b = {f[4], f[5], f[6], f[7]};

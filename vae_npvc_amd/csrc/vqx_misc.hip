@@ -307,7 +307,7 @@ template <> struct Vec<bf16_t> {
   __device__ static __forceinline__ void store(bf16_t* p, const float* f) {
     unsigned w[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = (unsigned)f2bf(f[2 * i]) | ((unsigned)f2bf(f[2 * i + 1]) << 16);
+    for (int i = 0; i < 4; ++i) w[i] = pack_bf16x2(f[2 * i], f[2 * i + 1]);
     *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
   }
 };

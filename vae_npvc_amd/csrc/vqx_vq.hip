@@ -181,8 +181,8 @@ __global__ __launch_bounds__(256) void vq_forward_kernel(const float* __restrict
         if (zq_dt == VQX_BF16) {
           bf16_t* o = (bf16_t*)zq_c + my_row * VQ_D + d0;
           uint2 pk;
-          pk.x = (unsigned)f2bf(e[0]) | ((unsigned)f2bf(e[1]) << 16);
-          pk.y = (unsigned)f2bf(e[2]) | ((unsigned)f2bf(e[3]) << 16);
+          pk.x = pack_bf16x2(e[0], e[1]);
+          pk.y = pack_bf16x2(e[2], e[3]);
           *(uint2*)o = pk;
         } else {
           *(f32x4_t*)((float*)zq_c + my_row * VQ_D + d0) = e;
