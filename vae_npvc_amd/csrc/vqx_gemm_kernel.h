@@ -650,6 +650,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
   }  // WGRAD: boff already carries the (ntaps-1)-row margin b_lo
   // incremental (tap, channel) position of the next K-tile to load (FWD/DGRAD fast path)
   int ld_tap = 0, ld_c0 = 0;
+  int ld_t0 = MODE == MODE_WGRAD ? (int)(kbeg % P.T) : 0;  // WGRAD: frame-in-utterance of the next K-tile
 
   // Byte offsets of K-tile kt's chunks (kOOB where the im2col / edge reads zero).
   auto tile_offsets = [&](int kt, unsigned (&oa)[PW], unsigned (&ob)[PW]) {
@@ -695,7 +696,15 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
     } else {
       const unsigned ksa = (unsigned)(k0 * P.lda * ES);
       const unsigned ksb = (unsigned)(k0 * P.ldb * ES);
-      const int t0 = (int)((int)k0 % P.T);
+      // frame-in-utterance of the K-tile, advanced per call (tiles are loaded in
+      // order; non-GEN: T % BK == 0) instead of a scalar 64-bit modulo per tile
+      int t0 = ld_t0;
+      if constexpr (!GEN) {
+        ld_t0 += BK;
+        if (ld_t0 >= P.T) ld_t0 -= P.T;
+      } else {
+        t0 = (int)((int)k0 % P.T);
+      }
 #pragma unroll
       for (int i = 0; i < PW; ++i) {
         unsigned offa = aoff[i] + ksa;
@@ -842,9 +851,13 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
       compute_tile(buf);
 #endif
       // tile kt+1 must have landed; tiles kt+2 .. min(nk, kt+NST)-1 may stay in flight
-      int ahead = (kt + NST - 1 < nk ? kt + NST : nk) - (kt + 2);
-      if (ahead < 0) ahead = 0;
-      wait_vm(NP * ahead);
+      if constexpr (NST == 2) {  // one tile in flight: it must have landed
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        int ahead = (kt + NST - 1 < nk ? kt + NST : nk) - (kt + 2);
+        if (ahead < 0) ahead = 0;
+        wait_vm(NP * ahead);
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       buf = buf + 1 == NST ? 0 : buf + 1;
@@ -1097,9 +1110,13 @@ __global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void wgrad_tr_kernel(Gem
   const __amdgpu_buffer_rsrc_t rsB = rsrc_at(P.b, -(int64_t)P.ldb * ES, P.b_bytes);
   char* gsm = smem + grp * NST * STAGE;  // this group's ring
 
-  auto dma_stage = [&](int buf, int kt) {
+  int ld_t0 = (int)((kbeg + (int64_t)grp * BK) % P.T);  // frame-in-utterance of this group's next K-tile
+  auto dma_stage = [&](int buf, int kt) {  // called for kt = grp, grp+KG, ... in order
     const int64_t k0 = kbeg + (int64_t)kt * BK;
-    const int t0 = (int)k0 % P.T;
+    const int t0 = ld_t0;
+    ld_t0 += KG * BK;  // KG * BK <= 2T (T % 64 == 0)
+    if (ld_t0 >= P.T) ld_t0 -= P.T;
+    if (KG > 1 && ld_t0 >= P.T) ld_t0 -= P.T;
     const int edge = (t0 == 0 ? 1 : 0) | (t0 + BK == P.T ? 2 : 0);  // halo rows outside the utterance
     const unsigned ksa = (unsigned)(k0 * P.lda * ES), ksb = (unsigned)(k0 * P.ldb * ES);
     char* st = gsm + buf * STAGE;
