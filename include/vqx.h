@@ -199,6 +199,14 @@ int vqx_gn_glu_fwd(const void* u, int32_t ldu, void* g, int32_t ldg, int32_t dty
                    int32_t T, int32_t C, const float* mean_rstd, const float* gamma, const float* beta,
                    vqx_stream_t stream);
 
+/* vqx_gn_glu_fwd with the GroupNorm statistics merged from the producing
+ * GEMM's GNSTATS tiles (G = 2, as vqx_gn_finalize_tiles computes them) inside
+ * the same launch; mean_rstd [B][2][2] is written for the backward.
+ * Needs T % 128 == 0 and C % 256 == 0. */
+int vqx_gn_glu_fwd_tiles(const void* u, int32_t ldu, void* g, int32_t ldg, int32_t dtype, int64_t n_rows,
+                         int32_t T, int32_t C, const float* parts, float eps, float* mean_rstd,
+                         const float* gamma, const float* beta, vqx_stream_t stream);
+
 /*
  * Backward of GroupNorm(G) optionally preceded by the gated unit:
  *   glu=1: dy is dL/dg [N][C/2], u is the GN input [N][C]: computes dL/dh
@@ -275,11 +283,12 @@ int vqx_vq_forward(const float* z, int64_t n_rows, int32_t D, const float* E, in
  *   E        = usage ? emb_sum/emb_elem : rand_rows
  *   diag[0..3] = {entropy (perplexity of bcnt), used_curr, usage, diff_emb}
  * rand_rows [K][D] are the rows z[perm[:K]] gathered by vqx_gather_rows.
- * Single workgroup, deterministic.
+ * partials: workspace of ceil(K*D/1024) floats.  Deterministic (fixed
+ * summation order).
  */
 int vqx_vq_ema_update(float* emb_sum, float* emb_elem, float* E, const float* bsum,
                       const float* bcnt, const float* rand_rows, int32_t K, int32_t D, float mu,
-                      float threshold, float* diag, vqx_stream_t stream);
+                      float threshold, float* diag, float* partials, vqx_stream_t stream);
 
 /* out[i][:] = src[rows[i]][:] for i < n_out  (f32, row length D).  rows are
  * int64 indices; negative indices write zero rows (rows owned by another
@@ -437,7 +446,7 @@ int vqx_probe_count(int64_t* n);
 int vqx_probe_read(int64_t i, int32_t* info5, double* flops, float* ms);
 
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
-#define VQX_ABI_VERSION 111
+#define VQX_ABI_VERSION 113
 int vqx_version(void);
 
 #ifdef __cplusplus

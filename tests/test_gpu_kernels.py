@@ -421,3 +421,30 @@ def test_split_epilogue_with_narrow_residual(acc, tile):
     full = x.double().cpu() @ w.double().cpu()[:, :, 0].t() + bias.double().cpu()
     assert relerr(y, full[:, :C] + res.double().cpu()) < 2e-2
     assert relerr(skip, full[:, C:] + (skip0.double().cpu() if acc else 0)) < 2e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,T", [(3, 256), (2, 128), (1, 384)])
+def test_gn_glu_fwd_tiles_equals_finalize_then_glu(dtype, B, T):
+    """vqx_gn_glu_fwd_tiles (statistics merged from the GEMM's GNSTATS tiles
+    inside the GLU launch) = vqx_gn_finalize_tiles + vqx_gn_glu_fwd, bit for
+    bit, including the mean/rstd it writes for the backward."""
+    ops = _ops()
+    torch.manual_seed(9)
+    cin, cout = 512, 1024
+    x = torch.randn(B * T, cin, device=DEV).to(dtype)
+    w = (torch.randn(cout, 3 * cin, device=DEV) / (3 * cin) ** 0.5).to(dtype)
+    bias = torch.randn(cout, device=DEV)
+    gamma, beta = torch.randn(cout, device=DEV), torch.randn(cout, device=DEV)
+    u = torch.empty(B * T, cout, device=DEV, dtype=dtype)
+    tiles = torch.empty(B * T // 128 * (cout // 128) * 4, device=DEV)
+    ops.conv_fwd(x, w, u, T=T, cin=cin, cout=cout, ntaps=3, pad=1, bias=bias, gn_stats=tiles, gn_groups=2)
+    mr1, mr2 = torch.empty(B, 2, 2, device=DEV), torch.full((B, 2, 2), float("nan"), device=DEV)
+    g1 = torch.empty(B * T, cout // 2, device=DEV, dtype=dtype)
+    g2 = torch.empty_like(g1)
+    ops.gn_finalize_tiles(tiles, B * T, T, cout, 2, mr1)
+    ops.gn_glu_fwd(u, g1, T, mr1, gamma, beta)
+    ops.gn_glu_fwd_tiles(u, g2, T, tiles, mr2, gamma, beta)
+    torch.cuda.synchronize()
+    assert torch.equal(mr1, mr2)
+    assert torch.equal(g1, g2)

@@ -546,17 +546,51 @@ __global__ __launch_bounds__(256) void gn_glu_fwd_vec_kernel(const T* __restrict
                                                              int ldg, int n_rows, int T_, int half, int cpr,
                                                              const float* __restrict__ mr,
                                                              const float* __restrict__ gamma,
-                                                             const float* __restrict__ beta) {
+                                                             const float* __restrict__ beta,
+                                                             const float* __restrict__ tiles, float eps,
+                                                             float* __restrict__ mr_out) {
   // block = 16 frames; thread = (chunk, row slot); cpr divides 256
   constexpr int V = Vec<T>::N;
   const int ch = threadIdx.x % cpr, rs = threadIdx.x / cpr, nrs = 256 / cpr;
   const int c = ch * V;
+  __shared__ float smr[4];
+  if (tiles) {
+    // statistics of this block's utterance (T % 128 == 0: the 16 frames share
+    // one) merged from the producing GEMM's GNSTATS tiles, as
+    // gn_finalize_tiles_kernel does; the utterance's first block stores them
+    const int b0 = blockIdx.x * 16 / T_, rg = T_ / 128, ntn = 2 * half / 128, tpg = ntn / 2;
+    if (threadIdx.x < 2) {
+      const int gi = threadIdx.x;
+      double n = 0.0, mean = 0.0, m2 = 0.0;
+      for (int r = 0; r < rg; ++r)
+        for (int t = 0; t < tpg; ++t) {
+          const float* o = tiles + ((int64_t)(b0 * rg + r) * ntn + gi * tpg + t) * 4;
+          const double nb = o[0];
+          if (nb == 0.0) continue;
+          const double d = (double)o[1] - mean;
+          const double nn = n + nb;
+          mean += d * nb / nn;
+          m2 += (double)o[2] + d * d * n * nb / nn;
+          n = nn;
+        }
+      const float var = n > 0.0 ? (float)(m2 / n) : 0.f;
+      smr[2 * gi] = (float)mean;
+      smr[2 * gi + 1] = 1.0f / sqrtf(var + eps);
+      if ((blockIdx.x * 16) % T_ == 0) {
+        mr_out[4 * b0 + 2 * gi] = smr[2 * gi];
+        mr_out[4 * b0 + 2 * gi + 1] = smr[2 * gi + 1];
+      }
+    }
+    __syncthreads();
+  }
   float ga[V], ba[V], gb[V], bb[V];
 #pragma unroll
   for (int i = 0; i < V; ++i) { ga[i] = gamma[c + i]; ba[i] = beta[c + i]; gb[i] = gamma[c + half + i]; bb[i] = beta[c + half + i]; }
   for (int r = blockIdx.x * 16 + rs; r < min(n_rows, blockIdx.x * 16 + 16); r += nrs) {
     const int b = r / T_;
-    const float ma = mr[4 * b + 0], ra = mr[4 * b + 1], mb = mr[4 * b + 2], rb = mr[4 * b + 3];
+    float ma, ra, mb, rb;
+    if (tiles) { ma = smr[0]; ra = smr[1]; mb = smr[2]; rb = smr[3]; }
+    else { ma = mr[4 * b + 0]; ra = mr[4 * b + 1]; mb = mr[4 * b + 2]; rb = mr[4 * b + 3]; }
     float ua[V], ub[V], o[V];
     Vec<T>::load(u + (int64_t)r * ldu + c, ua);
     Vec<T>::load(u + (int64_t)r * ldu + c + half, ub);
@@ -1171,9 +1205,29 @@ extern "C" int vqx_groupnorm_stats(const void* x, int32_t ldx, int32_t dtype, in
   return launch_status("vqx_groupnorm_stats");
 }
 
+static int gn_glu_fwd_impl(const void* u, int32_t ldu, void* g, int32_t ldg, int32_t dtype, int64_t n_rows,
+                           int32_t T, int32_t C, const float* mean_rstd, const float* gamma, const float* beta,
+                           const float* tiles, float eps, float* mr_out, vqx_stream_t stream);
+
 extern "C" int vqx_gn_glu_fwd(const void* u, int32_t ldu, void* g, int32_t ldg, int32_t dtype, int64_t n_rows,
                               int32_t T, int32_t C, const float* mean_rstd, const float* gamma, const float* beta,
                               vqx_stream_t stream) {
+  return gn_glu_fwd_impl(u, ldu, g, ldg, dtype, n_rows, T, C, mean_rstd, gamma, beta, nullptr, 0.f, nullptr, stream);
+}
+
+extern "C" int vqx_gn_glu_fwd_tiles(const void* u, int32_t ldu, void* g, int32_t ldg, int32_t dtype, int64_t n_rows,
+                                    int32_t T, int32_t C, const float* parts, float eps, float* mean_rstd,
+                                    const float* gamma, const float* beta, vqx_stream_t stream) {
+  if (!parts || !mean_rstd || T % 128 || n_rows % T || C % 256) {
+    set_error("vqx_gn_glu_fwd_tiles: needs T %% 128 == 0 and C %% 256 == 0");
+    return -1;
+  }
+  return gn_glu_fwd_impl(u, ldu, g, ldg, dtype, n_rows, T, C, nullptr, gamma, beta, parts, eps, mean_rstd, stream);
+}
+
+static int gn_glu_fwd_impl(const void* u, int32_t ldu, void* g, int32_t ldg, int32_t dtype, int64_t n_rows,
+                           int32_t T, int32_t C, const float* mean_rstd, const float* gamma, const float* beta,
+                           const float* tiles, float eps, float* mr_out, vqx_stream_t stream) {
   if (C % 2) { set_error("vqx_gn_glu_fwd: odd C"); return -1; }
   const int V = dtype == VQX_BF16 ? 8 : 4;
   if ((C / 2) % V || ldu % V || ldg % V || (((uintptr_t)u | (uintptr_t)g) & 15)) {
@@ -1185,9 +1239,9 @@ extern "C" int vqx_gn_glu_fwd(const void* u, int32_t ldu, void* g, int32_t ldg, 
   const int grid = (int)((n_rows + 15) / 16);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == VQX_BF16)
-    hipLaunchKernelGGL(gn_glu_fwd_vec_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)u, ldu, (bf16_t*)g, ldg, (int)n_rows, T, C / 2, cpr, mean_rstd, gamma, beta);
+    hipLaunchKernelGGL(gn_glu_fwd_vec_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)u, ldu, (bf16_t*)g, ldg, (int)n_rows, T, C / 2, cpr, mean_rstd, gamma, beta, tiles, eps, mr_out);
   else
-    hipLaunchKernelGGL(gn_glu_fwd_vec_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)u, ldu, (float*)g, ldg, (int)n_rows, T, C / 2, cpr, mean_rstd, gamma, beta);
+    hipLaunchKernelGGL(gn_glu_fwd_vec_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)u, ldu, (float*)g, ldg, (int)n_rows, T, C / 2, cpr, mean_rstd, gamma, beta, tiles, eps, mr_out);
   return launch_status("vqx_gn_glu_fwd");
 }
 

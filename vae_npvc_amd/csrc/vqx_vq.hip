@@ -261,16 +261,23 @@ __global__ void sum_partials_kernel(const float* __restrict__ p, int n, float sc
 }
 
 // EMA codebook update, one workgroup (layers_vq.py:203-233).
-__global__ __launch_bounds__(1024) void vq_ema_update_kernel(float* __restrict__ emb_sum, float* __restrict__ emb_elem,
-                                                             float* __restrict__ E, const float* __restrict__ bsum,
-                                                             const float* __restrict__ bcnt,
-                                                             const float* __restrict__ rand_rows, int K, int D,
-                                                             float mu, float one_minus_mu, float thr,
-                                                             float* __restrict__ diag) {
+// EMA update in two launches: the K*D elementwise update over many workgroups
+// (one exact division per element; a single workgroup took ~48 us), each
+// writing its squared-difference partial; then one workgroup for the per-code
+// terms, the emb_elem update and the diagnostics, summing the partials in a
+// fixed order (deterministic).
+constexpr int kEmaElems = 1024;  // elements per workgroup of vq_ema_elem_kernel
+
+__global__ __launch_bounds__(256) void vq_ema_elem_kernel(float* __restrict__ emb_sum,
+                                                          const float* __restrict__ emb_elem, float* __restrict__ E,
+                                                          const float* __restrict__ bsum,
+                                                          const float* __restrict__ bcnt,
+                                                          const float* __restrict__ rand_rows, int K, int D, float mu,
+                                                          float one_minus_mu, float thr, float* __restrict__ part) {
   __shared__ float red[16];
-  // elements
+  const int i0 = blockIdx.x * kEmaElems;
   float dsq = 0.f;
-  for (int i = threadIdx.x; i < K * D; i += blockDim.x) {
+  for (int i = i0 + threadIdx.x; i < min(K * D, i0 + kEmaElems); i += blockDim.x) {
     const int k = i / D;
     const float s = __fadd_rn(__fmul_rn(mu, emb_sum[i]), __fmul_rn(one_minus_mu, bsum[i]));
     const float el = __fadd_rn(__fmul_rn(mu, emb_elem[k]), __fmul_rn(one_minus_mu, bcnt[k]));
@@ -283,8 +290,19 @@ __global__ __launch_bounds__(1024) void vq_ema_update_kernel(float* __restrict__
     E[i] = newe;
   }
   dsq = block_sum(dsq, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = dsq;
+}
+
+__global__ __launch_bounds__(1024) void vq_ema_final_kernel(float* __restrict__ emb_elem,
+                                                            const float* __restrict__ bcnt, int K, int D, float mu,
+                                                            float one_minus_mu, float thr,
+                                                            const float* __restrict__ part, int nparts,
+                                                            float* __restrict__ diag) {
+  __shared__ float red[16];
+  float dsq = 0.f;
+  for (int b = threadIdx.x; b < nparts; b += blockDim.x) dsq += part[b];
+  dsq = block_sum(dsq, red);
   __syncthreads();
-  // per-code terms
   float total = 0.f;
   for (int k = threadIdx.x; k < K; k += blockDim.x) total += bcnt[k];
   total = block_sum(total, red);
@@ -351,11 +369,15 @@ extern "C" int vqx_vq_forward(const float* z, int64_t n_rows, int32_t D, const f
 
 extern "C" int vqx_vq_ema_update(float* emb_sum, float* emb_elem, float* E, const float* bsum, const float* bcnt,
                                  const float* rand_rows, int32_t K, int32_t D, float mu, float threshold, float* diag,
-                                 vqx_stream_t stream) {
-  if (K <= 0 || D <= 0) { set_error("vqx_vq_ema_update: bad K/D"); return -1; }
+                                 float* partials, vqx_stream_t stream) {
+  if (K <= 0 || D <= 0 || !partials) { set_error("vqx_vq_ema_update: bad K/D or no partials"); return -1; }
   const float omm = (float)(1.0 - (double)mu);  // (1. - mu) in double, as the reference's Python float
-  hipLaunchKernelGGL(vq_ema_update_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, emb_sum, emb_elem, E, bsum,
-                     bcnt, rand_rows, K, D, mu, omm, threshold, diag);
+  const int nb = (K * D + kEmaElems - 1) / kEmaElems;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(vq_ema_elem_kernel, dim3(nb), dim3(256), 0, s, emb_sum, emb_elem, E, bsum, bcnt, rand_rows, K,
+                     D, mu, omm, threshold, partials);
+  hipLaunchKernelGGL(vq_ema_final_kernel, dim3(1), dim3(1024), 0, s, emb_elem, bcnt, K, D, mu, omm, threshold,
+                     partials, nb, diag);
   return launch_status("vqx_vq_ema_update");
 }
 

@@ -97,6 +97,7 @@ class Workspace:
         self.bsum = self.ema[: K * D].view(K, D)
         self.bcnt = self.ema[K * D: K * D + K]
         self.rand_rows = self.ema[K * D + K:].view(K, D)
+        self.ema_part = e((K * D + 1023) // 1024, dt=F32)  # vqx_vq_ema_update workspace
         self.yemb = e(B, d["ydim"], dt=F32)
         self.condbias = e(nd, B, 2 * Cd, dt=F32)
         self.xs = [e(N, Cd) for _ in range(nd + 1)]
@@ -397,13 +398,13 @@ class VQVAEEngine:
         self.fwd(self.dec0, zq_c, w.xs[0], T, bias=self.dec0.mod.bias)
         for i in range(nd):
             ci, gn, rs = self.dec_in[i], self.dec_gn[i], self.dec_rs[i]
-            if w.fuse_gn:
+            if w.fuse_gn:  # statistics from the GEMM's epilogue tiles, finalised inside the GLU launch
                 self.fwd(ci, w.xs[i], w.u[i], T, bias=ci.mod.bias, rowbias=w.condbias[i], gn_stats=w.gst, gn_groups=2)
-                ops.gn_finalize_tiles(w.gst, w.N, T, ci.cout, 2, w.dec_mr[i])
+                ops.gn_glu_fwd_tiles(w.u[i], w.g[i], T, w.gst, w.dec_mr[i], gn.weight, gn.bias)
             else:
                 self.fwd(ci, w.xs[i], w.u[i], T, bias=ci.mod.bias, rowbias=w.condbias[i])
                 ops.groupnorm_stats(w.u[i], T, 2, w.gn_part, w.dec_mr[i])
-            ops.gn_glu_fwd(w.u[i], w.g[i], T, w.dec_mr[i], gn.weight, gn.bias)
+                ops.gn_glu_fwd(w.u[i], w.g[i], T, w.dec_mr[i], gn.weight, gn.bias)
             self.fwd(rs, w.g[i], w.xs[i + 1], T, bias=rs.mod.bias, res=w.xs[i], out2=w.skip32, split_col=Cd,
                      out2_accumulate=(i > 0))
         # final_layer = ReLU, conv, ReLU, conv on sqrt(1/(nd+1)) * sum(skips) (vqvae.py:316-318)
@@ -625,7 +626,7 @@ class VQVAEEngine:
             self._ema_work.wait()
             self._ema_work = None
         ops.vq_ema_update(q.emb_sum, q.emb_elem, q.embeddings, w.bsum, w.bcnt, w.rand_rows, q.mu, q.threshold,
-                          w.stats[4:8])
+                          w.stats[4:8], w.ema_part)
 
     # ------------------------------------------------------------ full step
     world, rank, comm = 1, 0, None

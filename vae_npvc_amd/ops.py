@@ -259,6 +259,13 @@ def gn_glu_fwd(u, g, T, mean_rstd, gamma, beta):
     return g
 
 
+def gn_glu_fwd_tiles(u, g, T, parts, mean_rstd, gamma, beta, eps=1e-5):
+    """gn_finalize_tiles(G=2) + gn_glu_fwd in one launch; writes mean_rstd."""
+    call("vqx_gn_glu_fwd_tiles", ptr(u), u.stride(0), ptr(g), g.stride(0), dt_code(u.dtype), u.shape[0], T,
+         u.shape[1], ptr(parts), eps, ptr(mean_rstd), ptr(gamma), ptr(beta), stream_ptr())
+    return g
+
+
 def gn_bwd(dy, u, du, T, G, glu, mean_rstd, gamma, beta, partials, colsum_b=None, dgamma_b=None, dbeta_b=None,
            nparts=0):
     """nparts > 0: `partials` already holds the producing GEMM's GNBWD tiles (nparts per utterance)."""
@@ -307,10 +314,14 @@ def vq_forward(z, E, idx, zq, zq_c, sqerr, partials, bsum=None, bcnt=None):
          stream_ptr())
 
 
-def vq_ema_update(emb_sum, emb_elem, E, bsum, bcnt, rand_rows, mu, threshold, diag):
+def vq_ema_update(emb_sum, emb_elem, E, bsum, bcnt, rand_rows, mu, threshold, diag, partials=None):
+    """partials: workspace of ceil(K*D/1024) floats (allocated here if None)."""
     K, D = E.shape
+    if partials is None:
+        partials = torch.empty((K * D + 1023) // 1024, device=E.device, dtype=torch.float32)
+    assert partials.numel() >= (K * D + 1023) // 1024
     call("vqx_vq_ema_update", ptr(emb_sum), ptr(emb_elem), ptr(E), ptr(bsum), ptr(bcnt), ptr(rand_rows), K, D,
-         mu, threshold, ptr(diag), stream_ptr())
+         mu, threshold, ptr(diag), ptr(partials), stream_ptr())
 
 
 def gather_rows(src, rows, out):
