@@ -243,14 +243,15 @@ class VQVAEEngine:
         # tile count comes from the library (3-tap layers use the tap-reuse
         # kernel's 128 x 192 tiles).
         N_ref, T_ref = 64 * 256, 256
-        wg_target = int(os.environ.get("VQX_WGRAD_WGS", "512"))  # A/B knob: workgroups per wgrad launch
+        wg_target = int(os.environ.get("VQX_WGRAD_WGS", "512"))  # A/B knobs: workgroups per wgrad launch
+        wg_1x1 = int(os.environ.get("VQX_WGRAD_WGS_1X1", str(wg_target)))  # ... for the 1x1 layers
         for Lr in self.convs:
             if Lr in self.dec_cond:
                 Lr.splits = 1
                 continue
             r, c = (Lr.cin, Lr.cout) if Lr.kind else (Lr.cout, Lr.cin)
             tiles = ops.wgrad_tiles(N_ref, T_ref, r, c, Lr.k, Lr.pad, self.dt)
-            Lr.splits = max(1, min(wg_target // tiles, N_ref // 256))
+            Lr.splits = max(1, min((wg_1x1 if Lr.k == 1 else wg_target) // tiles, N_ref // 256))
         # slab arena: one backward group's slabs at a time (kept L2/MALL-resident)
         groups = self._bwd_groups()
         arena = max(sum(Lr.splits * Lr.rows * Lr.cols for Lr in grp) for grp in groups)
