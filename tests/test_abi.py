@@ -99,3 +99,24 @@ def test_missing_library_fails_loudly(tmp_path, monkeypatch):
     monkeypatch.setattr(L, "_lib", None)
     with pytest.raises(L.VqxError):
         L.load(tmp_path / "nope.so")
+
+
+def test_wgrad_tiles_reports_the_kernel_the_library_picks():
+    """vqx_wgrad_tiles is host-only (no GPU): 3-tap pad-1 bf16 layers with
+    T % 64 == 0 and c_dim % 64 == 0 get the tap-reuse tiling (128 r x 3 taps x
+    64 c), everything else 128 x 128 tiles of the (tap, channel) columns."""
+    import os
+    from vae_npvc_amd import _lib as L
+    from vae_npvc_amd import ops
+    if os.environ.get("VQX_TAP_REUSE") == "0":
+        pytest.skip("tap reuse disabled in this environment")
+    kg = 2 if os.environ.get("VQX_WGRAD_KG") == "2" else 1
+    N, T = 64 * 256, 256
+    assert ops.wgrad_tiles(N, T, 512, 512, 3, 1, L.VQX_BF16) == 4 * 8 * kg
+    assert ops.wgrad_tiles(N, T, 512, 1024, 3, 1, L.VQX_BF16) == 4 * 16 * kg
+    assert ops.wgrad_tiles(N, T, 512, 512, 1, 0, L.VQX_BF16) == 4 * 4      # 1x1: im2col tiles
+    assert ops.wgrad_tiles(N, T, 512, 512, 3, 1, L.VQX_F32) == 4 * 12      # fp32 parity mode
+    assert ops.wgrad_tiles(N, 100, 512, 512, 3, 1, L.VQX_BF16) == 4 * 12   # T % 64 != 0
+    assert ops.wgrad_tiles(N, T, 512, 80, 3, 1, L.VQX_BF16) == 4 * 2       # c_dim % 64 != 0: ceil(240/128)
+    with pytest.raises(L.VqxError):
+        ops.wgrad_tiles(N, T, 0, 512, 3, 1, L.VQX_BF16)
