@@ -61,6 +61,14 @@ bool tap_reuse_enabled() {
   return env_on && g_gemm_policy == 0;
 }
 
+int tr_stage_channels() {
+  static const int bkc = [] {
+    const char* e = getenv("VQX_TR_BKC");
+    return (e && e[0] == '1' && e[1] == '6') ? 16 : 32;
+  }();
+  return bkc;
+}
+
 int wgrad_kgroups() {
   static const int kg = [] {
     const char* e = getenv("VQX_WGRAD_KG");  // 2 measured 0.5-1% slower end to end (profiles/r01)

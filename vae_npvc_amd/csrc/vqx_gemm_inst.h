@@ -36,11 +36,17 @@ inline bool wgrad_tr_ok(int64_t n_rows, int T, int c_dim, int ntaps, int pad, bo
          n_rows % 64 == 0 && tap_reuse_enabled();
 }
 
+// channels per tap-reuse stage: 32 (2-deep ring, default) or 16 (4-deep ring; env VQX_TR_BKC=16)
+int tr_stage_channels();
+
 template <int MODE, int EK>
 void launch_tr(const GemmParams& P, int grid, hipStream_t s) {
   const double flops = 2.0 * (double)P.n_rows * P.Nc * P.K;
-  const int info[5] = {VQX_BF16, MODE, VQX_PRO_NONE, 2, EK};  // gen = 2: tap-reuse kernel
-  gemm_launch((const void*)conv_tr_kernel<MODE, EK>, grid, s, P, info, flops);
+  const int bkc = tr_stage_channels();
+  // gen = 2: tap-reuse kernel; the prologue slot carries the stage depth in channels
+  const int info[5] = {VQX_BF16, MODE, bkc, 2, EK};
+  if (bkc == 16) gemm_launch((const void*)conv_tr_kernel<MODE, EK, 16>, grid, s, P, info, flops);
+  else gemm_launch((const void*)conv_tr_kernel<MODE, EK, 32>, grid, s, P, info, flops);
 }
 
 // smallest epilogue kind whose feature mask covers `epi`

@@ -372,7 +372,7 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, unsig
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (VQX_LDS(void)*)lds, 16, (int)off, 0, 0, 0);
 }
 
-// vmcnt immediate from a small runtime count (0..8, 12, 16; anything else waits for all)
+// vmcnt immediate from a small runtime count (0..8, 10, 12, 16; anything else waits for all)
 __device__ __forceinline__ void wait_vm(int n) {
   switch (n) {
     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
@@ -384,6 +384,7 @@ __device__ __forceinline__ void wait_vm(int n) {
     case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
     case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
     case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
     case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
     case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
@@ -901,18 +902,32 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
 // last row), which is exactly the im2col zero padding.  The row-shifted
 // fragment reads stay conflict-free because the K-major swizzle depends on
 // row % 16 only and a fragment's 16-lane groups cover 16 distinct residues.
-template <int MODE, int EK>
+// KSWZ for 32-B K-major rows (BKC = 16): rows r and r+8 share banks, so the
+// 16-B half is flipped on bit 3 of the row; any 16 consecutive rows are then
+// conflict-free for ds_read_b128, whatever the tap shift.
+template <int KCH_>
+__device__ __forceinline__ int tr_kswz(int row) {
+  if constexpr (KCH_ == 2) return (row >> 3) & 1;
+  else return kswz<KCH_>(row);
+}
+template <int KCH_>
+__device__ __forceinline__ int tr_kmaj_off(int row, int ch) { return row * (16 * KCH_) + 16 * (ch ^ tr_kswz<KCH_>(row)); }
+
+// BKC = channels per stage: 32 (2-deep ring, 33 KiB stages) or 16 (4-deep
+// ring of 17 KiB stages: the same LDS, twice the prefetch distance)
+template <int MODE, int EK, int BKC>
 __global__ __launch_bounds__(256, 2) void conv_tr_kernel(GemmParams P) {
   using T = bf16_t;
-  constexpr int ES = 2, EPC = 8, BKC = 32, KCH = 4;  // 32 channels per stage: 64-B K-major rows
-  constexpr int A_PIECES = 9;                          // 130 rows x 64 B, rounded up to 1-KiB pieces
+  constexpr int ES = 2, EPC = 8, KCH = BKC * ES / 16;  // 16-B chunks per K-major row
+  constexpr int NST = BKC == 32 ? 2 : 4;
+  constexpr int A_PIECES = (130 * BKC * ES + 1023) / 1024;  // 130 rows, rounded up to 1-KiB pieces
   constexpr int A_BYTES = A_PIECES * 1024;
-  constexpr int TAP_BYTES = 128 * BKC * ES;            // one tap's weight slice: 8 KiB
-  constexpr int STAGE = A_BYTES + 3 * TAP_BYTES;       // 33 KiB
-  constexpr int NST = 2;
-  constexpr int PWB = 3 * TAP_BYTES / 1024 / 4;        // weight pieces per wave per stage (6)
-  static_assert(NST * STAGE >= 45056, "epilogue staging needs 44 KiB of LDS");
-  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE];
+  constexpr int TAP_BYTES = 128 * BKC * ES;            // one tap's weight slice
+  constexpr int STAGE = A_BYTES + 3 * TAP_BYTES;
+  constexpr int PWB = 3 * TAP_BYTES / 1024 / 4;        // weight pieces per wave per stage
+  constexpr int TAP_PIECES = TAP_BYTES / 1024;
+  constexpr int SMEM = NST * STAGE > 45056 ? NST * STAGE : 45056;  // the epilogue needs 44 KiB
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -922,27 +937,29 @@ __global__ __launch_bounds__(256, 2) void conv_tr_kernel(GemmParams P) {
   const int m0 = tm * 128, n0 = tn * kBN;
   const int nk = P.kcin / BKC;
 
-  // activation pieces of this wave: wid, wid+4 and (wave 0) 8; stage row sr holds frame m0-1+sr
+  // activation pieces of this wave: wid, wid+4, wid+8; stage row sr holds frame m0-1+sr
   unsigned aoff[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const int piece = wid + 4 * i;
     const int c = piece * 64 + lane;
-    const int row = c / KCH, kch = (c % KCH) ^ kswz<KCH>(row);
+    const int row = c / KCH, kch = (c % KCH) ^ tr_kswz<KCH>(row);
     bool ok = piece < A_PIECES && row < 130;
     if (row == 0 && m0 % P.T == 0) ok = false;
     if (row == 129 && (m0 + 128) % P.T == 0) ok = false;
     // the descriptor base sits one activation row before P.a, so frame m0-1+row is at (m0+row) rows
     aoff[i] = ok ? (unsigned)((((int64_t)m0 + row) * P.lda + kch * EPC) * ES) : kOOB;
   }
-  // weight pieces wid*6 .. wid*6+5 of the stage: piece pb is tap pb/8, 1-KiB slice pb%8 of it
+  const int npa = (wid < A_PIECES ? 1 : 0) + (wid + 4 < A_PIECES ? 1 : 0) + (wid + 8 < A_PIECES ? 1 : 0);
+  const int npw = npa + PWB;  // DMA instructions of this wave per stage
+  // weight pieces wid*PWB .. : piece pb is tap pb / TAP_PIECES, 1-KiB slice pb % TAP_PIECES of it
   unsigned boff[PWB];
 #pragma unroll
   for (int i = 0; i < PWB; ++i) {
     const int pb = wid * PWB + i;
-    const int tap = pb >> 3, c = (pb & 7) * 64 + lane;
-    if constexpr (MODE == MODE_FWD) {  // We[co][tap*kcin + ci], K-major rows of 32 channels
-      const int row = c / KCH, kch = (c % KCH) ^ kswz<KCH>(row);
+    const int tap = pb / TAP_PIECES, c = (pb % TAP_PIECES) * 64 + lane;
+    if constexpr (MODE == MODE_FWD) {  // We[co][tap*kcin + ci], K-major rows of BKC channels
+      const int row = c / KCH, kch = (c % KCH) ^ tr_kswz<KCH>(row);
       const int co = n0 + row;
       boff[i] = co < P.Nc ? (unsigned)(((int64_t)co * P.K + tap * P.kcin + kch * EPC) * ES) : kOOB;
     } else {  // forward weight We[co][j][ci] read as rows co of tap j = 2 - tap (taps flipped)
@@ -983,14 +1000,15 @@ __global__ __launch_bounds__(256, 2) void conv_tr_kernel(GemmParams P) {
 #pragma unroll
     for (int tap = 0; tap < 3; ++tap) {
       const char* lb = la + A_BYTES + tap * TAP_BYTES;
-      bf16x8_t af[2][2], bfr[2][2];
+      constexpr int KS = BKC / 16;
+      bf16x8_t af[KS][2], bfr[KS][2];
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
+      for (int s = 0; s < KS; ++s)
 #pragma unroll
         for (int x = 0; x < 2; ++x) {
-          af[s][x] = *(const bf16x8_t*)(la + kmaj_off<KCH>(wm * 64 + x * 32 + r32 + tap, 2 * s + h));
+          af[s][x] = *(const bf16x8_t*)(la + tr_kmaj_off<KCH>(wm * 64 + x * 32 + r32 + tap, 2 * s + h));
           if constexpr (MODE == MODE_FWD) {
-            bfr[s][x] = *(const bf16x8_t*)(lb + kmaj_off<KCH>(wn * 64 + x * 32 + r32, 2 * s + h));
+            bfr[s][x] = *(const bf16x8_t*)(lb + tr_kmaj_off<KCH>(wn * 64 + x * 32 + r32, 2 * s + h));
           } else {
             const int kb = 16 * s + (g >> 1) * 8;
             const int ch = ((wn * 64 + x * 32 + (g & 1) * 16) >> 3) + (p >> 1);
@@ -1003,7 +1021,7 @@ __global__ __launch_bounds__(256, 2) void conv_tr_kernel(GemmParams P) {
           }
         }
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
+      for (int s = 0; s < KS; ++s)
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -1013,17 +1031,28 @@ __global__ __launch_bounds__(256, 2) void conv_tr_kernel(GemmParams P) {
   };
 
   if (nk > 0) {
-    dma_stage(0, 0);
-    wait_vm(0);
+    // NST-1 stages in flight ahead of the one being multiplied
+    const int pre = nk < NST - 1 ? nk : NST - 1;
+#pragma unroll
+    for (int t = 0; t < NST - 1; ++t)
+      if (t < pre) dma_stage(t, t);
+    if constexpr (NST == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else wait_vm(npw * (pre - 1));
     __builtin_amdgcn_s_barrier();
     int buf = 0;
     for (int kt = 0; kt < nk; ++kt) {
-      if (kt + 1 < nk) dma_stage(buf ^ 1, kt + 1);
+      if (kt + NST - 1 < nk) dma_stage(buf == 0 ? NST - 1 : buf - 1, kt + NST - 1);
       compute_stage(buf);
-      wait_vm(0);
+      if constexpr (NST == 2) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {  // stage kt+1 must have landed; later ones may stay in flight
+        int ahead = (kt + NST - 1 < nk ? kt + NST : nk) - (kt + 2);
+        if (ahead < 0) ahead = 0;
+        wait_vm(npw * ahead);
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      buf ^= 1;
+      buf = buf + 1 == NST ? 0 : buf + 1;
     }
   }
   tile_epilogue<T, MODE, EK>(P, acc, smem, m0, n0, tn, 0);

@@ -117,7 +117,7 @@ class LaunchProbe:
             if gen == 2 and mode == 2:  # tap-reuse weight gradient (vqx_gemm_kernel.h wgrad_tr_kernel)
                 sym = f"vqx::wgrad_tr_kernel<{ek}, {pro}>"  # pro slot = K groups
             elif gen == 2:  # tap-reuse kernel (3-tap FWD/DGRAD, vqx_gemm_kernel.h conv_tr_kernel)
-                sym = f"vqx::conv_tr_kernel<{mode}, {ek}>"
+                sym = f"vqx::conv_tr_kernel<{mode}, {ek}, {pro}>"  # pro slot = channels per stage
             else:
                 sym = f"vqx::conv_gemm_kernel<{self._DT[dt]}, {mode}, {pro}, {'true' if gen else 'false'}, {bk}, 2, {ek}>"
             out.append((sym, fl.value, ms.value * 1e-3, self.shapes[i] if i < len(self.shapes) else ""))
