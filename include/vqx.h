@@ -110,6 +110,12 @@ typedef struct vqx_conv_args {
   float* colsum_part;        /* COLSUM destination [ceil(N/128)][cout]         */
   float* stat_part;          /* GNSTATS / GNBWD destination [N/128][ceil(cout/128)][4] */
   int32_t gn_groups, gn_glu;
+  /* GNADD with gn_stat_tiles != NULL: the GroupNorm statistics (G = 1) are
+   * merged from the producing GEMM's GNSTATS tiles inside this launch (as
+   * vqx_gn_finalize_tiles computes them, eps gn_eps) and written to
+   * gn_mean_rstd [B][2]; needs T % 128 == 0 and cout % 128 == 0. */
+  const float* gn_stat_tiles;
+  float gn_eps;
 } vqx_conv_args;
 
 int vqx_conv1d_fwd(const vqx_conv_args* a, vqx_stream_t stream);
@@ -446,7 +452,7 @@ int vqx_probe_count(int64_t* n);
 int vqx_probe_read(int64_t i, int32_t* info5, double* flops, float* ms);
 
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
-#define VQX_ABI_VERSION 113
+#define VQX_ABI_VERSION 114
 int vqx_version(void);
 
 #ifdef __cplusplus

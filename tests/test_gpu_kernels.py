@@ -448,3 +448,38 @@ def test_gn_glu_fwd_tiles_equals_finalize_then_glu(dtype, B, T):
     torch.cuda.synchronize()
     assert torch.equal(mr1, mr2)
     assert torch.equal(g1, g2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,T", [(3, 256), (2, 128), (1, 384)])
+def test_gnadd_with_in_launch_statistics(dtype, B, T, tile):
+    """Encoder residual block (layers.py:139-178): the 1x1 skip GEMM's GNADD
+    epilogue with the GroupNorm statistics merged from the k3 GEMM's GNSTATS
+    tiles inside its own launch = vqx_gn_finalize_tiles + GNADD, bit for bit,
+    including the mean/rstd it stores for the backward."""
+    ops = _ops()
+    from vae_npvc_amd import _lib as L
+    torch.manual_seed(13)
+    C = 512
+    a = torch.randn(B * T, C, device=DEV).to(dtype)
+    c = torch.randn(B * T, C, device=DEV).to(dtype)
+    w3 = (torch.randn(C, 3 * C, device=DEV) / (3 * C) ** 0.5).to(dtype)
+    w1 = (torch.randn(C, C, device=DEV) / C ** 0.5).to(dtype)
+    b3, b1 = torch.randn(C, device=DEV), torch.randn(C, device=DEV)
+    gamma, beta = torch.randn(C, device=DEV), torch.randn(C, device=DEV)
+    h = torch.empty(B * T, C, device=DEV, dtype=dtype)
+    tiles = torch.empty(B * T // 128 * (C // 128) * 4, device=DEV)
+    ops.conv_fwd(a, w3, h, T=T, cin=C, cout=C, ntaps=3, pad=1, bias=b3, gn_stats=tiles, gn_groups=1)
+    outs = []
+    for fused in (False, True):
+        mr = torch.full((B, 1, 2), float("nan"), device=DEV)
+        y, y2 = torch.empty(B * T, C, device=DEV, dtype=dtype), torch.empty(B * T, C, device=DEV, dtype=dtype)
+        kw = dict(gn_tiles=tiles) if fused else {}
+        if not fused:
+            ops.gn_finalize_tiles(tiles, B * T, T, C, 1, mr)
+        ops.conv_fwd(c, w1, y, T=T, cin=C, cout=C, ntaps=1, pad=0, bias=b1, gn_h=h, gn_mr=mr, gn_gamma=gamma,
+                     gn_beta=beta, act=L.PRO_LRELU, y2=y2, **kw)
+        torch.cuda.synchronize()
+        outs.append((mr, y, y2))
+    for u, v in zip(*outs):
+        assert torch.equal(u, v)

@@ -15,7 +15,7 @@ from pathlib import Path
 import torch  # noqa: F401  (loads the HIP runtime first; see module docstring)
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libvqx.so"
-ABI_VERSION = 113  # include/vqx.h VQX_ABI_VERSION
+ABI_VERSION = 114  # include/vqx.h VQX_ABI_VERSION
 
 VQX_F32, VQX_BF16 = 0, 1
 PRO_NONE, PRO_LRELU, PRO_RELU, PRO_SCALE_RELU = 0, 1, 2, 3
@@ -39,6 +39,7 @@ class ConvArgs(ctypes.Structure):
         ("pro_scale", c_float), ("mask_slope", c_float), ("mask_scale", c_float),
         ("y2", c_void_p), ("ldy2", c_int32), ("epi_act", c_int32), ("colsum_part", c_void_p),
         ("stat_part", c_void_p), ("gn_groups", c_int32), ("gn_glu", c_int32),
+        ("gn_stat_tiles", c_void_p), ("gn_eps", c_float),
     ]
 
 

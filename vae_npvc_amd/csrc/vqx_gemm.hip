@@ -141,6 +141,12 @@ static int conv_common(const vqx_conv_args* a, int mode, hipStream_t s) {
   P.y2 = a->y2; P.ldy2 = a->ldy2; P.epi_act = a->epi_act;
   P.colsum_part = a->colsum_part;
   P.stat_part = a->stat_part; P.gn_groups = a->gn_groups; P.gn_glu = a->gn_glu;
+  P.gn_tiles = a->gn_stat_tiles; P.gn_eps = a->gn_eps;
+  if (P.gn_tiles && (mode != MODE_FWD || !(epi & VQX_EPI_GNADD) || a->T % 128 || a->cout % 128 ||
+                     a->gn_groups != 1 || !a->gn_mean_rstd)) {
+    set_error("vqx_conv: gn_stat_tiles needs FWD with GNADD, G = 1, T %% 128 == 0, cout %% 128 == 0 and gn_mean_rstd");
+    return -1;
+  }
   if (P.a_bytes > 0x7fffffffLL || P.b_bytes > 0x7fffffffLL) { set_error("vqx_conv: operand larger than 2 GiB"); return -1; }
   const bool gen = (a->cin % (a->dtype == VQX_BF16 ? 64 : 32)) != 0;
   launch_mode(P, mode, a->n_rows, 1, a->dtype == VQX_BF16, gen, s);

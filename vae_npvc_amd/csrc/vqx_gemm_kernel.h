@@ -79,6 +79,8 @@ struct GemmParams {
   float* stat_part;  // GNSTATS / GNBWD per-(128-row group, column tile) partials
   int gn_groups, gn_glu;
   int tap_reuse;   // WGRAD: 1 = wgrad_tr_kernel tiling (tiles_n counts 64-channel blocks of c)
+  const float* gn_tiles;  // GNADD: merge mean/rstd from these GNSTATS tiles (G = 1) and write gn_mr
+  float gn_eps;
 };
 
 template <typename T> struct Cfg;
@@ -243,7 +245,7 @@ __host__ __device__ constexpr int ek_mask(int ek) {
 // order bias, row bias, activation-derivative mask, split to out2 (returns),
 // residual, GroupNorm-apply add, activation, store.
 template <typename T, int EMASK>
-__device__ __forceinline__ void epilogue8(const GemmParams& P, int64_t row, int col, float* v) {
+__device__ __forceinline__ void epilogue8(const GemmParams& P, int64_t row, int col, float* v, const float* gmr) {
   const int epi = P.epi & EMASK;
   const int bidx = (epi & (VQX_EPI_ROWBIAS | VQX_EPI_GNADD)) ? (int)row / P.T : 0;  // 32-bit: n_rows < 2^31 (host-checked)
   float t[8];
@@ -284,7 +286,7 @@ __device__ __forceinline__ void epilogue8(const GemmParams& P, int64_t row, int 
     ld8<T>(P.gn_h, row * P.ldgn + col, t);
     ld8<float>(P.gn_gamma, col, ga);
     ld8<float>(P.gn_beta, col, be);
-    const float mean = P.gn_mr[2 * bidx], rstd = P.gn_mr[2 * bidx + 1];
+    const float mean = gmr[2 * bidx], rstd = gmr[2 * bidx + 1];  // gmr: P.gn_mr or the in-launch merge
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] += (t[e] - mean) * rstd * ga[e] + be[e];
   }
@@ -400,7 +402,7 @@ __device__ __forceinline__ void wait_vm(int n) {
 // 44 KiB of `smem`; the caller's staging buffers must be free.
 template <typename T, int MODE, int EK>
 __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&acc)[2][2], char* smem, int m0, int n0,
-                                              int tn, int split) {
+                                              int tn, int split, const float* gmr) {
   constexpr int EMASK = ek_mask(EK);
   constexpr int SUB = 1;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -446,7 +448,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
         }
       } else {
         if (row < P.n_rows && col < P.Nc) {
-          epilogue8<T, EMASK>(P, row, col, v);
+          epilogue8<T, EMASK>(P, row, col, v, gmr);
 #pragma unroll
           for (int e = 0; e < 8; ++e) cs[e] += v[e];
           if (P.epi & EMASK & VQX_EPI_GNSTATS) {  // two-pass moments of the 8 values, merged
@@ -566,6 +568,42 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
   const int tmn = lin - split * tiles_mn;
   const int tm = tmn / P.tiles_n, tn = tmn - tm * P.tiles_n;
   const int m0 = tm * BM, n0 = tn * kBN;
+
+  // GNADD with in-launch statistics (P.gn_tiles, T % 128 == 0: the tile is one
+  // utterance b0): lane 0 of wave 0 merges the producing GEMM's tiles for b0
+  // while the first K-tiles load (published by the main loop's barriers); the
+  // first column tile of the utterance's first row tile stores them for the
+  // backward.  gmr[2*bidx] then addresses gmr_s for bidx == b0.
+  __shared__ float gmr_s[2];
+  const float* gmr = P.gn_mr;
+  if constexpr ((ek_mask(EK) & VQX_EPI_GNADD) != 0 && MODE == MODE_FWD) {
+    if (P.gn_tiles != nullptr && (P.epi & VQX_EPI_GNADD)) {
+      const int b0 = m0 / P.T;
+      if (tid == 0) {
+        const int rg = P.T / 128, ntn = P.Nc / 128;
+        double n = 0.0, mean = 0.0, m2 = 0.0;
+        for (int r = 0; r < rg; ++r)
+          for (int t = 0; t < ntn; ++t) {
+            const float* o = P.gn_tiles + ((int64_t)(b0 * rg + r) * ntn + t) * 4;
+            const double nb = o[0];
+            if (nb == 0.0) continue;
+            const double d = (double)o[1] - mean;
+            const double nn = n + nb;
+            mean += d * nb / nn;
+            m2 += (double)o[2] + d * d * n * nb / nn;
+            n = nn;
+          }
+        const float var = n > 0.0 ? (float)(m2 / n) : 0.f;
+        gmr_s[0] = (float)mean;
+        gmr_s[1] = 1.0f / sqrtf(var + P.gn_eps);
+        if (tn == 0 && m0 % P.T == 0) {
+          ((float*)P.gn_mr)[2 * b0] = gmr_s[0];
+          ((float*)P.gn_mr)[2 * b0 + 1] = gmr_s[1];
+        }
+      }
+      gmr = gmr_s - 2 * b0;
+    }
+  }
 
   int64_t kbeg = 0, kend;
   if constexpr (MODE == MODE_WGRAD) {
@@ -878,7 +916,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
   }
   return;
 #endif
-  tile_epilogue<T, MODE, EK>(P, acc, smem, m0, n0, tn, split);
+  tile_epilogue<T, MODE, EK>(P, acc, smem, m0, n0, tn, split, gmr);
 }
 
 
@@ -1055,7 +1093,7 @@ __global__ __launch_bounds__(256, 2) void conv_tr_kernel(GemmParams P) {
       buf = buf + 1 == NST ? 0 : buf + 1;
     }
   }
-  tile_epilogue<T, MODE, EK>(P, acc, smem, m0, n0, tn, 0);
+  tile_epilogue<T, MODE, EK>(P, acc, smem, m0, n0, tn, 0, P.gn_mr);
 }
 
 // ---------------------------------------------------------------------------

@@ -172,6 +172,7 @@ class VQVAEEngine:
         self._build_layers()
         self._ws = {}
         self.opt_ready = False
+        self._enc_gn_separate = os.environ.get("VQX_ENC_GN_FINALIZE") == "1"
 
     # ------------------------------------------------------------ parameters
     def _flatten(self):
@@ -384,14 +385,19 @@ class VQVAEEngine:
         self.fwd(self.enc0, w.x, w.c[0], T, bias=self.enc0.mod.bias, act=L.PRO_LRELU, y2=w.a[0])
         for i in range(self.dims["ns"]):
             k3, sk, gn = self.enc_k3[i], self.enc_sk[i], self.enc_gn[i]
-            if w.fuse_gn:  # statistics of h_i from the k3 GEMM's epilogue tiles
+            if w.fuse_gn:  # statistics of h_i from the k3 GEMM's epilogue tiles, merged inside the skip GEMM
                 self.fwd(k3, w.a[i], w.h[i], T, bias=k3.mod.bias, gn_stats=w.gst, gn_groups=1)
-                ops.gn_finalize_tiles(w.gst, w.N, T, k3.cout, 1, w.enc_mr[i])
+                if self._enc_gn_separate:  # A/B: the separate finalize launch
+                    ops.gn_finalize_tiles(w.gst, w.N, T, k3.cout, 1, w.enc_mr[i])
+                    gkw = {}
+                else:
+                    gkw = dict(gn_tiles=w.gst)
             else:
                 self.fwd(k3, w.a[i], w.h[i], T, bias=k3.mod.bias)
                 ops.groupnorm_stats(w.h[i], T, 1, w.gn_part, w.enc_mr[i])
+                gkw = {}
             self.fwd(sk, w.c[i], w.c[i + 1], T, bias=sk.mod.bias, gn_h=w.h[i], gn_mr=w.enc_mr[i],
-                     gn_gamma=gn.weight, gn_beta=gn.bias, act=L.PRO_LRELU, y2=w.a[i + 1])
+                     gn_gamma=gn.weight, gn_beta=gn.bias, act=L.PRO_LRELU, y2=w.a[i + 1], **gkw)
         self.fwd(self.enc_out, w.a[-1], w.z, T, bias=self.enc_out.mod.bias, out_f32=True)
 
     def decoder_fwd(self, w, zq_c):

@@ -32,7 +32,8 @@ def _check_cuda(*ts):
 def conv_args(x, w, y, *, T, cin, cout, ntaps, pad, prologue=L.PRO_NONE, pro_scale=1.0, bias=None,
               rowbias=None, res=None, mask=None, mask_slope=0.0, mask_scale=1.0, gn_h=None, gn_mr=None,
               gn_gamma=None, gn_beta=None, out2=None, split_col=0, out2_accumulate=False, out_f32=False,
-              act=None, y2=None, colsum=None, gn_stats=None, gn_bwd=None, gn_groups=1, gn_glu=False):
+              act=None, y2=None, colsum=None, gn_stats=None, gn_bwd=None, gn_groups=1, gn_glu=False,
+              gn_tiles=None, gn_eps=1e-5):
     epi = 0
     if bias is not None:
         epi |= L.EPI_BIAS
@@ -75,6 +76,7 @@ def conv_args(x, w, y, *, T, cin, cout, ntaps, pad, prologue=L.PRO_NONE, pro_sca
     a.y2, a.ldy2 = ptr(y2), (y2.stride(0) if y2 is not None else 0)
     a.epi_act = act if act is not None else 0
     a.colsum_part = ptr(colsum)
+    a.gn_stat_tiles, a.gn_eps = ptr(gn_tiles), gn_eps
     a.stat_part = ptr(gn_stats if gn_stats is not None else gn_bwd)
     a.gn_groups, a.gn_glu = gn_groups, int(gn_glu)
     return a
