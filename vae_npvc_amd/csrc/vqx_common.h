@@ -55,22 +55,25 @@ __device__ __forceinline__ void st_dt(void* p, int64_t i, float v, int dt) {
 #ifndef VQX_FAST_RCP
 #define VQX_FAST_RCP 1
 #endif
+// FAST = false keeps the IEEE division: the fp32 compute mode is the parity
+// mode (smoke() and the golden-step tests compare it with the fp32 oracle),
+// so only the bf16 instantiations take the hardware reciprocal.
+template <bool FAST = true>
 __device__ __forceinline__ float frcp(float x) {
-#if VQX_FAST_RCP
-  return __builtin_amdgcn_rcpf(x);
-#else
-  return 1.f / x;
-#endif
+  if constexpr (FAST && VQX_FAST_RCP) return __builtin_amdgcn_rcpf(x);
+  else return 1.f / x;
 }
-__device__ __forceinline__ float fsigmoid(float x) { return frcp(1.f + __expf(-x)); }
-__device__ __forceinline__ float ftanh(float x) { return 2.f * frcp(1.f + __expf(-2.f * x)) - 1.f; }
+template <bool FAST = true>
+__device__ __forceinline__ float fsigmoid(float x) { return frcp<FAST>(1.f + __expf(-x)); }
+template <bool FAST = true>
+__device__ __forceinline__ float ftanh(float x) { return 2.f * frcp<FAST>(1.f + __expf(-2.f * x)) - 1.f; }
 
 // Chan et al. parallel merge of (count, mean, M2) moments: a <- a (+) b.
 __device__ __forceinline__ void moments_merge(float& na, float& ma, float& qa, float nb, float mb, float qb) {
   const float n = na + nb;
   if (nb == 0.f) return;
   const float d = mb - ma;
-  const float f = nb * frcp(n);
+  const float f = nb / n;  // exact: GroupNorm statistics feed the parity checks
   ma = fmaf(d, f, ma);
   qa = qa + qb + d * d * na * f;
   na = n;

@@ -336,8 +336,8 @@ __device__ __forceinline__ void gnbwd8(const GemmParams& P, int64_t row, int col
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const float xa = (ua[e] - ma) * ra, xb = (ub[e] - mb) * rb;
-    const float ta = ftanh(xa * ga[e] + ba[e]);
-    const float sb = fsigmoid(xb * gb[e] + bb[e]);
+    const float ta = ftanh<sizeof(T) == 2>(xa * ga[e] + ba[e]);
+    const float sb = fsigmoid<sizeof(T) == 2>(xb * gb[e] + bb[e]);
     const float dga = ga[e] * (dy[e] * sb * (1.f - ta * ta));
     const float dgb = gb[e] * (dy[e] * ta * (sb * (1.f - sb)));
     s[0] += dga;

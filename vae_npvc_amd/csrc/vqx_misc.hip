@@ -388,8 +388,8 @@ __device__ __forceinline__ void gn_dh_chunk(const T* dy, int lddy, const T* u, i
     const float xhb = (ub[i] - mr4[2]) * mr4[3];
     const float ha = xha * gamma[c + i] + beta[c + i];
     const float hb = xhb * gamma[c + half + i] + beta[c + half + i];
-    const float ta = ftanh(ha);
-    const float sb = fsigmoid(hb);
+    const float ta = ftanh<sizeof(T) == 2>(ha);
+    const float sb = fsigmoid<sizeof(T) == 2>(hb);
     dha[i] = g[i] * sb * (1.f - ta * ta);
     dhb[i] = g[i] * ta * (sb * (1.f - sb));
     xa[i] = xha;
@@ -596,7 +596,8 @@ __global__ __launch_bounds__(256) void gn_glu_fwd_vec_kernel(const T* __restrict
     Vec<T>::load(u + (int64_t)r * ldu + c + half, ub);
 #pragma unroll
     for (int i = 0; i < V; ++i)
-      o[i] = ftanh((ua[i] - ma) * ra * ga[i] + ba[i]) * fsigmoid((ub[i] - mb) * rb * gb[i] + bb[i]);
+      o[i] = ftanh<sizeof(T) == 2>((ua[i] - ma) * ra * ga[i] + ba[i]) *
+             fsigmoid<sizeof(T) == 2>((ub[i] - mb) * rb * gb[i] + bb[i]);
     Vec<T>::store(g + (int64_t)r * ldg + c, o);
   }
 }
