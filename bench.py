@@ -5,8 +5,11 @@ Adam, StepLR, EMA codebook) on synthetic 80-dim mel batches.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
 
-N > 1: launched by torch.distributed.run, one rank per GPU (RCCL over xGMI);
-each rank trains 64 x 256 frames (weak scaling, global batch 64*N).
+N > 1: one rank per GPU (RCCL over xGMI); each rank trains 64 x 256 frames
+(weak scaling, global batch 64*N).  Under torch.distributed.run (WORLD_SIZE
+set) this process is one rank; started directly with --gpus N > 1 it
+launches torch.distributed.run itself as a child process (the parent never
+touches the GPU) and exits with its status.
 Rank 0 prints ONE JSON line.  Workload = BASELINE configs[1] (vcc20 VQ-VAE,
 codebook 512, 80 mel, batch 64 x 256 frames per GPU, bf16 conv GEMMs with
 fp32 accumulation; statistics, VQ and optimizer in fp32).  Weights are random
@@ -14,8 +17,9 @@ fp32 accumulation; statistics, VQ and optimizer in fp32).  Weights are random
 """
 import argparse
 import json
-import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -42,7 +46,10 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--config", default="vcc20", choices=["vcc20", "aishell3"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--fp32-steps", type=int, default=5,
+                    help="N=1: also time this many fp32 (parity-mode) steps, reported under 'fp32' (0 = skip)")
+    ap.add_argument("--vq-reps", type=int, default=50, help="VQ kernel launches timed for the 'vq' roofline")
     ap.add_argument("--no-probe", action="store_true", help="skip the per-launch GEMM event probe")
     ap.add_argument("--probe-every", type=int, default=5, help="probe one step in this many of the timed region")
     return ap.parse_args()
@@ -68,6 +75,72 @@ def cpu_baseline(cfg, steps):
                       f"torch-CPU {torch.__version__}, s/step={dt:.2f}"}
 
 
+def launch_ranks(n):
+    """--gpus N > 1 without a launcher: run N ranks under torch.distributed.run
+    (127.0.0.1 rendezvous) as a child process; the parent never initialises
+    the GPU (no exec from a GPU-initialised process)."""
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def time_vq(tr, reps):
+    """The fused VQ kernel (distance, argmin, gather, commitment, EMA
+    statistics; vqx_vq_forward) re-launched `reps` times on the step's own
+    workspace (N = 16,384 frames, K codes, D = 128), timed with events on the
+    stream it runs on.  Algorithmic bytes: z (N*D f32) + E (K*D f32) + idx
+    (N int64) = 536 B/frame + E; FLOPs 2*N*K*D."""
+    from vae_npvc_amd import ops
+    eng = tr.engine
+    w = eng._ws[(B_PER_GPU, T_FRAMES, True)]
+    q = tr.model.quantizer
+    N, D, K = w.N, eng.dims["Z"], eng.dims["K"]
+    args = (w.z, q.embeddings, w.idx, w.zq, w.zq_c, w.stats[1:2], w.vq_part, w.bsum, w.bcnt)
+    for _ in range(3):
+        ops.vq_forward(*args)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        ops.vq_forward(*args)
+    e1.record()
+    e1.synchronize()
+    t = e0.elapsed_time(e1) * 1e-3 / reps
+    nbytes = N * D * 4 + K * D * 4 + N * 8
+    flops = 2.0 * N * K * D
+    return {"kernel": "vqx::vq_forward_kernel", "us": round(t * 1e6, 2), "bytes": nbytes, "flops": flops,
+            "hbm_GBps": round(nbytes / t / 1e9, 1), "hbm_frac": round(nbytes / t / HBM_PEAK, 4),
+            "tflops": round(flops / t / 1e12, 2), "mfma_f32_frac": round(flops / t / PEAK_F32, 4),
+            "roofline_frac": round(max(nbytes / HBM_PEAK, flops / PEAK_F32) / t, 4),
+            "bound": "mfma_f32" if flops / PEAK_F32 > nbytes / HBM_PEAK else "hbm", "launches": reps}
+
+
+def time_fp32(cfg, steps, dev):
+    """The same workload in the parity dtype (fp32 GEMMs on v_mfma_f32_32x32x2_f32):
+    `steps` timed train steps after 2 warm-up steps, 1 GPU."""
+    from vae_npvc_amd.trainer.basic import Trainer
+    c = dict(cfg, compute_dtype="fp32")
+    tr = Trainer(c)
+    mel = c["encoder"]["in_channels"][0]
+    gen = torch.Generator(device="cpu").manual_seed(4321)
+    x = torch.randn(B_PER_GPU, mel, T_FRAMES, generator=gen).to(dev)
+    y = torch.randint(0, c["y_num"], (B_PER_GPU, 1), generator=gen).to(dev)
+    for _ in range(2):
+        _, det = tr.train_step((x, y))
+    dict(det)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tr.train_step((x, y))
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    flops = FLOP_PER_FRAME * B_PER_GPU * T_FRAMES
+    return {"value": round(B_PER_GPU * T_FRAMES / dt, 1), "unit": "mel-frames/s", "ms_per_step": round(1e3 * dt, 3),
+            "steps": steps, "dtype": "fp32", "step_mfma_frac": round(flops / dt / PEAK_F32, 4)}
+
+
 def committed_traffic(symbol):
     """HBM bytes per launch of `symbol` from the newest committed PMC summary
     (profiles/rNN/hbm.json, written by tools/pmc_hbm.py from rocprofv3
@@ -85,6 +158,8 @@ def committed_traffic(symbol):
 
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -138,6 +213,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     detail = dict(det)
+    if world > 1 and world != a.gpus and rank == 0:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}; reporting n_gpus={world}", file=sys.stderr)
     frames = B_PER_GPU * T_FRAMES * world * a.steps
     value = frames / elapsed
     ms = 1e3 * elapsed / a.steps
@@ -172,6 +249,10 @@ def main():
         "roofline": roof,
         "loss": {k: round(v, 4) for k, v in detail.items()},
     }
+    vq = time_vq(tr, a.vq_reps) if a.vq_reps > 0 else None
+    out["vq"] = vq
+    if world == 1 and a.fp32_steps > 0 and a.dtype != "fp32":
+        out["fp32"] = time_fp32(cfg, a.fp32_steps, dev)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, a.cpu_steps)
     else:

@@ -235,13 +235,13 @@ class OracleVQVAE:
     def reduce_sum(self, t):
         return t
 
-    def pick_rows(self, zt):
+    def pick_rows(self, z):  # _tile (noise drawn first), then randperm (layers_vq.py:197,212-213)
+        zt = self._tile(z)
         return zt[torch.randperm(zt.shape[0])][: self.K]
 
     def init_emb(self, z):  # layers_vq.py:192-201
         self.emb_init = not self.emb_init
-        _z = self._tile(z)
-        self.embeddings = self.pick_rows(_z)
+        self.embeddings = self.pick_rows(z)
         self.emb_sum = self.embeddings.clone()
         self.emb_elem = torch.ones(self.K)
 
@@ -252,8 +252,7 @@ class OracleVQVAE:
             onehot.scatter_(0, idx.view(1, z.shape[0]), 1)
             s = self.reduce_sum(torch.matmul(onehot, z))
             n = self.reduce_sum(onehot.sum(dim=-1))
-            _z = self._tile(z)
-            rand = self.pick_rows(_z)
+            rand = self.pick_rows(z)
             old = self.embeddings.clone()
             self.emb_sum = mu * self.emb_sum + (1.0 - mu) * s
             self.emb_elem = mu * self.emb_elem + (1.0 - mu) * n

@@ -98,12 +98,20 @@ def _ddp_step_worker(rank, port, cfg, B, T, steps, q):
             dist.all_reduce(t, op=dist.ReduceOp.SUM)
             return t
 
-        def pick_rows(zt):  # every rank draws randperm(N_global); owners fill, SUM assembles
-            perm = torch.randperm(zt.shape[0] * WORLD)[: model.K]
+        def pick_rows(z):
+            if z.shape[0] * WORLD < model.K:
+                # N_global < K: every rank tiles the gathered global batch with the
+                # same CPU generator, so all ranks draw identical rows (no SUM)
+                parts = [torch.empty_like(z) for _ in range(WORLD)]
+                dist.all_gather(parts, z.contiguous())
+                zt = model._tile(torch.cat(parts))
+                return zt[torch.randperm(zt.shape[0])][: model.K]
+            # every rank draws randperm(N_global); owners fill, SUM assembles
+            perm = torch.randperm(z.shape[0] * WORLD)[: model.K]
             loc = owned_rows(perm, rank * n_local, n_local)
-            out = torch.zeros(model.K, zt.shape[1])
+            out = torch.zeros(model.K, z.shape[1])
             mine = loc >= 0
-            out[mine] = zt[loc[mine]]
+            out[mine] = z[loc[mine]]
             return reduce_sum(out)
 
         def grad_hook(params):
@@ -133,9 +141,10 @@ def _ddp_step_worker(rank, port, cfg, B, T, steps, q):
 
 
 @pytest.mark.timeout(600)
-def test_two_rank_step_equals_global_batch_step():
+@pytest.mark.parametrize("B,T", [(4, 64), (2, 16)])  # (2, 16): N_global = 32 < K = 64, the _tile path
+def test_two_rank_step_equals_global_batch_step(B, T):
     from oracle.vqvae_cpu import OracleTrainer, seeded_batch, seeded_state_dict
-    cfg, B, T, steps = small_cfg(), 4, 64, 2
+    cfg, steps = small_cfg(), 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -157,15 +166,26 @@ def test_two_rank_step_equals_global_batch_step():
         _, det = ref.train_step((x, y))
         ref_losses.append((det["X like"], det["VQ loss"]))
 
-    for s in range(steps):
+    # N_global < K: each frame sits between its own noisy tiled copies at squared
+    # distances ~1e-4 against |z|^2 ~ 1e2, so the argmin between them flips with
+    # the matmul blocking of the local vs global batch (fp32 rounding ~1e-5):
+    # the commitment loss is then only reproducible to ~1%, and the flips change
+    # which codes survive the first EMA update: later steps are compared only
+    # between the ranks (which must agree exactly: the rows are drawn from the
+    # gathered global batch, not from each rank's own frames)
+    tiled = B * T < cfg["z_num"]
+    for s in range(1 if tiled else steps):
         # frame_mean losses: the global value is the mean over the equal shards
         for j in range(2):
             got = 0.5 * (res[0][1][s][j] + res[1][1][s][j])
-            assert got == pytest.approx(ref_losses[s][j], rel=2e-5)
+            rt = 2e-2 if (tiled and j == 1) else 2e-5
+            assert got == pytest.approx(ref_losses[s][j], rel=rt), (s, j, res[0][1], res[1][1], ref_losses)
     # both ranks hold identical weights and codebooks
     for k in res[0][2]:
         assert np.array_equal(res[0][2][k], res[1][2][k]), k
     assert np.array_equal(res[0][3], res[1][3])
+    if tiled:
+        return
     # ... equal to the single-process global-batch step (fp32 summation order differs)
     for k, v in ref.model.params.items():
         v = v.detach().numpy()

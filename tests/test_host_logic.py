@@ -87,3 +87,53 @@ def test_owned_rows_partition_the_permutation():
         total += part
     assert torch.equal(hits, torch.ones(K, dtype=torch.int64))  # every row owned exactly once
     assert torch.equal(total, z[perm])  # the SUM all-reduce assembles z_global[perm]
+
+
+def _loop_trainer(monkeypatch, start=0):
+    """A Trainer whose device work is stubbed, to drive the host-side
+    iteration contract on the CPU."""
+    import vae_npvc_amd.trainer.basic as tb
+    monkeypatch.setattr(tb, "LazyLossDetail", lambda eng, w, s: {"X like": 1.0})
+    tr = tb.Trainer.__new__(tb.Trainer)
+    tr.model = SimpleNamespace(training=True)
+    tr.device = torch.device("cpu")
+    tr.engine = SimpleNamespace(train_step=lambda x, y: SimpleNamespace(stats=None))
+    tr.iteration = start
+    return tr
+
+
+def test_train_step_advances_under_reference_loop(monkeypatch):
+    """bin/train.py:54,126 feeds the returned iteration back in
+    (`iteration, d = trainer.train_step(batch, iteration=iteration)`); the
+    reference Trainer ignores the argument and increments its own counter
+    (trainer/basic.py:74-77), so the loop reaches max_iter."""
+    tr = _loop_trainer(monkeypatch)
+    batch = (torch.zeros(1, 2, 3), torch.zeros(1, 1, dtype=torch.int64))
+    iteration, seen = 1, []
+    while iteration <= 5:
+        iteration, _ = tr.train_step(batch, iteration=iteration)
+        seen.append(iteration)
+    assert seen == [1, 2, 3, 4, 5, 6]
+    # resume: load_checkpoint restores the counter, train.py passes ckpt + 1
+    tr2 = _loop_trainer(monkeypatch, start=20)
+    it, _ = tr2.train_step(batch, iteration=21)
+    assert it == 21
+    assert tr2.train_step(batch)[0] == 22  # iteration=None counts the same way
+
+
+def test_load_state_dict_resizes_plain_codebook():
+    """vqvae.py:106-119: a straight-through-VQ checkpoint with another codebook
+    size rebuilds the quantizer at the checkpoint's shape and loads."""
+    from tests.helpers import cfg_of
+    from vae_npvc_amd.model.vqvae import Model
+    cfg = cfg_of("vcc20", use_ema=False)
+    src = Model(dict(cfg, z_num=256))
+    sd = src.state_dict()
+    m = Model(cfg)
+    assert tuple(m.quantizer.embeddings.shape) == (512, 128)
+    order = [k for k, _ in m.named_parameters()]
+    m.load_state_dict(sd)
+    assert tuple(m.quantizer.embeddings.shape) == (256, 128)
+    assert torch.equal(m.quantizer.embeddings, sd["quantizer.embeddings"])
+    assert m.quantizer.normalize == src.quantizer.normalize
+    assert [k for k, _ in m.named_parameters()] == order  # parameter order kept (optimizer state lines up)

@@ -191,6 +191,7 @@ class VQVAEEngine:
                 self.gviews[p] = self.flat_g[off:off + n].view_as(p)
                 off += n
         self.n_params = total
+        self._p_off = [o for _, o in self._offsets_of(params)]
         self._p0_ptr = params[0].data_ptr()
         enc_ids = {id(p) for p in self.m.encoder.parameters()}
         self.enc_end = sum(p.numel() for p in params if id(p) in enc_ids)
@@ -201,13 +202,66 @@ class VQVAEEngine:
             p.data_ptr() == self.flat_p.data_ptr() + 4 * o for p, o in self._offsets())
 
     def _offsets(self):
+        return self._offsets_of(self.params)
+
+    @staticmethod
+    def _offsets_of(params):
         off = 0
-        for p in self.params:
+        for p in params:
             yield p, off
             off += p.numel()
 
     def g(self, p):
         return self.gviews[p]
+
+    def _params_written(self, tensors):
+        """Indices (flat order) of the parameters whose gradient views overlap
+        any of `tensors` (views into flat_g; None entries are skipped)."""
+        import bisect
+        base = self.flat_g.data_ptr()
+        hit = set()
+        for t in tensors:
+            if t is None or t.numel() == 0:
+                continue
+            lo = (t.data_ptr() - base) // 4
+            if lo < 0 or lo >= self.n_params:
+                continue
+            hi = lo + t.numel()
+            i = bisect.bisect_right(self._p_off, lo) - 1
+            while i < len(self.params) and self._p_off[i] < hi:
+                hit.add(i)
+                i += 1
+        return sorted(hit)
+
+    # ---- data parallel: issue each gradient range's all-reduce when it is final
+    DDP_MIN_RUN = 64 << 10  # floats; smaller ready runs wait (they may still grow) until the flush
+
+    def _grads_reset(self):
+        self._g_ready = [False] * len(self.params)
+        self._g_issued = [False] * len(self.params)
+
+    def _grads_final(self, idxs, flush=False):
+        """Mark parameters' gradients final and launch async mean all-reduces
+        over every maximal contiguous run of final, not yet reduced gradients
+        (runs below DDP_MIN_RUN floats wait unless `flush`)."""
+        if self.world <= 1:
+            return
+        for i in idxs:
+            self._g_ready[i] = True
+        n, i = len(self.params), 0
+        while i < n:
+            if not self._g_ready[i] or self._g_issued[i]:
+                i += 1
+                continue
+            j = i
+            while j < n and self._g_ready[j] and not self._g_issued[j]:
+                j += 1
+            lo, hi = self._p_off[i], self._p_off[j - 1] + self.params[j - 1].numel()
+            if flush or hi - lo >= self.DDP_MIN_RUN:
+                self.comm.grads_ready(self.flat_g, lo, hi)
+                for k in range(i, j):
+                    self._g_issued[k] = True
+            i = j
 
     def _build_layers(self):
         m, d, dev = self.m, self.dims, self.device
@@ -323,6 +377,10 @@ class VQVAEEngine:
                              cr(cs_enc_b, g(k3.mod.bias)), cr(dg_enc_b, g(gn.weight)), cr(db_enc_b, g(gn.bias))]
         t["enc0"] = [self._wn_entry(self.enc0, True), cr(w.cs_enc[ns % 2], g(self.enc0.mod.bias))]
         w.bwd_tables = {k: ops.wn_table(v) for k, v in t.items()}
+        # parameters whose gradients are final once a group's launch is done
+        # (data parallel: their all-reduce is issued right then, parallel/ddp.py)
+        w.bwd_params = {k: self._params_written([t_ for e in entries for t_ in (e.get("dv"), e.get("dg"))])
+                        for k, entries in t.items()}
         # all ResSkip blocks' conditioning linears, forward and backward, one table
         w.cond_table = ops.linear_table([dict(W=Lr.wp, bias=Lr.mod.bias, out=w.condbias[i], dout=w.cs_all[i],
                                               dW=Lr.slab.view(Lr.rows, Lr.cols), dbias=g(Lr.mod.bias))
@@ -431,8 +489,15 @@ class VQVAEEngine:
 
     def _tile_rows(self, w):
         """N < K path of _tile (layers_vq.py:183-190): repeat z with N(0, 0.01/sqrt(D))
-        noise drawn on the CPU generator, then take perm rows.  Host side; rare."""
-        z = w.z.detach().cpu()
+        noise drawn on the CPU generator, then take perm rows.  Host side; rare.
+        Data parallel: the tiling runs on the gathered GLOBAL batch (rank
+        order = the single-process batch order), and every rank draws the same
+        noise and permutation from its identically seeded CPU generator, so all
+        ranks hold the single-process global-batch rows."""
+        z = w.z.detach()
+        if self.world > 1:
+            z = self.comm.all_gather_cat(z)
+        z = z.cpu()
         n, dd = z.shape
         K = self.dims["K"]
         rep = (K + n - 1) // n
@@ -464,6 +529,12 @@ class VQVAEEngine:
         return src
 
     # ------------------------------------------------------------ backward
+    def _wn_bwd(self, w, key):
+        """A backward group's weight-norm backward + bias/affine reductions;
+        its gradients are final afterwards (data parallel: reduce them now)."""
+        ops.weight_norm_bwd(w.bwd_tables[key])
+        self._grads_final(w.bwd_params[key])
+
     def _gnb(self, w, i):
         """GNBWD epilogue arguments: the GEMM producing dL/d(GN_i output) also
         writes block i's GroupNorm-backward sums (encoder, G=1)."""
@@ -489,14 +560,13 @@ class VQVAEEngine:
         if not self.plain:  # EMA: the commitment term is the encoder's only gradient
             ops.vq_commit_bwd(w.z, w.zq, 2.0 * self.m.beta * grad_scale / N, w.dz)
         eo = self.enc_out
-        tb = w.bwd_tables
         self.bias_grad(eo, w.dz, w)
         self.wgrad(eo, w.dz, w.a[ns], T)
         cur = w.dc[0]
         # every dL/dc_i producer also writes its bias-gradient partials (COLSUM)
         # and, for the block below, the GroupNorm-backward sums (GNBWD)
         self.dgrad(eo, w.dz, cur, T, mask=w.a[ns], mask_slope=0.2, colsum=w.cs_enc[0], **self._gnb(w, ns - 1))
-        ops.weight_norm_bwd(tb["enc_out"])
+        self._wn_bwd(w, "enc_out")
         cs_b, dg_b, db_b = (self._bview(t, B, C) for t in (w.colsum_b, w.dgam_b, w.dbet_b))
         for i in reversed(range(ns)):
             k3, sk, gn = self.enc_k3[i], self.enc_sk[i], self.enc_gn[i]
@@ -510,17 +580,16 @@ class VQVAEEngine:
             self.dgrad(k3, w.dh, w.tmp, T, mask=w.a[i], mask_slope=0.2)
             self.dgrad(sk, cur, nxt, T, res=w.tmp, colsum=w.cs_enc[j], **(self._gnb(w, i - 1) if i > 0 else {}))
             # weight norms of k3/sk + biases of sk (cur partials), k3 and the GN affine
-            ops.weight_norm_bwd(tb[("enc", i)])
+            self._wn_bwd(w, ("enc", i))
             cur = nxt
         # cur = dL/dc_0 (conv0 output); conv0's input (the mel batch) needs no gradient
         self.wgrad(self.enc0, cur, w.x, T)
-        ops.weight_norm_bwd(tb["enc0"])
+        self._wn_bwd(w, "enc0")
 
     def decoder_bwd(self, w):
         T, nd, Cd, B = w.T, self.dims["nd"], self.dims["Cd"], w.B
         f1, f2 = self.fin1, self.fin2
         dxhat = w.dxhat
-        tb = w.bwd_tables
         self.bias_grad(f2, dxhat, w)
         self.wgrad(f2, dxhat, w.f1, T)
         self.dgrad(f2, dxhat, w.df1, T, mask=w.f1, mask_slope=0.0, colsum=w.cs_f1)
@@ -532,7 +601,7 @@ class VQVAEEngine:
         ops.convert_2d(cur[:, Cd:], nxt[:, Cd:])
         ops.convert_2d(None, cur, cols=Cd)  # dL/dx_{nd+1} = 0: the last residual output is unused
         ops.zero_(w.cs_dec[0])  # ... and so are its bias-gradient partials (read by block nd-1)
-        ops.weight_norm_bwd(tb["fin"])
+        self._wn_bwd(w, "fin")
         C2 = 2 * Cd
         dg_b, db_b = (self._bview(t, B, C2) for t in (w.dgam_b, w.dbet_b))
         for i in reversed(range(nd)):
@@ -550,17 +619,17 @@ class VQVAEEngine:
             self.wgrad(ci, w.du, w.xs[i], T)
             self.dgrad(ci, w.du, nxt[:, :Cd], T, res=cur[:, :Cd], colsum=w.cs_dec[1 - j])
             # weight norms of conv_in/res_skip + biases of res_skip, conv_in and the GN affine
-            ops.weight_norm_bwd(tb[("dec", i)])
+            self._wn_bwd(w, ("dec", i))
             cur, nxt = nxt, cur
         # speaker conditioning of all blocks at once: dW, bias and d(embedding)
         cond = self.dec_cond[0]
         ops.linear_batched_bwd(w.cond_table, w.yemb, B, cond.cin, cond.cout, w.dyemb, w.lin_part)
-        ops.weight_norm_bwd(tb["cond"])
+        self._wn_bwd(w, "cond")
         dx1 = cur[:, :Cd]  # dL/dx_1, the ConvT0 output
         self.wgrad(self.dec0, dx1, w.zq_in, T)
         if self.plain:  # straight-through VQ: the decoder input's gradient reaches the encoder
             self.dgrad(self.dec0, dx1, w.dzq, T)
-        ops.weight_norm_bwd(tb["dec0"])
+        self._wn_bwd(w, "dec0")
         emb_g = self.g(self.m.embeds._embedding.weight)
         ops.zero_(emb_g)
         ops.embedding_bwd(w.dyemb, w.y_dev, emb_g)
@@ -572,7 +641,7 @@ class VQVAEEngine:
         if q.initialized:
             return False
         K = self.dims["K"]
-        if w.N * self.world < K:  # N_global < K: noisy tiling (local rows; DESIGN.md "multi-GPU")
+        if w.N * self.world < K:  # N_global < K: noisy tiling of the global batch (identical on every rank)
             rows = self._tile_rows(w)
             q.embeddings.copy_(rows)
         else:
@@ -618,7 +687,10 @@ class VQVAEEngine:
         ops.vq_forward(w.z, q.embeddings, w.idx, w.zq, w.zq_c, w.stats[1:2], w.vq_part, w.bsum, w.bcnt)
         # rows for dead-code replacement: z[randperm(N)[:K]] (update_emb, layers_vq.py:212-213)
         if w.N * self.world < K:
-            w.rand_rows.copy_(self._tile_rows(w))
+            rows = self._tile_rows(w)
+            if self.rank != 0:  # every rank holds the same rows; the EMA bundle is SUM-reduced
+                rows.zero_()
+            w.rand_rows.copy_(rows)
         else:
             perm = self._perm_rows(w.N * self.world, K, self.rank * w.N, w.N if self.world > 1 else None)
             ops.gather_rows(w.z, perm, w.rand_rows)
@@ -662,23 +734,22 @@ class VQVAEEngine:
         return w
 
     def backward(self, w, grad_loss=None):
+        """Data parallel: every backward group's gradients are all-reduced as
+        soon as its weight-norm backward has finalised them (_wn_bwd), so the
+        reduces overlap the rest of the backward; the remainder (conditioning,
+        ConvT0, embedding, codebook) is flushed at the end."""
+        if self.world > 1:
+            self._grads_reset()
         if self.plain:
             # straight-through: the encoder's gradient comes through the decoder
             self.decoder_bwd(w)
             self.vq_plain_backward(w)
-            if self.world > 1:
-                self.comm.grads_ready(self.flat_g, self.enc_end, self.n_params)
             self.encoder_bwd(w)
-            if self.world > 1:
-                self.comm.grads_ready(self.flat_g, 0, self.enc_end)
-                self.comm.finish()
-            return
-        self.encoder_bwd(w)
+        else:
+            self.encoder_bwd(w)
+            self.decoder_bwd(w)
         if self.world > 1:
-            self.comm.grads_ready(self.flat_g, 0, self.enc_end)
-        self.decoder_bwd(w)
-        if self.world > 1:
-            self.comm.grads_ready(self.flat_g, self.enc_end, self.n_params)
+            self._grads_final(range(len(self.params)), flush=True)
             self.comm.finish()
 
     def init_optimizer(self, lr, betas=(0.5, 0.999), eps=1e-8, max_grad_norm=10.0, sched_step=None, sched_gamma=1.0,

@@ -166,8 +166,21 @@ class Model(nn.Module):
         self._engine = None
 
     def load_state_dict(self, state_dict, strict=True):
-        out = super().load_state_dict(state_dict, strict=strict)
-        return out
+        """vqvae.py:106-119: with the straight-through quantizer, a checkpoint
+        whose codebook shape differs rebuilds the quantizer at that shape
+        (same normalize / reduction) before loading; the engine re-flattens
+        the parameters on its next use."""
+        if not self.use_ema and "quantizer.embeddings" in state_dict:
+            want = tuple(state_dict["quantizer.embeddings"].shape)
+            have = tuple(self.quantizer.embeddings.shape)
+            if want != have:
+                print(f"Embedding size mismatch for model.quantizer: copying a param with shape {want} from "
+                      f"checkpoint, resizing the param with shape {have} in current model.")
+                dev = self.quantizer.embeddings.device
+                self.quantizer = VectorQuantizer(want[0], want[1], normalize=self.quantizer.normalize,
+                                                 reduction=self.quantizer.reduction).to(dev)
+                self._engine = None
+        return super().load_state_dict(state_dict, strict=strict)
 
 
 LOG_2PI = math.log(2.0 * math.pi)

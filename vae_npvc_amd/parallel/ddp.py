@@ -44,6 +44,14 @@ class Comm:
     def all_reduce_sum(self, t, async_op=False):
         return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
 
+    def all_gather_cat(self, t):
+        """Concatenation over ranks (rank order) of a per-rank tensor; gloo
+        gathers through host memory."""
+        src = t.contiguous() if self.backend == "nccl" else t.detach().cpu()
+        parts = [torch.empty_like(src) for _ in range(self.world)]
+        dist.all_gather(parts, src, group=self.group)
+        return torch.cat(parts).to(t.device)
+
     def grads_ready(self, flat, lo, hi):
         """Launch async mean all-reduces over flat[lo:hi] in buckets."""
         op = self._avg_op()

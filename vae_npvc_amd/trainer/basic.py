@@ -118,12 +118,20 @@ class Trainer(object):
         self.device = torch.device("cuda", torch.cuda.current_device())
         self.model = getattr(module, model_name)(config).to(self.device)
         self.model.train()
+        self._setup_engine()
+        self.optimizer = FusedOptimState(self)
+        self.scheduler = None  # StepLR runs on the device inside the Adam kernel's hyper-parameter step
+        self.iteration = 0
+
+    def _setup_engine(self):
+        """(Re)build the fused engine over the model's current parameters:
+        data-parallel wiring, identical initial weights on every rank, fresh
+        optimizer moments."""
         self.engine = self.model.engine(self.device)
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             from ..parallel.ddp import Comm
             comm = Comm()
             self.engine.world, self.engine.rank, self.engine.comm = comm.world, comm.rank, comm
-            # identical initial weights on every rank
             dist.broadcast(self.engine.flat_p, 0)
             for b in self.model.buffers():
                 dist.broadcast(b, 0)
@@ -133,9 +141,6 @@ class Trainer(object):
                                    sched_step=sp.get("step_size") if self.scheduler_cfg else None,
                                    sched_gamma=sp.get("gamma", 1.0) if self.scheduler_cfg else 1.0,
                                    kind=self.optim_kind)
-        self.optimizer = FusedOptimState(self)
-        self.scheduler = None  # StepLR runs on the device inside the Adam kernel's hyper-parameter step
-        self.iteration = 0
 
     def train_step(self, input, iteration=None):
         assert self.model.training
@@ -143,10 +148,12 @@ class Trainer(object):
         x = x.to(self.device, non_blocking=True).float().contiguous()
         y = y.to(self.device, non_blocking=True)
         w = self.engine.train_step(x, y)
-        if iteration is None:
-            self.iteration += 1
-        else:
-            self.iteration = iteration
+        # trainer/basic.py:74-77: the passed iteration is ignored and the
+        # trainer's own counter advances (bin/train.py:126 feeds the returned
+        # value back in).  The reference's iteration=None branch raises
+        # (None + 1); here it counts the same way.  load_checkpoint restores
+        # the counter, so a resumed run continues at checkpoint + 1.
+        self.iteration += 1
         return self.iteration, LazyLossDetail(self.engine, w, w.stats)
 
     def valid(self, data_loader):
@@ -176,6 +183,8 @@ class Trainer(object):
         data = torch.load(checkpoint_file, map_location="cpu", weights_only=True)
         with torch.no_grad():
             self.model.load_state_dict(data["model"])
+        if self.model._engine is not self.engine or not self.engine.params_intact():
+            self._setup_engine()  # the codebook was resized (Model.load_state_dict, vqvae.py:106-119)
         self.optimizer.load_state_dict(data["optimizer"])
         self.iteration = int(data["iteration"])
         return self.iteration
