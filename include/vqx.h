@@ -274,13 +274,18 @@ int vqx_logloss_fwd_bwd(const float* x_nct, const float* xhat, int32_t ldxh, int
  *   zq[n]      = E[idx[n]]  (f32 [N][D]) and zq_c (dtype, decoder input)
  *   sqerr      : sum_n ||zq_n - z_n||^2  into sqerr_out[0] (deterministic)
  *   bsum[k][d] += sum_{n: idx=k} z[n][d], bcnt[k] += |{n: idx=k}|
- *                 (fp32 atomics; pass NULL to skip, e.g. eval / encode())
- * z [N][D] f32 (frame-major, D = 128), E [K][D] f32, K % 16 == 0.
- * `partials` is a caller workspace of >= ceil(N/64) floats.
+ *                 (per-chunk LDS tables reduced in chunk order; pass NULL to
+ *                 skip, e.g. eval / encode())
+ * z [N][D] f32 (frame-major, D = 128), E [K][D] f32, K % 16 == 0, K <= 3264.
+ * `partials` is a caller workspace of >= vqx_vq_workspace(N, K, bsum != NULL)
+ * floats.
  */
 int vqx_vq_forward(const float* z, int64_t n_rows, int32_t D, const float* E, int32_t K,
                    int64_t* idx, float* zq, void* zq_c, int32_t zq_c_dtype, float* sqerr_out,
                    float* partials, float* bsum, float* bcnt, vqx_stream_t stream);
+/* Workspace (floats) vqx_vq_forward needs for N frames and K codes, with or
+ * without the EMA statistics. */
+int vqx_vq_workspace(int64_t n_rows, int32_t K, int32_t with_stats, int64_t* floats);
 
 /*
  * EMA codebook update (update_emb, layers_vq.py:203-233; init_emb :192-201):
@@ -452,7 +457,7 @@ int vqx_probe_count(int64_t* n);
 int vqx_probe_read(int64_t i, int32_t* info5, double* flops, float* ms);
 
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
-#define VQX_ABI_VERSION 114
+#define VQX_ABI_VERSION 115
 int vqx_version(void);
 
 #ifdef __cplusplus

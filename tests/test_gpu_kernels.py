@@ -146,7 +146,7 @@ def test_vq_argmin_exact(K):
     zq = torch.empty(N, D, device=DEV)
     zqc = torch.empty(N, D, device=DEV, dtype=torch.bfloat16)
     sq = torch.zeros(1, device=DEV)
-    part = torch.empty((N + 63) // 64, device=DEV)
+    part = torch.empty(ops.vq_workspace(N, K, True), device=DEV)
     bsum = torch.zeros(K, D, device=DEV)
     bcnt = torch.zeros(K, device=DEV)
     ops.vq_forward(zd, Ed, idx, zq, zqc, sq, part, bsum, bcnt)
@@ -159,6 +159,38 @@ def test_vq_argmin_exact(K):
     onehot = F.one_hot(ref, K).float()
     assert torch.allclose(bcnt.cpu(), onehot.sum(0))
     assert torch.allclose(bsum.cpu(), onehot.t() @ z, atol=1e-4, rtol=1e-5)
+
+
+@pytest.mark.parametrize("N,K,collapse", [(1000, 16, False), (777, 128, True), (16384, 512, True),
+                                          (5000, 1024, False), (3001, 2048, False), (33, 512, False)])
+def test_vq_ema_statistics_ragged_and_collapsed(N, K, collapse):
+    """EMA statistics of vqx_vq_forward (update_emb, layers_vq.py:207-211):
+    bsum = onehot(idx)^T z and bcnt = code counts, accumulated (+=) into
+    nonzero buffers, for ragged N (partial frame groups and chunks), every
+    LDS slice width (K 16 .. 2048) and a collapsed codebook where all frames
+    pick 2 codes (the round-1 kernel's same-address atomic pile-up case)."""
+    ops = _ops()
+    torch.manual_seed(N + K)
+    D = 128
+    z = torch.randn(N, D)
+    E = torch.randn(K, D)
+    if collapse:
+        E[2:] += 50.0  # every frame is nearest to code 0 or 1
+    ref = ((z.pow(2).sum(1, keepdim=True) + E.pow(2).sum(1)) - 2 * z @ E.t()).argmin(1)
+    idx = torch.empty(N, dtype=torch.int64, device=DEV)
+    part = torch.empty(ops.vq_workspace(N, K, True), device=DEV)
+    bsum0, bcnt0 = torch.randn(K, D), torch.rand(K)
+    bsum, bcnt = bsum0.to(DEV), bcnt0.to(DEV)
+    sq = torch.zeros(1, device=DEV)
+    ops.vq_forward(z.to(DEV), E.to(DEV), idx, None, None, sq, part, bsum, bcnt)
+    idx = idx.cpu()
+    assert torch.equal(idx, ref)
+    onehot = F.one_hot(ref, K).double()
+    assert torch.equal(bcnt.cpu(), bcnt0 + onehot.sum(0).float())  # counts are exact; one f32 add
+    want = bsum0.double() + onehot.t() @ z.double()
+    assert torch.allclose(bsum.cpu().double(), want, atol=1e-3, rtol=1e-5)
+    if collapse:
+        assert int((onehot.sum(0) > 0).sum()) <= 2
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

@@ -140,7 +140,7 @@ def test_vq_full_size_matches_reference_golden(K):
     idx = torch.empty(N, dtype=torch.int64, device="cuda")
     zq = torch.empty(N, D, device="cuda")
     sq = torch.zeros(1, device="cuda")
-    part = torch.empty((N + 63) // 64, device="cuda")
+    part = torch.empty(ops.vq_workspace(N, K, True), device="cuda")
     ema = torch.zeros(K * D + K, device="cuda")
     bsum, bcnt = ema[:K * D].view(K, D), ema[K * D:]
     ops.vq_forward(zf, Ed, idx, zq, None, sq, part, bsum, bcnt)

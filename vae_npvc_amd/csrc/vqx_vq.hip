@@ -1,49 +1,125 @@
 // EMA vector quantizer kernels (layers_vq.py:166-334) for gfx950.
 //
 // vq_forward: one launch does distance -> argmin -> gather -> commitment
-// partial sums -> EMA scatter statistics, reading z in its frame-major
-// layout (no transpose copy, layers_vq.py:274-276) and never materialising
-// the (N, K) distance matrix (layers_vq.py:285-289).
+// partial sums, reading z in its frame-major layout (no transpose copy,
+// layers_vq.py:274-276) and never materialising the (N, K) distance matrix
+// (layers_vq.py:285-289); the EMA statistics follow as a dense per-chunk
+// reduction (vq_stats_kernel + vq_stats_reduce_kernel).
 //
-// Geometry: 4 waves x 16 frames per workgroup.  Each wave keeps its 16x128
-// f32 z block in registers as the A operand of v_mfma_f32_16x16x4_f32; the
-// codebook streams through LDS in 64-code tiles (double-buffered, XOR-
-// swizzled 16-B chunks so the ds_read_b128 B-fragment reads are
-// conflict-free).  Dot products are exact f32 (fmaf chains), the distance
+// Geometry: see vq_forward_kernel.  The codebook streams through LDS in
+// 64-code steps (XOR-swizzled 16-B chunks so the ds_read_b128 B-fragment
+// reads are conflict-free).  Dot products are exact f32 (fmaf chains), the distance
 // is formed in the reference's order (||z||^2 + ||e||^2) - 2 z.e, and the
 // argmin keeps the first minimum (strict '<' in ascending code order, then
 // a lowest-index tie-break across lanes), matching torch.argmin.
 #include "vqx_common.h"
 
+// tools/vq_lab.sh only: 1 = no score loop, 2 = no epilogue gather/stores, 3 = both
+#ifndef VQX_VQ_LAB
+#define VQX_VQ_LAB 0
+#endif
+
 namespace vqx {
 
 constexpr int VQ_D = 128;
-constexpr int VQ_TILE = 64;                 // codes per LDS tile
-constexpr int VQ_TILE_BYTES = VQ_TILE * VQ_D * 4;
+// Workgroup geometry of vq_forward_kernel: VQ_FG groups of 16 frames x VQ_CS
+// code splits = 8 waves.  A wave keeps its 16 frames' z (16 x 128 f32) in
+// registers as the A operand of v_mfma_f32_16x16x4_f32 and, per step, scores
+// them against VQ_SUB codes (one accumulator chain per 16 codes; the 40-cycle
+// dependent-MFMA latency is covered by the other waves of the SIMD).  The
+// VQ_CS waves of a frame group take disjoint code ranges of the
+// step; their (distance, index) minima merge through LDS at the end.  512
+// workgroups of 8 waves at 32 KiB LDS and <= 128 VGPRs: two workgroups per
+// CU, four waves per SIMD, so one wave's barrier / LDS / epilogue stalls run under another's
+// MFMAs (the round-1 kernel had one wave per SIMD).
+constexpr int VQ_FG = 2;
+constexpr int VQ_CS = 4;
+constexpr int VQ_SUB = 16;
+constexpr int VQ_STEP = VQ_CS * VQ_SUB;            // 64 codes per LDS step
+constexpr int VQ_STEP_BYTES = VQ_STEP * VQ_D * 4;  // 32 KiB
+constexpr int VQ_THREADS = 64 * VQ_FG * VQ_CS;     // 512
+constexpr int VQ_FRAMES = 16 * VQ_FG;              // 32 frames per workgroup
+constexpr int VQ_STAGE = VQ_STEP_BYTES / 16 / VQ_THREADS;  // 16-B chunks staged per thread per step
 
-__global__ __launch_bounds__(256) void vq_forward_kernel(const float* __restrict__ z, int64_t N,
-                                                         const float* __restrict__ E, int K,
-                                                         int64_t* __restrict__ idx_out,
-                                                         float* __restrict__ zq, void* __restrict__ zq_c,
-                                                         int zq_dt, float* __restrict__ partials,
-                                                         float* __restrict__ bsum, float* __restrict__ bcnt) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * VQ_TILE_BYTES];
-  __shared__ float ee_lds[2][VQ_TILE];
+// EMA statistics (vq_stats_kernel): frames per chunk and the per-code sum
+// slabs [chunks][K][D] + counts [chunks][K] that vq_stats_reduce_kernel sums
+// in chunk order.
+__host__ __device__ constexpr int vq_stats_dsl(int K) {  // dims per LDS slice: K * (dsl + 1) * 4 B <= 64 KiB
+  int d = 128;
+  while (d > 4 && K * (d + 1) > 16384) d >>= 1;
+  return d;
+}
+inline int vq_stats_chunks(int64_t N, int K) {
+  const int slices = VQ_D / vq_stats_dsl(K);
+  int64_t c = (256 + slices - 1) / slices;  // ~256 workgroups
+  const int64_t cmax = (N + 255) / 256;     // >= 256 frames per chunk
+  if (c > cmax) c = cmax;
+  return (int)(c < 1 ? 1 : c);
+}
+inline int64_t vq_partials_floats(int64_t N) { return (N + VQ_FRAMES - 1) / VQ_FRAMES; }
+inline int64_t vq_workspace_floats(int64_t N, int K, bool stats) {
+  int64_t f = (vq_partials_floats(N) + 63) & ~(int64_t)63;
+  if (stats) f += (int64_t)vq_stats_chunks(N, K) * K * (VQ_D + 1);
+  return f;
+}
+
+__global__ __launch_bounds__(VQ_THREADS, 4) void vq_forward_kernel(const float* __restrict__ z, int64_t N,
+                                                                   const float* __restrict__ E, int K,
+                                                                   int64_t* __restrict__ idx_out,
+                                                                   float* __restrict__ zq, void* __restrict__ zq_c,
+                                                                   int zq_dt, float* __restrict__ partials) {
+  __shared__ __attribute__((aligned(16))) char smem[VQ_STEP_BYTES];
+  __shared__ float eeL[VQ_STEP];
   __shared__ float red[16];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int fg = w % VQ_FG, cs = w / VQ_FG;
   const int q = lane >> 4, j16 = lane & 15;
-  const int64_t row0 = (int64_t)blockIdx.x * 64 + w * 16;
-  const int64_t my_row = row0 + j16;  // A-operand row of this lane
+  const int64_t my_row = (int64_t)blockIdx.x * VQ_FRAMES + fg * 16 + j16;  // A-operand row of this lane
   const bool row_ok = my_row < N;
 
-  // z fragments: zf[kb] = z[my_row][16kb + 4q .. +3]
+  const int nsteps = (VQX_VQ_LAB & 1) ? 0 : (K + VQ_STEP - 1) / VQ_STEP;
+  // Staging: thread t holds 4 consecutive 16-B chunks (64 B) of code t >> 3 of
+  // the step, loaded through one buffer descriptor over E (codes >= K read as
+  // zeros, no branches).  The 8 threads of a code also form its ||e||^2
+  // (the 32 fmaf of each thread, then two quad-DPP and one half-row-mirror
+  // adds) into eeL, so the score loop needs one LDS read per code block.
+  static_assert(VQ_STAGE == 4 && VQ_STEP * 8 == VQ_THREADS, "staging layout");
+  const __amdgpu_buffer_rsrc_t rsE =
+      __builtin_amdgcn_make_buffer_rsrc((void*)E, (short)0, (int)((int64_t)K * VQ_D * 4), 0x00020000);
+  const int s_code = tid >> 3, s_part = tid & 7;
+  const unsigned s_off = (unsigned)(s_code * 512 + s_part * 64);
+  f32x4_t stage[VQ_STAGE];
+  auto load_step = [&](int st) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int j = 0; j < VQ_STAGE; ++j) {
+      const f4v v = __builtin_amdgcn_raw_buffer_load_b128(rsE, (int)(s_off + 16 * j), st * VQ_STEP_BYTES, 0);
+      stage[j] = f32x4_t{v[0], v[1], v[2], v[3]};
+    }
+  };
+  auto lds_at = [&](int code, int ch) { return smem + code * 512 + 16 * (ch ^ (code & 15)); };
+  char* s_dst[VQ_STAGE];
+#pragma unroll
+  for (int j = 0; j < VQ_STAGE; ++j) s_dst[j] = lds_at(s_code, 4 * s_part + j);
+
+  load_step(0);  // the first codebook step and z travel together
+
+  // z fragments: zf[kb] = z[my_row][16kb + 4q .. +3] (rows >= N read as zeros
+  // through a descriptor that starts at this workgroup's first frame)
   f32x4_t zf[8];
   float zz = 0.f;
+  const int64_t wg_row0 = (int64_t)blockIdx.x * VQ_FRAMES;
+  int64_t z_rec = (N - wg_row0) * VQ_D * 4;
+  if (z_rec > VQ_FRAMES * VQ_D * 4) z_rec = VQ_FRAMES * VQ_D * 4;
+  const __amdgpu_buffer_rsrc_t rsZ =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(z + wg_row0 * VQ_D), (short)0, (int)z_rec, 0x00020000);
+  const unsigned z_off = (unsigned)((fg * 16 + j16) * 512 + 16 * q);
 #pragma unroll
   for (int kb = 0; kb < 8; ++kb) {
-    f32x4_t v = {0.f, 0.f, 0.f, 0.f};
-    if (row_ok) v = *(const f32x4_t*)(z + my_row * VQ_D + 16 * kb + 4 * q);
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v u = __builtin_amdgcn_raw_buffer_load_b128(rsZ, (int)(z_off + 64 * kb), 0, 0);
+    const f32x4_t v = {u[0], u[1], u[2], u[3]};
     zf[kb] = v;
     zz = fmaf(v[0], v[0], zz);
     zz = fmaf(v[1], v[1], zz);
@@ -62,93 +138,69 @@ __global__ __launch_bounds__(256) void vq_forward_kernel(const float* __restrict
 #pragma unroll
   for (int r = 0; r < 4; ++r) { best_d[r] = INFINITY; best_i[r] = 0x7fffffff; }
 
-  const int ntiles = (K + VQ_TILE - 1) / VQ_TILE;
-  f32x4_t stage[8];
-  auto load_tile = [&](int t) {
+  const int cbase = cs * VQ_SUB;  // this wave's codes inside a step
+  for (int st = 0; st < nsteps; ++st) {
+    if (st > 0) __syncthreads();  // every wave is done with the previous step's codes
+    float e2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int c = tid + 256 * i;        // chunk id in tile: code c>>5, chunk c&31
-      const int code = t * VQ_TILE + (c >> 5);
-      f32x4_t v = {0.f, 0.f, 0.f, 0.f};
-      if (code < K) v = *(const f32x4_t*)(E + (int64_t)code * VQ_D + 4 * (c & 31));
-      stage[i] = v;
+    for (int j = 0; j < VQ_STAGE; ++j) {
+      *(f32x4_t*)s_dst[j] = stage[j];
+      e2 = fmaf(stage[j][0], stage[j][0], e2);
+      e2 = fmaf(stage[j][1], stage[j][1], e2);
+      e2 = fmaf(stage[j][2], stage[j][2], e2);
+      e2 = fmaf(stage[j][3], stage[j][3], e2);
     }
-  };
-  auto store_tile = [&](int buf) {
-    char* base = smem + buf * VQ_TILE_BYTES;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int c = tid + 256 * i;
-      const int code = c >> 5, ch = c & 31;
-      *(f32x4_t*)(base + code * 512 + 16 * (ch ^ (code & 15))) = stage[i];
-    }
-  };
-  auto ee_tile = [&](int buf, int t) {
-    // 4 threads per code, 32 elements each, read back from LDS
-    const char* base = smem + buf * VQ_TILE_BYTES;
-    const int code = tid >> 2, part = tid & 3;
-    float s = 0.f;
-#pragma unroll
-    for (int cc = 0; cc < 8; ++cc) {
-      const int ch = part * 8 + cc;
-      f32x4_t v = *(const f32x4_t*)(base + code * 512 + 16 * (ch ^ (code & 15)));
-      s = fmaf(v[0], v[0], s); s = fmaf(v[1], v[1], s); s = fmaf(v[2], v[2], s); s = fmaf(v[3], v[3], s);
-    }
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    if (part == 0) ee_lds[buf][code] = s;
-    (void)t;
-  };
-
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
-  ee_tile(0, 0);
-  __syncthreads();
-
-  for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
-    const bool more = (t + 1) < ntiles;
-    if (more) load_tile(t + 1);
-    const char* base = smem + buf * VQ_TILE_BYTES;
-#pragma unroll
-    for (int cb = 0; cb < VQ_TILE / 16; cb += 2) {
-      f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-      const int c0 = cb * 16 + j16, c1 = c0 + 16;
-#pragma unroll
-      for (int kb = 0; kb < 8; ++kb) {
-        const int ch = 4 * kb + q;
-        f32x4_t b0 = *(const f32x4_t*)(base + c0 * 512 + 16 * (ch ^ (c0 & 15)));
-        f32x4_t b1 = *(const f32x4_t*)(base + c1 * 512 + 16 * (ch ^ (c1 & 15)));
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(zf[kb][m], b0[m], acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(zf[kb][m], b1[m], acc1, 0, 0, 0);
-        }
-      }
-      const int code0 = t * VQ_TILE + c0, code1 = code0 + 16;
-      const float e0 = ee_lds[buf][c0], e1 = ee_lds[buf][c1];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (code0 < K) {
-          const float d0 = __fsub_rn(__fadd_rn(zz_r[r], e0), __fmul_rn(2.f, acc0[r]));
-          if (d0 < best_d[r]) { best_d[r] = d0; best_i[r] = code0; }
-        }
-        if (code1 < K) {
-          const float d1 = __fsub_rn(__fadd_rn(zz_r[r], e1), __fmul_rn(2.f, acc1[r]));
-          if (d1 < best_d[r]) { best_d[r] = d1; best_i[r] = code1; }
-        }
-      }
-    }
-    if (more) {
-      store_tile(buf ^ 1);
-      __syncthreads();
-      ee_tile(buf ^ 1, t + 1);
-    }
+    e2 += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, e2), 0xB1, 0xF, 0xF, false));
+    e2 += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, e2), 0x4E, 0xF, 0xF, false));
+    e2 += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, e2), 0x141, 0xF, 0xF, false));
+    if (s_part == 0) eeL[s_code] = e2;
     __syncthreads();
+    if (st + 1 < nsteps) load_step(st + 1);  // next step's codes land during this step's MFMAs
+    constexpr int NB = VQ_SUB / 16;
+    // two independent accumulator chains per code block (even / odd 16-dim
+    // blocks, added at the end): the 40-cycle dependent-MFMA latency hides
+    // under the other chain's 32-cycle issue within the wave
+    float eb[NB];
+    f32x4_t acc[NB], acc2[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      eb[b] = eeL[cbase + 16 * b + j16];
+      acc[b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      acc2[b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int kb = 0; kb < 8; kb += 2) {
+      f32x4_t bf[NB], bg[NB];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        bf[b] = *(const f32x4_t*)lds_at(cbase + 16 * b + j16, 4 * kb + q);
+        bg[b] = *(const f32x4_t*)lds_at(cbase + 16 * b + j16, 4 * kb + 4 + q);
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          acc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(zf[kb][m], bf[b][m], acc[b], 0, 0, 0);
+          acc2[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(zf[kb + 1][m], bg[b][m], acc2[b], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[b] += acc2[b];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int code = st * VQ_STEP + cbase + 16 * b + j16;
+      if (code < K) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          // codes ascend within a lane, so strict '<' keeps the first minimum
+          const float d = __fsub_rn(__fadd_rn(zz_r[r], eb[b]), __fmul_rn(2.f, acc[b][r]));
+          if (d < best_d[r]) { best_d[r] = d; best_i[r] = code; }
+        }
+      }
+    }
   }
 
-  // argmin across the 16 lanes of each row group (lowest index on ties)
+  // argmin across the 16 code lanes of each row (lowest index on ties)
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
 #pragma unroll
@@ -158,97 +210,140 @@ __global__ __launch_bounds__(256) void vq_forward_kernel(const float* __restrict
       if (od < best_d[r] || (od == best_d[r] && oi < best_i[r])) { best_d[r] = od; best_i[r] = oi; }
     }
   }
-  // NaN rows (all comparisons false) fall back to code 0 like torch.argmin's
-  // first-element seed would not; keep them well-defined.
-  // idx of this lane's A-row j16: held by group j16>>2, register j16&3.
-  int my_idx = 0;
+  // ... and across the code splits: (distance, index) minima through LDS, merged
+  // in ascending split order with the same comparison = torch.argmin's first minimum
+  __syncthreads();  // the last step's codes are no longer read
+  float* md = (float*)smem;                       // [VQ_FG][VQ_CS][16]
+  int* mi = (int*)(smem + VQ_FG * VQ_CS * 16 * 4);
+  if (j16 == 0) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int v = __shfl(best_i[r], 16 * (j16 >> 2), 64);
-    if ((j16 & 3) == r) my_idx = v;
+    for (int r = 0; r < 4; ++r) {
+      md[(fg * VQ_CS + cs) * 16 + 4 * q + r] = best_d[r];
+      mi[(fg * VQ_CS + cs) * 16 + 4 * q + r] = best_i[r];
+    }
   }
-  if (my_idx >= K || my_idx < 0) my_idx = 0;
-
+  __syncthreads();
   float sq = 0.f;
-  if (row_ok) {
-    if (q == 0) idx_out[my_row] = my_idx;
+  if (cs == 0) {  // the frame group's epilogue (every split wave holds the same z)
+    float bd = md[fg * VQ_CS * 16 + j16];
+    int bi = mi[fg * VQ_CS * 16 + j16];
 #pragma unroll
-    for (int kb = 0; kb < 8; ++kb) {
-      const int d0 = 16 * kb + 4 * q;
-      const f32x4_t e = *(const f32x4_t*)(E + (int64_t)my_idx * VQ_D + d0);
-      if (zq) *(f32x4_t*)(zq + my_row * VQ_D + d0) = e;
-      if (zq_c) {
-        if (zq_dt == VQX_BF16) {
-          bf16_t* o = (bf16_t*)zq_c + my_row * VQ_D + d0;
-          uint2 pk;
-          pk.x = pack_bf16x2(e[0], e[1]);
-          pk.y = pack_bf16x2(e[2], e[3]);
-          *(uint2*)o = pk;
-        } else {
-          *(f32x4_t*)((float*)zq_c + my_row * VQ_D + d0) = e;
+    for (int c = 1; c < VQ_CS; ++c) {
+      const float od = md[(fg * VQ_CS + c) * 16 + j16];
+      const int oi = mi[(fg * VQ_CS + c) * 16 + j16];
+      if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; }
+    }
+    // NaN rows (every comparison false) keep a well-defined index
+    const int my_idx = (bi >= K || bi < 0) ? 0 : bi;
+    if ((VQX_VQ_LAB & 2) && row_ok && q == 0) idx_out[my_row] = my_idx;
+    if (row_ok && !(VQX_VQ_LAB & 2)) {
+      if (q == 0) idx_out[my_row] = my_idx;
+#pragma unroll
+      for (int kb = 0; kb < 8; ++kb) {
+        const int d0 = 16 * kb + 4 * q;
+        const f32x4_t e = *(const f32x4_t*)(E + (int64_t)my_idx * VQ_D + d0);
+        if (zq) *(f32x4_t*)(zq + my_row * VQ_D + d0) = e;
+        if (zq_c) {
+          if (zq_dt == VQX_BF16) {
+            bf16_t* o = (bf16_t*)zq_c + my_row * VQ_D + d0;
+            uint2 pk;
+            pk.x = pack_bf16x2(e[0], e[1]);
+            pk.y = pack_bf16x2(e[2], e[3]);
+            *(uint2*)o = pk;
+          } else {
+            *(f32x4_t*)((float*)zq_c + my_row * VQ_D + d0) = e;
+          }
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const float df = __fsub_rn(e[m], zf[kb][m]);
+          sq = fmaf(df, df, sq);
         }
       }
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const float df = __fsub_rn(e[m], zf[kb][m]);
-        sq = fmaf(df, df, sq);
-      }
-    }
-  }
-
-  // ---- EMA statistics: per-code sums of z over this workgroup's 64 frames.
-  // Sort the (code, frame) pairs with a wave-wide bitonic network, then each
-  // thread walks a run of the sorted frames for one dimension d and flushes a
-  // partial sum per code segment: one contiguous 256-B atomic wave-instruction
-  // per (segment, 64 dims) instead of one scattered atomic per element, and no
-  // same-address pile-up when the codebook usage is concentrated.
-  if (bsum) {
-    float* zl = (float*)smem;                       // [64][128] frame block (tile buffers are free now)
-    int* codes = (int*)(smem + 64 * VQ_D * 4);      // [64] code per local frame (K = invalid)
-    int* order = codes + 64;                        // [64] frames sorted by code
-#pragma unroll
-    for (int kb = 0; kb < 8; ++kb) *(f32x4_t*)(zl + (w * 16 + j16) * VQ_D + 16 * kb + 4 * q) = zf[kb];
-    if (q == 0) codes[w * 16 + j16] = row_ok ? my_idx : K;
-    __syncthreads();
-    if (w == 0) {
-      int key = codes[lane] * 64 + lane;
-#pragma unroll
-      for (int k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-          const int other = __shfl_xor(key, j, 64);
-          const bool up = (lane & k) == 0, lower = (lane & j) == 0;
-          key = (lower == up) ? min(key, other) : max(key, other);
-        }
-      }
-      order[lane] = key & 63;
-    }
-    __syncthreads();
-    const int d = tid & 127, half = tid >> 7;
-    int cur = -1, cnt = 0;
-    float acc = 0.f;
-    for (int p = 32 * half; p < 32 * half + 32; ++p) {
-      const int r = order[p];
-      const int c = codes[r];
-      if (c != cur) {
-        if (cur >= 0 && cur < K) {
-          atomicAdd(bsum + (int64_t)cur * VQ_D + d, acc);
-          if (d == 0 && bcnt) atomicAdd(bcnt + cur, (float)cnt);
-        }
-        cur = c;
-        acc = 0.f;
-        cnt = 0;
-      }
-      acc += zl[r * VQ_D + d];
-      ++cnt;
-    }
-    if (cur >= 0 && cur < K) {
-      atomicAdd(bsum + (int64_t)cur * VQ_D + d, acc);
-      if (d == 0 && bcnt) atomicAdd(bcnt + cur, (float)cnt);
     }
   }
   const float tot = block_sum(sq, red);
   if (tid == 0) partials[blockIdx.x] = tot;
+}
+
+// EMA statistics (update_emb, layers_vq.py:207-211: onehot(idx) @ z and the
+// code counts), as a dense per-chunk reduction instead of scattered global
+// atomics: workgroup (chunk c, dim slice y) accumulates its frames' z[:, slice]
+// into an LDS table [K][DSL] (ds_add_f32) and the code counts, then writes
+// the whole table to its slab.  Every z element is read once.
+template <int DSL>
+__global__ __launch_bounds__(256) void vq_stats_kernel(const float* __restrict__ z, int64_t N,
+                                                       const int64_t* __restrict__ idx, int K, int64_t frames_per_chunk,
+                                                       float* __restrict__ slab, float* __restrict__ cnt_slab) {
+  extern __shared__ __attribute__((aligned(16))) float acc[];  // [K][DSL] + int counts [K]
+  int* cnt = (int*)(acc + K * DSL);
+  const int tid = threadIdx.x;
+  const int c = blockIdx.x, d0 = blockIdx.y * DSL;
+  const bool counts = blockIdx.y == 0;
+  for (int i = tid; i < K * DSL; i += 256) acc[i] = 0.f;
+  if (counts)
+    for (int i = tid; i < K; i += 256) cnt[i] = 0;
+  __syncthreads();
+  const int64_t n0 = (int64_t)c * frames_per_chunk;
+  const int64_t n1 = n0 + frames_per_chunk < N ? n0 + frames_per_chunk : N;
+  constexpr int TPF = DSL / 4;   // threads per frame (4 dims each, one 16-B load)
+  constexpr int P = 256 / TPF;   // frames per pass
+  constexpr int U = 8;           // passes whose loads are in flight together
+  const int d = 4 * (tid % TPF);
+  for (int64_t nb = n0 + tid / TPF; nb < n1; nb += (int64_t)P * U) {
+    int k[U];
+    f32x4_t v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t n = nb + (int64_t)u * P;
+      k[u] = n < n1 ? (int)idx[n] : -1;
+      v[u] = n < n1 ? *(const f32x4_t*)(z + n * VQ_D + d0 + d) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (k[u] < 0 || k[u] >= K) continue;
+      float* a = &acc[k[u] * DSL + d];
+      atomicAdd(a, v[u][0]);
+      atomicAdd(a + 1, v[u][1]);
+      atomicAdd(a + 2, v[u][2]);
+      atomicAdd(a + 3, v[u][3]);
+      if (counts && d == 0) atomicAdd(&cnt[k[u]], 1);
+    }
+  }
+  __syncthreads();
+  float* out = slab + (int64_t)c * K * VQ_D + d0;
+  for (int i = tid; i < K * DSL; i += 256) out[(int64_t)(i / DSL) * VQ_D + (i % DSL)] = acc[i];
+  if (counts)
+    for (int i = tid; i < K; i += 256) cnt_slab[(int64_t)c * K + i] = (float)cnt[i];
+}
+
+// bsum[i] += sum_c slab[c][i], bcnt[k] += sum_c cnt_slab[c][k], chunks in
+// order (4 elements per thread; the chunk loads are independent).
+__global__ __launch_bounds__(256) void vq_stats_reduce_kernel(const float* __restrict__ slab,
+                                                              const float* __restrict__ cnt_slab, int chunks, int K,
+                                                              float* __restrict__ bsum, float* __restrict__ bcnt) {
+  const int64_t total = (int64_t)K * VQ_D;
+  const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i4 < total) {
+    f32x4_t s = {0.f, 0.f, 0.f, 0.f};
+    int c = 0;
+    for (; c + 4 <= chunks; c += 4) {
+      f32x4_t v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *(const f32x4_t*)(slab + (int64_t)(c + u) * total + i4);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s += v[u];
+    }
+    for (; c < chunks; ++c) s += *(const f32x4_t*)(slab + (int64_t)c * total + i4);
+    f32x4_t o = *(f32x4_t*)(bsum + i4);
+    *(f32x4_t*)(bsum + i4) = o + s;
+  }
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (bcnt && k < K) {
+    float s = 0.f;
+    for (int c = 0; c < chunks; ++c) s += cnt_slab[(int64_t)c * K + k];
+    bcnt[k] += s;
+  }
 }
 
 // Deterministic single-workgroup sum of n partials into out[0] (optionally scaled).
@@ -352,18 +447,51 @@ __global__ void commit_bwd_kernel(const float* __restrict__ z, const float* __re
 
 using namespace vqx;
 
+extern "C" int vqx_vq_workspace(int64_t n_rows, int32_t K, int32_t with_stats, int64_t* floats) {
+  if (n_rows <= 0 || K <= 0 || !floats) { set_error("vqx_vq_workspace: bad arguments"); return -1; }
+  *floats = vq_workspace_floats(n_rows, K, with_stats != 0);
+  return 0;
+}
+
+template <int DSL>
+static void launch_vq_stats(const float* z, int64_t N, const int64_t* idx, int K, float* ws, float* bsum, float* bcnt,
+                            hipStream_t s) {
+  const int chunks = vq_stats_chunks(N, K);
+  const int64_t fpc = (N + chunks - 1) / chunks;
+  float* slab = ws + ((vq_partials_floats(N) + 63) & ~(int64_t)63);
+  float* cnt_slab = slab + (int64_t)chunks * K * VQ_D;
+  const size_t lds = (size_t)K * DSL * 4 + (size_t)K * 4;
+  hipLaunchKernelGGL(vq_stats_kernel<DSL>, dim3(chunks, VQ_D / DSL), dim3(256), lds, s, z, N, idx, K, fpc, slab,
+                     cnt_slab);
+  const int64_t total4 = (int64_t)K * VQ_D / 4;
+  hipLaunchKernelGGL(vq_stats_reduce_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, s, slab, cnt_slab,
+                     chunks, K, bsum, bcnt);
+}
+
 extern "C" int vqx_vq_forward(const float* z, int64_t n_rows, int32_t D, const float* E, int32_t K, int64_t* idx,
                               float* zq, void* zq_c, int32_t zq_c_dtype, float* sqerr_out, float* partials,
                               float* bsum, float* bcnt, vqx_stream_t stream) {
   if (D != VQ_D) { set_error("vqx_vq_forward: only D=128 supported (got %d)", D); return -1; }
   if (K <= 0 || K % 16) { set_error("vqx_vq_forward: K=%d must be a positive multiple of 16", K); return -1; }
+  if (K > 3264) { set_error("vqx_vq_forward: K=%d > 3264", K); return -1; }
   if (n_rows <= 0 || !z || !E || !idx || !partials) { set_error("vqx_vq_forward: bad arguments"); return -1; }
+  if (bcnt && !bsum) { set_error("vqx_vq_forward: bcnt needs bsum"); return -1; }
   if (((uintptr_t)z | (uintptr_t)E) & 15) { set_error("vqx_vq_forward: z/E must be 16-byte aligned"); return -1; }
   hipStream_t s = (hipStream_t)stream;
-  const int grid = (int)((n_rows + 63) / 64);
-  hipLaunchKernelGGL(vq_forward_kernel, dim3(grid), dim3(256), 0, s, z, n_rows, E, K, idx, zq, zq_c, zq_c_dtype,
-                     partials, bsum, bcnt);
+  const int grid = (int)vq_partials_floats(n_rows);
+  hipLaunchKernelGGL(vq_forward_kernel, dim3(grid), dim3(VQ_THREADS), 0, s, z, n_rows, E, K, idx, zq, zq_c,
+                     zq_c_dtype, partials);
   if (sqerr_out) hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(1024), 0, s, partials, grid, 1.0f, sqerr_out);
+  if (bsum) {
+    switch (vq_stats_dsl(K)) {
+      case 128: launch_vq_stats<128>(z, n_rows, idx, K, partials, bsum, bcnt, s); break;
+      case 64: launch_vq_stats<64>(z, n_rows, idx, K, partials, bsum, bcnt, s); break;
+      case 32: launch_vq_stats<32>(z, n_rows, idx, K, partials, bsum, bcnt, s); break;
+      case 16: launch_vq_stats<16>(z, n_rows, idx, K, partials, bsum, bcnt, s); break;
+      case 8: launch_vq_stats<8>(z, n_rows, idx, K, partials, bsum, bcnt, s); break;
+      default: launch_vq_stats<4>(z, n_rows, idx, K, partials, bsum, bcnt, s); break;
+    }
+  }
   return launch_status("vqx_vq_forward");
 }
 

@@ -91,7 +91,7 @@ class Workspace:
             self.embn = e(K, Z, dt=F32)
             self.e_len = e(K, dt=F32)
             self.pv_part = e(N // 4 + 8, dt=F32)
-        self.vq_part = e((N + 63) // 64, dt=F32)
+        self.vq_part = e(ops.vq_workspace(N, K, True), dt=F32)  # VQ partials + EMA-statistics slabs
         # EMA statistics bundle (all-reduced as one buffer in data parallel)
         self.ema = e(K * D + K + K * D, dt=F32)
         self.bsum = self.ema[: K * D].view(K, D)

@@ -52,8 +52,7 @@ class EMAVectorQuantizer(nn.Module):
             zf = z.reshape(-1, D).float().contiguous()
         n = zf.shape[0]
         idx = torch.empty(n, dtype=torch.int64, device=z.device)
-        part = torch.empty((n + 63) // 64, device=z.device)
-        ops.vq_forward(zf, self.embeddings.contiguous(), idx, None, None, None, part)
+        ops.vq_forward(zf, self.embeddings.contiguous(), idx, None, None, None)
         return idx.view(B, T)
 
     def decode(self, z_id, time_last=True):
@@ -122,8 +121,7 @@ class VectorQuantizer(nn.Module):
                              torch.empty(n // 4 + 2, device=z.device))
             zf = zn
         idx = torch.empty(n, dtype=torch.int64, device=z.device)
-        part = torch.empty((n + 63) // 64, device=z.device)
-        ops.vq_forward(zf, emb, idx, None, None, None, part)
+        ops.vq_forward(zf, emb, idx, None, None, None)
         return idx.view(B, T)
 
     def decode(self, z_id, time_last=True):

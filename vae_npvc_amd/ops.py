@@ -309,8 +309,21 @@ def logloss_fwd_bwd(x_nct, xhat, grad_scale, dxhat, loss_out, partials):
     return loss_out
 
 
-def vq_forward(z, E, idx, zq, zq_c, sqerr, partials, bsum=None, bcnt=None):
+def vq_workspace(n_rows, K, stats):
+    """Floats of workspace vqx_vq_forward needs (with or without EMA statistics)."""
+    out = ctypes.c_int64()
+    call("vqx_vq_workspace", int(n_rows), int(K), int(bool(stats)), ctypes.byref(out))
+    return out.value
+
+
+def vq_forward(z, E, idx, zq, zq_c, sqerr, partials=None, bsum=None, bcnt=None):
+    """partials: f32 workspace of >= vq_workspace(N, K, bsum is not None) floats (allocated if None)."""
     N, D = z.shape
+    need = vq_workspace(N, E.shape[0], bsum is not None)
+    if partials is None:
+        partials = torch.empty(need, device=z.device, dtype=torch.float32)
+    if partials.numel() < need:
+        raise ValueError(f"vq_forward: workspace {partials.numel()} < {need} floats")
     call("vqx_vq_forward", ptr(z), N, D, ptr(E), E.shape[0], ptr(idx), ptr(zq), ptr(zq_c),
          dt_code(zq_c.dtype) if zq_c is not None else 0, ptr(sqerr), ptr(partials), ptr(bsum), ptr(bcnt),
          stream_ptr())
