@@ -73,8 +73,8 @@ enum {
 
 /*
  * Stride-1 Conv1d / ConvTranspose1d as an implicit-im2col GEMM on MFMA.
- *   fwd  : y[n][co] = epi( sum_{j,ci} w[co][j*cin+ci] * pro(x[n+j-pad][ci]) )
- *          rows n+j-pad outside the utterance of n read as zero (padding).
+ *   fwd  : y[n][co] = epi( sum_{j,ci} w[co][j*cin+ci] * pro(x[n+j*dil-pad][ci]) )
+ *          rows n+j*dil-pad outside the utterance of n read as zero (padding).
  *   dgrad: the same args with x = dy [N][cin], w = the FORWARD layer's packed
  *          weight [cout][ntaps*cin_fwd]; computes
  *          dx[n][ci] = epi( sum_{j,c} w[c][(ntaps-1-j)*cout_total.. ] ... )
@@ -116,6 +116,10 @@ typedef struct vqx_conv_args {
    * gn_mean_rstd [B][2]; needs T % 128 == 0 and cout % 128 == 0. */
   const float* gn_stat_tiles;
   float gn_eps;
+  int32_t dil;               /* tap spacing (dilation, vqvae.py:166,274); 0 or 1 = dense.
+                                Taps sit at n + j*dil - pad; 1 <= ntaps <= 8 and
+                                0 <= pad <= (ntaps-1)*dil.  DGRAD takes the forward
+                                layer's ntaps/dil and pad' = (ntaps-1)*dil - pad    */
 } vqx_conv_args;
 
 int vqx_conv1d_fwd(const vqx_conv_args* a, vqx_stream_t stream);
@@ -123,7 +127,7 @@ int vqx_conv1d_dgrad(const vqx_conv_args* a, vqx_stream_t stream);
 
 /*
  * Weight gradient of a stride-1 conv as split-K partial slabs:
- *   slabs[s][r][j*c_dim + c] = sum_{n in split s} p[n][r] * pro(q[n + sign*(j-pad)][c])
+ *   slabs[s][r][j*c_dim + c] = sum_{n in split s} p[n][r] * pro(q[n + sign*(j*dil-pad)][c])
  * Conv1d  (dW[co][ci][j]): p = dy, q = x,  sign = +1.
  * ConvT1d (dW[ci][co][k-1-j]): p = x, q = du, sign = -1.
  * vqx_weight_norm_bwd reduces the slabs.  Reference: autograd of the convs
@@ -137,6 +141,7 @@ typedef struct vqx_wgrad_args {
   int32_t T, r_dim, c_dim, ntaps, pad, shift_sign, ldp, ldq;
   int32_t dtype, q_prologue, splits;
   float pro_scale;
+  int32_t dil;       /* taps at n + sign*(j*dil - pad); 0 or 1 = dense */
 } vqx_wgrad_args;
 
 int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream);
@@ -434,7 +439,7 @@ int vqx_convert_2d(const void* src, int32_t ld_src, int32_t src_dtype, void* dst
  * per tile, two 4-wave K groups per tile), the rest one group per 128 x 128
  * tile.  Callers size `splits` (and the slab buffer) from it. */
 int vqx_wgrad_tiles(int64_t n_rows, int32_t T, int32_t r_dim, int32_t c_dim, int32_t ntaps, int32_t pad,
-                    int32_t dtype, int32_t q_prologue, int32_t* tiles);
+                    int32_t dil, int32_t dtype, int32_t q_prologue, int32_t* tiles);
 
 /* Thread-local description of the last failure. */
 const char* vqx_last_error(void);
@@ -457,7 +462,7 @@ int vqx_probe_count(int64_t* n);
 int vqx_probe_read(int64_t i, int32_t* info5, double* flops, float* ms);
 
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
-#define VQX_ABI_VERSION 115
+#define VQX_ABI_VERSION 116
 int vqx_version(void);
 
 #ifdef __cplusplus

@@ -10,10 +10,11 @@ Pinned against golden vectors produced by importing the reference itself in
 the survey container (tests/golden/make_golden.py -> tests/golden/*.npz);
 tests/test_oracle_golden.py checks this restatement against them.
 
-Scope: the single-stage Encoder/Decoder of
-egs/vcc20/vae1/conf/train_pytorch_vqvae.yaml and
-egs/aishell3/vc2/conf/train_pytorch_vqvae.yaml (one resolution stage, k=3,
-stack_layers 1, no dilation), EMAVectorQuantizer (use_ema: true) and the
+Scope: the Encoder/Decoder of vqvae.py in
+any topology the constructor accepts -- the single-stage recipes
+(egs/vcc20/vae1, egs/aishell3/vc2) and the constructor defaults: several
+resolution stages with strided down-/up-sampling convs, dilation 2**j,
+stack_layers > 1, decoder kernel_size 5 -- EMAVectorQuantizer (use_ema: true) and the
 straight-through VectorQuantizer (use_ema: false, embed_norm on/off), Jitter,
 log_loss and Trainer.train_step (Adam, clip_grad_norm_, StepLR).  Every function cites the
 reference file:line it restates (paths relative to the reference root).
@@ -29,22 +30,70 @@ LOG_2PI = math.log(2.0 * math.pi)  # vae_npvc/model/layers.py:8
 
 
 # ----------------------------------------------------------------- structure
+def encoder_plan(enc):
+    """Encoder.__init__ (vqvae.py:123-183): per resolution stage a conv
+    (kernel_size, or kernel 2s / stride s / padding s//2 + s%2 when the stage
+    down-samples by s, :146-157), `stacks` Conv1d_Layernorm_LRelu_Residual
+    blocks with dilation 2**j (`dilation: true`) and `stack_layers` convs each
+    (layers.py:129-165), a LeakyReLU; then the 1x1 conv to z_channels.
+    Returns (stages, final): stage = dict(idx, cin, cout, k, stride, pad,
+    blocks=[dict(idx, dil)]); indices are positions in the nn.Sequential."""
+    k0 = enc.get("kernel_size", 3)
+    ks = enc.get("stack_kernel_size", 3)
+    L = enc.get("stack_layers", 2)
+    dil_on = enc.get("dilation", True)
+    assert not enc.get("use_causal_conv", False) and (ks - 1) % 2 == 0
+    stages, idx = [], 0
+    for cin, cout, ds, nst in zip(enc["in_channels"], enc["out_channels"], enc.get("downsample_scales", [1] * 4),
+                                  enc["stacks"]):
+        if ds == 1:
+            k, stride, pad = k0, 1, (k0 - 1) // 2
+        else:
+            k, stride, pad = 2 * ds, ds, ds // 2 + ds % 2
+        st = dict(idx=idx, cin=cin, cout=cout, k=k, stride=stride, pad=pad, blocks=[], ks=ks, L=L)
+        idx += 1
+        for j in range(nst):
+            st["blocks"].append(dict(idx=idx, dil=2 ** j if dil_on else 1))
+            idx += 1
+        idx += 1  # the stage's LeakyReLU
+        stages.append(st)
+    return stages, idx
+
+
+def decoder_plan(dec):
+    """Decoder.__init__ (vqvae.py:221-296): per stage a ConvTranspose1d
+    (kernel_size, padding (k-1)//2; or kernel 2s / stride s / padding
+    s//2 + s%2 / output_padding s%2 when the stage up-samples, :245-265) and
+    `stacks` DeConv1d_Layernorm_GLU_ResSkip blocks with dilation 2**j
+    (layers.py:181-215); positions are indices into the ModuleList."""
+    k0 = dec.get("kernel_size", 5)
+    ks = dec.get("stack_kernel_size", 3)
+    dil_on = dec.get("dilation", True)
+    assert not dec.get("use_causal_conv", False) and (ks - 1) % 2 == 0
+    stages, idx = [], 0
+    for cin, cout, us, nst in zip(dec["in_channels"], dec["out_channels"], dec.get("upsample_scales", [1] * 4),
+                                  dec["stacks"]):
+        if us == 1:
+            k, stride, pad, opad = k0, 1, (k0 - 1) // 2, 0
+        else:
+            k, stride, pad, opad = 2 * us, us, us // 2 + us % 2, us % 2
+        st = dict(idx=idx, cin=cin, cout=cout, k=k, stride=stride, pad=pad, opad=opad, blocks=[], ks=ks)
+        idx += 1
+        for j in range(nst):
+            st["blocks"].append(dict(idx=idx, dil=2 ** j if dil_on else 1))
+            idx += 1
+        stages.append(st)
+    return stages, idx
+
+
 def layer_specs(cfg):
     """Ordered parameter spec [(name, shape)] of vae_npvc.model.vqvae.Model in
     registration order (== model.parameters() order; vqvae.py:15-40,
     layers.py:139-165,191-215; weight_norm registers weight_g/weight_v after
-    bias).  Only the single-stage architecture of the baseline YAMLs."""
+    bias), for any Encoder/Decoder topology of vqvae.py."""
     enc, dec = cfg["encoder"], cfg["decoder"]
-    assert len(enc["in_channels"]) == 1 and enc.get("stack_layers", 2) == 1 and not enc.get("dilation", True)
-    assert len(dec["in_channels"]) == 1 and not dec.get("dilation", True)
-    assert enc.get("kernel_size", 3) == 3 and enc.get("stack_kernel_size", 3) == 3
-    assert dec.get("kernel_size", 5) == 3 and dec.get("stack_kernel_size", 3) == 3
-    mel, C = enc["in_channels"][0], enc["out_channels"][0]
     Z = enc.get("z_channels", 128)
-    ns = enc["stacks"][0]
-    Cd = dec["out_channels"][0]
     cond, skip, fin = dec["cond_channels"], dec["skip_channels"], dec["final_channels"]
-    nd = dec["stacks"][0]
     spec = []
 
     def conv(name, cin, cout, k, transposed=False):
@@ -58,18 +107,26 @@ def layer_specs(cfg):
         spec.append((name + ".weight", (c,)))
         spec.append((name + ".bias", (c,)))
 
-    conv("encoder.encode.0", mel, C, 3)
-    for i in range(1, ns + 1):
-        conv(f"encoder.encode.{i}.stack.1", C, C, 3)
-        gn(f"encoder.encode.{i}.stack.2", C)
-        conv(f"encoder.encode.{i}.skip_layer", C, C, 1)
-    conv(f"encoder.encode.{ns + 2}", C, Z, 1)
-    conv("decoder.layers.0", dec["in_channels"][0], Cd, 3, transposed=True)
-    for i in range(1, nd + 1):
-        conv(f"decoder.layers.{i}.conv_in", Cd, 2 * Cd, 3, transposed=True)
-        gn(f"decoder.layers.{i}.norm_layer", 2 * Cd)
-        conv(f"decoder.layers.{i}.conv_cond", cond, 2 * Cd, 1)
-        conv(f"decoder.layers.{i}.res_skip_layers", Cd, Cd + skip, 1)
+    stages, fidx = encoder_plan(enc)
+    for st in stages:
+        C = st["cout"]
+        conv(f"encoder.encode.{st['idx']}", st["cin"], C, st["k"])
+        for b in st["blocks"]:
+            pre = f"encoder.encode.{b['idx']}"
+            for l in range(st["L"]):
+                conv(f"{pre}.stack.{3 * l + 1}", C, C, st["ks"])
+                gn(f"{pre}.stack.{3 * l + 2}", C)
+            conv(f"{pre}.skip_layer", C, C, 1)
+    conv(f"encoder.encode.{fidx}", enc["out_channels"][-1], Z, 1)
+    for st in decoder_plan(dec)[0]:
+        C = st["cout"]
+        conv(f"decoder.layers.{st['idx']}", st["cin"], C, st["k"], transposed=True)
+        for b in st["blocks"]:
+            pre = f"decoder.layers.{b['idx']}"
+            conv(f"{pre}.conv_in", C, 2 * C, st["ks"], transposed=True)
+            gn(f"{pre}.norm_layer", 2 * C)
+            conv(f"{pre}.conv_cond", cond, 2 * C, 1)
+            conv(f"{pre}.res_skip_layers", C, C + skip, 1)
     conv("decoder.final_layer.1", skip, skip, 1)
     conv("decoder.final_layer.3", skip, fin, 1)
     if not cfg.get("use_ema", False):  # VectorQuantizer's codebook is a parameter (layers_vq.py:18)
@@ -84,6 +141,11 @@ def buffer_specs(cfg):
         return []
     return [("quantizer.emb_init", ()), ("quantizer.emb_sum", (K, D)), ("quantizer.emb_elem", (K,)),
             ("quantizer.embeddings", (K, D))]
+
+
+def _is_gn(name):  # GroupNorm affine parameters: stack.{2,5,8,..} and norm_layer
+    parts = name.split(".")
+    return "norm_layer" in parts or ("stack" in parts and int(parts[parts.index("stack") + 1]) % 3 == 2)
 
 
 def seeded_state_dict(cfg, seed):
@@ -104,9 +166,9 @@ def seeded_state_dict(cfg, seed):
             sd[name[:-1] + "g"] = torch.from_numpy((norm * g.numpy().reshape(-1)).reshape(g.shape).astype(np.float32))
         elif name.endswith(".weight_g"):
             sd[name] = torch.from_numpy(rng.uniform(0.8, 1.2, size=shape).astype(np.float32))
-        elif name.endswith(".bias") and (".stack.2." in name or ".norm_layer." in name):
+        elif name.endswith(".bias") and _is_gn(name):
             sd[name] = torch.from_numpy((0.1 * rng.standard_normal(shape)).astype(np.float32))
-        elif name.endswith(".weight") and (".stack.2." in name or ".norm_layer." in name):
+        elif name.endswith(".weight") and _is_gn(name):
             sd[name] = torch.from_numpy((1.0 + 0.1 * rng.standard_normal(shape)).astype(np.float32))
         elif name.endswith(".bias"):
             sd[name] = torch.from_numpy(rng.uniform(-0.05, 0.05, size=shape).astype(np.float32))
@@ -160,8 +222,6 @@ class OracleVQVAE:
         self.jitter_p = cfg.get("jitter_p", 0.0)
         self.K, self.D = cfg.get("z_num", 512), cfg.get("z_dim", 128)
         self.threshold = 1.0
-        self.ns = cfg["encoder"]["stacks"][0]
-        self.nd = cfg["decoder"]["stacks"][0]
         self.training = True
         self.last = {}
 
@@ -179,41 +239,60 @@ class OracleVQVAE:
     def _w(self, name):
         return torch._weight_norm(self.params[name + ".weight_v"], self.params[name + ".weight_g"], 0)
 
-    def _conv(self, x, name, pad, transposed=False):
-        f = F.conv_transpose1d if transposed else F.conv1d
-        return f(x, self._w(name), self.params[name + ".bias"], padding=pad)
+    def _conv(self, x, name, pad, transposed=False, stride=1, dilation=1, output_padding=0):
+        if transposed:
+            return F.conv_transpose1d(x, self._w(name), self.params[name + ".bias"], stride=stride, padding=pad,
+                                      output_padding=output_padding, dilation=dilation)
+        return F.conv1d(x, self._w(name), self.params[name + ".bias"], stride=stride, padding=pad,
+                        dilation=dilation)
 
     # vqvae.py:185-192 with the Sequential of :144-176; block layers.py:168-178
     def encoder(self, x):
         p = self.params
-        h = self._conv(x, "encoder.encode.0", 1)
-        for i in range(1, self.ns + 1):
-            pre = f"encoder.encode.{i}"
-            a = F.leaky_relu(h, 0.2)
-            a = self._conv(a, pre + ".stack.1", 1)
-            a = F.group_norm(a, 1, p[pre + ".stack.2.weight"], p[pre + ".stack.2.bias"], 1e-5)
-            h = a + self._conv(h, pre + ".skip_layer", 0)
+        stages, fidx = encoder_plan(self.cfg["encoder"])
+        h = x
+        for si, st in enumerate(stages):
+            if si > 0:
+                h = F.leaky_relu(h, 0.2)  # the previous stage's trailing LeakyReLU (vqvae.py:171)
+            h = self._conv(h, f"encoder.encode.{st['idx']}", st["pad"], stride=st["stride"])
+            ks = st["ks"]
+            for b in st["blocks"]:
+                pre = f"encoder.encode.{b['idx']}"
+                a = h
+                for l in range(st["L"]):  # layers.py:151-161
+                    dil = b["dil"] if l == 0 else 1
+                    a = F.leaky_relu(a, 0.2)
+                    a = self._conv(a, f"{pre}.stack.{3 * l + 1}", (ks - 1) // 2 * dil, dilation=dil)
+                    a = F.group_norm(a, 1, p[f"{pre}.stack.{3 * l + 2}.weight"], p[f"{pre}.stack.{3 * l + 2}.bias"],
+                                     1e-5)
+                h = a + self._conv(h, pre + ".skip_layer", 0)
         h = F.leaky_relu(h, 0.2)
-        return self._conv(h, f"encoder.encode.{self.ns + 2}", 0)
+        return self._conv(h, f"encoder.encode.{fidx}", 0)
 
     # vqvae.py:298-318; block layers.py:218-249
     def decoder(self, zq, c):
         p = self.params
-        x = self._conv(zq, "decoder.layers.0", 1, transposed=True)
-        T = x.size(2)
+        stages, n_layers = decoder_plan(self.cfg["decoder"])
         c = c[:, :, :1]
         x_out = 0.0
-        Cd = x.size(1)
-        for i in range(1, self.nd + 1):
-            pre = f"decoder.layers.{i}"
-            xr = self._conv(x, pre + ".conv_in", 1, transposed=True)
-            xc = self._conv(c.repeat(1, 1, T), pre + ".conv_cond", 0)
-            h = F.group_norm(xr + xc, 2, p[pre + ".norm_layer.weight"], p[pre + ".norm_layer.bias"], 1e-5)
-            g = torch.tanh(h[:, :Cd]) * torch.sigmoid(h[:, Cd:])
-            r = self._conv(g, pre + ".res_skip_layers", 0)
-            x = r[:, :Cd, :] + x
-            x_out += r[:, Cd:, :]
-        x = x_out * math.sqrt(1.0 / (self.nd + 1))
+        x = zq
+        for st in stages:
+            x = self._conv(x, f"decoder.layers.{st['idx']}", st["pad"], transposed=True, stride=st["stride"],
+                           output_padding=st["opad"])
+            T = x.size(2)
+            Cd = x.size(1)
+            ks = st["ks"]
+            for b in st["blocks"]:
+                pre = f"decoder.layers.{b['idx']}"
+                dil = b["dil"]
+                xr = self._conv(x, pre + ".conv_in", (ks - 1) // 2 * dil, transposed=True, dilation=dil)
+                xc = self._conv(c.repeat(1, 1, T), pre + ".conv_cond", 0)
+                h = F.group_norm(xr + xc, 2, p[pre + ".norm_layer.weight"], p[pre + ".norm_layer.bias"], 1e-5)
+                g = torch.tanh(h[:, :Cd]) * torch.sigmoid(h[:, Cd:])
+                r = self._conv(g, pre + ".res_skip_layers", 0)
+                x = r[:, :Cd, :] + x
+                x_out += r[:, Cd:, :]
+        x = x_out * math.sqrt(1.0 / n_layers)
         x = F.relu(x)
         x = self._conv(x, "decoder.final_layer.1", 0)
         x = F.relu(x)

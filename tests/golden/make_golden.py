@@ -22,6 +22,11 @@ stored):
   * step_vcc20_radam      8 steps with optim_type RAdam (trainer/radam.py,
                           SURVEY §8f row 4); RAdam switches to the adaptive
                           update at step 6
+  * step_vcc20_multi*     3 steps of the general Encoder/Decoder topology
+                          (two resolution stages with strided resampling
+                          convs, dilation 2**j, stack_layers 2, decoder
+                          kernel 5; EMA + jitter, and straight-through VQ),
+                          SURVEY §8f row 4 (--only-multi)
 Weights/inputs come from numpy PCG64 seeds (oracle/vqvae_cpu.py), so the GPU
 box regenerates them bit-identically without receiving any weights.
 """
@@ -56,7 +61,8 @@ VARIANTS = {  # derived configs: base recipe + overrides
     "aishell3_plain": ("aishell3", {"use_ema": False}),
 }
 RADAM = {"vcc20_radam": ("vcc20", {"optim_type": "RAdam"})}
-VARIANTS_ALL = dict(VARIANTS, **RADAM)
+from tests.helpers import MULTI  # noqa: E402  (the general-topology variants)
+VARIANTS_ALL = dict(VARIANTS, **RADAM, **MULTI)
 
 
 def load_cfg(name):
@@ -118,6 +124,7 @@ def step_fixture(name, B, T, steps, wseed, bseed, tseed, nseed, out_prefix, keep
     cfg = load_cfg(name)
     sd = seeded_state_dict(cfg, wseed)
     model = ref_model(cfg, sd)
+    assert [k for k, _ in model.named_parameters()] == [k for k, _ in layer_specs(cfg)], "parameter order"
     ema = cfg.get("use_ema", False)
     rec = Recorder(model.quantizer) if ema else None
     if str(cfg.get("optim_type", "Adam")).upper() == "RADAM":  # trainer/basic.py:30-34
@@ -249,6 +256,11 @@ if __name__ == "__main__":
         step_fixture("vcc20_radam", B=4, T=128, steps=8, wseed=1201, bseed=2201, tseed=3201, nseed=4201,
                      out_prefix="step_vcc20_radam")
         sys.exit(0)
+    if "--only-multi" in sys.argv:  # the §8f row-4 general topology
+        for i, name in enumerate(MULTI):
+            step_fixture(name, B=4, T=128, steps=3, wseed=1301 + i, bseed=2301 + i, tseed=3301 + i, nseed=4301 + i,
+                         out_prefix=f"step_{name}")
+        sys.exit(0)
     if "--only-plain" in sys.argv:  # just the §8f row-1 fixtures
         for i, name in enumerate(VARIANTS):
             step_fixture(name, B=4, T=128, steps=3, wseed=1101 + i, bseed=2101 + i, tseed=3101 + i,
@@ -261,6 +273,9 @@ if __name__ == "__main__":
                  out_prefix="step_aishell3")
     for i, name in enumerate(VARIANTS):
         step_fixture(name, B=4, T=128, steps=3, wseed=1101 + i, bseed=2101 + i, tseed=3101 + i, nseed=4101 + i,
+                     out_prefix=f"step_{name}")
+    for i, name in enumerate(MULTI):
+        step_fixture(name, B=4, T=128, steps=3, wseed=1301 + i, bseed=2301 + i, tseed=3301 + i, nseed=4301 + i,
                      out_prefix=f"step_{name}")
     step_fixture("vcc20_radam", B=4, T=128, steps=8, wseed=1201, bseed=2201, tseed=3201, nseed=4201,
                  out_prefix="step_vcc20_radam")

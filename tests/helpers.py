@@ -11,8 +11,30 @@ GOLD = ROOT / "tests" / "golden"
 CONF = ROOT / "vae_npvc_amd" / "conf"
 
 
+# The general Encoder/Decoder topology of vqvae.py (fixtures
+# tests/golden/step_vcc20_multi*): two resolution stages (the encoder
+# down-samples by 2 in its second stage, the decoder up-samples by 2 in its
+# first), dilation 2**j, stack_layers 2, the decoder's default kernel_size 5,
+# mixed channel widths.
+MULTI_ENC = {"in_channels": [80, 128], "out_channels": [128, 256], "downsample_scales": [1, 2], "kernel_size": 3,
+             "z_channels": 128, "dilation": True, "stack_kernel_size": 3, "stack_layers": 2, "stacks": [2, 2],
+             "use_weight_norm": True, "use_causal_conv": False}
+MULTI_DEC = {"in_channels": [128, 256], "out_channels": [256, 128], "upsample_scales": [2, 1], "cond_channels": 64,
+             "skip_channels": 64, "final_channels": 80, "kernel_size": 5, "dilation": True, "stack_kernel_size": 3,
+             "stacks": [2, 2], "use_weight_norm": True, "use_causal_conv": False}
+MULTI = {"vcc20_multi": ("vcc20", {"encoder": MULTI_ENC, "decoder": MULTI_DEC, "z_num": 128, "y_dim": 64,
+                                   "jitter_p": 0.12}),
+         "vcc20_multi_plain": ("vcc20", {"encoder": MULTI_ENC, "decoder": MULTI_DEC, "z_num": 128, "y_dim": 64,
+                                         "use_ema": False})}
+
+
 def cfg_of(name, **over):
-    cfg = yaml.safe_load(open(CONF / f"{name}.yaml"))
+    if name in MULTI:
+        base, mo = MULTI[name]
+        cfg = yaml.safe_load(open(CONF / f"{base}.yaml"))
+        cfg.update(mo)
+    else:
+        cfg = yaml.safe_load(open(CONF / f"{name}.yaml"))
     cfg.update(over)
     return cfg
 

@@ -100,6 +100,56 @@ def test_conv_dgrad_wgrad(dtype, cin, cout, k, tile):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cin,cout,k,dil,T", [(512, 512, 3, 2, 128), (256, 256, 3, 4, 64), (128, 256, 5, 1, 96),
+                                              (80, 128, 5, 1, 64), (64, 128, 3, 8, 40), (128, 128, 7, 1, 64),
+                                              (256, 512, 5, 2, 128)])
+def test_conv_dilated_and_wide_kernels(dtype, cin, cout, k, dil, T, tile):
+    """Dilated convs (dilation 2**j of the residual stacks, vqvae.py:166,274;
+    layers.py:143,153,198-200) and 5/7-tap convs (the decoder's default
+    kernel_size 5, vqvae.py:228): FWD, DGRAD and WGRAD against fp64 torch
+    autograd, padding (k-1)//2*dil as the reference builds them, including
+    utterances shorter than the dilated receptive field."""
+    ops = _ops()
+    torch.manual_seed(cin + k + dil)
+    B = 3
+    pad = (k - 1) // 2 * dil
+    x = torch.randn(B * T, cin, device=DEV).to(dtype)
+    dy = torch.randn(B * T, cout, device=DEV).to(dtype)
+    w = (torch.randn(cout, cin, k, device=DEV) / (cin * k) ** 0.5).to(dtype).float()
+    xr = x.double().cpu().view(B, T, cin).permute(0, 2, 1).clone().requires_grad_(True)
+    wr = w.double().cpu().clone().requires_grad_(True)
+    yr = F.conv1d(xr, wr, padding=pad, dilation=dil)
+    yr.backward(dy.double().cpu().view(B, T, cout).permute(0, 2, 1))
+    y = torch.empty(B * T, cout, device=DEV)
+    ops.conv_fwd(x, pack(w).to(dtype), y, T=T, cin=cin, cout=cout, ntaps=k, pad=pad, dil=dil, out_f32=True)
+    dx = torch.empty(B * T, cin, device=DEV)
+    ops.conv_dgrad(dy, pack(w).to(dtype), dx, T=T, cin=cout, cout=cin, ntaps=k, pad=(k - 1) * dil - pad, dil=dil,
+                   out_f32=True)
+    slabs = torch.empty(3, cout, k * cin, device=DEV)
+    ops.conv_wgrad(dy, x, slabs, T=T, r_dim=cout, c_dim=cin, ntaps=k, pad=pad, dil=dil, splits=3)
+    torch.cuda.synchronize()
+    assert relerr(y, yr.detach().permute(0, 2, 1).reshape(B * T, cout)) < TOL[dtype]
+    assert relerr(dx, xr.grad.permute(0, 2, 1).reshape(B * T, cin)) < TOL[dtype]
+    assert relerr(slabs.sum(0), pack(wr.grad)) < TOL[dtype]
+    # the dilated ConvTranspose1d of the ResSkip blocks (conv_in, layers.py:199) as the
+    # flipped-tap conv with pad (k-1)*dil - p, and its weight gradient (shift sign -1)
+    xt = xr.detach().clone().requires_grad_(True)
+    wt = wr.detach().permute(1, 0, 2).contiguous().clone().requires_grad_(True)  # [cin, cout, k]
+    yt = F.conv_transpose1d(xt, wt, padding=pad, dilation=dil)
+    yt.backward(dy.double().cpu().view(B, T, cout).permute(0, 2, 1))
+    wp_t = wt.detach().flip(-1).permute(1, 2, 0).reshape(cout, k * cin).float().to(DEV).to(dtype)
+    y2 = torch.empty(B * T, cout, device=DEV)
+    ops.conv_fwd(x, wp_t, y2, T=T, cin=cin, cout=cout, ntaps=k, pad=(k - 1) * dil - pad, dil=dil, out_f32=True)
+    slabs2 = torch.empty(2, cin, k * cout, device=DEV)
+    ops.conv_wgrad(x, dy, slabs2, T=T, r_dim=cin, c_dim=cout, ntaps=k, pad=(k - 1) * dil - pad, dil=dil,
+                   shift_sign=-1, splits=2)
+    torch.cuda.synchronize()
+    assert relerr(y2, yt.detach().permute(0, 2, 1).reshape(B * T, cout)) < TOL[dtype]
+    dwt = slabs2.sum(0).view(cin, k, cout).permute(0, 2, 1).flip(-1)
+    assert relerr(dwt, wt.grad) < TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_convtranspose_via_weight_norm_pack(dtype, tile):
     """ConvTranspose1d(cin->cout, k3, p1) through the weight-norm pack kernel
     (dim 0 = in-channels) and the conv GEMM, fwd + wgrad(sign -1)."""

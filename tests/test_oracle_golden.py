@@ -18,6 +18,11 @@ def cfg_of(name):
     return yaml.safe_load(open(CONF / f"{name}.yaml"))
 
 
+def helpers_cfg(name):
+    from tests.helpers import cfg_of as hc
+    return hc(name)
+
+
 def load_fixture(prefix):
     meta = json.load(open(GOLD / f"{prefix}.json"))
     arr = dict(np.load(GOLD / f"{prefix}.npz", allow_pickle=False))
@@ -38,16 +43,18 @@ def test_structure_matches_reference():
 
 
 FIXTURE_CFG = {"step_vcc20": ("vcc20", {}), "step_aishell3": ("aishell3", {}),
-               "step_vcc20_radam": ("vcc20", {"optim_type": "RAdam"})}
+               "step_vcc20_radam": ("vcc20", {"optim_type": "RAdam"}), "step_vcc20_multi": ("vcc20_multi", {})}
 
 
 @pytest.mark.parametrize("prefix", list(FIXTURE_CFG))
 def test_oracle_train_steps_match_reference(prefix):
     """Adam (3 steps) and RAdam (8 steps: the rectified update starts at step 6,
-    trainer/radam.py:53-59) against the reference run."""
+    trainer/radam.py:53-59) against the reference run; step_vcc20_multi is the
+    general Encoder/Decoder topology (two stages with strided resampling,
+    dilation, stack_layers 2, decoder kernel 5) with EMA and jitter."""
     meta, arr = load_fixture(prefix)
     base, over = FIXTURE_CFG[prefix]
-    cfg = dict(cfg_of(base), **over)
+    cfg = dict(helpers_cfg(base), **over)
     torch.set_num_threads(4)
     tr = OracleTrainer(cfg, seeded_state_dict(cfg, meta["wseed"]))
     torch.manual_seed(meta["tseed"])
@@ -78,12 +85,13 @@ def test_oracle_train_steps_match_reference(prefix):
 
 PLAIN = {"vcc20_plain": ("vcc20", {"use_ema": False}),
          "vcc20_plain_nonorm": ("vcc20", {"use_ema": False, "embed_norm": False}),
-         "aishell3_plain": ("aishell3", {"use_ema": False})}
+         "aishell3_plain": ("aishell3", {"use_ema": False}),
+         "vcc20_multi_plain": ("vcc20_multi_plain", {})}
 
 
 def plain_cfg(name):
     base, over = PLAIN[name]
-    return dict(cfg_of(base), **over)
+    return dict(helpers_cfg(base), **over)
 
 
 @pytest.mark.parametrize("name", list(PLAIN))

@@ -93,7 +93,8 @@ static int conv_common(const vqx_conv_args* a, int mode, hipStream_t s) {
   if (a->dtype != VQX_F32 && a->dtype != VQX_BF16) { set_error("vqx_conv: bad dtype %d", a->dtype); return -1; }
   const int epc = a->dtype == VQX_BF16 ? 8 : 4;
   const int es = a->dtype == VQX_BF16 ? 2 : 4;
-  if (a->ntaps < 1 || a->ntaps > 3 || a->pad < 0 || a->pad >= a->ntaps + 1) { set_error("vqx_conv: ntaps %d / pad %d", a->ntaps, a->pad); return -1; }
+  const int dil = a->dil > 0 ? a->dil : 1;
+  if (a->ntaps < 1 || a->ntaps > 8 || a->pad < 0 || a->pad > (a->ntaps - 1) * dil) { set_error("vqx_conv: ntaps %d / pad %d / dil %d", a->ntaps, a->pad, dil); return -1; }
   if (a->n_rows <= 0 || a->T <= 0 || a->n_rows % a->T) { set_error("vqx_conv: n_rows %lld not a multiple of T %d", (long long)a->n_rows, a->T); return -1; }
   if (a->cin <= 0 || a->cout <= 0 || a->cin % epc || a->ldx % epc || a->cin > a->ldx) { set_error("vqx_conv: cin %d / ldx %d must be multiples of %d", a->cin, a->ldx, epc); return -1; }
   if (a->cout % 8 || a->ldy % 8) { set_error("vqx_conv: cout %d / ldy %d must be multiples of 8", a->cout, a->ldy); return -1; }
@@ -129,7 +130,7 @@ static int conv_common(const vqx_conv_args* a, int mode, hipStream_t s) {
   P.n_rows = a->n_rows; P.T = a->T; P.lda = a->ldx;
   P.kcin = a->cin; P.K = a->ntaps * a->cin; P.Mc = (int)a->n_rows; P.Nc = a->cout;
   P.b_bytes = (int64_t)a->ntaps * a->cin * a->cout * es;  // packed weight, either orientation
-  P.ntaps = a->ntaps; P.pad = a->pad; P.sign = 1;
+  P.ntaps = a->ntaps; P.pad = a->pad; P.sign = 1; P.dil = dil;
   P.cdim = a->cout;
   P.pro = a->prologue; P.pro_scale = a->pro_scale;
   P.tiles_n = (a->cout + kBN - 1) / kBN; P.splits = 1;  // tiles_m: launch_mode (tile height)
@@ -170,7 +171,8 @@ extern "C" int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream) {
   if (a->dtype != VQX_F32 && a->dtype != VQX_BF16) { set_error("vqx_conv1d_wgrad: bad dtype"); return -1; }
   const int epc = a->dtype == VQX_BF16 ? 8 : 4;
   const int es = a->dtype == VQX_BF16 ? 2 : 4;
-  if (a->ntaps < 1 || a->ntaps > 3) { set_error("vqx_conv1d_wgrad: ntaps %d", a->ntaps); return -1; }
+  const int dil = a->dil > 0 ? a->dil : 1;
+  if (a->ntaps < 1 || a->ntaps > 8 || a->pad < 0 || a->pad > (a->ntaps - 1) * dil) { set_error("vqx_conv1d_wgrad: ntaps %d / pad %d / dil %d", a->ntaps, a->pad, dil); return -1; }
   if (a->n_rows <= 0 || a->T <= 0 || a->n_rows % a->T) { set_error("vqx_conv1d_wgrad: bad n_rows/T"); return -1; }
   if (a->r_dim % epc || a->c_dim % epc || a->ldp % epc || a->ldq % epc || a->c_dim % 8) { set_error("vqx_conv1d_wgrad: dims must be multiples of %d (c_dim of 8)", epc); return -1; }
   if (a->splits < 1) { set_error("vqx_conv1d_wgrad: splits < 1"); return -1; }
@@ -181,7 +183,7 @@ extern "C" int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream) {
   P.a_bytes = ((a->n_rows - 1) * (int64_t)a->ldp + a->r_dim) * es;
   P.b_bytes = ((a->n_rows - 1) * (int64_t)a->ldq + a->c_dim) * es;
   if (P.a_bytes > 0x7fffffffLL || P.b_bytes > 0x7fffffffLL) { set_error("vqx_conv1d_wgrad: operand larger than 2 GiB"); return -1; }
-  P.Mc = a->r_dim; P.Nc = a->ntaps * a->c_dim; P.ntaps = a->ntaps; P.pad = a->pad; P.sign = a->shift_sign;
+  P.Mc = a->r_dim; P.Nc = a->ntaps * a->c_dim; P.ntaps = a->ntaps; P.pad = a->pad; P.sign = a->shift_sign; P.dil = dil;
   P.cdim = a->c_dim; P.pro = a->q_prologue; P.pro_scale = a->pro_scale;
   P.tiles_n = (P.Nc + kBN - 1) / kBN; P.splits = a->splits;  // tiles_m: launch_mode
   int64_t kps = (a->n_rows + a->splits - 1) / a->splits;
@@ -191,7 +193,7 @@ extern "C" int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream) {
   P.y = a->slabs;
   const int bkv = a->dtype == VQX_BF16 ? 64 : 32;
   const bool gen = (a->T % bkv) != 0 || (a->n_rows % bkv) != 0;
-  if (!gen && wgrad_tr_ok(a->n_rows, a->T, a->c_dim, a->ntaps, a->pad, a->dtype == VQX_BF16, a->q_prologue)) {
+  if (!gen && wgrad_tr_ok(a->n_rows, a->T, a->c_dim, a->ntaps, a->pad, dil, a->dtype == VQX_BF16, a->q_prologue)) {
     P.tap_reuse = wgrad_kgroups();
     P.tiles_n = a->c_dim / 64;
   }
@@ -201,8 +203,8 @@ extern "C" int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream) {
 }
 
 extern "C" int vqx_wgrad_tiles(int64_t n_rows, int32_t T, int32_t r_dim, int32_t c_dim, int32_t ntaps, int32_t pad,
-                               int32_t dtype, int32_t q_prologue, int32_t* tiles) {
-  if (!tiles || n_rows <= 0 || T <= 0 || r_dim <= 0 || c_dim <= 0 || ntaps < 1 || ntaps > 3) {
+                               int32_t dil, int32_t dtype, int32_t q_prologue, int32_t* tiles) {
+  if (!tiles || n_rows <= 0 || T <= 0 || r_dim <= 0 || c_dim <= 0 || ntaps < 1 || ntaps > 8) {
     set_error("vqx_wgrad_tiles: bad arguments");
     return -1;
   }
@@ -210,7 +212,8 @@ extern "C" int vqx_wgrad_tiles(int64_t n_rows, int32_t T, int32_t r_dim, int32_t
   const int bkv = bf16 ? 64 : 32;
   const bool gen = (T % bkv) != 0 || (n_rows % bkv) != 0;
   const int tm = (r_dim + 127) / 128;
-  if (!gen && wgrad_tr_ok(n_rows, T, c_dim, ntaps, pad, bf16, q_prologue)) *tiles = tm * (c_dim / 64) * wgrad_kgroups();
+  if (!gen && wgrad_tr_ok(n_rows, T, c_dim, ntaps, pad, dil > 0 ? dil : 1, bf16, q_prologue))
+    *tiles = tm * (c_dim / 64) * wgrad_kgroups();
   else *tiles = tm * ((ntaps * c_dim + kBN - 1) / kBN);
   return 0;
 }

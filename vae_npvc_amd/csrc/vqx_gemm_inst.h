@@ -22,7 +22,7 @@ bool tap_reuse_enabled();
 // conv_tr_kernel applies: bf16, no prologue, 3 taps / pad 1, 32-channel K
 // slices, and every 128-frame tile inside one utterance
 inline bool tap_reuse_ok(const GemmParams& P, bool bf16, bool gen) {
-  return bf16 && !gen && P.pro == VQX_PRO_NONE && P.ntaps == 3 && P.pad == 1 && P.kcin % 32 == 0 &&
+  return bf16 && !gen && P.pro == VQX_PRO_NONE && P.ntaps == 3 && P.pad == 1 && P.dil == 1 && P.kcin % 32 == 0 &&
          P.K == 3 * P.kcin && P.T % 128 == 0 && P.n_rows % 128 == 0 && tap_reuse_enabled();
 }
 
@@ -31,8 +31,8 @@ inline bool tap_reuse_ok(const GemmParams& P, bool bf16, bool gen) {
 // K groups per tap-reuse WGRAD workgroup (default 1; env VQX_WGRAD_KG=2: two 4-wave groups)
 int wgrad_kgroups();
 
-inline bool wgrad_tr_ok(int64_t n_rows, int T, int c_dim, int ntaps, int pad, bool bf16, int pro) {
-  return bf16 && pro == VQX_PRO_NONE && ntaps == 3 && pad == 1 && c_dim % 64 == 0 && T % 64 == 0 &&
+inline bool wgrad_tr_ok(int64_t n_rows, int T, int c_dim, int ntaps, int pad, int dil, bool bf16, int pro) {
+  return bf16 && pro == VQX_PRO_NONE && ntaps == 3 && pad == 1 && dil == 1 && c_dim % 64 == 0 && T % 64 == 0 &&
          n_rows % 64 == 0 && tap_reuse_enabled();
 }
 

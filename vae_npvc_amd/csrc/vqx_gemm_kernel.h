@@ -1,9 +1,10 @@
 // Conv1d / ConvTranspose1d (stride 1) as implicit-im2col GEMMs on gfx950 MFMA.
 //
 // One kernel template covers the three products of a conv layer:
-//   FWD   Y[n][co]      = sum_{j,ci} pro(x[n+j-pad][ci]) * We[co][j][ci]
-//   DGRAD Y[n][ci]      = sum_{j,co} dy[n+j-pad][co]     * We[co][k-1-j][ci]
-//   WGRAD S[r][j*cd+c]  = sum_n      p[n][r]             * pro(q[n+s(j-pad)][c])
+//   FWD   Y[n][co]      = sum_{j,ci} pro(x[n+j*d-pad][ci]) * We[co][j][ci]
+//   DGRAD Y[n][ci]      = sum_{j,co} dy[n+j*d-pad][co]     * We[co][k-1-j][ci]
+//   WGRAD S[r][j*cd+c]  = sum_n      p[n][r]               * pro(q[n+s(j*d-pad)][c])
+// (d = dilation; up to 8 taps)
 // Frames (n = b*T + t) are the long GEMM dimension: 16,384 at config 2.
 //
 // Workgroup: 256 threads, 128x128 output tile, 4 waves in 2x2, each wave a
@@ -51,6 +52,7 @@ struct GemmParams {
   int K;           // FWD/DGRAD: ntaps*kcin
   int Mc, Nc;      // output dims: FWD/DGRAD rows = frames, cols = channels; WGRAD rows = r, cols = j*cd+c
   int ntaps, pad, sign;
+  int dil;         // tap spacing in frames (dilation), >= 1
   int cdim;        // DGRAD: cin of the forward layer (= Nc); WGRAD: c_dim
   int pro;
   float pro_scale;
@@ -116,7 +118,14 @@ __device__ __forceinline__ uint4 pro_chunk(uint4 u, float s) {
   }
 }
 
-__device__ __forceinline__ int tap_of(int k, int c) { return (k >= c) + (k >= 2 * c); }
+// tap of K index k when each tap spans c channels (ntaps <= 8)
+__device__ __forceinline__ int tap_of(int k, int c, int nt) {
+  if (nt <= 3) return (k >= c) + (k >= 2 * c);
+  int j = 0;
+#pragma unroll
+  for (int t = 1; t < 8; ++t) j += (t < nt && k >= t * c) ? 1 : 0;
+  return j;
+}
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_at(const void* base, int64_t shift_bytes, int64_t total_bytes) {
   int64_t rec = total_bytes - shift_bytes;
@@ -631,7 +640,10 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
       int msk = 0;
       if (n < P.n_rows)
 #pragma unroll
-        for (int j = 0; j < 3; ++j) msk |= ((t + j - P.pad >= 0) && (t + j - P.pad < P.T)) ? (1 << j) : 0;
+        for (int j = 0; j < 8; ++j) {
+          const int tt = t + j * P.dil - P.pad;
+          msk |= (j < P.ntaps && tt >= 0 && tt < P.T) ? (1 << j) : 0;
+        }
       amask[i] = msk;
       ak[i] = kch * EPC;
       aoff[i] = (unsigned)((n * P.lda + (GEN ? 0 : kch * EPC)) * ES);
@@ -663,13 +675,13 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
       const int krow = c / CPR;
       const int cch = (sizeof(T) == 2) ? ((c % CPR) ^ mn_swz(krow)) : (c % CPR);
       const int col = n0 + cch * EPC;
-      const int j = tap_of(col, P.cdim);
+      const int j = tap_of(col, P.cdim, P.ntaps);
       const int cc = col - j * P.cdim;
-      const int sh = P.sign * (j - P.pad);
+      const int sh = P.sign * (j * P.dil - P.pad);
       bk[i] = krow;
       bsh[i] = krow + sh;
-      // the q descriptor base sits (ntaps-1) rows before the tile so shifted offsets stay >= 0
-      boff[i] = col < P.Nc ? (unsigned)(((int64_t)(krow + sh + P.ntaps - 1) * P.ldb + cc) * ES) : kOOB;
+      // the q descriptor base sits (ntaps-1)*dil rows before the tile so shifted offsets stay >= 0
+      boff[i] = col < P.Nc ? (unsigned)(((int64_t)(krow + sh + (P.ntaps - 1) * P.dil) * P.ldb + cc) * ES) : kOOB;
     }
   }
 
@@ -680,7 +692,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
   // of range).
   int64_t a_lo = 0, b_lo = 0;
   if constexpr (MODE != MODE_WGRAD) a_lo = (int64_t)P.pad * P.lda * ES;
-  if constexpr (MODE == MODE_WGRAD) b_lo = (int64_t)(P.ntaps - 1) * P.ldb * ES;
+  if constexpr (MODE == MODE_WGRAD) b_lo = (int64_t)(P.ntaps - 1) * P.dil * P.ldb * ES;
   const __amdgpu_buffer_rsrc_t rsA = rsrc_at(P.a, -a_lo, P.a_bytes);
   const __amdgpu_buffer_rsrc_t rsB = rsrc_at(P.b, -b_lo, P.b_bytes);
   if constexpr (MODE != MODE_WGRAD) {
@@ -699,7 +711,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
         const int tap = ld_tap, c0 = ld_c0;  // k0 == tap*kcin + c0
         ld_c0 += BK;
         if (ld_c0 >= P.kcin) { ld_c0 = 0; ld_tap += 1; }
-        const unsigned ksa = (unsigned)(((tap - P.pad) * P.lda + c0) * ES);
+        const unsigned ksa = (unsigned)(((tap * P.dil - P.pad) * P.lda + c0) * ES);
 #pragma unroll
         for (int i = 0; i < PW; ++i) oa[i] = ((amask[i] >> tap) & 1) ? aoff[i] + ksa : kOOB;
         unsigned ksb;
@@ -712,10 +724,10 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
 #pragma unroll
         for (int i = 0; i < PW; ++i) {
           const int k = (int)k0 + ak[i];
-          const int tap = tap_of(k, P.kcin);
+          const int tap = tap_of(k, P.kcin, P.ntaps);
           const int ci = k - tap * P.kcin;
           const bool ok = k < P.K && ((amask[i] >> tap) & 1);
-          oa[i] = ok ? aoff[i] + (unsigned)((((tap - P.pad) * P.lda) + ci) * ES) : kOOB;
+          oa[i] = ok ? aoff[i] + (unsigned)((((tap * P.dil - P.pad) * P.lda) + ci) * ES) : kOOB;
         }
         if constexpr (MODE == MODE_FWD) {
 #pragma unroll
@@ -724,7 +736,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
 #pragma unroll
           for (int i = 0; i < PW; ++i) {
             const int k = (int)k0 + bk[i];
-            const int j = tap_of(k, P.kcin);
+            const int j = tap_of(k, P.kcin, P.ntaps);
             const int co = k - j * P.kcin;
             ob[i] = (k < P.K && boff[i] != kOOB)
                         ? boff[i] + (unsigned)(((int64_t)co * P.ntaps * P.cdim + (P.ntaps - 1 - j) * P.cdim) * ES)

@@ -33,7 +33,7 @@ def conv_args(x, w, y, *, T, cin, cout, ntaps, pad, prologue=L.PRO_NONE, pro_sca
               rowbias=None, res=None, mask=None, mask_slope=0.0, mask_scale=1.0, gn_h=None, gn_mr=None,
               gn_gamma=None, gn_beta=None, out2=None, split_col=0, out2_accumulate=False, out_f32=False,
               act=None, y2=None, colsum=None, gn_stats=None, gn_bwd=None, gn_groups=1, gn_glu=False,
-              gn_tiles=None, gn_eps=1e-5):
+              gn_tiles=None, gn_eps=1e-5, dil=1):
     epi = 0
     if bias is not None:
         epi |= L.EPI_BIAS
@@ -63,7 +63,7 @@ def conv_args(x, w, y, *, T, cin, cout, ntaps, pad, prologue=L.PRO_NONE, pro_sca
     a.x, a.w, a.y = ptr(x), ptr(w), ptr(y)
     a.bias, a.rowbias, a.res, a.mask = ptr(bias), ptr(rowbias), ptr(res), ptr(mask)
     a.gn_h, a.gn_mean_rstd, a.gn_gamma, a.gn_beta, a.out2 = ptr(gn_h), ptr(gn_mr), ptr(gn_gamma), ptr(gn_beta), ptr(out2)
-    a.n_rows, a.T, a.cin, a.cout, a.ntaps, a.pad = x.shape[0], T, cin, cout, ntaps, pad
+    a.n_rows, a.T, a.cin, a.cout, a.ntaps, a.pad, a.dil = x.shape[0], T, cin, cout, ntaps, pad, dil
     a.ldx, a.ldy = x.stride(0), y.stride(0)
     a.ldres = res.stride(0) if res is not None else 0
     a.ldmask = mask.stride(0) if mask is not None else 0
@@ -174,24 +174,24 @@ def conv_dgrad(dy, w, dx, **kw):
 
 
 def conv_wgrad(p, q, slabs, *, T, r_dim, c_dim, ntaps, pad, shift_sign=1, q_prologue=L.PRO_NONE, pro_scale=1.0,
-               splits=1):
-    """slabs[s, r, j*c_dim + c] = sum_{n in split s} p[n, r] * pro(q[n + sign*(j-pad), c])."""
+               splits=1, dil=1):
+    """slabs[s, r, j*c_dim + c] = sum_{n in split s} p[n, r] * pro(q[n + sign*(j*dil-pad), c])."""
     _check_cuda(p, q, slabs)
     a = L.WgradArgs()
     a.p, a.q, a.slabs = ptr(p), ptr(q), ptr(slabs)
     a.n_rows, a.T, a.r_dim, a.c_dim, a.ntaps, a.pad, a.shift_sign = p.shape[0], T, r_dim, c_dim, ntaps, pad, shift_sign
     a.ldp, a.ldq = p.stride(0), q.stride(0)
-    a.dtype, a.q_prologue, a.splits, a.pro_scale = dt_code(p.dtype), q_prologue, splits, pro_scale
+    a.dtype, a.q_prologue, a.splits, a.pro_scale, a.dil = dt_code(p.dtype), q_prologue, splits, pro_scale, dil
     if _probe is not None:
         _probe.shapes.append(f"{r_dim}x{ntaps}x{c_dim} s{splits}")
     call("vqx_conv1d_wgrad", ctypes.byref(a), stream_ptr())
     return slabs
 
 
-def wgrad_tiles(n_rows, T, r_dim, c_dim, ntaps, pad, dtype, q_prologue=L.PRO_NONE):
+def wgrad_tiles(n_rows, T, r_dim, c_dim, ntaps, pad, dtype, q_prologue=L.PRO_NONE, dil=1):
     """Output tiles per split of the weight-gradient kernel conv_wgrad would launch."""
     t = ctypes.c_int32()
-    call("vqx_wgrad_tiles", n_rows, T, r_dim, c_dim, ntaps, pad, dtype, q_prologue, ctypes.byref(t))
+    call("vqx_wgrad_tiles", n_rows, T, r_dim, c_dim, ntaps, pad, dil, dtype, q_prologue, ctypes.byref(t))
     return t.value
 
 
