@@ -279,9 +279,10 @@ int vqx_logloss_fwd_bwd(const float* x_nct, const float* xhat, int32_t ldxh, int
  *   zq[n]      = E[idx[n]]  (f32 [N][D]) and zq_c (dtype, decoder input)
  *   sqerr      : sum_n ||zq_n - z_n||^2  into sqerr_out[0] (deterministic)
  *   bsum[k][d] += sum_{n: idx=k} z[n][d], bcnt[k] += |{n: idx=k}|
- *                 (per-chunk LDS tables reduced in chunk order; pass NULL to
- *                 skip, e.g. eval / encode())
- * z [N][D] f32 (frame-major, D = 128), E [K][D] f32, K % 16 == 0, K <= 3264.
+ *                 (deterministic: 512-frame chunks sorted by code, segmented
+ *                 sums, chunk tables reduced in order; pass NULL to skip, e.g.
+ *                 eval / encode())
+ * z [N][D] f32 (frame-major, D = 128), E [K][D] f32, K % 16 == 0, K <= 2048.
  * `partials` is a caller workspace of >= vqx_vq_workspace(N, K, bsum != NULL)
  * floats.
  */

@@ -44,17 +44,14 @@ constexpr int VQ_STAGE = VQ_STEP_BYTES / 16 / VQ_THREADS;  // 16-B chunks staged
 // EMA statistics (vq_stats_kernel): frames per chunk and the per-code sum
 // slabs [chunks][K][D] + counts [chunks][K] that vq_stats_reduce_kernel sums
 // in chunk order.
-__host__ __device__ constexpr int vq_stats_dsl(int K) {  // dims per LDS slice: K * (dsl + 1) * 4 B <= 64 KiB
-  int d = 128;
-  while (d > 4 && K * (d + 1) > 16384) d >>= 1;
+__host__ __device__ constexpr int vq_stats_dsl(int K) {  // dims per LDS slice: K * (dsl + 1) * 4 B + ~10 KiB <= 64 KiB
+  int d = 32;  // <= 32: a thread holds VQ_CHUNK * dsl / 1024 sorted rows in registers
+  while (d > 4 && K * (d + 1) > 13824) d >>= 1;
   return d;
 }
 inline int vq_stats_chunks(int64_t N, int K) {
-  const int slices = VQ_D / vq_stats_dsl(K);
-  int64_t c = (256 + slices - 1) / slices;  // ~256 workgroups
-  const int64_t cmax = (N + 255) / 256;     // >= 256 frames per chunk
-  if (c > cmax) c = cmax;
-  return (int)(c < 1 ? 1 : c);
+  (void)K;
+  return (int)((N + 511) / 512);  // VQ_CHUNK frames per chunk
 }
 inline int64_t vq_partials_floats(int64_t N) { return (N + VQ_FRAMES - 1) / VQ_FRAMES; }
 inline int64_t vq_workspace_floats(int64_t N, int K, bool stats) {
@@ -267,82 +264,170 @@ __global__ __launch_bounds__(VQ_THREADS, 4) void vq_forward_kernel(const float* 
 }
 
 // EMA statistics (update_emb, layers_vq.py:207-211: onehot(idx) @ z and the
-// code counts), as a dense per-chunk reduction instead of scattered global
-// atomics: workgroup (chunk c, dim slice y) accumulates its frames' z[:, slice]
-// into an LDS table [K][DSL] (ds_add_f32) and the code counts, then writes
-// the whole table to its slab.  Every z element is read once.
+// code counts) as a dense per-chunk reduction, deterministic and free of
+// atomics: workgroup (chunk c of <= VQ_CHUNK frames, dim slice y of DSL
+// dims) bitonic-sorts its frames by (code, frame) in LDS; thread (g, r) then
+// sums 4 dims of the r-th range of sorted frames, writing every run that lies
+// inside its range straight into the LDS table [K][DSL] and leaving the two
+// runs cut by range edges as partials, which the thread holding each run's
+// first frame completes in ascending range order.  The table becomes the
+// chunk's slab row; vq_stats_reduce_kernel sums the slabs in chunk order.
+// (LDS float atomics measured ~11 us of an 18 us kernel: ~one lane per clock.)
+constexpr int VQ_CHUNK = 512;
+
 template <int DSL>
 __global__ __launch_bounds__(256) void vq_stats_kernel(const float* __restrict__ z, int64_t N,
                                                        const int64_t* __restrict__ idx, int K, int64_t frames_per_chunk,
                                                        float* __restrict__ slab, float* __restrict__ cnt_slab) {
-  extern __shared__ __attribute__((aligned(16))) float acc[];  // [K][DSL] + int counts [K]
-  int* cnt = (int*)(acc + K * DSL);
+  constexpr int G = DSL / 4;             // 4-dim groups per slice
+  constexpr int R = 256 / G;             // ranges of sorted frames
+  constexpr int LEN = VQ_CHUNK / R;      // sorted frames per range
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* acc = lds;                                  // [K][DSL]
+  int* keys = (int*)(acc + K * DSL);                 // [VQ_CHUNK] code << 9 | frame (sorted)
+  int* runk = keys + VQ_CHUNK;                       // [R][2] head / tail run code (-1: none)
+  int* cnt = runk + 2 * R;                           // [K] (slice 0)
+  f32x4_t* part = (f32x4_t*)(cnt + ((K + 3) & ~3));  // [R][2][G] head / tail partial sums
   const int tid = threadIdx.x;
   const int c = blockIdx.x, d0 = blockIdx.y * DSL;
   const bool counts = blockIdx.y == 0;
+  const int64_t n0 = (int64_t)c * frames_per_chunk;
+  const int nf = (int)((n0 + frames_per_chunk < N ? n0 + frames_per_chunk : N) - n0);
   for (int i = tid; i < K * DSL; i += 256) acc[i] = 0.f;
   if (counts)
     for (int i = tid; i < K; i += 256) cnt[i] = 0;
+  for (int i = tid; i < VQ_CHUNK; i += 256) {
+    int code = i < nf ? (int)idx[n0 + i] : K;
+    if (code < 0 || code > K) code = K;  // out-of-range codes sort last and are dropped
+    keys[i] = code < K ? (code << 9) | i : 0x7fffffff;
+  }
   __syncthreads();
-  const int64_t n0 = (int64_t)c * frames_per_chunk;
-  const int64_t n1 = n0 + frames_per_chunk < N ? n0 + frames_per_chunk : N;
-  constexpr int TPF = DSL / 4;   // threads per frame (4 dims each, one 16-B load)
-  constexpr int P = 256 / TPF;   // frames per pass
-  constexpr int U = 8;           // passes whose loads are in flight together
-  const int d = 4 * (tid % TPF);
-  for (int64_t nb = n0 + tid / TPF; nb < n1; nb += (int64_t)P * U) {
-    int k[U];
-    f32x4_t v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t n = nb + (int64_t)u * P;
-      k[u] = n < n1 ? (int)idx[n] : -1;
-      v[u] = n < n1 ? *(const f32x4_t*)(z + n * VQ_D + d0 + d) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+  if (counts)
+    for (int i = tid; i < nf; i += 256) {
+      const int k = keys[i];
+      if (k != 0x7fffffff) atomicAdd(&cnt[k >> 9], 1);  // integer counts: exact in any order
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (k[u] < 0 || k[u] >= K) continue;
-      float* a = &acc[k[u] * DSL + d];
-      atomicAdd(a, v[u][0]);
-      atomicAdd(a + 1, v[u][1]);
-      atomicAdd(a + 2, v[u][2]);
-      atomicAdd(a + 3, v[u][3]);
-      if (counts && d == 0) atomicAdd(&cnt[k[u]], 1);
+  // bitonic sort, ascending (VQ_CHUNK = 2 elements per thread per step)
+  for (int k = 2; k <= VQ_CHUNK; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const int i = 2 * tid - (tid & (j - 1));
+      const int a = keys[i], b = keys[i + j];
+      const bool up = (i & k) == 0;
+      if ((a > b) == up) { keys[i] = b; keys[i + j] = a; }
+      __syncthreads();
     }
+  }
+  // segmented sums over range r, 4 dims (group g)
+  const int g = tid % G, r = tid / G, dd = d0 + 4 * g;
+  const int p0 = r * LEN;
+  f32x4_t rows[LEN];
+  int rc[LEN];
+#pragma unroll
+  for (int u = 0; u < LEN; ++u) {
+    const int key = keys[p0 + u];
+    rc[u] = key == 0x7fffffff ? -1 : key >> 9;
+    rows[u] = rc[u] < 0 ? f32x4_t{0.f, 0.f, 0.f, 0.f} : *(const f32x4_t*)(z + (n0 + (key & 511)) * VQ_D + dd);
+  }
+  f32x4_t run = rows[0];
+  int cur = rc[0];
+  bool head = true;
+#pragma unroll
+  for (int u = 1; u <= LEN; ++u) {
+    const int nc = u < LEN ? rc[u] : -2;
+    if (nc != cur) {
+      if (head) {  // first run of the range: may have started in an earlier range
+        part[(r * 2 + 0) * G + g] = run;
+        if (g == 0) runk[2 * r] = cur;
+        head = false;
+      } else if (u == LEN) {  // last run: may continue into the next range
+        part[(r * 2 + 1) * G + g] = run;
+        if (g == 0) runk[2 * r + 1] = cur;
+      } else if (cur >= 0) {  // a run wholly inside the range: exclusive
+        *(f32x4_t*)&acc[cur * DSL + 4 * g] = run;
+      }
+      if (u < LEN) { run = rows[u]; cur = nc; }
+    } else {
+      run += rows[u];
+    }
+  }
+  if (head == false && g == 0 && rc[LEN - 1] == runk[2 * r]) {
+    // the range is one run: the head partial also serves as its tail
+    runk[2 * r + 1] = -1;
+  }
+  __syncthreads();
+  // complete the runs cut by range edges: the range holding a run's first frame
+  // adds the continuations in ascending range order
+  auto finish = [&](int code, int rr, f32x4_t sum) {
+    for (int q = rr + 1; q < R; ++q) {
+      if (runk[2 * q] != code) break;
+      sum += part[(q * 2 + 0) * G + g];
+      if (runk[2 * q + 1] != -1) break;  // the run ends inside range q
+    }
+    *(f32x4_t*)&acc[code * DSL + 4 * g] = sum;
+  };
+  {
+    const int kh = runk[2 * r];
+    // the head run starts here unless the previous range ends with the same code
+    const int prev_tail = r > 0 ? (runk[2 * (r - 1) + 1] != -1 ? runk[2 * (r - 1) + 1] : runk[2 * (r - 1)]) : -3;
+    if (kh >= 0 && kh != prev_tail) {
+      if (runk[2 * r + 1] == -1) finish(kh, r, part[(r * 2 + 0) * G + g]);          // single run: may continue
+      else *(f32x4_t*)&acc[kh * DSL + 4 * g] = part[(r * 2 + 0) * G + g];          // ends inside the range
+    }
+    const int kt = runk[2 * r + 1];
+    if (kt >= 0) finish(kt, r, part[(r * 2 + 1) * G + g]);
   }
   __syncthreads();
   float* out = slab + (int64_t)c * K * VQ_D + d0;
-  for (int i = tid; i < K * DSL; i += 256) out[(int64_t)(i / DSL) * VQ_D + (i % DSL)] = acc[i];
+  for (int i = tid; i < K * G; i += 256) {
+    const int k = i / G, q = i % G;
+    *(f32x4_t*)(out + (int64_t)k * VQ_D + 4 * q) = *(const f32x4_t*)&acc[k * DSL + 4 * q];
+  }
   if (counts)
     for (int i = tid; i < K; i += 256) cnt_slab[(int64_t)c * K + i] = (float)cnt[i];
 }
 
-// bsum[i] += sum_c slab[c][i], bcnt[k] += sum_c cnt_slab[c][k], chunks in
-// order (4 elements per thread; the chunk loads are independent).
+// bsum[i] += sum_c slab[c][i], bcnt[k] += sum_c cnt_slab[c][k], summed in
+// chunk order: 64 float4 columns per workgroup, 4 threads per column each
+// loading a quarter of the chunks (independent loads), combined in order.
 __global__ __launch_bounds__(256) void vq_stats_reduce_kernel(const float* __restrict__ slab,
                                                               const float* __restrict__ cnt_slab, int chunks, int K,
                                                               float* __restrict__ bsum, float* __restrict__ bcnt) {
+  __shared__ f32x4_t red[4][64];
   const int64_t total = (int64_t)K * VQ_D;
-  const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  const int col = threadIdx.x & 63, qg = threadIdx.x >> 6;
+  const int64_t i4 = ((int64_t)blockIdx.x * 64 + col) * 4;
+  const int per = (chunks + 3) / 4, c0 = qg * per, c1 = min(chunks, c0 + per);
+  f32x4_t s = {0.f, 0.f, 0.f, 0.f};
   if (i4 < total) {
-    f32x4_t s = {0.f, 0.f, 0.f, 0.f};
-    int c = 0;
-    for (; c + 4 <= chunks; c += 4) {
-      f32x4_t v[4];
+    int c = c0;
+    for (; c + 8 <= c1; c += 8) {
+      f32x4_t v[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = *(const f32x4_t*)(slab + (int64_t)(c + u) * total + i4);
+      for (int u = 0; u < 8; ++u) v[u] = *(const f32x4_t*)(slab + (int64_t)(c + u) * total + i4);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) s += v[u];
+      for (int u = 0; u < 8; ++u) s += v[u];
     }
-    for (; c < chunks; ++c) s += *(const f32x4_t*)(slab + (int64_t)c * total + i4);
-    f32x4_t o = *(f32x4_t*)(bsum + i4);
-    *(f32x4_t*)(bsum + i4) = o + s;
+    for (; c < c1; ++c) s += *(const f32x4_t*)(slab + (int64_t)c * total + i4);
+  }
+  red[qg][col] = s;
+  __syncthreads();
+  if (qg == 0 && i4 < total) {
+    const f32x4_t t = ((red[0][col] + red[1][col]) + red[2][col]) + red[3][col];
+    *(f32x4_t*)(bsum + i4) = *(f32x4_t*)(bsum + i4) + t;
   }
   const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (bcnt && k < K) {
-    float s = 0.f;
-    for (int c = 0; c < chunks; ++c) s += cnt_slab[(int64_t)c * K + k];
-    bcnt[k] += s;
+    float t = 0.f;
+    int c = 0;
+    for (; c + 8 <= chunks; c += 8) {  // independent loads in flight (the sum order stays 0, 1, 2, ...)
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = cnt_slab[(int64_t)(c + u) * K + k];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t += v[u];
+    }
+    for (; c < chunks; ++c) t += cnt_slab[(int64_t)c * K + k];
+    bcnt[k] += t;
   }
 }
 
@@ -457,15 +542,17 @@ template <int DSL>
 static void launch_vq_stats(const float* z, int64_t N, const int64_t* idx, int K, float* ws, float* bsum, float* bcnt,
                             hipStream_t s) {
   const int chunks = vq_stats_chunks(N, K);
-  const int64_t fpc = (N + chunks - 1) / chunks;
+  const int64_t fpc = VQ_CHUNK;
   float* slab = ws + ((vq_partials_floats(N) + 63) & ~(int64_t)63);
   float* cnt_slab = slab + (int64_t)chunks * K * VQ_D;
-  const size_t lds = (size_t)K * DSL * 4 + (size_t)K * 4;
+  constexpr int R = 256 / (DSL / 4);
+  const size_t lds = (size_t)K * DSL * 4 + VQ_CHUNK * 4 + 2 * R * 4 + (size_t)((K + 3) & ~3) * 4 + 2 * R * (DSL / 4) * 16;
   hipLaunchKernelGGL(vq_stats_kernel<DSL>, dim3(chunks, VQ_D / DSL), dim3(256), lds, s, z, N, idx, K, fpc, slab,
                      cnt_slab);
   const int64_t total4 = (int64_t)K * VQ_D / 4;
-  hipLaunchKernelGGL(vq_stats_reduce_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, s, slab, cnt_slab,
-                     chunks, K, bsum, bcnt);
+  unsigned nb = (unsigned)((total4 + 63) / 64);
+  if (nb * 256u < (unsigned)K) nb = (unsigned)((K + 255) / 256);
+  hipLaunchKernelGGL(vq_stats_reduce_kernel, dim3(nb), dim3(256), 0, s, slab, cnt_slab, chunks, K, bsum, bcnt);
 }
 
 extern "C" int vqx_vq_forward(const float* z, int64_t n_rows, int32_t D, const float* E, int32_t K, int64_t* idx,
@@ -473,7 +560,7 @@ extern "C" int vqx_vq_forward(const float* z, int64_t n_rows, int32_t D, const f
                               float* bsum, float* bcnt, vqx_stream_t stream) {
   if (D != VQ_D) { set_error("vqx_vq_forward: only D=128 supported (got %d)", D); return -1; }
   if (K <= 0 || K % 16) { set_error("vqx_vq_forward: K=%d must be a positive multiple of 16", K); return -1; }
-  if (K > 3264) { set_error("vqx_vq_forward: K=%d > 3264", K); return -1; }
+  if (K > 2048) { set_error("vqx_vq_forward: K=%d > 2048", K); return -1; }
   if (n_rows <= 0 || !z || !E || !idx || !partials) { set_error("vqx_vq_forward: bad arguments"); return -1; }
   if (bcnt && !bsum) { set_error("vqx_vq_forward: bcnt needs bsum"); return -1; }
   if (((uintptr_t)z | (uintptr_t)E) & 15) { set_error("vqx_vq_forward: z/E must be 16-byte aligned"); return -1; }
@@ -484,8 +571,6 @@ extern "C" int vqx_vq_forward(const float* z, int64_t n_rows, int32_t D, const f
   if (sqerr_out) hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(1024), 0, s, partials, grid, 1.0f, sqerr_out);
   if (bsum) {
     switch (vq_stats_dsl(K)) {
-      case 128: launch_vq_stats<128>(z, n_rows, idx, K, partials, bsum, bcnt, s); break;
-      case 64: launch_vq_stats<64>(z, n_rows, idx, K, partials, bsum, bcnt, s); break;
       case 32: launch_vq_stats<32>(z, n_rows, idx, K, partials, bsum, bcnt, s); break;
       case 16: launch_vq_stats<16>(z, n_rows, idx, K, partials, bsum, bcnt, s); break;
       case 8: launch_vq_stats<8>(z, n_rows, idx, K, partials, bsum, bcnt, s); break;
