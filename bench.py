@@ -97,7 +97,7 @@ def time_vq(tr, reps):
     eng = tr.engine
     w = eng._ws[(B_PER_GPU, T_FRAMES, True)]
     q = tr.model.quantizer
-    N, D, K = w.N, eng.dims["Z"], eng.dims["K"]
+    N, D, K = w.Nz, eng.dims["Z"], eng.dims["K"]
     args = (w.z, q.embeddings, w.idx, w.zq, w.zq_c, w.stats[1:2], w.vq_part, w.bsum, w.bcnt)
     for _ in range(3):
         ops.vq_forward(*args)

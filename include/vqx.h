@@ -218,6 +218,15 @@ int vqx_gn_glu_fwd_tiles(const void* u, int32_t ldu, void* g, int32_t ldg, int32
                          int32_t T, int32_t C, const float* parts, float eps, float* mean_rstd,
                          const float* gamma, const float* beta, vqx_stream_t stream);
 
+/* GroupNorm(G=1) + LeakyReLU(0.2): g = lrelu((h - mean)*rstd*gamma + beta),
+ * the operand of each further conv of a residual stack with stack_layers > 1
+ * (layers.py:156-161).  h, g [N][ld*] dtype; mean_rstd [B][2] from
+ * vqx_groupnorm_stats / vqx_gn_finalize_tiles.  The backward needs no kernel
+ * of its own: the next conv's DGRAD applies the LeakyReLU derivative with
+ * VQX_EPI_MASK (mask = g, slope 0.2) and vqx_gn_bwd(glu = 0) the GroupNorm. */
+int vqx_gn_lrelu_fwd(const void* h, int32_t ldh, void* g, int32_t ldg, int32_t dtype, int64_t n_rows, int32_t T,
+                     int32_t C, const float* mean_rstd, const float* gamma, const float* beta, vqx_stream_t stream);
+
 /*
  * Backward of GroupNorm(G) optionally preceded by the gated unit:
  *   glu=1: dy is dL/dg [N][C/2], u is the GN input [N][C]: computes dL/dh
@@ -463,7 +472,7 @@ int vqx_probe_count(int64_t* n);
 int vqx_probe_read(int64_t i, int32_t* info5, double* flops, float* ms);
 
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
-#define VQX_ABI_VERSION 116
+#define VQX_ABI_VERSION 117
 int vqx_version(void);
 
 #ifdef __cplusplus

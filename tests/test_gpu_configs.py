@@ -147,3 +147,68 @@ def test_bf16_training_tracks_fp32_over_50_steps(name):
     assert rel.max() < 2e-2, rel
     assert rel[-10:].mean() < 1e-2
     assert abs(b[-1, 1] - f[-1, 1]) <= 2e-2 * abs(f[-1, 1])
+
+
+@pytest.mark.parametrize("name", ["vcc20_multi", "vcc20_multi_plain"])
+def test_fp32_general_topology_matches_reference_golden(name):
+    """The general Encoder/Decoder topology of vqvae.py:
+    two resolution stages -- the encoder down-samples by 2 in its second
+    stage (strided conv, kernel 4, run as a folded 3-tap conv), the decoder
+    up-samples by 2 in its first (strided ConvTranspose, output_padding 0) --
+    dilation 2**j in every residual stack, stack_layers 2 (inner GN +
+    LeakyReLU), the decoder's default kernel_size 5, channel widths 128/256,
+    against the reference's own 3-step run (tests/golden/step_<name>; EMA with
+    jitter 0.12 at the latent rate, and the straight-through quantizer).
+    Bars as the single-stage golden tests: losses 1e-4 at step 1 and 1e-3
+    later (the perplexity 2e-2), indices equal except at the reference's
+    near-ties, step-1 gradient norms 2e-3, parameters after 3 steps 1e-3."""
+    from oracle.vqvae_cpu import seeded_batch
+    meta, arr = load_fixture(f"step_{name}")
+    cfg = cfg_of(name, compute_dtype="fp32")
+    tr = make_trainer(cfg, meta["wseed"])
+    eng = tr.engine
+    assert [st.scale for st in eng.enc_stages] == [1, 2] and [st.scale for st in eng.dec_stages] == [2, 1]
+    torch.manual_seed(meta["tseed"])
+    np.random.seed(meta["nseed"])
+    ema = cfg.get("use_ema", False)
+    for s in range(meta["steps"]):
+        x, y = seeded_batch(cfg, meta["B"], meta["T"], meta["bseed"] + s)
+        _, detail = tr.train_step((x.cuda(), y.cuda()))
+        detail = dict(detail)
+        assert set(detail) == set(meta["detail"][s])
+        for k, v in meta["detail"][s].items():
+            rt = 1e-4 if s == 0 else (2e-2 if k == "entropy" else 1e-3)
+            assert relclose(detail[k], v, rt, 1e-6 if k in ("diff_emb", "VQ loss") else 0.0), (s, k, detail[k], v)
+        if ema:
+            w = eng._ws[(meta["B"], meta["T"], True)]
+            idx = w.idx.cpu().numpy()
+            mism = idx != arr[f"idx{s}"]
+            assert (arr[f"gap{s}"][mism] < 1e-4).all(), (s, int(mism.sum()))
+        if s == 0:
+            for n, p in tr.model.named_parameters():
+                ref = meta["grads"][n]["norm"]
+                gn = float(eng.g(p).double().norm())
+                assert relclose(gn, ref, 2e-3, 1e-9), (n, gn, ref)
+    for n, p in tr.model.named_parameters():
+        assert relclose(float(p.detach().double().norm()), meta["params_after"][n]["norm"], 1e-3), n
+
+
+def test_bf16_general_topology_tracks_oracle():
+    """The general topology in bf16 (the dilated 3-tap and 5-tap layers and the
+    folded resampling convs on bf16 MFMA) tracks the fp32 oracle: losses
+    within 1e-2 over two steps."""
+    from oracle.vqvae_cpu import OracleTrainer, seeded_batch, seeded_state_dict
+    cfg = cfg_of("vcc20_multi", compute_dtype="bf16")
+    tr = make_trainer(cfg, 93)
+    orc = OracleTrainer(dict(cfg), seeded_state_dict(cfg, 93))
+    for s in range(2):
+        x, y = seeded_batch(cfg, 4, 128, 500 + s)
+        torch.manual_seed(40 + s)
+        np.random.seed(40 + s)
+        _, do = orc.train_step((x, y))
+        torch.manual_seed(40 + s)
+        np.random.seed(40 + s)
+        _, dg = tr.train_step((x.cuda(), y.cuda()))
+        dg = dict(dg)
+        assert relclose(dg["X like"], do["X like"], 1e-2), (s, dg, do)
+        assert relclose(dg["VQ loss"], do["VQ loss"], 2e-2, atol=1e-6), (s, dg, do)

@@ -15,7 +15,7 @@ from pathlib import Path
 import torch  # noqa: F401  (loads the HIP runtime first; see module docstring)
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libvqx.so"
-ABI_VERSION = 116  # include/vqx.h VQX_ABI_VERSION
+ABI_VERSION = 117  # include/vqx.h VQX_ABI_VERSION
 
 VQX_F32, VQX_BF16 = 0, 1
 PRO_NONE, PRO_LRELU, PRO_RELU, PRO_SCALE_RELU = 0, 1, 2, 3
@@ -77,6 +77,8 @@ _SIGS = {
     "vqx_weight_norm_bwd": [c_void_p, c_void_p, c_int32, c_void_p],
     "vqx_groupnorm_stats": [c_void_p, c_int32, c_int32, c_int64, c_int32, c_int32, c_int32, c_float, c_void_p,
                             c_void_p, c_void_p],
+    "vqx_gn_lrelu_fwd": [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int64, c_int32, c_int32, c_void_p,
+                         c_void_p, c_void_p, c_void_p],
     "vqx_gn_glu_fwd": [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int64, c_int32, c_int32, c_void_p,
                        c_void_p, c_void_p, c_void_p],
     "vqx_gn_glu_fwd_tiles": [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int64, c_int32, c_int32, c_void_p,

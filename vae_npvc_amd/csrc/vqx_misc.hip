@@ -5,6 +5,8 @@
 #include "vqx_common.h"
 #include <math.h>
 
+#include <algorithm>
+
 namespace vqx {
 
 constexpr float kLog2Pi = 1.8378770664093453f;  // log(2*pi), layers.py:8
@@ -44,6 +46,8 @@ __global__ __launch_bounds__(256) void wn_norm_kernel(const vqx_wn_layer* __rest
 //   segments (64*K contiguous floats per ci) into LDS, write wp[co][j][ci0..]
 //   rows of 64 consecutive ci.
 constexpr int kWnRow = 4096;
+// ConvT pack tile width in co: the LDS tile holds 64 ci x (TCO*K + pad) floats
+__host__ __device__ inline int wn_tco(int K) { return K <= 4 ? 16 : (K <= 64 ? 64 / K : 1); }
 __global__ __launch_bounds__(256) void wn_pack_kernel(const vqx_wn_layer* __restrict__ L, int n_layers) {
   const vqx_wn_layer& l = L[blockIdx.y];
   const int K = l.k, cin = l.cin, cout = l.cout;
@@ -102,11 +106,11 @@ __global__ __launch_bounds__(256) void wn_pack_kernel(const vqx_wn_layer* __rest
     }
     return;
   }
-  // kind 1: tile of 64 ci x 16 co (x K taps) = 64 x 16K floats <= 64 x 48 in LDS
-  constexpr int TCO = 16;
+  // kind 1: tile of 64 ci x TCO co (x K taps) = 64 x TCO*K floats <= 64 x 64 in LDS
+  const int TCO = wn_tco(K);
   const int ntc = (cout + TCO - 1) / TCO;
   const int ci0 = (blockIdx.x / ntc) * 64, co0 = (blockIdx.x % ntc) * TCO;
-  if (ci0 >= cin || K > 3) return;
+  if (ci0 >= cin || K > 64) return;
   const int wseg = TCO * K;  // floats per ci row segment (contiguous in v)
   for (int e = threadIdx.x; e < 64 * wseg; e += 256) {
     const int r = e / wseg, q = e - r * wseg;  // r: ci offset, q = co_local*K + tap
@@ -599,6 +603,33 @@ __global__ __launch_bounds__(256) void gn_glu_fwd_vec_kernel(const T* __restrict
       o[i] = ftanh<sizeof(T) == 2>((ua[i] - ma) * ra * ga[i] + ba[i]) *
              fsigmoid<sizeof(T) == 2>((ub[i] - mb) * rb * gb[i] + bb[i]);
     Vec<T>::store(g + (int64_t)r * ldg + c, o);
+  }
+}
+
+// g = LeakyReLU_0.2(GroupNorm_{G=1}(h)): the LeakyReLU heading each further
+// conv of a residual stack with stack_layers > 1 (layers.py:156-161), one
+// 16-B chunk of V channels per thread.
+template <typename T>
+__global__ __launch_bounds__(256) void gn_lrelu_fwd_kernel(const T* __restrict__ h, int ldh, T* __restrict__ g, int ldg,
+                                                           int64_t n_rows, int T_, int cpr,
+                                                           const float* __restrict__ mr,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta) {
+  constexpr int V = Vec<T>::N;
+  const int64_t total = n_rows * cpr;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / cpr;
+    const int c = (int)(i - r * cpr) * V;
+    const int b = (int)(r / T_);
+    const float m = mr[2 * b], rs = mr[2 * b + 1];
+    float x[V];
+    Vec<T>::load(h + r * ldh + c, x);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const float v = (x[k] - m) * rs * gamma[c + k] + beta[c + k];
+      x[k] = v > 0.f ? v : 0.2f * v;
+    }
+    Vec<T>::store(g + r * ldg + c, x);
   }
 }
 
@@ -1143,14 +1174,14 @@ extern "C" int vqx_weight_norm_fwd(const vqx_wn_layer* lh, const vqx_wn_layer* l
     const int64_t el = (int64_t)l.cout * l.cin * l.k;
     max_el = el > max_el ? el : max_el;
   }
-  // kind 0: one block per row; kind 1: 64 ci x 16 co tiles (after the row norms)
+  // kind 0: one block per row; kind 1: 64 ci x wn_tco(K) co tiles (after the row norms)
   int max_units = 1, max_t_rows = 1;
   for (int i = 0; i < n_layers; ++i) {
     const vqx_wn_layer& l = lh[i];
     const bool rsm = l.kind >= VQX_WN_RESAMPLE;
     const bool row_is_cout = l.kind == 0 || l.kind == VQX_WN_RESAMPLE;
-    if ((row_is_cout ? l.cin : l.cout) * l.k > kWnRow || (!rsm && l.k > 3)) { set_error("vqx_weight_norm_fwd: layer %d row too long", i); return -1; }
-    const int units = rsm ? (row_is_cout ? l.cout : l.cin) : l.kind == 0 ? l.cout : ((l.cin + 63) / 64) * ((l.cout + 15) / 16);
+    if ((row_is_cout ? l.cin : l.cout) * l.k > kWnRow || (!rsm && l.k > 64)) { set_error("vqx_weight_norm_fwd: layer %d row too long", i); return -1; }
+    const int units = rsm ? (row_is_cout ? l.cout : l.cin) : l.kind == 0 ? l.cout : ((l.cin + 63) / 64) * ((l.cout + wn_tco(l.k) - 1) / wn_tco(l.k));
     max_units = units > max_units ? units : max_units;
     if (l.kind == 1) max_t_rows = l.cin > max_t_rows ? l.cin : max_t_rows;
   }
@@ -1244,6 +1275,28 @@ static int gn_glu_fwd_impl(const void* u, int32_t ldu, void* g, int32_t ldg, int
   else
     hipLaunchKernelGGL(gn_glu_fwd_vec_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)u, ldu, (float*)g, ldg, (int)n_rows, T, C / 2, cpr, mean_rstd, gamma, beta, tiles, eps, mr_out);
   return launch_status("vqx_gn_glu_fwd");
+}
+
+extern "C" int vqx_gn_lrelu_fwd(const void* h, int32_t ldh, void* g, int32_t ldg, int32_t dtype, int64_t n_rows,
+                                int32_t T, int32_t C, const float* mean_rstd, const float* gamma, const float* beta,
+                                vqx_stream_t stream) {
+  const int V = dtype == VQX_BF16 ? 8 : 4;
+  if (!h || !g || !mean_rstd || !gamma || !beta || T < 1 || n_rows % T || C % V || ldh % V || ldg % V ||
+      (((uintptr_t)h | (uintptr_t)g) & 15)) {
+    set_error("vqx_gn_lrelu_fwd: bad arguments (C, strides multiples of %d, 16-B aligned)", V);
+    return -1;
+  }
+  const int cpr = C / V;
+  const int64_t total = n_rows * cpr;
+  const int grid = (int)std::min<int64_t>((total + 255) / 256, 4096);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == VQX_BF16)
+    hipLaunchKernelGGL(gn_lrelu_fwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)h, ldh, (bf16_t*)g, ldg,
+                       n_rows, T, cpr, mean_rstd, gamma, beta);
+  else
+    hipLaunchKernelGGL(gn_lrelu_fwd_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)h, ldh, (float*)g, ldg,
+                       n_rows, T, cpr, mean_rstd, gamma, beta);
+  return launch_status("vqx_gn_lrelu_fwd");
 }
 
 extern "C" int vqx_gn_bwd(const void* dy, int32_t lddy, const void* u, int32_t ldu, void* du, int32_t lddu,

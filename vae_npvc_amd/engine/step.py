@@ -4,18 +4,22 @@ torch's current stream; torch is used only for device memory and streams.
 
 Step anatomy (frame-major activations [N = B*T, C], see include/vqx.h):
 
-  pack     weight norm of all 44 convs -> packed effective weights (1 launch pair)
-  encoder  conv0 | 10 x {k3 conv -> GN stats -> 1x1 skip conv with the
-           GroupNorm-apply + residual fused in its epilogue} | 1x1 out conv
-           (f32 out).  Each GEMM producing c_i also stores LeakyReLU(c_i), so
-           no GEMM applies an activation to its staged operands
-                                                                 (vqvae.py:185-192)
-  vq       fused distance/argmin/gather/commitment/EMA-statistics kernel
+  pack     weight norm of every conv -> packed effective weights (1 launch pair)
+  encoder  per resolution stage: stage conv (stride 1, or the strided
+           down-sampler run as a 3-tap conv on s-frame-folded rows) | blocks
+           {stack_layers x (conv (dilation 2**j on the first) -> GN stats
+           [-> GN + LeakyReLU]) -> 1x1 skip conv with the last GroupNorm-apply
+           + residual fused in its epilogue} | 1x1 out conv (f32 out).  Each
+           GEMM producing c also stores LeakyReLU(c), so no GEMM applies an
+           activation to its staged operands                      (vqvae.py:122-217)
+  vq       distance/argmin/gather/commitment kernel + EMA statistics
                                                                  (layers_vq.py:268-323)
-  decoder  ConvT0 | 10 x {ConvT k3 (+ speaker term as a per-utterance row bias)
-           -> GN stats -> GN+tanh*sigmoid -> 1x1 res/skip conv with the
-           residual add and the skip accumulation split in its epilogue} |
-           ReLU(s*skip) -> 1x1 (ReLU epilogue) -> 1x1            (vqvae.py:298-318)
+  decoder  per stage: ConvT (stride 1, or the strided up-sampler run as the
+           adjoint of a folded 3-tap conv) | blocks {ConvT k (dilation 2**j;
+           + speaker term as a per-utterance row bias) -> GN stats ->
+           GN+tanh*sigmoid -> 1x1 res/skip conv with the residual add and the
+           skip accumulation split in its epilogue} |
+           ReLU(s*skip) -> 1x1 (ReLU epilogue) -> 1x1            (vqvae.py:220-343)
   loss     log-likelihood + its gradient in one pass            (layers.py:283-296)
   backward encoder (driven only by beta*commitment, the reference quirk:
            z_vq carries no gradient, layers_vq.py:315) and decoder: dgrad GEMMs
@@ -23,13 +27,19 @@ Step anatomy (frame-major activations [N = B*T, C], see include/vqx.h):
            reduced by the weight-norm backward, GN backward (2 passes).
   update   global grad norm -> fused clip + Adam (+ StepLR on device); EMA codebook.
 
+The recipe topologies (one stage, stack_layers 1, no dilation, kernel 3) run
+exactly the fused schedule tuned for them; the general topology of vqvae.py
+(several stages, resampling, dilation, stack_layers > 1, kernel 5) runs the
+same kernels with the fusions that stay valid for each stage's shape.
+
 The engine owns flat fp32 buffers for parameters, gradients and Adam moments;
 model parameters are views into them, so `model.state_dict()` stays the
 reference's and the optimizer touches one contiguous buffer.
 """
+import bisect
 import math
 import os
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import numpy as np
 import torch
@@ -38,29 +48,87 @@ from .. import _lib as L
 from .. import ops
 
 F32 = torch.float32
+KIND_CONV, KIND_CONVT, KIND_DOWN, KIND_UP = 0, 1, 3, 4
 
 
-@dataclass
+@dataclass(eq=False)
 class ConvLayer:
-    mod: object          # WNConv1d
+    """One conv of the model as the stride-1 GEMM it runs as.
+    kind 0 Conv1d / 1 ConvTranspose1d (flipped-tap conv, pad (k-1)*dil - p) /
+    3 strided Conv1d (down-sampler) / 4 strided ConvTranspose1d (up-sampler):
+    kinds 3-4 fold `scale` frames into channels (x'[u] = x[s*u .. s*u+s-1])
+    and run a 3-tap, pad-1 conv (include/vqx.h VQX_WN_RESAMPLE)."""
+    mod: object
     name: str
-    kind: int            # 0 Conv1d, 1 ConvTranspose1d
-    cin: int             # effective-conv input channels
-    cout: int            # effective-conv output channels
+    kind: int
+    cin: int
+    cout: int
     k: int
     pad: int
-    wp: torch.Tensor = None     # packed effective weight [cout, k*cin]
+    dil: int = 1
+    scale: int = 1
+    wp: torch.Tensor = None     # packed effective weight [rows, cols] (kinds 0/1: [cout, k*cin])
     norm: torch.Tensor = None   # ||v_o||
     slab: torch.Tensor = None   # wgrad partials [splits, rows, cols]
     splits: int = 1
+    btile: torch.Tensor = None  # kind 4: bias tiled over the s folded frames [s*cout]
 
     @property
     def rows(self):
-        return self.cin if self.kind == 1 else self.cout
+        return self.cin if self.kind in (KIND_CONVT, KIND_UP) else self.cout
 
     @property
     def cols(self):
-        return (self.cout if self.kind == 1 else self.cin) * self.k
+        if self.kind == KIND_DOWN:
+            return 3 * self.scale * self.cin
+        if self.kind == KIND_UP:
+            return 3 * self.scale * self.cout
+        return (self.cout if self.kind == KIND_CONVT else self.cin) * self.k
+
+
+@dataclass
+class EncBlock:
+    """Conv1d_Layernorm_LRelu_Residual (layers.py:129-178)."""
+    key: tuple
+    convs: list
+    gns: list
+    skip: ConvLayer
+
+
+@dataclass
+class EncStage:
+    conv: ConvLayer
+    scale: int
+    C: int
+    blocks: list = field(default_factory=list)
+    L: int = 1
+
+
+@dataclass
+class DecBlock:
+    """DeConv1d_Layernorm_GLU_ResSkip (layers.py:181-249)."""
+    key: tuple
+    gidx: int            # position among all decoder blocks (skip accumulation order)
+    conv_in: ConvLayer
+    gn: object
+    cond: ConvLayer
+    rs: ConvLayer
+
+
+@dataclass
+class DecStage:
+    conv: ConvLayer
+    scale: int
+    C: int
+    blocks: list = field(default_factory=list)
+
+
+def _tm(N):
+    return (N + L.CONV_TILE_ROWS - 1) // L.CONV_TILE_ROWS
+
+
+class _Stage:
+    """Per-stage activation buffers of a Workspace."""
 
 
 class Workspace:
@@ -68,89 +136,127 @@ class Workspace:
 
     def __init__(self, eng, B, T, train=True):
         d, cd, dev = eng.dims, eng.cd, eng.device
-        N = B * T
-        self.B, self.T, self.N = B, T, N
+        self.B, self.T, self.N = B, T, B * T
         e = lambda *s, dt=cd: torch.empty(*s, device=dev, dtype=dt)  # noqa: E731
-        C, Z, Cd, S, Fo, mel = d["C"], d["Z"], d["Cd"], d["S"], d["F"], d["mel"]
-        ns, nd, K, D = d["ns"], d["nd"], d["K"], d["Z"]
-        self.x = e(N, mel)
-        self.c = [e(N, C) for _ in range(ns + 1)]
-        self.a = [e(N, C) for _ in range(ns + 1)]   # LeakyReLU(c_i), written by the producing GEMM (ACT2)
-        self.h = [e(N, C) for _ in range(ns)]
-        self.enc_mr = e(ns, B, 2, dt=F32)
-        self.z = e(N, Z, dt=F32)
-        self.idx = torch.empty(N, device=dev, dtype=torch.int64)
-        self.zq = e(N, Z, dt=F32)
-        self.zq_c = e(N, Z)
-        self.zq_j = e(N, Z) if d["jitter_p"] > 0 else None
-        self.src_t = torch.empty(T, device=dev, dtype=torch.int32)
+        Z, S, Fo, mel, K = d["Z"], d["S"], d["F"], d["mel"], d["K"]
+        fuse_env = os.environ.get("VQX_FUSE_GN", "1") != "0"
+        self.x = e(self.N, mel)
+        # ---- encoder stages
+        self.enc = []
+        Tc = T
+        for st in eng.enc_stages:
+            if Tc % st.scale:
+                raise ValueError(f"utterance length {Tc} is not a multiple of the down-sampling scale {st.scale}")
+            Tc //= st.scale
+            sw = _Stage()
+            sw.T, sw.N, sw.C = Tc, B * Tc, st.C
+            N, C, nb = sw.N, sw.C, len(st.blocks)
+            sw.c = [e(N, C) for _ in range(nb + 1)]
+            sw.a = [e(N, C) for _ in range(nb + 1)]   # LeakyReLU(c_j), written by the producing GEMM (ACT2)
+            sw.h = [[e(N, C) for _ in range(st.L)] for _ in range(nb)]
+            sw.g = [[e(N, C) for _ in range(st.L - 1)] for _ in range(nb)]  # LeakyReLU(GN(h)) of inner layers
+            sw.mr = [[e(B, 2, dt=F32) for _ in range(st.L)] for _ in range(nb)]
+            sw.fuse = Tc % 128 == 0 and C % 128 == 0 and fuse_env
+            if train:
+                # colsum partials of dL/dc_j (the producing dgrad's COLSUM epilogue)
+                sw.cs = [e(_tm(N), C, dt=F32) for _ in range(nb + 1)]
+            self.enc.append(sw)
+        self.Tz, self.Nz = Tc, B * Tc
+        Nz = self.Nz
+        self.z = e(Nz, Z, dt=F32)
+        self.idx = torch.empty(Nz, device=dev, dtype=torch.int64)
+        self.zq = e(Nz, Z, dt=F32)
+        self.zq_c = e(Nz, Z)
+        self.zq_j = e(Nz, Z) if d["jitter_p"] > 0 else None
+        self.src_t = torch.empty(Tc, device=dev, dtype=torch.int32)
         self.jittered = False
         if eng.plain:  # straight-through quantizer: normalised frames / codebook and their norms
-            self.z_norm = e(N, Z, dt=F32)
-            self.z_len = e(N, dt=F32)
+            self.z_norm = e(Nz, Z, dt=F32)
+            self.z_len = e(Nz, dt=F32)
             self.embn = e(K, Z, dt=F32)
             self.e_len = e(K, dt=F32)
-            self.pv_part = e(N // 4 + 8, dt=F32)
-        self.vq_part = e(ops.vq_workspace(N, K, True), dt=F32)  # VQ partials + EMA-statistics slabs
+            self.pv_part = e(Nz // 4 + 8, dt=F32)
+        self.vq_part = e(ops.vq_workspace(Nz, K, True), dt=F32)  # VQ partials + EMA-statistics slabs
         # EMA statistics bundle (all-reduced as one buffer in data parallel)
-        self.ema = e(K * D + K + K * D, dt=F32)
-        self.bsum = self.ema[: K * D].view(K, D)
-        self.bcnt = self.ema[K * D: K * D + K]
-        self.rand_rows = self.ema[K * D + K:].view(K, D)
-        self.ema_part = e((K * D + 1023) // 1024, dt=F32)  # vqx_vq_ema_update workspace
+        self.ema = e(K * Z + K + K * Z, dt=F32)
+        self.bsum = self.ema[: K * Z].view(K, Z)
+        self.bcnt = self.ema[K * Z: K * Z + K]
+        self.rand_rows = self.ema[K * Z + K:].view(K, Z)
+        self.ema_part = e((K * Z + 1023) // 1024, dt=F32)  # vqx_vq_ema_update workspace
         self.yemb = e(B, d["ydim"], dt=F32)
-        self.condbias = e(nd, B, 2 * Cd, dt=F32)
-        self.xs = [e(N, Cd) for _ in range(nd + 1)]
-        self.u = [e(N, 2 * Cd) for _ in range(nd)]
-        self.g = [e(N, Cd) for _ in range(nd)]
-        self.dec_mr = e(nd, B, 4, dt=F32)
-        self.skip32 = e(N, S, dt=F32)
-        self.a_skip = e(N, S)                       # ReLU(sqrt(1/(nd+1)) * skip)
-        self.f1 = e(N, S)                           # ReLU(final conv 1 output)
-        self.xhat = e(N, Fo, dt=F32)
+        # ---- decoder stages
+        self.dec = []
+        Td = Tc
+        for st in eng.dec_stages:
+            Td *= st.scale
+            sw = _Stage()
+            sw.T, sw.N, sw.C = Td, B * Td, st.C
+            N, C, nb = sw.N, sw.C, len(st.blocks)
+            sw.xs = [e(N, C) for _ in range(nb + 1)]
+            sw.u = [e(N, 2 * C) for _ in range(nb)]
+            sw.g = [e(N, C) for _ in range(nb)]
+            sw.mr = [e(B, 4, dt=F32) for _ in range(nb)]
+            sw.condbias = [e(B, 2 * C, dt=F32) for _ in range(nb)]
+            sw.fuse = Td % 128 == 0 and C % 128 == 0 and fuse_env
+            if train:
+                sw.dr = [e(N, C + S) for _ in range(2)] if nb else None   # [dL/dx | dL/dskip] ping-pong
+                sw.dx = e(N, C) if not nb else None                        # stages without blocks
+                sw.cs = [e(_tm(N), C, dt=F32) for _ in range(nb + 1)]     # colsum partials of dL/dx_j
+                sw.cs_all = [e(B, 2 * C, dt=F32) for _ in range(nb)]      # per-utterance colsums of du
+            self.dec.append(sw)
+        if Td != T:
+            raise ValueError(f"decoder output length {Td} != input length {T} (resampling scales do not cancel)")
+        if eng.n_dec_blocks:
+            Ts = self.dec[eng.skip_stage].T
+            if any(sw.T != Ts for sw, st in zip(self.dec, eng.dec_stages) if st.blocks):
+                raise ValueError("the decoder sums the skip outputs of all blocks: they must share one frame rate")
+        self.Nskip = B * T
+        self.skip32 = e(self.Nskip, S, dt=F32)
+        self.a_skip = e(self.Nskip, S)                 # ReLU(sqrt(1/len(layers)) * skip)
+        self.f1 = e(self.Nskip, S)                     # ReLU(final conv 1 output)
+        self.xhat = e(self.N, Fo, dt=F32)
         self.xhat_nct = e(B, Fo, T, dt=F32)
         # scalars: 0 x_loss, 1 sqerr, 4..7 EMA diagnostics
         self.stats = torch.zeros(8, device=dev, dtype=F32)
         # GroupNorm partials written by GEMM epilogues (GNSTATS / GNBWD tiles:
         # [N/128][column tile][4]) when T and the group widths are multiples of 128
-        self.fuse_gn = (T % 128 == 0 and C % 128 == 0 and Cd % 128 == 0
-                        and os.environ.get("VQX_FUSE_GN", "1") != "0")
-        self.gn_rg = N // 128 if self.fuse_gn else 0
-        self.gst = e(max(1, self.gn_rg) * ((max(C, 2 * Cd) + 127) // 128) * 4, dt=F32)
+        Cmax = max([sw.C for sw in self.enc] + [2 * sw.C for sw in self.dec] + [1])
+        Nmax = max([sw.N for sw in self.enc] + [sw.N for sw in self.dec] + [self.N])
+        self.gst = e(max(1, Nmax // 128) * ((Cmax + 127) // 128) * 4, dt=F32)
         self.loss_part = e(1024, dt=F32)
         self.gn_part = e(B * 2 * 8 * 3, dt=F32)
         if not train:
             return
-        self.dxhat = e(N, Fo)
-        self.df1 = e(N, S)
-        self.dr = [e(N, Cd + S) for _ in range(2)]
-        self.dg = e(N, Cd)
-        self.du = e(N, 2 * Cd)
-        self.gnb_part = e(max(B * 64 * 2, max(1, self.gn_rg) * ((max(C, Cd) + 127) // 128) * 4), dt=F32)
-        self.colsum_b = e(B * 2 * max(Cd, C), dt=F32)   # per-utterance column sums of du
-        self.dgam_b = e(B * 2 * max(Cd, C), dt=F32)
-        self.dbet_b = e(B * 2 * max(Cd, C), dt=F32)
-        self.dz = e(N, Z)
-        self.dzq = e(N, Z) if eng.plain else None  # decoder gradient w.r.t. its (jittered) input
-        self.dc = [e(N, C) for _ in range(2)]
-        self.dh = e(N, C)
-        self.tmp = e(N, C)
+        NCe = max([sw.N * sw.C for sw in self.enc] + [1])
+        self.dxhat = e(self.N, Fo)
+        self.df1 = e(self.Nskip, S)
+        NCd = max([sw.N * sw.C for sw in self.dec] + [1])
+        self.dg_flat = e(NCd)
+        self.du_flat = e(2 * NCd)
+        self.gnb_part = e(max(B * 64 * 2, max(1, Nmax // 128) * ((Cmax + 127) // 128) * 4), dt=F32)
+        Lmax = max([st.L for st in eng.enc_stages] + [1])
+        # per-utterance GN-backward sums per stack layer: conv bias, GN weight, GN bias
+        self.colsum_b = [e(B * 2 * Cmax, dt=F32) for _ in range(Lmax)]
+        self.dgam_b = [e(B * 2 * Cmax, dt=F32) for _ in range(Lmax)]
+        self.dbet_b = [e(B * 2 * Cmax, dt=F32) for _ in range(Lmax)]
+        self.dz = e(Nz, Z)
+        self.dzq = e(Nz, Z) if eng.plain else None  # decoder gradient w.r.t. its (jittered) input
+        self.dc_flat = [e(NCe) for _ in range(2)]   # encoder dL/dc ping-pong (viewed per stage)
+        self.dh_flat = e(NCe)
+        self.dy_flat = e(NCe)                       # inner-layer gradients (stack_layers > 1)
+        self.tmp_flat = e(NCe)
         self.dyemb = e(B, d["ydim"], dt=F32)
-        self.cs_part = e(64 * max(C, 2 * Cd, Cd + S, mel, 1024), dt=F32)
-        # bias-gradient partials: GEMM COLSUM epilogues write [row tile][C]
-        # sums of the gradient they produce; the group's weight-norm backward
-        # launch reduces them (VQX_WN_COLREDUCE entries)
-        tm = (N + L.CONV_TILE_ROWS - 1) // L.CONV_TILE_ROWS
-        self.cs_enc = [e(tm, C, dt=F32) for _ in range(2)]   # dL/dc_i (ping-pong)
-        self.cs_dec = [e(tm, Cd, dt=F32) for _ in range(2)]  # dL/dx_i (ping-pong)
-        self.cs_skip = e(tm, S, dt=F32)                      # dL/dskip
-        self.cs_f1 = e(tm, S, dt=F32)                        # dL/d(final conv 1 output)
-        # per-utterance column sums of du per decoder block: conv_in and
-        # conv_cond bias gradients, and dout of the batched conditioning backward
-        self.cs_all = e(nd, B, 2 * Cd, dt=F32)
-        O = 2 * Cd
-        self.lin_part = e(nd * ((O + 63) // 64) * B * d["ydim"], dt=F32)  # split-K partials of d(embedding)
+        self.cs_part = e(64 * max(Cmax, S + Cmax, mel, 1024), dt=F32)
+        self.cs_skip = e(_tm(self.Nskip), S, dt=F32)  # dL/dskip
+        self.cs_f1 = e(_tm(self.Nskip), S, dt=F32)    # dL/d(final conv 1 output)
+        self.lin_part = e(max(len(g) * ((O + 63) // 64) for O, g in eng.cond_groups.items()) * B * d["ydim"]
+                          if eng.cond_groups else 1, dt=F32)  # split-K partials of d(embedding)
         eng._build_bwd_tables(self)
+
+    # flat scratch viewed at a stage's shape
+    @staticmethod
+    def view(flat, N, C):
+        return flat[: N * C].view(N, C)
 
 
 class VQVAEEngine:
@@ -161,9 +267,9 @@ class VQVAEEngine:
         self.dt = ops.dt_code(self.cd)
         L.load()
         enc, dec = model.encoder, model.decoder
-        self.dims = d = dict(mel=enc.in_ch, C=enc.ch, Z=enc.z_ch, ns=enc.n_stacks, Cd=dec.ch, S=dec.skip_ch,
-                             F=dec.final_ch, cond=dec.cond_ch, nd=dec.n_stacks, K=model.quantizer.z_num,
-                             ydim=model.embeds._embedding.weight.shape[1], jitter_p=model.jitter.probability)
+        self.dims = d = dict(mel=enc.in_ch, Z=enc.z_ch, S=dec.skip_ch, F=dec.final_ch, cond=dec.cond_ch,
+                             K=model.quantizer.z_num, ydim=model.embeds._embedding.weight.shape[1],
+                             jitter_p=model.jitter.probability)
         assert d["Z"] == 128 and model.quantizer.z_dim == 128, "the fused VQ kernel is built for z_dim = 128"
         # straight-through VectorQuantizer (use_ema: false)
         self.plain = not model.use_ema
@@ -217,7 +323,6 @@ class VQVAEEngine:
     def _params_written(self, tensors):
         """Indices (flat order) of the parameters whose gradient views overlap
         any of `tensors` (views into flat_g; None entries are skipped)."""
-        import bisect
         base = self.flat_g.data_ptr()
         hit = set()
         for t in tensors:
@@ -263,54 +368,133 @@ class VQVAEEngine:
                     self._g_issued[k] = True
             i = j
 
-    def _build_layers(self):
-        m, d, dev = self.m, self.dims, self.device
-        enc, dec = m.encoder.encode, m.decoder
-        ns, nd = d["ns"], d["nd"]
-
-        def mk(mod, name, dtype=None):
-            kind = 1 if mod.transposed else 0
-            Lr = ConvLayer(mod, name, kind, mod.cin, mod.cout, mod.k, mod.k - 1 - mod.padding if kind else mod.padding)
+    # ------------------------------------------------------------ layers
+    def _mk(self, mod, name, dtype=None):
+        from ..model.resample import ResampleConv1d
+        dev = self.device
+        if isinstance(mod, ResampleConv1d):
+            Lr = ConvLayer(mod, name, KIND_UP if mod.transposed else KIND_DOWN, mod.cin, mod.cout, 3, 1, 1,
+                           mod.scale)
+            Lr.wp = torch.empty(Lr.rows, Lr.cols, device=dev, dtype=dtype or self.cd)
+            if Lr.kind == KIND_UP:
+                Lr.btile = torch.empty(mod.scale * mod.cout, device=dev, dtype=F32)
+        else:
+            kind = KIND_CONVT if mod.transposed else KIND_CONV
+            dil = getattr(mod, "dilation", 1)
+            pad = (mod.k - 1) * dil - mod.padding if kind == KIND_CONVT else mod.padding
+            if 2 * pad != (mod.k - 1) * dil:
+                raise NotImplementedError(f"{name}: asymmetric padding (the output length would change)")
+            Lr = ConvLayer(mod, name, kind, mod.cin, mod.cout, mod.k, pad, dil)
             Lr.wp = torch.empty(Lr.cout, Lr.k * Lr.cin, device=dev, dtype=dtype or self.cd)
-            Lr.norm = torch.empty(Lr.rows, device=dev, dtype=F32)
-            return Lr
+        Lr.norm = torch.empty(Lr.rows, device=dev, dtype=F32)
+        return Lr
 
-        self.enc0 = mk(enc[0], "encoder.encode.0")
-        self.enc_k3 = [mk(enc[i].stack[1], f"encoder.encode.{i}.stack.1") for i in range(1, ns + 1)]
-        self.enc_gn = [enc[i].stack[2] for i in range(1, ns + 1)]
-        self.enc_sk = [mk(enc[i].skip_layer, f"encoder.encode.{i}.skip_layer") for i in range(1, ns + 1)]
-        self.enc_out = mk(enc[ns + 2], f"encoder.encode.{ns + 2}")
-        self.dec0 = mk(dec.layers[0], "decoder.layers.0")
-        self.dec_in = [mk(dec.layers[i].conv_in, f"decoder.layers.{i}.conv_in") for i in range(1, nd + 1)]
-        self.dec_gn = [dec.layers[i].norm_layer for i in range(1, nd + 1)]
-        self.dec_cond = [mk(dec.layers[i].conv_cond, f"decoder.layers.{i}.conv_cond", F32) for i in range(1, nd + 1)]
-        self.dec_rs = [mk(dec.layers[i].res_skip_layers, f"decoder.layers.{i}.res_skip_layers")
-                       for i in range(1, nd + 1)]
-        self.fin1 = mk(dec.final_layer[1], "decoder.final_layer.1")
-        self.fin2 = mk(dec.final_layer[3], "decoder.final_layer.3")
-        self.convs = ([self.enc0] + [x for pair in zip(self.enc_k3, self.enc_sk) for x in pair] + [self.enc_out, self.dec0]
-                      + [x for tr in zip(self.dec_in, self.dec_cond, self.dec_rs) for x in tr] + [self.fin1, self.fin2])
+    def _build_layers(self):
+        m, d = self.m, self.dims
+        from ..model.layers import ResidualBlock
+        enc_seq, dec_layers = m.encoder.encode, m.decoder.layers
+        # ---- encoder stages
+        self.enc_stages = []
+        starts = list(m.encoder.stage_index)
+        for si, i0 in enumerate(starts):
+            conv = self._mk(enc_seq[i0], f"encoder.encode.{i0}")
+            st = EncStage(conv, conv.scale, conv.cout)
+            i = i0 + 1
+            while i < len(enc_seq) and isinstance(enc_seq[i], ResidualBlock):
+                blk = enc_seq[i]
+                pre = f"encoder.encode.{i}"
+                convs = [self._mk(c, f"{pre}.stack.{3 * l + 1}") for l, c in enumerate(blk.convs)]
+                st.blocks.append(EncBlock(("enc", si, len(st.blocks)), convs, list(blk.norms),
+                                          self._mk(blk.skip_layer, f"{pre}.skip_layer")))
+                st.L = blk.layers
+                i += 1
+            self.enc_stages.append(st)
+        self.enc_out = self._mk(enc_seq[len(enc_seq) - 1], f"encoder.encode.{len(enc_seq) - 1}")
+        # ---- decoder stages
+        self.dec_stages = []
+        starts = list(m.decoder.stage_index) + [len(dec_layers)]
+        gidx = 0
+        for si in range(len(starts) - 1):
+            i0 = starts[si]
+            conv = self._mk(dec_layers[i0], f"decoder.layers.{i0}")
+            st = DecStage(conv, conv.scale, conv.cout)
+            for i in range(i0 + 1, starts[si + 1]):
+                blk = dec_layers[i]
+                pre = f"decoder.layers.{i}"
+                st.blocks.append(DecBlock(("dec", si, len(st.blocks)), gidx, self._mk(blk.conv_in, f"{pre}.conv_in"),
+                                          blk.norm_layer, self._mk(blk.conv_cond, f"{pre}.conv_cond", F32),
+                                          self._mk(blk.res_skip_layers, f"{pre}.res_skip_layers")))
+                gidx += 1
+            self.dec_stages.append(st)
+        self.n_dec_blocks = gidx
+        self.n_dec_layers = len(dec_layers)      # vqvae.py:316 scales by sqrt(1/len(self.layers))
+        with_blocks = [i for i, st in enumerate(self.dec_stages) if st.blocks]
+        if not with_blocks:
+            raise NotImplementedError("decoder without ResSkip blocks (no skip outputs to sum)")
+        if with_blocks[-1] != len(self.dec_stages) - 1:
+            raise NotImplementedError("decoder whose last stage has no ResSkip blocks (its output is unused)")
+        self.skip_stage = with_blocks[0]
+        self.fin1 = self._mk(m.decoder.final_layer[1], "decoder.final_layer.1")
+        self.fin2 = self._mk(m.decoder.final_layer[3], "decoder.final_layer.3")
+        self.dec_blocks = [b for st in self.dec_stages for b in st.blocks]
+        self.dec_cond = [b.cond for b in self.dec_blocks]
+        # speaker-conditioning linears grouped by output width (one batched launch per group)
+        self.cond_groups = {}
+        for b in self.dec_blocks:
+            self.cond_groups.setdefault(b.cond.cout, []).append(b)
+        self.convs = [st.conv for st in self.enc_stages]
+        for st in self.enc_stages:
+            for b in st.blocks:
+                self.convs += b.convs + [b.skip]
+        self.convs += [self.enc_out] + [st.conv for st in self.dec_stages]
+        for b in self.dec_blocks:
+            self.convs += [b.conv_in, b.cond, b.rs]
+        self.convs += [self.fin1, self.fin2]
         # split-K factors for the wgrad GEMMs: one full round of ~480-512
         # workgroups (2 per CU) at config 2 (64 x 256 frames), at least 4
         # K-tiles (256 frames) per split.  Measured sweep (tools/gemm_bench.py
         # --sweep-splits) on 128 x 128 tiles: dec_in best at 5, enc k3 at 10,
         # res/skip at 24, enc skip at 32 -- exactly floor(512 / tiles).  The
         # tile count comes from the library (3-tap layers use the tap-reuse
-        # kernel's 128 x 192 tiles).
-        N_ref, T_ref = 64 * 256, 256
+        # kernel's 128 x 192 tiles).  Frame counts follow each stage's rate.
         wg_target = int(os.environ.get("VQX_WGRAD_WGS", "512"))  # A/B knobs: workgroups per wgrad launch
         wg_1x1 = int(os.environ.get("VQX_WGRAD_WGS_1X1", str(wg_target)))  # ... for the 1x1 layers
+        B_ref, T_ref = 64, 256
+        rate = {}
+        Tc = T_ref
+        for st in self.enc_stages:
+            Tc //= max(1, st.scale)
+            rate[id(st.conv)] = (Tc, Tc * st.scale)   # (output frames, input frames) per utterance
+            for b in st.blocks:
+                for Lr in b.convs + [b.skip]:
+                    rate[id(Lr)] = (Tc, Tc)
+        rate[id(self.enc_out)] = (Tc, Tc)
+        for st in self.dec_stages:
+            rate[id(st.conv)] = (Tc * st.scale, Tc)
+            Tc *= st.scale
+            for b in st.blocks:
+                for Lr in (b.conv_in, b.cond, b.rs):
+                    rate[id(Lr)] = (Tc, Tc)
+        rate[id(self.fin1)] = rate[id(self.fin2)] = (T_ref, T_ref)
         for Lr in self.convs:
             if Lr in self.dec_cond:
                 Lr.splits = 1
                 continue
-            r, c = (Lr.cin, Lr.cout) if Lr.kind else (Lr.cout, Lr.cin)
-            tiles = ops.wgrad_tiles(N_ref, T_ref, r, c, Lr.k, Lr.pad, self.dt)
-            Lr.splits = max(1, min((wg_1x1 if Lr.k == 1 else wg_target) // tiles, N_ref // 256))
+            To, Ti = rate[id(Lr)]
+            To, Ti = max(1, To), max(1, Ti)
+            if Lr.kind == KIND_DOWN:
+                n, T_, r, c, k, pad, dil = B_ref * To, To, Lr.cout, Lr.scale * Lr.cin, 3, 1, 1
+            elif Lr.kind == KIND_UP:
+                n, T_, r, c, k, pad, dil = B_ref * Ti, Ti, Lr.cin, Lr.scale * Lr.cout, 3, 1, 1
+            else:
+                r, c = (Lr.cin, Lr.cout) if Lr.kind == KIND_CONVT else (Lr.cout, Lr.cin)
+                n, T_, k, pad, dil = B_ref * To, To, Lr.k, Lr.pad, Lr.dil
+            tiles = ops.wgrad_tiles(n, T_, r, c, k, pad, self.dt, dil=dil)
+            Lr.splits = max(1, min((wg_1x1 if Lr.k == 1 else wg_target) // tiles, n // 256))
         # slab arena: one backward group's slabs at a time (kept L2/MALL-resident)
         groups = self._bwd_groups()
         arena = max(sum(Lr.splits * Lr.rows * Lr.cols for Lr in grp) for grp in groups)
-        self.arena = torch.empty(arena, device=dev, dtype=F32)
+        self.arena = torch.empty(arena, device=self.device, dtype=F32)
         for grp in groups:
             off = 0
             for Lr in grp:
@@ -321,21 +505,30 @@ class VQVAEEngine:
         self.groups = groups
 
     def _bwd_groups(self):
-        ns, nd = self.dims["ns"], self.dims["nd"]
         gr = [[self.fin1, self.fin2]]
-        gr += [[self.dec_in[i], self.dec_rs[i]] for i in range(nd)]
-        gr += [list(self.dec_cond), [self.dec0], [self.enc_out]]
-        gr += [[self.enc_k3[i], self.enc_sk[i]] for i in range(ns)]
-        gr += [[self.enc0]]
+        for st in reversed(self.dec_stages):
+            gr += [[b.conv_in, b.rs] for b in reversed(st.blocks)]
+            gr += [[st.conv]]
+        gr += [list(self.dec_cond), [self.enc_out]]
+        for st in reversed(self.enc_stages):
+            gr += [b.convs + [b.skip] for b in reversed(st.blocks)]
+            gr += [[st.conv]]
         return gr
 
     def _wn_entry(self, Lr, bwd):
         mod = Lr.mod
-        wn = mod.has_weight_norm
-        v = mod.weight_v if wn else mod.weight
-        e = dict(v=v, g=mod.weight_g if wn else None, w_packed=Lr.wp, norm=Lr.norm, kind=Lr.kind, cout=Lr.cout,
-                 cin=Lr.cin, k=Lr.k, dtype=ops.dt_code(Lr.wp.dtype), splits=Lr.splits)
+        if Lr.kind in (KIND_DOWN, KIND_UP):
+            e = dict(v=mod.weight_v, g=mod.weight_g, w_packed=Lr.wp, norm=Lr.norm,
+                     kind=L.WN_RESAMPLE_T if Lr.kind == KIND_UP else L.WN_RESAMPLE, cout=mod.cout, cin=mod.cin,
+                     k=mod.k, dtype=ops.dt_code(Lr.wp.dtype), splits=Lr.splits, stride=mod.scale, pad=mod.padding)
+            wn = True
+        else:
+            wn = mod.has_weight_norm
+            v = mod.weight_v if wn else mod.weight
+            e = dict(v=v, g=mod.weight_g if wn else None, w_packed=Lr.wp, norm=Lr.norm, kind=Lr.kind, cout=Lr.cout,
+                     cin=Lr.cin, k=Lr.k, dtype=ops.dt_code(Lr.wp.dtype), splits=Lr.splits)
         if bwd:
+            v = e["v"]
             e.update(dv=self.g(v), dg=self.g(mod.weight_g) if wn else None, slabs=Lr.slab)
         return e
 
@@ -346,45 +539,77 @@ class VQVAEEngine:
             if train:
                 self._build_bwd_tables(w)
 
+    def _bias_partials(self, w, producer_folded, buf):
+        """COLSUM partial rows of a gradient tensor: the producing GEMM's row
+        tiles, or one row of a standalone colsum when the producer is a folded
+        (resampling) GEMM whose epilogue cannot sum unfolded columns."""
+        return buf[:1] if producer_folded else buf
+
     def _build_bwd_tables(self, w):
         """Per-workspace backward tables: each group's weight-norm backward plus
         the column reductions of the bias / GroupNorm-affine partials that are
         final when the group's GEMMs are done (one launch per group)."""
-        ns, nd, B = self.dims["ns"], self.dims["nd"], w.B
-        C, Cd, S = self.dims["C"], self.dims["Cd"], self.dims["S"]
+        B, S = w.B, self.dims["S"]
         g = self.g
         cr = ops.colreduce_entry
-        cs_enc_b = self._bview(w.colsum_b, B, C)
-        dg_enc_b, db_enc_b = self._bview(w.dgam_b, B, C), self._bview(w.dbet_b, B, C)
-        dg_dec_b, db_dec_b = self._bview(w.dgam_b, B, 2 * Cd), self._bview(w.dbet_b, B, 2 * Cd)
         t = {}
-        f1 = self.fin1
-        t["fin"] = [self._wn_entry(f1, True), self._wn_entry(self.fin2, True),
-                    cr(w.cs_f1, g(f1.mod.bias))]
-        for i in range(nd):
-            ci, rs, gn, cond = self.dec_in[i], self.dec_rs[i], self.dec_gn[i], self.dec_cond[i]
-            rb = g(rs.mod.bias)
-            t[("dec", i)] = [self._wn_entry(ci, True), self._wn_entry(rs, True),
-                             cr(w.cs_dec[(nd - 1 - i) % 2], rb[:Cd]), cr(w.cs_skip, rb[Cd:]),
-                             cr(w.cs_all[i], g(ci.mod.bias)), cr(dg_dec_b, g(gn.weight)), cr(db_dec_b, g(gn.bias))]
+        t["fin"] = [self._wn_entry(self.fin1, True), self._wn_entry(self.fin2, True),
+                    cr(w.cs_f1, g(self.fin1.mod.bias))]
+        ns = len(self.dec_stages)
+        for si, st in enumerate(self.dec_stages):
+            sw = w.dec[si]
+            C2 = 2 * sw.C
+            nb = len(st.blocks)
+            dg_b, db_b = self._bview(w.dgam_b[0], B, C2), self._bview(w.dbet_b[0], B, C2)
+            for j, b in enumerate(st.blocks):
+                rb = g(b.rs.mod.bias)
+                # dL/dx_{j+1}: zero after the last block of the last stage (cs zeroed), else the
+                # colsums of the next block's / next stage conv's dgrad
+                nxt_folded = (j == nb - 1 and si + 1 < ns and self.dec_stages[si + 1].conv.kind == KIND_UP)
+                t[b.key] = [self._wn_entry(b.conv_in, True), self._wn_entry(b.rs, True),
+                            cr(self._bias_partials(w, nxt_folded, sw.cs[j + 1]), rb[:sw.C]), cr(w.cs_skip, rb[sw.C:]),
+                            cr(sw.cs_all[j], g(b.conv_in.mod.bias)), cr(dg_b, g(b.gn.weight)), cr(db_b, g(b.gn.bias))]
+            first_folded = not st.blocks and si + 1 < ns and self.dec_stages[si + 1].conv.kind == KIND_UP
+            t[("dec_stage", si)] = [self._wn_entry(st.conv, True),
+                                    cr(self._bias_partials(w, first_folded, sw.cs[0]), g(st.conv.mod.bias))]
         t["cond"] = [self._wn_entry(Lr, True) for Lr in self.dec_cond]
-        t["dec0"] = [self._wn_entry(self.dec0, True), cr(w.cs_dec[nd % 2], g(self.dec0.mod.bias))]
         t["enc_out"] = [self._wn_entry(self.enc_out, True)]
-        for i in range(ns):
-            k3, sk, gn = self.enc_k3[i], self.enc_sk[i], self.enc_gn[i]
-            t[("enc", i)] = [self._wn_entry(k3, True), self._wn_entry(sk, True),
-                             cr(w.cs_enc[(ns - 1 - i) % 2], g(sk.mod.bias)),
-                             cr(cs_enc_b, g(k3.mod.bias)), cr(dg_enc_b, g(gn.weight)), cr(db_enc_b, g(gn.bias))]
-        t["enc0"] = [self._wn_entry(self.enc0, True), cr(w.cs_enc[ns % 2], g(self.enc0.mod.bias))]
+        ne = len(self.enc_stages)
+        for si, st in enumerate(self.enc_stages):
+            sw = w.enc[si]
+            C = sw.C
+            nb = len(st.blocks)
+            for j, b in enumerate(st.blocks):
+                # dL/dc_{j+1} comes from the next block's skip dgrad, the next stage conv's
+                # dgrad (folded when it down-samples) or the output conv's dgrad
+                nxt_folded = j == nb - 1 and si + 1 < ne and self.enc_stages[si + 1].conv.kind == KIND_DOWN
+                ent = [self._wn_entry(Lr, True) for Lr in b.convs] + [self._wn_entry(b.skip, True),
+                                                                       cr(self._bias_partials(w, nxt_folded,
+                                                                                              sw.cs[j + 1]),
+                                                                          g(b.skip.mod.bias))]
+                for l, (Lr, gn) in enumerate(zip(b.convs, b.gns)):
+                    ent += [cr(self._bview(w.colsum_b[l], B, C), g(Lr.mod.bias)),
+                            cr(self._bview(w.dgam_b[l], B, C), g(gn.weight)),
+                            cr(self._bview(w.dbet_b[l], B, C), g(gn.bias))]
+                t[b.key] = ent
+            first_folded = not st.blocks and si + 1 < ne and self.enc_stages[si + 1].conv.kind == KIND_DOWN
+            t[("enc_stage", si)] = [self._wn_entry(st.conv, True),
+                                    cr(self._bias_partials(w, first_folded, sw.cs[0]), g(st.conv.mod.bias))]
         w.bwd_tables = {k: ops.wn_table(v) for k, v in t.items()}
         # parameters whose gradients are final once a group's launch is done
         # (data parallel: their all-reduce is issued right then, parallel/ddp.py)
         w.bwd_params = {k: self._params_written([t_ for e in entries for t_ in (e.get("dv"), e.get("dg"))])
                         for k, entries in t.items()}
-        # all ResSkip blocks' conditioning linears, forward and backward, one table
-        w.cond_table = ops.linear_table([dict(W=Lr.wp, bias=Lr.mod.bias, out=w.condbias[i], dout=w.cs_all[i],
-                                              dW=Lr.slab.view(Lr.rows, Lr.cols), dbias=g(Lr.mod.bias))
-                                         for i, Lr in enumerate(self.dec_cond)])
+        # all ResSkip blocks' conditioning linears, forward and backward, one table per output width
+        w.cond_tables = {}
+        for O, blocks in self.cond_groups.items():
+            ents = []
+            for b in blocks:
+                si, j = b.key[1], b.key[2]
+                sw = w.dec[si]
+                ents.append(dict(W=b.cond.wp, bias=b.cond.mod.bias, out=sw.condbias[j], dout=sw.cs_all[j],
+                                 dW=b.cond.slab.view(b.cond.rows, b.cond.cols), dbias=g(b.cond.mod.bias)))
+            w.cond_tables[O] = ops.linear_table(ents)
 
     MAX_EVAL_WS = 4  # inference over variable-length utterances keeps only the latest shapes
 
@@ -405,19 +630,54 @@ class VQVAEEngine:
 
     # ------------------------------------------------------------ conv helpers
     def fwd(self, Lr, x, y, T, **kw):
-        ops.conv_fwd(x, Lr.wp, y, T=T, cin=Lr.cin, cout=Lr.cout, ntaps=Lr.k, pad=Lr.pad, **kw)
+        """y = conv(x); T = frames per utterance of the input x."""
+        if Lr.kind in (KIND_CONV, KIND_CONVT):
+            ops.conv_fwd(x, Lr.wp, y, T=T, cin=Lr.cin, cout=Lr.cout, ntaps=Lr.k, pad=Lr.pad, dil=Lr.dil, **kw)
+        elif Lr.kind == KIND_DOWN:
+            s = Lr.scale
+            ops.conv_fwd(x.view(-1, s * Lr.cin), Lr.wp, y, T=T // s, cin=s * Lr.cin, cout=Lr.cout, ntaps=3, pad=1,
+                         **kw)
+        else:  # up-sampler: the adjoint of the folded conv, bias tiled over the s output frames
+            s = Lr.scale
+            if kw.get("bias") is not None:
+                kw["bias"] = Lr.btile
+            ops.conv_dgrad(x, Lr.wp, y.view(-1, s * Lr.cout), T=T, cin=Lr.cin, cout=s * Lr.cout, ntaps=3, pad=1,
+                           **kw)
 
     def dgrad(self, Lr, dy, dx, T, **kw):
-        ops.conv_dgrad(dy, Lr.wp, dx, T=T, cin=Lr.cout, cout=Lr.cin, ntaps=Lr.k, pad=Lr.pad, **kw)
+        """dx = dL/d(input) from dy = dL/d(output); T = frames per utterance of dy."""
+        if Lr.kind in (KIND_CONV, KIND_CONVT):
+            ops.conv_dgrad(dy, Lr.wp, dx, T=T, cin=Lr.cout, cout=Lr.cin, ntaps=Lr.k,
+                           pad=(Lr.k - 1) * Lr.dil - Lr.pad, dil=Lr.dil, **kw)
+        elif Lr.kind == KIND_DOWN:
+            s = Lr.scale
+            if kw.get("mask") is not None:
+                kw["mask"] = kw["mask"].view(-1, s * Lr.cin)
+            ops.conv_dgrad(dy, Lr.wp, dx.view(-1, s * Lr.cin), T=T, cin=Lr.cout, cout=s * Lr.cin, ntaps=3, pad=1,
+                           **kw)
+        else:
+            s = Lr.scale
+            ops.conv_fwd(dy.view(-1, s * Lr.cout), Lr.wp, dx, T=T // s, cin=s * Lr.cout, cout=Lr.cin, ntaps=3,
+                         pad=1, **kw)
 
     def wgrad(self, Lr, dy, x, T, pro=L.PRO_NONE, scale=1.0):
-        if Lr.kind == 0:
-            ops.conv_wgrad(dy, x, Lr.slab, T=T, r_dim=Lr.cout, c_dim=Lr.cin, ntaps=Lr.k, pad=Lr.pad, shift_sign=1,
-                           q_prologue=pro, pro_scale=scale, splits=Lr.splits)
+        """Weight-gradient slabs from dy (output gradient, T frames per utterance) and the input x."""
+        if Lr.kind == KIND_CONV:
+            ops.conv_wgrad(dy, x, Lr.slab, T=T, r_dim=Lr.cout, c_dim=Lr.cin, ntaps=Lr.k, pad=Lr.pad, dil=Lr.dil,
+                           shift_sign=1, q_prologue=pro, pro_scale=scale, splits=Lr.splits)
+            return
+        assert pro == L.PRO_NONE
+        if Lr.kind == KIND_CONVT:
+            ops.conv_wgrad(x, dy, Lr.slab, T=T, r_dim=Lr.cin, c_dim=Lr.cout, ntaps=Lr.k, pad=Lr.pad, dil=Lr.dil,
+                           shift_sign=-1, splits=Lr.splits)
+        elif Lr.kind == KIND_DOWN:
+            s = Lr.scale
+            ops.conv_wgrad(dy, x.view(-1, s * Lr.cin), Lr.slab, T=T, r_dim=Lr.cout, c_dim=s * Lr.cin, ntaps=3, pad=1,
+                           shift_sign=1, splits=Lr.splits)
         else:
-            assert pro == L.PRO_NONE
-            ops.conv_wgrad(x, dy, Lr.slab, T=T, r_dim=Lr.cin, c_dim=Lr.cout, ntaps=Lr.k, pad=Lr.pad, shift_sign=-1,
-                           splits=Lr.splits)
+            s = Lr.scale
+            ops.conv_wgrad(x, dy.view(-1, s * Lr.cout), Lr.slab, T=T // s, r_dim=Lr.cin, c_dim=s * Lr.cout, ntaps=3,
+                           pad=1, shift_sign=1, splits=Lr.splits)
 
     def bias_grad(self, Lr, dy, w):
         ops.colsum(dy, w.cs_part, self.g(Lr.mod.bias))
@@ -425,57 +685,77 @@ class VQVAEEngine:
     # ------------------------------------------------------------ forward
     def pack_weights(self):
         ops.weight_norm_fwd(self.wn_fwd_table)
+        for st in self.dec_stages:
+            if st.conv.kind == KIND_UP:  # the up-sampler's bias, once per folded frame
+                s = st.conv.scale
+                ops.convert_2d(st.conv.mod.bias.detach().view(1, -1).expand(s, -1), st.conv.btile.view(s, -1))
 
     def embed_and_cond(self, w, y):
         ops.embedding_fwd(self.m.embeds._embedding.weight, y.reshape(-1), w.yemb)
-        if getattr(w, "cond_table", None) is not None:
-            Lr = self.dec_cond[0]
-            ops.linear_batched_fwd(w.cond_table, w.yemb, w.B, Lr.cin, Lr.cout)
-        else:
-            for i, Lr in enumerate(self.dec_cond):
-                ops.linear_f32(w.yemb, Lr.wp, Lr.mod.bias, w.condbias[i])
+        tabs = getattr(w, "cond_tables", None)
+        for O, blocks in self.cond_groups.items():
+            if tabs is not None:
+                ops.linear_batched_fwd(tabs[O], w.yemb, w.B, blocks[0].cond.cin, O)
+            else:
+                for b in blocks:
+                    ops.linear_f32(w.yemb, b.cond.wp, b.cond.mod.bias, w.dec[b.key[1]].condbias[b.key[2]])
 
     def encoder_fwd(self, w, x_nct):
-        T = w.T
         ops.nct_to_ntc(x_nct, w.x)
-        # every GEMM producing c_i also writes a_i = LeakyReLU(c_i), the operand
-        # of the next k3 conv / the output conv (vqvae.py:86-87 stack[0], 190)
-        self.fwd(self.enc0, w.x, w.c[0], T, bias=self.enc0.mod.bias, act=L.PRO_LRELU, y2=w.a[0])
-        for i in range(self.dims["ns"]):
-            k3, sk, gn = self.enc_k3[i], self.enc_sk[i], self.enc_gn[i]
-            if w.fuse_gn:  # statistics of h_i from the k3 GEMM's epilogue tiles, merged inside the skip GEMM
-                self.fwd(k3, w.a[i], w.h[i], T, bias=k3.mod.bias, gn_stats=w.gst, gn_groups=1)
-                if self._enc_gn_separate:  # A/B: the separate finalize launch
-                    ops.gn_finalize_tiles(w.gst, w.N, T, k3.cout, 1, w.enc_mr[i])
-                    gkw = {}
-                else:
-                    gkw = dict(gn_tiles=w.gst)
-            else:
-                self.fwd(k3, w.a[i], w.h[i], T, bias=k3.mod.bias)
-                ops.groupnorm_stats(w.h[i], T, 1, w.gn_part, w.enc_mr[i])
+        inp, T_in = w.x, w.T
+        for si, st in enumerate(self.enc_stages):
+            sw = w.enc[si]
+            T = sw.T
+            # every GEMM producing c_j also writes a_j = LeakyReLU(c_j), the operand
+            # of the next conv stack / stage conv / output conv (vqvae.py:171, layers.py:152)
+            self.fwd(st.conv, inp, sw.c[0], T_in, bias=st.conv.mod.bias, act=L.PRO_LRELU, y2=sw.a[0])
+            for j, b in enumerate(st.blocks):
+                src = sw.a[j]
                 gkw = {}
-            self.fwd(sk, w.c[i], w.c[i + 1], T, bias=sk.mod.bias, gn_h=w.h[i], gn_mr=w.enc_mr[i],
-                     gn_gamma=gn.weight, gn_beta=gn.bias, act=L.PRO_LRELU, y2=w.a[i + 1], **gkw)
-        self.fwd(self.enc_out, w.a[-1], w.z, T, bias=self.enc_out.mod.bias, out_f32=True)
+                for l, (Lr, gn) in enumerate(zip(b.convs, b.gns)):
+                    h, mr = sw.h[j][l], sw.mr[j][l]
+                    last = l == st.L - 1
+                    if sw.fuse:  # statistics of h from the GEMM's epilogue tiles
+                        self.fwd(Lr, src, h, T, bias=Lr.mod.bias, gn_stats=w.gst, gn_groups=1)
+                        if last and not self._enc_gn_separate:
+                            gkw = dict(gn_tiles=w.gst)  # merged inside the skip GEMM
+                        else:
+                            ops.gn_finalize_tiles(w.gst, sw.N, T, sw.C, 1, mr)
+                    else:
+                        self.fwd(Lr, src, h, T, bias=Lr.mod.bias)
+                        ops.groupnorm_stats(h, T, 1, w.gn_part, mr)
+                    if not last:  # LeakyReLU(GN(h)): the next conv's operand (layers.py:156-161)
+                        ops.gn_lrelu_fwd(h, sw.g[j][l], T, mr, gn.weight, gn.bias)
+                        src = sw.g[j][l]
+                gn = b.gns[-1]
+                self.fwd(b.skip, sw.c[j], sw.c[j + 1], T, bias=b.skip.mod.bias, gn_h=sw.h[j][-1], gn_mr=sw.mr[j][-1],
+                         gn_gamma=gn.weight, gn_beta=gn.bias, act=L.PRO_LRELU, y2=sw.a[j + 1], **gkw)
+            inp, T_in = sw.a[-1], T
+        self.fwd(self.enc_out, inp, w.z, T_in, bias=self.enc_out.mod.bias, out_f32=True)
 
     def decoder_fwd(self, w, zq_c):
-        T, nd, Cd = w.T, self.dims["nd"], self.dims["Cd"]
-        self.fwd(self.dec0, zq_c, w.xs[0], T, bias=self.dec0.mod.bias)
-        for i in range(nd):
-            ci, gn, rs = self.dec_in[i], self.dec_gn[i], self.dec_rs[i]
-            if w.fuse_gn:  # statistics from the GEMM's epilogue tiles, finalised inside the GLU launch
-                self.fwd(ci, w.xs[i], w.u[i], T, bias=ci.mod.bias, rowbias=w.condbias[i], gn_stats=w.gst, gn_groups=2)
-                ops.gn_glu_fwd_tiles(w.u[i], w.g[i], T, w.gst, w.dec_mr[i], gn.weight, gn.bias)
-            else:
-                self.fwd(ci, w.xs[i], w.u[i], T, bias=ci.mod.bias, rowbias=w.condbias[i])
-                ops.groupnorm_stats(w.u[i], T, 2, w.gn_part, w.dec_mr[i])
-                ops.gn_glu_fwd(w.u[i], w.g[i], T, w.dec_mr[i], gn.weight, gn.bias)
-            self.fwd(rs, w.g[i], w.xs[i + 1], T, bias=rs.mod.bias, res=w.xs[i], out2=w.skip32, split_col=Cd,
-                     out2_accumulate=(i > 0))
-        # final_layer = ReLU, conv, ReLU, conv on sqrt(1/(nd+1)) * sum(skips) (vqvae.py:316-318)
-        ops.scale_act_2d(w.skip32, w.a_skip, math.sqrt(1.0 / (nd + 1)), L.PRO_RELU)
-        self.fwd(self.fin1, w.a_skip, w.f1, T, bias=self.fin1.mod.bias, act=L.PRO_RELU)
-        self.fwd(self.fin2, w.f1, w.xhat, T, bias=self.fin2.mod.bias, out_f32=True)
+        inp, T_in = zq_c, w.Tz
+        for si, st in enumerate(self.dec_stages):
+            sw = w.dec[si]
+            T, C = sw.T, sw.C
+            self.fwd(st.conv, inp, sw.xs[0], T_in, bias=st.conv.mod.bias)
+            for j, b in enumerate(st.blocks):
+                ci, gn, rs = b.conv_in, b.gn, b.rs
+                if sw.fuse:  # statistics from the GEMM's epilogue tiles, finalised inside the GLU launch
+                    self.fwd(ci, sw.xs[j], sw.u[j], T, bias=ci.mod.bias, rowbias=sw.condbias[j], gn_stats=w.gst,
+                             gn_groups=2)
+                    ops.gn_glu_fwd_tiles(sw.u[j], sw.g[j], T, w.gst, sw.mr[j], gn.weight, gn.bias)
+                else:
+                    self.fwd(ci, sw.xs[j], sw.u[j], T, bias=ci.mod.bias, rowbias=sw.condbias[j])
+                    ops.groupnorm_stats(sw.u[j], T, 2, w.gn_part, sw.mr[j])
+                    ops.gn_glu_fwd(sw.u[j], sw.g[j], T, sw.mr[j], gn.weight, gn.bias)
+                self.fwd(rs, sw.g[j], sw.xs[j + 1], T, bias=rs.mod.bias, res=sw.xs[j], out2=w.skip32, split_col=C,
+                         out2_accumulate=(b.gidx > 0))
+            inp, T_in = sw.xs[-1], T
+        # final_layer = ReLU, conv, ReLU, conv on sqrt(1/len(layers)) * sum(skips) (vqvae.py:316-318)
+        ops.scale_act_2d(w.skip32, w.a_skip, math.sqrt(1.0 / self.n_dec_layers), L.PRO_RELU)
+        self.fwd(self.fin1, w.a_skip, w.f1, w.T, bias=self.fin1.mod.bias, act=L.PRO_RELU)
+        self.fwd(self.fin2, w.f1, w.xhat, w.T, bias=self.fin2.mod.bias, out_f32=True)
 
     # ------------------------------------------------------------ quantizer host logic
     def _perm_rows(self, n, K, rank_offset=0, n_local=None):
@@ -535,104 +815,204 @@ class VQVAEEngine:
         ops.weight_norm_bwd(w.bwd_tables[key])
         self._grads_final(w.bwd_params[key])
 
-    def _gnb(self, w, i):
-        """GNBWD epilogue arguments: the GEMM producing dL/d(GN_i output) also
-        writes block i's GroupNorm-backward sums (encoder, G=1)."""
-        if not w.fuse_gn:
+    def _gnb(self, w, si, j):
+        """GNBWD epilogue arguments: the GEMM producing dL/dc_{j+1} of encoder
+        stage si also writes block j's (last layer's) GroupNorm-backward sums."""
+        sw = w.enc[si]
+        if not sw.fuse:
             return {}
-        gn = self.enc_gn[i]
-        return dict(gn_bwd=w.gnb_part, gn_h=w.h[i], gn_mr=w.enc_mr[i], gn_gamma=gn.weight, gn_beta=gn.bias,
+        gn = self.enc_stages[si].blocks[j].gns[-1]
+        return dict(gn_bwd=w.gnb_part, gn_h=sw.h[j][-1], gn_mr=sw.mr[j][-1], gn_gamma=gn.weight, gn_beta=gn.bias,
                     gn_groups=1)
 
-    def _gnb_parts(self, w, cols):
+    @staticmethod
+    def _gnb_parts(sw, cols, fused=True):
         """GNBWD tiles per utterance (0 = vqx_gn_bwd reduces itself)."""
-        return (w.T // 128) * ((cols + 127) // 128) if w.fuse_gn else 0
+        return (sw.T // 128) * ((cols + 127) // 128) if (sw.fuse and fused) else 0
 
-    def _bview(self, buf, B, C):
+    @staticmethod
+    def _bview(buf, B, C):
         return buf.view(-1)[: B * C].view(B, C)
+
+    def _enc_cur(self, w, si, k):
+        sw = w.enc[si]
+        return Workspace.view(w.dc_flat[k], sw.N, sw.C)
+
+    def _producer_into_enc(self, w, si, dst, colsum_buf, gnb_ok):
+        """Epilogue kwargs for a dgrad whose output is dL/dc_nb of encoder stage si
+        (its last block's input gradient): bias partials and, when the stage's
+        last block exists and the producer is unfolded, its GNBWD sums."""
+        kw = dict(colsum=colsum_buf)
+        st = self.enc_stages[si]
+        if st.blocks and gnb_ok:
+            kw.update(self._gnb(w, si, len(st.blocks) - 1))
+        return kw
 
     def encoder_bwd(self, w, grad_scale=1.0):
         """Backward of beta*z_enc_loss through the encoder: the commitment term is
         the encoder's only gradient source (z_vq is a no-grad gather under
         reduction='frame_mean', layers_vq.py:292,315)."""
-        T, N, ns, C = w.T, w.N, self.dims["ns"], self.dims["C"]
         B = w.B
         if not self.plain:  # EMA: the commitment term is the encoder's only gradient
-            ops.vq_commit_bwd(w.z, w.zq, 2.0 * self.m.beta * grad_scale / N, w.dz)
+            ops.vq_commit_bwd(w.z, w.zq, 2.0 * self.m.beta * grad_scale / w.Nz, w.dz)
         eo = self.enc_out
+        ne = len(self.enc_stages)
+        last = w.enc[-1]
         self.bias_grad(eo, w.dz, w)
-        self.wgrad(eo, w.dz, w.a[ns], T)
-        cur = w.dc[0]
-        # every dL/dc_i producer also writes its bias-gradient partials (COLSUM)
-        # and, for the block below, the GroupNorm-backward sums (GNBWD)
-        self.dgrad(eo, w.dz, cur, T, mask=w.a[ns], mask_slope=0.2, colsum=w.cs_enc[0], **self._gnb(w, ns - 1))
+        self.wgrad(eo, w.dz, last.a[-1], last.T)
+        k = 0
+        cur = self._enc_cur(w, ne - 1, k)
+        self.dgrad(eo, w.dz, cur, last.T, mask=last.a[-1], mask_slope=0.2,
+                   **self._producer_into_enc(w, ne - 1, None, last.cs[-1], True))
         self._wn_bwd(w, "enc_out")
-        cs_b, dg_b, db_b = (self._bview(t, B, C) for t in (w.colsum_b, w.dgam_b, w.dbet_b))
-        for i in reversed(range(ns)):
-            k3, sk, gn = self.enc_k3[i], self.enc_sk[i], self.enc_gn[i]
-            j = (ns - i) % 2
-            nxt = w.dc[j]
-            # cur = dL/dc_{i+1}, the gradient w.r.t. block i's output GN(h_i) + skip(c_i)
-            self.wgrad(sk, cur, w.c[i], T)
-            ops.gn_bwd(cur, w.h[i], w.dh, T, 1, False, w.enc_mr[i], gn.weight, gn.bias, w.gnb_part, cs_b, dg_b, db_b,
-                       nparts=self._gnb_parts(w, C))
-            self.wgrad(k3, w.dh, w.a[i], T)
-            self.dgrad(k3, w.dh, w.tmp, T, mask=w.a[i], mask_slope=0.2)
-            self.dgrad(sk, cur, nxt, T, res=w.tmp, colsum=w.cs_enc[j], **(self._gnb(w, i - 1) if i > 0 else {}))
-            # weight norms of k3/sk + biases of sk (cur partials), k3 and the GN affine
-            self._wn_bwd(w, ("enc", i))
-            cur = nxt
-        # cur = dL/dc_0 (conv0 output); conv0's input (the mel batch) needs no gradient
-        self.wgrad(self.enc0, cur, w.x, T)
-        self._wn_bwd(w, "enc0")
+        for si in reversed(range(ne)):
+            st, sw = self.enc_stages[si], w.enc[si]
+            T, N, C = sw.T, sw.N, sw.C
+            dh = Workspace.view(w.dh_flat, N, C)
+            tmp = Workspace.view(w.tmp_flat, N, C)
+            dy2 = Workspace.view(w.dy_flat, N, C)
+            nb = len(st.blocks)
+            # the producer of dL/dc_nb (output conv or next stage conv) fused GNBWD only when unfolded
+            top_fused = si == ne - 1 or self.enc_stages[si + 1].conv.kind != KIND_DOWN
+            for j in reversed(range(nb)):
+                b = st.blocks[j]
+                k ^= 1
+                nxt = self._enc_cur(w, si, k)
+                # cur = dL/dc_{j+1}, the gradient w.r.t. block j's output GN(h_L) + skip(c_j)
+                self.wgrad(b.skip, cur, sw.c[j], T)
+                dy = cur
+                fused_here = top_fused if j == nb - 1 else True
+                for l in reversed(range(st.L)):
+                    Lr, gn = b.convs[l], b.gns[l]
+                    cs_b = self._bview(w.colsum_b[l], B, C)
+                    dg_b = self._bview(w.dgam_b[l], B, C)
+                    db_b = self._bview(w.dbet_b[l], B, C)
+                    nparts = self._gnb_parts(sw, C, fused_here) if l == st.L - 1 else 0
+                    ops.gn_bwd(dy, sw.h[j][l], dh, T, 1, False, sw.mr[j][l], gn.weight, gn.bias, w.gnb_part, cs_b,
+                               dg_b, db_b, nparts=nparts)
+                    src = sw.a[j] if l == 0 else sw.g[j][l - 1]
+                    self.wgrad(Lr, dh, src, T)
+                    if l > 0:  # into LeakyReLU(GN(h_{l-1})): its derivative from the sign of the stored output
+                        self.dgrad(Lr, dh, dy2, T, mask=sw.g[j][l - 1], mask_slope=0.2)
+                        dy = dy2
+                    else:
+                        self.dgrad(Lr, dh, tmp, T, mask=sw.a[j], mask_slope=0.2)
+                prod = dict(colsum=sw.cs[j])
+                if j > 0:
+                    prod.update(self._gnb(w, si, j - 1))
+                self.dgrad(b.skip, cur, nxt, T, res=tmp, **prod)
+                # weight norms of the stack convs and skip + their biases and the GN affine
+                self._wn_bwd(w, b.key)
+                cur = nxt
+            # cur = dL/dc_0 of the stage (the stage conv's output)
+            if si == 0:  # the mel batch needs no gradient
+                self.wgrad(st.conv, cur, w.x, T)
+            else:
+                prev = w.enc[si - 1]
+                self.wgrad(st.conv, cur, prev.a[-1], T)
+                k ^= 1
+                pcur = self._enc_cur(w, si - 1, k)
+                if st.conv.kind == KIND_DOWN:  # folded: no column epilogues, colsum separately
+                    self.dgrad(st.conv, cur, pcur, T, mask=prev.a[-1], mask_slope=0.2)
+                    ops.colsum(pcur, w.cs_part, prev.cs[-1][0])
+                else:
+                    self.dgrad(st.conv, cur, pcur, T, mask=prev.a[-1], mask_slope=0.2,
+                               **self._producer_into_enc(w, si - 1, None, prev.cs[-1], True))
+                cur = pcur
+            self._wn_bwd(w, ("enc_stage", si))
+
+    def _dec_dr(self, w, si, k):
+        return w.dec[si].dr[k]
 
     def decoder_bwd(self, w):
-        T, nd, Cd, B = w.T, self.dims["nd"], self.dims["Cd"], w.B
+        B, S = w.B, self.dims["S"]
         f1, f2 = self.fin1, self.fin2
         dxhat = w.dxhat
+        ns = len(self.dec_stages)
         self.bias_grad(f2, dxhat, w)
-        self.wgrad(f2, dxhat, w.f1, T)
-        self.dgrad(f2, dxhat, w.df1, T, mask=w.f1, mask_slope=0.0, colsum=w.cs_f1)
-        s = math.sqrt(1.0 / (nd + 1))
-        self.wgrad(f1, w.df1, w.a_skip, T)
-        cur, nxt = w.dr[0], w.dr[1]
-        # dL/dskip (identical for every block) -> tail columns of both [dx | dskip] buffers
-        self.dgrad(f1, w.df1, cur[:, Cd:], T, mask=w.a_skip, mask_slope=0.0, mask_scale=s, colsum=w.cs_skip)
-        ops.convert_2d(cur[:, Cd:], nxt[:, Cd:])
-        ops.convert_2d(None, cur, cols=Cd)  # dL/dx_{nd+1} = 0: the last residual output is unused
-        ops.zero_(w.cs_dec[0])  # ... and so are its bias-gradient partials (read by block nd-1)
+        self.wgrad(f2, dxhat, w.f1, w.T)
+        self.dgrad(f2, dxhat, w.df1, w.T, mask=w.f1, mask_slope=0.0, colsum=w.cs_f1)
+        s = math.sqrt(1.0 / self.n_dec_layers)
+        self.wgrad(f1, w.df1, w.a_skip, w.T)
+        # dL/dskip (identical for every block) -> tail columns of every [dx | dskip] buffer
+        lst = ns - 1
+        sw = w.dec[lst]
+        k = 0
+        cur = sw.dr[k]
+        self.dgrad(f1, w.df1, cur[:, sw.C:], w.T, mask=w.a_skip, mask_slope=0.0, mask_scale=s, colsum=w.cs_skip)
+        for si in range(ns):
+            if self.dec_stages[si].blocks:
+                for q in range(2):
+                    if si == lst and q == k:
+                        continue
+                    ops.convert_2d(cur[:, sw.C:], w.dec[si].dr[q][:, w.dec[si].C:])
+        ops.convert_2d(None, cur, cols=sw.C)  # dL/dx at the decoder output is 0: the last residual is unused
+        ops.zero_(sw.cs[-1])                   # ... and so are its bias-gradient partials
         self._wn_bwd(w, "fin")
-        C2 = 2 * Cd
-        dg_b, db_b = (self._bview(t, B, C2) for t in (w.dgam_b, w.dbet_b))
-        for i in reversed(range(nd)):
-            ci, gn, rs = self.dec_in[i], self.dec_gn[i], self.dec_rs[i]
-            j = (nd - 1 - i) % 2
-            # cur = [dL/dx_{i+1} | dL/dskip]
-            self.wgrad(rs, cur, w.g[i], T)
-            if w.fuse_gn:  # GLU + GroupNorm backward sums from the res/skip dgrad's epilogue
-                self.dgrad(rs, cur, w.dg, T, gn_bwd=w.gnb_part, gn_h=w.u[i], gn_mr=w.dec_mr[i], gn_gamma=gn.weight,
-                           gn_beta=gn.bias, gn_groups=2, gn_glu=True)
+        cur_x = cur[:, :sw.C]
+        for si in reversed(range(ns)):
+            st, sw = self.dec_stages[si], w.dec[si]
+            T, C = sw.T, sw.C
+            C2 = 2 * C
+            dg = Workspace.view(w.dg_flat, sw.N, C)
+            du = Workspace.view(w.du_flat, sw.N, C2)
+            dg_b, db_b = (self._bview(t[0], B, C2) for t in (w.dgam_b, w.dbet_b))
+            for j in reversed(range(len(st.blocks))):
+                b = st.blocks[j]
+                ci, gn, rs = b.conv_in, b.gn, b.rs
+                nxt = sw.dr[k ^ 1]
+                # cur = [dL/dx_{j+1} | dL/dskip]
+                self.wgrad(rs, cur, sw.g[j], T)
+                if sw.fuse:  # GLU + GroupNorm backward sums from the res/skip dgrad's epilogue
+                    self.dgrad(rs, cur, dg, T, gn_bwd=w.gnb_part, gn_h=sw.u[j], gn_mr=sw.mr[j], gn_gamma=gn.weight,
+                               gn_beta=gn.bias, gn_groups=2, gn_glu=True)
+                else:
+                    self.dgrad(rs, cur, dg, T)
+                ops.gn_bwd(dg, sw.u[j], du, T, 2, True, sw.mr[j], gn.weight, gn.bias, w.gnb_part, sw.cs_all[j],
+                           dg_b, db_b, nparts=self._gnb_parts(sw, C))
+                self.wgrad(ci, du, sw.xs[j], T)
+                self.dgrad(ci, du, nxt[:, :C], T, res=cur[:, :C], colsum=sw.cs[j])
+                # weight norms of conv_in/res_skip + biases of res_skip, conv_in and the GN affine
+                self._wn_bwd(w, b.key)
+                k ^= 1
+                cur = nxt
+                cur_x = cur[:, :C]
+            # cur_x = dL/dx_0 of the stage (the stage conv's output)
+            if st.conv.kind == KIND_UP and not cur_x.is_contiguous():  # the folded GEMMs need whole rows
+                ops.convert_2d(cur_x, dg)
+                cur_x = dg
+            if si > 0:
+                prev, pst = w.dec[si - 1], self.dec_stages[si - 1]
+                self.wgrad(st.conv, cur_x, prev.xs[-1], T)
+                if pst.blocks:
+                    k = 0
+                    pcur = prev.dr[k]
+                    dst = pcur[:, :prev.C]
+                else:
+                    pcur = None
+                    dst = prev.dx
+                if st.conv.kind == KIND_UP:
+                    self.dgrad(st.conv, cur_x, dst, T)
+                    ops.colsum(dst, w.cs_part, prev.cs[-1][0])
+                else:
+                    self.dgrad(st.conv, cur_x, dst, T, colsum=prev.cs[-1])
+                self._wn_bwd(w, ("dec_stage", si))
+                cur, cur_x = pcur, dst
             else:
-                self.dgrad(rs, cur, w.dg, T)
-            ops.gn_bwd(w.dg, w.u[i], w.du, T, 2, True, w.dec_mr[i], gn.weight, gn.bias, w.gnb_part, w.cs_all[i],
-                       dg_b, db_b, nparts=self._gnb_parts(w, Cd))
-            self.wgrad(ci, w.du, w.xs[i], T)
-            self.dgrad(ci, w.du, nxt[:, :Cd], T, res=cur[:, :Cd], colsum=w.cs_dec[1 - j])
-            # weight norms of conv_in/res_skip + biases of res_skip, conv_in and the GN affine
-            self._wn_bwd(w, ("dec", i))
-            cur, nxt = nxt, cur
-        # speaker conditioning of all blocks at once: dW, bias and d(embedding)
-        cond = self.dec_cond[0]
-        ops.linear_batched_bwd(w.cond_table, w.yemb, B, cond.cin, cond.cout, w.dyemb, w.lin_part)
-        self._wn_bwd(w, "cond")
-        dx1 = cur[:, :Cd]  # dL/dx_1, the ConvT0 output
-        self.wgrad(self.dec0, dx1, w.zq_in, T)
-        if self.plain:  # straight-through VQ: the decoder input's gradient reaches the encoder
-            self.dgrad(self.dec0, dx1, w.dzq, T)
-        self._wn_bwd(w, "dec0")
+                self.wgrad(st.conv, cur_x, w.zq_in, T)
+                if self.plain:  # straight-through VQ: the decoder input's gradient reaches the encoder
+                    self.dgrad(st.conv, cur_x, w.dzq, T)
+                self._wn_bwd(w, ("dec_stage", 0))
+        # speaker conditioning of all blocks: dW, bias and d(embedding), per output width
         emb_g = self.g(self.m.embeds._embedding.weight)
         ops.zero_(emb_g)
-        ops.embedding_bwd(w.dyemb, w.y_dev, emb_g)
+        for O, blocks in self.cond_groups.items():
+            ops.linear_batched_bwd(w.cond_tables[O], w.yemb, B, blocks[0].cond.cin, O, w.dyemb, w.lin_part)
+            ops.embedding_bwd(w.dyemb, w.y_dev, emb_g)
+        self._wn_bwd_cond(w)
+
+    def _wn_bwd_cond(self, w):
+        self._wn_bwd(w, "cond")
 
     # ------------------------------------------------------------ quantizer
     def vq_init_if_needed(self, w):
@@ -641,11 +1021,11 @@ class VQVAEEngine:
         if q.initialized:
             return False
         K = self.dims["K"]
-        if w.N * self.world < K:  # N_global < K: noisy tiling of the global batch (identical on every rank)
+        if w.Nz * self.world < K:  # N_global < K: noisy tiling of the global batch (identical on every rank)
             rows = self._tile_rows(w)
             q.embeddings.copy_(rows)
         else:
-            perm = self._perm_rows(w.N * self.world, K, self.rank * w.N, w.N if self.world > 1 else None)
+            perm = self._perm_rows(w.Nz * self.world, K, self.rank * w.Nz, w.Nz if self.world > 1 else None)
             ops.gather_rows(w.z, perm, q.embeddings)
             if self.world > 1:
                 self.comm.all_reduce_sum(q.embeddings)
@@ -666,7 +1046,7 @@ class VQVAEEngine:
         else:
             zin, emb = w.z, q.embeddings.data
         ops.vq_forward(zin, emb, w.idx, w.zq, w.zq_c, w.stats[1:2], w.vq_part, w.bsum, w.bcnt)
-        ops.vq_perplexity(w.bcnt, w.N, w.stats[4:5])
+        ops.vq_perplexity(w.bcnt, w.Nz, w.stats[4:5])
 
     def vq_plain_backward(self, w):
         """Straight-through + codebook + commitment (+ normalisation) gradients."""
@@ -674,7 +1054,7 @@ class VQVAEEngine:
         zin = w.z_norm if self.vq_normalize else w.z
         emb = w.embn if self.vq_normalize else q.embeddings.data
         ops.vq_plain_bwd(w.z, zin, w.z_len if self.vq_normalize else None, w.zq, w.dzq,
-                         w.src_t if w.jittered else None, w.T, self.vq_normalize, float(self.m.beta), 2.0 / w.N,
+                         w.src_t if w.jittered else None, w.Tz, self.vq_normalize, float(self.m.beta), 2.0 / w.Nz,
                          w.dz, w.bsum, w.bcnt, emb, w.e_len if self.vq_normalize else None, self.g(q.embeddings))
 
     def vq_forward_train(self, w):
@@ -686,13 +1066,13 @@ class VQVAEEngine:
         ops.zero_(w.ema)
         ops.vq_forward(w.z, q.embeddings, w.idx, w.zq, w.zq_c, w.stats[1:2], w.vq_part, w.bsum, w.bcnt)
         # rows for dead-code replacement: z[randperm(N)[:K]] (update_emb, layers_vq.py:212-213)
-        if w.N * self.world < K:
+        if w.Nz * self.world < K:
             rows = self._tile_rows(w)
             if self.rank != 0:  # every rank holds the same rows; the EMA bundle is SUM-reduced
                 rows.zero_()
             w.rand_rows.copy_(rows)
         else:
-            perm = self._perm_rows(w.N * self.world, K, self.rank * w.N, w.N if self.world > 1 else None)
+            perm = self._perm_rows(w.Nz * self.world, K, self.rank * w.Nz, w.Nz if self.world > 1 else None)
             ops.gather_rows(w.z, perm, w.rand_rows)
         if self.world > 1:
             self._ema_work = self.comm.all_reduce_sum(w.ema, async_op=True)
@@ -724,9 +1104,9 @@ class VQVAEEngine:
         w.zq_in = w.zq_c
         w.jittered = False
         if self.dims["jitter_p"] > 0 and self.m.jitter.training:
-            src = torch.from_numpy(self.jitter_map(T)).pin_memory()
+            src = torch.from_numpy(self.jitter_map(w.Tz)).pin_memory()
             w.src_t.copy_(src, non_blocking=True)
-            ops.time_gather(w.zq_c, w.zq_j, B, T, w.src_t)
+            ops.time_gather(w.zq_c, w.zq_j, B, w.Tz, w.src_t)
             w.zq_in = w.zq_j
             w.jittered = True
         self.decoder_fwd(w, w.zq_in)
@@ -736,8 +1116,8 @@ class VQVAEEngine:
     def backward(self, w, grad_loss=None):
         """Data parallel: every backward group's gradients are all-reduced as
         soon as its weight-norm backward has finalised them (_wn_bwd), so the
-        reduces overlap the rest of the backward; the remainder (conditioning,
-        ConvT0, embedding, codebook) is flushed at the end."""
+        reduces overlap the rest of the backward; the remainder (embedding,
+        codebook) is flushed at the end."""
         if self.world > 1:
             self._grads_reset()
         if self.plain:
@@ -800,7 +1180,7 @@ class VQVAEEngine:
 
     def total_loss(self, w):
         """(total, VQ loss) device scalars of the step's loss (vqvae.py:83)."""
-        n = w.N
+        n = w.Nz
         xl = w.stats[0:1]
         if self.plain:
             qut = w.stats[1:2] / n
@@ -812,7 +1192,7 @@ class VQVAEEngine:
     def loss_detail(self, w, stats_host):
         """The reference's loss dict (vqvae.py:85-87, layers_vq.py:228-233 / 112-116)."""
         s = stats_host.tolist()
-        n = w.N
+        n = w.Nz
         if self.plain:
             f = np.float32
             qut, enc, xl = f(s[1]) / f(n), (f(s[1]) + f(s[2])) / f(n), f(s[0])
@@ -825,10 +1205,13 @@ class VQVAEEngine:
         return d
 
     # ------------------------------------------------------------ inference
+    def _eval_ws(self, B, T):
+        return self.ws(B, T, train=False) if (B, T, True) not in self._ws else self._ws[(B, T, True)]
+
     def forward_eval(self, x, y):
         """model.eval() forward: no EMA init/update, no jitter (layers_vq.py:282,295,354)."""
         B, _, T = x.shape
-        w = self.ws(B, T, train=False) if (B, T, True) not in self._ws else self._ws[(B, T, True)]
+        w = self._eval_ws(B, T)
         w.y_dev = y.reshape(-1)
         self.pack_weights()
         self.embed_and_cond(w, w.y_dev)
@@ -845,21 +1228,24 @@ class VQVAEEngine:
         return w
 
     def encode(self, x):
-        """Model.encode (vqvae.py:45-52): encoder + nearest-code index, (B, T) int64."""
+        """Model.encode (vqvae.py:45-52): encoder + nearest-code index, (B, T_z) int64."""
         B, _, T = x.shape
-        w = self.ws(B, T, train=False) if (B, T, True) not in self._ws else self._ws[(B, T, True)]
+        w = self._eval_ws(B, T)
         self.pack_weights()
         self.encoder_fwd(w, x)
         q = self.m.quantizer
         if self.plain:
-            return q.encode(w.z.view(B, T, -1), time_last=False)
+            return q.encode(w.z.view(B, w.Tz, -1), time_last=False)
         ops.vq_forward(w.z, q.embeddings, w.idx, None, None, None, w.vq_part, None, None)
-        return w.idx.view(B, T).clone()
+        return w.idx.view(B, w.Tz).clone()
 
     def decode(self, z_idx, y):
         """Model.decode (vqvae.py:55-60): codebook gather + decoder, (B, F, T) f32."""
-        B, T = z_idx.shape
-        w = self.ws(B, T, train=False) if (B, T, True) not in self._ws else self._ws[(B, T, True)]
+        B, Tz = z_idx.shape
+        T = Tz
+        for st in self.enc_stages:
+            T *= st.scale
+        w = self._eval_ws(B, T)
         w.y_dev = y.reshape(-1)
         self.pack_weights()
         self.embed_and_cond(w, w.y_dev)

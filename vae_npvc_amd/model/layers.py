@@ -18,10 +18,11 @@ class WNConv1d(nn.Module):
     ConvTranspose1d (kind 1, v [cin, cout, k], g [cin,1,1]); nn.utils.weight_norm
     with dim=0 as applied at vqvae.py:203-208,329-334."""
 
-    def __init__(self, cin, cout, k, transposed=False, padding=None):
+    def __init__(self, cin, cout, k, transposed=False, padding=None, dilation=1):
         super().__init__()
         self.cin, self.cout, self.k, self.transposed = cin, cout, k, transposed
-        self.padding = (k - 1) // 2 if padding is None else padding
+        self.dilation = dilation
+        self.padding = (k - 1) // 2 * dilation if padding is None else padding
         bound = 1.0 / math.sqrt((cout if transposed else cin) * k)
         self.bias = nn.Parameter(torch.empty(cout).uniform_(-bound, bound))
         vshape = (cin, cout, k) if transposed else (cout, cin, k)
@@ -51,32 +52,55 @@ class WNConv1d(nn.Module):
         self.has_weight_norm = False
 
     def extra_repr(self):
-        return f"{self.cin}, {self.cout}, kernel_size={self.k}, padding={self.padding}, transposed={self.transposed}"
+        return (f"{self.cin}, {self.cout}, kernel_size={self.k}, padding={self.padding}, dilation={self.dilation}, "
+                f"transposed={self.transposed}")
 
 
 class ResidualBlock(nn.Module):
-    """Conv1d_Layernorm_LRelu_Residual (layers.py:129-178) with layers=1:
-    out = GroupNorm(1, C)(Conv_k(LReLU0.2(c))) + Conv_1(c)."""
+    """Conv1d_Layernorm_LRelu_Residual (layers.py:129-178):
+    out = stack(c) + Conv_1(c), stack = [LReLU0.2, Conv_k(dilation), GN(1, C)]
+    followed by (layers - 1) x [LReLU0.2, Conv_k, GN(1, C)] (layers.py:151-161)."""
 
-    def __init__(self, channels, kernel_size=3):
+    def __init__(self, channels, kernel_size=3, layers=1, dilation=1):
         super().__init__()
-        self.stack = nn.Sequential(nn.LeakyReLU(0.2), WNConv1d(channels, channels, kernel_size),
-                                   nn.GroupNorm(1, channels, eps=1e-5, affine=True))
+        if (kernel_size - 1) % 2:
+            raise ValueError("Not support even number kernel size.")  # layers.py:142
+        stack = [nn.LeakyReLU(0.2), WNConv1d(channels, channels, kernel_size, dilation=dilation),
+                 nn.GroupNorm(1, channels, eps=1e-5, affine=True)]
+        for _ in range(layers - 1):
+            stack += [nn.LeakyReLU(0.2), WNConv1d(channels, channels, kernel_size),
+                      nn.GroupNorm(1, channels, eps=1e-5, affine=True)]
+        self.stack = nn.Sequential(*stack)
         self.skip_layer = WNConv1d(channels, channels, 1)
+        self.layers, self.dilation = layers, dilation
+
+    @property
+    def convs(self):
+        return [self.stack[3 * l + 1] for l in range(self.layers)]
+
+    @property
+    def norms(self):
+        return [self.stack[3 * l + 2] for l in range(self.layers)]
 
 
 class ResSkipBlock(nn.Module):
     """DeConv1d_Layernorm_GLU_ResSkip (layers.py:181-249): h = GN(2, 2C)(ConvT(x) +
-    Conv_1(c)); g = tanh(h[:C])*sigmoid(h[C:]); r = Conv_1(g); x' = r[:C] + x;
-    skip = r[C:]."""
+    Conv_1(c)) with ConvT of dilation d and padding (k-1)//2*d (layers.py:198-200);
+    g = tanh(h[:C])*sigmoid(h[C:]); r = Conv_1(g); x' = r[:C] + x; skip = r[C:]."""
 
-    def __init__(self, channels, cond_channels, skip_channels, kernel_size=3):
+    def __init__(self, channels, cond_channels, skip_channels, kernel_size=3, dilation=1):
         super().__init__()
-        self.conv_in = WNConv1d(channels, 2 * channels, kernel_size, transposed=True)
+        if (kernel_size - 1) % 2:
+            raise ValueError("Not support even number kernel size.")  # layers.py:197
+        if not cond_channels:
+            raise NotImplementedError("decoder blocks without speaker conditioning (cond_channels 0)")
+        self.conv_in = WNConv1d(channels, 2 * channels, kernel_size, transposed=True,
+                                padding=(kernel_size - 1) // 2 * dilation, dilation=dilation)
         self.norm_layer = nn.GroupNorm(2, 2 * channels, eps=1e-5, affine=True)
         self.conv_cond = WNConv1d(cond_channels, 2 * channels, 1)
         self.res_skip_layers = WNConv1d(channels, channels + skip_channels, 1)
         self.in_channels = channels
+        self.dilation = dilation
 
 
 class Conditions(nn.Module):

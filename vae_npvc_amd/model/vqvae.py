@@ -17,56 +17,75 @@ import torch.nn as nn
 
 from ..engine.step import VQVAEEngine
 from .layers import Conditions, ResidualBlock, ResSkipBlock, WNConv1d
+from .resample import ResampleConv1d
 from .layers_vq import EMAVectorQuantizer, Jitter, VectorQuantizer
 
 
-def _single(lst, what):
-    if len(lst) != 1:
-        raise NotImplementedError(f"{what}: only single-stage models (the baseline recipes) are supported")
-    return lst[0]
-
-
 class Encoder(nn.Module):
-    """vqvae.py:122-217 restricted to the baseline recipes' single stage
-    (stride 1, stack_layers 1, no dilation, non-causal)."""
+    """vqvae.py:122-217: per resolution stage a conv (kernel_size, or the
+    strided down-sampler of kernel 2s when the stage's downsample_scale s > 1,
+    :146-157), `stacks` residual blocks with dilation 2**j (`dilation: true`)
+    and `stack_layers` convs each, a LeakyReLU; then the 1x1 conv to
+    z_channels.  Same nn.Sequential indices as the reference, so the
+    state_dict keys match."""
 
-    def __init__(self, in_channels=(513,), out_channels=(1024,), downsample_scales=(1,), kernel_size=3,
-                 z_channels=128, dilation=True, stack_kernel_size=3, stack_layers=2, stacks=(3,),
-                 use_weight_norm=True, use_causal_conv=False):
+    def __init__(self, in_channels=(513, 1024, 512, 256), out_channels=(1024, 512, 256, 128),
+                 downsample_scales=(1, 1, 1, 1), kernel_size=3, z_channels=128, dilation=True, stack_kernel_size=3,
+                 stack_layers=2, stacks=(3, 3, 3, 3), use_weight_norm=True, use_causal_conv=False):
         super().__init__()
-        cin = _single(in_channels, "encoder.in_channels")
-        ch = _single(out_channels, "encoder.out_channels")
-        ns = _single(stacks, "encoder.stacks")
-        if _single(downsample_scales, "encoder.downsample_scales") != 1 or dilation or stack_layers != 1 \
-                or use_causal_conv or not use_weight_norm or kernel_size != 3 or stack_kernel_size != 3:
-            raise NotImplementedError("encoder: supported = k3, stride 1, stack_layers 1, no dilation, weight norm")
-        layers = [WNConv1d(cin, ch, kernel_size)]
-        layers += [ResidualBlock(ch, stack_kernel_size) for _ in range(ns)]
-        layers += [nn.LeakyReLU(negative_slope=0.2), WNConv1d(ch, z_channels, 1)]
+        if use_causal_conv:
+            raise NotImplementedError("Not supported yet.")  # vqvae.py:139
+        if not use_weight_norm:
+            raise NotImplementedError("encoder: use_weight_norm false (every reference recipe uses weight norm)")
+        layers, self.stage_index = [], []
+        for cin, cout, ds, nst in zip(in_channels, out_channels, downsample_scales, stacks):
+            self.stage_index.append(len(layers))
+            if ds == 1:
+                if (kernel_size - 1) % 2:
+                    raise NotImplementedError("encoder: even kernel_size changes the frame count")
+                layers.append(WNConv1d(cin, cout, kernel_size))
+            else:
+                layers.append(ResampleConv1d(cin, cout, ds))
+            for j in range(nst):
+                layers.append(ResidualBlock(cout, stack_kernel_size, stack_layers, 2 ** j if dilation else 1))
+            layers.append(nn.LeakyReLU(negative_slope=0.2))
+        layers.append(WNConv1d(out_channels[-1], z_channels, 1))
         self.encode = nn.Sequential(*layers)
-        self.in_ch, self.ch, self.z_ch, self.n_stacks = cin, ch, z_channels, ns
+        self.in_ch, self.z_ch = in_channels[0], z_channels
 
 
 class Decoder(nn.Module):
-    """vqvae.py:220-343 restricted to the single stage of the baseline recipes."""
+    """vqvae.py:220-343: per stage a ConvTranspose1d (kernel_size, padding
+    (k-1)//2; or the strided up-sampler of kernel 2s when upsample_scale
+    s > 1, :245-265) and `stacks` ResSkip blocks with dilation 2**j; the skip
+    outputs of all blocks are summed, scaled by sqrt(1/len(layers)) and sent
+    through ReLU, 1x1, ReLU, 1x1 (:281-286, 308-318)."""
 
-    def __init__(self, in_channels=(128,), out_channels=(256,), upsample_scales=(1,), cond_channels=128,
-                 skip_channels=80, final_channels=80, kernel_size=5, dilation=True, stack_kernel_size=3,
-                 stacks=(3,), use_weight_norm=True, use_causal_conv=False):
+    def __init__(self, in_channels=(128, 256, 512, 1024), out_channels=(256, 512, 1024, 513),
+                 upsample_scales=(1, 1, 1, 1), cond_channels=128, skip_channels=80, final_channels=80, kernel_size=5,
+                 dilation=True, stack_kernel_size=3, stacks=(3, 3, 3, 3), use_weight_norm=True,
+                 use_causal_conv=False):
         super().__init__()
-        cin = _single(in_channels, "decoder.in_channels")
-        ch = _single(out_channels, "decoder.out_channels")
-        nd = _single(stacks, "decoder.stacks")
-        if _single(upsample_scales, "decoder.upsample_scales") != 1 or dilation or use_causal_conv \
-                or not use_weight_norm or kernel_size != 3 or stack_kernel_size != 3:
-            raise NotImplementedError("decoder: supported = k3, stride 1, no dilation, weight norm")
-        self.layers = nn.ModuleList([WNConv1d(cin, ch, kernel_size, transposed=True)]
-                                    + [ResSkipBlock(ch, cond_channels, skip_channels, stack_kernel_size)
-                                       for _ in range(nd)])
+        if use_causal_conv:
+            raise NotImplementedError("Not supported yet.")  # vqvae.py:238
+        if not use_weight_norm:
+            raise NotImplementedError("decoder: use_weight_norm false (every reference recipe uses weight norm)")
+        layers, self.stage_index = [], []
+        for cin, cout, us, nst in zip(in_channels, out_channels, upsample_scales, stacks):
+            self.stage_index.append(len(layers))
+            if us == 1:
+                if (kernel_size - 1) % 2:
+                    raise NotImplementedError("decoder: even kernel_size changes the frame count")
+                layers.append(WNConv1d(cin, cout, kernel_size, transposed=True))
+            else:
+                layers.append(ResampleConv1d(cin, cout, us, transposed=True))
+            for j in range(nst):
+                layers.append(ResSkipBlock(cout, cond_channels, skip_channels, stack_kernel_size,
+                                           2 ** j if dilation else 1))
+        self.layers = nn.ModuleList(layers)
         self.final_layer = nn.Sequential(nn.ReLU(), WNConv1d(skip_channels, skip_channels, 1), nn.ReLU(),
                                          WNConv1d(skip_channels, final_channels, 1))
-        self.ch, self.skip_ch, self.final_ch, self.cond_ch, self.n_stacks = (ch, skip_channels, final_channels,
-                                                                             cond_channels, nd)
+        self.skip_ch, self.final_ch, self.cond_ch = skip_channels, final_channels, cond_channels
 
 
 class _StepFunction(torch.autograd.Function):
@@ -160,6 +179,8 @@ class Model(nn.Module):
         return self.decode((self.encode(x), y_idx))
 
     def remove_weight_norm(self):
+        if any(isinstance(m, ResampleConv1d) for m in self.modules()):
+            raise NotImplementedError("remove_weight_norm with resampling convs")
         for m in self.modules():
             if isinstance(m, WNConv1d) and m.has_weight_norm:
                 m.remove_weight_norm()

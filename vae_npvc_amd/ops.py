@@ -255,6 +255,12 @@ def groupnorm_stats(x, T, G, partials, mean_rstd, eps=1e-5):
     return mean_rstd
 
 
+def gn_lrelu_fwd(h, g, T, mean_rstd, gamma, beta):
+    """g = LeakyReLU_0.2(GroupNorm_1(h)) with precomputed statistics mean_rstd [B, 2]."""
+    call("vqx_gn_lrelu_fwd", ptr(h), h.stride(0), ptr(g), g.stride(0), dt_code(h.dtype), h.shape[0], T, h.shape[1],
+         ptr(mean_rstd), ptr(gamma), ptr(beta), stream_ptr())
+
+
 def gn_glu_fwd(u, g, T, mean_rstd, gamma, beta):
     call("vqx_gn_glu_fwd", ptr(u), u.stride(0), ptr(g), g.stride(0), dt_code(u.dtype), u.shape[0], T, u.shape[1],
          ptr(mean_rstd), ptr(gamma), ptr(beta), stream_ptr())
