@@ -456,7 +456,10 @@ const char* vqx_last_error(void);
 /* bf16 conv GEMM kernel policy (process-wide, for tests and A/B runs):
  * 0 = automatic (3-tap, pad-1 FWD/DGRAD with T % 128 == 0 run the tap-reuse
  * kernel, everything else the implicit-im2col kernel), 1 = implicit-im2col
- * kernel only.  The environment variable VQX_TAP_REUSE=0 forces 1. */
+ * kernel only, 2 / 3 = the tall tap-reuse kernel with 256 / 512-frame tiles
+ * wherever T % 256 == 0 and the frames divide, 4 = the 128-frame tap-reuse
+ * kernel only.  The environment variable VQX_TAP_REUSE=0 forces 1, VQX_TR8=0/1/2
+ * fixes the tall kernel's choice under policy 0. */
 int vqx_set_gemm_tile(int32_t policy);
 
 /* Launch probe (measurement only; not reentrant while enabled).  While on,

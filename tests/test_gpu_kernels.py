@@ -442,6 +442,60 @@ def test_conv_tap_reuse_matches_im2col_and_fp64(mode, n_utt, T, cin, cout):
     assert relerr(outs[0], ref) < 2e-5
 
 
+@pytest.mark.parametrize("mode", ["fwd", "dgrad"])
+@pytest.mark.parametrize("n_utt,T,cin,cout", [(2, 256, 512, 512), (1, 512, 512, 1024), (4, 256, 1024, 512),
+                                               (2, 768, 128, 224), (8, 256, 512, 1024)])
+def test_conv_tall_tap_reuse_matches_tap_reuse_and_fp64(mode, n_utt, T, cin, cout):
+    """The tall tap-reuse kernel (vqx_gemm_kernel.h conv_tr8_kernel: 256 or 512
+    frames x 128 columns per 8-wave workgroup, one staged window with halo rows
+    per 256-frame segment) against the 128-frame tap-reuse kernel and fp64
+    torch: segments that start / end utterances and segments whose halo frames
+    belong to the same utterance (T = 512, 768), ragged columns (224), and the
+    fused epilogues the engine runs on it (bias + residual, GroupNorm
+    statistics tiles in FWD, column sums in DGRAD)."""
+    ops = _ops()
+    from vae_npvc_amd import _lib as L
+    torch.manual_seed(17)
+    N = n_utt * T
+    k_in, k_out = (cin, cout) if mode == "fwd" else (cout, cin)
+    a = torch.randn(N, k_in, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(cout, cin, 3, device=DEV) / (cin * 3) ** 0.5).to(torch.bfloat16).float()
+    wp = pack(w).to(torch.bfloat16)
+    bias = torch.randn(k_out, device=DEV)
+    res = torch.randn(N, k_out, device=DEV).to(torch.bfloat16)
+    tn = -(-k_out // 128)
+    outs = []
+    policies = [4, 2] + ([3] if N % 512 == 0 else [])
+    for policy in policies:
+        L.call("vqx_set_gemm_tile", policy)
+        y = torch.empty(N, k_out, device=DEV, dtype=torch.float32)
+        y2 = torch.empty(N, k_out, device=DEV, dtype=torch.bfloat16)
+        red = torch.full((N // 128, tn * 4 if mode == "fwd" else k_out), float("nan"), device=DEV)
+        call = ops.conv_fwd if mode == "fwd" else ops.conv_dgrad
+        kw = dict(T=T, cin=k_in, cout=k_out, ntaps=3, pad=1)
+        call(a, wp, y, bias=bias, res=res, out_f32=True, **kw)
+        if mode == "fwd" and k_out % 128 == 0:
+            call(a, wp, y2, bias=bias, gn_stats=red, gn_groups=k_out // 128 if k_out <= 512 else 2, **kw)
+        elif mode == "dgrad":
+            call(a, wp, y2, bias=bias, colsum=red, **kw)
+        torch.cuda.synchronize()
+        outs.append((y, y2, red))
+    L.call("vqx_set_gemm_tile", 0)
+    ad = a.double().cpu().view(n_utt, T, k_in).permute(0, 2, 1)
+    ref = F.conv1d(ad, w.double().cpu(), padding=1) if mode == "fwd" else \
+        F.conv_transpose1d(ad, w.double().cpu(), padding=1)
+    ref = ref.permute(0, 2, 1).reshape(N, k_out) + bias.double().cpu()
+    for y, y2, red in outs:
+        assert relerr(y, ref + res.double().cpu()) < 2e-5
+        assert relerr(y, outs[0][0]) < 1e-5
+        if mode == "dgrad" or k_out % 128 == 0:
+            assert relerr(y2.float(), outs[0][1].float()) < 1e-2  # one bf16 rounding apart at most
+            assert relerr(red, outs[0][2]) < 1e-4, (red - outs[0][2]).abs().max()
+    if mode == "dgrad":  # per-128-frame column sums of the stored bf16 output
+        cs = outs[-1][1].double().cpu().view(N // 128, 128, k_out).sum(1)
+        assert relerr(outs[-1][2], cs) < 5e-3  # fp32 sums of the values before their bf16 rounding
+
+
 @pytest.mark.parametrize("sign", [1, -1])
 @pytest.mark.parametrize("n_utt,T,r_dim,c_dim,splits", [(2, 128, 512, 512, 3), (3, 64, 80, 192, 2), (1, 256, 128, 64, 4),
                                                          (2, 256, 1024, 512, 5), (4, 64, 256, 128, 16),

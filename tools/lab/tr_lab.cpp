@@ -1,0 +1,119 @@
+// Stand-alone timing lab for the tap-reuse conv kernels (conv_tr_kernel,
+// conv_tr8_kernel) at the config-2 3-tap shapes.  Built per variant with
+// -DVQX_GEMM_LAB=0..3 (full / no operand DMA / no MFMA / no epilogue) by
+// tools/lab/tr_lab.sh; prints the mean launch time over 20 launches.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "vqx_gemm_kernel.h"
+
+using namespace vqx;
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                 \
+    }                                                                          \
+  } while (0)
+
+struct Shape {
+  const char* name;
+  int mode;
+  int64_t N;
+  int T, kin, kout;
+};
+
+static float time_us(const void* fn, int grid, int block, GemmParams P, int reps) {
+  void* args[] = {(void*)&P};
+  for (int i = 0; i < 3; ++i) CK(hipLaunchKernel(fn, dim3(grid), dim3(block), args, 0, 0));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  CK(hipEventRecord(a, 0));
+  for (int i = 0; i < reps; ++i) CK(hipLaunchKernel(fn, dim3(grid), dim3(block), args, 0, 0));
+  CK(hipEventRecord(b, 0));
+  CK(hipEventSynchronize(b));
+  float ms = 0.f;
+  CK(hipEventElapsedTime(&ms, a, b));
+  CK(hipEventDestroy(a));
+  CK(hipEventDestroy(b));
+  return 1e3f * ms / reps;
+}
+
+template <int MODE, int EK>
+static void run(const Shape& s, void* x, void* w, void* y, float* part) {
+  GemmParams P = {};
+  P.a = x;
+  P.b = w;
+  P.a_bytes = ((s.N - 1) * (int64_t)s.kin + s.kin) * 2;
+  P.b_bytes = (int64_t)3 * s.kin * s.kout * 2;
+  P.n_rows = s.N;
+  P.T = s.T;
+  P.lda = s.kin;
+  P.kcin = s.kin;
+  P.K = 3 * s.kin;
+  P.Mc = (int)s.N;
+  P.Nc = s.kout;
+  P.ntaps = 3;
+  P.pad = 1;
+  P.sign = 1;
+  P.dil = 1;
+  P.cdim = s.kout;
+  P.tiles_n = s.kout / 128;
+  P.splits = 1;
+  P.y = y;
+  P.ldy = s.kout;
+  P.epi = EK == EK_GNSTATS ? VQX_EPI_GNSTATS : 0;
+  P.stat_part = part;
+  P.gn_groups = s.kout > 512 ? 2 : s.kout / 128;
+  const double fl = 2.0 * s.N * s.kout * 3.0 * s.kin;
+  struct V {
+    const char* name;
+    const void* fn;
+    int rows, block;
+  } vs[] = {{"tr128", (const void*)conv_tr_kernel<MODE, EK, 32>, 128, 256},
+            {"tr8x256", (const void*)conv_tr8_kernel<MODE, EK, 1>, 256, 512},
+            {"tr8x512", (const void*)conv_tr8_kernel<MODE, EK, 2>, 512, 512}};
+  for (const V& v : vs) {
+    P.tiles_m = (int)(s.N / v.rows);
+    const float us = time_us(v.fn, P.tiles_m * P.tiles_n, v.block, P, 20);
+    printf("lab%d %-13s EK%d %-8s %7.1f us %7.1f TF\n", VQX_GEMM_LAB, s.name, EK, v.name, us, fl / us * 1e-6);
+  }
+}
+
+int main() {
+  const Shape shapes[] = {{"dec_in_fwd", MODE_FWD, 16384, 256, 512, 1024},
+                          {"enc_k3_fwd", MODE_FWD, 16384, 256, 512, 512},
+                          {"dec_in_dgrad", MODE_DGRAD, 16384, 256, 1024, 512},
+                          {"enc_k3_dgrad", MODE_DGRAD, 16384, 256, 512, 512}};
+  const size_t xb = (size_t)16384 * 1024 * 2, wb = (size_t)3 * 1024 * 1024 * 2;
+  std::vector<unsigned short> h(xb / 2);
+  unsigned r = 12345u;
+  for (auto& v : h) {
+    r = r * 1664525u + 1013904223u;
+    v = (unsigned short)(0x3c00 + ((r >> 16) & 0x7f) - 0x40) | ((r & 1) << 15);  // small bf16 values
+  }
+  void *x, *w, *y;
+  float* part;
+  CK(hipMalloc(&x, xb));
+  CK(hipMalloc(&w, wb));
+  CK(hipMalloc(&y, xb));
+  CK(hipMalloc(&part, (size_t)128 * 8 * 4 * 4));
+  CK(hipMemcpy(x, h.data(), xb, hipMemcpyHostToDevice));
+  CK(hipMemcpy(w, h.data(), wb, hipMemcpyHostToDevice));
+  for (const Shape& s : shapes) {
+    if (s.mode == MODE_FWD) {
+      run<MODE_FWD, EK_NONE>(s, x, w, y, part);
+      run<MODE_FWD, EK_GNSTATS>(s, x, w, y, part);
+    } else {
+      run<MODE_DGRAD, EK_NONE>(s, x, w, y, part);
+    }
+  }
+  CK(hipDeviceSynchronize());
+  return 0;
+}

@@ -50,7 +50,9 @@ void gemm_launch(const void* fn, int grid, hipStream_t s, const GemmParams& P, c
   (void)hipExtLaunchKernel(fn, dim3(grid), dim3(block), args, 0, s, ev.first, ev.second, 0);
 }
 
-// vqx_set_gemm_tile: 0 = automatic, 1 = implicit-im2col kernel only
+// vqx_set_gemm_tile: 0 = automatic, 1 = implicit-im2col kernel only,
+// 2 / 3 = tap reuse through conv_tr8_kernel with 1 / 2 frame segments where it
+// applies, 4 = tap reuse through conv_tr_kernel only
 static int g_gemm_policy = 0;
 
 bool tap_reuse_enabled() {
@@ -58,7 +60,7 @@ bool tap_reuse_enabled() {
     const char* e = getenv("VQX_TAP_REUSE");
     return !(e && e[0] == '0');
   }();
-  return env_on && g_gemm_policy == 0;
+  return env_on && g_gemm_policy != 1;
 }
 
 int tr_stage_channels() {
@@ -67,6 +69,15 @@ int tr_stage_channels() {
     return (e && e[0] == '1' && e[1] == '6') ? 16 : 32;
   }();
   return bkc;
+}
+
+int tr8_policy() {
+  static const int pol = [] {
+    const char* e = getenv("VQX_TR8");  // 0 = off, 1/2 = SEGS, unset = automatic (-1)
+    return (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : -1;
+  }();
+  if (g_gemm_policy >= 2) return g_gemm_policy == 4 ? 0 : g_gemm_policy - 1;
+  return pol;
 }
 
 int wgrad_kgroups() {
@@ -219,7 +230,7 @@ extern "C" int vqx_wgrad_tiles(int64_t n_rows, int32_t T, int32_t r_dim, int32_t
 }
 
 extern "C" int vqx_set_gemm_tile(int32_t policy) {
-  if (policy < 0 || policy > 1) { set_error("vqx_set_gemm_tile: policy %d not in 0..1", policy); return -1; }
+  if (policy < 0 || policy > 4) { set_error("vqx_set_gemm_tile: policy %d not in 0..4", policy); return -1; }
   g_gemm_policy = policy;
   return 0;
 }

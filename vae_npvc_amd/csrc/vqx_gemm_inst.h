@@ -39,9 +39,33 @@ inline bool wgrad_tr_ok(int64_t n_rows, int T, int c_dim, int ntaps, int pad, in
 // channels per tap-reuse stage: 32 (2-deep ring, default) or 16 (4-deep ring; env VQX_TR_BKC=16)
 int tr_stage_channels();
 
+// frame segments per conv_tr8_kernel tile (0 = use conv_tr_kernel).  Env
+// VQX_TR8=0/1/2 forces it.  By default the 512-frame tile where it still gives
+// every CU a workgroup (config 2: dec_in FWD, 57 vs 61 us in the step); the
+// 256-frame tile measured equal on enc FWD and 7-10% slower on both DGRADs
+// (profiles/r02/tr_lab.txt), so it is never picked automatically.
+int tr8_policy();
+inline int tr8_segs(const GemmParams& P) {
+  if (P.T % 256 || tr_stage_channels() != 32) return 0;
+  const int pol = tr8_policy();
+  const int tn = (P.Nc + kBN - 1) / kBN;
+  if (pol == 0) return 0;
+  if (pol == 1 || pol == 2) return P.n_rows % (256 * pol) == 0 ? pol : 0;
+  if (P.n_rows % 512 == 0 && (P.n_rows / 512) * tn >= 256) return 2;
+  return 0;
+}
+
 template <int MODE, int EK>
 void launch_tr(const GemmParams& P, int grid, hipStream_t s) {
   const double flops = 2.0 * (double)P.n_rows * P.Nc * P.K;
+  if (const int segs = tr8_segs(P)) {
+    GemmParams Q = P;
+    Q.tiles_m = (int)(P.n_rows / (256 * segs));
+    const int info8[5] = {VQX_BF16, MODE, segs, 3, EK};  // gen = 3: conv_tr8_kernel, prologue slot = SEGS
+    if (segs == 2) gemm_launch((const void*)conv_tr8_kernel<MODE, EK, 2>, Q.tiles_m * Q.tiles_n, s, Q, info8, flops, 512);
+    else gemm_launch((const void*)conv_tr8_kernel<MODE, EK, 1>, Q.tiles_m * Q.tiles_n, s, Q, info8, flops, 512);
+    return;
+  }
   const int bkc = tr_stage_channels();
   // gen = 2: tap-reuse kernel; the prologue slot carries the stage depth in channels
   const int info[5] = {VQX_BF16, MODE, bkc, 2, EK};

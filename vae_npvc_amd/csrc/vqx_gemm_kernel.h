@@ -28,6 +28,9 @@
 // consecutive output elements per register group: the epilogue does vector
 // loads/stores (8 B bf16, 16 B f32) for bias, residual, masks and results.
 #pragma once
+#include <type_traits>
+#include <utility>
+
 #include "vqx_common.h"
 
 // tools/gemm_lab.hip only: 1 = no operand DMA in the main loop, 2 = no MFMA
@@ -39,8 +42,27 @@
 namespace vqx {
 
 constexpr int kBN = 128;  // tile width (and height)
+// tools/lab/tr_lab.hip builds the tap-reuse kernels with VQX_GEMM_LAB = 1 (no
+// operand DMA in the main loop), 2 (no fragment reads / MFMAs), 3 (no epilogue)
+#ifndef VQX_GEMM_LAB
+#define VQX_GEMM_LAB 0
+#endif
+#ifndef VQX_EPI_PREFETCH  // 0: the 1x1 epilogues load their row operands pass by pass (A/B)
+#define VQX_EPI_PREFETCH 1
+#endif
 constexpr unsigned kOOB = 0x80000000u;  // buffer offset that is always out of range -> loads 0
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
+
+// f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>): loop bodies
+// whose index must be a compile-time constant before inlining-time SROA
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 
 struct GemmParams {
   const void* a;   // FWD/DGRAD: activation [N][lda]   WGRAD: p [N][lda]
@@ -250,16 +272,130 @@ __host__ __device__ constexpr int ek_mask(int ek) {
        : ~0;
 }
 
+// Row operands of a bf16 fused epilogue, prefetched into registers for the
+// thread's 8 (slab, pass) rows right after the prologue DMA is issued
+// (conv_gemm_kernel, FWD), instead of one dependent load per row pass inside
+// the epilogue.  Two slots per row; the roles are picked from the flags in
+// the order GroupNorm input (GNADD / GNBWD), its second GLU half, mask,
+// residual; operands without a slot are loaded in the epilogue as before.
+// The 1x1 epilogues are bound by the burst of HBM traffic every workgroup
+// issues at the same moment, not by these latencies: the prefetch buys 3-8%
+// (tools/lab/k1_lab.cpp).
+enum { EPR_NONE = 0, EPR_GNH, EPR_GNH2, EPR_MASK, EPR_RES };
+typedef unsigned u32x4e_t __attribute__((ext_vector_type(4)));  // plain vector (HIP's uint4 is a union: kept in scratch)
+struct EpiRows {
+  u32x4e_t r0[8], r1[8];
+  int k0, k1;
+};
+
+template <int EK>
+__device__ __forceinline__ void epi_prefetch(const GemmParams& P, int m0, int n0, int tid, EpiRows& R) {
+  constexpr int EM = ek_mask(EK);
+  const int epi = P.epi & EM;
+  const int er = tid >> 4, col = n0 + (tid & 15) * 8;
+  const bool to_out2 = (epi & VQX_EPI_SPLIT) && col >= P.split_col;  // neither mask nor res read there
+  const bool g = epi & (VQX_EPI_GNADD | VQX_EPI_GNBWD), g2 = (epi & VQX_EPI_GNBWD) && P.gn_glu;  // g2 implies g
+  const bool mk = (epi & VQX_EPI_MASK) && !to_out2, rs = (epi & VQX_EPI_RES) && !to_out2;
+  const int k0 = g ? EPR_GNH : mk ? EPR_MASK : rs ? EPR_RES : EPR_NONE;
+  const int k1 = g ? (g2 ? EPR_GNH2 : mk ? EPR_MASK : rs ? EPR_RES : EPR_NONE) : (mk && rs) ? EPR_RES : EPR_NONE;
+  R.k0 = k0;
+  R.k1 = k1;
+  auto addr = [&](int k, int64_t row) -> const u32x4e_t* {
+    const bf16_t* b = k == EPR_MASK ? (const bf16_t*)P.mask + row * P.ldmask
+                    : k == EPR_RES  ? (const bf16_t*)P.res + row * P.ldres
+                                    : (const bf16_t*)P.gn_h + row * P.ldgn + (k == EPR_GNH2 ? P.Nc : 0);
+    return (const u32x4e_t*)(b + col);
+  };
+  static_for<8>([&](auto i_c) __attribute__((always_inline)) {
+    constexpr int i = decltype(i_c)::value;
+    const int64_t row = (int64_t)m0 + (i >> 2) * 64 + (i & 3) * 16 + er;
+    const bool ok = row < P.n_rows && col < P.Nc;
+    const u32x4e_t z = {0u, 0u, 0u, 0u};
+    R.r0[i] = (ok && k0 != EPR_NONE) ? *addr(k0, row) : z;
+    R.r1[i] = (ok && k1 != EPR_NONE) ? *addr(k1, row) : z;
+  });
+}
+
+__device__ __forceinline__ void unpack8(u32x4e_t u, float* f) {
+  const unsigned w[4] = {u[0], u[1], u[2], u[3]};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    f[2 * k] = __uint_as_float(w[k] << 16);
+    f[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+  }
+}
+
+// The prefetched operands of one epilogue row (by value: the 8-row arrays
+// are indexed with compile-time pass numbers only, so they stay in VGPRs).
+struct EpiOps {
+  u32x4e_t p0, p1;
+  int k0, k1;
+};
+template <int I, bool PRE>
+__device__ __forceinline__ EpiOps epi_ops(const EpiRows* R) {
+  EpiOps o = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, EPR_NONE, EPR_NONE};
+  if constexpr (PRE) {  // (a runtime null test on R would keep the struct out of registers)
+    o.p0 = R->r0[I];
+    o.p1 = R->r1[I];
+    o.k0 = R->k0;
+    o.k1 = R->k1;
+  }
+  return o;
+}
+
+// Per-channel vectors of the thread's 8 output columns (bias, GroupNorm
+// gamma/beta of both GLU halves), loaded once per tile instead of once per row
+// pass when the epilogue prefetches (PRE).
+struct EpiVec {
+  float b[8], ga[8], be[8], gb[8], bb[8];
+};
+template <int EMASK>
+__device__ __forceinline__ void epi_vec_load(const GemmParams& P, int col, EpiVec& V) {
+  const int epi = P.epi & EMASK;
+  if (col >= P.Nc) return;
+  if (epi & VQX_EPI_BIAS) ld8<float>(P.bias, col, V.b);
+  if (epi & (VQX_EPI_GNADD | VQX_EPI_GNBWD)) {
+    ld8<float>(P.gn_gamma, col, V.ga);
+    if (!(epi & VQX_EPI_GNBWD) || P.gn_glu) ld8<float>(P.gn_beta, col, V.be);
+    if ((epi & VQX_EPI_GNBWD) && P.gn_glu) {
+      ld8<float>(P.gn_gamma, col + P.Nc, V.gb);
+      ld8<float>(P.gn_beta, col + P.Nc, V.bb);
+    }
+  }
+}
+// 8 floats of a per-channel vector: the hoisted copy, else from memory
+template <bool PRE>
+__device__ __forceinline__ void vec8(const float (&pre)[8], const float* p, int64_t i, float* f) {
+  if constexpr (PRE) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = pre[e];
+  } else {
+    ld8<float>(p, i, f);
+  }
+}
+
+// 8 values of a row operand: from the prefetched slot holding `role`, else from memory
+template <typename T>
+__device__ __forceinline__ void row_op(const EpiOps& o, int role, const void* base, int64_t off, float* t) {
+  if constexpr (sizeof(T) == 2) {
+    if (o.k0 == role) { unpack8(o.p0, t); return; }
+    if (o.k1 == role) { unpack8(o.p1, t); return; }
+  }
+  ld8<T>(base, off, t);
+}
+
 // FWD/DGRAD epilogue on 8 consecutive output channels of one frame, in the
 // order bias, row bias, activation-derivative mask, split to out2 (returns),
-// residual, GroupNorm-apply add, activation, store.
-template <typename T, int EMASK>
-__device__ __forceinline__ void epilogue8(const GemmParams& P, int64_t row, int col, float* v, const float* gmr) {
+// residual, GroupNorm-apply add, activation, store.  `o`: prefetched row
+// operands (none: k0 = k1 = EPR_NONE).
+template <typename T, int EMASK, bool PRE = false>
+__device__ __forceinline__ void epilogue8(const GemmParams& P, int64_t row, int col, float* v, const float* gmr,
+                                          const EpiOps& o, const EpiVec& V) {
   const int epi = P.epi & EMASK;
   const int bidx = (epi & (VQX_EPI_ROWBIAS | VQX_EPI_GNADD)) ? (int)row / P.T : 0;  // 32-bit: n_rows < 2^31 (host-checked)
   float t[8];
   if (epi & VQX_EPI_BIAS) {
-    ld8<float>(P.bias, col, t);
+    vec8<PRE>(V.b, P.bias, col, t);
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] += t[e];
   }
@@ -269,7 +405,7 @@ __device__ __forceinline__ void epilogue8(const GemmParams& P, int64_t row, int 
     for (int e = 0; e < 8; ++e) v[e] += t[e];
   }
   if (epi & VQX_EPI_MASK) {
-    ld8<T>(P.mask, row * P.ldmask + col, t);
+    row_op<T>(o, EPR_MASK, P.mask, row * P.ldmask + col, t);
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] *= (t[e] > 0.f ? 1.f : P.mask_slope) * P.mask_scale;
   }
@@ -286,15 +422,15 @@ __device__ __forceinline__ void epilogue8(const GemmParams& P, int64_t row, int 
     return;
   }
   if (epi & VQX_EPI_RES) {
-    ld8<T>(P.res, row * P.ldres + col, t);
+    row_op<T>(o, EPR_RES, P.res, row * P.ldres + col, t);
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] += t[e];
   }
   if (epi & VQX_EPI_GNADD) {
     float ga[8], be[8];
-    ld8<T>(P.gn_h, row * P.ldgn + col, t);
-    ld8<float>(P.gn_gamma, col, ga);
-    ld8<float>(P.gn_beta, col, be);
+    row_op<T>(o, EPR_GNH, P.gn_h, row * P.ldgn + col, t);
+    vec8<PRE>(V.ga, P.gn_gamma, col, ga);
+    vec8<PRE>(V.be, P.gn_beta, col, be);
     const float mean = gmr[2 * bidx], rstd = gmr[2 * bidx + 1];  // gmr: P.gn_mr or the in-launch merge
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] += (t[e] - mean) * rstd * ga[e] + be[e];
@@ -318,12 +454,13 @@ __device__ __forceinline__ void epilogue8(const GemmParams& P, int64_t row, int 
 // of group a, s[2..3] of group b (GLU: u = [a | b], dh through
 // tanh(h_a)*sigmoid(h_b), layers.py:240-242).  u, mean/rstd, gamma, beta are
 // the forward GroupNorm's (gn_h, gn_mr, gn_gamma, gn_beta).
-template <typename T>
-__device__ __forceinline__ void gnbwd8(const GemmParams& P, int64_t row, int col, const float* dy, float* s) {
+template <typename T, bool PRE = false>
+__device__ __forceinline__ void gnbwd8(const GemmParams& P, int64_t row, int col, const float* dy, float* s,
+                                       const EpiOps& o, const EpiVec& V) {
   const int b = (int)row / P.T;
   float ua[8], ga[8];
-  ld8<T>(P.gn_h, row * P.ldgn + col, ua);
-  ld8<float>(P.gn_gamma, col, ga);
+  row_op<T>(o, EPR_GNH, P.gn_h, row * P.ldgn + col, ua);
+  vec8<PRE>(V.ga, P.gn_gamma, col, ga);
   if (!P.gn_glu) {
     const int grp = P.gn_groups == 1 ? 0 : col / (P.Nc / P.gn_groups);
     const float m = P.gn_mr[(b * P.gn_groups + grp) * 2], r = P.gn_mr[(b * P.gn_groups + grp) * 2 + 1];
@@ -337,10 +474,10 @@ __device__ __forceinline__ void gnbwd8(const GemmParams& P, int64_t row, int col
   }
   const int half = P.Nc;
   float ub[8], gb[8], ba[8], bb[8];
-  ld8<T>(P.gn_h, row * P.ldgn + col + half, ub);
-  ld8<float>(P.gn_gamma, col + half, gb);
-  ld8<float>(P.gn_beta, col, ba);
-  ld8<float>(P.gn_beta, col + half, bb);
+  row_op<T>(o, EPR_GNH2, P.gn_h, row * P.ldgn + col + half, ub);
+  vec8<PRE>(V.gb, P.gn_gamma, col + half, gb);
+  vec8<PRE>(V.be, P.gn_beta, col, ba);
+  vec8<PRE>(V.bb, P.gn_beta, col + half, bb);
   const float ma = P.gn_mr[b * 4], ra = P.gn_mr[b * 4 + 1], mb = P.gn_mr[b * 4 + 2], rb = P.gn_mr[b * 4 + 3];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -408,13 +545,16 @@ __device__ __forceinline__ void wait_vm(int n) {
 // columns per row, every global access 16 B and each row segment contiguous.
 // Lane holds (before the transpose) output row wm*64 + mi*32 + r32 and, per
 // register group gq, columns wn*64 + ni*32 + 8*gq + 4*h + (0..3).  Needs
-// 44 KiB of `smem`; the caller's staging buffers must be free.
-template <typename T, int MODE, int EK>
+// 44 KiB of `smem`; the caller's staging buffers must be free.  `tid` is the
+// thread's index in the 4-wave group that owns the tile (conv_tr8_kernel runs
+// two such groups side by side; every group passes the same barriers).
+template <typename T, int MODE, int EK, bool PRE = false>
 __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&acc)[2][2], char* smem, int m0, int n0,
-                                              int tn, int split, const float* gmr) {
+                                              int tn, int split, const float* gmr, int tid,
+                                              const EpiRows* R = nullptr) {
   constexpr int EMASK = ek_mask(EK);
   constexpr int SUB = 1;
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
   const int r32 = lane & 31, h = lane >> 5;
@@ -426,9 +566,13 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // COLSUM accumulators
   float mn = 0.f, mm = 0.f, mq = 0.f;                       // GNSTATS running (count, mean, M2)
   float gs[4] = {0.f, 0.f, 0.f, 0.f};                       // GNBWD sums
+  EpiVec V;
+  if constexpr (PRE && MODE != MODE_WGRAD) epi_vec_load<EMASK>(P, n0 + ec, V);
   __syncthreads();  // staging buffers are free
-#pragma unroll
-  for (int slab = 0; slab < 2 * SUB; ++slab) {
+  // slab and pass are compile-time constants (static_for), so the prefetched
+  // row operands R->r*[slab*4 + pass] are register-resident
+  static_for<2 * SUB>([&](auto slab_c) __attribute__((always_inline)) {
+    constexpr int slab = decltype(slab_c)::value;
     if (wm == slab) {
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
@@ -442,8 +586,8 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
           }
     }
     __syncthreads();
-#pragma unroll
-    for (int pass = 0; pass < 64 / EROWS; ++pass) {
+    static_for<64 / EROWS>([&](auto pass_c) __attribute__((always_inline)) {
+      constexpr int pass = decltype(pass_c)::value;
       const int lr = pass * EROWS + er;
       const f32x4_t lo = *(const f32x4_t*)(ep + lr * EP_LD + ec);
       const f32x4_t hi = *(const f32x4_t*)(ep + lr * EP_LD + ec + 4);
@@ -457,7 +601,8 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
         }
       } else {
         if (row < P.n_rows && col < P.Nc) {
-          epilogue8<T, EMASK>(P, row, col, v, gmr);
+          const EpiOps o = epi_ops<slab * 4 + pass, PRE>(R);
+          epilogue8<T, EMASK, PRE>(P, row, col, v, gmr, o, V);
 #pragma unroll
           for (int e = 0; e < 8; ++e) cs[e] += v[e];
           if (P.epi & EMASK & VQX_EPI_GNSTATS) {  // two-pass moments of the 8 values, merged
@@ -470,10 +615,10 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
             for (int e = 0; e < 8; ++e) q8 = fmaf(v[e] - m8, v[e] - m8, q8);
             moments_merge(mn, mm, mq, 8.f, m8, q8);
           }
-          if (P.epi & EMASK & VQX_EPI_GNBWD) gnbwd8<T>(P, row, col, v, gs);
+          if (P.epi & EMASK & VQX_EPI_GNBWD) gnbwd8<T, PRE>(P, row, col, v, gs, o, V);
         }
       }
-    }
+    });
     __syncthreads();
     if constexpr (MODE != MODE_WGRAD) {
       // per-(128-row group, column tile) GroupNorm partials
@@ -531,7 +676,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
         __syncthreads();
       }
     }
-  }
+  });
 }
 
 // Staging layout.  The block tile is 128 x 128 with 4 waves in a 2 x 2 grid
@@ -571,6 +716,10 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
+#ifdef VQX_GEMM_STAGGER  // lab only (tools/lab/k1_lab.cpp): delay the second resident workgroup of each CU
+  if (blockIdx.x >= gridDim.x / 2)
+    for (int i = 0; i < VQX_GEMM_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
+#endif
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
   const int tiles_mn = P.tiles_m * P.tiles_n;
   const int split = lin / tiles_mn;
@@ -884,12 +1033,22 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
     }
   };
 
+  // epilogue row operands of the bf16 FWD fused epilogues, prefetched with the
+  // prologue (tools/lab/k1_lab.cpp, profiles/r02/k1_lab.txt: SPLIT 33.4 -> 30.6 us,
+  // GNADD 26.9 -> 26.0 us; the DGRAD GNBWD epilogues, VALU-bound, ran 5-9% slower
+  // with it and keep loading pass by pass)
+  constexpr bool kPrefetch = sizeof(T) == 2 && MODE == MODE_FWD && EK != EK_NONE && EK != EK_ALL && VQX_EPI_PREFETCH;
+  EpiRows rows;
+  if constexpr (kPrefetch) {
+    if (nk <= 0) epi_prefetch<EK>(P, m0, n0, tid, rows);
+  }
   if (nk > 0) {
     // prologue: tiles 0 .. NST-2 in flight, then wait for tile 0
     const int pre = nk < NST - 1 ? nk : NST - 1;
 #pragma unroll
     for (int t = 0; t < NST - 1; ++t)
       if (t < pre) dma_tile(t, t);
+    if constexpr (kPrefetch) epi_prefetch<EK>(P, m0, n0, tid, rows);  // lands with the prologue DMA
     wait_vm(NP * (pre - 1));
     __builtin_amdgcn_s_barrier();
     int buf = 0;
@@ -928,7 +1087,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
   }
   return;
 #endif
-  tile_epilogue<T, MODE, EK>(P, acc, smem, m0, n0, tn, split, gmr);
+  tile_epilogue<T, MODE, EK, kPrefetch>(P, acc, smem, m0, n0, tn, split, gmr, (int)threadIdx.x, &rows);
 }
 
 
@@ -1091,8 +1250,8 @@ __global__ __launch_bounds__(256, 2) void conv_tr_kernel(GemmParams P) {
     __builtin_amdgcn_s_barrier();
     int buf = 0;
     for (int kt = 0; kt < nk; ++kt) {
-      if (kt + NST - 1 < nk) dma_stage(buf == 0 ? NST - 1 : buf - 1, kt + NST - 1);
-      compute_stage(buf);
+      if (VQX_GEMM_LAB != 1 && kt + NST - 1 < nk) dma_stage(buf == 0 ? NST - 1 : buf - 1, kt + NST - 1);
+      if (VQX_GEMM_LAB != 2) compute_stage(buf);
       if constexpr (NST == 2) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       } else {  // stage kt+1 must have landed; later ones may stay in flight
@@ -1105,7 +1264,196 @@ __global__ __launch_bounds__(256, 2) void conv_tr_kernel(GemmParams P) {
       buf = buf + 1 == NST ? 0 : buf + 1;
     }
   }
-  tile_epilogue<T, MODE, EK>(P, acc, smem, m0, n0, tn, 0, P.gn_mr);
+  if (VQX_GEMM_LAB == 3) {  // keep the accumulators live
+    float t = 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) t += acc[0][0][e] + acc[0][1][e] + acc[1][0][e] + acc[1][1][e];
+    if (t == 12345.f) ((float*)P.y)[threadIdx.x] = t;
+    return;
+  }
+  tile_epilogue<T, MODE, EK>(P, acc, smem, m0, n0, tn, 0, P.gn_mr, (int)threadIdx.x);
+}
+
+// ---------------------------------------------------------------------------
+// Tall tap-reuse conv GEMM: the same 3-tap FWD / DGRAD as conv_tr_kernel, with
+// 256*SEGS frames x 128 columns per 8-wave workgroup (one per CU), for
+// T % 256 == 0.  conv_tr_kernel is bound by the L2 -> LDS staging rate
+// (~65 GB/s per CU): a 128-frame tile stages 9 KiB of frames + 24 KiB of
+// weights per 32-channel stage for 3.1 MFLOP (95 FLOP per staged byte).  The
+// staged frames serve all three taps, so a taller tile pays for its frames
+// once while the weight slice is amortised over more rows: SEGS = 2 stages
+// 33 KiB of frames + 24 KiB of weights for 12.6 MFLOP (219 FLOP/B), which
+// moves the bound from the staging rate to the MFMA rate.
+//
+// Frames are staged per 256-frame segment with its own halo rows (row 0 =
+// frame f0-1, row 257 = frame f0+256, zero at utterance edges), so every
+// segment lies inside one utterance.  The tile is 2*SEGS quadrants of
+// 128 x 128; the two 4-wave groups own SEGS quadrants each, every wave a
+// 64 x 64 block of each, laid out exactly as conv_tr_kernel's waves so that
+// each group runs tile_epilogue on its quadrants in its own 44 KiB of LDS.
+template <int MODE, int EK, int SEGS>
+__global__ __launch_bounds__(512, 1) void conv_tr8_kernel(GemmParams P) {
+  using T = bf16_t;
+  constexpr int BKC = 32, ES = 2, EPC = 8, KCH = 4;  // 64-B K-major rows
+  constexpr int SROWS = 258;                         // staged frames per segment
+  constexpr int AROWS = SEGS * SROWS;
+  constexpr int A_PIECES = (AROWS * BKC * ES + 1023) / 1024;
+  constexpr int A_BYTES = A_PIECES * 1024;
+  constexpr int PWA = (A_PIECES + 7) / 8;            // activation pieces per wave (some waves one fewer)
+  constexpr int TAP_BYTES = 128 * BKC * ES;
+  constexpr int TAP_PIECES = TAP_BYTES / 1024;
+  constexpr int PWB = 3 * TAP_PIECES / 8;            // weight pieces per wave
+  constexpr int STAGE = A_BYTES + 3 * TAP_BYTES;
+  constexpr int EPI_BYTES = 45056;                   // tile_epilogue's LDS per group
+  constexpr int SMEM = 2 * STAGE > 2 * EPI_BYTES ? 2 * STAGE : 2 * EPI_BYTES;
+  static_assert(3 * TAP_PIECES % 8 == 0, "weight pieces split evenly over 8 waves");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wid >> 2, wm = (wid >> 1) & 1, wn = wid & 1;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = lin / P.tiles_n, tn = lin - tm * P.tiles_n;
+  const int64_t m0 = (int64_t)tm * (256 * SEGS);
+  const int n0 = tn * kBN;
+  const int nk = P.kcin / BKC;
+
+  // activation pieces wid, wid+8, ...: stage row sr = seg*258 + r holds frame m0 + seg*256 - 1 + r
+  unsigned aoff[PWA];
+#pragma unroll
+  for (int i = 0; i < PWA; ++i) {
+    const int piece = wid + 8 * i;
+    const int c = piece * 64 + lane;
+    const int sr = c / KCH, kch = (c % KCH) ^ tr_kswz<KCH>(sr);
+    const int seg = sr / SROWS, r = sr - seg * SROWS;
+    const int64_t f0 = m0 + (int64_t)seg * 256;
+    bool ok = piece < A_PIECES && sr < AROWS;
+    if (r == 0 && f0 % P.T == 0) ok = false;
+    if (r == SROWS - 1 && (f0 + 256) % P.T == 0) ok = false;
+    // the descriptor base sits one activation row before P.a: frame f0-1+r is at row f0+r
+    aoff[i] = ok ? (unsigned)(((f0 + r) * P.lda + kch * EPC) * ES) : kOOB;
+  }
+  unsigned boff[PWB];
+#pragma unroll
+  for (int i = 0; i < PWB; ++i) {
+    const int pb = wid * PWB + i;
+    const int tap = pb / TAP_PIECES, c = (pb % TAP_PIECES) * 64 + lane;
+    if constexpr (MODE == MODE_FWD) {  // We[co][tap*kcin + ci], K-major rows of BKC channels
+      const int row = c / KCH, kch = (c % KCH) ^ tr_kswz<KCH>(row);
+      const int co = n0 + row;
+      boff[i] = co < P.Nc ? (unsigned)(((int64_t)co * P.K + tap * P.kcin + kch * EPC) * ES) : kOOB;
+    } else {  // forward weight We[co][j][ci] read as rows co of tap j = 2 - tap (taps flipped)
+      const int krow = c / 16, cch = (c % 16) ^ mn_swz(krow);
+      const int ci = n0 + cch * EPC;
+      boff[i] = ci < P.Nc ? (unsigned)(((int64_t)krow * 3 * P.cdim + (2 - tap) * P.cdim + ci) * ES) : kOOB;
+    }
+  }
+  const __amdgpu_buffer_rsrc_t rsA = rsrc_at(P.a, -(int64_t)P.lda * ES, P.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsB = rsrc_at(P.b, 0, P.b_bytes);
+
+  auto dma_stage = [&](int buf, int kt) {
+    const int c0 = kt * BKC;
+    const unsigned ksa = (unsigned)(c0 * ES);
+    const unsigned ksb = MODE == MODE_FWD ? (unsigned)(c0 * ES) : (unsigned)((int64_t)c0 * 3 * P.cdim * ES);
+    char* st = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < PWA; ++i)
+      if (wid + 8 * i < A_PIECES) dma16(rsA, st + (wid + 8 * i) * 1024, aoff[i] + ksa);
+#pragma unroll
+    for (int i = 0; i < PWB; ++i) dma16(rsB, st + A_BYTES + (wid * PWB + i) * 1024, boff[i] + ksb);
+  };
+
+  f32x16_t acc[SEGS][2][2];
+#pragma unroll
+  for (int j = 0; j < SEGS; ++j)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[j][i][k][e] = 0.f;
+
+  const int r32 = lane & 31, h = lane >> 5;
+  const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+  typedef short s16x8_t __attribute__((ext_vector_type(8)));
+  // stage row of this wave's first fragment row in quadrant j (tap 0)
+  int qrow[SEGS];
+#pragma unroll
+  for (int j = 0; j < SEGS; ++j) {
+    const int qd = grp * SEGS + j;  // 128-row quadrant of the tile
+    qrow[j] = (qd >> 1) * SROWS + (qd & 1) * 128 + wm * 64 + r32;
+  }
+
+  // (software-pipelining the fragment reads one (tap, 16-channel) group ahead
+  // measured 2-10% slower: tools/lab/tr_lab.cpp, profiles/r02/tr_lab.txt)
+  auto compute_stage = [&](int buf) {
+    const char* la = smem + buf * STAGE;
+#pragma unroll
+    for (int tap = 0; tap < 3; ++tap) {
+      const char* lb = la + A_BYTES + tap * TAP_BYTES;
+      constexpr int KS = BKC / 16;
+      bf16x8_t af[KS][SEGS][2], bfr[KS][2];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+          if constexpr (MODE == MODE_FWD) {
+            bfr[s][x] = *(const bf16x8_t*)(lb + tr_kmaj_off<KCH>(wn * 64 + x * 32 + r32, 2 * s + h));
+          } else {
+            const int kb = 16 * s + (g >> 1) * 8;
+            const int ch = ((wn * 64 + x * 32 + (g & 1) * 16) >> 3) + (p >> 1);
+            const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (VQX_LDS(s16x4_t)*)(lb + mnmaj_off<T>(kb + q, ch) + 8 * (p & 1)));
+            const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (VQX_LDS(s16x4_t)*)(lb + mnmaj_off<T>(kb + 4 + q, ch) + 8 * (p & 1)));
+            const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            bfr[s][x] = __builtin_bit_cast(bf16x8_t, v);
+          }
+#pragma unroll
+          for (int j = 0; j < SEGS; ++j)
+            af[s][j][x] = *(const bf16x8_t*)(la + tr_kmaj_off<KCH>(qrow[j] + x * 32 + tap, 2 * s + h));
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int j = 0; j < SEGS; ++j)
+#pragma unroll
+          for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+              acc[j][mi][ni] =
+                  __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[s][ni], af[s][j][mi], acc[j][mi][ni], 0, 0, 0);
+    }
+  };
+
+  if (nk > 0) {
+    dma_stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    int buf = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      if (VQX_GEMM_LAB != 1 && kt + 1 < nk) dma_stage(buf ^ 1, kt + 1);
+      if (VQX_GEMM_LAB != 2) compute_stage(buf);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      buf ^= 1;
+    }
+  }
+  if (VQX_GEMM_LAB == 3) {  // keep the accumulators live
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < SEGS; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) t += acc[j][0][0][e] + acc[j][0][1][e] + acc[j][1][0][e] + acc[j][1][1][e];
+    if (t == 12345.f) ((float*)P.y)[tid] = t;
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < SEGS; ++j)
+    tile_epilogue<T, MODE, EK>(P, acc[j], smem + grp * EPI_BYTES, (int)(m0 + (grp * SEGS + j) * 128), n0, tn, 0,
+                               P.gn_mr, tid & 255);
 }
 
 // ---------------------------------------------------------------------------

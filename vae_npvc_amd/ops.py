@@ -118,6 +118,8 @@ class LaunchProbe:
             bk = 64 if dt == L.VQX_BF16 else 32
             if gen == 2 and mode == 2:  # tap-reuse weight gradient (vqx_gemm_kernel.h wgrad_tr_kernel)
                 sym = f"vqx::wgrad_tr_kernel<{ek}, {pro}>"  # pro slot = K groups
+            elif gen == 3:  # tall tap-reuse kernel (vqx_gemm_kernel.h conv_tr8_kernel)
+                sym = f"vqx::conv_tr8_kernel<{mode}, {ek}, {pro}>"  # pro slot = frame segments
             elif gen == 2:  # tap-reuse kernel (3-tap FWD/DGRAD, vqx_gemm_kernel.h conv_tr_kernel)
                 sym = f"vqx::conv_tr_kernel<{mode}, {ek}, {pro}>"  # pro slot = channels per stage
             else:
