@@ -136,12 +136,15 @@ int vqx_conv1d_dgrad(const vqx_conv_args* a, vqx_stream_t stream);
 typedef struct vqx_wgrad_args {
   const void* p;
   const void* q;
-  float* slabs;      /* [splits][r_dim][ntaps*c_dim] */
+  void* slabs;       /* [splits][r_dim][ntaps*c_dim] of slab_dtype */
   int64_t n_rows;
   int32_t T, r_dim, c_dim, ntaps, pad, shift_sign, ldp, ldq;
   int32_t dtype, q_prologue, splits;
   float pro_scale;
   int32_t dil;       /* taps at n + sign*(j*dil - pad); 0 or 1 = dense */
+  int32_t slab_dtype; /* VQX_F32, or VQX_BF16 (bf16 operands only): each split's fp32 partial
+                         rounded once to bf16, half the slab bytes written here and read by
+                         vqx_weight_norm_bwd, which sums them in fp32 */
 } vqx_wgrad_args;
 
 int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream);
@@ -178,9 +181,10 @@ typedef struct vqx_wn_layer {
   float* norm;          /* [rows] ||v_o|| saved for the backward */
   float* dv;            /* bwd: [rows][cols] */
   float* dg;            /* bwd: [rows] */
-  const float* slabs;   /* bwd: wgrad slabs */
+  const void* slabs;    /* bwd: wgrad slabs (slab_dtype) */
   int32_t kind, cout, cin, k, splits, dtype;
   int32_t stride, pad;  /* kinds VQX_WN_RESAMPLE(_T) only */
+  int32_t slab_dtype;   /* VQX_F32 | VQX_BF16 (vqx_wgrad_args.slab_dtype) */
 } vqx_wn_layer;
 
 /* `layers_host` sizes the launch; the kernels read the same table from the
@@ -475,7 +479,7 @@ int vqx_probe_count(int64_t* n);
 int vqx_probe_read(int64_t i, int32_t* info5, double* flops, float* ms);
 
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
-#define VQX_ABI_VERSION 117
+#define VQX_ABI_VERSION 118
 int vqx_version(void);
 
 #ifdef __cplusplus

@@ -309,6 +309,50 @@ def test_dgrad_colsum_partials(n_utt, T, tile):
     assert relerr(part, want) < 1e-5
 
 
+@pytest.mark.parametrize("sdt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("kind,rows,other,k,splits,wn", [(0, 512, 512, 1, 32, True), (0, 640, 512, 1, 25, True),
+                                                        (1, 512, 1024, 3, 8, True), (0, 512, 512, 3, 16, True),
+                                                        (0, 80, 128, 1, 3, True), (1, 128, 80, 5, 1, True),
+                                                        (0, 256, 64, 1, 7, False)])
+def test_weight_norm_bwd_reduces_slabs_like_torch(sdt, kind, rows, other, k, splits, wn):
+    """vqx_weight_norm_bwd (wn_bwd_kernel): sums the split-K slabs (fp32 or
+    bf16) in a fixed order, maps them to v's layout (Conv1d rows cout: x =
+    j*cin + ci; ConvTranspose1d rows cin: x = j'*cout + co, tap k-1-j') and
+    forms the weight-norm gradients dv, dg of torch._weight_norm(v, g, 0);
+    1x1 rows split their 25-32 slabs over thread groups, wide rows do not;
+    a plain weight (weight norm removed) gets dW itself."""
+    ops = _ops()
+    from vae_npvc_amd import _lib as L
+    torch.manual_seed(21 + rows + k)
+    cout, cin = (rows, other) if kind == 0 else (other, rows)
+    v = torch.randn(rows, other * k, device=DEV)
+    g = torch.rand(rows, device=DEV) + 0.5 if wn else None
+    slabs = torch.randn(splits, rows, k * other, device=DEV).to(sdt)
+    wp = torch.empty(cout, k * cin, device=DEV, dtype=torch.bfloat16)
+    norm = torch.empty(rows, device=DEV)
+    dv = torch.full_like(v, float("nan"))
+    dg = torch.full((rows,), float("nan"), device=DEV) if wn else None
+    ent = dict(v=v, g=g, w_packed=wp, norm=norm, kind=kind, cout=cout, cin=cin, k=k, dtype=L.VQX_BF16,
+               splits=splits)
+    if wn:
+        ops.weight_norm_fwd(ops.wn_table([ent]))
+    else:
+        norm.fill_(1.0)
+    ops.weight_norm_bwd(ops.wn_table([dict(ent, dv=dv, dg=dg, slabs=slabs)]))
+    torch.cuda.synchronize()
+    S = slabs.double().cpu().sum(0).view(rows, k, other)  # [row][j][c]
+    dW = S.permute(0, 2, 1) if kind == 0 else S.flip(1).permute(0, 2, 1)  # v layout [row][c][j]
+    dW = dW.reshape(rows, other * k)
+    if not wn:
+        assert relerr(dv, dW) < 1e-6
+        return
+    vd = v.double().cpu().requires_grad_(True)
+    gd = g.double().cpu().requires_grad_(True)
+    torch._weight_norm(vd, gd.view(rows, 1), 0).backward(dW)
+    assert relerr(dv, vd.grad) < 1e-5
+    assert relerr(dg, gd.grad) < 1e-5
+
+
 def test_linear_batched_and_colreduce():
     """Batched speaker-conditioning linears (fwd, dW, dbias, dc) and the
     weight-norm backward's column-reduce entries."""
@@ -494,6 +538,29 @@ def test_conv_tall_tap_reuse_matches_tap_reuse_and_fp64(mode, n_utt, T, cin, cou
     if mode == "dgrad":  # per-128-frame column sums of the stored bf16 output
         cs = outs[-1][1].double().cpu().view(N // 128, 128, k_out).sum(1)
         assert relerr(outs[-1][2], cs) < 5e-3  # fp32 sums of the values before their bf16 rounding
+
+
+@pytest.mark.parametrize("k,T,r_dim,c_dim,splits", [(3, 256, 512, 1024, 8), (1, 256, 640, 512, 25), (3, 96, 128, 80, 3),
+                                                     (5, 128, 256, 512, 4)])
+def test_wgrad_bf16_slabs_match_fp32_slabs(k, T, r_dim, c_dim, splits):
+    """bf16 split-K slabs (vqx_wgrad_args.slab_dtype, the bf16 step's default):
+    each split's fp32 partial rounded once to bf16.  Their fp32 sum stays
+    within 2e-3 of the fp32 slabs' sum on the tap-reuse, 1x1, generic
+    (T % 64 != 0) and 5-tap paths, and the bf16 slab bytes are exactly the
+    fp32 partials rounded to nearest-even."""
+    ops = _ops()
+    torch.manual_seed(13)
+    N = 4 * T
+    p = torch.randn(N, r_dim, device=DEV).to(torch.bfloat16)
+    q = torch.randn(N, c_dim, device=DEV).to(torch.bfloat16)
+    kw = dict(T=T, r_dim=r_dim, c_dim=c_dim, ntaps=k, pad=(k - 1) // 2, splits=splits)
+    s32 = torch.full((splits, r_dim, k * c_dim), float("nan"), device=DEV)
+    s16 = torch.full((splits, r_dim, k * c_dim), float("nan"), device=DEV, dtype=torch.bfloat16)
+    ops.conv_wgrad(p, q, s32, **kw)
+    ops.conv_wgrad(p, q, s16, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(s16, s32.to(torch.bfloat16))
+    assert relerr(s16.float().sum(0), s32.sum(0)) < 2e-3
 
 
 @pytest.mark.parametrize("sign", [1, -1])

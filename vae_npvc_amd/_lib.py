@@ -15,7 +15,7 @@ from pathlib import Path
 import torch  # noqa: F401  (loads the HIP runtime first; see module docstring)
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libvqx.so"
-ABI_VERSION = 117  # include/vqx.h VQX_ABI_VERSION
+ABI_VERSION = 118  # include/vqx.h VQX_ABI_VERSION
 
 VQX_F32, VQX_BF16 = 0, 1
 PRO_NONE, PRO_LRELU, PRO_RELU, PRO_SCALE_RELU = 0, 1, 2, 3
@@ -49,6 +49,7 @@ class WgradArgs(ctypes.Structure):
         ("r_dim", c_int32), ("c_dim", c_int32), ("ntaps", c_int32), ("pad", c_int32),
         ("shift_sign", c_int32), ("ldp", c_int32), ("ldq", c_int32), ("dtype", c_int32),
         ("q_prologue", c_int32), ("splits", c_int32), ("pro_scale", c_float), ("dil", c_int32),
+        ("slab_dtype", c_int32),
     ]
 
 
@@ -57,6 +58,7 @@ class WNLayer(ctypes.Structure):
         ("v", c_void_p), ("g", c_void_p), ("w_packed", c_void_p), ("norm", c_void_p), ("dv", c_void_p),
         ("dg", c_void_p), ("slabs", c_void_p), ("kind", c_int32), ("cout", c_int32), ("cin", c_int32),
         ("k", c_int32), ("splits", c_int32), ("dtype", c_int32), ("stride", c_int32), ("pad", c_int32),
+        ("slab_dtype", c_int32),
     ]
 
 

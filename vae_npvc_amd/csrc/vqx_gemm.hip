@@ -189,6 +189,7 @@ extern "C" int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream) {
   if (a->splits < 1) { set_error("vqx_conv1d_wgrad: splits < 1"); return -1; }
   if (!aligned16(a->p) || !aligned16(a->q) || !a->slabs || !aligned16(a->slabs)) { set_error("vqx_conv1d_wgrad: bad pointers"); return -1; }
   if (a->shift_sign != 1 && a->shift_sign != -1) { set_error("vqx_conv1d_wgrad: shift_sign must be +-1"); return -1; }
+  if (a->slab_dtype != VQX_F32 && !(a->slab_dtype == VQX_BF16 && a->dtype == VQX_BF16)) { set_error("vqx_conv1d_wgrad: slab_dtype %d (bf16 slabs need bf16 operands)", a->slab_dtype); return -1; }
   GemmParams P = {};
   P.a = a->p; P.b = a->q; P.n_rows = a->n_rows; P.T = a->T; P.lda = a->ldp; P.ldb = a->ldq;
   P.a_bytes = ((a->n_rows - 1) * (int64_t)a->ldp + a->r_dim) * es;
@@ -202,6 +203,7 @@ extern "C" int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream) {
   kps = (kps + kround - 1) / kround * kround;
   P.k_per_split = kps;
   P.y = a->slabs;
+  P.slab_bf16 = a->slab_dtype == VQX_BF16;
   const int bkv = a->dtype == VQX_BF16 ? 64 : 32;
   const bool gen = (a->T % bkv) != 0 || (a->n_rows % bkv) != 0;
   if (!gen && wgrad_tr_ok(a->n_rows, a->T, a->c_dim, a->ntaps, a->pad, dil, a->dtype == VQX_BF16, a->q_prologue)) {

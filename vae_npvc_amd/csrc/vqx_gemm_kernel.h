@@ -103,6 +103,7 @@ struct GemmParams {
   float* stat_part;  // GNSTATS / GNBWD per-(128-row group, column tile) partials
   int gn_groups, gn_glu;
   int tap_reuse;   // WGRAD: 1 = wgrad_tr_kernel tiling (tiles_n counts 64-channel blocks of c)
+  int slab_bf16;   // WGRAD: slabs stored as bf16 (bf16 operands only)
   const float* gn_tiles;  // GNADD: merge mean/rstd from these GNSTATS tiles (G = 1) and write gn_mr
   float gn_eps;
 };
@@ -596,8 +597,9 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
       const int col = n0 + ec;
       if constexpr (MODE == MODE_WGRAD) {
         if (row < P.Mc && col < P.Nc) {  // Nc % 8 == 0
-          float* out = (float*)P.y + (int64_t)split * P.Mc * P.Nc + row * P.Nc + col;
-          st8_nt<float, VQX_NT_SLAB>(out, 0, v);
+          const int64_t at = (int64_t)split * P.Mc * P.Nc + row * P.Nc + col;
+          if (sizeof(T) == 2 && P.slab_bf16) st8<bf16_t>(P.y, at, v);
+          else st8_nt<float, VQX_NT_SLAB>((float*)P.y + at, 0, v);
         }
       } else {
         if (row < P.n_rows && col < P.Nc) {
@@ -1654,7 +1656,7 @@ __global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void wgrad_tr_kernel(Gem
 
   // slab store, one tap at a time through LDS: rows of 64 channels, 8 lanes x 8 floats each
   float* ep = (float*)smem;
-  float* slab = (float*)P.y + (int64_t)split * P.Mc * P.Nc;
+  const int64_t slab0 = (int64_t)split * P.Mc * P.Nc;
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     __syncthreads();
@@ -1675,9 +1677,15 @@ __global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void wgrad_tr_kernel(Gem
       if (r < P.Mc && cc < P.cdim) {
         const f32x4_t lo = *(const f32x4_t*)(ep + lr * EP_LD + lc);
         const f32x4_t hi = *(const f32x4_t*)(ep + lr * EP_LD + lc + 4);
-        float* o = slab + (int64_t)r * P.Nc + j * P.cdim + cc;
-        *(f32x4_t*)o = lo;
-        *(f32x4_t*)(o + 4) = hi;
+        const int64_t at = slab0 + (int64_t)r * P.Nc + j * P.cdim + cc;
+        if (P.slab_bf16) {
+          const float v8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          st8<bf16_t>(P.y, at, v8);
+        } else {
+          float* o = (float*)P.y + at;
+          *(f32x4_t*)o = lo;
+          *(f32x4_t*)(o + 4) = hi;
+        }
       }
     }
   }

@@ -132,12 +132,56 @@ __global__ __launch_bounds__(256) void wn_pack_kernel(const vqx_wn_layer* __rest
   }
 }
 
+// a[0..NF-1] = partial sums over splits sp0, sp0+step, ... < splits of the 4
+// slab values at element offset p (slab stride `ss`), NF loads in flight
+#ifndef VQX_WN_NF  // 4 measured best: 8 -> 22.0, 16 -> 59 us per launch (registers, occupancy)
+#define VQX_WN_NF 4
+#endif
+#ifndef VQX_WN_VPRE  // 1: the row of v is loaded into registers before the slabs
+#define VQX_WN_VPRE 1
+#endif
+#ifndef VQX_WN_OCC  // minimum workgroups per CU requested from the register allocator (0 = none)
+#define VQX_WN_OCC 0
+#endif
+constexpr int kWnNF = VQX_WN_NF;
+template <bool BF>
+__device__ __forceinline__ void slab_sum8(const void* slabs, int64_t p, int64_t ss, int sp0, int step, int splits,
+                                          f32x4_t (&a)[kWnNF]) {
+  auto ld4 = [&](int64_t i) -> f32x4_t {
+    if constexpr (BF) {
+      const uint2 u = *(const uint2*)((const unsigned short*)slabs + i);
+      return {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+              __uint_as_float(u.y & 0xffff0000u)};
+    } else {
+      return *(const f32x4_t*)((const float*)slabs + i);
+    }
+  };
+#pragma unroll
+  for (int u = 0; u < kWnNF; ++u) a[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  int sp = sp0;
+  for (; sp + (kWnNF - 1) * step < splits; sp += kWnNF * step) {
+    f32x4_t t[kWnNF];
+#pragma unroll
+    for (int u = 0; u < kWnNF; ++u) t[u] = ld4(p + (int64_t)(sp + u * step) * ss);
+#pragma unroll
+    for (int u = 0; u < kWnNF; ++u) a[u] += t[u];
+  }
+  for (int u = 0; sp < splits; sp += step, ++u) a[u % kWnNF] += ld4(p + (int64_t)sp * ss);
+}
+
 // Backward per weight-norm row o.  slabs[s][o][x] with x = j*cin+ci (Conv1d,
 // row co) or x = j'*cout+co (ConvT, row ci); dW of the effective conv.
-// The split-K slabs are summed with 16-B loads (4 splits in flight per
-// thread), scattered into the row's (c, j) order in LDS, then the norm
-// gradient is formed from LDS with coalesced reads of v.
-__global__ __launch_bounds__(256) void wn_bwd_kernel(const vqx_wn_layer* __restrict__ L, int n_layers) {
+// The split-K slabs (fp32, or bf16 in bf16 runs) are summed in fp32 with
+// 16-B (8-B) loads, several splits in flight per thread, scattered into the
+// row's (c, j) order in LDS, then the norm gradient is formed from LDS and the
+// row of v held in registers.
+constexpr int kWnVRegs = 16;  // v row values per thread (row length <= 4096, 256 threads)
+#if VQX_WN_OCC > 0
+#define VQX_WN_BOUNDS __launch_bounds__(256, VQX_WN_OCC)
+#else
+#define VQX_WN_BOUNDS __launch_bounds__(256)
+#endif
+__global__ VQX_WN_BOUNDS void wn_bwd_kernel(const vqx_wn_layer* __restrict__ L, int n_layers) {
   const vqx_wn_layer& l = L[blockIdx.y];
   if (l.kind == VQX_WN_COLREDUCE) {  // dv[c] = sum_r v[r][c]: bias / affine gradients from partials
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -168,19 +212,44 @@ __global__ __launch_bounds__(256) void wn_bwd_kernel(const vqx_wn_layer* __restr
   __shared__ __attribute__((aligned(16))) float dw[4096];
   __shared__ float red[16];
   const int64_t slab_stride = (int64_t)rows * scols;
-  const float* srow = l.slabs + (int64_t)o * scols;
+  const int64_t srow = (int64_t)o * scols;  // element offset of this row in split 0
   const int splits = l.splits;
-  for (int x4 = threadIdx.x; x4 < scols / 4; x4 += blockDim.x) {
-    const float* p = srow + 4 * x4;
-    f32x4_t s0 = *(const f32x4_t*)p, s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1, s3 = s1;
-    int sp = 1;
-    for (; sp + 3 <= splits; sp += 3) {
-      s1 += *(const f32x4_t*)(p + (int64_t)sp * slab_stride);
-      s2 += *(const f32x4_t*)(p + (int64_t)(sp + 1) * slab_stride);
-      s3 += *(const f32x4_t*)(p + (int64_t)(sp + 2) * slab_stride);
+  const bool sbf = l.slab_dtype == VQX_BF16;
+  // the row of v, loaded before the slabs so both latencies overlap (cols <= 4096, 256 threads)
+  float vr[kWnVRegs];
+  const float* vrow = l.v + (int64_t)o * cols;
+  if (VQX_WN_VPRE) {
+#pragma unroll
+    for (int u = 0; u < kWnVRegs; ++u) {
+      const int i = threadIdx.x + u * 256;
+      vr[u] = (l.g && i < cols) ? vrow[i] : 0.f;
     }
-    for (; sp < splits; ++sp) s1 += *(const f32x4_t*)(p + (int64_t)sp * slab_stride);
-    const f32x4_t sum = (s0 + s1) + (s2 + s3);
+  }
+  // Thread t sums the splits g, g+G, ... of column group x4 = t % nx4 (G = the
+  // threads per group when a row has fewer than 256 groups), eight loads in
+  // flight, then the G partial sums are added in g order through LDS: a fixed
+  // order, so the result is deterministic.  The slab dtype is a template
+  // argument of the summing loop (a dtype branch per load kept the loads from
+  // being issued together).
+  const int nx4 = scols / 4;
+  const int G = nx4 >= (int)blockDim.x ? 1 : min(splits, (int)blockDim.x / nx4);
+  const int gidx = threadIdx.x / nx4;  // split group (G == 1: every thread is group 0)
+  f32x4_t* part = (f32x4_t*)dw;        // [G][nx4] partials (G > 1 only: nx4 * G <= 256 -> 4 KiB)
+  // G == 1: x4 = t, t + 256, ...;  G > 1: the one group x4 = t % nx4 (threads with gidx >= G idle)
+  const int x4_0 = G == 1 ? (int)threadIdx.x : ((int)threadIdx.x % nx4 + (gidx < G ? 0 : nx4));
+  for (int x4 = x4_0; x4 < nx4; x4 += (G == 1 ? (int)blockDim.x : nx4)) {
+    const int64_t p = srow + 4 * x4;
+    const int sp0 = G > 1 ? gidx : 0, step = G > 1 ? G : 1;
+    f32x4_t a[kWnNF];
+    if (sbf) slab_sum8<true>(l.slabs, p, slab_stride, sp0, step, splits, a);
+    else slab_sum8<false>(l.slabs, p, slab_stride, sp0, step, splits, a);
+    f32x4_t sum = a[0];
+#pragma unroll
+    for (int u = 1; u < kWnNF; ++u) sum += a[u];
+    if (G > 1) {
+      part[gidx * nx4 + x4] = sum;
+      continue;
+    }
     const int x = 4 * x4;
     if (rsm) {  // slab col x = m*S*C + q*C + c -> v index c*K + S*(m-1) + q + pad (4 c's share m, q)
       const int m = x / SC, rem = x - m * SC, q = rem / other, c = rem - q * other;
@@ -197,22 +266,54 @@ __global__ __launch_bounds__(256) void wn_bwd_kernel(const vqx_wn_layer* __restr
 #pragma unroll
     for (int e = 0; e < 4; ++e) dw[(c + e) * K + jj] = sum[e];
   }
+  if (G > 1) {  // add the split groups' partials in group order, then scatter as above
+    __syncthreads();
+    f32x4_t sum = {0.f, 0.f, 0.f, 0.f};
+    const int x4 = threadIdx.x;
+    if (x4 < nx4)
+      for (int g = 0; g < G; ++g) sum += part[g * nx4 + x4];
+    __syncthreads();  // dw doubles as the partial buffer
+    if (x4 < nx4) {
+      const int x = 4 * x4;
+      if (rsm) {
+        const int m = x / SC, rem = x - m * SC, q = rem / other, c = rem - q * other;
+        const int j = S * (m - 1) + q + l.pad;
+        if (j >= 0 && j < K) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dw[(c + e) * K + j] = sum[e];
+        }
+      } else {
+        const int j = x / other, c = x - j * other;
+        const int jj = l.kind == 0 ? j : K - 1 - j;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dw[(c + e) * K + jj] = sum[e];
+      }
+    }
+  }
   __syncthreads();
-  const float* v = l.v + (int64_t)o * cols;
   float* dv = l.dv + (int64_t)o * cols;
   if (!l.g) {  // plain weight (weight norm removed): dv is the weight gradient itself
     for (int i = threadIdx.x; i < cols; i += blockDim.x) dv[i] = dw[i];
     return;
   }
   float dot = 0.f;
-  for (int i = threadIdx.x; i < cols; i += blockDim.x) dot = fmaf(dw[i], v[i], dot);
+#pragma unroll
+  for (int u = 0; u < kWnVRegs; ++u) {
+    const int i = threadIdx.x + u * 256;
+    if (!VQX_WN_VPRE && i < cols) vr[u] = vrow[i];
+    if (i < cols) dot = fmaf(dw[i], vr[u], dot);
+  }
   dot = block_sum(dot, red);
   const float nrm = l.norm[o];
   const float gg = l.g[o];
   const float dg = dot / nrm;
   if (threadIdx.x == 0) l.dg[o] = dg;
   const float sc = gg / nrm, t = dg / nrm;
-  for (int i = threadIdx.x; i < cols; i += blockDim.x) dv[i] = sc * (dw[i] - v[i] * t);
+#pragma unroll
+  for (int u = 0; u < kWnVRegs; ++u) {
+    const int i = threadIdx.x + u * 256;
+    if (i < cols) dv[i] = sc * (dw[i] - vr[u] * t);
+  }
 }
 
 // --------------------------------------------------------------- groupnorm
@@ -1212,6 +1313,7 @@ extern "C" int vqx_weight_norm_bwd(const vqx_wn_layer* lh, const vqx_wn_layer* l
     if (cols > 4096) { set_error("vqx_weight_norm_bwd: row length %d > 4096", cols); return -1; }
     if (!l.slabs || !l.dv || (l.g && !l.dg) || l.splits < 1) { set_error("vqx_weight_norm_bwd: layer %d missing buffers", i); return -1; }
     if ((row_is_cout ? l.cin : l.cout) % 4 || ((uintptr_t)l.slabs & 15)) { set_error("vqx_weight_norm_bwd: layer %d: slab rows must be 16-B vectors", i); return -1; }
+    if (l.slab_dtype != VQX_F32 && l.slab_dtype != VQX_BF16) { set_error("vqx_weight_norm_bwd: layer %d: slab_dtype %d", i, l.slab_dtype); return -1; }
     max_rows = rows > max_rows ? rows : max_rows;
   }
   hipLaunchKernelGGL(wn_bwd_kernel, dim3(max_rows, n_layers), dim3(256), 0, (hipStream_t)stream, ld, n_layers);

@@ -491,16 +491,27 @@ class VQVAEEngine:
                 n, T_, k, pad, dil = B_ref * To, To, Lr.k, Lr.pad, Lr.dil
             tiles = ops.wgrad_tiles(n, T_, r, c, k, pad, self.dt, dil=dil)
             Lr.splits = max(1, min((wg_1x1 if Lr.k == 1 else wg_target) // tiles, n // 256))
-        # slab arena: one backward group's slabs at a time (kept L2/MALL-resident)
+        # slab arena: one backward group's slabs at a time (kept L2/MALL-resident).
+        # bf16 runs keep the conv slabs in bf16 (each split's fp32 partial rounded
+        # once, summed in fp32 by the weight-norm backward): half the bytes of the
+        # split-K round trip.  The conditioning linears write dW directly (fp32).
         groups = self._bwd_groups()
-        arena = max(sum(Lr.splits * Lr.rows * Lr.cols for Lr in grp) for grp in groups)
-        self.arena = torch.empty(arena, device=self.device, dtype=F32)
+        bf_slabs = self.dt == L.VQX_BF16 and os.environ.get("VQX_SLAB_F32") != "1"  # env: fp32 slabs (A/B)
+        sdt = {id(Lr): (torch.bfloat16 if bf_slabs and Lr not in self.dec_cond else F32)
+               for grp in groups for Lr in grp}
+
+        def nbytes(Lr):
+            n = Lr.splits * Lr.rows * Lr.cols * (4 if sdt[id(Lr)] == F32 else 2)
+            return (n + 255) // 256 * 256
+
+        arena = max(sum(nbytes(Lr) for Lr in grp) for grp in groups)
+        self.arena = torch.empty(arena, device=self.device, dtype=torch.uint8)
         for grp in groups:
             off = 0
             for Lr in grp:
-                n = Lr.splits * Lr.rows * Lr.cols
-                Lr.slab = self.arena[off:off + n].view(Lr.splits, Lr.rows, Lr.cols)
-                off += n
+                n = Lr.splits * Lr.rows * Lr.cols * (4 if sdt[id(Lr)] == F32 else 2)
+                Lr.slab = self.arena[off:off + n].view(sdt[id(Lr)]).view(Lr.splits, Lr.rows, Lr.cols)
+                off += nbytes(Lr)
         self.wn_fwd_table = ops.wn_table([self._wn_entry(Lr, bwd=False) for Lr in self.convs])
         self.groups = groups
 

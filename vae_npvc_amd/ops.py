@@ -177,13 +177,15 @@ def conv_dgrad(dy, w, dx, **kw):
 
 def conv_wgrad(p, q, slabs, *, T, r_dim, c_dim, ntaps, pad, shift_sign=1, q_prologue=L.PRO_NONE, pro_scale=1.0,
                splits=1, dil=1):
-    """slabs[s, r, j*c_dim + c] = sum_{n in split s} p[n, r] * pro(q[n + sign*(j*dil-pad), c])."""
+    """slabs[s, r, j*c_dim + c] = sum_{n in split s} p[n, r] * pro(q[n + sign*(j*dil-pad), c]);
+    slabs fp32, or bf16 for bf16 operands (each split's partial rounded once)."""
     _check_cuda(p, q, slabs)
     a = L.WgradArgs()
     a.p, a.q, a.slabs = ptr(p), ptr(q), ptr(slabs)
     a.n_rows, a.T, a.r_dim, a.c_dim, a.ntaps, a.pad, a.shift_sign = p.shape[0], T, r_dim, c_dim, ntaps, pad, shift_sign
     a.ldp, a.ldq = p.stride(0), q.stride(0)
     a.dtype, a.q_prologue, a.splits, a.pro_scale, a.dil = dt_code(p.dtype), q_prologue, splits, pro_scale, dil
+    a.slab_dtype = dt_code(slabs.dtype)
     if _probe is not None:
         _probe.shapes.append(f"{r_dim}x{ntaps}x{c_dim} s{splits}")
     call("vqx_conv1d_wgrad", ctypes.byref(a), stream_ptr())
@@ -207,6 +209,8 @@ def wn_table(layers):
         e.kind, e.cout, e.cin, e.k = d["kind"], d["cout"], d["cin"], d["k"]
         e.splits, e.dtype = d.get("splits", 1), d["dtype"]
         e.stride, e.pad = d.get("stride", 0), d.get("pad", 0)
+        sl = d.get("slabs")
+        e.slab_dtype = dt_code(sl.dtype) if sl is not None else L.VQX_F32
     raw = bytes(arr)
     dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to("cuda")
     return arr, dev
