@@ -17,7 +17,11 @@ def test_fp32_train_steps_match_reference_golden(prefix):
     Adam's m/sqrt(v) update turns ulp-level gradient differences on near-zero
     gradients into ~lr-sized parameter differences.  Codebook indices equal
     except where the reference's own top-2 distance gap is a near-tie (< 1e-4
-    relative); gradient norms within 2e-3; EMA buffers within 1e-4."""
+    relative); gradient norms within 1e-5 for the decoder and the speaker
+    embedding (no argmin or commitment dependence; measured <= 2.3e-7,
+    tools/grad_err_probe.py) and 1e-3 for the encoder, whose only gradient is
+    the commitment term (zq - z) (measured <= 2.1e-4 on aishell3 with
+    jitter); EMA buffers within 1e-4."""
     from oracle.vqvae_cpu import seeded_batch
     meta, arr = load_fixture(prefix)
     cfg = cfg_of(meta["config"], compute_dtype="fp32")
@@ -43,7 +47,8 @@ def test_fp32_train_steps_match_reference_golden(prefix):
             g = {n: eng.g(p) for n, p in tr.model.named_parameters()}
             for n, ref in meta["grads"].items():
                 gn = float(g[n].double().norm())
-                assert relclose(gn, ref["norm"], 2e-3, 1e-9), (n, gn, ref["norm"])
+                tol = 1e-3 if n.startswith("encoder.") else 1e-5
+                assert relclose(gn, ref["norm"], tol, 1e-9), (n, gn, ref["norm"])
     for n, p in tr.model.named_parameters():  # after 3 Adam steps (see docstring): 1e-3
         assert relclose(float(p.detach().double().norm()), meta["params_after"][n]["norm"], 1e-3), n
 
@@ -91,7 +96,9 @@ def test_fp32_plain_vq_steps_match_reference_golden(name):
     """Straight-through VectorQuantizer (use_ema: false):
     the HIP step against the reference's 3 steps -- loss dict (1e-4 at step 1,
     1e-3 later, see test_fp32_train_steps_match_reference_golden), step-1
-    gradient norms incl. the codebook parameter (2e-3), parameters after 3 Adam
+    gradient norms: 1e-5 for the decoder, embedding and codebook parameter,
+    5e-4 for the encoder (straight-through + commitment through z/||z||;
+    measured <= 6.2e-5, tools/grad_err_probe.py), parameters after 3 Adam
     steps (1e-3).  aishell3_plain exercises the Jitter backward (replaced
     frames pass no gradient)."""
     from oracle.vqvae_cpu import seeded_batch
@@ -118,7 +125,8 @@ def test_fp32_plain_vq_steps_match_reference_golden(name):
             g = {n: eng.g(p) for n, p in tr.model.named_parameters()}
             for n, ref in meta["grads"].items():
                 gn = float(g[n].double().norm())
-                assert relclose(gn, ref["norm"], 2e-3, 1e-9), (n, gn, ref["norm"])
+                tol = 5e-4 if n.startswith("encoder.") else 1e-5
+                assert relclose(gn, ref["norm"], tol, 1e-9), (n, gn, ref["norm"])
     for n, p in tr.model.named_parameters():
         assert relclose(float(p.detach().double().norm()), meta["params_after"][n]["norm"], 1e-3), n
 
@@ -163,7 +171,9 @@ def test_vq_full_size_matches_reference_golden(K):
 
 
 def test_fp32_step_matches_oracle_xhat_and_grads():
-    """Element-wise check of xhat and every gradient against the CPU oracle."""
+    """Element-wise check of xhat and every gradient against the CPU oracle:
+    decoder and embedding gradients within 2e-5 (fp32 summation order only;
+    measured <= 2.2e-6), the encoder's commitment-driven gradients 2e-3."""
     from oracle.vqvae_cpu import OracleTrainer, seeded_batch, seeded_state_dict
     cfg = cfg_of("vcc20", compute_dtype="fp32")
     B, T = 2, 256
@@ -186,7 +196,7 @@ def test_fp32_step_matches_oracle_xhat_and_grads():
         g = tr.engine.g(p).cpu()
         r = orc.grads[n]
         rel = (g - r).norm() / r.norm().clamp_min(1e-20)
-        assert rel < 2e-3, (n, float(rel))
+        assert rel < (2e-3 if n.startswith("encoder.") else 2e-5), (n, float(rel))
 
 
 def test_bf16_step_tracks_oracle():
