@@ -2,12 +2,14 @@
 over RCCL (backend "nccl" on ROCm) across the node's xGMI links.
 
 Per step:
-  * gradients — the flat fp32 gradient buffer is all-reduced (mean) in
-    buckets as soon as a region is final: the encoder's region right after the
-    encoder backward (the encoder depends only on the commitment loss, so it
-    runs first), overlapping the decoder backward; the decoder/embedding region
-    at the end.  Mean over ranks of per-rank frame_mean losses equals the
-    global-batch loss, so clipping after the reduce is identical on all ranks.
+  * gradients — the flat fp32 gradient buffer is laid out in backward order
+    and all-reduced (mean) run by run as soon as a run is final: the engine
+    tracks which parameters each backward layer group's weight-norm backward
+    finalises and launches the contiguous ready runs (>= 64 K floats, split
+    into buckets of BUCKET_BYTES) asynchronously, so the reduction overlaps
+    the rest of the backward (engine/step.py `_grads_final`).  Mean over ranks
+    of per-rank frame_mean losses equals the global-batch loss, so clipping
+    after the reduce is identical on all ranks.
   * EMA statistics — bsum [K, D], bcnt [K] and the dead-code rows are summed
     in ONE all-reduce right after the VQ kernel; it overlaps the decoder and
     the backward (the codebook update runs at the end of the step).  Every
