@@ -1,5 +1,5 @@
 // Stand-alone timing lab for the tap-reuse conv kernels (conv_tr_kernel,
-// conv_tr8_kernel) at the config-2 3-tap shapes.  Built per variant with
+// conv_tr8_kernel, wgrad_tr_kernel) at the config-2 3-tap shapes.  Built per variant with
 // -DVQX_GEMM_LAB=0..3 (full / no operand DMA / no MFMA / no epilogue) by
 // tools/lab/tr_lab.sh; prints the mean launch time over 20 launches.
 #include <hip/hip_runtime.h>
@@ -86,6 +86,38 @@ static void run(const Shape& s, void* x, void* w, void* y, float* part) {
   }
 }
 
+// wgrad_tr_kernel: S[r][j*c + cc] over split-K slabs (bf16 slabs, as the bf16 step)
+static void run_wgrad(const char* name, int64_t N, int T, int r_dim, int c_dim, int splits, int sign, void* p, void* q,
+                      void* slabs) {
+  GemmParams P = {};
+  P.a = p;
+  P.b = q;
+  P.n_rows = N;
+  P.T = T;
+  P.lda = r_dim;
+  P.ldb = c_dim;
+  P.a_bytes = N * r_dim * 2;
+  P.b_bytes = N * c_dim * 2;
+  P.Mc = r_dim;
+  P.Nc = 3 * c_dim;
+  P.ntaps = 3;
+  P.pad = 1;
+  P.sign = sign;
+  P.dil = 1;
+  P.cdim = c_dim;
+  P.splits = splits;
+  P.k_per_split = (N + splits - 1) / splits;
+  P.k_per_split = (P.k_per_split + 63) / 64 * 64;
+  P.y = slabs;
+  P.slab_bf16 = 1;
+  P.tap_reuse = 1;
+  P.tiles_m = (r_dim + 127) / 128;
+  P.tiles_n = c_dim / 64;
+  const double fl = 2.0 * N * r_dim * 3.0 * c_dim;
+  const float us = time_us((const void*)wgrad_tr_kernel<EK_NONE, 1>, P.tiles_m * P.tiles_n * splits, 256, P, 20);
+  printf("lab%d %-13s wgrad_tr s%-2d      %7.1f us %7.1f TF\n", VQX_GEMM_LAB, name, splits, us, fl / us * 1e-6);
+}
+
 int main() {
   const Shape shapes[] = {{"dec_in_fwd", MODE_FWD, 16384, 256, 512, 1024},
                           {"enc_k3_fwd", MODE_FWD, 16384, 256, 512, 512},
@@ -106,6 +138,17 @@ int main() {
   CK(hipMalloc(&part, (size_t)128 * 8 * 4 * 4));
   CK(hipMemcpy(x, h.data(), xb, hipMemcpyHostToDevice));
   CK(hipMemcpy(w, h.data(), wb, hipMemcpyHostToDevice));
+  CK(hipMemcpy(y, h.data(), xb, hipMemcpyHostToDevice));  // wgrad's q operand
+  {
+    void* sl;
+    CK(hipMalloc(&sl, (size_t)32 * 1024 * 3 * 1024 * 2));
+    run_wgrad("dec_in_wgrad", 16384, 256, 512, 1024, 8, -1, x, y, sl);
+    run_wgrad("enc_k3_wgrad", 16384, 256, 512, 512, 16, 1, x, y, sl);
+    run_wgrad("dec_in_wgrad", 16384, 256, 512, 1024, 4, -1, x, y, sl);
+    run_wgrad("dec_in_wgrad", 16384, 256, 512, 1024, 16, -1, x, y, sl);
+    CK(hipFree(sl));
+  }
+  if (getenv("TR_LAB_WGRAD_ONLY")) return 0;
   for (const Shape& s : shapes) {
     if (s.mode == MODE_FWD) {
       run<MODE_FWD, EK_NONE>(s, x, w, y, part);

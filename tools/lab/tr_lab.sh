@@ -12,5 +12,5 @@ if [ "$1" = build ]; then
 fi
 mkdir -p ../../gpurun_out
 for v in 0 1 2 3; do
-  timeout -k 10 60 ./tr_lab$v.bin || exit $?
+  TR_LAB_WGRAD_ONLY=$WGRAD_ONLY timeout -k 10 60 ./tr_lab$v.bin || exit $?
 done | tee ../../gpurun_out/tr_lab.txt

@@ -1616,8 +1616,8 @@ __global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void wgrad_tr_kernel(Gem
     int buf = 0;
     for (int it = 0; it < nit; ++it) {
       const int kt = it * KG + grp;
-      if (it + 1 < nit && kt + KG < nk) dma_stage(buf ^ 1, kt + KG);
-      if (kt < nk) compute_stage(buf);
+      if (VQX_GEMM_LAB != 1 && it + 1 < nit && kt + KG < nk) dma_stage(buf ^ 1, kt + KG);
+      if (VQX_GEMM_LAB != 2 && kt < nk) compute_stage(buf);
       wait_vm(0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -1654,6 +1654,13 @@ __global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void wgrad_tr_kernel(Gem
     }
   }
 
+  if (VQX_GEMM_LAB == 3) {  // keep the accumulators live
+    float t = 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) t += acc[0][0][e] + acc[0][1][e] + acc[0][2][e] + acc[1][0][e] + acc[1][1][e] + acc[1][2][e];
+    if (t == 12345.f) ((float*)P.y)[tid] = t;
+    return;
+  }
   // slab store, one tap at a time through LDS: rows of 64 channels, 8 lanes x 8 floats each
   float* ep = (float*)smem;
   const int64_t slab0 = (int64_t)split * P.Mc * P.Nc;
