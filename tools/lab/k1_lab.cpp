@@ -145,7 +145,10 @@ int main() {
 #ifndef VQX_EPI_PREFETCH
 #define VQX_EPI_PREFETCH 1
 #endif
-    printf("prefetch%d stagger%d mode%d %-20s %7.1f us %7.1f TF\n", VQX_EPI_PREFETCH, VQX_GEMM_STAGGER, VQX_LAB_MODE, c.name, us, fl / us * 1e-6);
+#ifndef VQX_EPI_PREVEC_DGRAD
+#define VQX_EPI_PREVEC_DGRAD 0
+#endif
+    printf("prevec_dgrad%d prefetch%d stagger%d mode%d %-20s %7.1f us %7.1f TF\n", VQX_EPI_PREVEC_DGRAD, VQX_EPI_PREFETCH, VQX_GEMM_STAGGER, VQX_LAB_MODE, c.name, us, fl / us * 1e-6);
   }
   CK(hipDeviceSynchronize());
   return 0;

@@ -50,6 +50,9 @@ constexpr int kBN = 128;  // tile width (and height)
 #ifndef VQX_EPI_PREFETCH  // 0: the 1x1 epilogues load their row operands pass by pass (A/B)
 #define VQX_EPI_PREFETCH 1
 #endif
+#ifndef VQX_EPI_PREVEC_DGRAD  // 1: DGRAD epilogues hoist the per-channel vectors too (A/B)
+#define VQX_EPI_PREVEC_DGRAD 0
+#endif
 constexpr unsigned kOOB = 0x80000000u;  // buffer offset that is always out of range -> loads 0
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 
@@ -549,7 +552,7 @@ __device__ __forceinline__ void wait_vm(int n) {
 // 44 KiB of `smem`; the caller's staging buffers must be free.  `tid` is the
 // thread's index in the 4-wave group that owns the tile (conv_tr8_kernel runs
 // two such groups side by side; every group passes the same barriers).
-template <typename T, int MODE, int EK, bool PRE = false>
+template <typename T, int MODE, int EK, bool PRE = false, bool PREVEC = PRE>
 __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&acc)[2][2], char* smem, int m0, int n0,
                                               int tn, int split, const float* gmr, int tid,
                                               const EpiRows* R = nullptr) {
@@ -568,7 +571,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
   float mn = 0.f, mm = 0.f, mq = 0.f;                       // GNSTATS running (count, mean, M2)
   float gs[4] = {0.f, 0.f, 0.f, 0.f};                       // GNBWD sums
   EpiVec V;
-  if constexpr (PRE && MODE != MODE_WGRAD) epi_vec_load<EMASK>(P, n0 + ec, V);
+  if constexpr (PREVEC && MODE != MODE_WGRAD) epi_vec_load<EMASK>(P, n0 + ec, V);
   __syncthreads();  // staging buffers are free
   // slab and pass are compile-time constants (static_for), so the prefetched
   // row operands R->r*[slab*4 + pass] are register-resident
@@ -604,7 +607,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
       } else {
         if (row < P.n_rows && col < P.Nc) {
           const EpiOps o = epi_ops<slab * 4 + pass, PRE>(R);
-          epilogue8<T, EMASK, PRE>(P, row, col, v, gmr, o, V);
+          epilogue8<T, EMASK, PREVEC>(P, row, col, v, gmr, o, V);
 #pragma unroll
           for (int e = 0; e < 8; ++e) cs[e] += v[e];
           if (P.epi & EMASK & VQX_EPI_GNSTATS) {  // two-pass moments of the 8 values, merged
@@ -617,7 +620,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
             for (int e = 0; e < 8; ++e) q8 = fmaf(v[e] - m8, v[e] - m8, q8);
             moments_merge(mn, mm, mq, 8.f, m8, q8);
           }
-          if (P.epi & EMASK & VQX_EPI_GNBWD) gnbwd8<T, PRE>(P, row, col, v, gs, o, V);
+          if (P.epi & EMASK & VQX_EPI_GNBWD) gnbwd8<T, PREVEC>(P, row, col, v, gs, o, V);
         }
       }
     });
@@ -1040,6 +1043,9 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
   // GNADD 26.9 -> 26.0 us; the DGRAD GNBWD epilogues, VALU-bound, ran 5-9% slower
   // with it and keep loading pass by pass)
   constexpr bool kPrefetch = sizeof(T) == 2 && MODE == MODE_FWD && EK != EK_NONE && EK != EK_ALL && VQX_EPI_PREFETCH;
+  // per-channel vectors (bias, GN affine) hoisted out of the row passes
+  constexpr bool kPreVec = kPrefetch || (sizeof(T) == 2 && MODE == MODE_DGRAD && EK != EK_NONE && EK != EK_ALL &&
+                                         VQX_EPI_PREVEC_DGRAD);
   EpiRows rows;
   if constexpr (kPrefetch) {
     if (nk <= 0) epi_prefetch<EK>(P, m0, n0, tid, rows);
@@ -1089,7 +1095,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
   }
   return;
 #endif
-  tile_epilogue<T, MODE, EK, kPrefetch>(P, acc, smem, m0, n0, tn, split, gmr, (int)threadIdx.x, &rows);
+  tile_epilogue<T, MODE, EK, kPrefetch, kPreVec>(P, acc, smem, m0, n0, tn, split, gmr, (int)threadIdx.x, &rows);
 }
 
 
