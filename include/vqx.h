@@ -305,6 +305,13 @@ int vqx_vq_forward(const float* z, int64_t n_rows, int32_t D, const float* E, in
 /* Workspace (floats) vqx_vq_forward needs for N frames and K codes, with or
  * without the EMA statistics. */
 int vqx_vq_workspace(int64_t n_rows, int32_t K, int32_t with_stats, int64_t* floats);
+/* The EMA statistics part of vqx_vq_forward on its own (bsum = one-hot^T z,
+ * bcnt = counts of idx; update_emb's onehot matmul, layers_vq.py:207-211),
+ * for callers that run it on another stream than the distance kernel.
+ * `partials` is the same workspace (with stats); it does not touch the
+ * commitment partials, so it may run beside vqx_vq_forward's sqerr sum. */
+int vqx_vq_stats(const float* z, int64_t n_rows, int32_t D, const int64_t* idx, int32_t K, float* partials,
+                 float* bsum, float* bcnt, vqx_stream_t stream);
 
 /*
  * EMA codebook update (update_emb, layers_vq.py:203-233; init_emb :192-201):
@@ -479,7 +486,7 @@ int vqx_probe_count(int64_t* n);
 int vqx_probe_read(int64_t i, int32_t* info5, double* flops, float* ms);
 
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
-#define VQX_ABI_VERSION 118
+#define VQX_ABI_VERSION 119
 int vqx_version(void);
 
 #ifdef __cplusplus

@@ -1,15 +1,12 @@
-# GPU tests, then bench A/B over an env setting: bash tools/gpu_ab_env.sh TAG "VAR=a" "VAR=b" ...
-TAG=$1; shift
-cd $GRAFT_REPO_ROOT
-export TMPDIR=/tmp
-O=gpurun_out/$TAG
-mkdir -p $O
-if [ -z "$NO_TESTS" ]; then timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1
-rc=$?; echo "pytest rc=$rc" >> $O/tests.log; tail -3 $O/tests.log
-if [ $rc -ne 0 ]; then exit $rc; fi; fi
-i=0
-for kv in "$@"; do
-  i=$((i+1))
-  env $kv timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_$i.log 2>&1 || exit $?
-  echo "$kv: $(grep '^{' $O/bench_$i.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')"
-done
+#!/bin/bash
+# Same-box A/B of one environment switch on the bf16 bench step:
+#   bash tools/gpu_ab_env.sh NAME VAR VALUE_A VALUE_B   (alternating A B A B, 20 steps each)
+set -o pipefail
+cd "$(dirname "$0")/.."
+NAME=$1; VAR=$2; A=$3; B=$4
+mkdir -p gpurun_out/ab_$NAME
+for v in $A $B $A $B; do
+  env $VAR=$v timeout -k 10 200 python -u bench.py --steps 30 --warmup 5 --no-cpu-baseline --fp32-steps 0 \
+    --vq-reps 0 --no-probe > gpurun_out/ab_$NAME/b_$v.json 2> gpurun_out/ab_$NAME/b_$v.err || exit $?
+  python3 -c "import json;d=json.load(open('gpurun_out/ab_$NAME/b_$v.json'));print('$VAR=$v', d['ms_per_step'], d['value'])"
+done | tee gpurun_out/ab_$NAME/summary.txt

@@ -580,6 +580,22 @@ extern "C" int vqx_vq_forward(const float* z, int64_t n_rows, int32_t D, const f
   return launch_status("vqx_vq_forward");
 }
 
+extern "C" int vqx_vq_stats(const float* z, int64_t n_rows, int32_t D, const int64_t* idx, int32_t K,
+                            float* partials, float* bsum, float* bcnt, vqx_stream_t stream) {
+  if (D != VQ_D) { set_error("vqx_vq_stats: only D=128 supported (got %d)", D); return -1; }
+  if (K <= 0 || K % 16 || K > 2048) { set_error("vqx_vq_stats: K=%d must be a multiple of 16 in [16, 2048]", K); return -1; }
+  if (n_rows <= 0 || !z || !idx || !partials || !bsum || !bcnt) { set_error("vqx_vq_stats: bad arguments"); return -1; }
+  if ((uintptr_t)z & 15) { set_error("vqx_vq_stats: z must be 16-byte aligned"); return -1; }
+  hipStream_t s = (hipStream_t)stream;
+  switch (vq_stats_dsl(K)) {
+    case 32: launch_vq_stats<32>(z, n_rows, idx, K, partials, bsum, bcnt, s); break;
+    case 16: launch_vq_stats<16>(z, n_rows, idx, K, partials, bsum, bcnt, s); break;
+    case 8: launch_vq_stats<8>(z, n_rows, idx, K, partials, bsum, bcnt, s); break;
+    default: launch_vq_stats<4>(z, n_rows, idx, K, partials, bsum, bcnt, s); break;
+  }
+  return launch_status("vqx_vq_stats");
+}
+
 extern "C" int vqx_vq_ema_update(float* emb_sum, float* emb_elem, float* E, const float* bsum, const float* bcnt,
                                  const float* rand_rows, int32_t K, int32_t D, float mu, float threshold, float* diag,
                                  float* partials, vqx_stream_t stream) {

@@ -279,6 +279,14 @@ class VQVAEEngine:
         self._ws = {}
         self.opt_ready = False
         self._enc_gn_separate = os.environ.get("VQX_ENC_GN_FINALIZE") == "1"
+        # optional side stream for the latency-bound work off the GEMM chain: the
+        # speaker conditioning linears (needed only by the decoder) and the EMA
+        # codebook statistics + update (needed only by the next step).  Measured
+        # 0.5-0.8% slower end to end (profiles/r02/side_stream_ab.txt: the small
+        # kernels squeeze into the GEMMs' single round of workgroups), so off by
+        # default; env VQX_SIDE_STREAM=1 turns it on
+        self._side_on = self.device.type == "cuda" and os.environ.get("VQX_SIDE_STREAM", "0") == "1"
+        self._side = None
 
     # ------------------------------------------------------------ parameters
     def _flatten(self):
@@ -701,6 +709,23 @@ class VQVAEEngine:
                 s = st.conv.scale
                 ops.convert_2d(st.conv.mod.bias.detach().view(1, -1).expand(s, -1), st.conv.btile.view(s, -1))
 
+    def _side_stream(self):
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        return self._side
+
+    def _join(self):
+        """Order the current stream after all side-stream work issued so far
+        (the previous step's codebook update, its loss diagnostics)."""
+        if self._side is not None:
+            torch.cuda.current_stream().wait_stream(self._side)
+
+    def _fork(self):
+        """The side stream, ordered after everything issued so far on the current stream."""
+        side = self._side_stream()
+        side.wait_stream(torch.cuda.current_stream())
+        return side
+
     def embed_and_cond(self, w, y):
         ops.embedding_fwd(self.m.embeds._embedding.weight, y.reshape(-1), w.yemb)
         tabs = getattr(w, "cond_tables", None)
@@ -1074,9 +1099,30 @@ class VQVAEEngine:
         q = self.m.quantizer
         K = self.dims["K"]
         self.vq_init_if_needed(w)
+        w.ev_ema = None
+        if self._side_on:
+            # distance/argmin/gather on the GEMM chain; the EMA statistics and the
+            # codebook update (update_emb, layers_vq.py:203-233) on the side stream:
+            # only the next step's distance kernel reads their results
+            ops.vq_forward(w.z, q.embeddings, w.idx, w.zq, w.zq_c, w.stats[1:2], w.vq_part, None, None)
+            side = self._fork()
+            with torch.cuda.stream(side):
+                ops.zero_(w.ema)
+                ops.vq_stats(w.z, w.idx, K, w.vq_part, w.bsum, w.bcnt)
+                self._ema_rows(w, K)
+                if self.world > 1:
+                    self.comm.all_reduce_sum(w.ema, async_op=True).wait()
+                self._ema_apply(w)
+            w.ev_ema = side.record_event()
+            return
         ops.zero_(w.ema)
         ops.vq_forward(w.z, q.embeddings, w.idx, w.zq, w.zq_c, w.stats[1:2], w.vq_part, w.bsum, w.bcnt)
-        # rows for dead-code replacement: z[randperm(N)[:K]] (update_emb, layers_vq.py:212-213)
+        self._ema_rows(w, K)
+        if self.world > 1:
+            self._ema_work = self.comm.all_reduce_sum(w.ema, async_op=True)
+
+    def _ema_rows(self, w, K):
+        """rand_rows for dead-code replacement: z[randperm(N)[:K]] (update_emb, layers_vq.py:212-213)."""
         if w.Nz * self.world < K:
             rows = self._tile_rows(w)
             if self.rank != 0:  # every rank holds the same rows; the EMA bundle is SUM-reduced
@@ -1085,18 +1131,25 @@ class VQVAEEngine:
         else:
             perm = self._perm_rows(w.Nz * self.world, K, self.rank * w.Nz, w.Nz if self.world > 1 else None)
             ops.gather_rows(w.z, perm, w.rand_rows)
-        if self.world > 1:
-            self._ema_work = self.comm.all_reduce_sum(w.ema, async_op=True)
+
+    def _ema_apply(self, w):
+        q = self.m.quantizer
+        ops.vq_ema_update(q.emb_sum, q.emb_elem, q.embeddings, w.bsum, w.bcnt, w.rand_rows, q.mu, q.threshold,
+                          w.stats[4:8], w.ema_part)
 
     def vq_ema_update(self, w):
+        """End of the step: apply the EMA update (or, when it ran on the side
+        stream, order the current stream after it)."""
         if self.plain:  # the straight-through codebook is a parameter updated by Adam
             return
-        q = self.m.quantizer
+        if getattr(w, "ev_ema", None) is not None:
+            torch.cuda.current_stream().wait_event(w.ev_ema)
+            w.ev_ema = None
+            return
         if getattr(self, "_ema_work", None) is not None:
             self._ema_work.wait()
             self._ema_work = None
-        ops.vq_ema_update(q.emb_sum, q.emb_elem, q.embeddings, w.bsum, w.bcnt, w.rand_rows, q.mu, q.threshold,
-                          w.stats[4:8], w.ema_part)
+        self._ema_apply(w)
 
     # ------------------------------------------------------------ full step
     world, rank, comm = 1, 0, None
@@ -1105,11 +1158,19 @@ class VQVAEEngine:
         """Training forward (saves every activation the backward needs).
         x (B, mel, T) f32 device, y (B, 1) int64 device."""
         B, _, T = x.shape
+        self._join()
         w = self.ws(B, T, train=True)
         w.y_dev = y.reshape(-1)
         w.x_nct = x
         self.pack_weights()
-        self.embed_and_cond(w, w.y_dev)
+        w.ev_cond = None
+        if self._side_on:  # the conditioning row biases are first read by the decoder
+            side = self._fork()
+            with torch.cuda.stream(side):
+                self.embed_and_cond(w, w.y_dev)
+            w.ev_cond = side.record_event()
+        else:
+            self.embed_and_cond(w, w.y_dev)
         self.encoder_fwd(w, x)
         self.vq_forward_train(w)
         w.zq_in = w.zq_c
@@ -1120,6 +1181,8 @@ class VQVAEEngine:
             ops.time_gather(w.zq_c, w.zq_j, B, w.Tz, w.src_t)
             w.zq_in = w.zq_j
             w.jittered = True
+        if w.ev_cond is not None:
+            torch.cuda.current_stream().wait_event(w.ev_cond)
         self.decoder_fwd(w, w.zq_in)
         ops.logloss_fwd_bwd(x, w.xhat, 1.0 / (B * T), w.dxhat, w.stats[0:1], w.loss_part)
         return w
@@ -1222,6 +1285,7 @@ class VQVAEEngine:
     def forward_eval(self, x, y):
         """model.eval() forward: no EMA init/update, no jitter (layers_vq.py:282,295,354)."""
         B, _, T = x.shape
+        self._join()
         w = self._eval_ws(B, T)
         w.y_dev = y.reshape(-1)
         self.pack_weights()
@@ -1241,6 +1305,7 @@ class VQVAEEngine:
     def encode(self, x):
         """Model.encode (vqvae.py:45-52): encoder + nearest-code index, (B, T_z) int64."""
         B, _, T = x.shape
+        self._join()
         w = self._eval_ws(B, T)
         self.pack_weights()
         self.encoder_fwd(w, x)
@@ -1256,6 +1321,7 @@ class VQVAEEngine:
         T = Tz
         for st in self.enc_stages:
             T *= st.scale
+        self._join()
         w = self._eval_ws(B, T)
         w.y_dev = y.reshape(-1)
         self.pack_weights()

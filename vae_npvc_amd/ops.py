@@ -341,6 +341,16 @@ def vq_forward(z, E, idx, zq, zq_c, sqerr, partials=None, bsum=None, bcnt=None):
          stream_ptr())
 
 
+def vq_stats(z, idx, K, partials, bsum, bcnt):
+    """EMA statistics alone (vqx_vq_stats): bsum [K, D] = sum of the frames per
+    code, bcnt [K] = counts; partials as vq_forward's workspace with stats."""
+    N, D = z.shape
+    need = vq_workspace(N, K, True)
+    if partials.numel() < need:
+        raise ValueError(f"vq_stats: workspace {partials.numel()} < {need} floats")
+    call("vqx_vq_stats", ptr(z), N, D, ptr(idx), K, ptr(partials), ptr(bsum), ptr(bcnt), stream_ptr())
+
+
 def vq_ema_update(emb_sum, emb_elem, E, bsum, bcnt, rand_rows, mu, threshold, diag, partials=None):
     """partials: workspace of ceil(K*D/1024) floats (allocated here if None)."""
     K, D = E.shape
