@@ -279,3 +279,28 @@ def test_autograd_path_matches_fused_trainer():
     for (n, p), (_, q) in zip(tr.model.named_parameters(), m.named_parameters()):
         d = (p.detach() - q.detach()).norm() / q.detach().norm().clamp_min(1e-20)
         assert d < 1e-5, (n, float(d))
+
+
+def test_side_stream_path_is_bit_identical():
+    """VQX_SIDE_STREAM=1 (conditioning linears and the EMA statistics +
+    codebook update on a second stream, vqx_vq_stats) computes exactly what
+    the single-stream path does: same kernels in the same order per buffer,
+    so the losses, the codebook and every weight after 3 steps are
+    bit-identical."""
+    from oracle.vqvae_cpu import seeded_batch
+    out = []
+    for side in (False, True):
+        cfg = cfg_of("aishell3", compute_dtype="bf16")
+        tr = make_trainer(cfg, 13)
+        tr.engine._side_on = side
+        torch.manual_seed(3)
+        np.random.seed(3)
+        dets = []
+        for s in range(3):
+            x, y = seeded_batch(cfg, 4, 128, 60 + s)
+            dets.append(dict(tr.train_step((x.cuda(), y.cuda()))[1]))
+        torch.cuda.synchronize()
+        out.append((dets, tr.engine.flat_p.detach().clone(), tr.model.quantizer.embeddings.detach().clone()))
+    assert out[0][0] == out[1][0]
+    assert torch.equal(out[0][1], out[1][1])
+    assert torch.equal(out[0][2], out[1][2])
