@@ -53,6 +53,9 @@ constexpr int kBN = 128;  // tile width (and height)
 #ifndef VQX_EPI_PREVEC_DGRAD  // 1: DGRAD epilogues hoist the per-channel vectors too (A/B)
 #define VQX_EPI_PREVEC_DGRAD 0
 #endif
+#ifndef VQX_EPI_PREFETCH_DGRAD  // 1: DGRAD epilogues prefetch their row operands too (A/B)
+#define VQX_EPI_PREFETCH_DGRAD 0
+#endif
 constexpr unsigned kOOB = 0x80000000u;  // buffer offset that is always out of range -> loads 0
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 
@@ -486,8 +489,12 @@ __device__ __forceinline__ void gnbwd8(const GemmParams& P, int64_t row, int col
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const float xa = (ua[e] - ma) * ra, xb = (ub[e] - mb) * rb;
+#ifdef VQX_LAB_GNBWD_NOTRANS  // lab only: the GLU derivative without its transcendentals (timing split)
+    const float ta = xa * ga[e] + ba[e], sb = xb * gb[e] + bb[e];
+#else
     const float ta = ftanh<sizeof(T) == 2>(xa * ga[e] + ba[e]);
     const float sb = fsigmoid<sizeof(T) == 2>(xb * gb[e] + bb[e]);
+#endif
     const float dga = ga[e] * (dy[e] * sb * (1.f - ta * ta));
     const float dgb = gb[e] * (dy[e] * ta * (sb * (1.f - sb)));
     s[0] += dga;
@@ -620,7 +627,9 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
             for (int e = 0; e < 8; ++e) q8 = fmaf(v[e] - m8, v[e] - m8, q8);
             moments_merge(mn, mm, mq, 8.f, m8, q8);
           }
+#ifndef VQX_LAB_NO_GNBWD  // lab only (tools/lab/k1_lab.cpp): skip the GroupNorm/GLU backward sums
           if (P.epi & EMASK & VQX_EPI_GNBWD) gnbwd8<T, PREVEC>(P, row, col, v, gs, o, V);
+#endif
         }
       }
     });
@@ -1042,10 +1051,11 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
   // prologue (tools/lab/k1_lab.cpp, profiles/r02/k1_lab.txt: SPLIT 33.4 -> 30.6 us,
   // GNADD 26.9 -> 26.0 us; the DGRAD GNBWD epilogues, VALU-bound, ran 5-9% slower
   // with it and keep loading pass by pass)
-  constexpr bool kPrefetch = sizeof(T) == 2 && MODE == MODE_FWD && EK != EK_NONE && EK != EK_ALL && VQX_EPI_PREFETCH;
+  constexpr bool kPrefetch = sizeof(T) == 2 && EK != EK_NONE && EK != EK_ALL && VQX_EPI_PREFETCH &&
+                             (MODE == MODE_FWD || (MODE == MODE_DGRAD && VQX_EPI_PREFETCH_DGRAD));
   // per-channel vectors (bias, GN affine) hoisted out of the row passes
-  constexpr bool kPreVec = kPrefetch || (sizeof(T) == 2 && MODE == MODE_DGRAD && EK != EK_NONE && EK != EK_ALL &&
-                                         VQX_EPI_PREVEC_DGRAD);
+  constexpr bool kPreVec = (kPrefetch && MODE == MODE_FWD) ||
+                          (sizeof(T) == 2 && MODE == MODE_DGRAD && EK != EK_NONE && EK != EK_ALL && VQX_EPI_PREVEC_DGRAD);
   EpiRows rows;
   if constexpr (kPrefetch) {
     if (nk <= 0) epi_prefetch<EK>(P, m0, n0, tid, rows);
