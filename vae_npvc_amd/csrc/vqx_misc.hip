@@ -1095,6 +1095,123 @@ __global__ __launch_bounds__(256) void linear_batched_bwd_x_kernel(const vqx_lin
   }
 }
 
+// ---- speaker-conditioning fast path: I = 128 inputs, B <= 64 rows, O % 32 == 0
+// (every recipe: cond dim 128).  One workgroup per (32 output channels,
+// layer) holds all of c (64 x 128) and the layer's 32 x 128 weight slice in
+// LDS and multiplies them in one pass: one global round trip instead of one
+// per 64-wide K tile, and 2x the workgroups of the tiled kernels above.  The
+// summation orders are those of the tiled kernels (i, resp. b, ascending), so
+// the results are bit-identical to them.
+constexpr int kCondI = 128, kCondB = 64, kCondO = 32;
+
+// out_l[b][o] = bias_l[o] + sum_i c[b][i] W_l[o][i]; grid (O/32, n)
+__global__ __launch_bounds__(256) void linear_cond_fwd_kernel(const vqx_linear_layer* __restrict__ L,
+                                                              const float* __restrict__ c, int B, int O) {
+  const vqx_linear_layer& l = L[blockIdx.y];
+  const int o0 = blockIdx.x * kCondO;
+  __shared__ __attribute__((aligned(16))) float cs[kCondB][kCondI + 4];  // [b][i]
+  __shared__ __attribute__((aligned(16))) float wt[kCondI][kCondO + 4];  // [i][o]
+  const int t = threadIdx.x;
+  for (int e = t; e < kCondB * kCondI / 4; e += 256) {
+    const int b = e / (kCondI / 4), i4 = e % (kCondI / 4);
+    const f32x4_t z = {0.f, 0.f, 0.f, 0.f};
+    *(f32x4_t*)&cs[b][4 * i4] = b < B ? *(const f32x4_t*)(c + (int64_t)b * kCondI + 4 * i4) : z;
+  }
+  for (int e = t; e < kCondO * kCondI / 4; e += 256) {
+    const int r = e / (kCondI / 4), i4 = e % (kCondI / 4);
+    const f32x4_t w = *(const f32x4_t*)(l.W + (int64_t)(o0 + r) * kCondI + 4 * i4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) wt[4 * i4 + k][r] = w[k];
+  }
+  __syncthreads();
+  const int b = t >> 2, oq = (t & 3) * 8;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+  for (int i = 0; i < kCondI; ++i) {
+    const float x = cs[b][i];
+    const f32x4_t w0 = *(const f32x4_t*)&wt[i][oq], w1 = *(const f32x4_t*)&wt[i][oq + 4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      acc[k] = fmaf(x, w0[k], acc[k]);
+      acc[4 + k] = fmaf(x, w1[k], acc[4 + k]);
+    }
+  }
+  if (b >= B) return;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int o = o0 + oq + j;
+    l.out[(int64_t)b * O + o] = acc[j] + (l.bias ? l.bias[o] : 0.f);
+  }
+}
+
+// dW_l[o][i] = sum_b dout_l[b][o] c[b][i], dbias_l[o] = sum_b dout_l[b][o]; grid (O/32, n)
+__global__ __launch_bounds__(256) void linear_cond_bwd_w_kernel(const vqx_linear_layer* __restrict__ L,
+                                                                const float* __restrict__ c, int B, int O) {
+  const vqx_linear_layer& l = L[blockIdx.y];
+  const int o0 = blockIdx.x * kCondO;
+  __shared__ __attribute__((aligned(16))) float cs[kCondB][kCondI + 4];  // [b][i]
+  __shared__ float ds[kCondB][kCondO + 1];                               // [b][o]
+  const int t = threadIdx.x;
+  for (int e = t; e < kCondB * kCondI / 4; e += 256) {
+    const int b = e / (kCondI / 4), i4 = e % (kCondI / 4);
+    const f32x4_t z = {0.f, 0.f, 0.f, 0.f};
+    *(f32x4_t*)&cs[b][4 * i4] = b < B ? *(const f32x4_t*)(c + (int64_t)b * kCondI + 4 * i4) : z;
+  }
+  for (int e = t; e < kCondB * kCondO; e += 256) {
+    const int b = e / kCondO, q = e % kCondO;
+    ds[b][q] = b < B ? l.dout[(int64_t)b * O + o0 + q] : 0.f;
+  }
+  __syncthreads();
+  const int ol = t >> 3, ic = (t & 7) * 16;
+  float acc[16], db = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+#pragma unroll 4
+  for (int b = 0; b < kCondB; ++b) {
+    const float d = ds[b][ol];
+    db += d;
+#pragma unroll
+    for (int j = 0; j < 16; j += 4) {
+      const f32x4_t x = *(const f32x4_t*)&cs[b][ic + j];
+      acc[j] = fmaf(d, x[0], acc[j]);
+      acc[j + 1] = fmaf(d, x[1], acc[j + 1]);
+      acc[j + 2] = fmaf(d, x[2], acc[j + 2]);
+      acc[j + 3] = fmaf(d, x[3], acc[j + 3]);
+    }
+  }
+  const int o = o0 + ol;
+  float* dw = l.dW + (int64_t)o * kCondI + ic;
+#pragma unroll
+  for (int j = 0; j < 16; j += 4) *(f32x4_t*)(dw + j) = f32x4_t{acc[j], acc[j + 1], acc[j + 2], acc[j + 3]};
+  if ((t & 7) == 0 && l.dbias) l.dbias[o] = db;
+}
+
+// dc[e] = sum_p part[p][e] in a fixed order: each of the 4 waves of a
+// workgroup sums a contiguous quarter of the slices (8 loads in flight) for
+// 64 elements, then the quarters are added in order (deterministic).
+__global__ __launch_bounds__(256) void sum_slices_wide_kernel(const float* __restrict__ part, int np, int64_t n,
+                                                              float* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+  const int q = threadIdx.x >> 6;
+  const int p0 = (int)((int64_t)np * q / 4), p1 = (int)((int64_t)np * (q + 1) / 4);
+  __shared__ float red[4][64];
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (e < n) {
+    int p = p0;
+    for (; p + 8 <= p1; p += 8) {
+      float t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = part[(int64_t)(p + u) * n + e];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] += t[u];
+    }
+    for (int u = 0; p < p1; ++p, ++u) a[u] += part[(int64_t)p * n + e];
+  }
+  red[q][threadIdx.x & 63] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  __syncthreads();
+  if (q == 0 && e < n) out[e] = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+}
+
 // dc[e] = sum_p part[p][e] in a fixed order (deterministic)
 __global__ __launch_bounds__(256) void sum_slices_kernel(const float* __restrict__ part, int np, int64_t n,
                                                          float* __restrict__ out) {
@@ -1600,8 +1717,12 @@ extern "C" int vqx_scale_act_2d(const void* src, int32_t ld_src, int32_t src_dty
 extern "C" int vqx_linear_batched_fwd(const vqx_linear_layer* table_dev, int32_t n, const float* c, int32_t B,
                                       int32_t I, int32_t O, vqx_stream_t stream) {
   if (!table_dev || n < 1 || !c || B < 1 || I < 1 || O < 1) { set_error("vqx_linear_batched_fwd: bad arguments"); return -1; }
-  hipLaunchKernelGGL(linear_batched_fwd_kernel, dim3((O + kLT - 1) / kLT, n, (B + kLT - 1) / kLT), dim3(256), 0,
-                     (hipStream_t)stream, table_dev, c, B, I, O);
+  if (I == kCondI && B <= kCondB && O % kCondO == 0 && ((uintptr_t)c & 15) == 0)
+    hipLaunchKernelGGL(linear_cond_fwd_kernel, dim3(O / kCondO, n), dim3(256), 0, (hipStream_t)stream, table_dev, c, B,
+                       O);
+  else
+    hipLaunchKernelGGL(linear_batched_fwd_kernel, dim3((O + kLT - 1) / kLT, n, (B + kLT - 1) / kLT), dim3(256), 0,
+                       (hipStream_t)stream, table_dev, c, B, I, O);
   return launch_status("vqx_linear_batched_fwd");
 }
 
@@ -1611,13 +1732,17 @@ extern "C" int vqx_linear_batched_bwd(const vqx_linear_layer* table_dev, int32_t
   if (dc && !partials) { set_error("vqx_linear_batched_bwd: dc needs partials [n*ceil(O/64)][B][I]"); return -1; }
   hipStream_t s = (hipStream_t)stream;
   const int nO = (O + kLT - 1) / kLT;
-  hipLaunchKernelGGL(linear_batched_bwd_w_kernel, dim3(nO, n, (I + kLT - 1) / kLT), dim3(256), 0, s,
-                     table_dev, c, B, I, O);
+  if (I == kCondI && B <= kCondB && O % kCondO == 0 && ((uintptr_t)c & 15) == 0)
+    hipLaunchKernelGGL(linear_cond_bwd_w_kernel, dim3(O / kCondO, n), dim3(256), 0, s, table_dev, c, B, O);
+  else
+    hipLaunchKernelGGL(linear_batched_bwd_w_kernel, dim3(nO, n, (I + kLT - 1) / kLT), dim3(256), 0, s,
+                       table_dev, c, B, I, O);
   if (dc) {
     hipLaunchKernelGGL(linear_batched_bwd_x_kernel, dim3(nO, n, ((B + kLT - 1) / kLT) * ((I + kLT - 1) / kLT)),
                        dim3(256), 0, s, table_dev, B, I, O, partials);
     const int64_t ne = (int64_t)B * I;
-    hipLaunchKernelGGL(sum_slices_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, s, partials, n * nO, ne, dc);
+    hipLaunchKernelGGL(sum_slices_wide_kernel, dim3((unsigned)((ne + 63) / 64)), dim3(256), 0, s, partials, n * nO, ne,
+                       dc);
   }
   return launch_status("vqx_linear_batched_bwd");
 }
