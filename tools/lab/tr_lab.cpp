@@ -78,11 +78,12 @@ static void run(const Shape& s, void* x, void* w, void* y, float* part) {
     int rows, block;
   } vs[] = {{"tr128", (const void*)conv_tr_kernel<MODE, EK, 32>, 128, 256},
             {"tr8x256", (const void*)conv_tr8_kernel<MODE, EK, 1>, 256, 512},
-            {"tr8x512", (const void*)conv_tr8_kernel<MODE, EK, 2>, 512, 512}};
+            {"tr8x512", (const void*)conv_tr8_kernel<MODE, EK, 2>, 512, 512},
+            {"tr8x512k16", (const void*)conv_tr8_kernel<MODE, EK, 2, 16>, 512, 512}};
   for (const V& v : vs) {
     P.tiles_m = (int)(s.N / v.rows);
     const float us = time_us(v.fn, P.tiles_m * P.tiles_n, v.block, P, 20);
-    printf("lab%d %-13s EK%d %-8s %7.1f us %7.1f TF\n", VQX_GEMM_LAB, s.name, EK, v.name, us, fl / us * 1e-6);
+    printf("lab%d %-13s EK%d %-10s %7.1f us %7.1f TF\n", VQX_GEMM_LAB, s.name, EK, v.name, us, fl / us * 1e-6);
   }
 }
 
@@ -148,7 +149,7 @@ int main() {
     run_wgrad("dec_in_wgrad", 16384, 256, 512, 1024, 16, -1, x, y, sl);
     CK(hipFree(sl));
   }
-  if (getenv("TR_LAB_WGRAD_ONLY")) return 0;
+  if (const char* e = getenv("TR_LAB_WGRAD_ONLY"); e && *e) return 0;
   for (const Shape& s : shapes) {
     if (s.mode == MODE_FWD) {
       run<MODE_FWD, EK_NONE>(s, x, w, y, part);

@@ -1309,10 +1309,13 @@ __global__ __launch_bounds__(256, 2) void conv_tr_kernel(GemmParams P) {
 // 128 x 128; the two 4-wave groups own SEGS quadrants each, every wave a
 // 64 x 64 block of each, laid out exactly as conv_tr_kernel's waves so that
 // each group runs tile_epilogue on its quadrants in its own 44 KiB of LDS.
-template <int MODE, int EK, int SEGS>
+// BKC = channels per stage: 32 (2-deep ring) or 16 (4-deep ring, two stages
+// in flight behind counted vmcnt waits: the same LDS, twice the prefetch distance).
+template <int MODE, int EK, int SEGS, int BKC = 32>
 __global__ __launch_bounds__(512, 1) void conv_tr8_kernel(GemmParams P) {
   using T = bf16_t;
-  constexpr int BKC = 32, ES = 2, EPC = 8, KCH = 4;  // 64-B K-major rows
+  constexpr int ES = 2, EPC = 8, KCH = BKC * ES / 16;  // 16-B chunks per K-major row
+  constexpr int NST = BKC == 32 ? 2 : 4;
   constexpr int SROWS = 258;                         // staged frames per segment
   constexpr int AROWS = SEGS * SROWS;
   constexpr int A_PIECES = (AROWS * BKC * ES + 1023) / 1024;
@@ -1320,11 +1323,11 @@ __global__ __launch_bounds__(512, 1) void conv_tr8_kernel(GemmParams P) {
   constexpr int PWA = (A_PIECES + 7) / 8;            // activation pieces per wave (some waves one fewer)
   constexpr int TAP_BYTES = 128 * BKC * ES;
   constexpr int TAP_PIECES = TAP_BYTES / 1024;
-  constexpr int PWB = 3 * TAP_PIECES / 8;            // weight pieces per wave
+  constexpr int B_PIECES = 3 * TAP_PIECES;
+  constexpr int PWB = (B_PIECES + 7) / 8;            // weight pieces per wave (wid, wid+8, ...)
   constexpr int STAGE = A_BYTES + 3 * TAP_BYTES;
   constexpr int EPI_BYTES = 45056;                   // tile_epilogue's LDS per group
-  constexpr int SMEM = 2 * STAGE > 2 * EPI_BYTES ? 2 * STAGE : 2 * EPI_BYTES;
-  static_assert(3 * TAP_PIECES % 8 == 0, "weight pieces split evenly over 8 waves");
+  constexpr int SMEM = NST * STAGE > 2 * EPI_BYTES ? NST * STAGE : 2 * EPI_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1354,18 +1357,21 @@ __global__ __launch_bounds__(512, 1) void conv_tr8_kernel(GemmParams P) {
   unsigned boff[PWB];
 #pragma unroll
   for (int i = 0; i < PWB; ++i) {
-    const int pb = wid * PWB + i;
+    const int pb = wid + 8 * i;
     const int tap = pb / TAP_PIECES, c = (pb % TAP_PIECES) * 64 + lane;
     if constexpr (MODE == MODE_FWD) {  // We[co][tap*kcin + ci], K-major rows of BKC channels
       const int row = c / KCH, kch = (c % KCH) ^ tr_kswz<KCH>(row);
       const int co = n0 + row;
-      boff[i] = co < P.Nc ? (unsigned)(((int64_t)co * P.K + tap * P.kcin + kch * EPC) * ES) : kOOB;
+      boff[i] = (pb < B_PIECES && co < P.Nc) ? (unsigned)(((int64_t)co * P.K + tap * P.kcin + kch * EPC) * ES) : kOOB;
     } else {  // forward weight We[co][j][ci] read as rows co of tap j = 2 - tap (taps flipped)
       const int krow = c / 16, cch = (c % 16) ^ mn_swz(krow);
       const int ci = n0 + cch * EPC;
-      boff[i] = ci < P.Nc ? (unsigned)(((int64_t)krow * 3 * P.cdim + (2 - tap) * P.cdim + ci) * ES) : kOOB;
+      boff[i] = (pb < B_PIECES && ci < P.Nc)
+                    ? (unsigned)(((int64_t)krow * 3 * P.cdim + (2 - tap) * P.cdim + ci) * ES) : kOOB;
     }
   }
+  // DMA instructions of this wave per stage (the counted vmcnt waits of the 4-deep ring)
+  const int npw = (A_PIECES - wid + 7) / 8 + (B_PIECES - wid + 7) / 8;
   const __amdgpu_buffer_rsrc_t rsA = rsrc_at(P.a, -(int64_t)P.lda * ES, P.a_bytes);
   const __amdgpu_buffer_rsrc_t rsB = rsrc_at(P.b, 0, P.b_bytes);
 
@@ -1378,7 +1384,8 @@ __global__ __launch_bounds__(512, 1) void conv_tr8_kernel(GemmParams P) {
     for (int i = 0; i < PWA; ++i)
       if (wid + 8 * i < A_PIECES) dma16(rsA, st + (wid + 8 * i) * 1024, aoff[i] + ksa);
 #pragma unroll
-    for (int i = 0; i < PWB; ++i) dma16(rsB, st + A_BYTES + (wid * PWB + i) * 1024, boff[i] + ksb);
+    for (int i = 0; i < PWB; ++i)
+      if (wid + 8 * i < B_PIECES) dma16(rsB, st + A_BYTES + (wid + 8 * i) * 1024, boff[i] + ksb);
   };
 
   f32x16_t acc[SEGS][2][2];
@@ -1446,17 +1453,28 @@ __global__ __launch_bounds__(512, 1) void conv_tr8_kernel(GemmParams P) {
   };
 
   if (nk > 0) {
-    dma_stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // NST-1 stages in flight ahead of the one being multiplied
+    const int pre = nk < NST - 1 ? nk : NST - 1;
+#pragma unroll
+    for (int t = 0; t < NST - 1; ++t)
+      if (t < pre) dma_stage(t, t);
+    if constexpr (NST == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else wait_vm(npw * (pre - 1));
     __builtin_amdgcn_s_barrier();
     int buf = 0;
     for (int kt = 0; kt < nk; ++kt) {
-      if (VQX_GEMM_LAB != 1 && kt + 1 < nk) dma_stage(buf ^ 1, kt + 1);
+      if (VQX_GEMM_LAB != 1 && kt + NST - 1 < nk) dma_stage(buf == 0 ? NST - 1 : buf - 1, kt + NST - 1);
       if (VQX_GEMM_LAB != 2) compute_stage(buf);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (NST == 2) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {  // stage kt+1 must have landed; later ones may stay in flight
+        int ahead = (kt + NST - 1 < nk ? kt + NST : nk) - (kt + 2);
+        if (ahead < 0) ahead = 0;
+        wait_vm(npw * ahead);
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      buf ^= 1;
+      buf = buf + 1 == NST ? 0 : buf + 1;
     }
   }
   if (VQX_GEMM_LAB == 3) {  // keep the accumulators live
