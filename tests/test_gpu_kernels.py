@@ -182,6 +182,46 @@ def test_convtranspose_via_weight_norm_pack(dtype, tile):
     assert relerr(dwt, wr.grad) < TOL[dtype]
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_weight_norm_pack_layouts(dtype):
+    """vqx_weight_norm_fwd over one table of mixed layers (the flat unit grid):
+    Conv1d 1x1 (wave-per-row path, incl. an unaligned row length), Conv1d k3/k5
+    (row-in-LDS transpose), ConvTranspose1d k3 (vectorised 64 x 32 tile) and
+    ragged / k5 ConvT (scalar tile) against torch._weight_norm packed to
+    wp[co][j*cin + ci] (ConvT taps flipped).  fp32: 1e-6 relative; bf16: the
+    fp32 result rounded to nearest-even exactly, up to 1 ulp where the norm's
+    summation order differs."""
+    ops = _ops()
+    torch.manual_seed(11)
+    specs = [(0, 512, 640, 1), (0, 128, 1024, 1), (0, 70, 33, 1), (0, 512, 512, 3), (0, 96, 80, 5),
+             (1, 512, 1024, 3), (1, 100, 70, 3), (1, 64, 48, 5), (1, 128, 96, 1)]
+    ents, refs = [], []
+    for kind, cin, cout, k in specs:
+        shape = (cout, cin, k) if kind == 0 else (cin, cout, k)
+        v = torch.randn(*shape, device=DEV)
+        rows = shape[0]
+        g = torch.rand(rows, device=DEV) + 0.5
+        wp = torch.empty(cout, k * cin, device=DEV, dtype=dtype)
+        norm = torch.empty(rows, device=DEV)
+        ents.append(dict(v=v, g=g, w_packed=wp, norm=norm, kind=kind, cout=cout, cin=cin, k=k,
+                         dtype=ops.dt_code(dtype)))
+        vd, gd = v.double().cpu(), g.double().cpu()
+        w = torch._weight_norm(vd, gd.view(rows, 1, 1), 0)
+        eff = w.permute(0, 2, 1) if kind == 0 else w.flip(-1).permute(1, 2, 0)  # [co][j][ci]
+        refs.append((eff.reshape(cout, k * cin), vd.flatten(1).norm(dim=1)))
+    ops.weight_norm_fwd(ops.wn_table(ents))
+    torch.cuda.synchronize()
+    for (kind, cin, cout, k), e, (ref, nref) in zip(specs, ents, refs):
+        got = e["w_packed"].double().cpu()
+        assert relerr(e["norm"], nref) < 1e-6, (kind, cin, cout, k)
+        if dtype == torch.float32:
+            assert relerr(got, ref) < 1e-6, (kind, cin, cout, k)
+        else:
+            r16 = ref.float().to(torch.bfloat16).double()
+            ulp = (r16.abs() * 2.0 ** -7).clamp_min(1e-30)
+            assert bool(((got - r16).abs() <= ulp).all()), (kind, cin, cout, k)
+
+
 @pytest.mark.parametrize("K", [128, 512, 1024])
 def test_vq_argmin_exact(K):
     ops = _ops()

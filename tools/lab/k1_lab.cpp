@@ -15,6 +15,9 @@
 #define VQX_LAB_MODE 0
 #endif
 #include "vqx_gemm_kernel.h"
+#ifndef K1_NST  // ring depth of the 64-deep K-tiles (lab: 3, 4 = one workgroup per CU)
+#define K1_NST 2
+#endif
 
 using namespace vqx;
 
@@ -131,11 +134,11 @@ int main() {
     P.gn_glu = c.kin == 640 ? 1 : 0;
     const void* fn = nullptr;
     if (c.mode == MODE_FWD) {
-      if (c.ek == EK_GNADD) fn = (const void*)conv_gemm_kernel<bf16_t, MODE_FWD, VQX_PRO_NONE, false, 64, 2, EK_GNADD>;
-      else if (c.ek == EK_SPLIT) fn = (const void*)conv_gemm_kernel<bf16_t, MODE_FWD, VQX_PRO_NONE, false, 64, 2, EK_SPLIT>;
-      else fn = (const void*)conv_gemm_kernel<bf16_t, MODE_FWD, VQX_PRO_NONE, false, 64, 2, EK_NONE>;
+      if (c.ek == EK_GNADD) fn = (const void*)conv_gemm_kernel<bf16_t, MODE_FWD, VQX_PRO_NONE, false, 64, K1_NST, EK_GNADD>;
+      else if (c.ek == EK_SPLIT) fn = (const void*)conv_gemm_kernel<bf16_t, MODE_FWD, VQX_PRO_NONE, false, 64, K1_NST, EK_SPLIT>;
+      else fn = (const void*)conv_gemm_kernel<bf16_t, MODE_FWD, VQX_PRO_NONE, false, 64, K1_NST, EK_NONE>;
     } else {
-      fn = (const void*)conv_gemm_kernel<bf16_t, MODE_DGRAD, VQX_PRO_NONE, false, 64, 2, EK_GNBWD>;
+      fn = (const void*)conv_gemm_kernel<bf16_t, MODE_DGRAD, VQX_PRO_NONE, false, 64, K1_NST, EK_GNBWD>;
     }
     const float us = time_us(fn, P.tiles_m * P.tiles_n, P, 20);
     const double fl = 2.0 * N * c.kin * c.kout;
@@ -148,7 +151,7 @@ int main() {
 #ifndef VQX_EPI_PREVEC_DGRAD
 #define VQX_EPI_PREVEC_DGRAD 0
 #endif
-    printf("prevec_dgrad%d prefetch%d stagger%d mode%d %-20s %7.1f us %7.1f TF\n", VQX_EPI_PREVEC_DGRAD, VQX_EPI_PREFETCH, VQX_GEMM_STAGGER, VQX_LAB_MODE, c.name, us, fl / us * 1e-6);
+    printf("nst%d prevec_dgrad%d prefetch%d stagger%d mode%d %-20s %7.1f us %7.1f TF\n", K1_NST, VQX_EPI_PREVEC_DGRAD, VQX_EPI_PREFETCH, VQX_GEMM_STAGGER, VQX_LAB_MODE, c.name, us, fl / us * 1e-6);
   }
   CK(hipDeviceSynchronize());
   return 0;

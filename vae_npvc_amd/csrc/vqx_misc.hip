@@ -39,25 +39,49 @@ __global__ __launch_bounds__(256) void wn_norm_kernel(const vqx_wn_layer* __rest
 }
 
 // Pack w = g*v/||v|| into the effective-conv layout wp[co][j][ci].
-// kind 0 (Conv1d, v[co][ci][j]): block = one row co: the row is read
+// kind 0 (Conv1d, v[co][ci][j]), K > 1: block = one row co: the row is read
 //   contiguously into LDS, its norm reduced there (and saved), then written
 //   transposed [j][ci] with coalesced stores.
-// kind 1 (ConvT, v[ci][co][K-1-j]): block = a 64 ci x 64 co tile, read row
-//   segments (64*K contiguous floats per ci) into LDS, write wp[co][j][ci0..]
-//   rows of 64 consecutive ci.
+// kind 0, K = 1: no transpose: block = 4 rows, one wave each (16-B loads, a
+//   wave reduction, then the scaled row re-read from cache and stored 8 B a
+//   lane) -- no LDS, no barriers.
+// kind 1 (ConvT, v[ci][co][K-1-j]): block = a 64 ci x TCO co tile, read row
+//   segments (TCO*K contiguous floats per ci; 384 B for K = 3) into LDS, write
+//   wp[co][j][ci0..] rows of 64 consecutive ci, 16 B a lane.
+// The grid is flat over every layer's units (WnUnits: per-layer prefix), so
+// no workgroup of a small layer launches only to exit.
 constexpr int kWnRow = 4096;
+constexpr int kWnMaxL = 128;  // layers per pack launch (the host launches larger tables in chunks)
+struct WnUnits {
+  int n;
+  int off[kWnMaxL + 1];
+};
 // ConvT pack tile width in co: the LDS tile holds 64 ci x (TCO*K + pad) floats
-__host__ __device__ inline int wn_tco(int K) { return K <= 4 ? 16 : (K <= 64 ? 64 / K : 1); }
-__global__ __launch_bounds__(256) void wn_pack_kernel(const vqx_wn_layer* __restrict__ L, int n_layers) {
-  const vqx_wn_layer& l = L[blockIdx.y];
+__host__ __device__ inline int wn_tco(int K) { return K <= 3 ? 32 : K <= 4 ? 16 : (K <= 64 ? 64 / K : 1); }
+constexpr int kWnBuf = 96 * 65;  // floats: the K = 3 ConvT tile (>= kWnRow + 64 for the Conv1d rows)
+static_assert(kWnBuf >= kWnRow + 64, "wn pack LDS");
+__host__ __device__ inline int wn_pack_units(const vqx_wn_layer& l) {
+  if (l.kind == VQX_WN_RESAMPLE) return l.cout;
+  if (l.kind == VQX_WN_RESAMPLE_T) return l.cin;
+  if (l.kind == 0) return l.k == 1 ? (l.cout + 3) / 4 : l.cout;
+  return ((l.cin + 63) / 64) * ((l.cout + wn_tco(l.k) - 1) / wn_tco(l.k));
+}
+__global__ __launch_bounds__(256) void wn_pack_kernel(const vqx_wn_layer* __restrict__ L, WnUnits U) {
+  int lo = 0, hi = U.n - 1;  // the layer owning this block: largest li with off[li] <= blockIdx.x
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (U.off[mid] <= (int)blockIdx.x) lo = mid; else hi = mid - 1;
+  }
+  const vqx_wn_layer& l = L[lo];
+  const int unit = (int)blockIdx.x - U.off[lo];
   const int K = l.k, cin = l.cin, cout = l.cout;
-  __shared__ float buf[kWnRow + 64];
+  __shared__ float buf[kWnBuf];
   __shared__ float red[16];
   if (l.kind == VQX_WN_RESAMPLE || l.kind == VQX_WN_RESAMPLE_T) {
     // strided conv (include/vqx.h): row r of v, norm, then the folded 3-tap row
     // w_packed[r][m][q*C + c] = w[r][c][S*(m-1) + q + pad]
     const int rows = l.kind == VQX_WN_RESAMPLE ? cout : cin, C = l.kind == VQX_WN_RESAMPLE ? cin : cout;
-    const int r = blockIdx.x;
+    const int r = unit;
     if (r >= rows) return;
     const int cols = C * K;
     const float* v = l.v + (int64_t)r * cols;
@@ -82,8 +106,45 @@ __global__ __launch_bounds__(256) void wn_pack_kernel(const vqx_wn_layer* __rest
     }
     return;
   }
+  if (l.kind == 0 && K == 1) {
+    const int co = unit * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (co >= cout) return;
+    const float* v = l.v + (int64_t)co * cin;
+    const bool vec = (cin & 3) == 0 && (((uintptr_t)v) & 15) == 0 &&
+                     ((((uintptr_t)l.w_packed) + (int64_t)co * cin * (l.dtype == VQX_BF16 ? 2 : 4)) & 15) == 0;
+    float s = 0.f;
+    if (vec) {
+      for (int i = lane * 4; i < cin; i += 256) {
+        const f32x4_t x = *(const f32x4_t*)(v + i);
+        s = fmaf(x[0], x[0], fmaf(x[1], x[1], fmaf(x[2], x[2], fmaf(x[3], x[3], s))));
+      }
+    } else {
+      for (int i = lane; i < cin; i += 64) s = fmaf(v[i], v[i], s);
+    }
+    s = wave_sum(s);
+    float sc = 1.f;
+    if (l.g) {
+      const float nrm = sqrtf(s);
+      if (lane == 0) l.norm[co] = nrm;
+      sc = l.g[co] / nrm;
+    }
+    if (vec) {
+      for (int i = lane * 4; i < cin; i += 256) {
+        const f32x4_t x = *(const f32x4_t*)(v + i);
+        if (l.dtype == VQX_BF16) {
+          *(uint2*)((bf16_t*)l.w_packed + (int64_t)co * cin + i) =
+              make_uint2(pack_bf16x2(x[0] * sc, x[1] * sc), pack_bf16x2(x[2] * sc, x[3] * sc));
+        } else {
+          *(f32x4_t*)((float*)l.w_packed + (int64_t)co * cin + i) = f32x4_t{x[0] * sc, x[1] * sc, x[2] * sc, x[3] * sc};
+        }
+      }
+    } else {
+      for (int i = lane; i < cin; i += 64) st_dt(l.w_packed, (int64_t)co * cin + i, v[i] * sc, l.dtype);
+    }
+    return;
+  }
   if (l.kind == 0) {
-    const int co = blockIdx.x;
+    const int co = unit;
     if (co >= cout) return;
     const int cols = cin * K;
     const float* v = l.v + (int64_t)co * cols;
@@ -106,29 +167,62 @@ __global__ __launch_bounds__(256) void wn_pack_kernel(const vqx_wn_layer* __rest
     }
     return;
   }
-  // kind 1: tile of 64 ci x TCO co (x K taps) = 64 x TCO*K floats <= 64 x 64 in LDS
+  // kind 1: tile of 64 ci x TCO co (x K taps) = 64 x TCO*K floats in LDS ([co_local*K + tap][ci], +1 pad)
   const int TCO = wn_tco(K);
   const int ntc = (cout + TCO - 1) / TCO;
-  const int ci0 = (blockIdx.x / ntc) * 64, co0 = (blockIdx.x % ntc) * TCO;
+  const int ci0 = (unit / ntc) * 64, co0 = (unit % ntc) * TCO;
   if (ci0 >= cin || K > 64) return;
   const int wseg = TCO * K;  // floats per ci row segment (contiguous in v)
-  for (int e = threadIdx.x; e < 64 * wseg; e += 256) {
-    const int r = e / wseg, q = e - r * wseg;  // r: ci offset, q = co_local*K + tap
-    const int ci = ci0 + r, co = co0 + q / K;
-    float x = 0.f;
-    if (ci < cin && co < cout) {
-      x = l.v[((int64_t)ci * cout + co0) * K + q];
-      if (l.g) x *= l.g[ci] / l.norm[ci];
+  const bool full = ci0 + 64 <= cin && co0 + TCO <= cout;
+  if (full && (wseg & 3) == 0 && ((cout * K) & 3) == 0 && (((uintptr_t)l.v) & 15) == 0) {
+    const int w4 = wseg >> 2;
+    for (int e = threadIdx.x; e < 64 * w4; e += 256) {
+      const int r = e / w4, q = (e - r * w4) * 4;
+      const int ci = ci0 + r;
+      f32x4_t x = *(const f32x4_t*)(l.v + ((int64_t)ci * cout + co0) * K + q);
+      if (l.g) {
+        const float sc = l.g[ci] / l.norm[ci];
+        x = f32x4_t{x[0] * sc, x[1] * sc, x[2] * sc, x[3] * sc};
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) buf[(q + u) * 65 + r] = x[u];
     }
-    buf[q * 65 + r] = x;  // [co_local*K + tap][ci] (+1 pad)
+  } else {
+    for (int e = threadIdx.x; e < 64 * wseg; e += 256) {
+      const int r = e / wseg, q = e - r * wseg;  // r: ci offset, q = co_local*K + tap
+      const int ci = ci0 + r, co = co0 + q / K;
+      float x = 0.f;
+      if (ci < cin && co < cout) {
+        x = l.v[((int64_t)ci * cout + co0) * K + q];
+        if (l.g) x *= l.g[ci] / l.norm[ci];
+      }
+      buf[q * 65 + r] = x;
+    }
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < TCO * K * 64; e += 256) {  // e = (co_local*K + j)*64 + ci_local
-    const int cj = e >> 6, r = e & 63;
-    const int cl = cj / K, j = cj - cl * K;
-    const int co = co0 + cl, ci = ci0 + r;
-    if (co < cout && ci < cin)
-      st_dt(l.w_packed, ((int64_t)co * K + j) * cin + ci, buf[(cl * K + (K - 1 - j)) * 65 + r], l.dtype);
+  const size_t es = l.dtype == VQX_BF16 ? 2 : 4;
+  if (full && (cin & 7) == 0 && (((uintptr_t)l.w_packed) & 15) == 0) {
+    for (int e = threadIdx.x; e < wseg * 8; e += 256) {  // e = (co_local*K + j)*8 + 8-ci chunk
+      const int cj = e >> 3, r8 = (e & 7) * 8;
+      const int cl = cj / K, j = cj - cl * K;
+      const float* src = buf + (cl * K + (K - 1 - j)) * 65 + r8;
+      const int64_t o = ((int64_t)(co0 + cl) * K + j) * cin + ci0 + r8;
+      if (es == 2) {
+        *(uint4*)((bf16_t*)l.w_packed + o) = make_uint4(pack_bf16x2(src[0], src[1]), pack_bf16x2(src[2], src[3]),
+                                                        pack_bf16x2(src[4], src[5]), pack_bf16x2(src[6], src[7]));
+      } else {
+        *(f32x4_t*)((float*)l.w_packed + o) = f32x4_t{src[0], src[1], src[2], src[3]};
+        *(f32x4_t*)((float*)l.w_packed + o + 4) = f32x4_t{src[4], src[5], src[6], src[7]};
+      }
+    }
+  } else {
+    for (int e = threadIdx.x; e < TCO * K * 64; e += 256) {  // e = (co_local*K + j)*64 + ci_local
+      const int cj = e >> 6, r = e & 63;
+      const int cl = cj / K, j = cj - cl * K;
+      const int co = co0 + cl, ci = ci0 + r;
+      if (co < cout && ci < cin)
+        st_dt(l.w_packed, ((int64_t)co * K + j) * cin + ci, buf[(cl * K + (K - 1 - j)) * 65 + r], l.dtype);
+    }
   }
 }
 
@@ -1392,21 +1486,25 @@ extern "C" int vqx_weight_norm_fwd(const vqx_wn_layer* lh, const vqx_wn_layer* l
     const int64_t el = (int64_t)l.cout * l.cin * l.k;
     max_el = el > max_el ? el : max_el;
   }
-  // kind 0: one block per row; kind 1: 64 ci x wn_tco(K) co tiles (after the row norms)
-  int max_units = 1, max_t_rows = 1;
+  int max_t_rows = 1;
   for (int i = 0; i < n_layers; ++i) {
     const vqx_wn_layer& l = lh[i];
     const bool rsm = l.kind >= VQX_WN_RESAMPLE;
     const bool row_is_cout = l.kind == 0 || l.kind == VQX_WN_RESAMPLE;
     if ((row_is_cout ? l.cin : l.cout) * l.k > kWnRow || (!rsm && l.k > 64)) { set_error("vqx_weight_norm_fwd: layer %d row too long", i); return -1; }
-    const int units = rsm ? (row_is_cout ? l.cout : l.cin) : l.kind == 0 ? l.cout : ((l.cin + 63) / 64) * ((l.cout + wn_tco(l.k) - 1) / wn_tco(l.k));
-    max_units = units > max_units ? units : max_units;
     if (l.kind == 1) max_t_rows = l.cin > max_t_rows ? l.cin : max_t_rows;
   }
   (void)max_el;
+  (void)max_rows;
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(wn_norm_kernel, dim3((max_t_rows + 3) / 4, n_layers), dim3(256), 0, s, ld, n_layers);
-  hipLaunchKernelGGL(wn_pack_kernel, dim3(max_units, n_layers), dim3(256), 0, s, ld, n_layers);
+  for (int i0 = 0; i0 < n_layers; i0 += kWnMaxL) {  // flat grid over the layers' units, kWnMaxL layers a launch
+    WnUnits U;
+    U.n = n_layers - i0 < kWnMaxL ? n_layers - i0 : kWnMaxL;
+    U.off[0] = 0;
+    for (int i = 0; i < U.n; ++i) U.off[i + 1] = U.off[i] + wn_pack_units(lh[i0 + i]);
+    if (U.off[U.n] > 0) hipLaunchKernelGGL(wn_pack_kernel, dim3(U.off[U.n]), dim3(256), 0, s, ld + i0, U);
+  }
   return launch_status("vqx_weight_norm_fwd");
 }
 
