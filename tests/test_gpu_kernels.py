@@ -487,6 +487,42 @@ def test_gnbwd_epilogue_matches_standalone(glu, tile):
         assert relerr(a, b) < 2e-2, relerr(a, b)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("glu,C,T", [(True, 1024, 256), (True, 256, 200), (False, 512, 256), (False, 128, 72)])
+def test_gn_bwd_matches_torch_autograd(dtype, glu, C, T):
+    """vqx_gn_bwd (GroupNorm [+ tanh*sigmoid GLU] backward: du and the
+    per-utterance sums of du, dh*xhat and dh) against fp64 torch autograd of
+    GroupNorm(G) -> GLU on the same operands and statistics, per utterance.
+    T = 200 / 72 exercise the odd trailing row of the two-rows-in-flight loop."""
+    ops = _ops()
+    torch.manual_seed(21)
+    B = 3
+    G = 2 if glu else 1
+    u = torch.randn(B * T, C, device=DEV).to(dtype)
+    cout = C // 2 if glu else C
+    dy = torch.randn(B * T, cout, device=DEV).to(dtype)
+    gamma, beta = torch.randn(C, device=DEV) * 0.5 + 1.0, torch.randn(C, device=DEV) * 0.5
+    mr = torch.empty(B, G, 2, device=DEV)
+    ops.groupnorm_stats(u, T, G, torch.empty(B * G * 64, device=DEV), mr)
+    du = torch.empty(B * T, C, device=DEV, dtype=dtype)
+    cs, dgm, dbt = (torch.empty(B, C, device=DEV) for _ in range(3))
+    ops.gn_bwd(dy, u, du, T, G, glu, mr, gamma, beta, torch.empty(B * 32 * 4, device=DEV), cs, dgm, dbt)
+    torch.cuda.synchronize()
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    for b in range(B):
+        ub = u[b * T:(b + 1) * T].double().cpu().requires_grad_(True)
+        gm = gamma.double().cpu().requires_grad_(True)
+        bt = beta.double().cpu().requires_grad_(True)
+        h = F.group_norm(ub.t().unsqueeze(0), G, gm, bt, eps=1e-5)[0].t()
+        h.retain_grad()
+        out = torch.tanh(h[:, :C // 2]) * torch.sigmoid(h[:, C // 2:]) if glu else h
+        out.backward(dy[b * T:(b + 1) * T].double().cpu())
+        assert relerr(du[b * T:(b + 1) * T], ub.grad) < tol, (b, relerr(du[b * T:(b + 1) * T], ub.grad))
+        assert relerr(cs[b], ub.grad.sum(0)) < tol
+        assert relerr(dgm[b], gm.grad) < tol
+        assert relerr(dbt[b], bt.grad) < tol
+
+
 @pytest.mark.parametrize("mode", ["fwd", "dgrad"])
 @pytest.mark.parametrize("n_utt,T,cin,cout", [(1, 128, 512, 512), (3, 128, 512, 1024), (2, 256, 1024, 512),
                                                (1, 384, 128, 512), (2, 256, 512, 80)])

@@ -648,24 +648,75 @@ __global__ __launch_bounds__(256) void gn_bwd_reduce_vec_kernel(const T* __restr
 
 // pass 2 (vectorised): du and per-(utterance, channel) sums of du (bias /
 // conv_cond gradients), dh*xhat (dgamma) and dh (dbeta).  Block = one
-// utterance x 8 channel chunks x all T rows (32 row groups), so the per-
-// utterance sums are complete inside the block (deterministic, no atomics).
+// utterance x 64 channels x all T rows, so the per-utterance sums are complete
+// inside the block (deterministic, no atomics).  A thread owns 4 channels
+// (8-B bf16 / 16-B fp32 accesses; 16 lanes cover a 64-channel row segment)
+// in one of 32 row groups and loads two rows before the math of either: the
+// kernel is bound by the loads in flight per CU, and 4 channels a thread keep
+// it at ~100 VGPRs (8 channels: 176, two waves per SIMD).
+constexpr int kGnApplyRG = 32, kGnApplyW = 4;
+template <typename T> struct Vec4;
+template <> struct Vec4<bf16_t> {
+  __device__ static __forceinline__ void load(const bf16_t* p, float* f) {
+    const uint2 u = *(const uint2*)p;
+    f[0] = __uint_as_float(u.x << 16); f[1] = __uint_as_float(u.x & 0xffff0000u);
+    f[2] = __uint_as_float(u.y << 16); f[3] = __uint_as_float(u.y & 0xffff0000u);
+  }
+  __device__ static __forceinline__ void store(bf16_t* p, const float* f) {
+    *(uint2*)p = make_uint2(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]));
+  }
+};
+template <> struct Vec4<float> : Vec<float> {};
 template <typename T>
-__global__ __launch_bounds__(256) void gn_bwd_apply_vec_kernel(const T* __restrict__ dy, int lddy,
+__device__ __forceinline__ void gn_row_load(const T* dy, int lddy, const T* u, int ldu, int64_t n, int c, int half,
+                                            bool glu, float (&g)[kGnApplyW], float (&ua)[kGnApplyW],
+                                            float (&ub)[kGnApplyW]) {
+  Vec4<T>::load(dy + n * lddy + c, g);
+  Vec4<T>::load(u + n * ldu + c, ua);
+  if (glu) Vec4<T>::load(u + n * ldu + c + half, ub);
+}
+template <typename T>
+__device__ __forceinline__ void gn_row_math(const float* g, const float* ua, const float* ub, bool glu,
+                                            const float* mr4, const float* ga, const float* ba, const float* gb,
+                                            const float* bb, float* dha, float* xa, float* dhb, float* xb) {
+  constexpr int W = kGnApplyW;
+  if (!glu) {
+#pragma unroll
+    for (int i = 0; i < W; ++i) { dha[i] = g[i]; xa[i] = (ua[i] - mr4[0]) * mr4[1]; }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    const float xha = (ua[i] - mr4[0]) * mr4[1];
+    const float xhb = (ub[i] - mr4[2]) * mr4[3];
+    const float ha = xha * ga[i] + ba[i];
+    const float hb = xhb * gb[i] + bb[i];
+    const float ta = ftanh<sizeof(T) == 2>(ha);
+    const float sb = fsigmoid<sizeof(T) == 2>(hb);
+    dha[i] = g[i] * sb * (1.f - ta * ta);
+    dhb[i] = g[i] * ta * (sb * (1.f - sb));
+    xa[i] = xha;
+    xb[i] = xhb;
+  }
+}
+template <typename T, bool GLU>
+__global__ __launch_bounds__(512) void gn_bwd_apply_vec_kernel(const T* __restrict__ dy, int lddy,
                                                                const T* __restrict__ u, int ldu, T* __restrict__ du,
-                                                               int lddu, int T_, int C, int G, int glu, int cpr,
+                                                               int lddu, int T_, int C, int G, int, int cpr,
                                                                const float* __restrict__ mr,
                                                                const float* __restrict__ gamma,
                                                                const float* __restrict__ beta,
                                                                const float* __restrict__ part, int nparts,
                                                                int pstride, float* __restrict__ colsum_b,
                                                                float* __restrict__ dgamma_b, float* __restrict__ dbeta_b) {
-  constexpr int V = Vec<T>::N;
+  constexpr bool glu = GLU;
+  constexpr int W = kGnApplyW, RG = kGnApplyRG;
+  const int cpw = cpr * (Vec<T>::N / W);  // W-channel chunks per half row
   const int b = blockIdx.y;
-  const int ch = blockIdx.x * 8 + (threadIdx.x & 7), rg = threadIdx.x >> 3;
-  const bool active = ch < cpr;
+  const int ch = blockIdx.x * 16 + (threadIdx.x & 15), rg = threadIdx.x >> 4;
+  const bool active = ch < cpw;
   const int half = C / 2;
-  const int c = ch * V;
+  const int c = ch * W;
   const float* mr4 = mr + (int64_t)b * G * 2;
   const int ng = glu ? 2 : 1;
   float m1a = 0.f, m2a = 0.f, m1b = 0.f, m2b = 0.f;
@@ -681,55 +732,76 @@ __global__ __launch_bounds__(256) void gn_bwd_apply_vec_kernel(const T* __restri
     }
     m1a = S1a / M; m2a = S2a / M; m1b = S1b / M; m2b = S2b / M;
   }
-  float a_du[2][V], a_dg[2][V], a_db[2][V];
+  float ga[W], ba[W], gb[W], bb[W];
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    ga[i] = active ? gamma[c + i] : 0.f;
+    ba[i] = active ? beta[c + i] : 0.f;
+    gb[i] = active && glu ? gamma[c + half + i] : 0.f;
+    bb[i] = active && glu ? beta[c + half + i] : 0.f;
+  }
+  float a_du[2][W], a_dg[2][W], a_db[2][W];
 #pragma unroll
   for (int s = 0; s < 2; ++s)
 #pragma unroll
-    for (int i = 0; i < V; ++i) { a_du[s][i] = 0.f; a_dg[s][i] = 0.f; a_db[s][i] = 0.f; }
+    for (int i = 0; i < W; ++i) { a_du[s][i] = 0.f; a_dg[s][i] = 0.f; a_db[s][i] = 0.f; }
+  auto row = [&](int64_t n, const float* g, const float* ua, const float* ub) {
+    float dha[W], xa[W], dhb[W], xb[W], oa[W];
+    gn_row_math<T>(g, ua, ub, glu, mr4, ga, ba, gb, bb, dha, xa, dhb, xb);
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+      oa[i] = mr4[1] * (ga[i] * dha[i] - m1a - xa[i] * m2a);
+      a_du[0][i] += oa[i];
+      a_dg[0][i] = fmaf(dha[i], xa[i], a_dg[0][i]);
+      a_db[0][i] += dha[i];
+    }
+    Vec4<T>::store(du + n * lddu + c, oa);
+    if (glu) {
+      float ob[W];
+#pragma unroll
+      for (int i = 0; i < W; ++i) {
+        ob[i] = mr4[3] * (gb[i] * dhb[i] - m1b - xb[i] * m2b);
+        a_du[1][i] += ob[i];
+        a_dg[1][i] = fmaf(dhb[i], xb[i], a_dg[1][i]);
+        a_db[1][i] += dhb[i];
+      }
+      Vec4<T>::store(du + n * lddu + c + half, ob);
+    }
+  };
   if (active) {
-    for (int r = rg; r < T_; r += 32) {
-      const int64_t n = (int64_t)b * T_ + r;
-      float dha[V], xa[V], dhb[V], xb[V];
-      gn_dh_chunk<T>(dy, lddy, u, ldu, n, c, half, glu, mr4, gamma, beta, dha, xa, dhb, xb);
-      float oa[V];
-#pragma unroll
-      for (int i = 0; i < V; ++i) {
-        oa[i] = mr4[1] * (gamma[c + i] * dha[i] - m1a - xa[i] * m2a);
-        a_du[0][i] += oa[i];
-        a_dg[0][i] = fmaf(dha[i], xa[i], a_dg[0][i]);
-        a_db[0][i] += dha[i];
-      }
-      Vec<T>::store(du + n * lddu + c, oa);
-      if (glu) {
-        float ob[V];
-#pragma unroll
-        for (int i = 0; i < V; ++i) {
-          ob[i] = mr4[3] * (gamma[c + half + i] * dhb[i] - m1b - xb[i] * m2b);
-          a_du[1][i] += ob[i];
-          a_dg[1][i] = fmaf(dhb[i], xb[i], a_dg[1][i]);
-          a_db[1][i] += dhb[i];
-        }
-        Vec<T>::store(du + n * lddu + c + half, ob);
-      }
+    int r = rg;
+    for (; r + RG < T_; r += 2 * RG) {
+      const int64_t n0 = (int64_t)b * T_ + r, n1 = n0 + RG;
+      float g0[W], ua0[W], ub0[W], g1[W], ua1[W], ub1[W];
+      gn_row_load<T>(dy, lddy, u, ldu, n0, c, half, glu, g0, ua0, ub0);
+      gn_row_load<T>(dy, lddy, u, ldu, n1, c, half, glu, g1, ua1, ub1);
+      row(n0, g0, ua0, ub0);
+      row(n1, g1, ua1, ub1);
+    }
+    if (r < T_) {
+      const int64_t n0 = (int64_t)b * T_ + r;
+      float g0[W], ua0[W], ub0[W];
+      gn_row_load<T>(dy, lddy, u, ldu, n0, c, half, glu, g0, ua0, ub0);
+      row(n0, g0, ua0, ub0);
     }
   }
-  __shared__ float lds[32][8][2 * V];
-  auto dump = [&](const float (&a)[2][V], float* out) {
+  __shared__ float lds[RG][16][2 * W];
+  auto dump = [&](const float (&a)[2][W], float* out) {
     __syncthreads();
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int i = 0; i < V; ++i) lds[rg][threadIdx.x & 7][s * V + i] = a[s][i];
+      for (int i = 0; i < W; ++i) lds[rg][threadIdx.x & 15][s * W + i] = a[s][i];
     __syncthreads();
-    // 256 threads finish 8 chunks x 2 halves x V columns
-    for (int e = threadIdx.x; e < 8 * 2 * V; e += 256) {
-      const int cl = e / (2 * V), rem = e - cl * 2 * V, s = rem / V, i = rem - s * V;
-      const int chg = blockIdx.x * 8 + cl;
-      if (chg >= cpr || s >= ng || !out) continue;
+    // 128 threads finish 16 chunks x 2 halves x W columns
+    for (int e = threadIdx.x; e < 16 * 2 * W; e += 512) {
+      const int cl = e / (2 * W), rem = e - cl * 2 * W, s = rem / W, i = rem - s * W;
+      const int chg = blockIdx.x * 16 + cl;
+      if (chg >= cpw || s >= ng || !out) continue;
       float t = 0.f;
 #pragma unroll
-      for (int q = 0; q < 32; ++q) t += lds[q][cl][rem];
-      out[(int64_t)b * C + chg * V + s * half + i] = t;
+      for (int q = 0; q < RG; ++q) t += lds[q][cl][rem];
+      out[(int64_t)b * C + chg * W + s * half + i] = t;
     }
   };
   dump(a_du, colsum_b);
@@ -785,19 +857,35 @@ __global__ __launch_bounds__(256) void gn_glu_fwd_vec_kernel(const T* __restrict
   float ga[V], ba[V], gb[V], bb[V];
 #pragma unroll
   for (int i = 0; i < V; ++i) { ga[i] = gamma[c + i]; ba[i] = beta[c + i]; gb[i] = gamma[c + half + i]; bb[i] = beta[c + half + i]; }
-  for (int r = blockIdx.x * 16 + rs; r < min(n_rows, blockIdx.x * 16 + 16); r += nrs) {
+  auto row = [&](int r, const float* ua, const float* ub) {
     const int b = r / T_;
     float ma, ra, mb, rb;
     if (tiles) { ma = smr[0]; ra = smr[1]; mb = smr[2]; rb = smr[3]; }
     else { ma = mr[4 * b + 0]; ra = mr[4 * b + 1]; mb = mr[4 * b + 2]; rb = mr[4 * b + 3]; }
-    float ua[V], ub[V], o[V];
-    Vec<T>::load(u + (int64_t)r * ldu + c, ua);
-    Vec<T>::load(u + (int64_t)r * ldu + c + half, ub);
+    float o[V];
 #pragma unroll
     for (int i = 0; i < V; ++i)
       o[i] = ftanh<sizeof(T) == 2>((ua[i] - ma) * ra * ga[i] + ba[i]) *
              fsigmoid<sizeof(T) == 2>((ub[i] - mb) * rb * gb[i] + bb[i]);
     Vec<T>::store(g + (int64_t)r * ldg + c, o);
+  };
+  // two rows' loads in flight before the math of either
+  const int rend = min(n_rows, blockIdx.x * 16 + 16);
+  int r = blockIdx.x * 16 + rs;
+  for (; r + nrs < rend; r += 2 * nrs) {
+    float ua0[V], ub0[V], ua1[V], ub1[V];
+    Vec<T>::load(u + (int64_t)r * ldu + c, ua0);
+    Vec<T>::load(u + (int64_t)r * ldu + c + half, ub0);
+    Vec<T>::load(u + (int64_t)(r + nrs) * ldu + c, ua1);
+    Vec<T>::load(u + (int64_t)(r + nrs) * ldu + c + half, ub1);
+    row(r, ua0, ub0);
+    row(r + nrs, ua1, ub1);
+  }
+  if (r < rend) {
+    float ua0[V], ub0[V];
+    Vec<T>::load(u + (int64_t)r * ldu + c, ua0);
+    Vec<T>::load(u + (int64_t)r * ldu + c + half, ub0);
+    row(r, ua0, ub0);
   }
 }
 
@@ -1640,10 +1728,12 @@ extern "C" int vqx_gn_bwd(const void* dy, int32_t lddy, const void* u, int32_t l
   const int np = nparts ? nparts : kGnBwdParts, ps = nparts ? 4 : G * 2;
   if (dtype == VQX_BF16) {
     if (!nparts) hipLaunchKernelGGL(gn_bwd_reduce_vec_kernel<bf16_t>, dim3(kGnBwdParts, B), dim3(256), 0, s, (const bf16_t*)dy, lddy, (const bf16_t*)u, ldu, T, C, G, glu, cpr, mean_rstd, gamma, beta, partials);
-    hipLaunchKernelGGL(gn_bwd_apply_vec_kernel<bf16_t>, dim3((cpr + 7) / 8, B), dim3(256), 0, s, (const bf16_t*)dy, lddy, (const bf16_t*)u, ldu, (bf16_t*)du, lddu, T, C, G, glu, cpr, mean_rstd, gamma, beta, partials, np, ps, colsum_p, dgamma_p, dbeta_p);
+    auto* kfn = glu ? gn_bwd_apply_vec_kernel<bf16_t, true> : gn_bwd_apply_vec_kernel<bf16_t, false>;
+    hipLaunchKernelGGL(kfn, dim3((cpr * 2 + 15) / 16, B), dim3(512), 0, s, (const bf16_t*)dy, lddy, (const bf16_t*)u, ldu, (bf16_t*)du, lddu, T, C, G, glu, cpr, mean_rstd, gamma, beta, partials, np, ps, colsum_p, dgamma_p, dbeta_p);
   } else {
     if (!nparts) hipLaunchKernelGGL(gn_bwd_reduce_vec_kernel<float>, dim3(kGnBwdParts, B), dim3(256), 0, s, (const float*)dy, lddy, (const float*)u, ldu, T, C, G, glu, cpr, mean_rstd, gamma, beta, partials);
-    hipLaunchKernelGGL(gn_bwd_apply_vec_kernel<float>, dim3((cpr + 7) / 8, B), dim3(256), 0, s, (const float*)dy, lddy, (const float*)u, ldu, (float*)du, lddu, T, C, G, glu, cpr, mean_rstd, gamma, beta, partials, np, ps, colsum_p, dgamma_p, dbeta_p);
+    auto* kfn = glu ? gn_bwd_apply_vec_kernel<float, true> : gn_bwd_apply_vec_kernel<float, false>;
+    hipLaunchKernelGGL(kfn, dim3((cpr + 15) / 16, B), dim3(512), 0, s, (const float*)dy, lddy, (const float*)u, ldu, (float*)du, lddu, T, C, G, glu, cpr, mean_rstd, gamma, beta, partials, np, ps, colsum_p, dgamma_p, dbeta_p);
   }
   return launch_status("vqx_gn_bwd");
 }
