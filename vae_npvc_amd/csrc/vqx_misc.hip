@@ -226,41 +226,60 @@ __global__ __launch_bounds__(256) void wn_pack_kernel(const vqx_wn_layer* __rest
   }
 }
 
-// a[0..NF-1] = partial sums over splits sp0, sp0+step, ... < splits of the 4
-// slab values at element offset p (slab stride `ss`), NF loads in flight
-#ifndef VQX_WN_NF  // 4 measured best: 8 -> 22.0, 16 -> 59 us per launch (registers, occupancy)
+// Sum over splits sp0, sp0+step, ... < splits of the 4 slab values at element
+// offset p (slab stride `ss`): NF loads issued before any add, added in split
+// order into one accumulator (fixed order: deterministic).
+#ifndef VQX_WN_NF  // loads in flight per thread
 #define VQX_WN_NF 4
 #endif
-#ifndef VQX_WN_VPRE  // 1: the row of v is loaded into registers before the slabs
-#define VQX_WN_VPRE 1
-#endif
-#ifndef VQX_WN_OCC  // minimum workgroups per CU requested from the register allocator (0 = none)
-#define VQX_WN_OCC 0
+#ifndef VQX_WN_THREADS  // threads per row block: the slab stream is bound by the loads in flight per CU
+#define VQX_WN_THREADS 256
 #endif
 constexpr int kWnNF = VQX_WN_NF;
+constexpr int kWnThreads = VQX_WN_THREADS;
 template <bool BF>
-__device__ __forceinline__ void slab_sum8(const void* slabs, int64_t p, int64_t ss, int sp0, int step, int splits,
-                                          f32x4_t (&a)[kWnNF]) {
-  auto ld4 = [&](int64_t i) -> f32x4_t {
-    if constexpr (BF) {
-      const uint2 u = *(const uint2*)((const unsigned short*)slabs + i);
-      return {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
-              __uint_as_float(u.y & 0xffff0000u)};
-    } else {
-      return *(const f32x4_t*)((const float*)slabs + i);
-    }
+__device__ __forceinline__ f32x4_t slab_sum(const void* slabs, int64_t p, int64_t ss, int sp0, int step, int splits) {
+  typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+  auto cvt = [](u32x2_t u) -> f32x4_t {
+    return {__uint_as_float(u[0] << 16), __uint_as_float(u[0] & 0xffff0000u), __uint_as_float(u[1] << 16),
+            __uint_as_float(u[1] & 0xffff0000u)};
   };
-#pragma unroll
-  for (int u = 0; u < kWnNF; ++u) a[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
   int sp = sp0;
-  for (; sp + (kWnNF - 1) * step < splits; sp += kWnNF * step) {
+  if constexpr (BF) {
+    const unsigned short* sl = (const unsigned short*)slabs;
+    for (; sp + (kWnNF - 1) * step < splits; sp += kWnNF * step) {
+      u32x2_t t[kWnNF];
+#pragma unroll
+      for (int u = 0; u < kWnNF; ++u) t[u] = *(const u32x2_t*)(sl + p + (int64_t)(sp + u * step) * ss);
+#pragma unroll
+      for (int u = 0; u < kWnNF; ++u) acc += cvt(t[u]);
+    }
+    u32x2_t t[kWnNF];
+#pragma unroll
+    for (int u = 0; u < kWnNF - 1; ++u)
+      if (sp + u * step < splits) t[u] = *(const u32x2_t*)(sl + p + (int64_t)(sp + u * step) * ss);
+#pragma unroll
+    for (int u = 0; u < kWnNF - 1; ++u)
+      if (sp + u * step < splits) acc += cvt(t[u]);
+  } else {
+    const float* sl = (const float*)slabs;
+    for (; sp + (kWnNF - 1) * step < splits; sp += kWnNF * step) {
+      f32x4_t t[kWnNF];
+#pragma unroll
+      for (int u = 0; u < kWnNF; ++u) t[u] = *(const f32x4_t*)(sl + p + (int64_t)(sp + u * step) * ss);
+#pragma unroll
+      for (int u = 0; u < kWnNF; ++u) acc += t[u];
+    }
     f32x4_t t[kWnNF];
 #pragma unroll
-    for (int u = 0; u < kWnNF; ++u) t[u] = ld4(p + (int64_t)(sp + u * step) * ss);
+    for (int u = 0; u < kWnNF - 1; ++u)
+      if (sp + u * step < splits) t[u] = *(const f32x4_t*)(sl + p + (int64_t)(sp + u * step) * ss);
 #pragma unroll
-    for (int u = 0; u < kWnNF; ++u) a[u] += t[u];
+    for (int u = 0; u < kWnNF - 1; ++u)
+      if (sp + u * step < splits) acc += t[u];
   }
-  for (int u = 0; sp < splits; sp += step, ++u) a[u % kWnNF] += ld4(p + (int64_t)sp * ss);
+  return acc;
 }
 
 // Backward per weight-norm row o.  slabs[s][o][x] with x = j*cin+ci (Conv1d,
@@ -268,35 +287,103 @@ __device__ __forceinline__ void slab_sum8(const void* slabs, int64_t p, int64_t 
 // The split-K slabs (fp32, or bf16 in bf16 runs) are summed in fp32 with
 // 16-B (8-B) loads, several splits in flight per thread, scattered into the
 // row's (c, j) order in LDS, then the norm gradient is formed from LDS and the
-// row of v held in registers.
-constexpr int kWnVRegs = 16;  // v row values per thread (row length <= 4096, 256 threads)
-#if VQX_WN_OCC > 0
-#define VQX_WN_BOUNDS __launch_bounds__(256, VQX_WN_OCC)
-#else
-#define VQX_WN_BOUNDS __launch_bounds__(256)
-#endif
-__global__ VQX_WN_BOUNDS void wn_bwd_kernel(const vqx_wn_layer* __restrict__ L, int n_layers) {
-  const vqx_wn_layer& l = L[blockIdx.y];
-  if (l.kind == VQX_WN_COLREDUCE) {  // dv[c] = sum_r v[r][c]: bias / affine gradients from partials
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= l.cout) return;
-    const float* p = l.v + c;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    int r = 0;
-    for (; r + 4 <= l.cin; r += 4) {
-      a0 += p[(int64_t)r * l.cout];
-      a1 += p[(int64_t)(r + 1) * l.cout];
-      a2 += p[(int64_t)(r + 2) * l.cout];
-      a3 += p[(int64_t)(r + 3) * l.cout];
+// row of v held in registers.  One kWnThreads-thread block per row over a flat
+// grid of every layer's rows (WnUnits): the big layers have only 512-640 rows,
+// so the block -- not the grid -- must carry the loads in flight.
+constexpr int kWnVRegs = 4096 / kWnThreads;  // v row values per thread (row length <= 4096)
+constexpr int kWnCrCols = 32;  // columns per column-reduce block
+constexpr int kWnWaveX4 = 4;   // 16-B column groups per lane on the wave-per-row path (rows <= 1024 columns)
+// wave-per-row path: Conv1d 1x1 rows of <= 1024 columns whose split sums are
+// at most one round of loads per lane
+__host__ __device__ inline bool wn_bwd_wave_rows(const vqx_wn_layer& l) {
+  return l.kind == 0 && l.k == 1 && l.cin <= 64 * 4 * kWnWaveX4 && (l.cin / 4) * l.splits <= 64 * kWnNF;
+}
+__global__ __launch_bounds__(kWnThreads) void wn_bwd_kernel(const vqx_wn_layer* __restrict__ L, WnUnits U) {
+  int lo = 0, hi = U.n - 1;  // the layer owning this block
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (U.off[mid] <= (int)blockIdx.x) lo = mid; else hi = mid - 1;
+  }
+  const vqx_wn_layer& l = L[lo];
+  const int unit = (int)blockIdx.x - U.off[lo];
+  if (l.kind == VQX_WN_COLREDUCE) {
+    // dv[c] = sum_r v[r][c] (bias / affine gradients from per-tile partials):
+    // block = kWnCrCols columns x kWnCrRG row groups, row group g summing rows
+    // g, g + kWnCrRG, ... (8 loads in flight), then the groups in order
+    // through LDS -- a fixed order, deterministic.
+    constexpr int CC = kWnCrCols, RG = kWnThreads / kWnCrCols;
+    __shared__ float crs[RG][CC];
+    const int cl = threadIdx.x % CC, g = threadIdx.x / CC;
+    const int c = unit * CC + cl;
+    float a = 0.f;
+    if (c < l.cout) {
+      const float* p = l.v + c;
+      int r = g;
+      for (; r + 7 * RG < l.cin; r += 8 * RG) {
+        float t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = p[(int64_t)(r + u * RG) * l.cout];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a += t[u];
+      }
+      for (; r < l.cin; r += RG) a += p[(int64_t)r * l.cout];
     }
-    for (; r < l.cin; ++r) a0 += p[(int64_t)r * l.cout];
-    l.dv[c] = (a0 + a1) + (a2 + a3);
+    crs[g][cl] = a;
+    __syncthreads();
+    if (g == 0 && c < l.cout) {
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < RG; ++q) t += crs[q][cl];
+      l.dv[c] = t;
+    }
+    return;
+  }
+  if (wn_bwd_wave_rows(l)) {
+    // short 1x1 rows with little split-K work (the speaker-conditioning
+    // linears: 128 columns, dW written directly): one wave per row, the row's
+    // sums held in registers, wave reductions only (no LDS, no barriers)
+    const int o = unit * (kWnThreads / 64) + (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (o >= l.cout) return;
+    const int cols = l.cin, nx4 = cols / 4;
+    const int64_t ss = (int64_t)l.cout * cols, srow = (int64_t)o * cols;
+    const bool sbf = l.slab_dtype == VQX_BF16;
+    const float* vrow = l.v + (int64_t)o * cols;
+    float* dv = l.dv + (int64_t)o * cols;
+    f32x4_t sm[kWnWaveX4], vv[kWnWaveX4];
+    float dot = 0.f;
+#pragma unroll
+    for (int u = 0; u < kWnWaveX4; ++u) {
+      const int x4 = lane + 64 * u;
+      if (x4 < nx4) {
+        vv[u] = l.g ? *(const f32x4_t*)(vrow + 4 * x4) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+        sm[u] = sbf ? slab_sum<true>(l.slabs, srow + 4 * x4, ss, 0, 1, l.splits)
+                    : slab_sum<false>(l.slabs, srow + 4 * x4, ss, 0, 1, l.splits);
+        dot = fmaf(sm[u][0], vv[u][0], fmaf(sm[u][1], vv[u][1], fmaf(sm[u][2], vv[u][2], fmaf(sm[u][3], vv[u][3], dot))));
+      }
+    }
+    if (!l.g) {
+#pragma unroll
+      for (int u = 0; u < kWnWaveX4; ++u)
+        if (lane + 64 * u < nx4) *(f32x4_t*)(dv + 4 * (lane + 64 * u)) = sm[u];
+      return;
+    }
+    dot = wave_sum(dot);
+    const float nrm = l.norm[o];
+    const float dg = dot / nrm;
+    if (lane == 0) l.dg[o] = dg;
+    const float sc = l.g[o] / nrm, t = dg / nrm;
+#pragma unroll
+    for (int u = 0; u < kWnWaveX4; ++u)
+      if (lane + 64 * u < nx4)
+        *(f32x4_t*)(dv + 4 * (lane + 64 * u)) =
+            f32x4_t{sc * (sm[u][0] - vv[u][0] * t), sc * (sm[u][1] - vv[u][1] * t), sc * (sm[u][2] - vv[u][2] * t),
+                    sc * (sm[u][3] - vv[u][3] * t)};
     return;
   }
   const bool rsm = l.kind == VQX_WN_RESAMPLE || l.kind == VQX_WN_RESAMPLE_T;
   const bool row_is_cout = l.kind == 0 || l.kind == VQX_WN_RESAMPLE;
   const int rows = row_is_cout ? l.cout : l.cin;
-  const int o = blockIdx.x;
+  const int o = unit;
   if (o >= rows) return;
   const int other = row_is_cout ? l.cin : l.cout;  // multiple of 4 (host-checked)
   const int K = l.k;
@@ -312,10 +399,10 @@ __global__ VQX_WN_BOUNDS void wn_bwd_kernel(const vqx_wn_layer* __restrict__ L, 
   // the row of v, loaded before the slabs so both latencies overlap (cols <= 4096, 256 threads)
   float vr[kWnVRegs];
   const float* vrow = l.v + (int64_t)o * cols;
-  if (VQX_WN_VPRE) {
+  {
 #pragma unroll
     for (int u = 0; u < kWnVRegs; ++u) {
-      const int i = threadIdx.x + u * 256;
+      const int i = threadIdx.x + u * kWnThreads;
       vr[u] = (l.g && i < cols) ? vrow[i] : 0.f;
     }
   }
@@ -328,18 +415,14 @@ __global__ VQX_WN_BOUNDS void wn_bwd_kernel(const vqx_wn_layer* __restrict__ L, 
   const int nx4 = scols / 4;
   const int G = nx4 >= (int)blockDim.x ? 1 : min(splits, (int)blockDim.x / nx4);
   const int gidx = threadIdx.x / nx4;  // split group (G == 1: every thread is group 0)
-  f32x4_t* part = (f32x4_t*)dw;        // [G][nx4] partials (G > 1 only: nx4 * G <= 256 -> 4 KiB)
+  f32x4_t* part = (f32x4_t*)dw;        // [G][nx4] partials (G > 1 only: nx4 * G <= kWnThreads -> <= 16 KiB)
   // G == 1: x4 = t, t + 256, ...;  G > 1: the one group x4 = t % nx4 (threads with gidx >= G idle)
   const int x4_0 = G == 1 ? (int)threadIdx.x : ((int)threadIdx.x % nx4 + (gidx < G ? 0 : nx4));
   for (int x4 = x4_0; x4 < nx4; x4 += (G == 1 ? (int)blockDim.x : nx4)) {
     const int64_t p = srow + 4 * x4;
     const int sp0 = G > 1 ? gidx : 0, step = G > 1 ? G : 1;
-    f32x4_t a[kWnNF];
-    if (sbf) slab_sum8<true>(l.slabs, p, slab_stride, sp0, step, splits, a);
-    else slab_sum8<false>(l.slabs, p, slab_stride, sp0, step, splits, a);
-    f32x4_t sum = a[0];
-#pragma unroll
-    for (int u = 1; u < kWnNF; ++u) sum += a[u];
+    const f32x4_t sum = sbf ? slab_sum<true>(l.slabs, p, slab_stride, sp0, step, splits)
+                            : slab_sum<false>(l.slabs, p, slab_stride, sp0, step, splits);
     if (G > 1) {
       part[gidx * nx4 + x4] = sum;
       continue;
@@ -393,8 +476,7 @@ __global__ VQX_WN_BOUNDS void wn_bwd_kernel(const vqx_wn_layer* __restrict__ L, 
   float dot = 0.f;
 #pragma unroll
   for (int u = 0; u < kWnVRegs; ++u) {
-    const int i = threadIdx.x + u * 256;
-    if (!VQX_WN_VPRE && i < cols) vr[u] = vrow[i];
+    const int i = threadIdx.x + u * kWnThreads;
     if (i < cols) dot = fmaf(dw[i], vr[u], dot);
   }
   dot = block_sum(dot, red);
@@ -405,7 +487,7 @@ __global__ VQX_WN_BOUNDS void wn_bwd_kernel(const vqx_wn_layer* __restrict__ L, 
   const float sc = gg / nrm, t = dg / nrm;
 #pragma unroll
   for (int u = 0; u < kWnVRegs; ++u) {
-    const int i = threadIdx.x + u * 256;
+    const int i = threadIdx.x + u * kWnThreads;
     if (i < cols) dv[i] = sc * (dw[i] - vr[u] * t);
   }
 }
@@ -1619,7 +1701,21 @@ extern "C" int vqx_weight_norm_bwd(const vqx_wn_layer* lh, const vqx_wn_layer* l
     if (l.slab_dtype != VQX_F32 && l.slab_dtype != VQX_BF16) { set_error("vqx_weight_norm_bwd: layer %d: slab_dtype %d", i, l.slab_dtype); return -1; }
     max_rows = rows > max_rows ? rows : max_rows;
   }
-  hipLaunchKernelGGL(wn_bwd_kernel, dim3(max_rows, n_layers), dim3(256), 0, (hipStream_t)stream, ld, n_layers);
+  (void)max_rows;
+  for (int i0 = 0; i0 < n_layers; i0 += kWnMaxL) {  // flat grid over the layers' rows, kWnMaxL layers a launch
+    WnUnits U;
+    U.n = n_layers - i0 < kWnMaxL ? n_layers - i0 : kWnMaxL;
+    U.off[0] = 0;
+    for (int i = 0; i < U.n; ++i) {
+      const vqx_wn_layer& l = lh[i0 + i];
+      const int units = l.kind == VQX_WN_COLREDUCE ? (l.cout + kWnCrCols - 1) / kWnCrCols
+                        : wn_bwd_wave_rows(l) ? (l.cout + kWnThreads / 64 - 1) / (kWnThreads / 64)
+                        : (l.kind == 0 || l.kind == VQX_WN_RESAMPLE) ? l.cout : l.cin;
+      U.off[i + 1] = U.off[i] + units;
+    }
+    if (U.off[U.n] > 0)
+      hipLaunchKernelGGL(wn_bwd_kernel, dim3(U.off[U.n]), dim3(kWnThreads), 0, (hipStream_t)stream, ld + i0, U);
+  }
   return launch_status("vqx_weight_norm_bwd");
 }
 
