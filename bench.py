@@ -88,29 +88,36 @@ def launch_ranks(n):
 
 
 def time_vq(tr, reps):
-    """The fused VQ kernel (distance, argmin, gather, commitment, EMA
-    statistics; vqx_vq_forward) re-launched `reps` times on the step's own
-    workspace (N = 16,384 frames, K codes, D = 128), timed with events on the
-    stream it runs on.  Algorithmic bytes: z (N*D f32) + E (K*D f32) + idx
-    (N int64) = 536 B/frame + E; FLOPs 2*N*K*D."""
+    """The VQ distance kernel (distance, argmin, gather, commitment partials +
+    their ordered sum; vqx_vq_forward without statistics) re-launched `reps`
+    times on the step's own workspace (N = 16,384 frames, K codes, D = 128),
+    timed with events on the stream it runs on; `us_with_stats` adds the EMA
+    statistics (sort + segmented sums) as the step runs them.  Algorithmic
+    bytes: z (N*D f32) + E (K*D f32) + idx (N int64) = 536 B/frame + E
+    (SURVEY §8d); FLOPs 2*N*K*D."""
     from vae_npvc_amd import ops
     eng = tr.engine
     w = eng._ws[(B_PER_GPU, T_FRAMES, True)]
     q = tr.model.quantizer
     N, D, K = w.Nz, eng.dims["Z"], eng.dims["K"]
-    args = (w.z, q.embeddings, w.idx, w.zq, w.zq_c, w.stats[1:2], w.vq_part, w.bsum, w.bcnt)
-    for _ in range(3):
-        ops.vq_forward(*args)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        ops.vq_forward(*args)
-    e1.record()
-    e1.synchronize()
-    t = e0.elapsed_time(e1) * 1e-3 / reps
+    base = (w.z, q.embeddings, w.idx, w.zq, w.zq_c, w.stats[1:2], w.vq_part)
+
+    def timed(args):
+        for _ in range(3):
+            ops.vq_forward(*args)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            ops.vq_forward(*args)
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) * 1e-3 / reps
+    t = timed(base)
+    t_stats = timed(base + (w.bsum, w.bcnt))
     nbytes = N * D * 4 + K * D * 4 + N * 8
     flops = 2.0 * N * K * D
-    return {"kernel": "vqx::vq_forward_kernel", "us": round(t * 1e6, 2), "bytes": nbytes, "flops": flops,
+    return {"kernel": "vqx::vq_forward_kernel", "us": round(t * 1e6, 2), "us_with_stats": round(t_stats * 1e6, 2),
+            "bytes": nbytes, "flops": flops,
             "hbm_GBps": round(nbytes / t / 1e9, 1), "hbm_frac": round(nbytes / t / HBM_PEAK, 4),
             "tflops": round(flops / t / 1e12, 2), "mfma_f32_frac": round(flops / t / PEAK_F32, 4),
             "roofline_frac": round(max(nbytes / HBM_PEAK, flops / PEAK_F32) / t, 4),

@@ -162,7 +162,8 @@ def test_fp32_general_topology_matches_reference_golden(name):
     Bars as the single-stage golden tests: losses 1e-4 at step 1 and 1e-3
     later (the perplexity 2e-2), indices equal except at the reference's
     near-ties, step-1 gradient norms 1e-5 (measured <= 6.2e-7 on every
-    parameter, tools/grad_err_probe.py), parameters after 3 steps 1e-3."""
+    parameter with EMA; 5e-4 on the straight-through encoder, as the
+    single-stage plain test), parameters after 3 steps 1e-3."""
     from oracle.vqvae_cpu import seeded_batch
     meta, arr = load_fixture(f"step_{name}")
     cfg = cfg_of(name, compute_dtype="fp32")
@@ -189,7 +190,12 @@ def test_fp32_general_topology_matches_reference_golden(name):
             for n, p in tr.model.named_parameters():
                 ref = meta["grads"][n]["norm"]
                 gn = float(eng.g(p).double().norm())
-                assert relclose(gn, ref, 1e-5, 1e-9), (n, gn, ref)
+                # straight-through quantizer: the encoder's gradient is the
+                # commitment term through z/||z||, as in
+                # test_gpu_step.test_fp32_plain_vq_steps_match_reference_golden
+                # (measured 9.5e-5 on encoder.encode.0.weight_g here)
+                tol = 5e-4 if (not ema and n.startswith("encoder.")) else 1e-5
+                assert relclose(gn, ref, tol, 1e-9), (n, gn, ref)
     for n, p in tr.model.named_parameters():
         assert relclose(float(p.detach().double().norm()), meta["params_after"][n]["norm"], 1e-3), n
 

@@ -56,6 +56,9 @@ constexpr int kBN = 128;  // tile width (and height)
 #ifndef VQX_EPI_PREFETCH_DGRAD  // 1: DGRAD epilogues prefetch their row operands too (A/B)
 #define VQX_EPI_PREFETCH_DGRAD 0
 #endif
+#ifndef VQX_EPI_PREFETCH_LATE  // n > 0: issue the row-operand prefetch at main-loop iteration nk-n, not with the prologue
+#define VQX_EPI_PREFETCH_LATE 0
+#endif
 constexpr unsigned kOOB = 0x80000000u;  // buffer offset that is always out of range -> loads 0
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 
@@ -1066,7 +1069,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
 #pragma unroll
     for (int t = 0; t < NST - 1; ++t)
       if (t < pre) dma_tile(t, t);
-    if constexpr (kPrefetch) epi_prefetch<EK>(P, m0, n0, tid, rows);  // lands with the prologue DMA
+    if constexpr (kPrefetch && VQX_EPI_PREFETCH_LATE == 0) epi_prefetch<EK>(P, m0, n0, tid, rows);  // lands with the prologue DMA
     wait_vm(NP * (pre - 1));
     __builtin_amdgcn_s_barrier();
     int buf = 0;
@@ -1075,6 +1078,11 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
 #if VQX_LAB_MODE != 1
       if (kt + NST - 1 < nk) dma_tile(fbuf, kt + NST - 1);
 #endif
+      if constexpr (kPrefetch && VQX_EPI_PREFETCH_LATE > 0) {
+        // vmcnt retires in issue order: issued after the last operand DMA, the
+        // prefetch delays no earlier K-tile's wait
+        if (kt == (nk > VQX_EPI_PREFETCH_LATE ? nk - VQX_EPI_PREFETCH_LATE : 0)) epi_prefetch<EK>(P, m0, n0, tid, rows);
+      }
 #if VQX_LAB_MODE != 2
       compute_tile(buf);
 #endif
