@@ -52,7 +52,8 @@ void gemm_launch(const void* fn, int grid, hipStream_t s, const GemmParams& P, c
 
 // vqx_set_gemm_tile: 0 = automatic, 1 = implicit-im2col kernel only,
 // 2 / 3 = tap reuse through conv_tr8_kernel with 1 / 2 frame segments where it
-// applies, 4 = tap reuse through conv_tr_kernel only
+// applies, 4 = tap reuse through conv_tr_kernel only, 5 = automatic with the
+// wide weight gradients (wgrad_tr2_kernel: 3-tap c_dim % 128 == 0, 1x1 c_dim % 256 == 0)
 static int g_gemm_policy = 0;
 
 bool tap_reuse_enabled() {
@@ -76,7 +77,7 @@ int tr8_policy() {
     const char* e = getenv("VQX_TR8");  // 0 = off, 1/2 = SEGS, unset = automatic (-1)
     return (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : -1;
   }();
-  if (g_gemm_policy >= 2) return g_gemm_policy == 4 ? 0 : g_gemm_policy - 1;
+  if (g_gemm_policy >= 2 && g_gemm_policy <= 4) return g_gemm_policy == 4 ? 0 : g_gemm_policy - 1;
   return pol;
 }
 
@@ -86,6 +87,14 @@ int wgrad_kgroups() {
     return (e && e[0] == '2') ? 2 : 1;
   }();
   return kg;
+}
+
+bool wgrad_wide() {
+  static const bool on = [] {
+    const char* e = getenv("VQX_WGRAD_WIDE");  // 1: wgrad_tr2_kernel where it applies
+    return e && e[0] == '1';
+  }();
+  return on || g_gemm_policy == 5;
 }
 
 static void launch_mode(GemmParams& P, int mode, int64_t rows, int extra_mult, bool bf16, bool gen, hipStream_t s) {
@@ -209,6 +218,13 @@ extern "C" int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream) {
   if (!gen && wgrad_tr_ok(a->n_rows, a->T, a->c_dim, a->ntaps, a->pad, dil, a->dtype == VQX_BF16, a->q_prologue)) {
     P.tap_reuse = wgrad_kgroups();
     P.tiles_n = a->c_dim / 64;
+    if (wgrad_wide() && a->c_dim % 128 == 0) {  // one 8-wave workgroup per two 64-channel tiles
+      P.tap_reuse = 3;
+      P.tiles_n = a->c_dim / 128;
+    }
+  } else if (!gen && wgrad_wide1_ok(a->n_rows, a->T, a->c_dim, a->ntaps, a->pad, a->dtype == VQX_BF16, a->q_prologue)) {
+    P.tap_reuse = 4;  // wide 1x1 kernel, 256 channels of c per workgroup
+    P.tiles_n = a->c_dim / 256;
   }
   hipStream_t s = (hipStream_t)stream;
   launch_mode(P, MODE_WGRAD, P.Mc, P.splits, a->dtype == VQX_BF16, gen, s);
@@ -232,7 +248,7 @@ extern "C" int vqx_wgrad_tiles(int64_t n_rows, int32_t T, int32_t r_dim, int32_t
 }
 
 extern "C" int vqx_set_gemm_tile(int32_t policy) {
-  if (policy < 0 || policy > 4) { set_error("vqx_set_gemm_tile: policy %d not in 0..4", policy); return -1; }
+  if (policy < 0 || policy > 5) { set_error("vqx_set_gemm_tile: policy %d not in 0..5", policy); return -1; }
   g_gemm_policy = policy;
   return 0;
 }

@@ -30,6 +30,13 @@ inline bool tap_reuse_ok(const GemmParams& P, bool bf16, bool gen) {
 // 64-frame K-tiles inside one utterance
 // K groups per tap-reuse WGRAD workgroup (default 1; env VQX_WGRAD_KG=2: two 4-wave groups)
 int wgrad_kgroups();
+// wgrad_tr2_kernel (8 waves): 3-tap layers with c_dim % 128 == 0 (128 c per
+// workgroup) and 1x1 layers with c_dim % 256 == 0 (256 c per workgroup)
+bool wgrad_wide();
+inline bool wgrad_wide1_ok(int64_t n_rows, int T, int c_dim, int ntaps, int pad, bool bf16, int pro) {
+  return bf16 && pro == VQX_PRO_NONE && ntaps == 1 && pad == 0 && c_dim % 256 == 0 && T % 64 == 0 &&
+         n_rows % 64 == 0 && wgrad_wide();
+}
 
 inline bool wgrad_tr_ok(int64_t n_rows, int T, int c_dim, int ntaps, int pad, int dil, bool bf16, int pro) {
   return bf16 && pro == VQX_PRO_NONE && ntaps == 3 && pad == 1 && dil == 1 && c_dim % 64 == 0 && T % 64 == 0 &&
@@ -119,6 +126,13 @@ void launch_mode_dt(const GemmParams& P, int grid, bool bf16, bool gen, hipStrea
     if (P.tap_reuse) {
       const double flops = 2.0 * (double)P.n_rows * P.Mc * P.Nc;
       // gen = 2: tap-reuse kernel; the prologue slot carries the K-group count
+      if (P.tap_reuse >= 3) {  // gen = 4: wide kernels, the prologue slot carries TAPS
+        const int taps = P.tap_reuse == 3 ? 3 : 1;
+        const int info4[5] = {VQX_BF16, MODE_WGRAD, taps, 4, EK_NONE};
+        if (taps == 3) gemm_launch((const void*)wgrad_tr2_kernel<3>, grid, s, P, info4, flops, 512);
+        else gemm_launch((const void*)wgrad_tr2_kernel<1>, grid, s, P, info4, flops, 512);
+        return;
+      }
       const int info[5] = {VQX_BF16, MODE_WGRAD, P.tap_reuse, 2, EK_NONE};
       if (P.tap_reuse == 2) gemm_launch((const void*)wgrad_tr_kernel<EK_NONE, 2>, grid, s, P, info, flops, 512);
       else gemm_launch((const void*)wgrad_tr_kernel<EK_NONE, 1>, grid, s, P, info, flops);

@@ -1740,4 +1740,223 @@ __global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void wgrad_tr_kernel(Gem
   }
 }
 
+// ---------------------------------------------------------------------------
+// Wide weight gradients (8 waves, one workgroup per CU).
+//
+// TAPS = 3: the same S[r][j*cd + c] as wgrad_tr_kernel over 128 rows r x
+// (3 taps x 128 channels c).  wgrad_tr_kernel stages 25 KiB (p 16 + q 9) per
+// 64-frame stage for 3.1 MFLOP, i.e. ~65 GB/s per CU of LDS-DMA fill at the
+// MFMA rate of two workgroups -- the fill rate the staging sustains.  Here the
+// 16 KiB p slice serves two 64-channel q blocks: 34 KiB per stage for
+// 6.3 MFLOP (1.5x the FLOPs per staged byte), with the waves' own work
+// unchanged (64 r x 3 taps x 32 c, 24 MFMAs per stage).  Wave w: r half
+// w & 1, 32-channel quarter w >> 1.
+//
+// TAPS = 1: the 1x1 weight gradient S[r][c] = sum_n p[n][r] q[n][c] over
+// 128 r x 256 c (conv_gemm_kernel's WGRAD stages 32 KiB per 2.1 MFLOP; here
+// 52 KiB per 8.4 MFLOP, 2.5x the FLOPs per staged byte).  Wave w: r half
+// w & 1, 64-channel q block w >> 1 (64 r x 64 c, 16 MFMAs per stage).
+//
+// Each 64-channel q block is laid out exactly as wgrad_tr_kernel's q (the
+// frames k0-1 .. k0+64 in 128-B rows, q_off128), so the tap-shifted fragment
+// reads keep its bank pattern; the 1x1 form reads the centre rows only.
+// tiles_n counts 64 * QBLK-channel blocks of c.
+template <int TAPS>
+__global__ __launch_bounds__(512, 1) void wgrad_tr2_kernel(GemmParams P) {
+  using T = bf16_t;
+  static_assert(TAPS == 1 || TAPS == 3, "TAPS");
+  constexpr int ES = 2, EPC = 8, BK = 64, NT = 512;
+  constexpr int QBLK = TAPS == 3 ? 2 : 4;       // 64-channel q blocks per workgroup
+  constexpr int NJ = TAPS == 3 ? 3 : 2;         // accumulator columns per wave (taps / 32-c halves)
+  constexpr int A_BYTES = BK * 256;             // p: 64 frames x 128 r (16 pieces)
+  constexpr int QB_PIECES = 9;                  // one q block: 66 frames (72-row capacity) x 128 B
+  constexpr int QB_BYTES = QB_PIECES * 1024;
+  constexpr int QP = QBLK * QB_PIECES;          // q pieces per stage
+  constexpr int QPW = (QP + 7) / 8;             // ... per wave (some waves one fewer)
+  constexpr int STAGE = A_BYTES + QBLK * QB_BYTES;  // 34 / 52 KiB
+  constexpr int NST = 2;
+  constexpr int EP_LD = 128 + 4;                // epilogue row pitch (floats)
+  constexpr int SMEM = NST * STAGE > 128 * EP_LD * 4 ? NST * STAGE : 128 * EP_LD * 4;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid & 1, wc = wid >> 1;                  // r half; 32-c quarter (TAPS 3) / q block (TAPS 1)
+  const int qb = TAPS == 3 ? wc >> 1 : wc;                // this wave's q block
+  const int wn = TAPS == 3 ? wc & 1 : 0;                  // 32-channel half of it (TAPS 3)
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int tiles_mn = P.tiles_m * P.tiles_n;
+  const int split = lin / tiles_mn;
+  const int tmn = lin - split * tiles_mn;
+  const int tm = tmn / P.tiles_n, tn = tmn - tm * P.tiles_n;
+  const int r0 = tm * 128, c0 = tn * (64 * QBLK);
+  const int64_t kbeg = (int64_t)split * P.k_per_split;
+  int64_t kend = kbeg + P.k_per_split;
+  if (kend > P.n_rows) kend = P.n_rows;
+  const int nk = kend > kbeg ? (int)((kend - kbeg) / BK) : 0;
+
+  // p pieces 2*wid, 2*wid+1
+  unsigned aoff[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = (2 * wid + i) * 64 + lane;
+    const int krow = c / 16, cch = (c % 16) ^ mn_swz(krow);
+    const int r = r0 + cch * EPC;
+    aoff[i] = r < P.Mc ? (unsigned)(((int64_t)krow * P.lda + r) * ES) : kOOB;
+  }
+  // q pieces wid, wid+8, ... (< QP): block pc / 9, piece pc % 9 of it; stage row sr holds frame k0-1+sr
+  unsigned boff[QPW];
+  int bedge[QPW], bdst[QPW];
+#pragma unroll
+  for (int i = 0; i < QPW; ++i) {
+    const int pc = wid + 8 * i;
+    const int blk = pc / QB_PIECES, lp = pc - blk * QB_PIECES;
+    const int c = lp * 64 + lane;
+    const int row = c / 8, ch = (c % 8) ^ (((row >> 1) & 1) << 2);
+    const int cc = c0 + blk * 64 + ch * EPC;
+    bedge[i] = row == 0 ? 1 : (row == 65 ? 2 : 0);
+    bdst[i] = A_BYTES + blk * QB_BYTES + lp * 1024;
+    // descriptor base one q row before P.b: frame k0-1+row sits at (k0+row) rows
+    boff[i] = (pc < QP && row < 66 && cc < P.cdim) ? (unsigned)(((int64_t)row * P.ldb + cc) * ES) : kOOB;
+  }
+  const int nqp = (QP - wid + 7) / 8;
+  const __amdgpu_buffer_rsrc_t rsA = rsrc_at(P.a, 0, P.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsB = rsrc_at(P.b, -(int64_t)P.ldb * ES, P.b_bytes);
+
+  int ld_t0 = (int)(kbeg % P.T);  // frame-in-utterance of the next K-tile to load
+  auto dma_stage = [&](int buf, int kt) {  // called for kt = 0, 1, ... in order
+    const int64_t k0 = kbeg + (int64_t)kt * BK;
+    const int t0 = ld_t0;
+    ld_t0 += BK;
+    if (ld_t0 >= P.T) ld_t0 -= P.T;
+    const int edge = (t0 == 0 ? 1 : 0) | (t0 + BK == P.T ? 2 : 0);  // halo rows outside the utterance
+    const unsigned ksa = (unsigned)(k0 * P.lda * ES), ksb = (unsigned)(k0 * P.ldb * ES);
+    char* st = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) dma16(rsA, st + (2 * wid + i) * 1024, aoff[i] + ksa);
+#pragma unroll
+    for (int i = 0; i < QPW; ++i)
+      if (i < nqp) dma16(rsB, st + bdst[i], (bedge[i] & edge) ? kOOB : boff[i] + ksb);
+  };
+
+  f32x16_t acc[2][NJ];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int r32 = lane & 31, h = lane >> 5;
+  const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+  typedef short s16x8_t __attribute__((ext_vector_type(8)));
+  const int ro0 = 1 - P.sign, ro2 = 1 + P.sign;  // stage-row offset of taps 0 and 2 (tap 1: 1)
+
+  auto compute_stage = [&](int buf) {
+    const char* la = smem + buf * STAGE;
+    const char* lb = la + A_BYTES + qb * QB_BYTES;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      bf16x8_t af[2], bfr[NJ];
+#pragma unroll
+      for (int x = 0; x < 2; ++x) {
+        const int kb = 16 * s + (g >> 1) * 8;
+        const int ch = ((wm * 64 + x * 32 + (g & 1) * 16) >> 3) + (p >> 1);
+        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (VQX_LDS(s16x4_t)*)(la + mnmaj_off<T>(kb + q, ch) + 8 * (p & 1)));
+        const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (VQX_LDS(s16x4_t)*)(la + mnmaj_off<T>(kb + 4 + q, ch) + 8 * (p & 1)));
+        const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[x] = __builtin_bit_cast(bf16x8_t, v);
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        // TAPS 3: tap j of the wave's 32 channels; TAPS 1: 32-channel half j at the centre rows
+        const int ro = TAPS == 1 ? 1 : (j == 0 ? ro0 : (j == 1 ? 1 : ro2));
+        const int kb = 16 * s + (g >> 1) * 8 + ro;
+        const int ch = (((TAPS == 1 ? j : wn) * 32 + (g & 1) * 16) >> 3) + (p >> 1);
+        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (VQX_LDS(s16x4_t)*)(lb + q_off128(kb + q, ch) + 8 * (p & 1)));
+        const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (VQX_LDS(s16x4_t)*)(lb + q_off128(kb + 4 + q, ch) + 8 * (p & 1)));
+        const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfr[j] = __builtin_bit_cast(bf16x8_t, v);
+      }
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[mi][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[mi], acc[mi][j], 0, 0, 0);
+    }
+  };
+
+  if (nk > 0) {
+    dma_stage(0, 0);
+    wait_vm(0);
+    __builtin_amdgcn_s_barrier();
+    int buf = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      if (VQX_GEMM_LAB != 1 && kt + 1 < nk) dma_stage(buf ^ 1, kt + 1);
+      if (VQX_GEMM_LAB != 2) compute_stage(buf);
+      wait_vm(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      buf ^= 1;
+    }
+  }
+  if (VQX_GEMM_LAB == 3) {  // keep the accumulators live
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) t += acc[0][j][e] + acc[1][j][e];
+    if (t == 12345.f) ((float*)P.y)[tid] = t;
+    return;
+  }
+  // slab store through LDS, 128 columns per pass (TAPS 3: one tap; TAPS 1: one
+  // 128-channel half): rows of 128 columns, 16 lanes x 8 values each
+  float* ep = (float*)smem;
+  const int64_t slab0 = (int64_t)split * P.Mc * P.Nc;
+#pragma unroll
+  for (int ps = 0; ps < (TAPS == 3 ? 3 : 2); ++ps) {
+    __syncthreads();
+    if (TAPS == 3 || (qb >> 1) == ps) {
+#pragma unroll
+      for (int jj = 0; jj < (TAPS == 3 ? 1 : 2); ++jj) {
+        const int j = TAPS == 3 ? ps : jj;                                  // accumulator column
+        const int col = TAPS == 3 ? wc * 32 : (qb & 1) * 64 + jj * 32;      // its LDS column
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int gq = 0; gq < 4; ++gq) {
+            const f32x4_t v = {acc[mi][j][4 * gq], acc[mi][j][4 * gq + 1], acc[mi][j][4 * gq + 2],
+                               acc[mi][j][4 * gq + 3]};
+            *(f32x4_t*)(ep + (wm * 64 + mi * 32 + r32) * EP_LD + col + 8 * gq + 4 * h) = v;
+          }
+      }
+    }
+    __syncthreads();
+    const int ccol = TAPS == 3 ? c0 : c0 + ps * 128;       // channel of LDS column 0
+    const int64_t cbase = TAPS == 3 ? (int64_t)ps * P.cdim : 0;  // slab column of channel 0
+#pragma unroll
+    for (int pass = 0; pass < 128 / (NT / 16); ++pass) {
+      const int lr = pass * (NT / 16) + (tid >> 4), lc = (tid & 15) * 8;
+      const int r = r0 + lr, cc = ccol + lc;
+      if (r < P.Mc && cc < P.cdim) {
+        const f32x4_t lo = *(const f32x4_t*)(ep + lr * EP_LD + lc);
+        const f32x4_t hi = *(const f32x4_t*)(ep + lr * EP_LD + lc + 4);
+        const int64_t at = slab0 + (int64_t)r * P.Nc + cbase + cc;
+        if (P.slab_bf16) {
+          const float v8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          st8<bf16_t>(P.y, at, v8);
+        } else {
+          float* o = (float*)P.y + at;
+          *(f32x4_t*)o = lo;
+          *(f32x4_t*)(o + 4) = hi;
+        }
+      }
+    }
+  }
+}
+
 }  // namespace vqx

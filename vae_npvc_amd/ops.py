@@ -116,7 +116,9 @@ class LaunchProbe:
             call("vqx_probe_read", i, info, ctypes.byref(fl), ctypes.byref(ms))
             dt, mode, pro, gen, ek = list(info)  # ek: epilogue kind (vqx_gemm_kernel.h EK_*)
             bk = 64 if dt == L.VQX_BF16 else 32
-            if gen == 2 and mode == 2:  # tap-reuse weight gradient (vqx_gemm_kernel.h wgrad_tr_kernel)
+            if gen == 4:  # wide tap-reuse weight gradient (vqx_gemm_kernel.h wgrad_tr2_kernel)
+                sym = f"vqx::wgrad_tr2_kernel<{pro}>"  # pro slot = taps
+            elif gen == 2 and mode == 2:  # tap-reuse weight gradient (vqx_gemm_kernel.h wgrad_tr_kernel)
                 sym = f"vqx::wgrad_tr_kernel<{ek}, {pro}>"  # pro slot = K groups
             elif gen == 3:  # tall tap-reuse kernel (vqx_gemm_kernel.h conv_tr8_kernel)
                 sym = f"vqx::conv_tr8_kernel<{mode}, {ek}, {pro}>"  # pro slot = frame segments
