@@ -150,6 +150,19 @@ typedef struct vqx_wgrad_args {
 int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream);
 
 /*
+ * One layer's data gradient (d, as vqx_conv1d_dgrad) and weight gradient (w,
+ * as vqx_conv1d_wgrad) from the same output gradient, in one launch whose
+ * workgroups interleave the two GEMMs (each CU runs one of each, so the data
+ * gradient's fused epilogue overlaps the weight gradient's main loop) where a
+ * fused instance covers the pair: bf16, no prologue, the 3-tap tap-reuse
+ * kernels (and 1x1 layers under VQX_DUAL=2).  Otherwise the two are launched in sequence
+ * (weight gradient first).  *fused (may be NULL) = 1 for one launch, 0 for
+ * two.  Results equal the separate calls bit for bit.  Replaces the two
+ * autograd calls of one conv in the reference backward.
+ */
+int vqx_conv1d_dgrad_wgrad(const vqx_conv_args* d, const vqx_wgrad_args* w, int32_t* fused, vqx_stream_t stream);
+
+/*
  * Weight norm (torch.nn.utils.weight_norm, dim=0; applied at vqvae.py:203-208,
  * 329-334): w = g * v / ||v|| per row o of v[rows][cols] (Conv1d rows = cout,
  * ConvT rows = cin).  The forward packs w into the effective-conv layout the
@@ -469,8 +482,13 @@ const char* vqx_last_error(void);
  * kernel, everything else the implicit-im2col kernel), 1 = implicit-im2col
  * kernel only, 2 / 3 = the tall tap-reuse kernel with 256 / 512-frame tiles
  * wherever T % 256 == 0 and the frames divide, 4 = the 128-frame tap-reuse
- * kernel only.  The environment variable VQX_TAP_REUSE=0 forces 1, VQX_TR8=0/1/2
- * fixes the tall kernel's choice under policy 0. */
+ * kernel only, 5 = automatic with the wide 8-wave weight-gradient kernels
+ * (3-tap c_dim % 128 == 0, 1x1 c_dim % 256 == 0), 6 = automatic with the
+ * fused 1x1 launches of vqx_conv1d_dgrad_wgrad.  The environment variable
+ * VQX_TAP_REUSE=0 forces 1, VQX_TR8=0/1/2 fixes the tall kernel's choice
+ * under policy 0, VQX_WGRAD_WIDE=1 selects the wide kernels, VQX_DUAL=0/1/2 sets
+ * the fused launches of vqx_conv1d_dgrad_wgrad (off / 3-tap pairs, the
+ * default / 3-tap and 1x1 pairs; policy 1 turns them off). */
 int vqx_set_gemm_tile(int32_t policy);
 
 /* Launch probe (measurement only; not reentrant while enabled).  While on,
@@ -486,7 +504,7 @@ int vqx_probe_count(int64_t* n);
 int vqx_probe_read(int64_t i, int32_t* info5, double* flops, float* ms);
 
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
-#define VQX_ABI_VERSION 119
+#define VQX_ABI_VERSION 120
 int vqx_version(void);
 
 #ifdef __cplusplus

@@ -490,6 +490,83 @@ def test_gnbwd_epilogue_matches_standalone(glu, tile):
         assert relerr(a, b) < 2e-2, relerr(a, b)
 
 
+@pytest.mark.parametrize("case", ["k1_glu", "k1_res", "k1_plain", "tr_mask", "tr_convt", "gen"])
+def test_fused_dgrad_wgrad_equals_separate_launches(case):
+    """vqx_conv1d_dgrad_wgrad (vqx_gemm_dual.hip: one launch interleaving a
+    layer's data- and weight-gradient GEMMs) against vqx_conv1d_wgrad +
+    vqx_conv1d_dgrad, bit for bit (the same kernel bodies on the same tiles):
+    the decoder res/skip 1x1 (GLU GroupNorm-backward epilogue, 640 rows = an
+    uneven split of the two grids), the encoder skip 1x1 (residual + column
+    sums + GroupNorm-backward sums), a plain 1x1, the 3-tap tap-reuse pair
+    with the activation-derivative mask, the ConvTranspose form (shift -1,
+    residual + column sums), and an im2col-only layer (cin 80: two launches)."""
+    ops = _ops()
+    from vae_npvc_amd import _lib as L
+    torch.manual_seed(31)
+    dt = torch.bfloat16
+    B, T = 4, 256
+    N = B * T
+    k = 3 if case.startswith("tr") else 1
+    cfg = {"k1_glu": (640, 512), "k1_res": (512, 512), "k1_plain": (512, 768), "tr_mask": (1024, 512),
+           "tr_convt": (512, 1024), "gen": (80, 512)}[case]
+    co, ci = cfg                                   # forward layer cout, cin
+    dy = torch.randn(N, co, device=DEV).to(dt)
+    x = torch.randn(N, ci, device=DEV).to(dt)
+    wp = (torch.randn(co, k * ci, device=DEV) / (k * ci) ** 0.5).to(dt)
+    dkw = dict(T=T, cin=co, cout=ci, ntaps=k, pad=(k - 1) // 2 * (1 if k == 3 else 0))
+    sign, r_dim, c_dim, p_op, q_op = 1, co, ci, dy, x
+    if case == "tr_convt":
+        sign, r_dim, c_dim, p_op, q_op = -1, ci, co, x, dy
+    splits = 8
+    slab_shape = (splits, r_dim, k * c_dim)
+    wkw = dict(T=T, r_dim=r_dim, c_dim=c_dim, ntaps=k, pad=(k - 1) // 2, shift_sign=sign, splits=splits)
+    extra = {}
+    if case == "k1_glu":
+        u = torch.randn(N, 2 * ci, device=DEV).to(dt)
+        mr = torch.empty(B, 2, 2, device=DEV)
+        ops.groupnorm_stats(u, T, 2, torch.empty(B * 2 * 24, device=DEV), mr)
+        extra = dict(gn_h=u, gn_mr=mr, gn_gamma=torch.randn(2 * ci, device=DEV), gn_beta=torch.randn(2 * ci, device=DEV),
+                     gn_groups=2, gn_glu=True)
+    elif case == "k1_res":
+        u = torch.randn(N, ci, device=DEV).to(dt)
+        mr = torch.empty(B, 1, 2, device=DEV)
+        ops.groupnorm_stats(u, T, 1, torch.empty(B * 24, device=DEV), mr)
+        extra = dict(gn_h=u, gn_mr=mr, gn_gamma=torch.randn(ci, device=DEV), gn_beta=torch.randn(ci, device=DEV),
+                     res=torch.randn(N, ci, device=DEV).to(dt))
+    elif case == "tr_mask":
+        extra = dict(mask=torch.randn(N, ci, device=DEV).to(dt), mask_slope=0.2)
+    elif case == "tr_convt":
+        extra = dict(res=torch.randn(N, ci, device=DEV).to(dt))
+    outs = []
+    for fused_call in (False, True):
+        o = {"dx": torch.full((N, ci), float("nan"), device=DEV, dtype=dt),
+             "slabs": torch.full(slab_shape, float("nan"), device=DEV, dtype=dt)}
+        kw = dict(extra)
+        if case in ("k1_glu", "k1_res"):
+            o["gnb"] = torch.full((N // 128 * (ci // 128) * 4,), float("nan"), device=DEV)
+            kw["gn_bwd"] = o["gnb"]
+        if case in ("k1_res", "tr_convt"):
+            o["cs"] = torch.full((N // 128, ci), float("nan"), device=DEV)
+            kw["colsum"] = o["cs"]
+        if fused_call:
+            # the 1x1 pairs fuse under gemm policy 6 / VQX_DUAL=2 only (vqx_gemm.hip dual_policy)
+            L.call("vqx_set_gemm_tile", 6 if case.startswith("k1") else 0)
+            try:
+                fused = ops.conv_dgrad_wgrad(dy, wp, o["dx"], dict(dkw, **kw), p_op, q_op, o["slabs"], wkw)
+            finally:
+                L.call("vqx_set_gemm_tile", 0)
+            assert fused == (case != "gen"), (case, fused)
+        else:
+            ops.conv_wgrad(p_op, q_op, o["slabs"], **wkw)
+            ops.conv_dgrad(dy, wp, o["dx"], **dkw, **kw)
+        torch.cuda.synchronize()
+        outs.append(o)
+    for key in outs[0]:
+        a, b = outs[0][key], outs[1][key]
+        assert torch.equal(a.view(torch.int16) if a.dtype == dt else a.view(torch.int32),
+                           b.view(torch.int16) if b.dtype == dt else b.view(torch.int32)), (case, key)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("glu,C,T", [(True, 1024, 256), (True, 256, 200), (False, 512, 256), (False, 128, 72)])
 def test_gn_bwd_matches_torch_autograd(dtype, glu, C, T):

@@ -15,7 +15,7 @@ from pathlib import Path
 import torch  # noqa: F401  (loads the HIP runtime first; see module docstring)
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libvqx.so"
-ABI_VERSION = 119  # include/vqx.h VQX_ABI_VERSION
+ABI_VERSION = 120  # include/vqx.h VQX_ABI_VERSION
 
 VQX_F32, VQX_BF16 = 0, 1
 PRO_NONE, PRO_LRELU, PRO_RELU, PRO_SCALE_RELU = 0, 1, 2, 3
@@ -75,6 +75,8 @@ _SIGS = {
     "vqx_conv1d_fwd": [ctypes.POINTER(ConvArgs), c_void_p],
     "vqx_conv1d_dgrad": [ctypes.POINTER(ConvArgs), c_void_p],
     "vqx_conv1d_wgrad": [ctypes.POINTER(WgradArgs), c_void_p],
+    "vqx_conv1d_dgrad_wgrad": [ctypes.POINTER(ConvArgs), ctypes.POINTER(WgradArgs), ctypes.POINTER(ctypes.c_int32),
+                               c_void_p],
     "vqx_weight_norm_fwd": [c_void_p, c_void_p, c_int32, c_void_p],
     "vqx_weight_norm_bwd": [c_void_p, c_void_p, c_int32, c_void_p],
     "vqx_groupnorm_stats": [c_void_p, c_int32, c_int32, c_int64, c_int32, c_int32, c_int32, c_float, c_void_p,

@@ -17,6 +17,7 @@ ROOT = PKG.parent
 OUT_DIR = PKG / "lib"
 LIB = OUT_DIR / "libvqx.so"
 SOURCES = ["vqx_runtime.hip", "vqx_gemm.hip", "vqx_gemm_fwd.hip", "vqx_gemm_dgrad.hip", "vqx_gemm_wgrad.hip",
+           "vqx_gemm_dual.hip",
            "vqx_vq.hip", "vqx_misc.hip"]
 HEADERS = ["vqx_common.h", "vqx_gemm_kernel.h", "vqx_gemm_inst.h", str(ROOT / "include" / "vqx.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -28,6 +28,11 @@ static size_t g_probe_used = 0;
 void gemm_launch(const void* fn, int grid, hipStream_t s, const GemmParams& P, const int info[5], double flops,
                  int block) {
   void* args[] = {(void*)&P};
+  gemm_launch_args(fn, grid, s, args, info, flops, block);
+}
+
+void gemm_launch_args(const void* fn, int grid, hipStream_t s, void** args, const int info[5], double flops,
+                      int block) {
   if (!g_probe_on) {
     (void)hipLaunchKernel(fn, dim3(grid), dim3(block), args, 0, s);
     return;
@@ -53,7 +58,8 @@ void gemm_launch(const void* fn, int grid, hipStream_t s, const GemmParams& P, c
 // vqx_set_gemm_tile: 0 = automatic, 1 = implicit-im2col kernel only,
 // 2 / 3 = tap reuse through conv_tr8_kernel with 1 / 2 frame segments where it
 // applies, 4 = tap reuse through conv_tr_kernel only, 5 = automatic with the
-// wide weight gradients (wgrad_tr2_kernel: 3-tap c_dim % 128 == 0, 1x1 c_dim % 256 == 0)
+// wide weight gradients (wgrad_tr2_kernel: 3-tap c_dim % 128 == 0, 1x1 c_dim % 256 == 0),
+// 6 = automatic with the fused 1x1 DGRAD+WGRAD launches too (dual_policy 2)
 static int g_gemm_policy = 0;
 
 bool tap_reuse_enabled() {
@@ -108,7 +114,9 @@ static void launch_mode(GemmParams& P, int mode, int64_t rows, int extra_mult, b
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-static int conv_common(const vqx_conv_args* a, int mode, hipStream_t s) {
+// Checks the arguments and fills P (tiles_m is set by the launch); gen = the
+// generic (cin % BK != 0) tile path.
+static int conv_prepare(const vqx_conv_args* a, int mode, GemmParams& P, bool& gen) {
   if (!a) { set_error("vqx_conv: null args"); return -1; }
   if (a->dtype != VQX_F32 && a->dtype != VQX_BF16) { set_error("vqx_conv: bad dtype %d", a->dtype); return -1; }
   const int epc = a->dtype == VQX_BF16 ? 8 : 4;
@@ -144,7 +152,7 @@ static int conv_common(const vqx_conv_args* a, int mode, hipStream_t s) {
   if ((epi & VQX_EPI_COLSUM) && !a->colsum_part) { set_error("vqx_conv: COLSUM needs colsum_part [ceil(n_rows/128)][cout]"); return -1; }
   if (!a->y || !aligned16(a->y)) { set_error("vqx_conv: y must be non-null and 16-byte aligned"); return -1; }
 
-  GemmParams P = {};
+  P = GemmParams{};
   P.a = a->x; P.b = a->w;
   P.a_bytes = ((a->n_rows - 1) * (int64_t)a->ldx + a->cin) * es;
   P.n_rows = a->n_rows; P.T = a->T; P.lda = a->ldx;
@@ -169,24 +177,20 @@ static int conv_common(const vqx_conv_args* a, int mode, hipStream_t s) {
     return -1;
   }
   if (P.a_bytes > 0x7fffffffLL || P.b_bytes > 0x7fffffffLL) { set_error("vqx_conv: operand larger than 2 GiB"); return -1; }
-  const bool gen = (a->cin % (a->dtype == VQX_BF16 ? 64 : 32)) != 0;
+  gen = (a->cin % (a->dtype == VQX_BF16 ? 64 : 32)) != 0;
+  return 0;
+}
+
+static int conv_common(const vqx_conv_args* a, int mode, hipStream_t s) {
+  GemmParams P;
+  bool gen;
+  if (conv_prepare(a, mode, P, gen)) return -1;
   launch_mode(P, mode, a->n_rows, 1, a->dtype == VQX_BF16, gen, s);
   return launch_status(mode == MODE_FWD ? "vqx_conv1d_fwd" : "vqx_conv1d_dgrad");
 }
 
-}  // namespace vqx
-
-using namespace vqx;
-
-extern "C" int vqx_conv1d_fwd(const vqx_conv_args* a, vqx_stream_t stream) {
-  return conv_common(a, MODE_FWD, (hipStream_t)stream);
-}
-
-extern "C" int vqx_conv1d_dgrad(const vqx_conv_args* a, vqx_stream_t stream) {
-  return conv_common(a, MODE_DGRAD, (hipStream_t)stream);
-}
-
-extern "C" int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream) {
+// Checks the arguments and fills P for the weight gradient (tiles_m is set by the launch)
+static int wgrad_prepare(const vqx_wgrad_args* a, GemmParams& P, bool& gen) {
   if (!a) { set_error("vqx_conv1d_wgrad: null args"); return -1; }
   if (a->dtype != VQX_F32 && a->dtype != VQX_BF16) { set_error("vqx_conv1d_wgrad: bad dtype"); return -1; }
   const int epc = a->dtype == VQX_BF16 ? 8 : 4;
@@ -199,7 +203,7 @@ extern "C" int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream) {
   if (!aligned16(a->p) || !aligned16(a->q) || !a->slabs || !aligned16(a->slabs)) { set_error("vqx_conv1d_wgrad: bad pointers"); return -1; }
   if (a->shift_sign != 1 && a->shift_sign != -1) { set_error("vqx_conv1d_wgrad: shift_sign must be +-1"); return -1; }
   if (a->slab_dtype != VQX_F32 && !(a->slab_dtype == VQX_BF16 && a->dtype == VQX_BF16)) { set_error("vqx_conv1d_wgrad: slab_dtype %d (bf16 slabs need bf16 operands)", a->slab_dtype); return -1; }
-  GemmParams P = {};
+  P = GemmParams{};
   P.a = a->p; P.b = a->q; P.n_rows = a->n_rows; P.T = a->T; P.lda = a->ldp; P.ldb = a->ldq;
   P.a_bytes = ((a->n_rows - 1) * (int64_t)a->ldp + a->r_dim) * es;
   P.b_bytes = ((a->n_rows - 1) * (int64_t)a->ldq + a->c_dim) * es;
@@ -214,7 +218,7 @@ extern "C" int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream) {
   P.y = a->slabs;
   P.slab_bf16 = a->slab_dtype == VQX_BF16;
   const int bkv = a->dtype == VQX_BF16 ? 64 : 32;
-  const bool gen = (a->T % bkv) != 0 || (a->n_rows % bkv) != 0;
+  gen = (a->T % bkv) != 0 || (a->n_rows % bkv) != 0;
   if (!gen && wgrad_tr_ok(a->n_rows, a->T, a->c_dim, a->ntaps, a->pad, dil, a->dtype == VQX_BF16, a->q_prologue)) {
     P.tap_reuse = wgrad_kgroups();
     P.tiles_n = a->c_dim / 64;
@@ -226,9 +230,63 @@ extern "C" int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream) {
     P.tap_reuse = 4;  // wide 1x1 kernel, 256 channels of c per workgroup
     P.tiles_n = a->c_dim / 256;
   }
-  hipStream_t s = (hipStream_t)stream;
-  launch_mode(P, MODE_WGRAD, P.Mc, P.splits, a->dtype == VQX_BF16, gen, s);
+  return 0;
+}
+
+// fused DGRAD+WGRAD launches: 0 = off, 1 = 3-tap tap-reuse pairs (default),
+// 2 = also the 1x1 pairs (env VQX_DUAL; measured: 3-tap pairs 3-8% faster than
+// two launches, 1x1 pairs 8-20% slower -- their DGRAD workgroups run ~1.5x
+// longer than the WGRAD ones, and two mixed rounds end on a DGRAD tail)
+int dual_policy() {
+  static const int pol = [] {
+    const char* e = getenv("VQX_DUAL");
+    return (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 1;
+  }();
+  return g_gemm_policy == 1 ? 0 : (g_gemm_policy == 6 ? 2 : pol);
+}
+static bool dual_enabled() { return dual_policy() > 0; }
+
+}  // namespace vqx
+
+using namespace vqx;
+
+extern "C" int vqx_conv1d_fwd(const vqx_conv_args* a, vqx_stream_t stream) {
+  return conv_common(a, MODE_FWD, (hipStream_t)stream);
+}
+
+extern "C" int vqx_conv1d_dgrad(const vqx_conv_args* a, vqx_stream_t stream) {
+  return conv_common(a, MODE_DGRAD, (hipStream_t)stream);
+}
+
+extern "C" int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream) {
+  GemmParams P;
+  bool gen;
+  if (wgrad_prepare(a, P, gen)) return -1;
+  launch_mode(P, MODE_WGRAD, P.Mc, P.splits, a->dtype == VQX_BF16, gen, (hipStream_t)stream);
   return launch_status("vqx_conv1d_wgrad");
+}
+
+extern "C" int vqx_conv1d_dgrad_wgrad(const vqx_conv_args* d, const vqx_wgrad_args* w, int32_t* fused,
+                                      vqx_stream_t stream) {
+  GemmParams PD, PW;
+  bool gd, gw;
+  if (conv_prepare(d, MODE_DGRAD, PD, gd)) return -1;
+  if (wgrad_prepare(w, PW, gw)) return -1;
+  hipStream_t s = (hipStream_t)stream;
+  const bool bf = d->dtype == VQX_BF16 && w->dtype == VQX_BF16;
+  if (bf && !gd && !gw && dual_enabled()) {
+    PD.tiles_m = (int)((d->n_rows + 127) / 128);
+    PW.tiles_m = (PW.Mc + 127) / 128;
+    if (launch_dual(PD, PD.tiles_m * PD.tiles_n, PW, PW.tiles_m * PW.tiles_n * PW.splits, s)) {
+      if (fused) *fused = 1;
+      return launch_status("vqx_conv1d_dgrad_wgrad");
+    }
+  }
+  // two launches in the engine's order: weight gradient, then data gradient
+  launch_mode(PW, MODE_WGRAD, PW.Mc, PW.splits, w->dtype == VQX_BF16, gw, s);
+  launch_mode(PD, MODE_DGRAD, d->n_rows, 1, d->dtype == VQX_BF16, gd, s);
+  if (fused) *fused = 0;
+  return launch_status("vqx_conv1d_dgrad_wgrad");
 }
 
 extern "C" int vqx_wgrad_tiles(int64_t n_rows, int32_t T, int32_t r_dim, int32_t c_dim, int32_t ntaps, int32_t pad,
@@ -248,7 +306,7 @@ extern "C" int vqx_wgrad_tiles(int64_t n_rows, int32_t T, int32_t r_dim, int32_t
 }
 
 extern "C" int vqx_set_gemm_tile(int32_t policy) {
-  if (policy < 0 || policy > 5) { set_error("vqx_set_gemm_tile: policy %d not in 0..5", policy); return -1; }
+  if (policy < 0 || policy > 6) { set_error("vqx_set_gemm_tile: policy %d not in 0..6", policy); return -1; }
   g_gemm_policy = policy;
   return 0;
 }

@@ -1,0 +1,98 @@
+// A layer's data gradient (DGRAD) and weight gradient (WGRAD) in ONE launch.
+// Default for the 3-tap layers only (dual_policy): measured on the config-2
+// step, dec conv_in 109.0 -> 105.8 us and enc k3 66.1 -> 61.1 us per pair,
+// while the 1x1 pairs ran 8-20% slower (profiles/r02/dual_ab.txt).
+//
+// Both read the same output gradient dy and are independent.  As two launches
+// each is one round of 512 four-wave workgroups (two per CU) whose slots all
+// reach the same phase together: the 1x1 DGRAD's fused GroupNorm/GLU-backward
+// epilogue is an HBM burst every workgroup issues at once, and each launch
+// pays its own ramp and tail.  Here the grid interleaves the two GEMMs'
+// workgroups, 8 + 8 per 16 blocks, so each CU runs one workgroup of each:
+// one's HBM-heavy epilogue runs beside the other's MFMA main loop, and one
+// ramp and one tail cover both.  Each workgroup runs the unchanged kernel body
+// (vqx_gemm_kernel.h conv_gemm_body / conv_tr_body / wgrad_tr_body) on its own
+// tile grid; the branch is uniform per workgroup.
+#include "vqx_gemm_inst.h"
+
+namespace vqx {
+
+// blockIdx -> (DGRAD?, workgroup index in that GEMM's grid): 16-block groups
+// of 8 DGRAD + 8 WGRAD while both have workgroups left, then the rest of
+// DGRAD, then the rest of WGRAD.  In the paired region the sub-index keeps
+// blockIdx % 8 (the XCD), so each body's XCD-aware tile map still applies.
+__device__ __forceinline__ bool dual_split(int b, int nd, int nw, int& sub) {
+  const int m = (nd < nw ? nd : nw) & ~7;
+  if (b < 2 * m) {
+    const int g = b >> 4, x = b & 15;
+    sub = 8 * g + (x & 7);
+    return x < 8;
+  }
+  const int j = b - 2 * m;
+  if (j < nd - m) {
+    sub = m + j;
+    return true;
+  }
+  sub = m + (j - (nd - m));
+  return false;
+}
+
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+
+// 1x1 layer: conv_gemm_kernel DGRAD (epilogue kind EKD) + conv_gemm_kernel WGRAD
+template <int EKD>
+__global__ __launch_bounds__(256, 2) void dual_k1_kernel(GemmParams PD, GemmParams PW, int nd, int nw) {
+  __shared__ __attribute__((aligned(16))) char smem[conv_gemm_smem<bf16_t, 64, 2>()];
+  int sub;
+  if (dual_split(blockIdx.x, nd, nw, sub))
+    conv_gemm_body<bf16_t, MODE_DGRAD, VQX_PRO_NONE, false, 64, 2, EKD>(PD, sub, nd, smem);
+  else
+    conv_gemm_body<bf16_t, MODE_WGRAD, VQX_PRO_NONE, false, 64, 2, EK_NONE>(PW, sub, nw, smem);
+}
+
+// 3-tap layer: conv_tr_kernel DGRAD (epilogue kind EKD) + wgrad_tr_kernel
+template <int EKD>
+__global__ __launch_bounds__(256, 2) void dual_tr_kernel(GemmParams PD, GemmParams PW, int nd, int nw) {
+  __shared__ __attribute__((aligned(16))) char smem[cmax(conv_tr_smem<32>(), wgrad_tr_smem<1>())];
+  int sub;
+  if (dual_split(blockIdx.x, nd, nw, sub)) conv_tr_body<MODE_DGRAD, EKD, 32>(PD, sub, nd, smem);
+  else wgrad_tr_body<EK_NONE, 1>(PW, sub, nw, smem);
+}
+
+bool launch_dual(const GemmParams& PD, int nd, const GemmParams& PW, int nw, hipStream_t s) {
+  if (PD.pro != VQX_PRO_NONE || PW.pro != VQX_PRO_NONE || nd <= 0 || nw <= 0) return false;
+  const int ekd = pick_ek(PD.epi);
+  const void* fn = nullptr;
+  int kind = 0;
+  if (tap_reuse_ok(PD, true, false) && tr8_segs(PD) == 0 && tr_stage_channels() == 32) {
+    if (PW.tap_reuse != 1) return false;
+    kind = 2;
+    switch (ekd) {
+      case EK_NONE: fn = (const void*)dual_tr_kernel<EK_NONE>; break;
+      case EK_ELEM: fn = (const void*)dual_tr_kernel<EK_ELEM>; break;
+      case EK_COLSUM: fn = (const void*)dual_tr_kernel<EK_COLSUM>; break;
+      default: return false;
+    }
+  } else if (PD.ntaps == 1 && PW.ntaps == 1 && PW.tap_reuse == 0 && dual_policy() >= 2) {
+    kind = 1;
+    switch (ekd) {
+      case EK_NONE: fn = (const void*)dual_k1_kernel<EK_NONE>; break;
+      case EK_ELEM: fn = (const void*)dual_k1_kernel<EK_ELEM>; break;
+      case EK_COLSUM: fn = (const void*)dual_k1_kernel<EK_COLSUM>; break;
+      case EK_GNBWD: fn = (const void*)dual_k1_kernel<EK_GNBWD>; break;
+      default: return false;
+    }
+  } else {
+    return false;
+  }
+  const double flops = 2.0 * (double)PD.n_rows * PD.Nc * PD.K + 2.0 * (double)PW.n_rows * PW.Mc * PW.Nc;
+  // probe label: mode 3 = dual, prologue slot = kind (1: 1x1, 2: 3-tap), gen = 5
+  const int info[5] = {VQX_BF16, 3, kind, 5, ekd};
+  GemmParams pd = PD, pw = PW;
+  int a = nd, b = nw;
+  void* args[] = {(void*)&pd, (void*)&pw, (void*)&a, (void*)&b};
+  gemm_launch_args(fn, nd + nw, s, args, info, flops, 256);
+  return true;
+}
+
+}  // namespace vqx

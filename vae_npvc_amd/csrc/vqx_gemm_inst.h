@@ -15,6 +15,14 @@ namespace vqx {
 // vqx_gemm.hip: plain launch, or the probe's event-stamped launch
 void gemm_launch(const void* fn, int grid, hipStream_t s, const GemmParams& P, const int info[5], double flops,
                  int block = 256);
+void gemm_launch_args(const void* fn, int grid, hipStream_t s, void** args, const int info[5], double flops,
+                      int block = 256);
+
+// vqx_gemm_dual.hip: one layer's data and weight gradients in ONE launch
+// (dual_k1_kernel / dual_tr_kernel) where an instance covers the pair;
+// false = not covered (the caller launches them separately)
+bool launch_dual(const GemmParams& PD, int nd, const GemmParams& PW, int nw, hipStream_t s);
+int dual_policy();  // vqx_gemm.hip: 0 off, 1 3-tap pairs, 2 3-tap and 1x1 pairs (env VQX_DUAL)
 
 // vqx_gemm.hip: tap-reuse kernel switch (env VQX_TAP_REUSE=0 turns it off, for A/B runs)
 bool tap_reuse_enabled();

@@ -59,6 +59,9 @@ constexpr int kBN = 128;  // tile width (and height)
 #ifndef VQX_EPI_PREFETCH_LATE  // n > 0: issue the row-operand prefetch at main-loop iteration nk-n, not with the prologue
 #define VQX_EPI_PREFETCH_LATE 0
 #endif
+#ifndef VQX_EPI_SLAB_PREFETCH  // 1: DGRAD epilogues load each 64-row slab's row operands before the slab's passes
+#define VQX_EPI_SLAB_PREFETCH 0
+#endif
 constexpr unsigned kOOB = 0x80000000u;  // buffer offset that is always out of range -> loads 0
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 
@@ -298,7 +301,7 @@ struct EpiRows {
   int k0, k1;
 };
 
-template <int EK>
+template <int EK, int I0 = 0, int NR = 8>  // slots I0 .. I0+NR-1 ((slab, pass) = (i >> 2, i & 3))
 __device__ __forceinline__ void epi_prefetch(const GemmParams& P, int m0, int n0, int tid, EpiRows& R) {
   constexpr int EM = ek_mask(EK);
   const int epi = P.epi & EM;
@@ -316,8 +319,8 @@ __device__ __forceinline__ void epi_prefetch(const GemmParams& P, int m0, int n0
                                     : (const bf16_t*)P.gn_h + row * P.ldgn + (k == EPR_GNH2 ? P.Nc : 0);
     return (const u32x4e_t*)(b + col);
   };
-  static_for<8>([&](auto i_c) __attribute__((always_inline)) {
-    constexpr int i = decltype(i_c)::value;
+  static_for<NR>([&](auto i_c) __attribute__((always_inline)) {
+    constexpr int i = I0 + decltype(i_c)::value;
     const int64_t row = (int64_t)m0 + (i >> 2) * 64 + (i & 3) * 16 + er;
     const bool ok = row < P.n_rows && col < P.Nc;
     const u32x4e_t z = {0u, 0u, 0u, 0u};
@@ -562,7 +565,11 @@ __device__ __forceinline__ void wait_vm(int n) {
 // 44 KiB of `smem`; the caller's staging buffers must be free.  `tid` is the
 // thread's index in the 4-wave group that owns the tile (conv_tr8_kernel runs
 // two such groups side by side; every group passes the same barriers).
-template <typename T, int MODE, int EK, bool PRE = false, bool PREVEC = PRE>
+// SLABPRE: the row operands of each 64-row slab's four passes are loaded
+// together at the start of the slab (before its LDS transpose), so the
+// passes' loads are in flight at once instead of one dependent round trip per
+// pass behind the previous pass's stores (which may alias them).
+template <typename T, int MODE, int EK, bool PRE = false, bool PREVEC = PRE, bool SLABPRE = false>
 __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&acc)[2][2], char* smem, int m0, int n0,
                                               int tn, int split, const float* gmr, int tid,
                                               const EpiRows* R = nullptr) {
@@ -587,6 +594,8 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
   // row operands R->r*[slab*4 + pass] are register-resident
   static_for<2 * SUB>([&](auto slab_c) __attribute__((always_inline)) {
     constexpr int slab = decltype(slab_c)::value;
+    EpiRows SR;
+    if constexpr (SLABPRE) epi_prefetch<EK, slab * 4, 4>(P, m0, n0, tid, SR);
     if (wm == slab) {
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
@@ -616,7 +625,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
         }
       } else {
         if (row < P.n_rows && col < P.Nc) {
-          const EpiOps o = epi_ops<slab * 4 + pass, PRE>(R);
+          const EpiOps o = SLABPRE ? epi_ops<slab * 4 + pass, true>(&SR) : epi_ops<slab * 4 + pass, PRE>(R);
           epilogue8<T, EMASK, PREVEC>(P, row, col, v, gmr, o, V);
 #pragma unroll
           for (int e = 0; e < 8; ++e) cs[e] += v[e];
@@ -715,8 +724,15 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
 //   BK=64, NST=2: 64 KiB per workgroup (the round-1 pipeline);
 //   BK=32, NST=4: 64 KiB, three 16-KiB K-tiles in flight (bf16 default).
 // Two 4-wave workgroups per CU either way.
+// LDS bytes of conv_gemm_body: the NST-deep ring of A+B K-tiles (>= the epilogue's 44 KiB)
+template <typename T, int BK, int NST>
+__host__ __device__ constexpr int conv_gemm_smem() { return NST * 2 * 128 * BK * (int)sizeof(T); }
+
+// The kernel body as a device function of (bid, nwg) = (this workgroup's
+// index, workgroup count) of its own tile grid, on the caller's LDS, so that
+// dual_*_kernel can host two GEMMs in one launch.
 template <typename T, int MODE, int PRO, bool GEN, int BK, int NST, int EK>
-__global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
+__device__ __forceinline__ void conv_gemm_body(const GemmParams& P, int bid, int nwg, char* smem) {
   using C = Cfg<T>;
   constexpr int EPC = C::EPC, CPR = C::MNCPR, ES = sizeof(T);
   constexpr int BM = 128;
@@ -728,16 +744,16 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
   constexpr int NP = 2 * PW;                  // DMA pieces per wave per K-tile
   static_assert(NST * STAGE >= 45056, "epilogue staging needs 44 KiB of LDS");
   static_assert(BK % (16 / ES * 2) == 0 || ES == 4, "BK");
-  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE];
+  static_assert(conv_gemm_smem<T, BK, NST>() == NST * STAGE, "LDS");
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
 #ifdef VQX_GEMM_STAGGER  // lab only (tools/lab/k1_lab.cpp): delay the second resident workgroup of each CU
-  if (blockIdx.x >= gridDim.x / 2)
+  if (bid >= nwg / 2)
     for (int i = 0; i < VQX_GEMM_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
 #endif
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int lin = xcd_remap(bid, nwg);
   const int tiles_mn = P.tiles_m * P.tiles_n;
   const int split = lin / tiles_mn;
   const int tmn = lin - split * tiles_mn;
@@ -1113,7 +1129,15 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
   }
   return;
 #endif
-  tile_epilogue<T, MODE, EK, kPrefetch, kPreVec>(P, acc, smem, m0, n0, tn, split, gmr, (int)threadIdx.x, &rows);
+  constexpr bool kSlabPre = sizeof(T) == 2 && MODE == MODE_DGRAD && EK != EK_NONE && EK != EK_ALL && !kPrefetch &&
+                            VQX_EPI_SLAB_PREFETCH;
+  tile_epilogue<T, MODE, EK, kPrefetch, kPreVec, kSlabPre>(P, acc, smem, m0, n0, tn, split, gmr, (int)threadIdx.x, &rows);
+}
+
+template <typename T, int MODE, int PRO, bool GEN, int BK, int NST, int EK>
+__global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
+  __shared__ __attribute__((aligned(16))) char smem[conv_gemm_smem<T, BK, NST>()];
+  conv_gemm_body<T, MODE, PRO, GEN, BK, NST, EK>(P, blockIdx.x, gridDim.x, smem);
 }
 
 
@@ -1150,8 +1174,16 @@ __device__ __forceinline__ int tr_kmaj_off(int row, int ch) { return row * (16 *
 
 // BKC = channels per stage: 32 (2-deep ring, 33 KiB stages) or 16 (4-deep
 // ring of 17 KiB stages: the same LDS, twice the prefetch distance)
+// LDS bytes of conv_tr_body (the stage ring, at least the epilogue's 44 KiB)
+template <int BKC>
+__host__ __device__ constexpr int conv_tr_smem() {
+  return (BKC == 32 ? 2 : 4) * (((130 * BKC * 2 + 1023) / 1024) * 1024 + 3 * 128 * BKC * 2) > 45056
+             ? (BKC == 32 ? 2 : 4) * (((130 * BKC * 2 + 1023) / 1024) * 1024 + 3 * 128 * BKC * 2)
+             : 45056;
+}
+
 template <int MODE, int EK, int BKC>
-__global__ __launch_bounds__(256, 2) void conv_tr_kernel(GemmParams P) {
+__device__ __forceinline__ void conv_tr_body(const GemmParams& P, int bid, int nwg, char* smem) {
   using T = bf16_t;
   constexpr int ES = 2, EPC = 8, KCH = BKC * ES / 16;  // 16-B chunks per K-major row
   constexpr int NST = BKC == 32 ? 2 : 4;
@@ -1161,13 +1193,12 @@ __global__ __launch_bounds__(256, 2) void conv_tr_kernel(GemmParams P) {
   constexpr int STAGE = A_BYTES + 3 * TAP_BYTES;
   constexpr int PWB = 3 * TAP_BYTES / 1024 / 4;        // weight pieces per wave per stage
   constexpr int TAP_PIECES = TAP_BYTES / 1024;
-  constexpr int SMEM = NST * STAGE > 45056 ? NST * STAGE : 45056;  // the epilogue needs 44 KiB
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  static_assert(conv_tr_smem<BKC>() >= NST * STAGE && conv_tr_smem<BKC>() >= 45056, "LDS");
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int lin = xcd_remap(bid, nwg);
   const int tm = lin / P.tiles_n, tn = lin - tm * P.tiles_n;
   const int m0 = tm * 128, n0 = tn * kBN;
   const int nk = P.kcin / BKC;
@@ -1298,6 +1329,12 @@ __global__ __launch_bounds__(256, 2) void conv_tr_kernel(GemmParams P) {
     return;
   }
   tile_epilogue<T, MODE, EK>(P, acc, smem, m0, n0, tn, 0, P.gn_mr, (int)threadIdx.x);
+}
+
+template <int MODE, int EK, int BKC>
+__global__ __launch_bounds__(256, 2) void conv_tr_kernel(GemmParams P) {
+  __shared__ __attribute__((aligned(16))) char smem[conv_tr_smem<BKC>()];
+  conv_tr_body<MODE, EK, BKC>(P, blockIdx.x, gridDim.x, smem);
 }
 
 // ---------------------------------------------------------------------------
@@ -1524,8 +1561,17 @@ __device__ __forceinline__ int q_off128(int row, int ch) { return row * 128 + 16
 // tile, each through its own LDS ring, and are summed in LDS before the slab
 // store.  Same waves per CU as two 4-wave workgroups, half the slabs to write
 // and to reduce in the weight-norm backward.
+// LDS bytes of wgrad_tr_body: KG rings of two 25-KiB stages, at least the
+// slab-store staging (128 x 68 floats) and the K-group reduction
+template <int KG>
+__host__ __device__ constexpr int wgrad_tr_smem() {
+  return (KG * 2 * 25600 > 128 * 68 * 4 ? KG * 2 * 25600 : 128 * 68 * 4) > (KG > 1 ? 4 * 6 * 64 * 64 : 0)
+             ? (KG * 2 * 25600 > 128 * 68 * 4 ? KG * 2 * 25600 : 128 * 68 * 4)
+             : (KG > 1 ? 4 * 6 * 64 * 64 : 0);
+}
+
 template <int EK, int KG>
-__global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void wgrad_tr_kernel(GemmParams P) {
+__device__ __forceinline__ void wgrad_tr_body(const GemmParams& P, int bid, int nwg, char* smem) {
   using T = bf16_t;
   constexpr int ES = 2, EPC = 8, BK = 64, NT = 256 * KG;
   constexpr int A_BYTES = BK * 256;              // p: 64 frames x 128 r
@@ -1537,13 +1583,13 @@ __global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void wgrad_tr_kernel(Gem
   constexpr int RED_BYTES = KG > 1 ? 4 * 6 * 64 * 64 : 0;  // one group's accumulators
   constexpr int SMEM0 = KG * NST * STAGE > 128 * EP_LD * 4 ? KG * NST * STAGE : 128 * EP_LD * 4;
   constexpr int SMEM = SMEM0 > RED_BYTES ? SMEM0 : RED_BYTES;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  static_assert(wgrad_tr_smem<KG>() == SMEM, "LDS");
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = wid >> 2, wl = wid & 3;  // K group, wave within the group
   const int wm = wl >> 1, wn = wl & 1;
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int lin = xcd_remap(bid, nwg);
   const int tiles_mn = P.tiles_m * P.tiles_n;
   const int split = lin / tiles_mn;
   const int tmn = lin - split * tiles_mn;
@@ -1738,6 +1784,12 @@ __global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void wgrad_tr_kernel(Gem
       }
     }
   }
+}
+
+template <int EK, int KG>
+__global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void wgrad_tr_kernel(GemmParams P) {
+  __shared__ __attribute__((aligned(16))) char smem[wgrad_tr_smem<KG>()];
+  wgrad_tr_body<EK, KG>(P, blockIdx.x, gridDim.x, smem);
 }
 
 // ---------------------------------------------------------------------------

@@ -698,6 +698,21 @@ class VQVAEEngine:
             ops.conv_wgrad(x, dy.view(-1, s * Lr.cout), Lr.slab, T=T // s, r_dim=Lr.cin, c_dim=s * Lr.cout, ntaps=3,
                            pad=1, shift_sign=1, splits=Lr.splits)
 
+    def wgrad_dgrad(self, Lr, dy, x, dx, T, **kw):
+        """self.wgrad(Lr, dy, x, T) then self.dgrad(Lr, dy, dx, T, **kw): for a plain
+        Conv1d as one vqx_conv1d_dgrad_wgrad call (one launch interleaving both
+        GEMMs where a fused kernel covers the layer)."""
+        if Lr.kind not in (KIND_CONV, KIND_CONVT):
+            self.wgrad(Lr, dy, x, T)
+            self.dgrad(Lr, dy, dx, T, **kw)
+            return
+        dkw = dict(T=T, cin=Lr.cout, cout=Lr.cin, ntaps=Lr.k, pad=(Lr.k - 1) * Lr.dil - Lr.pad, dil=Lr.dil, **kw)
+        wkw = dict(T=T, ntaps=Lr.k, pad=Lr.pad, dil=Lr.dil, splits=Lr.splits)
+        if Lr.kind == KIND_CONV:  # as self.wgrad
+            ops.conv_dgrad_wgrad(dy, Lr.wp, dx, dkw, dy, x, Lr.slab, dict(wkw, r_dim=Lr.cout, c_dim=Lr.cin, shift_sign=1))
+        else:
+            ops.conv_dgrad_wgrad(dy, Lr.wp, dx, dkw, x, dy, Lr.slab, dict(wkw, r_dim=Lr.cin, c_dim=Lr.cout, shift_sign=-1))
+
     def bias_grad(self, Lr, dy, w):
         ops.colsum(dy, w.cs_part, self.g(Lr.mod.bias))
 
@@ -915,7 +930,6 @@ class VQVAEEngine:
                 k ^= 1
                 nxt = self._enc_cur(w, si, k)
                 # cur = dL/dc_{j+1}, the gradient w.r.t. block j's output GN(h_L) + skip(c_j)
-                self.wgrad(b.skip, cur, sw.c[j], T)
                 dy = cur
                 fused_here = top_fused if j == nb - 1 else True
                 for l in reversed(range(st.L)):
@@ -927,16 +941,15 @@ class VQVAEEngine:
                     ops.gn_bwd(dy, sw.h[j][l], dh, T, 1, False, sw.mr[j][l], gn.weight, gn.bias, w.gnb_part, cs_b,
                                dg_b, db_b, nparts=nparts)
                     src = sw.a[j] if l == 0 else sw.g[j][l - 1]
-                    self.wgrad(Lr, dh, src, T)
                     if l > 0:  # into LeakyReLU(GN(h_{l-1})): its derivative from the sign of the stored output
-                        self.dgrad(Lr, dh, dy2, T, mask=sw.g[j][l - 1], mask_slope=0.2)
+                        self.wgrad_dgrad(Lr, dh, src, dy2, T, mask=sw.g[j][l - 1], mask_slope=0.2)
                         dy = dy2
                     else:
-                        self.dgrad(Lr, dh, tmp, T, mask=sw.a[j], mask_slope=0.2)
+                        self.wgrad_dgrad(Lr, dh, src, tmp, T, mask=sw.a[j], mask_slope=0.2)
                 prod = dict(colsum=sw.cs[j])
                 if j > 0:
                     prod.update(self._gnb(w, si, j - 1))
-                self.dgrad(b.skip, cur, nxt, T, res=tmp, **prod)
+                self.wgrad_dgrad(b.skip, cur, sw.c[j], nxt, T, res=tmp, **prod)
                 # weight norms of the stack convs and skip + their biases and the GN affine
                 self._wn_bwd(w, b.key)
                 cur = nxt
@@ -966,16 +979,15 @@ class VQVAEEngine:
         dxhat = w.dxhat
         ns = len(self.dec_stages)
         self.bias_grad(f2, dxhat, w)
-        self.wgrad(f2, dxhat, w.f1, w.T)
-        self.dgrad(f2, dxhat, w.df1, w.T, mask=w.f1, mask_slope=0.0, colsum=w.cs_f1)
+        self.wgrad_dgrad(f2, dxhat, w.f1, w.df1, w.T, mask=w.f1, mask_slope=0.0, colsum=w.cs_f1)
         s = math.sqrt(1.0 / self.n_dec_layers)
-        self.wgrad(f1, w.df1, w.a_skip, w.T)
         # dL/dskip (identical for every block) -> tail columns of every [dx | dskip] buffer
         lst = ns - 1
         sw = w.dec[lst]
         k = 0
         cur = sw.dr[k]
-        self.dgrad(f1, w.df1, cur[:, sw.C:], w.T, mask=w.a_skip, mask_slope=0.0, mask_scale=s, colsum=w.cs_skip)
+        self.wgrad_dgrad(f1, w.df1, w.a_skip, cur[:, sw.C:], w.T, mask=w.a_skip, mask_slope=0.0, mask_scale=s,
+                         colsum=w.cs_skip)
         for si in range(ns):
             if self.dec_stages[si].blocks:
                 for q in range(2):
@@ -998,16 +1010,14 @@ class VQVAEEngine:
                 ci, gn, rs = b.conv_in, b.gn, b.rs
                 nxt = sw.dr[k ^ 1]
                 # cur = [dL/dx_{j+1} | dL/dskip]
-                self.wgrad(rs, cur, sw.g[j], T)
                 if sw.fuse:  # GLU + GroupNorm backward sums from the res/skip dgrad's epilogue
-                    self.dgrad(rs, cur, dg, T, gn_bwd=w.gnb_part, gn_h=sw.u[j], gn_mr=sw.mr[j], gn_gamma=gn.weight,
-                               gn_beta=gn.bias, gn_groups=2, gn_glu=True)
+                    self.wgrad_dgrad(rs, cur, sw.g[j], dg, T, gn_bwd=w.gnb_part, gn_h=sw.u[j], gn_mr=sw.mr[j],
+                                     gn_gamma=gn.weight, gn_beta=gn.bias, gn_groups=2, gn_glu=True)
                 else:
-                    self.dgrad(rs, cur, dg, T)
+                    self.wgrad_dgrad(rs, cur, sw.g[j], dg, T)
                 ops.gn_bwd(dg, sw.u[j], du, T, 2, True, sw.mr[j], gn.weight, gn.bias, w.gnb_part, sw.cs_all[j],
                            dg_b, db_b, nparts=self._gnb_parts(sw, C))
-                self.wgrad(ci, du, sw.xs[j], T)
-                self.dgrad(ci, du, nxt[:, :C], T, res=cur[:, :C], colsum=sw.cs[j])
+                self.wgrad_dgrad(ci, du, sw.xs[j], nxt[:, :C], T, res=cur[:, :C], colsum=sw.cs[j])
                 # weight norms of conv_in/res_skip + biases of res_skip, conv_in and the GN affine
                 self._wn_bwd(w, b.key)
                 k ^= 1

@@ -116,7 +116,9 @@ class LaunchProbe:
             call("vqx_probe_read", i, info, ctypes.byref(fl), ctypes.byref(ms))
             dt, mode, pro, gen, ek = list(info)  # ek: epilogue kind (vqx_gemm_kernel.h EK_*)
             bk = 64 if dt == L.VQX_BF16 else 32
-            if gen == 4:  # wide tap-reuse weight gradient (vqx_gemm_kernel.h wgrad_tr2_kernel)
+            if gen == 5:  # data + weight gradient in one launch (vqx_gemm_dual.hip)
+                sym = f"vqx::dual_{'k1' if pro == 1 else 'tr'}_kernel<{ek}>"
+            elif gen == 4:  # wide tap-reuse weight gradient (vqx_gemm_kernel.h wgrad_tr2_kernel)
                 sym = f"vqx::wgrad_tr2_kernel<{pro}>"  # pro slot = taps
             elif gen == 2 and mode == 2:  # tap-reuse weight gradient (vqx_gemm_kernel.h wgrad_tr_kernel)
                 sym = f"vqx::wgrad_tr_kernel<{ek}, {pro}>"  # pro slot = K groups
@@ -177,21 +179,44 @@ def conv_dgrad(dy, w, dx, **kw):
     return dx
 
 
-def conv_wgrad(p, q, slabs, *, T, r_dim, c_dim, ntaps, pad, shift_sign=1, q_prologue=L.PRO_NONE, pro_scale=1.0,
+def wgrad_args(p, q, slabs, *, T, r_dim, c_dim, ntaps, pad, shift_sign=1, q_prologue=L.PRO_NONE, pro_scale=1.0,
                splits=1, dil=1):
-    """slabs[s, r, j*c_dim + c] = sum_{n in split s} p[n, r] * pro(q[n + sign*(j*dil-pad), c]);
-    slabs fp32, or bf16 for bf16 operands (each split's partial rounded once)."""
-    _check_cuda(p, q, slabs)
     a = L.WgradArgs()
     a.p, a.q, a.slabs = ptr(p), ptr(q), ptr(slabs)
     a.n_rows, a.T, a.r_dim, a.c_dim, a.ntaps, a.pad, a.shift_sign = p.shape[0], T, r_dim, c_dim, ntaps, pad, shift_sign
     a.ldp, a.ldq = p.stride(0), q.stride(0)
     a.dtype, a.q_prologue, a.splits, a.pro_scale, a.dil = dt_code(p.dtype), q_prologue, splits, pro_scale, dil
     a.slab_dtype = dt_code(slabs.dtype)
+    return a
+
+
+def conv_wgrad(p, q, slabs, **kw):
+    """slabs[s, r, j*c_dim + c] = sum_{n in split s} p[n, r] * pro(q[n + sign*(j*dil-pad), c]);
+    slabs fp32, or bf16 for bf16 operands (each split's partial rounded once).
+    Keywords: T, r_dim, c_dim, ntaps, pad, shift_sign, q_prologue, pro_scale, splits, dil."""
+    _check_cuda(p, q, slabs)
+    a = wgrad_args(p, q, slabs, **kw)
     if _probe is not None:
-        _probe.shapes.append(f"{r_dim}x{ntaps}x{c_dim} s{splits}")
+        _probe.shapes.append(f"{a.r_dim}x{a.ntaps}x{a.c_dim} s{a.splits}")
     call("vqx_conv1d_wgrad", ctypes.byref(a), stream_ptr())
     return slabs
+
+
+def conv_dgrad_wgrad(dy, w, dx, dgrad_kw, p, q, slabs, wgrad_kw):
+    """conv_wgrad(p, q, slabs, **wgrad_kw) and conv_dgrad(dy, w, dx, **dgrad_kw)
+    of one layer (same output gradient) through vqx_conv1d_dgrad_wgrad: one
+    launch interleaving both GEMMs where a fused kernel covers the pair, else
+    the two launches in that order.  Returns True when fused."""
+    _check_cuda(dy, w, dx, p, q, slabs)
+    ad = conv_args(dy, w, dx, **dgrad_kw)
+    aw = wgrad_args(p, q, slabs, **wgrad_kw)
+    fused = ctypes.c_int32(0)
+    call("vqx_conv1d_dgrad_wgrad", ctypes.byref(ad), ctypes.byref(aw), ctypes.byref(fused), stream_ptr())
+    if _probe is not None:
+        sd = f"{ad.cin}->{ad.cout} k{ad.ntaps} epi{ad.epilogue}"
+        sw = f"{aw.r_dim}x{aw.ntaps}x{aw.c_dim} s{aw.splits}"
+        _probe.shapes.extend([f"dual {sd} + {sw}"] if fused.value else [sw, sd])
+    return bool(fused.value)
 
 
 def wgrad_tiles(n_rows, T, r_dim, c_dim, ntaps, pad, dtype, q_prologue=L.PRO_NONE, dil=1):
