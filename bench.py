@@ -50,7 +50,9 @@ def parse():
     ap.add_argument("--fp32-steps", type=int, default=5,
                     help="N=1: also time this many fp32 (parity-mode) steps, reported under 'fp32' (0 = skip)")
     ap.add_argument("--vq-reps", type=int, default=50, help="VQ kernel launches timed for the 'vq' roofline")
-    ap.add_argument("--no-probe", action="store_true", help="skip the per-launch GEMM event probe")
+    ap.add_argument("--no-probe", action="store_true", help="skip the per-launch GEMM event probe "
+                    "(default: the dominant kernel's launches in every --probe-every-th timed step; "
+                    "VQX_BENCH_KERNELS=1/2: every GEMM launch of those steps, per kernel / per layer)")
     ap.add_argument("--probe-every", type=int, default=5, help="probe one step in this many of the timed region")
     return ap.parse_args()
 
@@ -197,6 +199,19 @@ def main():
     if a.warmup:
         dict(det)  # materialise once: surfaces any asynchronous error before timing
     probe = None if a.no_probe else ops.LaunchProbe()
+    per_kernel = bool(os.environ.get("VQX_BENCH_KERNELS"))
+    if probe is not None and not per_kernel:
+        # one untimed probed step names the dominant kernel (most time per step);
+        # the timed region then stamps only that kernel's launches (an
+        # event-stamped dispatch costs ~4.6 us of queue time)
+        probe.clear()
+        ops.set_probe(probe)
+        tr.train_step((xs[0], ys[0]))
+        ops.set_probe(None)
+        per = {}
+        for sym, _, sec, _, info in probe.records():
+            per.setdefault(sym, [0.0, info])[0] += sec
+        probe.select(max(per.values(), key=lambda v: v[0])[1])
     if probe is not None:
         probe.clear()
     if world > 1:
@@ -214,6 +229,8 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     ops.set_probe(None)
+    if probe is not None:
+        probe.select(None)
     elapsed = t1 - t0
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
@@ -265,7 +282,7 @@ def main():
     else:
         out["cpu_baseline"] = None
     if rank == 0:
-        if kernels is not None and os.environ.get("VQX_BENCH_KERNELS"):
+        if kernels is not None and per_kernel:
             out["kernels"] = kernels
             if os.environ.get("VQX_BENCH_KERNELS") == "2":
                 out["layers"] = {k: (v["launches"] // max(1, n_probed), round(v["avg_us"], 1), round(v["tflops"], 1))

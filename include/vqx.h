@@ -155,7 +155,8 @@ int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream);
  * workgroups interleave the two GEMMs (each CU runs one of each, so the data
  * gradient's fused epilogue overlaps the weight gradient's main loop) where a
  * fused instance covers the pair: bf16, no prologue, the 3-tap tap-reuse
- * kernels (and 1x1 layers under VQX_DUAL=2).  Otherwise the two are launched in sequence
+ * kernels, and 1x1 layers (their data gradient's workgroups first, then the
+ * weight gradient's in the slots they free).  Otherwise the two are launched in sequence
  * (weight gradient first).  *fused (may be NULL) = 1 for one launch, 0 for
  * two.  Results equal the separate calls bit for bit.  Replaces the two
  * autograd calls of one conv in the reference backward.
@@ -486,9 +487,10 @@ const char* vqx_last_error(void);
  * (3-tap c_dim % 128 == 0, 1x1 c_dim % 256 == 0), 6 = automatic with the
  * fused 1x1 launches of vqx_conv1d_dgrad_wgrad.  The environment variable
  * VQX_TAP_REUSE=0 forces 1, VQX_TR8=0/1/2 fixes the tall kernel's choice
- * under policy 0, VQX_WGRAD_WIDE=1 selects the wide kernels, VQX_DUAL=0/1/2 sets
- * the fused launches of vqx_conv1d_dgrad_wgrad (off / 3-tap pairs, the
- * default / 3-tap and 1x1 pairs; policy 1 turns them off). */
+ * under policy 0, VQX_WGRAD_WIDE=1 selects the wide kernels, VQX_DUAL=0/1/2/3 sets
+ * the fused launches of vqx_conv1d_dgrad_wgrad (off / 3-tap pairs / 3-tap
+ * and interleaved 1x1 pairs / 3-tap and in-sequence 1x1 pairs, the default;
+ * policy 1 turns them off, policy 6 forces the interleaved 1x1 form). */
 int vqx_set_gemm_tile(int32_t policy);
 
 /* Launch probe (measurement only; not reentrant while enabled).  While on,
@@ -499,12 +501,16 @@ int vqx_set_gemm_tile(int32_t policy);
  * resumes recording (an event-stamped dispatch costs a few us of queue time,
  * so callers sample); clear() empties the log. */
 int vqx_probe_enable(int32_t on);
+/* Record only the launches whose {dtype, mode, prologue, gen, epilogue kind}
+ * equal info5 (one kernel symbol; the others launch without events); NULL =
+ * every launch. */
+int vqx_probe_select(const int32_t* info5);
 int vqx_probe_clear(void);
 int vqx_probe_count(int64_t* n);
 int vqx_probe_read(int64_t i, int32_t* info5, double* flops, float* ms);
 
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
-#define VQX_ABI_VERSION 120
+#define VQX_ABI_VERSION 121
 int vqx_version(void);
 
 #ifdef __cplusplus

@@ -497,7 +497,8 @@ def test_fused_dgrad_wgrad_equals_separate_launches(case):
     vqx_conv1d_dgrad, bit for bit (the same kernel bodies on the same tiles):
     the decoder res/skip 1x1 (GLU GroupNorm-backward epilogue, 640 rows = an
     uneven split of the two grids), the encoder skip 1x1 (residual + column
-    sums + GroupNorm-backward sums), a plain 1x1, the 3-tap tap-reuse pair
+    sums + GroupNorm-backward sums), a plain 1x1 (each 1x1 case in the
+    default in-sequence and the interleaved form), the 3-tap tap-reuse pair
     with the activation-derivative mask, the ConvTranspose form (shift -1,
     residual + column sums), and an im2col-only layer (cin 80: two launches)."""
     ops = _ops()
@@ -538,7 +539,8 @@ def test_fused_dgrad_wgrad_equals_separate_launches(case):
     elif case == "tr_convt":
         extra = dict(res=torch.randn(N, ci, device=DEV).to(dt))
     outs = []
-    for fused_call in (False, True):
+    # separate launches, the default fused call (1x1: in sequence), the interleaved 1x1 form (policy 6)
+    for fused_call in ((False, 0), (True, 0)) + (((True, 6),) if case.startswith("k1") else ()):
         o = {"dx": torch.full((N, ci), float("nan"), device=DEV, dtype=dt),
              "slabs": torch.full(slab_shape, float("nan"), device=DEV, dtype=dt)}
         kw = dict(extra)
@@ -548,9 +550,8 @@ def test_fused_dgrad_wgrad_equals_separate_launches(case):
         if case in ("k1_res", "tr_convt"):
             o["cs"] = torch.full((N // 128, ci), float("nan"), device=DEV)
             kw["colsum"] = o["cs"]
-        if fused_call:
-            # the 1x1 pairs fuse under gemm policy 6 / VQX_DUAL=2 only (vqx_gemm.hip dual_policy)
-            L.call("vqx_set_gemm_tile", 6 if case.startswith("k1") else 0)
+        if fused_call[0]:
+            L.call("vqx_set_gemm_tile", fused_call[1])
             try:
                 fused = ops.conv_dgrad_wgrad(dy, wp, o["dx"], dict(dkw, **kw), p_op, q_op, o["slabs"], wkw)
             finally:
@@ -561,10 +562,11 @@ def test_fused_dgrad_wgrad_equals_separate_launches(case):
             ops.conv_dgrad(dy, wp, o["dx"], **dkw, **kw)
         torch.cuda.synchronize()
         outs.append(o)
-    for key in outs[0]:
-        a, b = outs[0][key], outs[1][key]
-        assert torch.equal(a.view(torch.int16) if a.dtype == dt else a.view(torch.int32),
-                           b.view(torch.int16) if b.dtype == dt else b.view(torch.int32)), (case, key)
+    for other in outs[1:]:
+        for key in outs[0]:
+            a, b = outs[0][key], other[key]
+            assert torch.equal(a.view(torch.int16) if a.dtype == dt else a.view(torch.int32),
+                               b.view(torch.int16) if b.dtype == dt else b.view(torch.int32)), (case, key)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

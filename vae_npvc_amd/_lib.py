@@ -15,7 +15,7 @@ from pathlib import Path
 import torch  # noqa: F401  (loads the HIP runtime first; see module docstring)
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libvqx.so"
-ABI_VERSION = 120  # include/vqx.h VQX_ABI_VERSION
+ABI_VERSION = 121  # include/vqx.h VQX_ABI_VERSION
 
 VQX_F32, VQX_BF16 = 0, 1
 PRO_NONE, PRO_LRELU, PRO_RELU, PRO_SCALE_RELU = 0, 1, 2, 3
@@ -123,6 +123,7 @@ _SIGS = {
                          c_int32, c_float, c_float, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_int32, c_void_p, c_void_p],
     "vqx_probe_enable": [c_int32],
+    "vqx_probe_select": [c_void_p],
     "vqx_probe_clear": [],
     "vqx_probe_count": [ctypes.POINTER(c_int64)],
     "vqx_probe_read": [c_int64, ctypes.POINTER(c_int32), ctypes.POINTER(c_double), ctypes.POINTER(c_float)],

@@ -21,6 +21,8 @@ struct ProbeRec {
   double flops;
 };
 static bool g_probe_on = false;
+static bool g_probe_sel_on = false;  // record only launches whose info equals g_probe_sel
+static int g_probe_sel[5];
 static std::vector<ProbeRec> g_probe;
 static std::vector<std::pair<hipEvent_t, hipEvent_t>> g_event_pool;
 static size_t g_probe_used = 0;
@@ -33,7 +35,10 @@ void gemm_launch(const void* fn, int grid, hipStream_t s, const GemmParams& P, c
 
 void gemm_launch_args(const void* fn, int grid, hipStream_t s, void** args, const int info[5], double flops,
                       int block) {
-  if (!g_probe_on) {
+  bool rec = g_probe_on;
+  if (rec && g_probe_sel_on)
+    for (int i = 0; i < 5; ++i) rec = rec && info[i] == g_probe_sel[i];
+  if (!rec) {
     (void)hipLaunchKernel(fn, dim3(grid), dim3(block), args, 0, s);
     return;
   }
@@ -233,14 +238,17 @@ static int wgrad_prepare(const vqx_wgrad_args* a, GemmParams& P, bool& gen) {
   return 0;
 }
 
-// fused DGRAD+WGRAD launches: 0 = off, 1 = 3-tap tap-reuse pairs (default),
-// 2 = also the 1x1 pairs (env VQX_DUAL; measured: 3-tap pairs 3-8% faster than
-// two launches, 1x1 pairs 8-20% slower -- their DGRAD workgroups run ~1.5x
-// longer than the WGRAD ones, and two mixed rounds end on a DGRAD tail)
+// fused DGRAD+WGRAD launches: 0 = off, 1 = 3-tap tap-reuse pairs, 2 = also
+// the 1x1 pairs interleaved, 3 = also the 1x1 pairs with DGRAD's workgroups
+// first (default; env VQX_DUAL).  Measured (profiles/r02/dual_ab.txt): 3-tap
+// pairs interleaved 3-8% faster than two launches; 1x1 pairs interleaved
+// 8-20% slower (their DGRAD workgroups run ~1.5x longer than the WGRAD ones,
+// and two mixed rounds end on a DGRAD tail), in sequence 0.7% faster per step
+// than two launches (one ramp/tail less)
 int dual_policy() {
   static const int pol = [] {
     const char* e = getenv("VQX_DUAL");
-    return (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 1;
+    return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 3;
   }();
   return g_gemm_policy == 1 ? 0 : (g_gemm_policy == 6 ? 2 : pol);
 }
@@ -313,6 +321,13 @@ extern "C" int vqx_set_gemm_tile(int32_t policy) {
 
 extern "C" int vqx_probe_enable(int32_t on) {
   g_probe_on = on != 0;  // pause / resume; the log is kept
+  return 0;
+}
+
+extern "C" int vqx_probe_select(const int32_t* info5) {
+  g_probe_sel_on = info5 != nullptr;
+  if (info5)
+    for (int i = 0; i < 5; ++i) g_probe_sel[i] = info5[i];
   return 0;
 }
 

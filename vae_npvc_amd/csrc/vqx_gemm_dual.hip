@@ -1,7 +1,8 @@
 // A layer's data gradient (DGRAD) and weight gradient (WGRAD) in ONE launch.
-// Default for the 3-tap layers only (dual_policy): measured on the config-2
-// step, dec conv_in 109.0 -> 105.8 us and enc k3 66.1 -> 61.1 us per pair,
-// while the 1x1 pairs ran 8-20% slower (profiles/r02/dual_ab.txt).
+// Measured on the config-2 step (profiles/r02/dual_ab.txt): the 3-tap pairs
+// interleaved, dec conv_in 109.0 -> 105.8 us and enc k3 66.1 -> 61.1 us per
+// pair; the 1x1 pairs interleaved ran 8-20% slower, so by default they run in
+// sequence inside the launch (DGRAD's round first), 0.7% off the step.
 //
 // Both read the same output gradient dy and are independent.  As two launches
 // each is one round of 512 four-wave workgroups (two per CU) whose slots all
@@ -39,12 +40,19 @@ __device__ __forceinline__ bool dual_split(int b, int nd, int nw, int& sub) {
 
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
-// 1x1 layer: conv_gemm_kernel DGRAD (epilogue kind EKD) + conv_gemm_kernel WGRAD
-template <int EKD>
+// blockIdx -> (DGRAD?, index): all DGRAD workgroups first, then WGRAD's (nd % 8 == 0 keeps the XCD map)
+__device__ __forceinline__ bool seq_split(int b, int nd, int& sub) {
+  sub = b < nd ? b : b - nd;
+  return b < nd;
+}
+
+// 1x1 layer: conv_gemm_kernel DGRAD (epilogue kind EKD) + conv_gemm_kernel WGRAD;
+// SEQ: DGRAD's workgroups first (one round), WGRAD's filling the slots they free
+template <int EKD, bool SEQ>
 __global__ __launch_bounds__(256, 2) void dual_k1_kernel(GemmParams PD, GemmParams PW, int nd, int nw) {
   __shared__ __attribute__((aligned(16))) char smem[conv_gemm_smem<bf16_t, 64, 2>()];
   int sub;
-  if (dual_split(blockIdx.x, nd, nw, sub))
+  if (SEQ ? seq_split(blockIdx.x, nd, sub) : dual_split(blockIdx.x, nd, nw, sub))
     conv_gemm_body<bf16_t, MODE_DGRAD, VQX_PRO_NONE, false, 64, 2, EKD>(PD, sub, nd, smem);
   else
     conv_gemm_body<bf16_t, MODE_WGRAD, VQX_PRO_NONE, false, 64, 2, EK_NONE>(PW, sub, nw, smem);
@@ -74,19 +82,24 @@ bool launch_dual(const GemmParams& PD, int nd, const GemmParams& PW, int nw, hip
       default: return false;
     }
   } else if (PD.ntaps == 1 && PW.ntaps == 1 && PW.tap_reuse == 0 && dual_policy() >= 2) {
-    kind = 1;
+    const bool seq = dual_policy() == 3 && nd % 8 == 0;
+    kind = seq ? 3 : 1;
     switch (ekd) {
-      case EK_NONE: fn = (const void*)dual_k1_kernel<EK_NONE>; break;
-      case EK_ELEM: fn = (const void*)dual_k1_kernel<EK_ELEM>; break;
-      case EK_COLSUM: fn = (const void*)dual_k1_kernel<EK_COLSUM>; break;
-      case EK_GNBWD: fn = (const void*)dual_k1_kernel<EK_GNBWD>; break;
+      case EK_NONE: fn = seq ? (const void*)dual_k1_kernel<EK_NONE, true> : (const void*)dual_k1_kernel<EK_NONE, false>; break;
+      case EK_ELEM: fn = seq ? (const void*)dual_k1_kernel<EK_ELEM, true> : (const void*)dual_k1_kernel<EK_ELEM, false>; break;
+      case EK_COLSUM:
+        fn = seq ? (const void*)dual_k1_kernel<EK_COLSUM, true> : (const void*)dual_k1_kernel<EK_COLSUM, false>;
+        break;
+      case EK_GNBWD:
+        fn = seq ? (const void*)dual_k1_kernel<EK_GNBWD, true> : (const void*)dual_k1_kernel<EK_GNBWD, false>;
+        break;
       default: return false;
     }
   } else {
     return false;
   }
   const double flops = 2.0 * (double)PD.n_rows * PD.Nc * PD.K + 2.0 * (double)PW.n_rows * PW.Mc * PW.Nc;
-  // probe label: mode 3 = dual, prologue slot = kind (1: 1x1, 2: 3-tap), gen = 5
+  // probe label: mode 3 = dual, prologue slot = kind (1: 1x1, 2: 3-tap, 3: 1x1 in sequence), gen = 5
   const int info[5] = {VQX_BF16, 3, kind, 5, ekd};
   GemmParams pd = PD, pw = PW;
   int a = nd, b = nw;

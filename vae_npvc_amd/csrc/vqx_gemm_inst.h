@@ -22,7 +22,7 @@ void gemm_launch_args(const void* fn, int grid, hipStream_t s, void** args, cons
 // (dual_k1_kernel / dual_tr_kernel) where an instance covers the pair;
 // false = not covered (the caller launches them separately)
 bool launch_dual(const GemmParams& PD, int nd, const GemmParams& PW, int nw, hipStream_t s);
-int dual_policy();  // vqx_gemm.hip: 0 off, 1 3-tap pairs, 2 3-tap and 1x1 pairs (env VQX_DUAL)
+int dual_policy();  // vqx_gemm.hip: 0 off, 1 3-tap pairs, 2 (3) 3-tap and 1x1 pairs (1x1 in sequence) (env VQX_DUAL)
 
 // vqx_gemm.hip: tap-reuse kernel switch (env VQX_TAP_REUSE=0 turns it off, for A/B runs)
 bool tap_reuse_enabled();

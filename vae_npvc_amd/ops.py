@@ -104,8 +104,17 @@ class LaunchProbe:
     def stop(self):
         call("vqx_probe_enable", 0)
 
+    def select(self, info=None):
+        """Record only launches of the kernel with this 5-int info (records()[i][4]);
+        None = all.  Other launches skip the event pair and its queue cost."""
+        if info is None:
+            call("vqx_probe_select", None)
+        else:
+            self._sel = (ctypes.c_int32 * 5)(*info)
+            call("vqx_probe_select", self._sel)
+
     def records(self):
-        """[(rocprof symbol, flops, seconds, shape label)] after a device sync."""
+        """[(rocprof symbol, flops, seconds, shape label, info5)] after a device sync."""
         torch.cuda.synchronize()
         n = ctypes.c_int64()
         call("vqx_probe_count", ctypes.byref(n))
@@ -117,7 +126,8 @@ class LaunchProbe:
             dt, mode, pro, gen, ek = list(info)  # ek: epilogue kind (vqx_gemm_kernel.h EK_*)
             bk = 64 if dt == L.VQX_BF16 else 32
             if gen == 5:  # data + weight gradient in one launch (vqx_gemm_dual.hip)
-                sym = f"vqx::dual_{'k1' if pro == 1 else 'tr'}_kernel<{ek}>"
+                sym = {1: f"vqx::dual_k1_kernel<{ek}, false>", 2: f"vqx::dual_tr_kernel<{ek}>",
+                       3: f"vqx::dual_k1_kernel<{ek}, true>"}.get(pro, "vqx::dual_kernel")
             elif gen == 4:  # wide tap-reuse weight gradient (vqx_gemm_kernel.h wgrad_tr2_kernel)
                 sym = f"vqx::wgrad_tr2_kernel<{pro}>"  # pro slot = taps
             elif gen == 2 and mode == 2:  # tap-reuse weight gradient (vqx_gemm_kernel.h wgrad_tr_kernel)
@@ -128,13 +138,14 @@ class LaunchProbe:
                 sym = f"vqx::conv_tr_kernel<{mode}, {ek}, {pro}>"  # pro slot = channels per stage
             else:
                 sym = f"vqx::conv_gemm_kernel<{self._DT[dt]}, {mode}, {pro}, {'true' if gen else 'false'}, {bk}, 2, {ek}>"
-            out.append((sym, fl.value, ms.value * 1e-3, self.shapes[i] if i < len(self.shapes) else ""))
+            out.append((sym, fl.value, ms.value * 1e-3, self.shapes[i] if i < len(self.shapes) else "",
+                        (dt, mode, pro, gen, ek)))
         return out
 
     def summary(self, by_shape=False):
         """Aggregate per kernel symbol (by_shape: per symbol and layer shape)."""
         agg = {}
-        for key, fl, sec, shape in self.records():
+        for key, fl, sec, shape, _ in self.records():
             if by_shape:
                 key = f"{key} {shape}"
             a = agg.setdefault(key, [0, 0.0, 0.0])
