@@ -8,7 +8,8 @@ mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rs --timeout 300 --timeout-method thread > $O/tests.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> $O/tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-VQX_BENCH_KERNELS=2 timeout -k 10 400 python bench.py > $O/bench.log 2>&1
+timeout -k 10 400 python bench.py > $O/bench_default.json 2> $O/bench_default.err || exit $?
+VQX_BENCH_KERNELS=2 timeout -k 10 400 python bench.py --no-cpu-baseline > $O/bench.log 2>&1
 rc=$?; echo "bench rc=$rc" >> $O/bench.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline > $O/prof.log 2>&1 || exit $?
