@@ -14,20 +14,23 @@
 // ramp and one tail cover both.  Each workgroup runs the unchanged kernel body
 // (vqx_gemm_kernel.h conv_gemm_body / conv_tr_body / wgrad_tr_body) on its own
 // tile grid; the branch is uniform per workgroup.
+#include <stdlib.h>
+
 #include "vqx_gemm_inst.h"
 
 namespace vqx {
 
-// blockIdx -> (DGRAD?, workgroup index in that GEMM's grid): 16-block groups
-// of 8 DGRAD + 8 WGRAD while both have workgroups left, then the rest of
-// DGRAD, then the rest of WGRAD.  In the paired region the sub-index keeps
-// blockIdx % 8 (the XCD), so each body's XCD-aware tile map still applies.
-__device__ __forceinline__ bool dual_split(int b, int nd, int nw, int& sub) {
-  const int m = (nd < nw ? nd : nw) & ~7;
+// blockIdx -> (DGRAD?, workgroup index in that GEMM's grid): groups of
+// ch DGRAD + ch WGRAD blocks (ch % 8 == 0) while both have workgroups left,
+// then the rest of DGRAD, then the rest of WGRAD.  In the paired region the
+// sub-index keeps blockIdx % 8 (the XCD), so each body's XCD-aware tile map
+// still applies.
+__device__ __forceinline__ bool dual_split(int b, int nd, int nw, int ch, int& sub) {
+  const int m = (nd < nw ? nd : nw) / ch * ch;
   if (b < 2 * m) {
-    const int g = b >> 4, x = b & 15;
-    sub = 8 * g + (x & 7);
-    return x < 8;
+    const int g = b / (2 * ch), x = b - g * 2 * ch;
+    sub = g * ch + (x < ch ? x : x - ch);
+    return x < ch;
   }
   const int j = b - 2 * m;
   if (j < nd - m) {
@@ -49,10 +52,10 @@ __device__ __forceinline__ bool seq_split(int b, int nd, int& sub) {
 // 1x1 layer: conv_gemm_kernel DGRAD (epilogue kind EKD) + conv_gemm_kernel WGRAD;
 // SEQ: DGRAD's workgroups first (one round), WGRAD's filling the slots they free
 template <int EKD, bool SEQ>
-__global__ __launch_bounds__(256, 2) void dual_k1_kernel(GemmParams PD, GemmParams PW, int nd, int nw) {
+__global__ __launch_bounds__(256, 2) void dual_k1_kernel(GemmParams PD, GemmParams PW, int nd, int nw, int ch) {
   __shared__ __attribute__((aligned(16))) char smem[conv_gemm_smem<bf16_t, 64, 2>()];
   int sub;
-  if (SEQ ? seq_split(blockIdx.x, nd, sub) : dual_split(blockIdx.x, nd, nw, sub))
+  if (SEQ ? seq_split(blockIdx.x, nd, sub) : dual_split(blockIdx.x, nd, nw, ch, sub))
     conv_gemm_body<bf16_t, MODE_DGRAD, VQX_PRO_NONE, false, 64, 2, EKD>(PD, sub, nd, smem);
   else
     conv_gemm_body<bf16_t, MODE_WGRAD, VQX_PRO_NONE, false, 64, 2, EK_NONE>(PW, sub, nw, smem);
@@ -60,10 +63,10 @@ __global__ __launch_bounds__(256, 2) void dual_k1_kernel(GemmParams PD, GemmPara
 
 // 3-tap layer: conv_tr_kernel DGRAD (epilogue kind EKD) + wgrad_tr_kernel
 template <int EKD>
-__global__ __launch_bounds__(256, 2) void dual_tr_kernel(GemmParams PD, GemmParams PW, int nd, int nw) {
+__global__ __launch_bounds__(256, 2) void dual_tr_kernel(GemmParams PD, GemmParams PW, int nd, int nw, int ch) {
   __shared__ __attribute__((aligned(16))) char smem[cmax(conv_tr_smem<32>(), wgrad_tr_smem<1>())];
   int sub;
-  if (dual_split(blockIdx.x, nd, nw, sub)) conv_tr_body<MODE_DGRAD, EKD, 32>(PD, sub, nd, smem);
+  if (dual_split(blockIdx.x, nd, nw, ch, sub)) conv_tr_body<MODE_DGRAD, EKD, 32>(PD, sub, nd, smem);
   else wgrad_tr_body<EK_NONE, 1>(PW, sub, nw, smem);
 }
 
@@ -101,9 +104,14 @@ bool launch_dual(const GemmParams& PD, int nd, const GemmParams& PW, int nw, hip
   const double flops = 2.0 * (double)PD.n_rows * PD.Nc * PD.K + 2.0 * (double)PW.n_rows * PW.Mc * PW.Nc;
   // probe label: mode 3 = dual, prologue slot = kind (1: 1x1, 2: 3-tap, 3: 1x1 in sequence), gen = 5
   const int info[5] = {VQX_BF16, 3, kind, 5, ekd};
+  static const int chunk = [] {  // interleave period (blocks of each GEMM per group; env VQX_DUAL_CHUNK, A/B)
+    const char* e = getenv("VQX_DUAL_CHUNK");
+    const int c = e ? atoi(e) : 256;
+    return c >= 8 && c % 8 == 0 ? c : 8;
+  }();
   GemmParams pd = PD, pw = PW;
-  int a = nd, b = nw;
-  void* args[] = {(void*)&pd, (void*)&pw, (void*)&a, (void*)&b};
+  int a = nd, b = nw, c = chunk;
+  void* args[] = {(void*)&pd, (void*)&pw, (void*)&a, (void*)&b, (void*)&c};
   gemm_launch_args(fn, nd + nw, s, args, info, flops, 256);
   return true;
 }
