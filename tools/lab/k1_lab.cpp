@@ -151,8 +151,8 @@ int main() {
 #ifndef VQX_EPI_PREVEC_DGRAD
 #define VQX_EPI_PREVEC_DGRAD 0
 #endif
-    printf("nst%d prevec_dgrad%d prefetch%d/dgrad%d/late%d stagger%d mode%d %-20s %7.1f us %7.1f TF\n", K1_NST,
-           VQX_EPI_PREVEC_DGRAD, VQX_EPI_PREFETCH, VQX_EPI_PREFETCH_DGRAD, VQX_EPI_PREFETCH_LATE, VQX_GEMM_STAGGER,
+    printf("nst%d prevec_dgrad%d prefetch%d/dgrad%d/late%d/slab%d stagger%d mode%d %-20s %7.1f us %7.1f TF\n", K1_NST,
+           VQX_EPI_PREVEC_DGRAD, VQX_EPI_PREFETCH, VQX_EPI_PREFETCH_DGRAD, VQX_EPI_PREFETCH_LATE, VQX_EPI_SLAB_PREFETCH, VQX_GEMM_STAGGER,
            VQX_LAB_MODE, c.name, us, fl / us * 1e-6);
   }
   CK(hipDeviceSynchronize());

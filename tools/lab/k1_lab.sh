@@ -16,6 +16,7 @@ if [ "$1" = build ]; then
     [ ${v:0:1} = n ] && D="$D -DK1_NST=$st"
     [ ${v:0:1} = l ] && D="$D -DVQX_EPI_PREFETCH_DGRAD=1 -DVQX_EPI_PREFETCH_LATE=$st"
     [ ${v:0:1} = f ] && D="$D -DVQX_EPI_PREFETCH_LATE=$st"
+    [ ${v:0:1} = e ] && D="$D -DVQX_EPI_SLAB_PREFETCH=$st"
     /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=fast -I ../../include \
       -I ../../vae_npvc_amd/csrc $D k1_lab.cpp -o k1_lab_$v.bin &
   done
