@@ -876,3 +876,48 @@ def test_gnadd_with_in_launch_statistics(dtype, B, T, tile):
         outs.append((mr, y, y2))
     for u, v in zip(*outs):
         assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("n", [4096 * 3 + 4, 1001, 4099, 257])
+def test_adam_step_vector_and_scalar_paths_track_torch(n):
+    """vqx_grad_sq_norm + vqx_adam_hyper + vqx_adam_step (clip, Adam, StepLR;
+    trainer/basic.py:63-75) over three steps (every step clips): the 16-B path
+    (16-B aligned buffers; its scalar tail when n % 4 != 0) against the scalar
+    path (the same buffers offset by one float) and both against
+    torch.optim.Adam (single-tensor, CPU fp32) fed the same clipped gradient,
+    to 1e-6 relative.  The two paths are not bit-identical: the 16-B path's
+    packed v_pk_mul/add_f32 differ from the scalar ops by one ulp on about
+    half of the second moments (measured 1.1e-13 absolute,
+    tools/adam_dbg.py)."""
+    ops = _ops()
+    torch.manual_seed(41)
+    lr, betas, eps, max_norm = 2e-4, (0.5, 0.999), 1e-8, 1.0
+    p0 = torch.randn(n)
+    pc = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([pc], lr=lr, betas=betas, eps=eps, foreach=False)
+    runs = []
+    for off in (0, 1):
+        base = {k: torch.zeros(n + 4, device=DEV) for k in ("p", "g", "m", "v")}
+        runs.append(dict({k: t[off:off + n] for k, t in base.items()},
+                         step=torch.zeros(1, dtype=torch.int64, device=DEV), hyper=torch.zeros(16, device=DEV),
+                         part=torch.zeros(2048, device=DEV), sumsq=torch.zeros(1, device=DEV)))
+        runs[-1]["p"].copy_(p0.to(DEV))
+    for s in range(3):
+        gs = torch.randn(n) * (3.0 if s == 1 else 0.01)
+        for r in runs:
+            r["g"].copy_(gs.to(DEV))
+        # one clip norm for both (the norm's own summation order follows the buffer's alignment)
+        ops.grad_sq_norm(runs[0]["g"], runs[0]["part"], runs[0]["sumsq"])
+        for r in runs:
+            ops.adam_hyper(r["step"], lr, 1.0, 10 ** 9, betas[0], betas[1], eps, r["hyper"])
+            ops.adam_step(r["p"], r["g"], r["m"], r["v"], r["hyper"], runs[0]["sumsq"], max_norm)
+        torch.cuda.synchronize()
+        for k in ("p", "m", "v"):
+            assert relerr(runs[0][k], runs[1][k]) < 1e-6, (s, k)
+        tn = runs[0]["sumsq"].cpu().sqrt()
+        coef = (torch.tensor(max_norm) / (tn + 1e-6)).clamp(max=1.0)
+        pc.grad = gs * coef
+        opt.step()
+        st = opt.state[pc]
+        assert relerr(runs[0]["p"], pc.detach()) < 1e-6, s
+        assert relerr(runs[0]["m"], st["exp_avg"]) < 1e-6 and relerr(runs[0]["v"], st["exp_avg_sq"]) < 1e-6, s

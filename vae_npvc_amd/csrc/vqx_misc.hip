@@ -1579,6 +1579,24 @@ __global__ __launch_bounds__(256) void radam_kernel(float* __restrict__ p, const
   }
 }
 
+// One Adam element update, torch's op order (bit-identical to torch.optim.Adam
+// on the same fp32 inputs)
+__device__ __forceinline__ void adam_elem(float& pi, float gi, float& mi, float& vi, float w, float b2, float omb2,
+                                          float bc2s, float eps, float step_size) {
+  // plain operators under contract(off): every product and sum is rounded on
+  // its own (the __f*_rn helpers are inlined bodies that -ffp-contract=fast
+  // may still fuse into FMAs)
+#pragma clang fp contract(off)
+  // torch.lerp: weight < 0.5 ? m + w*(g-m) : g - (g-m)*(1-w)
+  mi = (w < 0.5f) ? mi + w * (gi - mi) : gi - (gi - mi) * (1.f - w);
+  vi = vi * b2;
+  vi = vi + (omb2 * gi) * gi;
+  const float den = __fsqrt_rn(vi) / bc2s + eps;
+  pi = pi + (-step_size) * (mi / den);
+}
+
+// 16-B accesses (4 elements per thread per step, 16 loads in flight) when all
+// four buffers are 16-B aligned, else one element at a time; the tail is scalar.
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                    const float* __restrict__ hyper, const float* __restrict__ sumsq,
@@ -1591,16 +1609,31 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   }
   const float step_size = hyper[1], bc2s = hyper[2];
   const float w = hyper[4], b2 = hyper[5], omb2 = hyper[6], eps = hyper[7];
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const float gi = __fmul_rn(g[i], coef);
-    float mi = m[i];
-    // torch.lerp: weight < 0.5 ? m + w*(g-m) : g - (g-m)*(1-w)
-    mi = (w < 0.5f) ? __fadd_rn(mi, __fmul_rn(w, __fsub_rn(gi, mi)))
-                    : __fsub_rn(gi, __fmul_rn(__fsub_rn(gi, mi), 1.f - w));
-    float vi = __fmul_rn(v[i], b2);
-    vi = __fadd_rn(vi, __fmul_rn(__fmul_rn(omb2, gi), gi));
-    const float den = __fadd_rn(__fdiv_rn(__fsqrt_rn(vi), bc2s), eps);
-    p[i] = __fadd_rn(p[i], __fmul_rn(-step_size, __fdiv_rn(mi, den)));
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (int64_t)gridDim.x * blockDim.x;
+  int64_t done = 0;
+  if ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0) {
+    const int64_t n4 = n >> 2;
+    for (int64_t i = tid; i < n4; i += nth) {
+      f32x4_t pv = ((const f32x4_t*)p)[i], gv = ((const f32x4_t*)g)[i];
+      f32x4_t mv = ((const f32x4_t*)m)[i], vv = ((const f32x4_t*)v)[i];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float pi = pv[e], mi = mv[e], vi = vv[e];
+        adam_elem(pi, __fmul_rn(gv[e], coef), mi, vi, w, b2, omb2, bc2s, eps, step_size);
+        pv[e] = pi;
+        mv[e] = mi;
+        vv[e] = vi;
+      }
+      ((f32x4_t*)p)[i] = pv;
+      ((f32x4_t*)m)[i] = mv;
+      ((f32x4_t*)v)[i] = vv;
+    }
+    done = n4 << 2;
+  }
+  for (int64_t i = done + tid; i < n; i += nth) {
+    float pi = p[i], mi = m[i], vi = v[i];
+    adam_elem(pi, __fmul_rn(g[i], coef), mi, vi, w, b2, omb2, bc2s, eps, step_size);
+    p[i] = pi;
     m[i] = mi;
     v[i] = vi;
   }
@@ -1956,7 +1989,7 @@ extern "C" int vqx_adam_hyper(int64_t* step, double lr0, double gamma, int32_t s
 
 extern "C" int vqx_adam_step(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper,
                              const float* sumsq, float max_norm, vqx_stream_t stream) {
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for((n + 3) / 4, 256, 4096)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
                      hyper, sumsq, max_norm);
   return launch_status("vqx_adam_step");
 }
