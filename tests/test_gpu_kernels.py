@@ -490,7 +490,7 @@ def test_gnbwd_epilogue_matches_standalone(glu, tile):
         assert relerr(a, b) < 2e-2, relerr(a, b)
 
 
-@pytest.mark.parametrize("case", ["k1_glu", "k1_res", "k1_plain", "tr_mask", "tr_convt", "gen"])
+@pytest.mark.parametrize("case", ["k1_glu", "k1_res", "k1_plain", "tr_mask", "tr_convt", "gen", "tr_full", "k1_full"])
 def test_fused_dgrad_wgrad_equals_separate_launches(case):
     """vqx_conv1d_dgrad_wgrad (vqx_gemm_dual.hip: one launch interleaving a
     layer's data- and weight-gradient GEMMs) against vqx_conv1d_wgrad +
@@ -500,16 +500,18 @@ def test_fused_dgrad_wgrad_equals_separate_launches(case):
     sums + GroupNorm-backward sums), a plain 1x1 (each 1x1 case in the
     default in-sequence and the interleaved form), the 3-tap tap-reuse pair
     with the activation-derivative mask, the ConvTranspose form (shift -1,
-    residual + column sums), and an im2col-only layer (cin 80: two launches)."""
+    residual + column sums), and an im2col-only layer (cin 80: two launches);
+    *_full at the bench size (64 x 256 frames: 512 + 512 workgroups, so the
+    256-block interleaved groups are exercised)."""
     ops = _ops()
     from vae_npvc_amd import _lib as L
     torch.manual_seed(31)
     dt = torch.bfloat16
-    B, T = 4, 256
+    B, T = (64, 256) if case.endswith("_full") else (4, 256)
     N = B * T
     k = 3 if case.startswith("tr") else 1
     cfg = {"k1_glu": (640, 512), "k1_res": (512, 512), "k1_plain": (512, 768), "tr_mask": (1024, 512),
-           "tr_convt": (512, 1024), "gen": (80, 512)}[case]
+           "tr_convt": (512, 1024), "gen": (80, 512), "tr_full": (1024, 512), "k1_full": (512, 512)}[case]
     co, ci = cfg                                   # forward layer cout, cin
     dy = torch.randn(N, co, device=DEV).to(dt)
     x = torch.randn(N, ci, device=DEV).to(dt)
@@ -518,7 +520,7 @@ def test_fused_dgrad_wgrad_equals_separate_launches(case):
     sign, r_dim, c_dim, p_op, q_op = 1, co, ci, dy, x
     if case == "tr_convt":
         sign, r_dim, c_dim, p_op, q_op = -1, ci, co, x, dy
-    splits = 8
+    splits = 32 if case == "k1_full" else 8
     slab_shape = (splits, r_dim, k * c_dim)
     wkw = dict(T=T, r_dim=r_dim, c_dim=c_dim, ntaps=k, pad=(k - 1) // 2, shift_sign=sign, splits=splits)
     extra = {}
@@ -534,7 +536,7 @@ def test_fused_dgrad_wgrad_equals_separate_launches(case):
         ops.groupnorm_stats(u, T, 1, torch.empty(B * 24, device=DEV), mr)
         extra = dict(gn_h=u, gn_mr=mr, gn_gamma=torch.randn(ci, device=DEV), gn_beta=torch.randn(ci, device=DEV),
                      res=torch.randn(N, ci, device=DEV).to(dt))
-    elif case == "tr_mask":
+    elif case in ("tr_mask", "tr_full"):
         extra = dict(mask=torch.randn(N, ci, device=DEV).to(dt), mask_slope=0.2)
     elif case == "tr_convt":
         extra = dict(res=torch.randn(N, ci, device=DEV).to(dt))
