@@ -485,11 +485,13 @@ const char* vqx_last_error(void);
  * wherever T % 256 == 0 and the frames divide, 4 = the 128-frame tap-reuse
  * kernel only, 5 = automatic with the wide 8-wave weight-gradient kernels
  * (3-tap c_dim % 128 == 0, 1x1 c_dim % 256 == 0), 6 = automatic with the
- * fused 1x1 launches of vqx_conv1d_dgrad_wgrad.  The environment variable
+ * fused 1x1 launches of vqx_conv1d_dgrad_wgrad, 7 = their three-workgroups-
+ * per-CU form.  The environment variable
  * VQX_TAP_REUSE=0 forces 1, VQX_TR8=0/1/2 fixes the tall kernel's choice
- * under policy 0, VQX_WGRAD_WIDE=1 selects the wide kernels, VQX_DUAL=0/1/2/3 sets
+ * under policy 0, VQX_WGRAD_WIDE=1 selects the wide kernels, VQX_DUAL=0/1/2/3/4 sets
  * the fused launches of vqx_conv1d_dgrad_wgrad (off / 3-tap pairs / 3-tap
- * and interleaved 1x1 pairs / 3-tap and in-sequence 1x1 pairs, the default;
+ * and interleaved 1x1 pairs / 3-tap and in-sequence 1x1 pairs, the default /
+ * 3-tap and three-per-CU 1x1 pairs;
  * policy 1 turns them off, policy 6 forces the interleaved 1x1 form). */
 int vqx_set_gemm_tile(int32_t policy);
 

@@ -498,7 +498,8 @@ def test_fused_dgrad_wgrad_equals_separate_launches(case):
     the decoder res/skip 1x1 (GLU GroupNorm-backward epilogue, 640 rows = an
     uneven split of the two grids), the encoder skip 1x1 (residual + column
     sums + GroupNorm-backward sums), a plain 1x1 (each 1x1 case in the
-    default in-sequence and the interleaved form), the 3-tap tap-reuse pair
+    default in-sequence, the interleaved and the three-per-CU form), the
+    3-tap tap-reuse pair
     with the activation-derivative mask, the ConvTranspose form (shift -1,
     residual + column sums), and an im2col-only layer (cin 80: two launches);
     *_full at the bench size (64 x 256 frames: 512 + 512 workgroups, so the
@@ -542,7 +543,7 @@ def test_fused_dgrad_wgrad_equals_separate_launches(case):
         extra = dict(res=torch.randn(N, ci, device=DEV).to(dt))
     outs = []
     # separate launches, the default fused call (1x1: in sequence), the interleaved 1x1 form (policy 6)
-    for fused_call in ((False, 0), (True, 0)) + (((True, 6),) if case.startswith("k1") else ()):
+    for fused_call in ((False, 0), (True, 0)) + (((True, 6), (True, 7)) if case.startswith("k1") else ()):
         o = {"dx": torch.full((N, ci), float("nan"), device=DEV, dtype=dt),
              "slabs": torch.full(slab_shape, float("nan"), device=DEV, dtype=dt)}
         kw = dict(extra)

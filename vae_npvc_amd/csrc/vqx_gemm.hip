@@ -64,7 +64,8 @@ void gemm_launch_args(const void* fn, int grid, hipStream_t s, void** args, cons
 // 2 / 3 = tap reuse through conv_tr8_kernel with 1 / 2 frame segments where it
 // applies, 4 = tap reuse through conv_tr_kernel only, 5 = automatic with the
 // wide weight gradients (wgrad_tr2_kernel: 3-tap c_dim % 128 == 0, 1x1 c_dim % 256 == 0),
-// 6 = automatic with the fused 1x1 DGRAD+WGRAD launches too (dual_policy 2)
+// 6 = automatic with the fused 1x1 DGRAD+WGRAD launches interleaved (dual_policy 2),
+// 7 = ... with the three-per-CU 1x1 form (dual_policy 4)
 static int g_gemm_policy = 0;
 
 bool tap_reuse_enabled() {
@@ -240,7 +241,8 @@ static int wgrad_prepare(const vqx_wgrad_args* a, GemmParams& P, bool& gen) {
 
 // fused DGRAD+WGRAD launches: 0 = off, 1 = 3-tap tap-reuse pairs, 2 = also
 // the 1x1 pairs interleaved, 3 = also the 1x1 pairs with DGRAD's workgroups
-// first (default; env VQX_DUAL).  Measured (profiles/r02/dual_ab.txt): 3-tap
+// first (default; env VQX_DUAL), 4 = the 1x1 pairs three workgroups per CU
+// (32-deep K-tiles, 48 KiB).  Measured (profiles/r02/dual_ab.txt): 3-tap
 // pairs interleaved 3-8% faster than two launches; 1x1 pairs interleaved
 // 8-20% slower (their DGRAD workgroups run ~1.5x longer than the WGRAD ones,
 // and two mixed rounds end on a DGRAD tail), in sequence 0.7% faster per step
@@ -248,9 +250,9 @@ static int wgrad_prepare(const vqx_wgrad_args* a, GemmParams& P, bool& gen) {
 int dual_policy() {
   static const int pol = [] {
     const char* e = getenv("VQX_DUAL");
-    return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 3;
+    return (e && e[0] >= '0' && e[0] <= '4') ? e[0] - '0' : 3;
   }();
-  return g_gemm_policy == 1 ? 0 : (g_gemm_policy == 6 ? 2 : pol);
+  return g_gemm_policy == 1 ? 0 : (g_gemm_policy == 6 ? 2 : (g_gemm_policy == 7 ? 4 : pol));
 }
 static bool dual_enabled() { return dual_policy() > 0; }
 
@@ -314,7 +316,7 @@ extern "C" int vqx_wgrad_tiles(int64_t n_rows, int32_t T, int32_t r_dim, int32_t
 }
 
 extern "C" int vqx_set_gemm_tile(int32_t policy) {
-  if (policy < 0 || policy > 6) { set_error("vqx_set_gemm_tile: policy %d not in 0..6", policy); return -1; }
+  if (policy < 0 || policy > 7) { set_error("vqx_set_gemm_tile: policy %d not in 0..7", policy); return -1; }
   g_gemm_policy = policy;
   return 0;
 }

@@ -61,6 +61,21 @@ __global__ __launch_bounds__(256, 2) void dual_k1_kernel(GemmParams PD, GemmPara
     conv_gemm_body<bf16_t, MODE_WGRAD, VQX_PRO_NONE, false, 64, 2, EK_NONE>(PW, sub, nw, smem);
 }
 
+// 1x1 layer, three workgroups per CU: both bodies on 32-deep K-tiles in a
+// 3-deep ring (48 KiB of LDS instead of 64, <= 168 VGPRs), DGRAD's workgroups
+// first, so each CU holds two DGRAD workgroups and one WGRAD workgroup while
+// DGRAD's round runs (the MFMA-bound WGRAD beside the epilogue-bound DGRAD)
+template <int EKD>
+__global__ __launch_bounds__(256, 3) void dual_k1w_kernel(GemmParams PD, GemmParams PW, int nd, int nw, int ch) {
+  __shared__ __attribute__((aligned(16))) char smem[conv_gemm_smem<bf16_t, 32, 3>()];
+  int sub;
+  (void)ch;
+  if (seq_split(blockIdx.x, nd, sub))
+    conv_gemm_body<bf16_t, MODE_DGRAD, VQX_PRO_NONE, false, 32, 3, EKD>(PD, sub, nd, smem);
+  else
+    conv_gemm_body<bf16_t, MODE_WGRAD, VQX_PRO_NONE, false, 32, 3, EK_NONE>(PW, sub, nw, smem);
+}
+
 // 3-tap layer: conv_tr_kernel DGRAD (epilogue kind EKD) + wgrad_tr_kernel
 template <int EKD>
 __global__ __launch_bounds__(256, 2) void dual_tr_kernel(GemmParams PD, GemmParams PW, int nd, int nw, int ch) {
@@ -84,6 +99,15 @@ bool launch_dual(const GemmParams& PD, int nd, const GemmParams& PW, int nw, hip
       case EK_COLSUM: fn = (const void*)dual_tr_kernel<EK_COLSUM>; break;
       default: return false;
     }
+  } else if (PD.ntaps == 1 && PW.ntaps == 1 && PW.tap_reuse == 0 && dual_policy() == 4 && nd % 8 == 0) {
+    kind = 4;
+    switch (ekd) {
+      case EK_NONE: fn = (const void*)dual_k1w_kernel<EK_NONE>; break;
+      case EK_ELEM: fn = (const void*)dual_k1w_kernel<EK_ELEM>; break;
+      case EK_COLSUM: fn = (const void*)dual_k1w_kernel<EK_COLSUM>; break;
+      case EK_GNBWD: fn = (const void*)dual_k1w_kernel<EK_GNBWD>; break;
+      default: return false;
+    }
   } else if (PD.ntaps == 1 && PW.ntaps == 1 && PW.tap_reuse == 0 && dual_policy() >= 2) {
     const bool seq = dual_policy() == 3 && nd % 8 == 0;
     kind = seq ? 3 : 1;
@@ -102,7 +126,7 @@ bool launch_dual(const GemmParams& PD, int nd, const GemmParams& PW, int nw, hip
     return false;
   }
   const double flops = 2.0 * (double)PD.n_rows * PD.Nc * PD.K + 2.0 * (double)PW.n_rows * PW.Mc * PW.Nc;
-  // probe label: mode 3 = dual, prologue slot = kind (1: 1x1, 2: 3-tap, 3: 1x1 in sequence), gen = 5
+  // probe label: mode 3 = dual, prologue slot = kind (1: 1x1, 2: 3-tap, 3: 1x1 in sequence, 4: 1x1 three per CU), gen = 5
   const int info[5] = {VQX_BF16, 3, kind, 5, ekd};
   static const int chunk = [] {  // interleave period (blocks of each GEMM per group; env VQX_DUAL_CHUNK, A/B)
     const char* e = getenv("VQX_DUAL_CHUNK");

@@ -127,7 +127,7 @@ class LaunchProbe:
             bk = 64 if dt == L.VQX_BF16 else 32
             if gen == 5:  # data + weight gradient in one launch (vqx_gemm_dual.hip)
                 sym = {1: f"vqx::dual_k1_kernel<{ek}, false>", 2: f"vqx::dual_tr_kernel<{ek}>",
-                       3: f"vqx::dual_k1_kernel<{ek}, true>"}.get(pro, "vqx::dual_kernel")
+                       3: f"vqx::dual_k1_kernel<{ek}, true>", 4: f"vqx::dual_k1w_kernel<{ek}>"}.get(pro, "vqx::dual_kernel")
             elif gen == 4:  # wide tap-reuse weight gradient (vqx_gemm_kernel.h wgrad_tr2_kernel)
                 sym = f"vqx::wgrad_tr2_kernel<{pro}>"  # pro slot = taps
             elif gen == 2 and mode == 2:  # tap-reuse weight gradient (vqx_gemm_kernel.h wgrad_tr_kernel)
