@@ -1,5 +1,13 @@
-import sys, torch
-sys.path.insert(0, "/root/repo")
+"""Vector (16-B) vs scalar path of vqx_adam_step on the same data, three clipped
+steps: mismatch counts and the largest difference per state tensor (the packed
+f32 ops differ from the scalar ones by an ulp on some second moments).
+usage (GPU box): python tools/adam_dbg.py"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from vae_npvc_amd import ops
 DEV = "cuda"
 n = 12292
