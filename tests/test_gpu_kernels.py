@@ -610,12 +610,15 @@ def test_gn_bwd_matches_torch_autograd(dtype, glu, C, T):
 
 @pytest.mark.parametrize("mode", ["fwd", "dgrad"])
 @pytest.mark.parametrize("n_utt,T,cin,cout", [(1, 128, 512, 512), (3, 128, 512, 1024), (2, 256, 1024, 512),
-                                               (1, 384, 128, 512), (2, 256, 512, 80)])
+                                               (1, 384, 128, 512), (2, 256, 512, 80), (2, 256, 80, 512),
+                                               (1, 256, 512, 208), (1, 128, 48, 256)])
 def test_conv_tap_reuse_matches_im2col_and_fp64(mode, n_utt, T, cin, cout):
     """The tap-reuse kernel (vqx_gemm_kernel.h conv_tr_kernel: one staged
     130-frame window for all three taps, halo frames zeroed at utterance
     edges) against the implicit-im2col kernel on the same bf16 operands and
-    against fp64 torch, with a bias + residual epilogue and fp32 output."""
+    against fp64 torch, with a bias + residual epilogue and fp32 output.  K
+    sides of 80, 208 and 48 channels (cin % 32 != 0: 16-channel stages, e.g.
+    the 80-mel input conv) run the same kernel with BKC = 16."""
     ops = _ops()
     from vae_npvc_amd import _lib as L
     torch.manual_seed(7)

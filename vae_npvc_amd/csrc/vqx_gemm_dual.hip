@@ -90,7 +90,7 @@ bool launch_dual(const GemmParams& PD, int nd, const GemmParams& PW, int nw, hip
   const int ekd = pick_ek(PD.epi);
   const void* fn = nullptr;
   int kind = 0;
-  if (tap_reuse_ok(PD, true, false) && tr8_segs(PD) == 0 && tr_stage_channels() == 32) {
+  if (tap_reuse_ok(PD, true, false) && tr8_segs(PD) == 0 && tr_stage_channels() == 32 && PD.kcin % 32 == 0) {
     if (PW.tap_reuse != 1) return false;
     kind = 2;
     switch (ekd) {

@@ -28,10 +28,12 @@ int dual_policy();  // vqx_gemm.hip: 0 off, 1 3-tap pairs, 2 (3) 3-tap and 1x1 p
 bool tap_reuse_enabled();
 
 // conv_tr_kernel applies: bf16, no prologue, 3 taps / pad 1, 32-channel K
-// slices, and every 128-frame tile inside one utterance
+// slices (16-channel slices when cin % 32 != 0, e.g. the 80-mel input conv),
+// and every 128-frame tile inside one utterance
 inline bool tap_reuse_ok(const GemmParams& P, bool bf16, bool gen) {
-  return bf16 && !gen && P.pro == VQX_PRO_NONE && P.ntaps == 3 && P.pad == 1 && P.dil == 1 && P.kcin % 32 == 0 &&
-         P.K == 3 * P.kcin && P.T % 128 == 0 && P.n_rows % 128 == 0 && tap_reuse_enabled();
+  return bf16 && P.pro == VQX_PRO_NONE && P.ntaps == 3 && P.pad == 1 && P.dil == 1 && P.kcin % 16 == 0 &&
+         (!gen || P.kcin % 32 != 0) && P.K == 3 * P.kcin && P.T % 128 == 0 && P.n_rows % 128 == 0 &&
+         tap_reuse_enabled();
 }
 
 // wgrad_tr_kernel applies: bf16, no prologue, 3 taps / pad 1, c_dim % 64 == 0,
@@ -61,7 +63,7 @@ int tr_stage_channels();
 // (profiles/r02/tr_lab.txt), so it is never picked automatically.
 int tr8_policy();
 inline int tr8_segs(const GemmParams& P) {
-  if (P.T % 256 || tr_stage_channels() != 32) return 0;
+  if (P.T % 256 || tr_stage_channels() != 32 || P.kcin % 32) return 0;
   const int pol = tr8_policy();
   const int tn = (P.Nc + kBN - 1) / kBN;
   if (pol == 0) return 0;
@@ -81,7 +83,7 @@ void launch_tr(const GemmParams& P, int grid, hipStream_t s) {
     else gemm_launch((const void*)conv_tr8_kernel<MODE, EK, 1>, Q.tiles_m * Q.tiles_n, s, Q, info8, flops, 512);
     return;
   }
-  const int bkc = tr_stage_channels();
+  const int bkc = P.kcin % 32 == 0 ? tr_stage_channels() : 16;
   // gen = 2: tap-reuse kernel; the prologue slot carries the stage depth in channels
   const int info[5] = {VQX_BF16, MODE, bkc, 2, EK};
   if (bkc == 16) gemm_launch((const void*)conv_tr_kernel<MODE, EK, 16>, grid, s, P, info, flops);
@@ -93,6 +95,21 @@ inline int pick_ek(int epi) {
   for (int ek = EK_NONE; ek < EK_ALL; ++ek)
     if ((epi & ~ek_mask(ek)) == 0) return ek;
   return EK_ALL;
+}
+
+// tap-reuse FWD / DGRAD with the epilogue kind of P.epi
+template <int MODE>
+void dispatch_tr(const GemmParams& P, int grid, hipStream_t s) {
+  switch (pick_ek(P.epi)) {
+    case EK_NONE: launch_tr<MODE, EK_NONE>(P, grid, s); break;
+    case EK_ELEM: launch_tr<MODE, EK_ELEM>(P, grid, s); break;
+    case EK_GNADD: launch_tr<MODE, EK_GNADD>(P, grid, s); break;
+    case EK_SPLIT: launch_tr<MODE, EK_SPLIT>(P, grid, s); break;
+    case EK_COLSUM: launch_tr<MODE, EK_COLSUM>(P, grid, s); break;
+    case EK_GNSTATS: launch_tr<MODE, EK_GNSTATS>(P, grid, s); break;
+    case EK_GNBWD: launch_tr<MODE, EK_GNBWD>(P, grid, s); break;
+    default: launch_tr<MODE, EK_ALL>(P, grid, s); break;
+  }
 }
 
 template <typename T, int MODE, int PRO, bool GEN, int EK>
@@ -127,6 +144,12 @@ void launch_mode_dt(const GemmParams& P, int grid, bool bf16, bool gen, hipStrea
     return;
   }
   if (gen) {
+    if constexpr (MODE != MODE_WGRAD) {  // 16-channel tap reuse (cin % 32 != 0, e.g. the 80-mel input conv)
+      if (P.pro == VQX_PRO_NONE && tap_reuse_ok(P, bf16, gen)) {
+        dispatch_tr<MODE>(P, grid, s);
+        return;
+      }
+    }
     launch_pro<bf16_t, MODE, true, EKW>(P, grid, s);
     return;
   }
@@ -153,16 +176,7 @@ void launch_mode_dt(const GemmParams& P, int grid, bool bf16, bool gen, hipStrea
       return;
     }
     if (tap_reuse_ok(P, bf16, gen)) {
-      switch (pick_ek(P.epi)) {
-        case EK_NONE: launch_tr<MODE, EK_NONE>(P, grid, s); break;
-        case EK_ELEM: launch_tr<MODE, EK_ELEM>(P, grid, s); break;
-        case EK_GNADD: launch_tr<MODE, EK_GNADD>(P, grid, s); break;
-        case EK_SPLIT: launch_tr<MODE, EK_SPLIT>(P, grid, s); break;
-        case EK_COLSUM: launch_tr<MODE, EK_COLSUM>(P, grid, s); break;
-        case EK_GNSTATS: launch_tr<MODE, EK_GNSTATS>(P, grid, s); break;
-        case EK_GNBWD: launch_tr<MODE, EK_GNBWD>(P, grid, s); break;
-        default: launch_tr<MODE, EK_ALL>(P, grid, s); break;
-      }
+      dispatch_tr<MODE>(P, grid, s);
       return;
     }
     switch (pick_ek(P.epi)) {
