@@ -910,11 +910,10 @@ class VQVAEEngine:
         ne = len(self.enc_stages)
         last = w.enc[-1]
         self.bias_grad(eo, w.dz, w)
-        self.wgrad(eo, w.dz, last.a[-1], last.T)
         k = 0
         cur = self._enc_cur(w, ne - 1, k)
-        self.dgrad(eo, w.dz, cur, last.T, mask=last.a[-1], mask_slope=0.2,
-                   **self._producer_into_enc(w, ne - 1, None, last.cs[-1], True))
+        self.wgrad_dgrad(eo, w.dz, last.a[-1], cur, last.T, mask=last.a[-1], mask_slope=0.2,
+                         **self._producer_into_enc(w, ne - 1, None, last.cs[-1], True))
         self._wn_bwd(w, "enc_out")
         for si in reversed(range(ne)):
             st, sw = self.enc_stages[si], w.enc[si]
