@@ -927,3 +927,23 @@ def test_adam_step_vector_and_scalar_paths_track_torch(n):
         st = opt.state[pc]
         assert relerr(runs[0]["p"], pc.detach()) < 1e-6, s
         assert relerr(runs[0]["m"], st["exp_avg"]) < 1e-6 and relerr(runs[0]["v"], st["exp_avg_sq"]) < 1e-6, s
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n,C,ld", [(16384, 80, 80), (16384, 64, 64), (16384, 512, 512), (5, 80, 80),
+                                    (1000, 7, 7), (4099, 1000, 1000), (777, 128, 192), (65, 8, 8)])
+def test_colsum_matches_fp64_and_accumulates(dtype, n, C, ld):
+    """vqx_colsum (bias gradients): the narrow-column vector path (lane groups
+    narrower than 32), the scalar path (C or ldx not a multiple of the vector
+    width), the small-row path, and accumulate=1."""
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(n + C)
+    x = torch.randn(n, ld, generator=g).to(DEV, dtype)
+    part = torch.empty(64 * C, device=DEV)
+    out = torch.full((C,), 0.5, device=DEV)
+    ops.colsum(x, part, out, C=C)
+    ref = x[:, :C].double().sum(0)
+    tol = 1e-5 * (n ** 0.5) + 1e-5
+    torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=tol)
+    ops.colsum(x, part, out, accumulate=True, C=C)
+    torch.testing.assert_close(out.double(), 2 * ref, rtol=1e-5, atol=2 * tol)

@@ -1019,11 +1019,15 @@ __global__ __launch_bounds__(256) void colsum_small_kernel(const T* __restrict__
 
 // vectorised partial column sums: 32 chunks x 8 row groups per block
 template <typename T>
+// Lanes [0, L) of each row group cover L column chunks of V; 256/L row groups
+// stride the rows, so narrow outputs (bias gradients of 64..128 columns) keep
+// every lane of the block busy instead of 10 of 32.
 __global__ __launch_bounds__(256) void colsum_partial_vec_kernel(const T* __restrict__ x, int ldx, int64_t n_rows,
-                                                                 int C, int nparts, float* __restrict__ part) {
+                                                                 int C, int nparts, int L, float* __restrict__ part) {
   constexpr int V = Vec<T>::N;
-  const int chunk = blockIdx.x * 32 + (threadIdx.x & 31);
-  const int rg = threadIdx.x >> 5;
+  const int lane = threadIdx.x % L;
+  const int rg = threadIdx.x / L, R = 256 / L;
+  const int chunk = blockIdx.x * L + lane;
   const int p = blockIdx.y;
   const int64_t r0 = n_rows * p / nparts, r1 = n_rows * (p + 1) / nparts;
   const int c = chunk * V;
@@ -1031,21 +1035,22 @@ __global__ __launch_bounds__(256) void colsum_partial_vec_kernel(const T* __rest
 #pragma unroll
   for (int i = 0; i < V; ++i) s[i] = 0.f;
   if (c < C)
-    for (int64_t r = r0 + rg; r < r1; r += 8) {
+#pragma unroll 4
+    for (int64_t r = r0 + rg; r < r1; r += R) {
       float f[V];
       Vec<T>::load(x + r * ldx + c, f);
 #pragma unroll
       for (int i = 0; i < V; ++i) s[i] += f[i];
     }
-  __shared__ float lds[8][32 * V];
+  __shared__ float lds[256 * V];
 #pragma unroll
-  for (int i = 0; i < V; ++i) lds[rg][(threadIdx.x & 31) * V + i] = s[i];
+  for (int i = 0; i < V; ++i) lds[threadIdx.x * V + i] = s[i];
   __syncthreads();
-  for (int e = threadIdx.x; e < 32 * V; e += 256) {
-    const int cc = blockIdx.x * 32 * V + e;
+  for (int e = threadIdx.x; e < L * V; e += 256) {
+    const int cc = blockIdx.x * L * V + e;
     if (cc < C) {
       float t = 0.f;
-      for (int q = 0; q < 8; ++q) t += lds[q][e];
+      for (int q = 0; q < R; ++q) t += lds[q * L * V + e];
       part[(int64_t)p * C + cc] = t;
     }
   }
@@ -1071,13 +1076,18 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const T* __restrict
   }
 }
 
-__global__ void colsum_final_kernel(const float* __restrict__ part, int nparts, int C, float* __restrict__ out, int accum) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+// One wave per column: lanes stride the (<= 64) partials, then a fixed-order
+// butterfly, so the result is deterministic and no lane walks 64 loads.
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int nparts, int C,
+                                                           float* __restrict__ out, int accum) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (c >= C) return;
   float s = 0.f;
-#pragma unroll 8
-  for (int p = 0; p < nparts; ++p) s += part[(int64_t)p * C + c];
-  out[c] = accum ? out[c] + s : s;
+  for (int p = lane; p < nparts; p += 64) s += part[(int64_t)p * C + c];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) out[c] = accum ? out[c] + s : s;
 }
 
 // ------------------------------------------------------------------ layout
@@ -1879,7 +1889,9 @@ extern "C" int vqx_colsum(const void* x, int32_t ldx, int32_t dtype, int64_t n_r
     return launch_status("vqx_colsum");
   }
   const int V = dtype == VQX_BF16 ? 8 : 4;
-  const int colblocks = (C / V + 31) / 32;
+  int L = 1;  // lanes per row group in the vector kernel: pow2 >= C/V, <= 32
+  while (L < 32 && L * V < C) L <<= 1;
+  const int colblocks = (C + V * L - 1) / (V * L);  // >= 1 for any C > 0
   int nparts = (256 + colblocks - 1) / colblocks;
   if (nparts > 64) nparts = 64;
   if (nparts > n_rows / 8) nparts = (int)(n_rows / 8);
@@ -1888,15 +1900,15 @@ extern "C" int vqx_colsum(const void* x, int32_t ldx, int32_t dtype, int64_t n_r
   if (vec) {
     const int nch = C / V;
     if (dtype == VQX_BF16)
-      hipLaunchKernelGGL(colsum_partial_vec_kernel<bf16_t>, dim3((nch + 31) / 32, nparts), dim3(256), 0, s, (const bf16_t*)x, ldx, n_rows, C, nparts, partials);
+      hipLaunchKernelGGL(colsum_partial_vec_kernel<bf16_t>, dim3((nch + L - 1) / L, nparts), dim3(256), 0, s, (const bf16_t*)x, ldx, n_rows, C, nparts, L, partials);
     else
-      hipLaunchKernelGGL(colsum_partial_vec_kernel<float>, dim3((nch + 31) / 32, nparts), dim3(256), 0, s, (const float*)x, ldx, n_rows, C, nparts, partials);
+      hipLaunchKernelGGL(colsum_partial_vec_kernel<float>, dim3((nch + L - 1) / L, nparts), dim3(256), 0, s, (const float*)x, ldx, n_rows, C, nparts, L, partials);
   } else if (dtype == VQX_BF16) {
     hipLaunchKernelGGL(colsum_partial_kernel<bf16_t>, dim3((C + 63) / 64, nparts), dim3(256), 0, s, (const bf16_t*)x, ldx, n_rows, C, nparts, partials);
   } else {
     hipLaunchKernelGGL(colsum_partial_kernel<float>, dim3((C + 63) / 64, nparts), dim3(256), 0, s, (const float*)x, ldx, n_rows, C, nparts, partials);
   }
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 255) / 256), dim3(256), 0, s, partials, nparts, C, out, accumulate);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 3) / 4), dim3(256), 0, s, partials, nparts, C, out, accumulate);
   return launch_status("vqx_colsum");
 }
 
