@@ -161,6 +161,15 @@ __global__ __launch_bounds__(256) void wn_pack_kernel(const vqx_wn_layer* __rest
       if (threadIdx.x == 0) l.norm[co] = nrm;
       sc = l.g[co] / nrm;
     }
+    bf16_t* wb = (bf16_t*)l.w_packed + (int64_t)co * cols;
+    if (l.dtype == VQX_BF16 && (cin & 3) == 0 && (((uintptr_t)wb) & 7) == 0) {
+      for (int e = threadIdx.x * 4; e < cols; e += 1024) {  // 4 consecutive ci of one tap, 8 B a lane
+        const int j = e / cin, ci = e - j * cin;
+        const float* b = buf + ci * K + j;
+        *(uint2*)(wb + e) = make_uint2(pack_bf16x2(b[0] * sc, b[K] * sc), pack_bf16x2(b[2 * K] * sc, b[3 * K] * sc));
+      }
+      return;
+    }
     for (int e = threadIdx.x; e < cols; e += 256) {  // e = j*cin + ci
       const int j = e / cin, ci = e - j * cin;
       st_dt(l.w_packed, (int64_t)co * cols + e, buf[ci * K + j] * sc, l.dtype);
@@ -1512,6 +1521,7 @@ __global__ __launch_bounds__(256) void sqnorm_partial_kernel(const float* __rest
   float s = 0.f;
   const int64_t n4 = n / 4;
   const f32x4_t* g4 = (const f32x4_t*)g;
+#pragma unroll 4
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
     const f32x4_t v = g4[i];
     s = fmaf(v[0], v[0], s); s = fmaf(v[1], v[1], s); s = fmaf(v[2], v[2], s); s = fmaf(v[3], v[3], s);
