@@ -910,17 +910,17 @@ __global__ __launch_bounds__(256) void gn_glu_fwd_vec_kernel(const T* __restrict
                                                              const float* __restrict__ gamma,
                                                              const float* __restrict__ beta,
                                                              const float* __restrict__ tiles, float eps,
-                                                             float* __restrict__ mr_out) {
-  // block = 16 frames; thread = (chunk, row slot); cpr divides 256
+                                                             float* __restrict__ mr_out, int fpb) {
+  // block = fpb frames; thread = (chunk, row slot); cpr divides 256
   constexpr int V = Vec<T>::N;
   const int ch = threadIdx.x % cpr, rs = threadIdx.x / cpr, nrs = 256 / cpr;
   const int c = ch * V;
   __shared__ float smr[4];
   if (tiles) {
-    // statistics of this block's utterance (T % 128 == 0: the 16 frames share
+    // statistics of this block's utterance (T % fpb == 0: the fpb frames share
     // one) merged from the producing GEMM's GNSTATS tiles, as
     // gn_finalize_tiles_kernel does; the utterance's first block stores them
-    const int b0 = blockIdx.x * 16 / T_, rg = T_ / 128, ntn = 2 * half / 128, tpg = ntn / 2;
+    const int b0 = blockIdx.x * fpb / T_, rg = T_ / 128, ntn = 2 * half / 128, tpg = ntn / 2;
     if (threadIdx.x < 2) {
       const int gi = threadIdx.x;
       double n = 0.0, mean = 0.0, m2 = 0.0;
@@ -938,7 +938,7 @@ __global__ __launch_bounds__(256) void gn_glu_fwd_vec_kernel(const T* __restrict
       const float var = n > 0.0 ? (float)(m2 / n) : 0.f;
       smr[2 * gi] = (float)mean;
       smr[2 * gi + 1] = 1.0f / sqrtf(var + eps);
-      if ((blockIdx.x * 16) % T_ == 0) {
+      if ((blockIdx.x * fpb) % T_ == 0) {
         mr_out[4 * b0 + 2 * gi] = smr[2 * gi];
         mr_out[4 * b0 + 2 * gi + 1] = smr[2 * gi + 1];
       }
@@ -961,8 +961,8 @@ __global__ __launch_bounds__(256) void gn_glu_fwd_vec_kernel(const T* __restrict
     Vec<T>::store(g + (int64_t)r * ldg + c, o);
   };
   // two rows' loads in flight before the math of either
-  const int rend = min(n_rows, blockIdx.x * 16 + 16);
-  int r = blockIdx.x * 16 + rs;
+  const int rend = min(n_rows, blockIdx.x * fpb + fpb);
+  int r = blockIdx.x * fpb + rs;
   for (; r + nrs < rend; r += 2 * nrs) {
     float ua0[V], ub0[V], ua1[V], ub1[V];
     Vec<T>::load(u + (int64_t)r * ldu + c, ua0);
@@ -1822,12 +1822,17 @@ static int gn_glu_fwd_impl(const void* u, int32_t ldu, void* g, int32_t ldg, int
   }
   const int cpr = (C / 2) / V;
   if (cpr > 256 || 256 % cpr) { set_error("vqx_gn_glu_fwd: C/2/%d must divide 256", V); return -1; }
-  const int grid = (int)((n_rows + 15) / 16);
+  // frames per workgroup: every workgroup of the in-launch-statistics path
+  // merges its utterance's GEMM tiles first, so larger blocks amortise that
+  static const int fpb_env = [] { const char* e = getenv("VQX_GLU_FPB"); return e ? atoi(e) : 16; }();
+  int fpb = (fpb_env == 4 || fpb_env == 8 || fpb_env == 32 || fpb_env == 64) ? fpb_env : 16;
+  if (tiles && T % fpb) fpb = 16;
+  const int grid = (int)((n_rows + fpb - 1) / fpb);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == VQX_BF16)
-    hipLaunchKernelGGL(gn_glu_fwd_vec_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)u, ldu, (bf16_t*)g, ldg, (int)n_rows, T, C / 2, cpr, mean_rstd, gamma, beta, tiles, eps, mr_out);
+    hipLaunchKernelGGL(gn_glu_fwd_vec_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)u, ldu, (bf16_t*)g, ldg, (int)n_rows, T, C / 2, cpr, mean_rstd, gamma, beta, tiles, eps, mr_out, fpb);
   else
-    hipLaunchKernelGGL(gn_glu_fwd_vec_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)u, ldu, (float*)g, ldg, (int)n_rows, T, C / 2, cpr, mean_rstd, gamma, beta, tiles, eps, mr_out);
+    hipLaunchKernelGGL(gn_glu_fwd_vec_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)u, ldu, (float*)g, ldg, (int)n_rows, T, C / 2, cpr, mean_rstd, gamma, beta, tiles, eps, mr_out, fpb);
   return launch_status("vqx_gn_glu_fwd");
 }
 
