@@ -963,6 +963,18 @@ __global__ __launch_bounds__(256) void gn_glu_fwd_vec_kernel(const T* __restrict
   // two rows' loads in flight before the math of either
   const int rend = min(n_rows, blockIdx.x * fpb + fpb);
   int r = blockIdx.x * fpb + rs;
+#if VQX_GLU_ROWS4
+  for (; r + 3 * nrs < rend; r += 4 * nrs) {  // four rows' loads in flight
+    float ua[4][V], ub[4][V];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      Vec<T>::load(u + (int64_t)(r + q * nrs) * ldu + c, ua[q]);
+      Vec<T>::load(u + (int64_t)(r + q * nrs) * ldu + c + half, ub[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) row(r + q * nrs, ua[q], ub[q]);
+  }
+#endif
   for (; r + nrs < rend; r += 2 * nrs) {
     float ua0[V], ub0[V], ua1[V], ub1[V];
     Vec<T>::load(u + (int64_t)r * ldu + c, ua0);
