@@ -1,14 +1,14 @@
-#!/bin/bash
-# GN-GLU forward with four rows' loads in flight (build -D VQX_GLU_ROWS4=1 ->
-# lib/libvqx_r4.so) vs the default two: GN/GLU tests on the variant, then
-# per-kernel times from alternating rocprofv3 --stats runs.
+# GN-GLU forward A/B: the in-tree library (whole GPU suite first) vs a variant
+# built into lib/libvqx_r4.so (build.py -D ... --out; rounds so far: four rows
+# in flight, then the unfused tanh*sigmoid as the baseline), per-kernel times
+# from alternating rocprofv3 --stats runs.
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 O=gpurun_out/glu4
 mkdir -p $O
-VQX_LIB=vae_npvc_amd/lib/libvqx_r4.so timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_step.py -m gpu -x -q \
-  --timeout 120 --timeout-method thread -k "glu or gn or step" > $O/t.log 2>&1 || { tail -30 $O/t.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q \
+  --timeout 120 --timeout-method thread > $O/t.log 2>&1 || { tail -30 $O/t.log; exit 1; }
 tail -1 $O/t.log
 for v in base r4 base r4; do
   L=vae_npvc_amd/lib/libvqx.so; [ $v = r4 ] && L=vae_npvc_amd/lib/libvqx_r4.so
