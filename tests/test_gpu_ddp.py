@@ -98,14 +98,19 @@ def _rel(a, b):
     return abs(a - b) / max(abs(b), 1e-12)
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_two_rank_engine_step_matches_reference_golden(dtype):
+@pytest.mark.parametrize("prefix,dtype", [("step_vcc20", "fp32"), ("step_vcc20", "bf16"), ("step_aishell3", "fp32"),
+                                          ("step_vcc20_multi", "fp32")])
+def test_two_rank_engine_step_matches_reference_golden(prefix, dtype):
     """fp32: losses 1e-4 at step 1 and 1e-3 later, gradient norms 2e-3 (as the
     single-process golden test), parameters after 3 steps 1e-3.  bf16 (the
-    bench dtype): losses 1e-2 (VQ loss 2e-2), gradient norms 5e-2, parameters 1e-2."""
+    bench dtype): losses 1e-2 (VQ loss 2e-2), gradient norms 5e-2, parameters 1e-2.
+    aishell3 (BASELINE config 4: 160 mel, K=128, skip 256, jitter 0.12) needs
+    the same numpy stream on every rank: each rank draws the single-process
+    jitter map.  vcc20_multi is the general topology (two stages, stride-2
+    resampling, dilation, stack_layers 2, kernel 5)."""
     from tests.helpers import load_fixture
-    meta, _ = load_fixture("step_vcc20")
-    ranks = _spawn(dtype, "step_vcc20")
+    meta, _ = load_fixture(prefix)
+    ranks = _spawn(dtype, prefix)
     assert ranks[0][1] == ranks[1][1]  # identical weights on every rank
     assert np.array_equal(ranks[0][2], ranks[1][2])  # ... and codebooks
     f32 = dtype == "fp32"

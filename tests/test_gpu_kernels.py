@@ -1,6 +1,7 @@
 """Kernel-level parity of libvqx against plain PyTorch fp32/fp64 references of
 the same ops (conv fwd / dgrad / wgrad, ConvTranspose packing, VQ argmin).
 Runs on the MI355X only (-m gpu)."""
+import numpy as np
 import pytest
 import torch
 import torch.nn.functional as F
@@ -281,6 +282,37 @@ def test_vq_ema_statistics_ragged_and_collapsed(N, K, collapse):
     assert torch.allclose(bsum.cpu().double(), want, atol=1e-3, rtol=1e-5)
     if collapse:
         assert int((onehot.sum(0) > 0).sum()) <= 2
+
+
+@pytest.mark.parametrize("K", [16, 128, 512, 2048])
+def test_vq_stats_counts_equal_bincount_skewed(K):
+    """vq_stats_kernel's per-chunk code counts race-free (the count
+    loop read keys[] while the sort's first pass could swap them): bcnt must
+    equal torch.bincount exactly and bsum the per-code sums, over many 512-frame
+    chunks, for skewed index streams (geometric code popularity, long runs of
+    one code, a single code, ragged N), launched repeatedly."""
+    ops = _ops()
+    D = 128
+    g = torch.Generator().manual_seed(K)
+    N = 64 * 512 + 37
+    z = torch.randn(N, D, generator=g)
+    geo = torch.clamp((torch.log(torch.rand(N, generator=g)) / np.log(0.8)).long(), max=K - 1)
+    runs = (torch.arange(N) // 97 * 7919) % K
+    single = torch.full((N,), K // 3, dtype=torch.int64)
+    mixed = torch.where(torch.rand(N, generator=g) < 0.9, torch.zeros(N, dtype=torch.int64),
+                        torch.randint(0, K, (N,), generator=g))
+    zd = z.to(DEV)
+    part = torch.empty(ops.vq_workspace(N, K, True), device=DEV)
+    for idx in (geo, runs, single, mixed):
+        want_c = torch.bincount(idx, minlength=K).float()
+        want_s = torch.zeros(K, D, dtype=torch.float64).index_add_(0, idx, z.double())
+        idd = idx.to(DEV)
+        for _ in range(8):
+            bsum = torch.zeros(K, D, device=DEV)
+            bcnt = torch.zeros(K, device=DEV)
+            ops.vq_stats(zd, idd, K, part, bsum, bcnt)
+            assert torch.equal(bcnt.cpu(), want_c)
+            assert torch.allclose(bsum.cpu().double(), want_s, atol=2e-3, rtol=1e-5)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

@@ -108,3 +108,34 @@ def test_reference_training_loop_advances_checkpoints_and_resumes(tmp_path):
     res = run_reference_loop(dict(cfg, max_iter=7), out["ckpts"][0], tmp_path, train_set, valid_set)
     assert res["seen"] == [4, 5, 6, 7, 8]
     assert int(res["trainer"].engine.opt_step.item()) == 8  # optimizer state resumed with the weights
+
+
+def test_train_entry_single_gpu_runs_the_reference_loop(tmp_path):
+    """vae_npvc_amd/bin/train.py itself (world size 1: the reference's shuffled
+    DataLoader) with the real Trainer: iterations 1..7 for max_iter 6,
+    checkpoints iter.3 / iter.6 with the reference's keys, validation picks
+    the best checkpoint, resume continues at checkpoint + 1."""
+    import types
+
+    import yaml
+    from vae_npvc_amd.bin import train as entry
+    cfg = cfg_of("vcc20", compute_dtype="fp32", batch_size=2, max_iter=6, iters_per_log=2,
+                 iters_per_checkpoint=3, crop_length=64, num_jobs=0, n_utts=8, n_valid=2,
+                 dataset_type="tests.ddp_stubs:SynthMel")
+    path = tmp_path / "conf.yaml"
+    yaml.safe_dump(cfg, open(path, "w"))
+    args = types.SimpleNamespace(config=str(path), output_dir=str(tmp_path / "exp"), checkpoint=None,
+                                 train_dir="unused", valid_dir="unused", backend=None)
+    tr = entry.train(args)
+    assert tr.iteration == 7
+    exp = tmp_path / "exp"
+    ck = torch.load(exp / "iter.6", map_location="cpu", weights_only=True)
+    assert ck["iteration"] == 6 and set(ck) == {"model", "optimizer", "iteration"}
+    assert (exp / "model.loss.best").exists()
+    log = (exp / "train.log").read_text()
+    assert [l.split("Iter ")[1].split(":")[0] for l in log.splitlines() if " Iter " in l] == ["2", "4", "6"]
+    assert "Valid 3:" in log and "Valid 6:" in log
+    yaml.safe_dump(dict(cfg, max_iter=7), open(path, "w"))
+    args.checkpoint = str(exp / "iter.3")
+    tr2 = entry.train(args)
+    assert tr2.iteration == 8 and int(tr2.engine.opt_step.item()) == 8

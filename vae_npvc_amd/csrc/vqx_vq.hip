@@ -307,6 +307,7 @@ __global__ __launch_bounds__(256) void vq_stats_kernel(const float* __restrict__
       const int k = keys[i];
       if (k != 0x7fffffff) atomicAdd(&cnt[k >> 9], 1);  // integer counts: exact in any order
     }
+  __syncthreads();  // the count loop reads keys[] that the sort's first pass swaps
   // bitonic sort, ascending (VQ_CHUNK = 2 elements per thread per step)
   for (int k = 2; k <= VQ_CHUNK; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
@@ -560,7 +561,7 @@ extern "C" int vqx_vq_forward(const float* z, int64_t n_rows, int32_t D, const f
                               float* bsum, float* bcnt, vqx_stream_t stream) {
   if (D != VQ_D) { set_error("vqx_vq_forward: only D=128 supported (got %d)", D); return -1; }
   if (K <= 0 || K % 16) { set_error("vqx_vq_forward: K=%d must be a positive multiple of 16", K); return -1; }
-  if (K > 2048) { set_error("vqx_vq_forward: K=%d > 2048", K); return -1; }
+  if (bsum && K > 2048) { set_error("vqx_vq_forward: EMA statistics need K <= 2048 (got %d)", K); return -1; }
   if (n_rows <= 0 || !z || !E || !idx || !partials) { set_error("vqx_vq_forward: bad arguments"); return -1; }
   if (bcnt && !bsum) { set_error("vqx_vq_forward: bcnt needs bsum"); return -1; }
   if (((uintptr_t)z | (uintptr_t)E) & 15) { set_error("vqx_vq_forward: z/E must be 16-byte aligned"); return -1; }

@@ -176,7 +176,7 @@ class Workspace:
             self.embn = e(K, Z, dt=F32)
             self.e_len = e(K, dt=F32)
             self.pv_part = e(Nz // 4 + 8, dt=F32)
-        self.vq_part = e(ops.vq_workspace(Nz, K, True), dt=F32)  # VQ partials + EMA-statistics slabs
+        self.vq_part = e(ops.vq_workspace(Nz, K, train or eng.plain), dt=F32)  # VQ partials (+ statistics slabs)
         # EMA statistics bundle (all-reduced as one buffer in data parallel)
         self.ema = e(K * Z + K + K * Z, dt=F32)
         self.bsum = self.ema[: K * Z].view(K, Z)
@@ -357,7 +357,7 @@ class VQVAEEngine:
         """Mark parameters' gradients final and launch async mean all-reduces
         over every maximal contiguous run of final, not yet reduced gradients
         (runs below DDP_MIN_RUN floats wait unless `flush`)."""
-        if self.world <= 1:
+        if self.comm is None:
             return
         for i in idxs:
             self._g_ready[i] = True
@@ -826,7 +826,7 @@ class VQVAEEngine:
         noise and permutation from its identically seeded CPU generator, so all
         ranks hold the single-process global-batch rows."""
         z = w.z.detach()
-        if self.world > 1:
+        if self.comm is not None:
             z = self.comm.all_gather_cat(z)
         z = z.cpu()
         n, dd = z.shape
@@ -1070,9 +1070,9 @@ class VQVAEEngine:
             rows = self._tile_rows(w)
             q.embeddings.copy_(rows)
         else:
-            perm = self._perm_rows(w.Nz * self.world, K, self.rank * w.Nz, w.Nz if self.world > 1 else None)
+            perm = self._perm_rows(w.Nz * self.world, K, self.rank * w.Nz, w.Nz if self.comm is not None else None)
             ops.gather_rows(w.z, perm, q.embeddings)
-            if self.world > 1:
+            if self.comm is not None:
                 self.comm.all_reduce_sum(q.embeddings)
         ops.convert_2d(q.embeddings, q.emb_sum)
         q.emb_elem.fill_(1.0)
@@ -1119,7 +1119,7 @@ class VQVAEEngine:
                 ops.zero_(w.ema)
                 ops.vq_stats(w.z, w.idx, K, w.vq_part, w.bsum, w.bcnt)
                 self._ema_rows(w, K)
-                if self.world > 1:
+                if self.comm is not None:
                     self.comm.all_reduce_sum(w.ema, async_op=True).wait()
                 self._ema_apply(w)
             w.ev_ema = side.record_event()
@@ -1127,7 +1127,7 @@ class VQVAEEngine:
         ops.zero_(w.ema)
         ops.vq_forward(w.z, q.embeddings, w.idx, w.zq, w.zq_c, w.stats[1:2], w.vq_part, w.bsum, w.bcnt)
         self._ema_rows(w, K)
-        if self.world > 1:
+        if self.comm is not None:
             self._ema_work = self.comm.all_reduce_sum(w.ema, async_op=True)
 
     def _ema_rows(self, w, K):
@@ -1138,7 +1138,7 @@ class VQVAEEngine:
                 rows.zero_()
             w.rand_rows.copy_(rows)
         else:
-            perm = self._perm_rows(w.Nz * self.world, K, self.rank * w.Nz, w.Nz if self.world > 1 else None)
+            perm = self._perm_rows(w.Nz * self.world, K, self.rank * w.Nz, w.Nz if self.comm is not None else None)
             ops.gather_rows(w.z, perm, w.rand_rows)
 
     def _ema_apply(self, w):
@@ -1162,6 +1162,15 @@ class VQVAEEngine:
 
     # ------------------------------------------------------------ full step
     world, rank, comm = 1, 0, None
+
+    def attach_comm(self, comm):
+        """Run the data-parallel path over `comm` (parallel/ddp.py Comm): the
+        per-group gradient mean all-reduces, the EMA-statistics sum and the
+        owned-rows assembly of the dead-code rows.  The Trainer attaches one
+        when the process group has more than one rank; tests attach a
+        world-size-1 group to run the RCCL branch on one GPU, where every
+        collective is the identity and the step must equal the plain one."""
+        self.world, self.rank, self.comm = comm.world, comm.rank, comm
 
     def forward_train(self, x, y):
         """Training forward (saves every activation the backward needs).
@@ -1201,7 +1210,7 @@ class VQVAEEngine:
         soon as its weight-norm backward has finalised them (_wn_bwd), so the
         reduces overlap the rest of the backward; the remainder (embedding,
         codebook) is flushed at the end."""
-        if self.world > 1:
+        if self.comm is not None:
             self._grads_reset()
         if self.plain:
             # straight-through: the encoder's gradient comes through the decoder
@@ -1211,7 +1220,7 @@ class VQVAEEngine:
         else:
             self.encoder_bwd(w)
             self.decoder_bwd(w)
-        if self.world > 1:
+        if self.comm is not None:
             self._grads_final(range(len(self.params)), flush=True)
             self.comm.finish()
 

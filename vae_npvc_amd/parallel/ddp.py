@@ -2,12 +2,15 @@
 over RCCL (backend "nccl" on ROCm) across the node's xGMI links.
 
 Per step:
-  * gradients — the flat fp32 gradient buffer is laid out in backward order
-    and all-reduced (mean) run by run as soon as a run is final: the engine
-    tracks which parameters each backward layer group's weight-norm backward
-    finalises and launches the contiguous ready runs (>= 64 K floats, split
-    into buckets of BUCKET_BYTES) asynchronously, so the reduction overlaps
-    the rest of the backward (engine/step.py `_grads_final`).  Mean over ranks
+  * gradients — the flat fp32 gradient buffer follows model.parameters()
+    order (encoder first; each backward layer group's parameters -- weights,
+    biases, GroupNorm affine -- are contiguous in it) and is all-reduced
+    (mean) run by run as soon as a run is final: the engine tracks which
+    parameters each backward group's weight-norm + column-reduction launch
+    finalises and launches the maximal contiguous ready runs (>= 64 K floats,
+    split into buckets of BUCKET_BYTES) asynchronously, so the reduction
+    overlaps the rest of the backward whatever order the groups finish in
+    (engine/step.py `_grads_final`).  Mean over ranks
     of per-rank frame_mean losses equals the global-batch loss, so clipping
     after the reduce is identical on all ranks.
   * EMA statistics — bsum [K, D], bcnt [K] and the dead-code rows are summed

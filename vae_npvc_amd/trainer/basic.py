@@ -130,8 +130,7 @@ class Trainer(object):
         self.engine = self.model.engine(self.device)
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             from ..parallel.ddp import Comm
-            comm = Comm()
-            self.engine.world, self.engine.rank, self.engine.comm = comm.world, comm.rank, comm
+            self.engine.attach_comm(Comm())
             dist.broadcast(self.engine.flat_p, 0)
             for b in self.model.buffers():
                 dist.broadcast(b, 0)
