@@ -96,10 +96,14 @@ def layer_specs(cfg):
     cond, skip, fin = dec["cond_channels"], dec["skip_channels"], dec["final_channels"]
     spec = []
 
-    def conv(name, cin, cout, k, transposed=False):
+    def conv(name, cin, cout, k, transposed=False, wn=True):
+        v = (cin, cout, k) if transposed else (cout, cin, k)
+        if not wn:  # plain nn.Conv1d / ConvTranspose1d registration: weight, bias (use_weight_norm: false)
+            spec.append((name + ".weight", v))
+            spec.append((name + ".bias", (cout,)))
+            return
         spec.append((name + ".bias", (cout,)))
         g = (cin, 1, 1) if transposed else (cout, 1, 1)
-        v = (cin, cout, k) if transposed else (cout, cin, k)
         spec.append((name + ".weight_g", g))
         spec.append((name + ".weight_v", v))
 
@@ -107,28 +111,29 @@ def layer_specs(cfg):
         spec.append((name + ".weight", (c,)))
         spec.append((name + ".bias", (c,)))
 
+    ewn, dwn = enc.get("use_weight_norm", True), dec.get("use_weight_norm", True)  # vqvae.py:179-180,290-293
     stages, fidx = encoder_plan(enc)
     for st in stages:
         C = st["cout"]
-        conv(f"encoder.encode.{st['idx']}", st["cin"], C, st["k"])
+        conv(f"encoder.encode.{st['idx']}", st["cin"], C, st["k"], wn=ewn)
         for b in st["blocks"]:
             pre = f"encoder.encode.{b['idx']}"
             for l in range(st["L"]):
-                conv(f"{pre}.stack.{3 * l + 1}", C, C, st["ks"])
+                conv(f"{pre}.stack.{3 * l + 1}", C, C, st["ks"], wn=ewn)
                 gn(f"{pre}.stack.{3 * l + 2}", C)
-            conv(f"{pre}.skip_layer", C, C, 1)
-    conv(f"encoder.encode.{fidx}", enc["out_channels"][-1], Z, 1)
+            conv(f"{pre}.skip_layer", C, C, 1, wn=ewn)
+    conv(f"encoder.encode.{fidx}", enc["out_channels"][-1], Z, 1, wn=ewn)
     for st in decoder_plan(dec)[0]:
         C = st["cout"]
-        conv(f"decoder.layers.{st['idx']}", st["cin"], C, st["k"], transposed=True)
+        conv(f"decoder.layers.{st['idx']}", st["cin"], C, st["k"], transposed=True, wn=dwn)
         for b in st["blocks"]:
             pre = f"decoder.layers.{b['idx']}"
-            conv(f"{pre}.conv_in", C, 2 * C, st["ks"], transposed=True)
+            conv(f"{pre}.conv_in", C, 2 * C, st["ks"], transposed=True, wn=dwn)
             gn(f"{pre}.norm_layer", 2 * C)
-            conv(f"{pre}.conv_cond", cond, 2 * C, 1)
-            conv(f"{pre}.res_skip_layers", C, C + skip, 1)
-    conv("decoder.final_layer.1", skip, skip, 1)
-    conv("decoder.final_layer.3", skip, fin, 1)
+            conv(f"{pre}.conv_cond", cond, 2 * C, 1, wn=dwn)
+            conv(f"{pre}.res_skip_layers", C, C + skip, 1, wn=dwn)
+    conv("decoder.final_layer.1", skip, skip, 1, wn=dwn)
+    conv("decoder.final_layer.3", skip, fin, 1, wn=dwn)
     if not cfg.get("use_ema", False):  # VectorQuantizer's codebook is a parameter (layers_vq.py:18)
         spec.append(("quantizer.embeddings", (cfg.get("z_num", 512), cfg.get("z_dim", 128))))
     spec.append(("embeds._embedding.weight", (cfg.get("y_num", 10), cfg.get("y_dim", 128))))
@@ -174,6 +179,9 @@ def seeded_state_dict(cfg, seed):
             sd[name] = torch.from_numpy(rng.uniform(-0.05, 0.05, size=shape).astype(np.float32))
         elif name in ("embeds._embedding.weight", "quantizer.embeddings"):
             sd[name] = torch.from_numpy(rng.standard_normal(shape).astype(np.float32))
+        elif name.endswith(".weight"):  # a conv without weight norm: U(-1/sqrt(fan_in), +)
+            b = 1.0 / math.sqrt(int(np.prod(shape[1:])))
+            sd[name] = torch.from_numpy(rng.uniform(-b, b, size=shape).astype(np.float32))
         else:
             raise KeyError(name)
     K, D = cfg.get("z_num", 512), cfg.get("z_dim", 128)
@@ -237,6 +245,8 @@ class OracleVQVAE:
 
     # nn.utils.weight_norm pre-hook, torch._weight_norm(v, g, dim=0)
     def _w(self, name):
+        if name + ".weight" in self.params:  # use_weight_norm: false
+            return self.params[name + ".weight"]
         return torch._weight_norm(self.params[name + ".weight_v"], self.params[name + ".weight_g"], 0)
 
     def _conv(self, x, name, pad, transposed=False, stride=1, dilation=1, output_padding=0):

@@ -61,14 +61,14 @@ VARIANTS = {  # derived configs: base recipe + overrides
     "aishell3_plain": ("aishell3", {"use_ema": False}),
 }
 RADAM = {"vcc20_radam": ("vcc20", {"optim_type": "RAdam"})}
-from tests.helpers import MULTI  # noqa: E402  (the general-topology variants)
-VARIANTS_ALL = dict(VARIANTS, **RADAM, **MULTI)
+from tests.helpers import MULTI, NOWN  # noqa: E402  (general topology; use_weight_norm false)
+VARIANTS_ALL = dict(VARIANTS, **RADAM, **MULTI, **NOWN)
 
 
 def load_cfg(name):
     if name in VARIANTS_ALL:
         base, over = VARIANTS_ALL[name]
-        cfg = yaml.safe_load(open(CFGS[base]))
+        cfg = load_cfg(base) if base in VARIANTS_ALL else yaml.safe_load(open(CFGS[base]))
         cfg.update(over)
         return cfg
     return yaml.safe_load(open(CFGS[name]))
@@ -261,6 +261,11 @@ if __name__ == "__main__":
             step_fixture(name, B=4, T=128, steps=3, wseed=1301 + i, bseed=2301 + i, tseed=3301 + i, nseed=4301 + i,
                          out_prefix=f"step_{name}")
         sys.exit(0)
+    if "--only-nown" in sys.argv:  # use_weight_norm: false (vqvae.py:179-180,290-293), plain convs throughout
+        for i, name in enumerate(NOWN):
+            step_fixture(name, B=4, T=128, steps=3, wseed=1401 + i, bseed=2401 + i, tseed=3401 + i, nseed=4401 + i,
+                         out_prefix=f"step_{name}")
+        sys.exit(0)
     if "--only-plain" in sys.argv:  # just the §8f row-1 fixtures
         for i, name in enumerate(VARIANTS):
             step_fixture(name, B=4, T=128, steps=3, wseed=1101 + i, bseed=2101 + i, tseed=3101 + i,
@@ -279,6 +284,9 @@ if __name__ == "__main__":
                      out_prefix=f"step_{name}")
     step_fixture("vcc20_radam", B=4, T=128, steps=8, wseed=1201, bseed=2201, tseed=3201, nseed=4201,
                  out_prefix="step_vcc20_radam")
+    for i, name in enumerate(NOWN):
+        step_fixture(name, B=4, T=128, steps=3, wseed=1401 + i, bseed=2401 + i, tseed=3401 + i, nseed=4401 + i,
+                     out_prefix=f"step_{name}")
     for K in (128, 512, 1024):
         vq_fixture(K, 64, 256, 5000 + K, f"vq_K{K}")
     vq_tile_fixture(6001, "vq_tile")

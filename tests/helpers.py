@@ -28,8 +28,23 @@ MULTI = {"vcc20_multi": ("vcc20", {"encoder": MULTI_ENC, "decoder": MULTI_DEC, "
                                          "use_ema": False})}
 
 
+def _nown(base_cfg):
+    """use_weight_norm: false in both halves (vqvae.py:179-180,290-293): plain Conv1d / ConvTranspose1d."""
+    return {"encoder": dict(base_cfg["encoder"], use_weight_norm=False),
+            "decoder": dict(base_cfg["decoder"], use_weight_norm=False)}
+
+
+_VCC20 = yaml.safe_load(open(CONF / "vcc20.yaml"))
+NOWN = {"vcc20_nown": ("vcc20", _nown(_VCC20)),
+        "vcc20_multi_nown": ("vcc20_multi", dict(_nown({"encoder": MULTI_ENC, "decoder": MULTI_DEC})))}
+
+
 def cfg_of(name, **over):
-    if name in MULTI:
+    if name in NOWN:
+        base, mo = NOWN[name]
+        cfg = cfg_of(base)
+        cfg.update(mo)
+    elif name in MULTI:
         base, mo = MULTI[name]
         cfg = yaml.safe_load(open(CONF / f"{base}.yaml"))
         cfg.update(mo)

@@ -86,3 +86,42 @@ def test_extract_bnf_ids_match_oracle(tmp_path):
             assert (got[u] == cs).mean() > 0.99
         else:  # a near-tie flipped one index: lengths may differ by a merge
             assert abs(len(got[u]) - len(cs)) <= 2
+
+
+@pytest.mark.parametrize("name", ["vcc20", "vcc20_multi"])
+def test_remove_weight_norm_keeps_inference(name):
+    """Model.remove_weight_norm (vqvae.py:93-103) on a trained-shape model, with
+    the strided resampling convs of the general topology: the eval forward,
+    Model.encode and Model.infer after removal equal those before it (the
+    packed weights go from g*v/||v|| computed on the GPU to the baked plain
+    weights), and both match the oracle."""
+    from oracle.vqvae_cpu import OracleVQVAE, seeded_batch, seeded_state_dict
+    from tests.helpers import cfg_of, make_trainer
+    cfg = cfg_of(name, compute_dtype="fp32")
+    sd = seeded_state_dict(cfg, 77)
+    sd["quantizer.emb_init"] = torch.tensor(True)
+    g = torch.Generator().manual_seed(3)
+    sd["quantizer.embeddings"] = torch.randn(cfg["z_num"], 128, generator=g) * 0.1
+    tr = make_trainer(cfg, 77)
+    m = tr.model
+    m.load_state_dict(sd)
+    m.eval()
+    x, y = seeded_batch(cfg, 2, 128, 9)
+    xd, yd = x.cuda(), y.cuda()
+    with torch.no_grad():
+        xh0 = m((xd, yd))[0].cpu()
+        idx0 = m.encode(xd).cpu()
+        m.remove_weight_norm()
+        assert not any(n.endswith("weight_v") for n, _ in m.named_parameters())
+        xh1 = m((xd, yd))[0].cpu()
+        idx1 = m.encode(xd).cpu()
+        inf1 = m.infer((xd, yd)).cpu()
+    orc = OracleVQVAE(cfg, sd)
+    orc.training = False
+    with torch.no_grad():
+        ref_idx = orc.encode(x)
+    assert (idx1 == idx0).float().mean() > 0.99
+    assert (idx1 == ref_idx.view_as(idx1)).float().mean() > 0.99
+    scale = float(xh0.abs().max())
+    assert float((xh1 - xh0).abs().max()) <= 1e-5 * scale
+    assert float((inf1 - xh1).abs().max()) <= 1e-5 * scale

@@ -9,7 +9,7 @@ from tests.helpers import cfg_of, load_fixture, make_trainer, relclose
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("prefix", ["step_vcc20", "step_aishell3"])
+@pytest.mark.parametrize("prefix", ["step_vcc20", "step_aishell3", "step_vcc20_nown", "step_vcc20_multi_nown"])
 def test_fp32_train_steps_match_reference_golden(prefix):
     """fp32 mode.  Step 1: loss dict within 1e-4 relative (diff_emb: 1e-3 with a
     1e-6 absolute floor -- at step 1 every frame is its own code, so the
@@ -21,7 +21,9 @@ def test_fp32_train_steps_match_reference_golden(prefix):
     embedding (no argmin or commitment dependence; measured <= 2.3e-7,
     tools/grad_err_probe.py) and 1e-3 for the encoder, whose only gradient is
     the commitment term (zq - z) (measured <= 2.1e-4 on aishell3 with
-    jitter); EMA buffers within 1e-4."""
+    jitter); EMA buffers within 1e-4.  The *_nown fixtures run use_weight_norm
+    false (vqvae.py:179-180,290-293: plain `weight` parameters on every conv,
+    the multi-stage one including the strided resampling convs)."""
     from oracle.vqvae_cpu import seeded_batch
     meta, arr = load_fixture(prefix)
     cfg = cfg_of(meta["config"], compute_dtype="fp32")

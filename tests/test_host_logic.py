@@ -137,3 +137,43 @@ def test_load_state_dict_resizes_plain_codebook():
     assert torch.equal(m.quantizer.embeddings, sd["quantizer.embeddings"])
     assert m.quantizer.normalize == src.quantizer.normalize
     assert [k for k, _ in m.named_parameters()] == order  # parameter order kept (optimizer state lines up)
+
+
+@pytest.mark.parametrize("name", ["vcc20", "vcc20_multi", "vcc20_nown", "vcc20_multi_nown"])
+def test_model_parameters_match_reference_order(name):
+    """Model(cfg) registers the reference's parameters in the reference's order
+    (oracle.layer_specs, pinned by the reference-generated fixtures): with
+    weight norm bias, weight_g, weight_v; with use_weight_norm false
+    (vqvae.py:179-180,290-293) weight, bias -- on stride-1 and resampling convs."""
+    from oracle.vqvae_cpu import layer_specs
+    from tests.helpers import cfg_of
+    from vae_npvc_amd.model.vqvae import Model
+    cfg = cfg_of(name)
+    m = Model(cfg)
+    got = [(k, tuple(p.shape)) for k, p in m.named_parameters()]
+    assert got == [(k, tuple(s)) for k, s in layer_specs(cfg)]
+    if name.endswith("nown"):
+        meta = json.load(open(GOLD / f"step_{name}.json"))
+        assert [k for k, _ in got] == list(meta["params_after"])  # the reference's own parameter list
+
+
+def test_remove_weight_norm_bakes_every_conv_including_resampling():
+    """vqvae.py:93-103 on the general topology (stride-2 down-/up-sampling
+    convs included): every weight-normed conv ends with a plain `weight`
+    equal to g*v/||v|| (torch._weight_norm, dim 0) registered after `bias`,
+    like torch.nn.utils.remove_weight_norm."""
+    import torch
+    from tests.helpers import cfg_of
+    from vae_npvc_amd.model.resample import ResampleConv1d
+    from vae_npvc_amd.model.vqvae import Model
+    m = Model(cfg_of("vcc20_multi"))
+    before = {n[: -len(".weight_v")]: torch._weight_norm(p, dict(m.named_parameters())[n[:-1] + "g"], 0).detach()
+              for n, p in m.named_parameters() if n.endswith(".weight_v")}
+    assert any(isinstance(x, ResampleConv1d) for x in m.modules())
+    m.remove_weight_norm()
+    names = [n for n, _ in m.named_parameters()]
+    assert not any(n.endswith((".weight_g", ".weight_v")) for n in names)
+    params = dict(m.named_parameters())
+    for base, w in before.items():
+        assert torch.equal(params[base + ".weight"], w), base
+        assert names.index(base + ".weight") == names.index(base + ".bias") + 1

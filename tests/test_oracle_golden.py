@@ -43,7 +43,8 @@ def test_structure_matches_reference():
 
 
 FIXTURE_CFG = {"step_vcc20": ("vcc20", {}), "step_aishell3": ("aishell3", {}),
-               "step_vcc20_radam": ("vcc20", {"optim_type": "RAdam"}), "step_vcc20_multi": ("vcc20_multi", {})}
+               "step_vcc20_radam": ("vcc20", {"optim_type": "RAdam"}), "step_vcc20_multi": ("vcc20_multi", {}),
+               "step_vcc20_nown": ("vcc20_nown", {}), "step_vcc20_multi_nown": ("vcc20_multi_nown", {})}
 
 
 @pytest.mark.parametrize("prefix", list(FIXTURE_CFG))

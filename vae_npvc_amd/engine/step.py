@@ -537,10 +537,10 @@ class VQVAEEngine:
     def _wn_entry(self, Lr, bwd):
         mod = Lr.mod
         if Lr.kind in (KIND_DOWN, KIND_UP):
-            e = dict(v=mod.weight_v, g=mod.weight_g, w_packed=Lr.wp, norm=Lr.norm,
+            wn = mod.has_weight_norm
+            e = dict(v=mod.v_param, g=mod.g_param, w_packed=Lr.wp, norm=Lr.norm,
                      kind=L.WN_RESAMPLE_T if Lr.kind == KIND_UP else L.WN_RESAMPLE, cout=mod.cout, cin=mod.cin,
                      k=mod.k, dtype=ops.dt_code(Lr.wp.dtype), splits=Lr.splits, stride=mod.scale, pad=mod.padding)
-            wn = True
         else:
             wn = mod.has_weight_norm
             v = mod.weight_v if wn else mod.weight
@@ -899,12 +899,16 @@ class VQVAEEngine:
             kw.update(self._gnb(w, si, len(st.blocks) - 1))
         return kw
 
-    def encoder_bwd(self, w, grad_scale=1.0):
+    def encoder_bwd(self, w, grad_scale=1.0, dz=None):
         """Backward of beta*z_enc_loss through the encoder: the commitment term is
         the encoder's only gradient source (z_vq is a no-grad gather under
-        reduction='frame_mean', layers_vq.py:292,315)."""
+        reduction='frame_mean', layers_vq.py:292,315).  `dz` (frame-major
+        [B*T_z, Z] f32) replaces that source: parity tests feed the same
+        well-conditioned dL/dz to this path and to autograd of the oracle."""
         B = w.B
-        if not self.plain:  # EMA: the commitment term is the encoder's only gradient
+        if dz is not None:
+            ops.convert_2d(dz, w.dz)
+        elif not self.plain:  # EMA: the commitment term is the encoder's only gradient
             ops.vq_commit_bwd(w.z, w.zq, 2.0 * self.m.beta * grad_scale / w.Nz, w.dz)
         eo = self.enc_out
         ne = len(self.enc_stages)

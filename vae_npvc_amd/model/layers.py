@@ -18,15 +18,20 @@ class WNConv1d(nn.Module):
     ConvTranspose1d (kind 1, v [cin, cout, k], g [cin,1,1]); nn.utils.weight_norm
     with dim=0 as applied at vqvae.py:203-208,329-334."""
 
-    def __init__(self, cin, cout, k, transposed=False, padding=None, dilation=1):
+    def __init__(self, cin, cout, k, transposed=False, padding=None, dilation=1, weight_norm=True):
         super().__init__()
         self.cin, self.cout, self.k, self.transposed = cin, cout, k, transposed
         self.dilation = dilation
         self.padding = (k - 1) // 2 * dilation if padding is None else padding
         bound = 1.0 / math.sqrt((cout if transposed else cin) * k)
-        self.bias = nn.Parameter(torch.empty(cout).uniform_(-bound, bound))
         vshape = (cin, cout, k) if transposed else (cout, cin, k)
         v = torch.empty(vshape).uniform_(-bound, bound)
+        if not weight_norm:  # use_weight_norm: false -> a plain nn.Conv1d / ConvTranspose1d (weight, bias)
+            self.weight = nn.Parameter(v)
+            self.bias = nn.Parameter(torch.empty(cout).uniform_(-bound, bound))
+            self.has_weight_norm = False
+            return
+        self.bias = nn.Parameter(torch.empty(cout).uniform_(-bound, bound))
         self.weight_g = nn.Parameter(v.flatten(1).norm(dim=1).view(vshape[0], 1, 1))
         self.weight_v = nn.Parameter(v)
         self.has_weight_norm = True
@@ -61,17 +66,18 @@ class ResidualBlock(nn.Module):
     out = stack(c) + Conv_1(c), stack = [LReLU0.2, Conv_k(dilation), GN(1, C)]
     followed by (layers - 1) x [LReLU0.2, Conv_k, GN(1, C)] (layers.py:151-161)."""
 
-    def __init__(self, channels, kernel_size=3, layers=1, dilation=1):
+    def __init__(self, channels, kernel_size=3, layers=1, dilation=1, weight_norm=True):
         super().__init__()
         if (kernel_size - 1) % 2:
             raise ValueError("Not support even number kernel size.")  # layers.py:142
-        stack = [nn.LeakyReLU(0.2), WNConv1d(channels, channels, kernel_size, dilation=dilation),
+        wn = weight_norm
+        stack = [nn.LeakyReLU(0.2), WNConv1d(channels, channels, kernel_size, dilation=dilation, weight_norm=wn),
                  nn.GroupNorm(1, channels, eps=1e-5, affine=True)]
         for _ in range(layers - 1):
-            stack += [nn.LeakyReLU(0.2), WNConv1d(channels, channels, kernel_size),
+            stack += [nn.LeakyReLU(0.2), WNConv1d(channels, channels, kernel_size, weight_norm=wn),
                       nn.GroupNorm(1, channels, eps=1e-5, affine=True)]
         self.stack = nn.Sequential(*stack)
-        self.skip_layer = WNConv1d(channels, channels, 1)
+        self.skip_layer = WNConv1d(channels, channels, 1, weight_norm=wn)
         self.layers, self.dilation = layers, dilation
 
     @property
@@ -88,17 +94,18 @@ class ResSkipBlock(nn.Module):
     Conv_1(c)) with ConvT of dilation d and padding (k-1)//2*d (layers.py:198-200);
     g = tanh(h[:C])*sigmoid(h[C:]); r = Conv_1(g); x' = r[:C] + x; skip = r[C:]."""
 
-    def __init__(self, channels, cond_channels, skip_channels, kernel_size=3, dilation=1):
+    def __init__(self, channels, cond_channels, skip_channels, kernel_size=3, dilation=1, weight_norm=True):
         super().__init__()
         if (kernel_size - 1) % 2:
             raise ValueError("Not support even number kernel size.")  # layers.py:197
         if not cond_channels:
             raise NotImplementedError("decoder blocks without speaker conditioning (cond_channels 0)")
+        wn = weight_norm
         self.conv_in = WNConv1d(channels, 2 * channels, kernel_size, transposed=True,
-                                padding=(kernel_size - 1) // 2 * dilation, dilation=dilation)
+                                padding=(kernel_size - 1) // 2 * dilation, dilation=dilation, weight_norm=wn)
         self.norm_layer = nn.GroupNorm(2, 2 * channels, eps=1e-5, affine=True)
-        self.conv_cond = WNConv1d(cond_channels, 2 * channels, 1)
-        self.res_skip_layers = WNConv1d(channels, channels + skip_channels, 1)
+        self.conv_cond = WNConv1d(cond_channels, 2 * channels, 1, weight_norm=wn)
+        self.res_skip_layers = WNConv1d(channels, channels + skip_channels, 1, weight_norm=wn)
         self.in_channels = channels
         self.dilation = dilation
 

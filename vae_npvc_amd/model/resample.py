@@ -46,7 +46,7 @@ class ResampleConv1d(nn.Module):
     ConvTranspose1d(cin, cout, 2s, stride=s, output_padding=s%2)
     (transposed=True), computed by libvqx."""
 
-    def __init__(self, cin, cout, scale, transposed=False, compute_dtype="fp32", splits=None):
+    def __init__(self, cin, cout, scale, transposed=False, compute_dtype="fp32", splits=None, weight_norm=True):
         super().__init__()
         self.cin, self.cout, self.scale, self.transposed = cin, cout, scale, transposed
         self.k, self.padding, self.output_padding = resample_geometry(scale)
@@ -55,10 +55,35 @@ class ResampleConv1d(nn.Module):
         bound = 1.0 / math.sqrt(fan_in)
         vshape = (cin, cout, self.k) if transposed else (cout, cin, self.k)
         v = torch.empty(vshape).uniform_(-bound, bound)
+        self.splits = splits
+        self.has_weight_norm = bool(weight_norm)
+        if not weight_norm:  # a plain strided Conv1d / ConvTranspose1d: weight, bias (use_weight_norm: false)
+            self.weight = nn.Parameter(v)
+            self.bias = nn.Parameter(torch.empty(cout).uniform_(-bound, bound))
+            return
         self.bias = nn.Parameter(torch.empty(cout).uniform_(-bound, bound))
         self.weight_g = nn.Parameter(v.flatten(1).norm(dim=1).view(vshape[0], 1, 1))
         self.weight_v = nn.Parameter(v)
-        self.splits = splits
+
+    def remove_weight_norm(self):
+        """torch.nn.utils.remove_weight_norm (vqvae.py:93-103): bake w = g*v/||v||
+        (norm over all dims but 0) into a plain `weight` registered after `bias`."""
+        if not self.has_weight_norm:
+            raise ValueError("weight_norm not present")
+        w = torch._weight_norm(self.weight_v, self.weight_g, 0).detach()
+        del self.weight_g
+        del self.weight_v
+        self.weight = nn.Parameter(w)
+        self.has_weight_norm = False
+
+    @property
+    def v_param(self):
+        """The direction parameter the packing kernel reads: weight_v, or the plain weight."""
+        return self.weight_v if self.has_weight_norm else self.weight
+
+    @property
+    def g_param(self):
+        return self.weight_g if self.has_weight_norm else None
 
     @property
     def rows(self):
@@ -74,11 +99,13 @@ class ResampleConv1d(nn.Module):
 
     def _table(self, w_packed, norm, dv=None, dg=None, slabs=None, splits=1):
         kind = L.WN_RESAMPLE_T if self.transposed else L.WN_RESAMPLE
-        return ops.wn_table([dict(v=self.weight_v, g=self.weight_g, w_packed=w_packed, norm=norm, dv=dv, dg=dg,
+        return ops.wn_table([dict(v=self.v_param, g=self.g_param, w_packed=w_packed, norm=norm, dv=dv, dg=dg,
                                   slabs=slabs, kind=kind, cout=self.cout, cin=self.cin, k=self.k, splits=splits,
                                   dtype=ops.dt_code(w_packed.dtype), stride=self.scale, pad=self.padding)])
 
     def forward(self, x):
+        if not self.has_weight_norm:
+            return _ResampleFn.apply(self, x, self.bias, None, self.weight)
         return _ResampleFn.apply(self, x, self.bias, self.weight_g, self.weight_v)
 
 
@@ -138,8 +165,8 @@ class _ResampleFn(torch.autograd.Function):
             ops.conv_fwd(dyf, wp, dx, T=T, cin=s * mod.cout, cout=C, ntaps=3, pad=1)
             ops.conv_wgrad(xr, dyf, slabs, T=T_fold, r_dim=C, c_dim=s * mod.cout, ntaps=3, pad=1, shift_sign=1,
                            splits=splits)
-        dv = torch.empty_like(mod.weight_v)
-        dg = torch.empty_like(mod.weight_g)
+        dv = torch.empty_like(mod.v_param)
+        dg = torch.empty_like(mod.weight_g) if mod.has_weight_norm else None
         ops.weight_norm_bwd(mod._table(wp, norm, dv=dv, dg=dg, slabs=slabs, splits=splits))
         part = torch.empty(64 * mod.cout, device=dev, dtype=F32)
         dbias = torch.empty(mod.cout, device=dev, dtype=F32)

@@ -35,21 +35,21 @@ class Encoder(nn.Module):
         super().__init__()
         if use_causal_conv:
             raise NotImplementedError("Not supported yet.")  # vqvae.py:139
-        if not use_weight_norm:
-            raise NotImplementedError("encoder: use_weight_norm false (every reference recipe uses weight norm)")
+        wn = bool(use_weight_norm)  # false: plain convs with `weight` parameters (vqvae.py:179-180)
         layers, self.stage_index = [], []
         for cin, cout, ds, nst in zip(in_channels, out_channels, downsample_scales, stacks):
             self.stage_index.append(len(layers))
             if ds == 1:
                 if (kernel_size - 1) % 2:
                     raise NotImplementedError("encoder: even kernel_size changes the frame count")
-                layers.append(WNConv1d(cin, cout, kernel_size))
+                layers.append(WNConv1d(cin, cout, kernel_size, weight_norm=wn))
             else:
-                layers.append(ResampleConv1d(cin, cout, ds))
+                layers.append(ResampleConv1d(cin, cout, ds, weight_norm=wn))
             for j in range(nst):
-                layers.append(ResidualBlock(cout, stack_kernel_size, stack_layers, 2 ** j if dilation else 1))
+                layers.append(ResidualBlock(cout, stack_kernel_size, stack_layers, 2 ** j if dilation else 1,
+                                            weight_norm=wn))
             layers.append(nn.LeakyReLU(negative_slope=0.2))
-        layers.append(WNConv1d(out_channels[-1], z_channels, 1))
+        layers.append(WNConv1d(out_channels[-1], z_channels, 1, weight_norm=wn))
         self.encode = nn.Sequential(*layers)
         self.in_ch, self.z_ch = in_channels[0], z_channels
 
@@ -68,23 +68,22 @@ class Decoder(nn.Module):
         super().__init__()
         if use_causal_conv:
             raise NotImplementedError("Not supported yet.")  # vqvae.py:238
-        if not use_weight_norm:
-            raise NotImplementedError("decoder: use_weight_norm false (every reference recipe uses weight norm)")
+        wn = bool(use_weight_norm)  # false: plain convs with `weight` parameters (vqvae.py:290-293)
         layers, self.stage_index = [], []
         for cin, cout, us, nst in zip(in_channels, out_channels, upsample_scales, stacks):
             self.stage_index.append(len(layers))
             if us == 1:
                 if (kernel_size - 1) % 2:
                     raise NotImplementedError("decoder: even kernel_size changes the frame count")
-                layers.append(WNConv1d(cin, cout, kernel_size, transposed=True))
+                layers.append(WNConv1d(cin, cout, kernel_size, transposed=True, weight_norm=wn))
             else:
-                layers.append(ResampleConv1d(cin, cout, us, transposed=True))
+                layers.append(ResampleConv1d(cin, cout, us, transposed=True, weight_norm=wn))
             for j in range(nst):
                 layers.append(ResSkipBlock(cout, cond_channels, skip_channels, stack_kernel_size,
-                                           2 ** j if dilation else 1))
+                                           2 ** j if dilation else 1, weight_norm=wn))
         self.layers = nn.ModuleList(layers)
-        self.final_layer = nn.Sequential(nn.ReLU(), WNConv1d(skip_channels, skip_channels, 1), nn.ReLU(),
-                                         WNConv1d(skip_channels, final_channels, 1))
+        self.final_layer = nn.Sequential(nn.ReLU(), WNConv1d(skip_channels, skip_channels, 1, weight_norm=wn),
+                                         nn.ReLU(), WNConv1d(skip_channels, final_channels, 1, weight_norm=wn))
         self.skip_ch, self.final_ch, self.cond_ch = skip_channels, final_channels, cond_channels
 
 
@@ -179,10 +178,11 @@ class Model(nn.Module):
         return self.decode((self.encode(x), y_idx))
 
     def remove_weight_norm(self):
-        if any(isinstance(m, ResampleConv1d) for m in self.modules()):
-            raise NotImplementedError("remove_weight_norm with resampling convs")
+        """vqvae.py:93-103: bake w = g*v/||v|| into a plain `weight` on every
+        conv that has weight norm (stride-1 and resampling convs alike); the
+        engine is rebuilt over the new parameters on its next use."""
         for m in self.modules():
-            if isinstance(m, WNConv1d) and m.has_weight_norm:
+            if isinstance(m, (WNConv1d, ResampleConv1d)) and m.has_weight_norm:
                 m.remove_weight_norm()
         self._engine = None
 
