@@ -110,10 +110,9 @@ def test_wgrad_tiles_reports_the_kernel_the_library_picks():
     from vae_npvc_amd import ops
     if os.environ.get("VQX_TAP_REUSE") == "0":
         pytest.skip("tap reuse disabled in this environment")
-    kg = 2 if os.environ.get("VQX_WGRAD_KG") == "2" else 1
     N, T = 64 * 256, 256
-    assert ops.wgrad_tiles(N, T, 512, 512, 3, 1, L.VQX_BF16) == 4 * 8 * kg
-    assert ops.wgrad_tiles(N, T, 512, 1024, 3, 1, L.VQX_BF16) == 4 * 16 * kg
+    assert ops.wgrad_tiles(N, T, 512, 512, 3, 1, L.VQX_BF16) == 4 * 8
+    assert ops.wgrad_tiles(N, T, 512, 1024, 3, 1, L.VQX_BF16) == 4 * 16
     assert ops.wgrad_tiles(N, T, 512, 512, 1, 0, L.VQX_BF16) == 4 * 4      # 1x1: im2col tiles
     assert ops.wgrad_tiles(N, T, 512, 512, 3, 1, L.VQX_F32) == 4 * 12      # fp32 parity mode
     assert ops.wgrad_tiles(N, 100, 512, 512, 3, 1, L.VQX_BF16) == 4 * 12   # T % 64 != 0

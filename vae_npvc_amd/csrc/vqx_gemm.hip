@@ -62,10 +62,7 @@ void gemm_launch_args(const void* fn, int grid, hipStream_t s, void** args, cons
 
 // vqx_set_gemm_tile: 0 = automatic, 1 = implicit-im2col kernel only,
 // 2 / 3 = tap reuse through conv_tr8_kernel with 1 / 2 frame segments where it
-// applies, 4 = tap reuse through conv_tr_kernel only, 5 = automatic with the
-// wide weight gradients (wgrad_tr2_kernel: 3-tap c_dim % 128 == 0, 1x1 c_dim % 256 == 0),
-// 6 = automatic with the fused 1x1 DGRAD+WGRAD launches interleaved (dual_policy 2),
-// 7 = ... with the three-per-CU 1x1 form (dual_policy 4)
+// applies, 4 = tap reuse through conv_tr_kernel only
 static int g_gemm_policy = 0;
 
 bool tap_reuse_enabled() {
@@ -76,14 +73,6 @@ bool tap_reuse_enabled() {
   return env_on && g_gemm_policy != 1;
 }
 
-int tr_stage_channels() {
-  static const int bkc = [] {
-    const char* e = getenv("VQX_TR_BKC");
-    return (e && e[0] == '1' && e[1] == '6') ? 16 : 32;
-  }();
-  return bkc;
-}
-
 int tr8_policy() {
   static const int pol = [] {
     const char* e = getenv("VQX_TR8");  // 0 = off, 1/2 = SEGS, unset = automatic (-1)
@@ -91,22 +80,6 @@ int tr8_policy() {
   }();
   if (g_gemm_policy >= 2 && g_gemm_policy <= 4) return g_gemm_policy == 4 ? 0 : g_gemm_policy - 1;
   return pol;
-}
-
-int wgrad_kgroups() {
-  static const int kg = [] {
-    const char* e = getenv("VQX_WGRAD_KG");  // 2 measured 0.5-1% slower end to end (profiles/r01)
-    return (e && e[0] == '2') ? 2 : 1;
-  }();
-  return kg;
-}
-
-bool wgrad_wide() {
-  static const bool on = [] {
-    const char* e = getenv("VQX_WGRAD_WIDE");  // 1: wgrad_tr2_kernel where it applies
-    return e && e[0] == '1';
-  }();
-  return on || g_gemm_policy == 5;
 }
 
 static void launch_mode(GemmParams& P, int mode, int64_t rows, int extra_mult, bool bf16, bool gen, hipStream_t s) {
@@ -226,33 +199,24 @@ static int wgrad_prepare(const vqx_wgrad_args* a, GemmParams& P, bool& gen) {
   const int bkv = a->dtype == VQX_BF16 ? 64 : 32;
   gen = (a->T % bkv) != 0 || (a->n_rows % bkv) != 0;
   if (!gen && wgrad_tr_ok(a->n_rows, a->T, a->c_dim, a->ntaps, a->pad, dil, a->dtype == VQX_BF16, a->q_prologue)) {
-    P.tap_reuse = wgrad_kgroups();
+    P.tap_reuse = 1;
     P.tiles_n = a->c_dim / 64;
-    if (wgrad_wide() && a->c_dim % 128 == 0) {  // one 8-wave workgroup per two 64-channel tiles
-      P.tap_reuse = 3;
-      P.tiles_n = a->c_dim / 128;
-    }
-  } else if (!gen && wgrad_wide1_ok(a->n_rows, a->T, a->c_dim, a->ntaps, a->pad, a->dtype == VQX_BF16, a->q_prologue)) {
-    P.tap_reuse = 4;  // wide 1x1 kernel, 256 channels of c per workgroup
-    P.tiles_n = a->c_dim / 256;
   }
   return 0;
 }
 
-// fused DGRAD+WGRAD launches: 0 = off, 1 = 3-tap tap-reuse pairs, 2 = also
-// the 1x1 pairs interleaved, 3 = also the 1x1 pairs with DGRAD's workgroups
-// first (default; env VQX_DUAL), 4 = the 1x1 pairs three workgroups per CU
-// (32-deep K-tiles, 48 KiB).  Measured (profiles/r02/dual_ab.txt): 3-tap
-// pairs interleaved 3-8% faster than two launches; 1x1 pairs interleaved
-// 8-20% slower (their DGRAD workgroups run ~1.5x longer than the WGRAD ones,
-// and two mixed rounds end on a DGRAD tail), in sequence 0.7% faster per step
-// than two launches (one ramp/tail less)
+// fused DGRAD+WGRAD launches: 0 = off, 1 = 3-tap tap-reuse pairs only, 3 =
+// also the 1x1 pairs with DGRAD's workgroups first (default; env VQX_DUAL).
+// Measured (profiles/r02/dual_ab.txt): 3-tap pairs interleaved 3-8% faster
+// than two launches; 1x1 pairs in sequence 0.7% faster per step than two
+// launches (one ramp/tail less).  The interleaved and three-per-CU 1x1 forms
+// measured slower and were retired in round 3.
 int dual_policy() {
   static const int pol = [] {
     const char* e = getenv("VQX_DUAL");
-    return (e && e[0] >= '0' && e[0] <= '4') ? e[0] - '0' : 3;
+    return (e && (e[0] == '0' || e[0] == '1' || e[0] == '3')) ? e[0] - '0' : 3;
   }();
-  return g_gemm_policy == 1 ? 0 : (g_gemm_policy == 6 ? 2 : (g_gemm_policy == 7 ? 4 : pol));
+  return g_gemm_policy == 1 ? 0 : pol;
 }
 static bool dual_enabled() { return dual_policy() > 0; }
 
@@ -310,13 +274,13 @@ extern "C" int vqx_wgrad_tiles(int64_t n_rows, int32_t T, int32_t r_dim, int32_t
   const bool gen = (T % bkv) != 0 || (n_rows % bkv) != 0;
   const int tm = (r_dim + 127) / 128;
   if (!gen && wgrad_tr_ok(n_rows, T, c_dim, ntaps, pad, dil > 0 ? dil : 1, bf16, q_prologue))
-    *tiles = tm * (c_dim / 64) * wgrad_kgroups();
+    *tiles = tm * (c_dim / 64);
   else *tiles = tm * ((ntaps * c_dim + kBN - 1) / kBN);
   return 0;
 }
 
 extern "C" int vqx_set_gemm_tile(int32_t policy) {
-  if (policy < 0 || policy > 7) { set_error("vqx_set_gemm_tile: policy %d not in 0..7", policy); return -1; }
+  if (policy < 0 || policy > 4) { set_error("vqx_set_gemm_tile: policy %d not in 0..4", policy); return -1; }
   g_gemm_policy = policy;
   return 0;
 }

@@ -14,8 +14,6 @@
 // ramp and one tail cover both.  Each workgroup runs the unchanged kernel body
 // (vqx_gemm_kernel.h conv_gemm_body / conv_tr_body / wgrad_tr_body) on its own
 // tile grid; the branch is uniform per workgroup.
-#include <stdlib.h>
-
 #include "vqx_gemm_inst.h"
 
 namespace vqx {
@@ -43,46 +41,26 @@ __device__ __forceinline__ bool dual_split(int b, int nd, int nw, int ch, int& s
 
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
-// blockIdx -> (DGRAD?, index): all DGRAD workgroups first, then WGRAD's (nd % 8 == 0 keeps the XCD map)
-__device__ __forceinline__ bool seq_split(int b, int nd, int& sub) {
-  sub = b < nd ? b : b - nd;
-  return b < nd;
-}
-
-// 1x1 layer: conv_gemm_kernel DGRAD (epilogue kind EKD) + conv_gemm_kernel WGRAD;
-// SEQ: DGRAD's workgroups first (one round), WGRAD's filling the slots they free
-template <int EKD, bool SEQ>
+// 1x1 layer: conv_gemm_kernel DGRAD (epilogue kind EKD) + conv_gemm_kernel
+// WGRAD, DGRAD's workgroups first (one round), WGRAD's filling the slots they
+// free (nd % 8 == 0 keeps the XCD map of both)
+template <int EKD>
 __global__ __launch_bounds__(256, 2) void dual_k1_kernel(GemmParams PD, GemmParams PW, int nd, int nw, int ch) {
   __shared__ __attribute__((aligned(16))) char smem[conv_gemm_smem<bf16_t, 64, 2>()];
-  int sub;
-  if (SEQ ? seq_split(blockIdx.x, nd, sub) : dual_split(blockIdx.x, nd, nw, ch, sub))
-    conv_gemm_body<bf16_t, MODE_DGRAD, VQX_PRO_NONE, false, 64, 2, EKD>(PD, sub, nd, smem);
-  else
-    conv_gemm_body<bf16_t, MODE_WGRAD, VQX_PRO_NONE, false, 64, 2, EK_NONE>(PW, sub, nw, smem);
-}
-
-// 1x1 layer, three workgroups per CU: both bodies on 32-deep K-tiles in a
-// 3-deep ring (48 KiB of LDS instead of 64, <= 168 VGPRs), DGRAD's workgroups
-// first, so each CU holds two DGRAD workgroups and one WGRAD workgroup while
-// DGRAD's round runs (the MFMA-bound WGRAD beside the epilogue-bound DGRAD)
-template <int EKD>
-__global__ __launch_bounds__(256, 3) void dual_k1w_kernel(GemmParams PD, GemmParams PW, int nd, int nw, int ch) {
-  __shared__ __attribute__((aligned(16))) char smem[conv_gemm_smem<bf16_t, 32, 3>()];
-  int sub;
+  (void)nw;
   (void)ch;
-  if (seq_split(blockIdx.x, nd, sub))
-    conv_gemm_body<bf16_t, MODE_DGRAD, VQX_PRO_NONE, false, 32, 3, EKD>(PD, sub, nd, smem);
-  else
-    conv_gemm_body<bf16_t, MODE_WGRAD, VQX_PRO_NONE, false, 32, 3, EK_NONE>(PW, sub, nw, smem);
+  const int b = blockIdx.x;
+  if (b < nd) conv_gemm_body<bf16_t, MODE_DGRAD, VQX_PRO_NONE, false, 64, 2, EKD>(PD, b, nd, smem);
+  else conv_gemm_body<bf16_t, MODE_WGRAD, VQX_PRO_NONE, false, 64, 2, EK_NONE>(PW, b - nd, nw, smem);
 }
 
 // 3-tap layer: conv_tr_kernel DGRAD (epilogue kind EKD) + wgrad_tr_kernel
 template <int EKD>
 __global__ __launch_bounds__(256, 2) void dual_tr_kernel(GemmParams PD, GemmParams PW, int nd, int nw, int ch) {
-  __shared__ __attribute__((aligned(16))) char smem[cmax(conv_tr_smem<32>(), wgrad_tr_smem<1>())];
+  __shared__ __attribute__((aligned(16))) char smem[cmax(conv_tr_smem<32>(), wgrad_tr_smem())];
   int sub;
   if (dual_split(blockIdx.x, nd, nw, ch, sub)) conv_tr_body<MODE_DGRAD, EKD, 32>(PD, sub, nd, smem);
-  else wgrad_tr_body<EK_NONE, 1>(PW, sub, nw, smem);
+  else wgrad_tr_body<EK_NONE>(PW, sub, nw, smem);
 }
 
 bool launch_dual(const GemmParams& PD, int nd, const GemmParams& PW, int nw, hipStream_t s) {
@@ -90,7 +68,7 @@ bool launch_dual(const GemmParams& PD, int nd, const GemmParams& PW, int nw, hip
   const int ekd = pick_ek(PD.epi);
   const void* fn = nullptr;
   int kind = 0;
-  if (tap_reuse_ok(PD, true, false) && tr8_segs(PD) == 0 && tr_stage_channels() == 32 && PD.kcin % 32 == 0) {
+  if (tap_reuse_ok(PD, true, false) && tr8_segs(PD) == 0 && PD.kcin % 32 == 0) {
     if (PW.tap_reuse != 1) return false;
     kind = 2;
     switch (ekd) {
@@ -99,40 +77,22 @@ bool launch_dual(const GemmParams& PD, int nd, const GemmParams& PW, int nw, hip
       case EK_COLSUM: fn = (const void*)dual_tr_kernel<EK_COLSUM>; break;
       default: return false;
     }
-  } else if (PD.ntaps == 1 && PW.ntaps == 1 && PW.tap_reuse == 0 && dual_policy() == 4 && nd % 8 == 0) {
-    kind = 4;
+  } else if (PD.ntaps == 1 && PW.ntaps == 1 && PW.tap_reuse == 0 && dual_policy() >= 3 && nd % 8 == 0) {
+    kind = 3;
     switch (ekd) {
-      case EK_NONE: fn = (const void*)dual_k1w_kernel<EK_NONE>; break;
-      case EK_ELEM: fn = (const void*)dual_k1w_kernel<EK_ELEM>; break;
-      case EK_COLSUM: fn = (const void*)dual_k1w_kernel<EK_COLSUM>; break;
-      case EK_GNBWD: fn = (const void*)dual_k1w_kernel<EK_GNBWD>; break;
-      default: return false;
-    }
-  } else if (PD.ntaps == 1 && PW.ntaps == 1 && PW.tap_reuse == 0 && dual_policy() >= 2) {
-    const bool seq = dual_policy() == 3 && nd % 8 == 0;
-    kind = seq ? 3 : 1;
-    switch (ekd) {
-      case EK_NONE: fn = seq ? (const void*)dual_k1_kernel<EK_NONE, true> : (const void*)dual_k1_kernel<EK_NONE, false>; break;
-      case EK_ELEM: fn = seq ? (const void*)dual_k1_kernel<EK_ELEM, true> : (const void*)dual_k1_kernel<EK_ELEM, false>; break;
-      case EK_COLSUM:
-        fn = seq ? (const void*)dual_k1_kernel<EK_COLSUM, true> : (const void*)dual_k1_kernel<EK_COLSUM, false>;
-        break;
-      case EK_GNBWD:
-        fn = seq ? (const void*)dual_k1_kernel<EK_GNBWD, true> : (const void*)dual_k1_kernel<EK_GNBWD, false>;
-        break;
+      case EK_NONE: fn = (const void*)dual_k1_kernel<EK_NONE>; break;
+      case EK_ELEM: fn = (const void*)dual_k1_kernel<EK_ELEM>; break;
+      case EK_COLSUM: fn = (const void*)dual_k1_kernel<EK_COLSUM>; break;
+      case EK_GNBWD: fn = (const void*)dual_k1_kernel<EK_GNBWD>; break;
       default: return false;
     }
   } else {
     return false;
   }
   const double flops = 2.0 * (double)PD.n_rows * PD.Nc * PD.K + 2.0 * (double)PW.n_rows * PW.Mc * PW.Nc;
-  // probe label: mode 3 = dual, prologue slot = kind (1: 1x1, 2: 3-tap, 3: 1x1 in sequence, 4: 1x1 three per CU), gen = 5
+  // probe label: mode 3 = dual, prologue slot = kind (2: 3-tap, 3: 1x1 in sequence), gen = 5
   const int info[5] = {VQX_BF16, 3, kind, 5, ekd};
-  static const int chunk = [] {  // interleave period (blocks of each GEMM per group; env VQX_DUAL_CHUNK, A/B)
-    const char* e = getenv("VQX_DUAL_CHUNK");
-    const int c = e ? atoi(e) : 256;
-    return c >= 8 && c % 8 == 0 ? c : 8;
-  }();
+  const int chunk = 256;  // interleave period: blocks of each GEMM per group (profiles/r02/chunk_probe.txt)
   GemmParams pd = PD, pw = PW;
   int a = nd, b = nw, c = chunk;
   void* args[] = {(void*)&pd, (void*)&pw, (void*)&a, (void*)&b, (void*)&c};

@@ -22,7 +22,7 @@ void gemm_launch_args(const void* fn, int grid, hipStream_t s, void** args, cons
 // (dual_k1_kernel / dual_tr_kernel) where an instance covers the pair;
 // false = not covered (the caller launches them separately)
 bool launch_dual(const GemmParams& PD, int nd, const GemmParams& PW, int nw, hipStream_t s);
-int dual_policy();  // vqx_gemm.hip: 0 off, 1 3-tap pairs, 2 (3) 3-tap and 1x1 pairs (1x1 in sequence) (env VQX_DUAL)
+int dual_policy();  // vqx_gemm.hip: 0 off, 1 3-tap pairs, 3 3-tap and 1x1 pairs (1x1 in sequence) (env VQX_DUAL)
 
 // vqx_gemm.hip: tap-reuse kernel switch (env VQX_TAP_REUSE=0 turns it off, for A/B runs)
 bool tap_reuse_enabled();
@@ -38,23 +38,10 @@ inline bool tap_reuse_ok(const GemmParams& P, bool bf16, bool gen) {
 
 // wgrad_tr_kernel applies: bf16, no prologue, 3 taps / pad 1, c_dim % 64 == 0,
 // 64-frame K-tiles inside one utterance
-// K groups per tap-reuse WGRAD workgroup (default 1; env VQX_WGRAD_KG=2: two 4-wave groups)
-int wgrad_kgroups();
-// wgrad_tr2_kernel (8 waves): 3-tap layers with c_dim % 128 == 0 (128 c per
-// workgroup) and 1x1 layers with c_dim % 256 == 0 (256 c per workgroup)
-bool wgrad_wide();
-inline bool wgrad_wide1_ok(int64_t n_rows, int T, int c_dim, int ntaps, int pad, bool bf16, int pro) {
-  return bf16 && pro == VQX_PRO_NONE && ntaps == 1 && pad == 0 && c_dim % 256 == 0 && T % 64 == 0 &&
-         n_rows % 64 == 0 && wgrad_wide();
-}
-
 inline bool wgrad_tr_ok(int64_t n_rows, int T, int c_dim, int ntaps, int pad, int dil, bool bf16, int pro) {
   return bf16 && pro == VQX_PRO_NONE && ntaps == 3 && pad == 1 && dil == 1 && c_dim % 64 == 0 && T % 64 == 0 &&
          n_rows % 64 == 0 && tap_reuse_enabled();
 }
-
-// channels per tap-reuse stage: 32 (2-deep ring, default) or 16 (4-deep ring; env VQX_TR_BKC=16)
-int tr_stage_channels();
 
 // frame segments per conv_tr8_kernel tile (0 = use conv_tr_kernel).  Env
 // VQX_TR8=0/1/2 forces it.  By default the 512-frame tile where it still gives
@@ -63,7 +50,7 @@ int tr_stage_channels();
 // (profiles/r02/tr_lab.txt), so it is never picked automatically.
 int tr8_policy();
 inline int tr8_segs(const GemmParams& P) {
-  if (P.T % 256 || tr_stage_channels() != 32 || P.kcin % 32) return 0;
+  if (P.T % 256 || P.kcin % 32) return 0;
   const int pol = tr8_policy();
   const int tn = (P.Nc + kBN - 1) / kBN;
   if (pol == 0) return 0;
@@ -83,7 +70,7 @@ void launch_tr(const GemmParams& P, int grid, hipStream_t s) {
     else gemm_launch((const void*)conv_tr8_kernel<MODE, EK, 1>, Q.tiles_m * Q.tiles_n, s, Q, info8, flops, 512);
     return;
   }
-  const int bkc = P.kcin % 32 == 0 ? tr_stage_channels() : 16;
+  const int bkc = P.kcin % 32 == 0 ? 32 : 16;  // 16-channel stages (4-deep ring) only for cin % 32 != 0
   // gen = 2: tap-reuse kernel; the prologue slot carries the stage depth in channels
   const int info[5] = {VQX_BF16, MODE, bkc, 2, EK};
   if (bkc == 16) gemm_launch((const void*)conv_tr_kernel<MODE, EK, 16>, grid, s, P, info, flops);
@@ -156,17 +143,9 @@ void launch_mode_dt(const GemmParams& P, int grid, bool bf16, bool gen, hipStrea
   if constexpr (MODE == MODE_WGRAD) {
     if (P.tap_reuse) {
       const double flops = 2.0 * (double)P.n_rows * P.Mc * P.Nc;
-      // gen = 2: tap-reuse kernel; the prologue slot carries the K-group count
-      if (P.tap_reuse >= 3) {  // gen = 4: wide kernels, the prologue slot carries TAPS
-        const int taps = P.tap_reuse == 3 ? 3 : 1;
-        const int info4[5] = {VQX_BF16, MODE_WGRAD, taps, 4, EK_NONE};
-        if (taps == 3) gemm_launch((const void*)wgrad_tr2_kernel<3>, grid, s, P, info4, flops, 512);
-        else gemm_launch((const void*)wgrad_tr2_kernel<1>, grid, s, P, info4, flops, 512);
-        return;
-      }
-      const int info[5] = {VQX_BF16, MODE_WGRAD, P.tap_reuse, 2, EK_NONE};
-      if (P.tap_reuse == 2) gemm_launch((const void*)wgrad_tr_kernel<EK_NONE, 2>, grid, s, P, info, flops, 512);
-      else gemm_launch((const void*)wgrad_tr_kernel<EK_NONE, 1>, grid, s, P, info, flops);
+      // gen = 2: tap-reuse kernel (the prologue slot: 1 K group)
+      const int info[5] = {VQX_BF16, MODE_WGRAD, 1, 2, EK_NONE};
+      gemm_launch((const void*)wgrad_tr_kernel<EK_NONE>, grid, s, P, info, flops);
       return;
     }
     launch_pro<bf16_t, MODE, false, EK_NONE>(P, grid, s);

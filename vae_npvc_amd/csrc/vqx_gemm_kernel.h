@@ -33,35 +33,10 @@
 
 #include "vqx_common.h"
 
-// tools/gemm_lab.hip only: 1 = no operand DMA in the main loop, 2 = no MFMA
-#ifndef VQX_LAB_MODE
-#define VQX_LAB_MODE 0
-#endif
-
 
 namespace vqx {
 
 constexpr int kBN = 128;  // tile width (and height)
-// tools/lab/tr_lab.hip builds the tap-reuse kernels with VQX_GEMM_LAB = 1 (no
-// operand DMA in the main loop), 2 (no fragment reads / MFMAs), 3 (no epilogue)
-#ifndef VQX_GEMM_LAB
-#define VQX_GEMM_LAB 0
-#endif
-#ifndef VQX_EPI_PREFETCH  // 0: the 1x1 epilogues load their row operands pass by pass (A/B)
-#define VQX_EPI_PREFETCH 1
-#endif
-#ifndef VQX_EPI_PREVEC_DGRAD  // 1: DGRAD epilogues hoist the per-channel vectors too (A/B)
-#define VQX_EPI_PREVEC_DGRAD 0
-#endif
-#ifndef VQX_EPI_PREFETCH_DGRAD  // 1: DGRAD epilogues prefetch their row operands too (A/B)
-#define VQX_EPI_PREFETCH_DGRAD 0
-#endif
-#ifndef VQX_EPI_PREFETCH_LATE  // n > 0: issue the row-operand prefetch at main-loop iteration nk-n, not with the prologue
-#define VQX_EPI_PREFETCH_LATE 0
-#endif
-#ifndef VQX_EPI_SLAB_PREFETCH  // 1: DGRAD epilogues load each 64-row slab's row operands before the slab's passes
-#define VQX_EPI_SLAB_PREFETCH 0
-#endif
 constexpr unsigned kOOB = 0x80000000u;  // buffer offset that is always out of range -> loads 0
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 
@@ -232,12 +207,6 @@ __device__ __forceinline__ void st8(void* p, int64_t i, const float* f) {
 // (profiles/r01/gemm_lab.txt) but the whole step 1.3% (outputs) / 2.9% (also
 // the WGRAD slabs) slower: the consumer then reads from HBM instead of the
 // Infinity Cache (profiles/r01/nt_store_ab.txt).  Off by default.
-#ifndef VQX_NT_Y
-#define VQX_NT_Y 0     // non-temporal FWD/DGRAD output stores
-#endif
-#ifndef VQX_NT_SLAB
-#define VQX_NT_SLAB 0  // non-temporal WGRAD slab stores
-#endif
 template <typename T, bool NT = true>
 __device__ __forceinline__ void st8_nt(void* p, int64_t i, const float* f) {
   if constexpr (!NT) {
@@ -458,8 +427,8 @@ __device__ __forceinline__ void epilogue8(const GemmParams& P, int64_t row, int 
       for (int e = 0; e < 8; ++e) v[e] = t[e];
     }
   }
-  if (P.out_f32) st8_nt<float, VQX_NT_Y>(P.y, row * P.ldy + col, v);
-  else st8_nt<T, VQX_NT_Y>(P.y, row * P.ldy + col, v);
+  if (P.out_f32) st8_nt<float, false>(P.y, row * P.ldy + col, v);
+  else st8_nt<T, false>(P.y, row * P.ldy + col, v);
 }
 
 // GNBWD: GroupNorm-backward sums of this output (the GN input's gradient dy)
@@ -495,12 +464,8 @@ __device__ __forceinline__ void gnbwd8(const GemmParams& P, int64_t row, int col
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const float xa = (ua[e] - ma) * ra, xb = (ub[e] - mb) * rb;
-#ifdef VQX_LAB_GNBWD_NOTRANS  // lab only: the GLU derivative without its transcendentals (timing split)
-    const float ta = xa * ga[e] + ba[e], sb = xb * gb[e] + bb[e];
-#else
     const float ta = ftanh<sizeof(T) == 2>(xa * ga[e] + ba[e]);
     const float sb = fsigmoid<sizeof(T) == 2>(xb * gb[e] + bb[e]);
-#endif
     const float dga = ga[e] * (dy[e] * sb * (1.f - ta * ta));
     const float dgb = gb[e] * (dy[e] * ta * (sb * (1.f - sb)));
     s[0] += dga;
@@ -565,11 +530,7 @@ __device__ __forceinline__ void wait_vm(int n) {
 // 44 KiB of `smem`; the caller's staging buffers must be free.  `tid` is the
 // thread's index in the 4-wave group that owns the tile (conv_tr8_kernel runs
 // two such groups side by side; every group passes the same barriers).
-// SLABPRE: the row operands of each 64-row slab's four passes are loaded
-// together at the start of the slab (before its LDS transpose), so the
-// passes' loads are in flight at once instead of one dependent round trip per
-// pass behind the previous pass's stores (which may alias them).
-template <typename T, int MODE, int EK, bool PRE = false, bool PREVEC = PRE, bool SLABPRE = false>
+template <typename T, int MODE, int EK, bool PRE = false, bool PREVEC = PRE>
 __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&acc)[2][2], char* smem, int m0, int n0,
                                               int tn, int split, const float* gmr, int tid,
                                               const EpiRows* R = nullptr) {
@@ -594,8 +555,6 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
   // row operands R->r*[slab*4 + pass] are register-resident
   static_for<2 * SUB>([&](auto slab_c) __attribute__((always_inline)) {
     constexpr int slab = decltype(slab_c)::value;
-    EpiRows SR;
-    if constexpr (SLABPRE) epi_prefetch<EK, slab * 4, 4>(P, m0, n0, tid, SR);
     if (wm == slab) {
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
@@ -621,11 +580,11 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
         if (row < P.Mc && col < P.Nc) {  // Nc % 8 == 0
           const int64_t at = (int64_t)split * P.Mc * P.Nc + row * P.Nc + col;
           if (sizeof(T) == 2 && P.slab_bf16) st8<bf16_t>(P.y, at, v);
-          else st8_nt<float, VQX_NT_SLAB>((float*)P.y + at, 0, v);
+          else st8_nt<float, false>((float*)P.y + at, 0, v);
         }
       } else {
         if (row < P.n_rows && col < P.Nc) {
-          const EpiOps o = SLABPRE ? epi_ops<slab * 4 + pass, true>(&SR) : epi_ops<slab * 4 + pass, PRE>(R);
+          const EpiOps o = epi_ops<slab * 4 + pass, PRE>(R);
           epilogue8<T, EMASK, PREVEC>(P, row, col, v, gmr, o, V);
 #pragma unroll
           for (int e = 0; e < 8; ++e) cs[e] += v[e];
@@ -639,9 +598,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
             for (int e = 0; e < 8; ++e) q8 = fmaf(v[e] - m8, v[e] - m8, q8);
             moments_merge(mn, mm, mq, 8.f, m8, q8);
           }
-#ifndef VQX_LAB_NO_GNBWD  // lab only (tools/lab/k1_lab.cpp): skip the GroupNorm/GLU backward sums
           if (P.epi & EMASK & VQX_EPI_GNBWD) gnbwd8<T, PREVEC>(P, row, col, v, gs, o, V);
-#endif
         }
       }
     });
@@ -749,10 +706,6 @@ __device__ __forceinline__ void conv_gemm_body(const GemmParams& P, int bid, int
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
-#ifdef VQX_GEMM_STAGGER  // lab only (tools/lab/k1_lab.cpp): delay the second resident workgroup of each CU
-  if (bid >= nwg / 2)
-    for (int i = 0; i < VQX_GEMM_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
-#endif
   const int lin = xcd_remap(bid, nwg);
   const int tiles_mn = P.tiles_m * P.tiles_n;
   const int split = lin / tiles_mn;
@@ -1070,11 +1023,9 @@ __device__ __forceinline__ void conv_gemm_body(const GemmParams& P, int bid, int
   // prologue (tools/lab/k1_lab.cpp, profiles/r02/k1_lab.txt: SPLIT 33.4 -> 30.6 us,
   // GNADD 26.9 -> 26.0 us; the DGRAD GNBWD epilogues, VALU-bound, ran 5-9% slower
   // with it and keep loading pass by pass)
-  constexpr bool kPrefetch = sizeof(T) == 2 && EK != EK_NONE && EK != EK_ALL && VQX_EPI_PREFETCH &&
-                             (MODE == MODE_FWD || (MODE == MODE_DGRAD && VQX_EPI_PREFETCH_DGRAD));
-  // per-channel vectors (bias, GN affine) hoisted out of the row passes
-  constexpr bool kPreVec = (kPrefetch && MODE == MODE_FWD) ||
-                          (sizeof(T) == 2 && MODE == MODE_DGRAD && EK != EK_NONE && EK != EK_ALL && VQX_EPI_PREVEC_DGRAD);
+  constexpr bool kPrefetch = sizeof(T) == 2 && EK != EK_NONE && EK != EK_ALL && MODE == MODE_FWD;
+  // per-channel vectors (bias, GN affine) hoisted out of the row passes (FWD)
+  constexpr bool kPreVec = kPrefetch;
   EpiRows rows;
   if constexpr (kPrefetch) {
     if (nk <= 0) epi_prefetch<EK>(P, m0, n0, tid, rows);
@@ -1085,23 +1036,14 @@ __device__ __forceinline__ void conv_gemm_body(const GemmParams& P, int bid, int
 #pragma unroll
     for (int t = 0; t < NST - 1; ++t)
       if (t < pre) dma_tile(t, t);
-    if constexpr (kPrefetch && VQX_EPI_PREFETCH_LATE == 0) epi_prefetch<EK>(P, m0, n0, tid, rows);  // lands with the prologue DMA
+    if constexpr (kPrefetch) epi_prefetch<EK>(P, m0, n0, tid, rows);  // lands with the prologue DMA
     wait_vm(NP * (pre - 1));
     __builtin_amdgcn_s_barrier();
     int buf = 0;
     for (int kt = 0; kt < nk; ++kt) {
       const int fbuf = (buf + NST - 1) % NST;  // buffer of tile kt+NST-1 == buffer of tile kt-1
-#if VQX_LAB_MODE != 1
       if (kt + NST - 1 < nk) dma_tile(fbuf, kt + NST - 1);
-#endif
-      if constexpr (kPrefetch && VQX_EPI_PREFETCH_LATE > 0) {
-        // vmcnt retires in issue order: issued after the last operand DMA, the
-        // prefetch delays no earlier K-tile's wait
-        if (kt == (nk > VQX_EPI_PREFETCH_LATE ? nk - VQX_EPI_PREFETCH_LATE : 0)) epi_prefetch<EK>(P, m0, n0, tid, rows);
-      }
-#if VQX_LAB_MODE != 2
       compute_tile(buf);
-#endif
       // tile kt+1 must have landed; tiles kt+2 .. min(nk, kt+NST)-1 may stay in flight
       if constexpr (NST == 2) {  // one tile in flight: it must have landed
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1116,22 +1058,7 @@ __device__ __forceinline__ void conv_gemm_body(const GemmParams& P, int bid, int
     }
   }
 
-#if VQX_LAB_MODE == 3  // lab only: no epilogue (the accumulators stay live)
-  if (P.n_rows < 0) {
-    float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) t += acc[i][j][e];
-    ((float*)P.y)[tid] = t;
-  }
-  return;
-#endif
-  constexpr bool kSlabPre = sizeof(T) == 2 && MODE == MODE_DGRAD && EK != EK_NONE && EK != EK_ALL && !kPrefetch &&
-                            VQX_EPI_SLAB_PREFETCH;
-  tile_epilogue<T, MODE, EK, kPrefetch, kPreVec, kSlabPre>(P, acc, smem, m0, n0, tn, split, gmr, (int)threadIdx.x, &rows);
+  tile_epilogue<T, MODE, EK, kPrefetch, kPreVec>(P, acc, smem, m0, n0, tn, split, gmr, (int)threadIdx.x, &rows);
 }
 
 template <typename T, int MODE, int PRO, bool GEN, int BK, int NST, int EK>
@@ -1307,8 +1234,8 @@ __device__ __forceinline__ void conv_tr_body(const GemmParams& P, int bid, int n
     __builtin_amdgcn_s_barrier();
     int buf = 0;
     for (int kt = 0; kt < nk; ++kt) {
-      if (VQX_GEMM_LAB != 1 && kt + NST - 1 < nk) dma_stage(buf == 0 ? NST - 1 : buf - 1, kt + NST - 1);
-      if (VQX_GEMM_LAB != 2) compute_stage(buf);
+      if (kt + NST - 1 < nk) dma_stage(buf == 0 ? NST - 1 : buf - 1, kt + NST - 1);
+      compute_stage(buf);
       if constexpr (NST == 2) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       } else {  // stage kt+1 must have landed; later ones may stay in flight
@@ -1320,13 +1247,6 @@ __device__ __forceinline__ void conv_tr_body(const GemmParams& P, int bid, int n
       __builtin_amdgcn_s_barrier();
       buf = buf + 1 == NST ? 0 : buf + 1;
     }
-  }
-  if (VQX_GEMM_LAB == 3) {  // keep the accumulators live
-    float t = 0.f;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) t += acc[0][0][e] + acc[0][1][e] + acc[1][0][e] + acc[1][1][e];
-    if (t == 12345.f) ((float*)P.y)[threadIdx.x] = t;
-    return;
   }
   tile_epilogue<T, MODE, EK>(P, acc, smem, m0, n0, tn, 0, P.gn_mr, (int)threadIdx.x);
 }
@@ -1508,8 +1428,8 @@ __global__ __launch_bounds__(512, 1) void conv_tr8_kernel(GemmParams P) {
     __builtin_amdgcn_s_barrier();
     int buf = 0;
     for (int kt = 0; kt < nk; ++kt) {
-      if (VQX_GEMM_LAB != 1 && kt + NST - 1 < nk) dma_stage(buf == 0 ? NST - 1 : buf - 1, kt + NST - 1);
-      if (VQX_GEMM_LAB != 2) compute_stage(buf);
+      if (kt + NST - 1 < nk) dma_stage(buf == 0 ? NST - 1 : buf - 1, kt + NST - 1);
+      compute_stage(buf);
       if constexpr (NST == 2) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       } else {  // stage kt+1 must have landed; later ones may stay in flight
@@ -1521,15 +1441,6 @@ __global__ __launch_bounds__(512, 1) void conv_tr8_kernel(GemmParams P) {
       __builtin_amdgcn_s_barrier();
       buf = buf + 1 == NST ? 0 : buf + 1;
     }
-  }
-  if (VQX_GEMM_LAB == 3) {  // keep the accumulators live
-    float t = 0.f;
-#pragma unroll
-    for (int j = 0; j < SEGS; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) t += acc[j][0][0][e] + acc[j][0][1][e] + acc[j][1][0][e] + acc[j][1][1][e];
-    if (t == 12345.f) ((float*)P.y)[tid] = t;
-    return;
   }
 #pragma unroll
   for (int j = 0; j < SEGS; ++j)
@@ -1556,38 +1467,26 @@ __global__ __launch_bounds__(512, 1) void conv_tr8_kernel(GemmParams P) {
 // shift.
 __device__ __forceinline__ int q_off128(int row, int ch) { return row * 128 + 16 * (ch ^ (((row >> 1) & 1) << 2)); }
 
-// KG = 2 splits K inside the workgroup as well: two 4-wave groups (8 waves,
-// one workgroup per CU) take alternate 64-frame K-tiles of the same output
-// tile, each through its own LDS ring, and are summed in LDS before the slab
-// store.  Same waves per CU as two 4-wave workgroups, half the slabs to write
-// and to reduce in the weight-norm backward.
-// LDS bytes of wgrad_tr_body: KG rings of two 25-KiB stages, at least the
-// slab-store staging (128 x 68 floats) and the K-group reduction
-template <int KG>
-__host__ __device__ constexpr int wgrad_tr_smem() {
-  return (KG * 2 * 25600 > 128 * 68 * 4 ? KG * 2 * 25600 : 128 * 68 * 4) > (KG > 1 ? 4 * 6 * 64 * 64 : 0)
-             ? (KG * 2 * 25600 > 128 * 68 * 4 ? KG * 2 * 25600 : 128 * 68 * 4)
-             : (KG > 1 ? 4 * 6 * 64 * 64 : 0);
-}
+// LDS bytes of wgrad_tr_body: two 25-KiB stages, at least the slab-store
+// staging (128 x 68 floats)
+__host__ __device__ constexpr int wgrad_tr_smem() { return 2 * 25600 > 128 * 68 * 4 ? 2 * 25600 : 128 * 68 * 4; }
 
-template <int EK, int KG>
+template <int EK>
 __device__ __forceinline__ void wgrad_tr_body(const GemmParams& P, int bid, int nwg, char* smem) {
   using T = bf16_t;
-  constexpr int ES = 2, EPC = 8, BK = 64, NT = 256 * KG;
+  constexpr int ES = 2, EPC = 8, BK = 64, NT = 256;
   constexpr int A_BYTES = BK * 256;              // p: 64 frames x 128 r
   constexpr int B_PIECES = 9;                    // q: 66 frames x 64 c (72-row capacity)
   constexpr int B_BYTES = B_PIECES * 1024;
   constexpr int STAGE = A_BYTES + B_BYTES;       // 25 KiB
   constexpr int NST = 2;
   constexpr int EP_LD = 64 + 4;                  // epilogue row pitch (floats)
-  constexpr int RED_BYTES = KG > 1 ? 4 * 6 * 64 * 64 : 0;  // one group's accumulators
-  constexpr int SMEM0 = KG * NST * STAGE > 128 * EP_LD * 4 ? KG * NST * STAGE : 128 * EP_LD * 4;
-  constexpr int SMEM = SMEM0 > RED_BYTES ? SMEM0 : RED_BYTES;
-  static_assert(wgrad_tr_smem<KG>() == SMEM, "LDS");
+  constexpr int SMEM = NST * STAGE > 128 * EP_LD * 4 ? NST * STAGE : 128 * EP_LD * 4;
+  static_assert(wgrad_tr_smem() == SMEM, "LDS");
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = wid >> 2, wl = wid & 3;  // K group, wave within the group
+  const int wl = wid;
   const int wm = wl >> 1, wn = wl & 1;
   const int lin = xcd_remap(bid, nwg);
   const int tiles_mn = P.tiles_m * P.tiles_n;
@@ -1599,7 +1498,6 @@ __device__ __forceinline__ void wgrad_tr_body(const GemmParams& P, int bid, int 
   int64_t kend = kbeg + P.k_per_split;
   if (kend > P.n_rows) kend = P.n_rows;
   const int nk = kend > kbeg ? (int)((kend - kbeg) / BK) : 0;
-  const int nit = (nk + KG - 1) / KG;  // iterations per group; group g takes K-tiles g, g+KG, ...
 
   // p pieces wl*4 .. wl*4+3 (16 per stage)
   unsigned aoff[4];
@@ -1625,15 +1523,14 @@ __device__ __forceinline__ void wgrad_tr_body(const GemmParams& P, int bid, int 
   }
   const __amdgpu_buffer_rsrc_t rsA = rsrc_at(P.a, 0, P.a_bytes);
   const __amdgpu_buffer_rsrc_t rsB = rsrc_at(P.b, -(int64_t)P.ldb * ES, P.b_bytes);
-  char* gsm = smem + grp * NST * STAGE;  // this group's ring
+  char* gsm = smem;
 
-  int ld_t0 = (int)((kbeg + (int64_t)grp * BK) % P.T);  // frame-in-utterance of this group's next K-tile
-  auto dma_stage = [&](int buf, int kt) {  // called for kt = grp, grp+KG, ... in order
+  int ld_t0 = (int)(kbeg % P.T);  // frame-in-utterance of the next K-tile to load
+  auto dma_stage = [&](int buf, int kt) {  // called for kt = 0, 1, ... in order
     const int64_t k0 = kbeg + (int64_t)kt * BK;
     const int t0 = ld_t0;
-    ld_t0 += KG * BK;  // KG * BK <= 2T (T % 64 == 0)
+    ld_t0 += BK;  // BK <= T (T % 64 == 0)
     if (ld_t0 >= P.T) ld_t0 -= P.T;
-    if (KG > 1 && ld_t0 >= P.T) ld_t0 -= P.T;
     const int edge = (t0 == 0 ? 1 : 0) | (t0 + BK == P.T ? 2 : 0);  // halo rows outside the utterance
     const unsigned ksa = (unsigned)(k0 * P.lda * ES), ksb = (unsigned)(k0 * P.ldb * ES);
     char* st = gsm + buf * STAGE;
@@ -1695,17 +1592,14 @@ __device__ __forceinline__ void wgrad_tr_body(const GemmParams& P, int bid, int 
     }
   };
 
-  // every wave runs nit iterations and every barrier; a group's missing last
-  // K-tile (nk odd) is neither loaded nor multiplied
-  if (nit > 0) {
-    if (grp < nk) dma_stage(0, grp);
+  if (nk > 0) {
+    dma_stage(0, 0);
     wait_vm(0);
     __builtin_amdgcn_s_barrier();
     int buf = 0;
-    for (int it = 0; it < nit; ++it) {
-      const int kt = it * KG + grp;
-      if (VQX_GEMM_LAB != 1 && it + 1 < nit && kt + KG < nk) dma_stage(buf ^ 1, kt + KG);
-      if (VQX_GEMM_LAB != 2 && kt < nk) compute_stage(buf);
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) dma_stage(buf ^ 1, kt + 1);
+      compute_stage(buf);
       wait_vm(0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -1713,57 +1607,19 @@ __device__ __forceinline__ void wgrad_tr_body(const GemmParams& P, int bid, int 
     }
   }
 
-  if constexpr (KG > 1) {  // group 1's accumulators -> LDS (lane-linear) -> added by group 0
-    float* red = (float*)smem;
-    __syncthreads();
-    if (grp == 1) {
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-#pragma unroll
-          for (int gq = 0; gq < 4; ++gq) {
-            const f32x4_t v = {acc[mi][j][4 * gq], acc[mi][j][4 * gq + 1], acc[mi][j][4 * gq + 2], acc[mi][j][4 * gq + 3]};
-            *(f32x4_t*)(red + (((wl * 6 + mi * 3 + j) * 4 + gq) * 64 + lane) * 4) = v;
-          }
-    }
-    __syncthreads();
-    if (grp == 0) {
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-#pragma unroll
-          for (int gq = 0; gq < 4; ++gq) {
-            const f32x4_t v = *(const f32x4_t*)(red + (((wl * 6 + mi * 3 + j) * 4 + gq) * 64 + lane) * 4);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc[mi][j][4 * gq + e] += v[e];
-          }
-    }
-  }
-
-  if (VQX_GEMM_LAB == 3) {  // keep the accumulators live
-    float t = 0.f;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) t += acc[0][0][e] + acc[0][1][e] + acc[0][2][e] + acc[1][0][e] + acc[1][1][e] + acc[1][2][e];
-    if (t == 12345.f) ((float*)P.y)[tid] = t;
-    return;
-  }
   // slab store, one tap at a time through LDS: rows of 64 channels, 8 lanes x 8 floats each
   float* ep = (float*)smem;
   const int64_t slab0 = (int64_t)split * P.Mc * P.Nc;
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     __syncthreads();
-    if (grp == 0) {
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
+    for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          const f32x4_t v = {acc[mi][j][4 * gq], acc[mi][j][4 * gq + 1], acc[mi][j][4 * gq + 2], acc[mi][j][4 * gq + 3]};
-          *(f32x4_t*)(ep + (wm * 64 + mi * 32 + r32) * EP_LD + wn * 32 + 8 * gq + 4 * h) = v;
-        }
-    }
+      for (int gq = 0; gq < 4; ++gq) {
+        const f32x4_t v = {acc[mi][j][4 * gq], acc[mi][j][4 * gq + 1], acc[mi][j][4 * gq + 2], acc[mi][j][4 * gq + 3]};
+        *(f32x4_t*)(ep + (wm * 64 + mi * 32 + r32) * EP_LD + wn * 32 + 8 * gq + 4 * h) = v;
+      }
     __syncthreads();
 #pragma unroll
     for (int pass = 0; pass < 128 / (NT / 8); ++pass) {
@@ -1786,229 +1642,10 @@ __device__ __forceinline__ void wgrad_tr_body(const GemmParams& P, int bid, int 
   }
 }
 
-template <int EK, int KG>
-__global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void wgrad_tr_kernel(GemmParams P) {
-  __shared__ __attribute__((aligned(16))) char smem[wgrad_tr_smem<KG>()];
-  wgrad_tr_body<EK, KG>(P, blockIdx.x, gridDim.x, smem);
-}
-
-// ---------------------------------------------------------------------------
-// Wide weight gradients (8 waves, one workgroup per CU).
-//
-// TAPS = 3: the same S[r][j*cd + c] as wgrad_tr_kernel over 128 rows r x
-// (3 taps x 128 channels c).  wgrad_tr_kernel stages 25 KiB (p 16 + q 9) per
-// 64-frame stage for 3.1 MFLOP, i.e. ~65 GB/s per CU of LDS-DMA fill at the
-// MFMA rate of two workgroups -- the fill rate the staging sustains.  Here the
-// 16 KiB p slice serves two 64-channel q blocks: 34 KiB per stage for
-// 6.3 MFLOP (1.5x the FLOPs per staged byte), with the waves' own work
-// unchanged (64 r x 3 taps x 32 c, 24 MFMAs per stage).  Wave w: r half
-// w & 1, 32-channel quarter w >> 1.
-//
-// TAPS = 1: the 1x1 weight gradient S[r][c] = sum_n p[n][r] q[n][c] over
-// 128 r x 256 c (conv_gemm_kernel's WGRAD stages 32 KiB per 2.1 MFLOP; here
-// 52 KiB per 8.4 MFLOP, 2.5x the FLOPs per staged byte).  Wave w: r half
-// w & 1, 64-channel q block w >> 1 (64 r x 64 c, 16 MFMAs per stage).
-//
-// Each 64-channel q block is laid out exactly as wgrad_tr_kernel's q (the
-// frames k0-1 .. k0+64 in 128-B rows, q_off128), so the tap-shifted fragment
-// reads keep its bank pattern; the 1x1 form reads the centre rows only.
-// tiles_n counts 64 * QBLK-channel blocks of c.
-template <int TAPS>
-__global__ __launch_bounds__(512, 1) void wgrad_tr2_kernel(GemmParams P) {
-  using T = bf16_t;
-  static_assert(TAPS == 1 || TAPS == 3, "TAPS");
-  constexpr int ES = 2, EPC = 8, BK = 64, NT = 512;
-  constexpr int QBLK = TAPS == 3 ? 2 : 4;       // 64-channel q blocks per workgroup
-  constexpr int NJ = TAPS == 3 ? 3 : 2;         // accumulator columns per wave (taps / 32-c halves)
-  constexpr int A_BYTES = BK * 256;             // p: 64 frames x 128 r (16 pieces)
-  constexpr int QB_PIECES = 9;                  // one q block: 66 frames (72-row capacity) x 128 B
-  constexpr int QB_BYTES = QB_PIECES * 1024;
-  constexpr int QP = QBLK * QB_PIECES;          // q pieces per stage
-  constexpr int QPW = (QP + 7) / 8;             // ... per wave (some waves one fewer)
-  constexpr int STAGE = A_BYTES + QBLK * QB_BYTES;  // 34 / 52 KiB
-  constexpr int NST = 2;
-  constexpr int EP_LD = 128 + 4;                // epilogue row pitch (floats)
-  constexpr int SMEM = NST * STAGE > 128 * EP_LD * 4 ? NST * STAGE : 128 * EP_LD * 4;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid & 1, wc = wid >> 1;                  // r half; 32-c quarter (TAPS 3) / q block (TAPS 1)
-  const int qb = TAPS == 3 ? wc >> 1 : wc;                // this wave's q block
-  const int wn = TAPS == 3 ? wc & 1 : 0;                  // 32-channel half of it (TAPS 3)
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int tiles_mn = P.tiles_m * P.tiles_n;
-  const int split = lin / tiles_mn;
-  const int tmn = lin - split * tiles_mn;
-  const int tm = tmn / P.tiles_n, tn = tmn - tm * P.tiles_n;
-  const int r0 = tm * 128, c0 = tn * (64 * QBLK);
-  const int64_t kbeg = (int64_t)split * P.k_per_split;
-  int64_t kend = kbeg + P.k_per_split;
-  if (kend > P.n_rows) kend = P.n_rows;
-  const int nk = kend > kbeg ? (int)((kend - kbeg) / BK) : 0;
-
-  // p pieces 2*wid, 2*wid+1
-  unsigned aoff[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int c = (2 * wid + i) * 64 + lane;
-    const int krow = c / 16, cch = (c % 16) ^ mn_swz(krow);
-    const int r = r0 + cch * EPC;
-    aoff[i] = r < P.Mc ? (unsigned)(((int64_t)krow * P.lda + r) * ES) : kOOB;
-  }
-  // q pieces wid, wid+8, ... (< QP): block pc / 9, piece pc % 9 of it; stage row sr holds frame k0-1+sr
-  unsigned boff[QPW];
-  int bedge[QPW], bdst[QPW];
-#pragma unroll
-  for (int i = 0; i < QPW; ++i) {
-    const int pc = wid + 8 * i;
-    const int blk = pc / QB_PIECES, lp = pc - blk * QB_PIECES;
-    const int c = lp * 64 + lane;
-    const int row = c / 8, ch = (c % 8) ^ (((row >> 1) & 1) << 2);
-    const int cc = c0 + blk * 64 + ch * EPC;
-    bedge[i] = row == 0 ? 1 : (row == 65 ? 2 : 0);
-    bdst[i] = A_BYTES + blk * QB_BYTES + lp * 1024;
-    // descriptor base one q row before P.b: frame k0-1+row sits at (k0+row) rows
-    boff[i] = (pc < QP && row < 66 && cc < P.cdim) ? (unsigned)(((int64_t)row * P.ldb + cc) * ES) : kOOB;
-  }
-  const int nqp = (QP - wid + 7) / 8;
-  const __amdgpu_buffer_rsrc_t rsA = rsrc_at(P.a, 0, P.a_bytes);
-  const __amdgpu_buffer_rsrc_t rsB = rsrc_at(P.b, -(int64_t)P.ldb * ES, P.b_bytes);
-
-  int ld_t0 = (int)(kbeg % P.T);  // frame-in-utterance of the next K-tile to load
-  auto dma_stage = [&](int buf, int kt) {  // called for kt = 0, 1, ... in order
-    const int64_t k0 = kbeg + (int64_t)kt * BK;
-    const int t0 = ld_t0;
-    ld_t0 += BK;
-    if (ld_t0 >= P.T) ld_t0 -= P.T;
-    const int edge = (t0 == 0 ? 1 : 0) | (t0 + BK == P.T ? 2 : 0);  // halo rows outside the utterance
-    const unsigned ksa = (unsigned)(k0 * P.lda * ES), ksb = (unsigned)(k0 * P.ldb * ES);
-    char* st = smem + buf * STAGE;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) dma16(rsA, st + (2 * wid + i) * 1024, aoff[i] + ksa);
-#pragma unroll
-    for (int i = 0; i < QPW; ++i)
-      if (i < nqp) dma16(rsB, st + bdst[i], (bedge[i] & edge) ? kOOB : boff[i] + ksb);
-  };
-
-  f32x16_t acc[2][NJ];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-
-  const int r32 = lane & 31, h = lane >> 5;
-  const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
-  typedef short s16x8_t __attribute__((ext_vector_type(8)));
-  const int ro0 = 1 - P.sign, ro2 = 1 + P.sign;  // stage-row offset of taps 0 and 2 (tap 1: 1)
-
-  auto compute_stage = [&](int buf) {
-    const char* la = smem + buf * STAGE;
-    const char* lb = la + A_BYTES + qb * QB_BYTES;
-#pragma unroll
-    for (int s = 0; s < BK / 16; ++s) {
-      bf16x8_t af[2], bfr[NJ];
-#pragma unroll
-      for (int x = 0; x < 2; ++x) {
-        const int kb = 16 * s + (g >> 1) * 8;
-        const int ch = ((wm * 64 + x * 32 + (g & 1) * 16) >> 3) + (p >> 1);
-        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (VQX_LDS(s16x4_t)*)(la + mnmaj_off<T>(kb + q, ch) + 8 * (p & 1)));
-        const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (VQX_LDS(s16x4_t)*)(la + mnmaj_off<T>(kb + 4 + q, ch) + 8 * (p & 1)));
-        const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        af[x] = __builtin_bit_cast(bf16x8_t, v);
-      }
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        // TAPS 3: tap j of the wave's 32 channels; TAPS 1: 32-channel half j at the centre rows
-        const int ro = TAPS == 1 ? 1 : (j == 0 ? ro0 : (j == 1 ? 1 : ro2));
-        const int kb = 16 * s + (g >> 1) * 8 + ro;
-        const int ch = (((TAPS == 1 ? j : wn) * 32 + (g & 1) * 16) >> 3) + (p >> 1);
-        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (VQX_LDS(s16x4_t)*)(lb + q_off128(kb + q, ch) + 8 * (p & 1)));
-        const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (VQX_LDS(s16x4_t)*)(lb + q_off128(kb + 4 + q, ch) + 8 * (p & 1)));
-        const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        bfr[j] = __builtin_bit_cast(bf16x8_t, v);
-      }
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-          acc[mi][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[mi], acc[mi][j], 0, 0, 0);
-    }
-  };
-
-  if (nk > 0) {
-    dma_stage(0, 0);
-    wait_vm(0);
-    __builtin_amdgcn_s_barrier();
-    int buf = 0;
-    for (int kt = 0; kt < nk; ++kt) {
-      if (VQX_GEMM_LAB != 1 && kt + 1 < nk) dma_stage(buf ^ 1, kt + 1);
-      if (VQX_GEMM_LAB != 2) compute_stage(buf);
-      wait_vm(0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      buf ^= 1;
-    }
-  }
-  if (VQX_GEMM_LAB == 3) {  // keep the accumulators live
-    float t = 0.f;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) t += acc[0][j][e] + acc[1][j][e];
-    if (t == 12345.f) ((float*)P.y)[tid] = t;
-    return;
-  }
-  // slab store through LDS, 128 columns per pass (TAPS 3: one tap; TAPS 1: one
-  // 128-channel half): rows of 128 columns, 16 lanes x 8 values each
-  float* ep = (float*)smem;
-  const int64_t slab0 = (int64_t)split * P.Mc * P.Nc;
-#pragma unroll
-  for (int ps = 0; ps < (TAPS == 3 ? 3 : 2); ++ps) {
-    __syncthreads();
-    if (TAPS == 3 || (qb >> 1) == ps) {
-#pragma unroll
-      for (int jj = 0; jj < (TAPS == 3 ? 1 : 2); ++jj) {
-        const int j = TAPS == 3 ? ps : jj;                                  // accumulator column
-        const int col = TAPS == 3 ? wc * 32 : (qb & 1) * 64 + jj * 32;      // its LDS column
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-          for (int gq = 0; gq < 4; ++gq) {
-            const f32x4_t v = {acc[mi][j][4 * gq], acc[mi][j][4 * gq + 1], acc[mi][j][4 * gq + 2],
-                               acc[mi][j][4 * gq + 3]};
-            *(f32x4_t*)(ep + (wm * 64 + mi * 32 + r32) * EP_LD + col + 8 * gq + 4 * h) = v;
-          }
-      }
-    }
-    __syncthreads();
-    const int ccol = TAPS == 3 ? c0 : c0 + ps * 128;       // channel of LDS column 0
-    const int64_t cbase = TAPS == 3 ? (int64_t)ps * P.cdim : 0;  // slab column of channel 0
-#pragma unroll
-    for (int pass = 0; pass < 128 / (NT / 16); ++pass) {
-      const int lr = pass * (NT / 16) + (tid >> 4), lc = (tid & 15) * 8;
-      const int r = r0 + lr, cc = ccol + lc;
-      if (r < P.Mc && cc < P.cdim) {
-        const f32x4_t lo = *(const f32x4_t*)(ep + lr * EP_LD + lc);
-        const f32x4_t hi = *(const f32x4_t*)(ep + lr * EP_LD + lc + 4);
-        const int64_t at = slab0 + (int64_t)r * P.Nc + cbase + cc;
-        if (P.slab_bf16) {
-          const float v8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          st8<bf16_t>(P.y, at, v8);
-        } else {
-          float* o = (float*)P.y + at;
-          *(f32x4_t*)o = lo;
-          *(f32x4_t*)(o + 4) = hi;
-        }
-      }
-    }
-  }
+template <int EK>
+__global__ __launch_bounds__(256, 2) void wgrad_tr_kernel(GemmParams P) {
+  __shared__ __attribute__((aligned(16))) char smem[wgrad_tr_smem()];
+  wgrad_tr_body<EK>(P, blockIdx.x, gridDim.x, smem);
 }
 
 }  // namespace vqx

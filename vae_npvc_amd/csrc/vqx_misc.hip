@@ -963,18 +963,6 @@ __global__ __launch_bounds__(256) void gn_glu_fwd_vec_kernel(const T* __restrict
   // two rows' loads in flight before the math of either
   const int rend = min(n_rows, blockIdx.x * fpb + fpb);
   int r = blockIdx.x * fpb + rs;
-#if VQX_GLU_ROWS4
-  for (; r + 3 * nrs < rend; r += 4 * nrs) {  // four rows' loads in flight
-    float ua[4][V], ub[4][V];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      Vec<T>::load(u + (int64_t)(r + q * nrs) * ldu + c, ua[q]);
-      Vec<T>::load(u + (int64_t)(r + q * nrs) * ldu + c + half, ub[q]);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) row(r + q * nrs, ua[q], ub[q]);
-  }
-#endif
   for (; r + nrs < rend; r += 2 * nrs) {
     float ua0[V], ub0[V], ua1[V], ub1[V];
     Vec<T>::load(u + (int64_t)r * ldu + c, ua0);
@@ -1836,9 +1824,7 @@ static int gn_glu_fwd_impl(const void* u, int32_t ldu, void* g, int32_t ldg, int
   if (cpr > 256 || 256 % cpr) { set_error("vqx_gn_glu_fwd: C/2/%d must divide 256", V); return -1; }
   // frames per workgroup: every workgroup of the in-launch-statistics path
   // merges its utterance's GEMM tiles first, so larger blocks amortise that
-  static const int fpb_env = [] { const char* e = getenv("VQX_GLU_FPB"); return e ? atoi(e) : 16; }();
-  int fpb = (fpb_env == 4 || fpb_env == 8 || fpb_env == 32 || fpb_env == 64) ? fpb_env : 16;
-  if (tiles && T % fpb) fpb = 16;
+  const int fpb = 16;  // frames per workgroup (4/8/32/64 measured slower: profiles/r02/glu_fpb_ab.txt)
   const int grid = (int)((n_rows + fpb - 1) / fpb);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == VQX_BF16)

@@ -14,11 +14,6 @@
 // a lowest-index tie-break across lanes), matching torch.argmin.
 #include "vqx_common.h"
 
-// tools/vq_lab.sh only: 1 = no score loop, 2 = no epilogue gather/stores, 3 = both
-#ifndef VQX_VQ_LAB
-#define VQX_VQ_LAB 0
-#endif
-
 namespace vqx {
 
 constexpr int VQ_D = 128;
@@ -75,7 +70,7 @@ __global__ __launch_bounds__(VQ_THREADS, 4) void vq_forward_kernel(const float* 
   const int64_t my_row = (int64_t)blockIdx.x * VQ_FRAMES + fg * 16 + j16;  // A-operand row of this lane
   const bool row_ok = my_row < N;
 
-  const int nsteps = (VQX_VQ_LAB & 1) ? 0 : (K + VQ_STEP - 1) / VQ_STEP;
+  const int nsteps = (K + VQ_STEP - 1) / VQ_STEP;
   // Staging: thread t holds 4 consecutive 16-B chunks (64 B) of code t >> 3 of
   // the step, loaded through one buffer descriptor over E (codes >= K read as
   // zeros, no branches).  The 8 threads of a code also form its ||e||^2
@@ -232,8 +227,7 @@ __global__ __launch_bounds__(VQ_THREADS, 4) void vq_forward_kernel(const float* 
     }
     // NaN rows (every comparison false) keep a well-defined index
     const int my_idx = (bi >= K || bi < 0) ? 0 : bi;
-    if ((VQX_VQ_LAB & 2) && row_ok && q == 0) idx_out[my_row] = my_idx;
-    if (row_ok && !(VQX_VQ_LAB & 2)) {
+    if (row_ok) {
       if (q == 0) idx_out[my_row] = my_idx;
 #pragma unroll
       for (int kb = 0; kb < 8; ++kb) {
