@@ -223,9 +223,11 @@ def test_bf16_general_topology_tracks_oracle():
 
 def test_bf16_bench_step_tracks_fp32_at_full_size():
     """The exact bench configuration -- config 2 (vcc20), 64 x 256 frames,
-    bf16 -- which runs the tall tap-reuse kernel (conv_tr8_kernel, checked
-    through the launch probe), bf16 split-K slabs and the prefetched 1x1
-    epilogues, none of which the 4 x 128 tests reach.  Against the fp32 step
+    bf16 -- which runs the 512-frame ping-pong tap-reuse kernel
+    (conv_pp_kernel) and the three-per-CU 1x1 kernel on the 640-column res/skip
+    conv (conv_gemm3_kernel), both checked through the launch probe, bf16
+    split-K slabs and the prefetched 1x1 epilogues, none of which the 4 x 128
+    tests reach.  Against the fp32 step
     of the same engine on the same weights and batch (itself pinned to the
     reference's full-size run, test_fp32_full_size_step_matches_reference_golden):
     reconstruction loss within 1e-3, commitment loss within 2e-2, codebook
@@ -257,7 +259,9 @@ def test_bf16_bench_step_tracks_fp32_at_full_size():
                        g={n: float(tr.engine.g(p).double().norm()) for n, p in tr.model.named_parameters()})
         del tr, w
         torch.cuda.empty_cache()
-    assert any(s.startswith("vqx::conv_tr8_kernel") for s in res["bf16"]["syms"]), sorted(res["bf16"]["syms"])
+    syms = res["bf16"]["syms"]
+    assert any(s.startswith("vqx::conv_pp_kernel") for s in syms), sorted(syms)
+    assert any(s.startswith("vqx::conv_gemm3_kernel") for s in syms), sorted(syms)
     d32, d16 = res["fp32"]["det"], res["bf16"]["det"]
     assert relclose(d16["X like"], d32["X like"], 1e-3), (d16, d32)
     assert relclose(d16["VQ loss"], d32["VQ loss"], 2e-2, 1e-6), (d16, d32)

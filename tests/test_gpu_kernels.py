@@ -686,9 +686,11 @@ def test_conv_tap_reuse_matches_im2col_and_fp64(mode, n_utt, T, cin, cout):
 @pytest.mark.parametrize("n_utt,T,cin,cout", [(2, 256, 512, 512), (1, 512, 512, 1024), (4, 256, 1024, 512),
                                                (2, 768, 128, 224), (8, 256, 512, 1024)])
 def test_conv_tall_tap_reuse_matches_tap_reuse_and_fp64(mode, n_utt, T, cin, cout):
-    """The tall tap-reuse kernel (vqx_gemm_kernel.h conv_tr8_kernel: 256 or 512
-    frames x 128 columns per 8-wave workgroup, one staged window with halo rows
-    per 256-frame segment) against the 128-frame tap-reuse kernel and fp64
+    """The tall tap-reuse kernels (256 frames: vqx_gemm_kernel.h
+    conv_tr8_kernel; 512 frames: vqx_gemm_pp.h conv_pp_kernel, whose two
+    4-wave groups alternate loading and multiplying; 128 columns per 8-wave
+    workgroup, one staged window with halo rows per 256-frame segment) against
+    the 128-frame tap-reuse kernel and fp64
     torch: segments that start / end utterances and segments whose halo frames
     belong to the same utterance (T = 512, 768), ragged columns (224), and the
     fused epilogues the engine runs on it (bias + residual, GroupNorm
@@ -799,28 +801,41 @@ def test_wgrad_tap_reuse_matches_im2col_and_fp64(sign, n_utt, T, r_dim, c_dim, s
 
 
 @pytest.mark.parametrize("acc", [False, True])
-def test_split_epilogue_with_narrow_residual(acc, tile):
+@pytest.mark.parametrize("B,T", [(2, 128), (64, 256)])
+def test_split_epilogue_with_narrow_residual(acc, B, T, tile):
     """res/skip output split (decoder res_skip layer, layers.py:244-249): the
     GEMM's columns >= split_col go to the fp32 skip accumulator and only the
     first split_col columns take the residual, whose buffer is exactly
-    split_col wide (no read past it on the split columns)."""
+    split_col wide (no read past it on the split columns).  At config 2
+    (64 x 256 frames: 640 tiles, more than one round of two workgroups per CU)
+    the automatic policy runs conv_gemm3_kernel (three per CU); its outputs
+    equal the implicit-im2col kernel's bit for bit."""
     ops = _ops()
+    from vae_npvc_amd import _lib as L
     torch.manual_seed(5)
-    B, T, cin, C, S = 2, 128, 512, 512, 128
+    cin, C, S = 512, 512, 128
     N = B * T
     x = torch.randn(N, cin, device=DEV).to(torch.bfloat16)
     w = (torch.randn(C + S, cin, 1, device=DEV) / cin ** 0.5).to(torch.bfloat16)
     bias = torch.randn(C + S, device=DEV)
     res = torch.randn(N, C, device=DEV).to(torch.bfloat16)  # exactly split_col wide
     skip0 = torch.randn(N, S, device=DEV)
-    skip = skip0.clone()
-    y = torch.empty(N, C, device=DEV, dtype=torch.bfloat16)
-    ops.conv_fwd(x, pack(w.float()).to(torch.bfloat16), y, T=T, cin=cin, cout=C + S, ntaps=1, pad=0, bias=bias,
-                 res=res, out2=skip, split_col=C, out2_accumulate=acc)
-    torch.cuda.synchronize()
+    outs = []
+    for policy in ((0, 1) if tile == 0 else (tile,)):
+        L.call("vqx_set_gemm_tile", policy)
+        skip = skip0.clone()
+        y = torch.empty(N, C, device=DEV, dtype=torch.bfloat16)
+        ops.conv_fwd(x, pack(w.float()).to(torch.bfloat16), y, T=T, cin=cin, cout=C + S, ntaps=1, pad=0, bias=bias,
+                     res=res, out2=skip, split_col=C, out2_accumulate=acc)
+        torch.cuda.synchronize()
+        outs.append((y, skip))
+    L.call("vqx_set_gemm_tile", tile)
+    y, skip = outs[0]
     full = x.double().cpu() @ w.double().cpu()[:, :, 0].t() + bias.double().cpu()
     assert relerr(y, full[:, :C] + res.double().cpu()) < 2e-2
     assert relerr(skip, full[:, C:] + (skip0.double().cpu() if acc else 0)) < 2e-2
+    for y2, skip2 in outs[1:]:
+        assert torch.equal(y, y2) and torch.equal(skip, skip2)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

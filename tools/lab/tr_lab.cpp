@@ -6,9 +6,16 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <cmath>
+#include <algorithm>
 #include <vector>
 
 #include "vqx_gemm_kernel.h"
+#include "vqx_gemm_pp.h"
+#ifndef VQX_GEMM_LAB
+#define VQX_GEMM_LAB VQX_PP_LAB
+#endif
 
 using namespace vqx;
 
@@ -45,6 +52,40 @@ static float time_us(const void* fn, int grid, int block, GemmParams P, int reps
   return 1e3f * ms / reps;
 }
 
+static float bf2f(unsigned short v) {
+  unsigned u = (unsigned)v << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+// one launch of `fn` vs one of conv_tr_kernel (the tested kernel) on the same inputs: max |diff| / max |ref|
+static void check(const Shape& s, const char* name, const void* fn, int rows, int block, GemmParams P) {
+  const size_t n = (size_t)s.N * s.kout;
+  std::vector<unsigned short> a(n), b(n);
+  void* args[] = {(void*)&P};
+  CK(hipMemset(P.y, 0, n * 2));
+  CK(hipLaunchKernel(fn, dim3(P.tiles_m * P.tiles_n), dim3(block), args, 0, 0));
+  CK(hipMemcpy(a.data(), P.y, n * 2, hipMemcpyDeviceToHost));
+  GemmParams R = P;
+  R.tiles_m = (int)(s.N / 128);
+  void* rargs[] = {(void*)&R};
+  CK(hipMemset(P.y, 0, n * 2));
+  const void* ref = s.mode == MODE_FWD ? (const void*)conv_tr_kernel<MODE_FWD, EK_NONE, 32>
+                                       : (const void*)conv_tr_kernel<MODE_DGRAD, EK_NONE, 32>;
+  CK(hipLaunchKernel(ref, dim3(R.tiles_m * R.tiles_n), dim3(256), rargs, 0, 0));
+  CK(hipMemcpy(b.data(), P.y, n * 2, hipMemcpyDeviceToHost));
+  double mx = 0, md = 0;
+  size_t nbad = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const double x = bf2f(a[i]), y = bf2f(b[i]);
+    mx = std::max(mx, std::fabs(y));
+    md = std::max(md, std::fabs(x - y));
+    if (std::fabs(x - y) > 1e-2 * std::fabs(y) + 1e-3) ++nbad;
+  }
+  printf("check %-13s %-10s maxdiff/maxref %.3e  bad %zu of %zu\n", s.name, name, md / mx, nbad, n);
+}
+
 template <int MODE, int EK>
 static void run(const Shape& s, void* x, void* w, void* y, float* part) {
   GemmParams P = {};
@@ -79,9 +120,15 @@ static void run(const Shape& s, void* x, void* w, void* y, float* part) {
   } vs[] = {{"tr128", (const void*)conv_tr_kernel<MODE, EK, 32>, 128, 256},
             {"tr8x256", (const void*)conv_tr8_kernel<MODE, EK, 1>, 256, 512},
             {"tr8x512", (const void*)conv_tr8_kernel<MODE, EK, 2>, 512, 512},
-            {"tr8x512k16", (const void*)conv_tr8_kernel<MODE, EK, 2, 16>, 512, 512}};
+            {"pp512u2", (const void*)conv_pp_kernel<MODE, EK, 2, 2>, 512, 512},
+            {"pp256u1", (const void*)conv_pp_kernel<MODE, EK, 1, 1>, 256, 512},
+            {"pp512m16", MODE == MODE_FWD ? (const void*)conv_pp_kernel<MODE_FWD, EK, 2, 3, true> : nullptr, 512, 512},
+            {"pp256m16", MODE == MODE_FWD ? (const void*)conv_pp_kernel<MODE_FWD, EK, 1, 3, true> : nullptr, 256, 512},
+            {"pp256u2", (const void*)conv_pp_kernel<MODE, EK, 1, 2>, 256, 512}};
   for (const V& v : vs) {
+    if (!v.fn) continue;
     P.tiles_m = (int)(s.N / v.rows);
+    if (getenv("TR_LAB_CHECK")) check(s, v.name, v.fn, v.rows, v.block, P);
     const float us = time_us(v.fn, P.tiles_m * P.tiles_n, v.block, P, 20);
     printf("lab%d %-13s EK%d %-10s %7.1f us %7.1f TF\n", VQX_GEMM_LAB, s.name, EK, v.name, us, fl / us * 1e-6);
   }
@@ -115,7 +162,7 @@ static void run_wgrad(const char* name, int64_t N, int T, int r_dim, int c_dim, 
   P.tiles_m = (r_dim + 127) / 128;
   P.tiles_n = c_dim / 64;
   const double fl = 2.0 * N * r_dim * 3.0 * c_dim;
-  const float us = time_us((const void*)wgrad_tr_kernel<EK_NONE, 1>, P.tiles_m * P.tiles_n * splits, 256, P, 20);
+  const float us = time_us((const void*)wgrad_tr_kernel<EK_NONE>, P.tiles_m * P.tiles_n * splits, 256, P, 20);
   printf("lab%d %-13s wgrad_tr s%-2d      %7.1f us %7.1f TF\n", VQX_GEMM_LAB, name, splits, us, fl / us * 1e-6);
 }
 
@@ -140,7 +187,7 @@ int main() {
   CK(hipMemcpy(x, h.data(), xb, hipMemcpyHostToDevice));
   CK(hipMemcpy(w, h.data(), wb, hipMemcpyHostToDevice));
   CK(hipMemcpy(y, h.data(), xb, hipMemcpyHostToDevice));  // wgrad's q operand
-  {
+  if (!getenv("TR_LAB_SKIP_WGRAD")) {
     void* sl;
     CK(hipMalloc(&sl, (size_t)32 * 1024 * 3 * 1024 * 2));
     run_wgrad("dec_in_wgrad", 16384, 256, 512, 1024, 8, -1, x, y, sl);

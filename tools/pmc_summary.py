@@ -19,4 +19,5 @@ for k, v in agg.items():
     print(f"{k[0]:45s} grid={k[1]:>7s} mfma_busy={v['SQ_VALU_MFMA_BUSY_CYCLES'] / (v['GRBM_GUI_ACTIVE'] / 8 * 1024):.2f} "
           f"valu/mfma={v['SQ_INSTS_VALU'] / v['SQ_INSTS_MFMA']:.2f} salu/mfma={v['SQ_INSTS_SALU'] / v['SQ_INSTS_MFMA']:.2f} "
           f"lds/mfma={v['SQ_INSTS_LDS'] / v['SQ_INSTS_MFMA']:.2f} wait_any={v['SQ_WAIT_ANY'] / wc:.2f} "
-          f"wait_inst={v['SQ_WAIT_INST_ANY'] / wc:.2f} wait_lds={v['SQ_WAIT_INST_LDS'] / wc:.2f} active={v['SQ_ACTIVE_INST_ANY'] / wc:.2f}")
+          f"wait_inst={v['SQ_WAIT_INST_ANY'] / wc:.2f} wait_lds={v['SQ_WAIT_INST_LDS'] / wc:.2f} active={v['SQ_ACTIVE_INST_ANY'] / wc:.2f} "
+          f"lds_conf={v['SQ_LDS_BANK_CONFLICT'] / max(v['SQ_LDS_IDX_ACTIVE'], 1):.3f}")

@@ -65,6 +65,23 @@ void gemm_launch_args(const void* fn, int grid, hipStream_t s, void** args, cons
 // applies, 4 = tap reuse through conv_tr_kernel only
 static int g_gemm_policy = 0;
 
+int cu_count() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  static int cached_dev = -1, cached = 0;  // one device per process in practice; re-query on a switch
+  if (dev != cached_dev) {
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 0;
+    cached_dev = dev;
+    cached = n;
+  }
+  return cached;
+}
+
+bool three_per_cu(int grid) {
+  const int cus = cu_count();
+  return g_gemm_policy == 0 && cus > 0 && grid > 2 * cus && grid <= 3 * cus;
+}
+
 bool tap_reuse_enabled() {
   static const bool env_on = [] {
     const char* e = getenv("VQX_TAP_REUSE");

@@ -9,6 +9,7 @@
 // the generic EK_ALL kernel.  WGRAD's epilogue is the slab store (EK_NONE).
 #pragma once
 #include "vqx_gemm_kernel.h"
+#include "vqx_gemm_pp.h"
 
 namespace vqx {
 
@@ -65,9 +66,13 @@ void launch_tr(const GemmParams& P, int grid, hipStream_t s) {
   if (const int segs = tr8_segs(P)) {
     GemmParams Q = P;
     Q.tiles_m = (int)(P.n_rows / (256 * segs));
+    if (segs == 2) {  // gen = 6: conv_pp_kernel (ping-pong groups), prologue slot = SEGS
+      const int infop[5] = {VQX_BF16, MODE, 2, 6, EK};
+      gemm_launch((const void*)conv_pp_kernel<MODE, EK, 2, 2>, Q.tiles_m * Q.tiles_n, s, Q, infop, flops, 512);
+      return;
+    }
     const int info8[5] = {VQX_BF16, MODE, segs, 3, EK};  // gen = 3: conv_tr8_kernel, prologue slot = SEGS
-    if (segs == 2) gemm_launch((const void*)conv_tr8_kernel<MODE, EK, 2>, Q.tiles_m * Q.tiles_n, s, Q, info8, flops, 512);
-    else gemm_launch((const void*)conv_tr8_kernel<MODE, EK, 1>, Q.tiles_m * Q.tiles_n, s, Q, info8, flops, 512);
+    gemm_launch((const void*)conv_tr8_kernel<MODE, EK, 1>, Q.tiles_m * Q.tiles_n, s, Q, info8, flops, 512);
     return;
   }
   const int bkc = P.kcin % 32 == 0 ? 32 : 16;  // 16-channel stages (4-deep ring) only for cin % 32 != 0
@@ -99,11 +104,25 @@ void dispatch_tr(const GemmParams& P, int grid, hipStream_t s) {
   }
 }
 
+// vqx_gemm.hip: compute units of the current device; true when a grid of
+// 2-per-CU conv_gemm_kernel workgroups needs more than one round but at most
+// 1.5 (automatic tile policy only)
+int cu_count();
+bool three_per_cu(int grid);
+
 template <typename T, int MODE, int PRO, bool GEN, int EK>
 void launch_one(const GemmParams& P, int grid, hipStream_t s) {
   constexpr int BK = sizeof(T) == 2 ? 64 : 32;
   const double flops = MODE == MODE_WGRAD ? 2.0 * (double)P.n_rows * P.Mc * P.Nc
                                           : 2.0 * (double)P.n_rows * P.Nc * P.K;
+  if constexpr (sizeof(T) == 2 && !GEN && MODE != MODE_WGRAD && PRO == VQX_PRO_NONE &&
+                (EK == EK_NONE || EK == EK_ELEM || EK == EK_SPLIT)) {
+    if (three_per_cu(grid)) {  // gen = 4: conv_gemm3_kernel (32-deep K-tiles, three workgroups per CU)
+      const int info3[5] = {VQX_BF16, MODE, P.pro, 4, EK};
+      gemm_launch((const void*)conv_gemm3_kernel<T, MODE, PRO, GEN, EK>, grid, s, P, info3, flops);
+      return;
+    }
+  }
   const int info[5] = {sizeof(T) == 2 ? VQX_BF16 : VQX_F32, MODE, P.pro, GEN ? 1 : 0, EK};
   gemm_launch((const void*)conv_gemm_kernel<T, MODE, PRO, GEN, BK, 2, EK>, grid, s, P, info, flops);
 }

@@ -498,8 +498,22 @@ __device__ __forceinline__ f32x4_t pro_frag(f32x4_t f, float s) {
 }
 
 
+// One 16-B-per-lane LDS-DMA (buffer_load_dwordx4 ... lds: 1 KiB per wave,
+// lane-linear at the wave-uniform LDS address `lds`).  Issued as inline asm,
+// not through __builtin_amdgcn_raw_ptr_buffer_load_lds: the compiler's
+// waitcnt pass has no alias information for ds_read_b64_tr_b16, so after a
+// builtin DMA it put `s_waitcnt vmcnt(0)` in front of the first transposed
+// LDS read of every K-step -- the next stage's DMA landed before the current
+// stage was multiplied, and DGRAD / WGRAD main loops (whose transposed
+// operands use those reads) never overlapped staging with MFMAs.  Every
+// kernel orders its DMAs explicitly (counted `s_waitcnt vmcnt` + s_barrier
+// before a stage is read; the loops drain to vmcnt(0) before the epilogue
+// reuses the staging LDS), so hiding them from the pass is safe; M0 (the
+// DMA's LDS base) is set in the same statement.
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, unsigned off) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (VQX_LDS(void)*)lds, 16, (int)off, 0, 0, 0);
+  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(VQX_LDS(void)*)lds);
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(la), "v"(off), "s"(r)
+               : "memory", "m0");
 }
 
 // vmcnt immediate from a small runtime count (0..8, 10, 12, 16; anything else waits for all)
@@ -685,6 +699,22 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
 template <typename T, int BK, int NST>
 __host__ __device__ constexpr int conv_gemm_smem() { return NST * 2 * 128 * BK * (int)sizeof(T); }
 
+// Diagnostic builds only (tools/lab/k1_stamp.cpp, -DVQX_STAMP): s_memtime at the
+// phase boundaries of conv_gemm_body, stored by thread 0 into vqx_stamp_buf.
+#ifdef VQX_STAMP
+__device__ unsigned long long* vqx_stamp_buf;
+#define VQX_STAMP_AT(i)                                                                   \
+  do {                                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    unsigned long long t_;                                                                \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    stamp_[i] = t_;                                                                       \
+  } while (0)
+#else
+#define VQX_STAMP_AT(i)
+#endif
+
 // The kernel body as a device function of (bid, nwg) = (this workgroup's
 // index, workgroup count) of its own tile grid, on the caller's LDS, so that
 // dual_*_kernel can host two GEMMs in one launch.
@@ -703,6 +733,11 @@ __device__ __forceinline__ void conv_gemm_body(const GemmParams& P, int bid, int
   static_assert(BK % (16 / ES * 2) == 0 || ES == 4, "BK");
   static_assert(conv_gemm_smem<T, BK, NST>() == NST * STAGE, "LDS");
 
+#ifdef VQX_STAMP
+  unsigned long long stamp_[5];
+  stamp_[4] = __builtin_amdgcn_s_memrealtime();
+#endif
+  VQX_STAMP_AT(0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
@@ -1039,6 +1074,7 @@ __device__ __forceinline__ void conv_gemm_body(const GemmParams& P, int bid, int
     if constexpr (kPrefetch) epi_prefetch<EK>(P, m0, n0, tid, rows);  // lands with the prologue DMA
     wait_vm(NP * (pre - 1));
     __builtin_amdgcn_s_barrier();
+    VQX_STAMP_AT(1);
     int buf = 0;
     for (int kt = 0; kt < nk; ++kt) {
       const int fbuf = (buf + NST - 1) % NST;  // buffer of tile kt+NST-1 == buffer of tile kt-1
@@ -1058,13 +1094,34 @@ __device__ __forceinline__ void conv_gemm_body(const GemmParams& P, int bid, int
     }
   }
 
+  VQX_STAMP_AT(2);
   tile_epilogue<T, MODE, EK, kPrefetch, kPreVec>(P, acc, smem, m0, n0, tn, split, gmr, (int)threadIdx.x, &rows);
+#ifdef VQX_STAMP
+  __syncthreads();
+  VQX_STAMP_AT(3);
+  const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) {
+    unsigned long long* o = vqx_stamp_buf + (size_t)bid * 8;
+    for (int i = 0; i < 5; ++i) o[i] = stamp_[i];
+    o[5] = rt1;
+  }
+#endif
 }
 
 template <typename T, int MODE, int PRO, bool GEN, int BK, int NST, int EK>
 __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
   __shared__ __attribute__((aligned(16))) char smem[conv_gemm_smem<T, BK, NST>()];
   conv_gemm_body<T, MODE, PRO, GEN, BK, NST, EK>(P, blockIdx.x, gridDim.x, smem);
+}
+
+// Three workgroups per CU (48 KiB of LDS: 32-deep K-tiles in a 3-deep ring,
+// <= 168 VGPRs) for 1x1 layers whose tile count lies between one and 1.5
+// rounds of the two-per-CU kernel (config 2: the decoder's 512 -> 640
+// res/skip conv, 640 tiles, which ran as a full round plus a quarter round).
+template <typename T, int MODE, int PRO, bool GEN, int EK>
+__global__ __launch_bounds__(256, 3) void conv_gemm3_kernel(GemmParams P) {
+  __shared__ __attribute__((aligned(16))) char smem[conv_gemm_smem<T, 32, 3>()];
+  conv_gemm_body<T, MODE, PRO, GEN, 32, 3, EK>(P, blockIdx.x, gridDim.x, smem);
 }
 
 

@@ -126,10 +126,11 @@ class LaunchProbe:
             dt, mode, pro, gen, ek = list(info)  # ek: epilogue kind (vqx_gemm_kernel.h EK_*)
             bk = 64 if dt == L.VQX_BF16 else 32
             if gen == 5:  # data + weight gradient in one launch (vqx_gemm_dual.hip)
-                sym = {1: f"vqx::dual_k1_kernel<{ek}, false>", 2: f"vqx::dual_tr_kernel<{ek}>",
-                       3: f"vqx::dual_k1_kernel<{ek}, true>", 4: f"vqx::dual_k1w_kernel<{ek}>"}.get(pro, "vqx::dual_kernel")
-            elif gen == 4:  # wide tap-reuse weight gradient (vqx_gemm_kernel.h wgrad_tr2_kernel)
-                sym = f"vqx::wgrad_tr2_kernel<{pro}>"  # pro slot = taps
+                sym = {2: f"vqx::dual_tr_kernel<{ek}>", 3: f"vqx::dual_k1_kernel<{ek}>"}.get(pro, "vqx::dual_kernel")
+            elif gen == 4:  # three workgroups per CU (vqx_gemm_kernel.h conv_gemm3_kernel)
+                sym = f"vqx::conv_gemm3_kernel<{self._DT[dt]}, {mode}, {pro}, false, {ek}>"
+            elif gen == 6:  # ping-pong tap-reuse kernel (vqx_gemm_pp.h conv_pp_kernel)
+                sym = f"vqx::conv_pp_kernel<{mode}, {ek}, {pro}, 2>"  # pro slot = frame segments
             elif gen == 2 and mode == 2:  # tap-reuse weight gradient (vqx_gemm_kernel.h wgrad_tr_kernel)
                 sym = f"vqx::wgrad_tr_kernel<{ek}, {pro}>"  # pro slot = K groups
             elif gen == 3:  # tall tap-reuse kernel (vqx_gemm_kernel.h conv_tr8_kernel)
