@@ -19,7 +19,8 @@ LIB = OUT_DIR / "libvqx.so"
 SOURCES = ["vqx_runtime.hip", "vqx_gemm.hip", "vqx_gemm_fwd.hip", "vqx_gemm_dgrad.hip", "vqx_gemm_wgrad.hip",
            "vqx_gemm_dual.hip",
            "vqx_vq.hip", "vqx_misc.hip"]
-HEADERS = ["vqx_common.h", "vqx_gemm_kernel.h", "vqx_gemm_inst.h", str(ROOT / "include" / "vqx.h")]
+HEADERS = ["vqx_common.h", "vqx_gemm_kernel.h", "vqx_gemm_inst.h", "vqx_gemm_pp.h", "vqx_gn_math.h",
+           str(ROOT / "include" / "vqx.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=fast",

@@ -3,6 +3,7 @@
 // deterministic fixed-shape trees (no float atomics), so a step is bitwise
 // reproducible apart from the EMA scatter statistics of vq_forward.
 #include "vqx_common.h"
+#include "vqx_gn_math.h"
 #include <math.h>
 
 #include <algorithm>
@@ -766,30 +767,6 @@ __device__ __forceinline__ void gn_row_load(const T* dy, int lddy, const T* u, i
   Vec4<T>::load(u + n * ldu + c, ua);
   if (glu) Vec4<T>::load(u + n * ldu + c + half, ub);
 }
-template <typename T>
-__device__ __forceinline__ void gn_row_math(const float* g, const float* ua, const float* ub, bool glu,
-                                            const float* mr4, const float* ga, const float* ba, const float* gb,
-                                            const float* bb, float* dha, float* xa, float* dhb, float* xb) {
-  constexpr int W = kGnApplyW;
-  if (!glu) {
-#pragma unroll
-    for (int i = 0; i < W; ++i) { dha[i] = g[i]; xa[i] = (ua[i] - mr4[0]) * mr4[1]; }
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < W; ++i) {
-    const float xha = (ua[i] - mr4[0]) * mr4[1];
-    const float xhb = (ub[i] - mr4[2]) * mr4[3];
-    const float ha = xha * ga[i] + ba[i];
-    const float hb = xhb * gb[i] + bb[i];
-    const float ta = ftanh<sizeof(T) == 2>(ha);
-    const float sb = fsigmoid<sizeof(T) == 2>(hb);
-    dha[i] = g[i] * sb * (1.f - ta * ta);
-    dhb[i] = g[i] * ta * (sb * (1.f - sb));
-    xa[i] = xha;
-    xb[i] = xhb;
-  }
-}
 template <typename T, bool GLU>
 __global__ __launch_bounds__(512) void gn_bwd_apply_vec_kernel(const T* __restrict__ dy, int lddy,
                                                                const T* __restrict__ u, int ldu, T* __restrict__ du,
@@ -838,10 +815,10 @@ __global__ __launch_bounds__(512) void gn_bwd_apply_vec_kernel(const T* __restri
     for (int i = 0; i < W; ++i) { a_du[s][i] = 0.f; a_dg[s][i] = 0.f; a_db[s][i] = 0.f; }
   auto row = [&](int64_t n, const float* g, const float* ua, const float* ub) {
     float dha[W], xa[W], dhb[W], xb[W], oa[W];
-    gn_row_math<T>(g, ua, ub, glu, mr4, ga, ba, gb, bb, dha, xa, dhb, xb);
+    gn_row_math<T, W>(g, ua, ub, glu, mr4, ga, ba, gb, bb, dha, xa, dhb, xb);
+    gn_dx<W>(dha, xa, ga, mr4[1], m1a, m2a, oa);
 #pragma unroll
     for (int i = 0; i < W; ++i) {
-      oa[i] = mr4[1] * (ga[i] * dha[i] - m1a - xa[i] * m2a);
       a_du[0][i] += oa[i];
       a_dg[0][i] = fmaf(dha[i], xa[i], a_dg[0][i]);
       a_db[0][i] += dha[i];
@@ -849,9 +826,9 @@ __global__ __launch_bounds__(512) void gn_bwd_apply_vec_kernel(const T* __restri
     Vec4<T>::store(du + n * lddu + c, oa);
     if (glu) {
       float ob[W];
+      gn_dx<W>(dhb, xb, gb, mr4[3], m1b, m2b, ob);
 #pragma unroll
       for (int i = 0; i < W; ++i) {
-        ob[i] = mr4[3] * (gb[i] * dhb[i] - m1b - xb[i] * m2b);
         a_du[1][i] += ob[i];
         a_dg[1][i] = fmaf(dhb[i], xb[i], a_dg[1][i]);
         a_db[1][i] += dhb[i];
