@@ -60,8 +60,11 @@ __global__ __launch_bounds__(VQ_THREADS, 4) void vq_forward_kernel(const float* 
                                                                    int64_t* __restrict__ idx_out,
                                                                    float* __restrict__ zq, void* __restrict__ zq_c,
                                                                    int zq_dt, float* __restrict__ partials) {
-  __shared__ __attribute__((aligned(16))) char smem[VQ_STEP_BYTES];
-  __shared__ float eeL[VQ_STEP];
+  // two code steps in LDS (double buffer) + their ||e||^2: one barrier per step,
+  // the next step's LDS writes issued beside this step's MFMAs.  64.5 KiB:
+  // two workgroups per CU.
+  __shared__ __attribute__((aligned(16))) char smem[2 * VQ_STEP_BYTES];
+  __shared__ float eeL[2][VQ_STEP];
   __shared__ float red[16];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -73,9 +76,10 @@ __global__ __launch_bounds__(VQ_THREADS, 4) void vq_forward_kernel(const float* 
   const int nsteps = (K + VQ_STEP - 1) / VQ_STEP;
   // Staging: thread t holds 4 consecutive 16-B chunks (64 B) of code t >> 3 of
   // the step, loaded through one buffer descriptor over E (codes >= K read as
-  // zeros, no branches).  The 8 threads of a code also form its ||e||^2
-  // (the 32 fmaf of each thread, then two quad-DPP and one half-row-mirror
-  // adds) into eeL, so the score loop needs one LDS read per code block.
+  // zeros, no branches) one step ahead of its LDS write.  The 8 threads of a
+  // code also form its ||e||^2 (the 32 fmaf of each thread, then two quad-DPP
+  // and one half-row-mirror adds) into eeL, so the score loop needs one LDS
+  // read per code block.
   static_assert(VQ_STAGE == 4 && VQ_STEP * 8 == VQ_THREADS, "staging layout");
   const __amdgpu_buffer_rsrc_t rsE =
       __builtin_amdgcn_make_buffer_rsrc((void*)E, (short)0, (int)((int64_t)K * VQ_D * 4), 0x00020000);
@@ -90,10 +94,25 @@ __global__ __launch_bounds__(VQ_THREADS, 4) void vq_forward_kernel(const float* 
       stage[j] = f32x4_t{v[0], v[1], v[2], v[3]};
     }
   };
-  auto lds_at = [&](int code, int ch) { return smem + code * 512 + 16 * (ch ^ (code & 15)); };
-  char* s_dst[VQ_STAGE];
+  auto lds_at = [&](int buf, int code, int ch) {
+    return smem + buf * VQ_STEP_BYTES + code * 512 + 16 * (ch ^ (code & 15));
+  };
+  // the staged step into buffer buf, its codes' squared norms into eeL[buf]
+  auto write_step = [&](int buf) {
+    float e2 = 0.f;
 #pragma unroll
-  for (int j = 0; j < VQ_STAGE; ++j) s_dst[j] = lds_at(s_code, 4 * s_part + j);
+    for (int j = 0; j < VQ_STAGE; ++j) {
+      *(f32x4_t*)lds_at(buf, s_code, 4 * s_part + j) = stage[j];
+      e2 = fmaf(stage[j][0], stage[j][0], e2);
+      e2 = fmaf(stage[j][1], stage[j][1], e2);
+      e2 = fmaf(stage[j][2], stage[j][2], e2);
+      e2 = fmaf(stage[j][3], stage[j][3], e2);
+    }
+    e2 += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, e2), 0xB1, 0xF, 0xF, false));
+    e2 += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, e2), 0x4E, 0xF, 0xF, false));
+    e2 += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, e2), 0x141, 0xF, 0xF, false));
+    if (s_part == 0) eeL[buf][s_code] = e2;
+  };
 
   load_step(0);  // the first codebook step and z travel together
 
@@ -130,24 +149,18 @@ __global__ __launch_bounds__(VQ_THREADS, 4) void vq_forward_kernel(const float* 
 #pragma unroll
   for (int r = 0; r < 4; ++r) { best_d[r] = INFINITY; best_i[r] = 0x7fffffff; }
 
+  write_step(0);
+  if (nsteps > 1) load_step(1);
+  __syncthreads();
   const int cbase = cs * VQ_SUB;  // this wave's codes inside a step
   for (int st = 0; st < nsteps; ++st) {
-    if (st > 0) __syncthreads();  // every wave is done with the previous step's codes
-    float e2 = 0.f;
-#pragma unroll
-    for (int j = 0; j < VQ_STAGE; ++j) {
-      *(f32x4_t*)s_dst[j] = stage[j];
-      e2 = fmaf(stage[j][0], stage[j][0], e2);
-      e2 = fmaf(stage[j][1], stage[j][1], e2);
-      e2 = fmaf(stage[j][2], stage[j][2], e2);
-      e2 = fmaf(stage[j][3], stage[j][3], e2);
+    const int cur = st & 1;
+    // step st+1 into the other buffer (its step st-1 readers passed the last
+    // barrier); step st+2's loads go out behind it
+    if (st + 1 < nsteps) {
+      write_step(cur ^ 1);
+      if (st + 2 < nsteps) load_step(st + 2);
     }
-    e2 += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, e2), 0xB1, 0xF, 0xF, false));
-    e2 += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, e2), 0x4E, 0xF, 0xF, false));
-    e2 += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, e2), 0x141, 0xF, 0xF, false));
-    if (s_part == 0) eeL[s_code] = e2;
-    __syncthreads();
-    if (st + 1 < nsteps) load_step(st + 1);  // next step's codes land during this step's MFMAs
     constexpr int NB = VQ_SUB / 16;
     // two independent accumulator chains per code block (even / odd 16-dim
     // blocks, added at the end): the 40-cycle dependent-MFMA latency hides
@@ -156,7 +169,7 @@ __global__ __launch_bounds__(VQ_THREADS, 4) void vq_forward_kernel(const float* 
     f32x4_t acc[NB], acc2[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      eb[b] = eeL[cbase + 16 * b + j16];
+      eb[b] = eeL[cur][cbase + 16 * b + j16];
       acc[b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
       acc2[b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     }
@@ -165,8 +178,8 @@ __global__ __launch_bounds__(VQ_THREADS, 4) void vq_forward_kernel(const float* 
       f32x4_t bf[NB], bg[NB];
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
-        bf[b] = *(const f32x4_t*)lds_at(cbase + 16 * b + j16, 4 * kb + q);
-        bg[b] = *(const f32x4_t*)lds_at(cbase + 16 * b + j16, 4 * kb + 4 + q);
+        bf[b] = *(const f32x4_t*)lds_at(cur, cbase + 16 * b + j16, 4 * kb + q);
+        bg[b] = *(const f32x4_t*)lds_at(cur, cbase + 16 * b + j16, 4 * kb + 4 + q);
       }
 #pragma unroll
       for (int m = 0; m < 4; ++m)
@@ -190,6 +203,7 @@ __global__ __launch_bounds__(VQ_THREADS, 4) void vq_forward_kernel(const float* 
         }
       }
     }
+    __syncthreads();  // step st+1 is in LDS; step st's buffer may be rewritten
   }
 
   // argmin across the 16 code lanes of each row (lowest index on ties)
@@ -204,7 +218,7 @@ __global__ __launch_bounds__(VQ_THREADS, 4) void vq_forward_kernel(const float* 
   }
   // ... and across the code splits: (distance, index) minima through LDS, merged
   // in ascending split order with the same comparison = torch.argmin's first minimum
-  __syncthreads();  // the last step's codes are no longer read
+  // (the loop's last barrier: no wave reads codes any more)
   float* md = (float*)smem;                       // [VQ_FG][VQ_CS][16]
   int* mi = (int*)(smem + VQ_FG * VQ_CS * 16 * 4);
   if (j16 == 0) {
