@@ -1,12 +1,18 @@
 #!/bin/bash
-# Same-box A/B of one environment switch on the bf16 bench step:
-#   bash tools/gpu_ab_env.sh NAME VAR VALUE_A VALUE_B   (alternating A B A B, 20 steps each)
+# A/B of environment knobs on the bench line, interleaved over two passes so
+# clock drift cancels: tools/gpu_ab_env.sh TAG "K1=a K2=b" "K1=c" ...
+# (the empty setting -- the defaults -- always runs first in each pass).
 set -o pipefail
-cd "$(dirname "$0")/.."
-NAME=$1; VAR=$2; A=$3; B=$4
-mkdir -p gpurun_out/ab_$NAME
-for v in $A $B $A $B; do
-  env $VAR=$v timeout -k 10 200 python -u bench.py --steps 30 --warmup 5 --no-cpu-baseline --fp32-steps 0 \
-    --vq-reps 0 --no-probe > gpurun_out/ab_$NAME/b_$v.json 2> gpurun_out/ab_$NAME/b_$v.err || exit $?
-  python3 -c "import json;d=json.load(open('gpurun_out/ab_$NAME/b_$v.json'));print('$VAR=$v', d['ms_per_step'], d['value'])"
-done | tee gpurun_out/ab_$NAME/summary.txt
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+TAG=${1:-ab}; shift
+O=gpurun_out/$TAG; mkdir -p $O
+for pass in 0 1; do
+  i=0
+  for e in "" "$@"; do
+    env $e timeout -k 10 300 python bench.py --no-cpu-baseline --fp32-steps 0 --vq-reps 0 --steps 40 \
+      > $O/ab${pass}_$i.json 2> $O/ab${pass}_$i.err || exit $?
+    echo "pass $pass [$e] $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(round(d['value']), d['ms_per_step'])" $O/ab${pass}_$i.json)"
+    i=$((i+1))
+  done
+done

@@ -23,7 +23,7 @@ HEADERS = ["vqx_common.h", "vqx_gemm_kernel.h", "vqx_gemm_inst.h", "vqx_gemm_pp.
            str(ROOT / "include" / "vqx.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
-FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=fast",
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=fast-honor-pragmas",
          "-Wno-unused-result", "-I", str(ROOT / "include")]
 
 

@@ -1,8 +1,9 @@
-// GroupNorm(/GLU)-backward element math shared by the standalone apply kernel
-// (vqx_misc.hip gn_bwd_apply_vec_kernel) and the apply phase fused into the
-// 1x1 DGRAD launch (vqx_gemm_dual.hip dual_k1g_kernel): one definition, so
-// both produce the same dx bit for bit.  Reference: autograd of layers.py
-// 236-242 (tanh * sigmoid of the GroupNorm halves) and 170-176 (GroupNorm).
+// GroupNorm(/GLU)-backward element math of the apply kernel (vqx_misc.hip
+// gn_bwd_apply_vec_kernel), kept in one header so any other kernel applying it
+// (the measured-and-rejected fused 1x1 DGRAD apply, tools/lab/
+// dual_k1g_apply.patch) produces the same dx bit for bit.  Reference: autograd
+// of layers.py 236-242 (tanh * sigmoid of the GroupNorm halves) and 170-176
+// (GroupNorm).
 #pragma once
 #include "vqx_common.h"
 

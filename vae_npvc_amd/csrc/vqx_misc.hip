@@ -1576,13 +1576,16 @@ __global__ __launch_bounds__(256) void radam_kernel(float* __restrict__ p, const
   }
 }
 
-// One Adam element update, torch's op order (bit-identical to torch.optim.Adam
-// on the same fp32 inputs)
+// One Adam element update in torch's op order (torch.optim.Adam single-tensor,
+// trainer/basic.py:63-75).  Plain operators under contract(off): every product
+// and sum is rounded on its own, so the 16-B path and the scalar path agree bit
+// for bit.  The pragma holds because the library is built with
+// -ffp-contract=fast-honor-pragmas (plain "fast" lets the backend fuse across
+// it: the packed path then carried v_pk_fma_f32 and differed by an ulp).
+// Against torch's CPU Adam the bound is 1e-6 relative (its vectorised
+// lerp/addcmul may fuse).
 __device__ __forceinline__ void adam_elem(float& pi, float gi, float& mi, float& vi, float w, float b2, float omb2,
                                           float bc2s, float eps, float step_size) {
-  // plain operators under contract(off): every product and sum is rounded on
-  // its own (the __f*_rn helpers are inlined bodies that -ffp-contract=fast
-  // may still fuse into FMAs)
 #pragma clang fp contract(off)
   // torch.lerp: weight < 0.5 ? m + w*(g-m) : g - (g-m)*(1-w)
   mi = (w < 0.5f) ? mi + w * (gi - mi) : gi - (gi - mi) * (1.f - w);
