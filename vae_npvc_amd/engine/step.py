@@ -465,8 +465,15 @@ class VQVAEEngine:
         # res/skip at 24, enc skip at 32 -- exactly floor(512 / tiles).  The
         # tile count comes from the library (3-tap layers use the tap-reuse
         # kernel's 128 x 192 tiles).  Frame counts follow each stage's rate.
-        wg_target = int(os.environ.get("VQX_WGRAD_WGS", "512"))  # A/B knobs: workgroups per wgrad launch
-        wg_1x1 = int(os.environ.get("VQX_WGRAD_WGS_1X1", str(wg_target)))  # ... for the 1x1 layers
+        # Round 3 (profiles/r03/wgs_ab.txt): with the 3-tap WGRAD inside the fused
+        # DGRAD+WGRAD launch (512 DGRAD workgroups of its own), 256 split-K
+        # workgroups for the 3-tap layers (dec conv_in 4 splits, enc k3 8) beat
+        # 512: 5.43 vs 5.53 ms per step; 1x1 layers stay at 512, and so do the
+        # stage convolutions, whose WGRAD runs alone (no DGRAD beside it).
+        wg_target = int(os.environ.get("VQX_WGRAD_WGS", "256"))  # A/B knobs: workgroups per wgrad launch
+        wg_1x1 = int(os.environ.get("VQX_WGRAD_WGS_1X1", "512"))  # ... for the 1x1 layers
+        wg_solo = int(os.environ.get("VQX_WGRAD_WGS_SOLO", "512"))  # ... for the stage convs (WGRAD alone)
+        solo = {id(st.conv) for st in self.enc_stages} | {id(st.conv) for st in self.dec_stages}
         B_ref, T_ref = 64, 256
         rate = {}
         Tc = T_ref
@@ -498,7 +505,8 @@ class VQVAEEngine:
                 r, c = (Lr.cin, Lr.cout) if Lr.kind == KIND_CONVT else (Lr.cout, Lr.cin)
                 n, T_, k, pad, dil = B_ref * To, To, Lr.k, Lr.pad, Lr.dil
             tiles = ops.wgrad_tiles(n, T_, r, c, k, pad, self.dt, dil=dil)
-            Lr.splits = max(1, min((wg_1x1 if Lr.k == 1 else wg_target) // tiles, n // 256))
+            wgs = wg_solo if id(Lr) in solo else wg_1x1 if Lr.k == 1 else wg_target
+            Lr.splits = max(1, min(wgs // tiles, n // 256))
         # slab arena: one backward group's slabs at a time (kept L2/MALL-resident).
         # bf16 runs keep the conv slabs in bf16 (each split's fp32 partial rounded
         # once, summed in fp32 by the weight-norm backward): half the bytes of the
