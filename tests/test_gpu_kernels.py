@@ -462,6 +462,38 @@ def test_linear_batched_and_colreduce():
     assert L.WN_COLREDUCE == 2
 
 
+@pytest.mark.parametrize("B", [64, 13])
+def test_linear_cond_fast_path_equals_tiled_kernels(B):
+    """The one-pass conditioning kernels (I = 128, B <= 64, 16-B aligned c;
+    vqx_misc.hip linear_cond_*) against the 64x64-tiled kernels the same call
+    takes for an unaligned c: the same summation orders, so bit for bit (the
+    config-2 shape: 10 layers, O = 1024; B = 13 leaves rows of the tiles empty)."""
+    ops = _ops()
+    torch.manual_seed(16)
+    n, I, O = 10, 128, 1024
+    c0 = torch.randn(B, I, device=DEV)
+    runs = []
+    for off in (0, 1):  # off = 1: c not 16-B aligned -> tiled kernels
+        base = torch.zeros(B * I + 4, device=DEV)
+        c = base[off:off + B * I].view(B, I)
+        c.copy_(c0)
+        g = torch.Generator(device="cpu").manual_seed(3)
+        lay = [dict(W=(torch.randn(O, I, generator=g) / I ** 0.5).to(DEV), bias=torch.randn(O, generator=g).to(DEV),
+                    out=torch.empty(B, O, device=DEV), dout=torch.randn(B, O, generator=g).to(DEV),
+                    dW=torch.empty(O, I, device=DEV), dbias=torch.empty(O, device=DEV)) for _ in range(n)]
+        tab = ops.linear_table(lay)
+        dc = torch.empty(B, I, device=DEV)
+        ops.linear_batched_fwd(tab, c, B, I, O)
+        ops.linear_batched_bwd(tab, c, B, I, O, dc)
+        torch.cuda.synchronize()
+        runs.append((lay, dc))
+    (la, dca), (lb, dcb) = runs
+    for a, b in zip(la, lb):
+        for k in ("out", "dW", "dbias"):
+            assert torch.equal(a[k], b[k]), k
+    assert torch.equal(dca, dcb)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("G,cout", [(1, 512), (2, 1024)])
 def test_gnstats_epilogue_matches_standalone(dtype, G, cout, tile):

@@ -1319,15 +1319,30 @@ __global__ __launch_bounds__(256) void linear_batched_bwd_w_kernel(const vqx_lin
 __global__ __launch_bounds__(256) void linear_batched_bwd_x_kernel(const vqx_linear_layer* __restrict__ L, int B,
                                                                    int I, int O, float* __restrict__ part) {
   const vqx_linear_layer& l = L[blockIdx.y];
+  const float* __restrict__ dout = l.dout;
+  const float* __restrict__ W = l.W;
   const int nI = (I + kLT - 1) / kLT;
   const int o0 = blockIdx.x * kLT, b0 = (blockIdx.z / nI) * kLT, i0 = (blockIdx.z % nI) * kLT;
   __shared__ float ds[kLT][kLT + 1];   // [b][o]
   __shared__ __attribute__((aligned(16))) float ws[kLT][kLT + 4];  // [o][i]
   const int t = threadIdx.x, tb = t >> 2, ti = (t & 3) * 16;
-  for (int e = t; e < kLT * kLT; e += 256) {
-    const int r = e >> 6, q = e & 63;
-    ds[r][q] = (b0 + r < B && o0 + q < O) ? l.dout[(int64_t)(b0 + r) * O + o0 + q] : 0.f;
-    ws[r][q] = (o0 + r < O && i0 + q < I) ? l.W[(int64_t)(o0 + r) * I + i0 + q] : 0.f;
+  // every operand load of the thread issued before the first is used (indices
+  // clamped in range, the out-of-range elements zeroed at the LDS write): a
+  // predicated load per element serialised them, one memory latency each
+  constexpr int NE = kLT * kLT / 256;
+  float dv[NE], wv[NE];
+#pragma unroll
+  for (int u = 0; u < NE; ++u) {
+    const int e = t + 256 * u, r = e >> 6, q = e & 63;
+    const int br = min(b0 + r, B - 1), oq = min(o0 + q, O - 1), orr = min(o0 + r, O - 1), iq = min(i0 + q, I - 1);
+    dv[u] = dout[(int64_t)br * O + oq];
+    wv[u] = W[(int64_t)orr * I + iq];
+  }
+#pragma unroll
+  for (int u = 0; u < NE; ++u) {
+    const int e = t + 256 * u, r = e >> 6, q = e & 63;
+    ds[r][q] = (b0 + r < B && o0 + q < O) ? dv[u] : 0.f;
+    ws[r][q] = (o0 + r < O && i0 + q < I) ? wv[u] : 0.f;
   }
   __syncthreads();
   float acc[16];
@@ -1368,23 +1383,44 @@ constexpr int kCondI = 128, kCondB = 64, kCondO = 32;
 __global__ __launch_bounds__(256) void linear_cond_fwd_kernel(const vqx_linear_layer* __restrict__ L,
                                                               const float* __restrict__ c, int B, int O) {
   const vqx_linear_layer& l = L[blockIdx.y];
+  const float* __restrict__ W = l.W;
+  const float* __restrict__ bias = l.bias;
+  float* __restrict__ out = l.out;
   const int o0 = blockIdx.x * kCondO;
   __shared__ __attribute__((aligned(16))) float cs[kCondB][kCondI + 4];  // [b][i]
   __shared__ __attribute__((aligned(16))) float wt[kCondI][kCondO + 4];  // [i][o]
   const int t = threadIdx.x;
-  for (int e = t; e < kCondB * kCondI / 4; e += 256) {
-    const int b = e / (kCondI / 4), i4 = e % (kCondI / 4);
-    const f32x4_t z = {0.f, 0.f, 0.f, 0.f};
-    *(f32x4_t*)&cs[b][4 * i4] = b < B ? *(const f32x4_t*)(c + (int64_t)b * kCondI + 4 * i4) : z;
-  }
-  for (int e = t; e < kCondO * kCondI / 4; e += 256) {
-    const int r = e / (kCondI / 4), i4 = e % (kCondI / 4);
-    const f32x4_t w = *(const f32x4_t*)(l.W + (int64_t)(o0 + r) * kCondI + 4 * i4);
+  const int b = t >> 2, oq = (t & 3) * 8;
+  // all operand loads in flight at once (rows b >= B read row B-1 and are
+  // zeroed at the LDS write), the bias with them
+  constexpr int NC = kCondB * kCondI / 4 / 256, NW = kCondO * kCondI / 4 / 256;
+  f32x4_t cv[NC], wv[NW];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) wt[4 * i4 + k][r] = w[k];
+  for (int u = 0; u < NC; ++u) {
+    const int e = t + 256 * u, r = e / (kCondI / 4), i4 = e % (kCondI / 4);
+    cv[u] = *(const f32x4_t*)(c + (int64_t)min(r, B - 1) * kCondI + 4 * i4);
+  }
+#pragma unroll
+  for (int u = 0; u < NW; ++u) {
+    const int e = t + 256 * u, r = e / (kCondI / 4), i4 = e % (kCondI / 4);
+    wv[u] = *(const f32x4_t*)(W + (int64_t)(o0 + r) * kCondI + 4 * i4);
+  }
+  float bj[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bj[j] = bias ? bias[o0 + oq + j] : 0.f;
+#pragma unroll
+  for (int u = 0; u < NC; ++u) {
+    const int e = t + 256 * u, r = e / (kCondI / 4), i4 = e % (kCondI / 4);
+    const f32x4_t z = {0.f, 0.f, 0.f, 0.f};
+    *(f32x4_t*)&cs[r][4 * i4] = r < B ? cv[u] : z;
+  }
+#pragma unroll
+  for (int u = 0; u < NW; ++u) {
+    const int e = t + 256 * u, r = e / (kCondI / 4), i4 = e % (kCondI / 4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) wt[4 * i4 + k][r] = wv[u][k];
   }
   __syncthreads();
-  const int b = t >> 2, oq = (t & 3) * 8;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll 8
   for (int i = 0; i < kCondI; ++i) {
@@ -1398,28 +1434,43 @@ __global__ __launch_bounds__(256) void linear_cond_fwd_kernel(const vqx_linear_l
   }
   if (b >= B) return;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int o = o0 + oq + j;
-    l.out[(int64_t)b * O + o] = acc[j] + (l.bias ? l.bias[o] : 0.f);
-  }
+  for (int j = 0; j < 8; ++j) out[(int64_t)b * O + o0 + oq + j] = acc[j] + bj[j];
 }
 
 // dW_l[o][i] = sum_b dout_l[b][o] c[b][i], dbias_l[o] = sum_b dout_l[b][o]; grid (O/32, n)
 __global__ __launch_bounds__(256) void linear_cond_bwd_w_kernel(const vqx_linear_layer* __restrict__ L,
                                                                 const float* __restrict__ c, int B, int O) {
   const vqx_linear_layer& l = L[blockIdx.y];
+  const float* __restrict__ dout = l.dout;
   const int o0 = blockIdx.x * kCondO;
   __shared__ __attribute__((aligned(16))) float cs[kCondB][kCondI + 4];  // [b][i]
   __shared__ float ds[kCondB][kCondO + 1];                               // [b][o]
   const int t = threadIdx.x;
-  for (int e = t; e < kCondB * kCondI / 4; e += 256) {
-    const int b = e / (kCondI / 4), i4 = e % (kCondI / 4);
-    const f32x4_t z = {0.f, 0.f, 0.f, 0.f};
-    *(f32x4_t*)&cs[b][4 * i4] = b < B ? *(const f32x4_t*)(c + (int64_t)b * kCondI + 4 * i4) : z;
+  // all operand loads in flight at once (rows b >= B read row B-1 and are
+  // zeroed at the LDS write)
+  constexpr int NC = kCondB * kCondI / 4 / 256, ND = kCondB * kCondO / 256;
+  f32x4_t cv[NC];
+  float dv[ND];
+#pragma unroll
+  for (int u = 0; u < NC; ++u) {
+    const int e = t + 256 * u, r = e / (kCondI / 4), i4 = e % (kCondI / 4);
+    cv[u] = *(const f32x4_t*)(c + (int64_t)min(r, B - 1) * kCondI + 4 * i4);
   }
-  for (int e = t; e < kCondB * kCondO; e += 256) {
-    const int b = e / kCondO, q = e % kCondO;
-    ds[b][q] = b < B ? l.dout[(int64_t)b * O + o0 + q] : 0.f;
+#pragma unroll
+  for (int u = 0; u < ND; ++u) {
+    const int e = t + 256 * u, r = e / kCondO, q = e % kCondO;
+    dv[u] = dout[(int64_t)min(r, B - 1) * O + o0 + q];
+  }
+#pragma unroll
+  for (int u = 0; u < NC; ++u) {
+    const int e = t + 256 * u, r = e / (kCondI / 4), i4 = e % (kCondI / 4);
+    const f32x4_t z = {0.f, 0.f, 0.f, 0.f};
+    *(f32x4_t*)&cs[r][4 * i4] = r < B ? cv[u] : z;
+  }
+#pragma unroll
+  for (int u = 0; u < ND; ++u) {
+    const int e = t + 256 * u, r = e / kCondO, q = e % kCondO;
+    ds[r][q] = r < B ? dv[u] : 0.f;
   }
   __syncthreads();
   const int ol = t >> 3, ic = (t & 7) * 16;
