@@ -243,28 +243,34 @@ __global__ __launch_bounds__(VQ_THREADS, 4) void vq_forward_kernel(const float* 
     const int my_idx = (bi >= K || bi < 0) ? 0 : bi;
     if (row_ok) {
       if (q == 0) idx_out[my_row] = my_idx;
+      // the code row's 8 loads all in flight before the first store (a
+      // load-store pair per 16 dims paid one memory latency each)
+      f32x4_t ev[8];
 #pragma unroll
-      for (int kb = 0; kb < 8; ++kb) {
-        const int d0 = 16 * kb + 4 * q;
-        const f32x4_t e = *(const f32x4_t*)(E + (int64_t)my_idx * VQ_D + d0);
-        if (zq) *(f32x4_t*)(zq + my_row * VQ_D + d0) = e;
-        if (zq_c) {
-          if (zq_dt == VQX_BF16) {
-            bf16_t* o = (bf16_t*)zq_c + my_row * VQ_D + d0;
-            uint2 pk;
-            pk.x = pack_bf16x2(e[0], e[1]);
-            pk.y = pack_bf16x2(e[2], e[3]);
-            *(uint2*)o = pk;
-          } else {
-            *(f32x4_t*)((float*)zq_c + my_row * VQ_D + d0) = e;
-          }
+      for (int kb = 0; kb < 8; ++kb) ev[kb] = *(const f32x4_t*)(E + (int64_t)my_idx * VQ_D + 16 * kb + 4 * q);
+      if (zq) {
+#pragma unroll
+        for (int kb = 0; kb < 8; ++kb) *(f32x4_t*)(zq + my_row * VQ_D + 16 * kb + 4 * q) = ev[kb];
+      }
+      if (zq_c && zq_dt == VQX_BF16) {
+#pragma unroll
+        for (int kb = 0; kb < 8; ++kb) {
+          uint2 pk;
+          pk.x = pack_bf16x2(ev[kb][0], ev[kb][1]);
+          pk.y = pack_bf16x2(ev[kb][2], ev[kb][3]);
+          *(uint2*)((bf16_t*)zq_c + my_row * VQ_D + 16 * kb + 4 * q) = pk;
         }
+      } else if (zq_c) {
+#pragma unroll
+        for (int kb = 0; kb < 8; ++kb) *(f32x4_t*)((float*)zq_c + my_row * VQ_D + 16 * kb + 4 * q) = ev[kb];
+      }
+#pragma unroll
+      for (int kb = 0; kb < 8; ++kb)
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
-          const float df = __fsub_rn(e[m], zf[kb][m]);
+          const float df = __fsub_rn(ev[kb][m], zf[kb][m]);
           sq = fmaf(df, df, sq);
         }
-      }
     }
   }
   const float tot = block_sum(sq, red);
@@ -304,10 +310,20 @@ __global__ __launch_bounds__(256) void vq_stats_kernel(const float* __restrict__
   for (int i = tid; i < K * DSL; i += 256) acc[i] = 0.f;
   if (counts)
     for (int i = tid; i < K; i += 256) cnt[i] = 0;
-  for (int i = tid; i < VQ_CHUNK; i += 256) {
-    int code = i < nf ? (int)idx[n0 + i] : K;
-    if (code < 0 || code > K) code = K;  // out-of-range codes sort last and are dropped
-    keys[i] = code < K ? (code << 9) | i : 0x7fffffff;
+  {
+    // both index loads in flight at once (clamped to the chunk's last frame,
+    // the frames past it marked invalid after the load)
+    static_assert(VQ_CHUNK == 2 * 256, "two keys per thread");
+    int64_t iv[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) iv[u] = idx[n0 + min(tid + 256 * u, nf - 1)];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = tid + 256 * u;
+      int code = i < nf ? (int)iv[u] : K;
+      if (code < 0 || code > K) code = K;  // out-of-range codes sort last and are dropped
+      keys[i] = code < K ? (code << 9) | i : 0x7fffffff;
+    }
   }
   __syncthreads();
   if (counts)
@@ -331,12 +347,17 @@ __global__ __launch_bounds__(256) void vq_stats_kernel(const float* __restrict__
   const int p0 = r * LEN;
   f32x4_t rows[LEN];
   int rc[LEN];
+  // every row load of the thread in flight at once (invalid keys read frame 0
+  // of the chunk and are zeroed after the load)
 #pragma unroll
   for (int u = 0; u < LEN; ++u) {
     const int key = keys[p0 + u];
     rc[u] = key == 0x7fffffff ? -1 : key >> 9;
-    rows[u] = rc[u] < 0 ? f32x4_t{0.f, 0.f, 0.f, 0.f} : *(const f32x4_t*)(z + (n0 + (key & 511)) * VQ_D + dd);
+    rows[u] = *(const f32x4_t*)(z + (n0 + (rc[u] < 0 ? 0 : (key & 511))) * VQ_D + dd);
   }
+#pragma unroll
+  for (int u = 0; u < LEN; ++u)
+    if (rc[u] < 0) rows[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   f32x4_t run = rows[0];
   int cur = rc[0];
   bool head = true;
