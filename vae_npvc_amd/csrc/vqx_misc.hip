@@ -27,10 +27,17 @@ __global__ __launch_bounds__(256) void wn_norm_kernel(const vqx_wn_layer* __rest
   const int cols = l.cout * l.k;
   const float* v = l.v + (int64_t)o * cols;
   float s = 0.f;
-  if ((cols & 3) == 0 && (((uintptr_t)v) & 15) == 0) {
-    for (int i = lane * 4; i < cols; i += 256) {
-      const f32x4_t x = *(const f32x4_t*)(v + i);
-      s = fmaf(x[0], x[0], fmaf(x[1], x[1], fmaf(x[2], x[2], fmaf(x[3], x[3], s))));
+  if ((cols & 3) == 0 && (((uintptr_t)v) & 15) == 0 && cols <= 4096) {
+    // the lane's 16-B loads all in flight before the first add (a runtime
+    // loop of load + add paid one memory latency per iteration)
+    f32x4_t xv[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      xv[u] = 256 * u < cols ? *(const f32x4_t*)(v + min(lane * 4 + 256 * u, cols - 4)) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const f32x4_t x = xv[u];
+      if (lane * 4 + 256 * u < cols) s = fmaf(x[0], x[0], fmaf(x[1], x[1], fmaf(x[2], x[2], fmaf(x[3], x[3], s))));
     }
   } else {
     for (int i = lane; i < cols; i += 64) s = fmaf(v[i], v[i], s);
@@ -150,10 +157,19 @@ __global__ __launch_bounds__(256) void wn_pack_kernel(const vqx_wn_layer* __rest
     const int cols = cin * K;
     const float* v = l.v + (int64_t)co * cols;
     float s = 0.f;
-    for (int i = threadIdx.x; i < cols; i += 256) {
-      const float x = v[i];
-      buf[i] = x;
-      s = fmaf(x, x, s);
+    // the row's loads all in flight before the first use (a load + use per
+    // iteration of a runtime-bound loop paid one memory latency each)
+    float xr[kWnRow / 256];
+#pragma unroll
+    for (int u = 0; u < kWnRow / 256; ++u)
+      xr[u] = 256 * u < cols ? v[min((int)threadIdx.x + 256 * u, cols - 1)] : 0.f;
+#pragma unroll
+    for (int u = 0; u < kWnRow / 256; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      if (i < cols) {
+        buf[i] = xr[u];
+        s = fmaf(xr[u], xr[u], s);
+      }
     }
     s = block_sum(s, red);  // includes the barriers that publish buf
     float sc = 1.f;
@@ -184,18 +200,35 @@ __global__ __launch_bounds__(256) void wn_pack_kernel(const vqx_wn_layer* __rest
   if (ci0 >= cin || K > 64) return;
   const int wseg = TCO * K;  // floats per ci row segment (contiguous in v)
   const bool full = ci0 + 64 <= cin && co0 + TCO <= cout;
-  if (full && (wseg & 3) == 0 && ((cout * K) & 3) == 0 && (((uintptr_t)l.v) & 15) == 0) {
+  constexpr int kTileV4 = 6;  // 16-B loads per thread of a full tile: 64 x wseg floats, wseg <= 96
+  if (full && (wseg & 3) == 0 && ((cout * K) & 3) == 0 && (((uintptr_t)l.v) & 15) == 0 && 64 * wseg <= kTileV4 * 1024) {
     const int w4 = wseg >> 2;
-    for (int e = threadIdx.x; e < 64 * w4; e += 256) {
-      const int r = e / w4, q = (e - r * w4) * 4;
-      const int ci = ci0 + r;
-      f32x4_t x = *(const f32x4_t*)(l.v + ((int64_t)ci * cout + co0) * K + q);
-      if (l.g) {
-        const float sc = l.g[ci] / l.norm[ci];
-        x = f32x4_t{x[0] * sc, x[1] * sc, x[2] * sc, x[3] * sc};
-      }
+    // all of the thread's loads (row segments, gains, norms) in flight at once
+    f32x4_t xv[kTileV4];
+    float gs[kTileV4], ns[kTileV4];
+    const float* __restrict__ gp = l.g;
+    const float* __restrict__ np = l.norm;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) buf[(q + u) * 65 + r] = x[u];
+    for (int u = 0; u < kTileV4; ++u) {
+      const int e = min((int)threadIdx.x + 256 * u, 64 * w4 - 1), r = e / w4, q = (e - r * w4) * 4;
+      const int ci = ci0 + r;
+      xv[u] = 256 * u < 64 * w4 ? *(const f32x4_t*)(l.v + ((int64_t)ci * cout + co0) * K + q) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+      gs[u] = gp && 256 * u < 64 * w4 ? gp[ci] : 1.f;
+      ns[u] = gp && 256 * u < 64 * w4 ? np[ci] : 1.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kTileV4; ++u) {
+      const int e = threadIdx.x + 256 * u;
+      if (e < 64 * w4) {
+        const int r = e / w4, q = (e - r * w4) * 4;
+        f32x4_t x = xv[u];
+        if (gp) {
+          const float sc = gs[u] / ns[u];
+          x = f32x4_t{x[0] * sc, x[1] * sc, x[2] * sc, x[3] * sc};
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) buf[(q + k) * 65 + r] = x[k];
+      }
     }
   } else {
     for (int e = threadIdx.x; e < 64 * wseg; e += 256) {
