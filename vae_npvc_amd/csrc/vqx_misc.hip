@@ -825,11 +825,29 @@ __global__ __launch_bounds__(512) void gn_bwd_apply_vec_kernel(const T* __restri
     const int cg = C / G;
     const float M = (float)T_ * (float)cg;
     float S1a = 0.f, S2a = 0.f, S1b = 0.f, S2b = 0.f;
-    for (int q = 0; q < nparts; ++q) {
-      const float* o = part + ((int64_t)b * nparts + q) * pstride;
-      S1a += o[0];
-      S2a += o[1];
-      if (glu) { S1b += o[2]; S2b += o[3]; }
+    // the utterance's partials staged through LDS by one load per thread, then
+    // summed by every thread in part order (a runtime loop of loads + adds
+    // paid one memory latency per part)
+    constexpr int kMaxP = 64;
+    __shared__ float sp[kMaxP][4];
+    if (nparts <= kMaxP) {
+      if ((int)threadIdx.x < 4 * nparts) {
+        const int q = threadIdx.x >> 2, k = threadIdx.x & 3;
+        sp[q][k] = (k < 2 || glu) ? part[((int64_t)b * nparts + q) * pstride + k] : 0.f;
+      }
+      __syncthreads();
+      for (int q = 0; q < nparts; ++q) {
+        S1a += sp[q][0];
+        S2a += sp[q][1];
+        if (glu) { S1b += sp[q][2]; S2b += sp[q][3]; }
+      }
+    } else {
+      for (int q = 0; q < nparts; ++q) {
+        const float* o = part + ((int64_t)b * nparts + q) * pstride;
+        S1a += o[0];
+        S2a += o[1];
+        if (glu) { S1b += o[2]; S2b += o[3]; }
+      }
     }
     m1a = S1a / M; m2a = S2a / M; m1b = S1b / M; m2b = S2b / M;
   }
@@ -931,12 +949,30 @@ __global__ __launch_bounds__(256) void gn_glu_fwd_vec_kernel(const T* __restrict
     // one) merged from the producing GEMM's GNSTATS tiles, as
     // gn_finalize_tiles_kernel does; the utterance's first block stores them
     const int b0 = blockIdx.x * fpb / T_, rg = T_ / 128, ntn = 2 * half / 128, tpg = ntn / 2;
+    // the utterance's tiles staged through LDS by one thread each (a serial
+    // merge loop over global loads paid one memory latency per tile), then
+    // merged by threads 0 / 1 in the same order
+    constexpr int kMaxTl = 64;
+    __shared__ float tl[2 * kMaxTl][3];
+    const int nt = rg * tpg;
+    const bool staged = nt <= kMaxTl;
+    if (staged) {
+      if ((int)threadIdx.x < 2 * nt) {
+        const int gi = threadIdx.x / nt, k = threadIdx.x - gi * nt, r = k / tpg, t = k - r * tpg;
+        const float* o = tiles + ((int64_t)(b0 * rg + r) * ntn + gi * tpg + t) * 4;
+        tl[threadIdx.x][0] = o[0];
+        tl[threadIdx.x][1] = o[1];
+        tl[threadIdx.x][2] = o[2];
+      }
+      __syncthreads();
+    }
     if (threadIdx.x < 2) {
       const int gi = threadIdx.x;
       double n = 0.0, mean = 0.0, m2 = 0.0;
       for (int r = 0; r < rg; ++r)
         for (int t = 0; t < tpg; ++t) {
-          const float* o = tiles + ((int64_t)(b0 * rg + r) * ntn + gi * tpg + t) * 4;
+          const float* o = staged ? tl[gi * nt + r * tpg + t]
+                                  : tiles + ((int64_t)(b0 * rg + r) * ntn + gi * tpg + t) * 4;
           const double nb = o[0];
           if (nb == 0.0) continue;
           const double d = (double)o[1] - mean;
