@@ -459,8 +459,10 @@ class VQVAEEngine:
             self.convs += [b.conv_in, b.cond, b.rs]
         self.convs += [self.fin1, self.fin2]
         # split-K factors for the wgrad GEMMs: one full round of ~480-512
-        # workgroups (2 per CU) at config 2 (64 x 256 frames), at least 4
-        # K-tiles (256 frames) per split.  Measured sweep (tools/gemm_bench.py
+        # workgroups (2 per CU) at config 2 (64 x 256 frames), at least 512
+        # frames per split (round 3: the few-tile layers -- encoder output,
+        # final convs, stage convs -- at 32 instead of 64 splits, -0.4% per
+        # step; profiles/r03/wgs_ab.txt).  Measured sweep (tools/gemm_bench.py
         # --sweep-splits) on 128 x 128 tiles: dec_in best at 5, enc k3 at 10,
         # res/skip at 24, enc skip at 32 -- exactly floor(512 / tiles).  The
         # tile count comes from the library (3-tap layers use the tap-reuse
@@ -474,6 +476,7 @@ class VQVAEEngine:
         wg_1x1 = int(os.environ.get("VQX_WGRAD_WGS_1X1", "512"))  # ... for the 1x1 layers
         wg_solo = int(os.environ.get("VQX_WGRAD_WGS_SOLO", "512"))  # ... for the stage convs (WGRAD alone)
         solo = {id(st.conv) for st in self.enc_stages} | {id(st.conv) for st in self.dec_stages}
+        min_k = int(os.environ.get("VQX_WGRAD_MIN_K", "512"))  # frames per split at least (256: +0.4%, 1024: +1.9%)
         B_ref, T_ref = 64, 256
         rate = {}
         Tc = T_ref
@@ -506,7 +509,7 @@ class VQVAEEngine:
                 n, T_, k, pad, dil = B_ref * To, To, Lr.k, Lr.pad, Lr.dil
             tiles = ops.wgrad_tiles(n, T_, r, c, k, pad, self.dt, dil=dil)
             wgs = wg_solo if id(Lr) in solo else wg_1x1 if Lr.k == 1 else wg_target
-            Lr.splits = max(1, min(wgs // tiles, n // 256))
+            Lr.splits = max(1, min(wgs // tiles, n // min_k))
         # slab arena: one backward group's slabs at a time (kept L2/MALL-resident).
         # bf16 runs keep the conv slabs in bf16 (each split's fp32 partial rounded
         # once, summed in fp32 by the weight-norm backward): half the bytes of the
