@@ -54,6 +54,9 @@ def parse():
                     "(default: the dominant kernel's launches in every --probe-every-th timed step; "
                     "VQX_BENCH_KERNELS=1/2: every GEMM launch of those steps, per kernel / per layer)")
     ap.add_argument("--probe-every", type=int, default=5, help="probe one step in this many of the timed region")
+    ap.add_argument("--reserve-cus", type=int, default=0,
+                    help="run the step on a stream that leaves this many CUs idle (vqx_stream_create_cu_mask): "
+                         "the cost of co-resident work such as RCCL's all-reduce kernels")
     return ap.parse_args()
 
 
@@ -194,6 +197,11 @@ def main():
     xs = [torch.randn(B_PER_GPU, mel, T_FRAMES, generator=gen).to(dev) for _ in range(n_batches)]
     ys = [torch.randint(0, cfg["y_num"], (B_PER_GPU, 1), generator=gen).to(dev) for _ in range(n_batches)]
 
+    masked = None
+    if a.reserve_cus > 0:
+        masked, cus_used = ops.cu_masked_stream(a.reserve_cus)
+        torch.cuda.set_stream(masked)
+    comm = tr.engine.comm
     for i in range(a.warmup):
         _, det = tr.train_step((xs[i % n_batches], ys[i % n_batches]))
     if a.warmup:
@@ -214,6 +222,9 @@ def main():
         probe.select(max(per.values(), key=lambda v: v[0])[1])
     if probe is not None:
         probe.clear()
+    if comm is not None:  # communication diagnostics over the timed region
+        comm.reset_stats()
+        comm.timing = True
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -232,6 +243,21 @@ def main():
     if probe is not None:
         probe.select(None)
     elapsed = t1 - t0
+    comm_out = None
+    if comm is not None:
+        comm.timing = False
+        nbytes, calls, grad_ms, ema_ms = comm.stats()
+        per = torch.tensor([nbytes / a.steps, calls / a.steps, grad_ms / a.steps, ema_ms / a.steps],
+                           device=dev, dtype=torch.float64)
+        allr = [torch.empty_like(per) for _ in range(world)]
+        dist.all_gather(allr, per)
+        allr = torch.stack(allr).cpu().tolist()
+        # per rank and step: bytes all-reduced, collectives issued, and how long
+        # the compute stream stood still behind the gradient all-reduces
+        # (Comm.finish) and the EMA-statistics all-reduce (codebook update)
+        comm_out = {"bytes_per_step": round(allr[0][0]), "collectives_per_step": allr[0][1],
+                    "grad_wait_ms": [round(r[2], 4) for r in allr], "ema_wait_ms": [round(r[3], 4) for r in allr],
+                    "bucket_bytes": comm.bucket * 4, "backend": comm.backend}
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -272,7 +298,10 @@ def main():
         "step_mfma_frac": round(FLOP_PER_FRAME * value / world / (PEAK_BF16 if a.dtype == "bf16" else PEAK_F32), 4),
         "roofline": roof,
         "loss": {k: round(v, 4) for k, v in detail.items()},
+        "comm": comm_out,
     }
+    if masked is not None:
+        out["reserved_cus"] = {"reserved": a.reserve_cus, "cus_used": cus_used}
     vq = time_vq(tr, a.vq_reps) if a.vq_reps > 0 else None
     out["vq"] = vq
     if world == 1 and a.fp32_steps > 0 and a.dtype != "fp32":

@@ -511,6 +511,14 @@ int vqx_probe_clear(void);
 int vqx_probe_count(int64_t* n);
 int vqx_probe_read(int64_t i, int32_t* info5, double* flops, float* ms);
 
+/* A stream on all but `reserve_cus` of the current device's CUs
+ * (hipExtStreamCreateWithCUMask; reserved CUs spread evenly over the CU
+ * indices), for measuring what co-resident work such as RCCL's all-reduce
+ * kernels costs the step (bench.py --reserve-cus).  *cus_used = the CUs the
+ * stream may use.  No reference counterpart (measurement only). */
+int vqx_stream_create_cu_mask(int32_t reserve_cus, vqx_stream_t* out, int32_t* cus_used);
+int vqx_stream_destroy(vqx_stream_t stream);
+
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
 #define VQX_ABI_VERSION 121
 int vqx_version(void);

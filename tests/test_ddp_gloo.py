@@ -57,9 +57,15 @@ def _comm_worker(rank, port, q):
         want = torch.arange(1000, dtype=torch.float32) * 1.5  # mean of x1 and x2
         s = torch.full((3,), float(rank + 1))
         work = comm.all_reduce_sum(s, async_op=True)
-        work.wait()
+        comm.wait(work, "ema")
         m = comm.mean_scalars(torch.tensor([float(rank)]))
-        q.put((rank, torch.equal(flat, want), s.tolist(), m.item()))
+        # diagnostics (bench.py "comm"): 1000 gradient floats in 64-float buckets
+        # (10 + 7) plus the 3-float sum; waits are timed under RCCL only
+        nbytes, calls, grad_ms, ema_ms = comm.stats()
+        ok_stats = (nbytes, calls, grad_ms, ema_ms) == (1003 * 4, 18, 0, 0)
+        comm.reset_stats()
+        ok_stats = ok_stats and comm.stats() == (0, 0, 0, 0)
+        q.put((rank, torch.equal(flat, want) and ok_stats, s.tolist(), m.item()))
         dist.destroy_process_group()
     except Exception as e:  # surface the failure to the parent
         q.put((rank, repr(e), None, None))

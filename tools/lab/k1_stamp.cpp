@@ -1,4 +1,6 @@
 // Diagnostic build: per-workgroup phase times of the 1x1 conv GEMMs (s_memtime
+// Needs the stamp points of tools/lab/k1_stamp.patch applied to
+// vae_npvc_amd/csrc/vqx_gemm_kernel.h (git apply tools/lab/k1_stamp.patch).
 // stamps in conv_gemm_body, -DVQX_STAMP) at the config-2 shapes.  For one launch
 // (after warm-ups) prints, per case: the effective clock, and over workgroups
 // the median / p10 / p90 of start, end of prologue, end of main loop, end of

@@ -122,6 +122,8 @@ _SIGS = {
     "vqx_vq_plain_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int64, c_int32,
                          c_int32, c_float, c_float, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_int32, c_void_p, c_void_p],
+    "vqx_stream_create_cu_mask": [c_int32, ctypes.POINTER(c_void_p), ctypes.POINTER(c_int32)],
+    "vqx_stream_destroy": [c_void_p],
     "vqx_probe_enable": [c_int32],
     "vqx_probe_select": [c_void_p],
     "vqx_probe_clear": [],

@@ -31,6 +31,7 @@ ran, the reference copies the nonexistent `iter.0` and crashes
     python -m vae_npvc_amd.bin.train -c conf.yaml --output_dir exp --train_dir data/train [--valid_dir ...]
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 -m vae_npvc_amd.bin.train ...
 """
+import datetime
 import logging
 import os
 from importlib import import_module
@@ -45,10 +46,13 @@ from torch.utils.data import DataLoader
 from ..dataset.sampler import ShardSampler
 
 
-def setup_distributed(backend=None):
+def setup_distributed(backend=None, timeout_s=None):
     """Initialise the process group from torchrun's environment (before any
     other GPU call) and select GPU LOCAL_RANK.  Returns (world, rank, backend)
-    -- (1, 0, None) when not launched with more than one process."""
+    -- (1, 0, None) when not launched with more than one process.
+    `timeout_s` (config key `dist_timeout_s`) bounds every collective wait,
+    e.g. the other ranks' barrier while rank 0 validates at a checkpoint;
+    None keeps torch's default."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world <= 1:
         return 1, 0, None
@@ -59,12 +63,13 @@ def setup_distributed(backend=None):
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if backend is None:
         backend = "nccl" if torch.cuda.device_count() > 0 else "gloo"  # device_count() does not initialise HIP
+    kw = {} if timeout_s is None else dict(timeout=datetime.timedelta(seconds=float(timeout_s)))
     if backend == "nccl":
         dev = torch.device("cuda", local)
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group("nccl", device_id=dev, **kw)
         torch.cuda.set_device(dev)
     else:
-        dist.init_process_group(backend)
+        dist.init_process_group(backend, **kw)
     return world, rank, backend
 
 
@@ -103,15 +108,16 @@ def _ranks_mean(train_log, backend):
 
 
 def train(args):
-    world, rank, backend = setup_distributed(getattr(args, "backend", None))
+    import yaml
+    config = yaml.safe_load(open(args.config))  # host only: the process group comes before any GPU call
+    # rank 0 alone validates at a checkpoint while the others wait in a barrier:
+    # a long validation set needs more than torch's default collective timeout
+    world, rank, backend = setup_distributed(getattr(args, "backend", None), config.get("dist_timeout_s", 7200))
     ddp = world > 1
     output_dir = args.output_dir
     checkpoint_path = args.checkpoint
     train_dir = args.train_dir
     valid_dir = args.valid_dir
-
-    import yaml
-    config = yaml.safe_load(open(args.config))
 
     trainer_type = config.get("trainer_type", "vae_npvc_amd.trainer.basic:Trainer")
     dataset_type = config.get("dataset_type", "vae_npvc_amd.dataset.utt2mel_spk:Dataset")

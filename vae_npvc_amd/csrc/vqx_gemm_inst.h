@@ -117,7 +117,9 @@ void launch_one(const GemmParams& P, int grid, hipStream_t s) {
                                           : 2.0 * (double)P.n_rows * P.Nc * P.K;
   if constexpr (sizeof(T) == 2 && !GEN && MODE != MODE_WGRAD && PRO == VQX_PRO_NONE &&
                 (EK == EK_NONE || EK == EK_ELEM || EK == EK_SPLIT)) {
-    if (three_per_cu(grid)) {  // gen = 4: conv_gemm3_kernel (32-deep K-tiles, three workgroups per CU)
+    // gen = 4: conv_gemm3_kernel (32-deep K-tiles, three workgroups per CU);
+    // measured on the 1x1 640-column res/skip layers only, so 1x1 only
+    if (P.ntaps == 1 && three_per_cu(grid)) {
       const int info3[5] = {VQX_BF16, MODE, P.pro, 4, EK};
       gemm_launch((const void*)conv_gemm3_kernel<T, MODE, PRO, GEN, EK>, grid, s, P, info3, flops);
       return;

@@ -509,10 +509,13 @@ __device__ __forceinline__ f32x4_t pro_frag(f32x4_t f, float s) {
 // kernel orders its DMAs explicitly (counted `s_waitcnt vmcnt` + s_barrier
 // before a stage is read; the loops drain to vmcnt(0) before the epilogue
 // reuses the staging LDS), so hiding them from the pass is safe; M0 (the
-// DMA's LDS base) is set in the same statement.
+// DMA's LDS base) is set in the same statement.  An SALU write of M0 needs
+// one wait state before an LDS-DMA reads it; the hazard recognizer that
+// inserts it for the builtin does not look inside inline asm, hence the
+// explicit s_nop.
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, unsigned off) {
   const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(VQX_LDS(void)*)lds);
-  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(la), "v"(off), "s"(r)
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(la), "v"(off), "s"(r)
                : "memory", "m0");
 }
 
@@ -699,22 +702,6 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
 template <typename T, int BK, int NST>
 __host__ __device__ constexpr int conv_gemm_smem() { return NST * 2 * 128 * BK * (int)sizeof(T); }
 
-// Diagnostic builds only (tools/lab/k1_stamp.cpp, -DVQX_STAMP): s_memtime at the
-// phase boundaries of conv_gemm_body, stored by thread 0 into vqx_stamp_buf.
-#ifdef VQX_STAMP
-__device__ unsigned long long* vqx_stamp_buf;
-#define VQX_STAMP_AT(i)                                                                   \
-  do {                                                                                    \
-    __builtin_amdgcn_sched_barrier(0);                                                    \
-    unsigned long long t_;                                                                \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
-    __builtin_amdgcn_sched_barrier(0);                                                    \
-    stamp_[i] = t_;                                                                       \
-  } while (0)
-#else
-#define VQX_STAMP_AT(i)
-#endif
-
 // The kernel body as a device function of (bid, nwg) = (this workgroup's
 // index, workgroup count) of its own tile grid, on the caller's LDS, so that
 // dual_*_kernel can host two GEMMs in one launch.
@@ -733,11 +720,6 @@ __device__ __forceinline__ void conv_gemm_body(const GemmParams& P, int bid, int
   static_assert(BK % (16 / ES * 2) == 0 || ES == 4, "BK");
   static_assert(conv_gemm_smem<T, BK, NST>() == NST * STAGE, "LDS");
 
-#ifdef VQX_STAMP
-  unsigned long long stamp_[5];
-  stamp_[4] = __builtin_amdgcn_s_memrealtime();
-#endif
-  VQX_STAMP_AT(0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
@@ -1074,7 +1056,6 @@ __device__ __forceinline__ void conv_gemm_body(const GemmParams& P, int bid, int
     if constexpr (kPrefetch) epi_prefetch<EK>(P, m0, n0, tid, rows);  // lands with the prologue DMA
     wait_vm(NP * (pre - 1));
     __builtin_amdgcn_s_barrier();
-    VQX_STAMP_AT(1);
     int buf = 0;
     for (int kt = 0; kt < nk; ++kt) {
       const int fbuf = (buf + NST - 1) % NST;  // buffer of tile kt+NST-1 == buffer of tile kt-1
@@ -1094,18 +1075,7 @@ __device__ __forceinline__ void conv_gemm_body(const GemmParams& P, int bid, int
     }
   }
 
-  VQX_STAMP_AT(2);
   tile_epilogue<T, MODE, EK, kPrefetch, kPreVec>(P, acc, smem, m0, n0, tn, split, gmr, (int)threadIdx.x, &rows);
-#ifdef VQX_STAMP
-  __syncthreads();
-  VQX_STAMP_AT(3);
-  const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
-  if (threadIdx.x == 0) {
-    unsigned long long* o = vqx_stamp_buf + (size_t)bid * 8;
-    for (int i = 0; i < 5; ++i) o[i] = stamp_[i];
-    o[5] = rt1;
-  }
-#endif
 }
 
 template <typename T, int MODE, int PRO, bool GEN, int BK, int NST, int EK>

@@ -270,7 +270,8 @@ class VQVAEEngine:
         self.dims = d = dict(mel=enc.in_ch, Z=enc.z_ch, S=dec.skip_ch, F=dec.final_ch, cond=dec.cond_ch,
                              K=model.quantizer.z_num, ydim=model.embeds._embedding.weight.shape[1],
                              jitter_p=model.jitter.probability)
-        assert d["Z"] == 128 and model.quantizer.z_dim == 128, "the fused VQ kernel is built for z_dim = 128"
+        if d["Z"] != 128 or model.quantizer.z_dim != 128:  # Model's constructor refuses these already
+            raise NotImplementedError("the fused VQ kernel is built for z_dim = 128")
         # straight-through VectorQuantizer (use_ema: false)
         self.plain = not model.use_ema
         self.vq_normalize = bool(getattr(model.quantizer, "normalize", False)) if self.plain else False
@@ -1171,7 +1172,7 @@ class VQVAEEngine:
             w.ev_ema = None
             return
         if getattr(self, "_ema_work", None) is not None:
-            self._ema_work.wait()
+            self.comm.wait(self._ema_work, "ema")
             self._ema_work = None
         self._ema_apply(w)
 

@@ -27,6 +27,10 @@ class WNConv1d(nn.Module):
         vshape = (cin, cout, k) if transposed else (cout, cin, k)
         v = torch.empty(vshape).uniform_(-bound, bound)
         if not weight_norm:  # use_weight_norm: false -> a plain nn.Conv1d / ConvTranspose1d (weight, bias)
+            # reset_parameters (vqvae.py:210-217, 336-343) re-draws every conv
+            # weight N(0, 2/fan_in), torch's fan_in = weight.size(1) * k; with
+            # weight norm on it is a no-op (it writes the recomputed .weight)
+            nn.init.kaiming_normal_(v, nonlinearity="relu")
             self.weight = nn.Parameter(v)
             self.bias = nn.Parameter(torch.empty(cout).uniform_(-bound, bound))
             self.has_weight_norm = False

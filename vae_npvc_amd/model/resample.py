@@ -58,6 +58,7 @@ class ResampleConv1d(nn.Module):
         self.splits = splits
         self.has_weight_norm = bool(weight_norm)
         if not weight_norm:  # a plain strided Conv1d / ConvTranspose1d: weight, bias (use_weight_norm: false)
+            nn.init.kaiming_normal_(v, nonlinearity="relu")  # reset_parameters, vqvae.py:210-217 (as WNConv1d)
             self.weight = nn.Parameter(v)
             self.bias = nn.Parameter(torch.empty(cout).uniform_(-bound, bound))
             return

@@ -120,6 +120,11 @@ class Model(nn.Module):
         self.encoder = Encoder(**arch["encoder"])
         self.decoder = Decoder(**arch["decoder"])
         self.use_ema = arch.get("use_ema", False)
+        # the reference's quantizers take any z_dim (layers_vq.py:166-173); the
+        # fused VQ kernel (vqx_vq_forward) keeps a frame's 128 dims in registers
+        z_dim, z_ch = arch.get("z_dim", 128), self.encoder.z_ch
+        if z_dim != 128 or z_ch != 128:
+            raise NotImplementedError(f"z_dim {z_dim} / encoder output {z_ch}: the HIP quantizer is built for 128")
         if self.use_ema:
             self.quantizer = EMAVectorQuantizer(arch.get("z_num", 512), arch.get("z_dim", 128), arch.get("mu", 0.9),
                                                 reduction="frame_mean")

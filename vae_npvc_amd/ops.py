@@ -500,3 +500,17 @@ def vq_plain_bwd(z, z_norm, z_len, zq, dzq, src_t, T, normalize, beta, scale, dz
     call("vqx_vq_plain_bwd", ptr(z), ptr(z_norm), ptr(z_len), ptr(zq), ptr(dzq), ptr(src_t), T, zq.shape[0],
          zq.shape[1], int(normalize), beta, scale, ptr(dz), dt_code(dz.dtype), ptr(bsum), ptr(bcnt), ptr(emb),
          ptr(e_len), emb.shape[0], ptr(dE), stream_ptr())
+
+
+def cu_masked_stream(reserve_cus):
+    """A torch ExternalStream on all but `reserve_cus` CUs of the current
+    device (vqx_stream_create_cu_mask) and the CU count it may use; release it
+    with release_stream(stream)."""
+    s = ctypes.c_void_p()
+    used = ctypes.c_int32()
+    call("vqx_stream_create_cu_mask", int(reserve_cus), ctypes.byref(s), ctypes.byref(used))
+    return torch.cuda.ExternalStream(s.value), used.value
+
+
+def release_stream(stream):
+    call("vqx_stream_destroy", ctypes.c_void_p(stream.cuda_stream))

@@ -42,11 +42,45 @@ class Comm:
         self.backend = dist.get_backend(group)
         self.bucket = max(1, bucket_bytes // 4)
         self.pending = []
+        # diagnostics (bench.py): bytes all-reduced, collectives issued and,
+        # when `timing` is on, the time the compute stream stood still behind
+        # the gradient / EMA all-reduces (event pairs around each wait)
+        self.bytes = 0
+        self.calls = 0
+        self.timing = False
+        self._waits = {"grad": [], "ema": []}
+
+    def _account(self, t):
+        self.bytes += t.numel() * t.element_size()
+        self.calls += 1
+
+    def wait(self, work, tag):
+        """work.wait() on the current stream; timed under `timing` (RCCL: the
+        compute stream's stall until the collective has finished)."""
+        if not (self.timing and self.backend == "nccl"):
+            work.wait()
+            return
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        work.wait()
+        e1.record()
+        self._waits[tag].append((e0, e1))
+
+    def reset_stats(self):
+        self.bytes = self.calls = 0
+        self._waits = {"grad": [], "ema": []}
+
+    def stats(self):
+        """(bytes, collectives, grad-wait ms, EMA-wait ms) since reset_stats();
+        synchronises on the recorded events."""
+        ms = {k: sum(a.elapsed_time(b) for a, b in v) for k, v in self._waits.items()}
+        return self.bytes, self.calls, ms["grad"], ms["ema"]
 
     def _avg_op(self):
         return dist.ReduceOp.AVG if self.backend == "nccl" else dist.ReduceOp.SUM
 
     def all_reduce_sum(self, t, async_op=False):
+        self._account(t)
         return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
 
     def all_gather_cat(self, t):
@@ -62,15 +96,23 @@ class Comm:
         op = self._avg_op()
         for s in range(lo, hi, self.bucket):
             view = flat[s: min(hi, s + self.bucket)]
+            self._account(view)
             work = dist.all_reduce(view, op=op, group=self.group, async_op=True)
             self.pending.append((work, view))
 
     def finish(self):
         """Make the current stream wait for every launched reduce."""
+        timed = self.timing and self.backend == "nccl" and self.pending
+        if timed:  # one event pair around all the waits: the stream's total stall
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
         for work, view in self.pending:
             work.wait()
             if self.backend != "nccl":
                 view.div_(self.world)
+        if timed:
+            e1.record()
+            self._waits["grad"].append((e0, e1))
         self.pending = []
 
     def mean_scalars(self, t):
