@@ -185,6 +185,8 @@ def main():
     cfg = yaml.safe_load(open(os.path.join(ROOT, "vae_npvc_amd", "conf", f"{a.config}.yaml")))
     cfg["compute_dtype"] = a.dtype
     cfg["batch_size"] = B_PER_GPU
+    if os.environ.get("VQX_ENGINE"):  # A/B runs: engine schedule options as JSON (engine/step.py EngineOptions)
+        cfg["engine"] = json.loads(os.environ["VQX_ENGINE"])
 
     from vae_npvc_amd import ops
     from vae_npvc_amd.trainer.basic import Trainer

@@ -120,7 +120,25 @@ typedef struct vqx_conv_args {
                                 Taps sit at n + j*dil - pad; 1 <= ntaps <= 8 and
                                 0 <= pad <= (ntaps-1)*dil.  DGRAD takes the forward
                                 layer's ntaps/dil and pad' = (ntaps-1)*dil - pad    */
+  int32_t kernel_policy;     /* VQX_POLICY_* (ABI 122): which bf16 GEMM kernels this call may
+                                use; 0 = automatic.  Per call, no process-wide state.         */
 } vqx_conv_args;
+
+/* Kernel policy of a conv GEMM call (vqx_conv_args / vqx_wgrad_args
+ * .kernel_policy; the data-gradient args decide for vqx_conv1d_dgrad_wgrad):
+ * AUTO picks by shape (3-tap, pad-1 bf16 layers with T % 128 == 0 run the
+ * tap-reuse kernels, the 512-frame tall kernel where it fills the GPU, 1x1
+ * layers the implicit-im2col kernel, layer pairs the fused DGRAD + WGRAD
+ * launches); IM2COL keeps every GEMM on the implicit-im2col kernel and turns
+ * the fused launches off; TALL256 / TALL512 force the tall tap-reuse kernel's
+ * 256 / 512-frame tiles where they apply; TR128 keeps 3-tap layers on the
+ * 128-frame tap-reuse kernel.  All produce the same values (tests compare
+ * them); the choice is speed only. */
+#define VQX_POLICY_AUTO 0
+#define VQX_POLICY_IM2COL 1
+#define VQX_POLICY_TALL256 2
+#define VQX_POLICY_TALL512 3
+#define VQX_POLICY_TR128 4
 
 int vqx_conv1d_fwd(const vqx_conv_args* a, vqx_stream_t stream);
 int vqx_conv1d_dgrad(const vqx_conv_args* a, vqx_stream_t stream);
@@ -145,6 +163,7 @@ typedef struct vqx_wgrad_args {
   int32_t slab_dtype; /* VQX_F32, or VQX_BF16 (bf16 operands only): each split's fp32 partial
                          rounded once to bf16, half the slab bytes written here and read by
                          vqx_weight_norm_bwd, which sums them in fp32 */
+  int32_t kernel_policy; /* VQX_POLICY_* (ABI 122); IM2COL: no tap-reuse weight-gradient kernel */
 } vqx_wgrad_args;
 
 int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream);
@@ -478,24 +497,9 @@ int vqx_wgrad_tiles(int64_t n_rows, int32_t T, int32_t r_dim, int32_t c_dim, int
 
 /* Thread-local description of the last failure. */
 const char* vqx_last_error(void);
-/* bf16 conv GEMM kernel policy (process-wide, for tests and A/B runs):
- * 0 = automatic (3-tap, pad-1 FWD/DGRAD with T % 128 == 0 run the tap-reuse
- * kernel, everything else the implicit-im2col kernel), 1 = implicit-im2col
- * kernel only, 2 / 3 = the tall tap-reuse kernel with 256 / 512-frame tiles
- * wherever T % 256 == 0 and the frames divide, 4 = the 128-frame tap-reuse
- * kernel only, 5 = automatic with the wide 8-wave weight-gradient kernels
- * (3-tap c_dim % 128 == 0, 1x1 c_dim % 256 == 0), 6 = automatic with the
- * fused 1x1 launches of vqx_conv1d_dgrad_wgrad, 7 = their three-workgroups-
- * per-CU form.  The environment variable
- * VQX_TAP_REUSE=0 forces 1, VQX_TR8=0/1/2 fixes the tall kernel's choice
- * under policy 0, VQX_WGRAD_WIDE=1 selects the wide kernels, VQX_DUAL=0/1/2/3/4 sets
- * the fused launches of vqx_conv1d_dgrad_wgrad (off / 3-tap pairs / 3-tap
- * and interleaved 1x1 pairs / 3-tap and in-sequence 1x1 pairs, the default /
- * 3-tap and three-per-CU 1x1 pairs;
- * policy 1 turns them off, policy 6 forces the interleaved 1x1 form). */
-int vqx_set_gemm_tile(int32_t policy);
 
-/* Launch probe (measurement only; not reentrant while enabled).  While on,
+/* Launch probe (measurement only; its log and switches are per host thread,
+ * so calls on other threads are unaffected).  While on,
  * each conv GEMM launch records a start/stop event pair stamped on its own
  * dispatch (hipExtLaunchKernelGGL); after the stream is synchronised,
  * vqx_probe_read returns per launch {dtype, mode, prologue, gen, epilogue kind},
@@ -520,7 +524,7 @@ int vqx_stream_create_cu_mask(int32_t reserve_cus, vqx_stream_t* out, int32_t* c
 int vqx_stream_destroy(vqx_stream_t stream);
 
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
-#define VQX_ABI_VERSION 121
+#define VQX_ABI_VERSION 122
 int vqx_version(void);
 
 #ifdef __cplusplus

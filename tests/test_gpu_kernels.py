@@ -18,13 +18,13 @@ def _ops():
 
 @pytest.fixture(params=[0, 1], ids=["auto", "im2col"])
 def tile(request):
-    """Run a GEMM test under both kernel policies (vqx_set_gemm_tile): 0 lets
-    3-tap bf16 layers with T % 128 == 0 take the tap-reuse kernel, 1 keeps
-    every layer on the implicit-im2col kernel."""
-    from vae_npvc_amd import _lib as L
-    L.call("vqx_set_gemm_tile", request.param)
-    yield request.param
-    L.call("vqx_set_gemm_tile", 0)
+    """Run a GEMM test under both kernel policies (vqx_conv_args.kernel_policy,
+    through ops.kernel_policy): 0 lets 3-tap bf16 layers with T % 128 == 0
+    take the tap-reuse kernel, 1 keeps every layer on the implicit-im2col
+    kernel."""
+    ops = _ops()
+    with ops.kernel_policy(request.param):
+        yield request.param
 
 
 def ref_conv(x_ntc, w, B, T, pad, pro=None):
@@ -554,7 +554,8 @@ def test_gnbwd_epilogue_matches_standalone(glu, tile):
         assert relerr(a, b) < 2e-2, relerr(a, b)
 
 
-@pytest.mark.parametrize("case", ["k1_glu", "k1_res", "k1_plain", "tr_mask", "tr_convt", "gen", "tr_full", "k1_full"])
+@pytest.mark.parametrize("case", ["k1_glu", "k1_res", "k1_plain", "tr_mask", "tr_convt", "gen", "tr_full", "k1_full",
+                                  "tr_gnbwd", "tr_gnbwd_full"])
 def test_fused_dgrad_wgrad_equals_separate_launches(case):
     """vqx_conv1d_dgrad_wgrad (vqx_gemm_dual.hip: one launch interleaving a
     layer's data- and weight-gradient GEMMs) against vqx_conv1d_wgrad +
@@ -565,7 +566,10 @@ def test_fused_dgrad_wgrad_equals_separate_launches(case):
     default in-sequence, the interleaved and the three-per-CU form), the
     3-tap tap-reuse pair
     with the activation-derivative mask, the ConvTranspose form (shift -1,
-    residual + column sums), and an im2col-only layer (cin 80: two launches);
+    residual + column sums), the encoder's first stack conv (mask, residual
+    = the skip conv's data gradient, column sums and the previous block's
+    GroupNorm-backward sums; engine/step.py encoder_bwd), and an im2col-only
+    layer (cin 80: two launches);
     *_full at the bench size (64 x 256 frames: 512 + 512 workgroups, so the
     256-block interleaved groups are exercised)."""
     ops = _ops()
@@ -576,7 +580,8 @@ def test_fused_dgrad_wgrad_equals_separate_launches(case):
     N = B * T
     k = 3 if case.startswith("tr") else 1
     cfg = {"k1_glu": (640, 512), "k1_res": (512, 512), "k1_plain": (512, 768), "tr_mask": (1024, 512),
-           "tr_convt": (512, 1024), "gen": (80, 512), "tr_full": (1024, 512), "k1_full": (512, 512)}[case]
+           "tr_convt": (512, 1024), "gen": (80, 512), "tr_full": (1024, 512), "k1_full": (512, 512),
+           "tr_gnbwd": (512, 512), "tr_gnbwd_full": (512, 512)}[case]
     co, ci = cfg                                   # forward layer cout, cin
     dy = torch.randn(N, co, device=DEV).to(dt)
     x = torch.randn(N, ci, device=DEV).to(dt)
@@ -603,6 +608,13 @@ def test_fused_dgrad_wgrad_equals_separate_launches(case):
                      res=torch.randn(N, ci, device=DEV).to(dt))
     elif case in ("tr_mask", "tr_full"):
         extra = dict(mask=torch.randn(N, ci, device=DEV).to(dt), mask_slope=0.2)
+    elif case.startswith("tr_gnbwd"):
+        u = torch.randn(N, ci, device=DEV).to(dt)
+        mr = torch.empty(B, 1, 2, device=DEV)
+        ops.groupnorm_stats(u, T, 1, torch.empty(B * 24, device=DEV), mr)
+        extra = dict(mask=torch.randn(N, ci, device=DEV).to(dt), mask_slope=0.2, gn_h=u, gn_mr=mr,
+                     gn_gamma=torch.randn(ci, device=DEV), gn_beta=torch.randn(ci, device=DEV),
+                     res=torch.randn(N, ci, device=DEV).to(dt))
     elif case == "tr_convt":
         extra = dict(res=torch.randn(N, ci, device=DEV).to(dt))
     outs = []
@@ -611,18 +623,18 @@ def test_fused_dgrad_wgrad_equals_separate_launches(case):
         o = {"dx": torch.full((N, ci), float("nan"), device=DEV, dtype=dt),
              "slabs": torch.full(slab_shape, float("nan"), device=DEV, dtype=dt)}
         kw = dict(extra)
-        if case in ("k1_glu", "k1_res"):
+        if case in ("k1_glu", "k1_res") or case.startswith("tr_gnbwd"):
             o["gnb"] = torch.full((N // 128 * (ci // 128) * 4,), float("nan"), device=DEV)
             kw["gn_bwd"] = o["gnb"]
-        if case in ("k1_res", "tr_convt"):
+        if case in ("k1_res", "tr_convt") or case.startswith("tr_gnbwd"):
             o["cs"] = torch.full((N // 128, ci), float("nan"), device=DEV)
             kw["colsum"] = o["cs"]
         if fused_call[0]:
-            L.call("vqx_set_gemm_tile", fused_call[1])
+            ops.set_kernel_policy(fused_call[1])
             try:
                 fused = ops.conv_dgrad_wgrad(dy, wp, o["dx"], dict(dkw, **kw), p_op, q_op, o["slabs"], wkw)
             finally:
-                L.call("vqx_set_gemm_tile", 0)
+                ops.set_kernel_policy(0)
             assert fused == (case != "gen"), (case, fused)
         else:
             ops.conv_wgrad(p_op, q_op, o["slabs"], **wkw)
@@ -695,7 +707,7 @@ def test_conv_tap_reuse_matches_im2col_and_fp64(mode, n_utt, T, cin, cout):
     res = torch.randn(N, k_out, device=DEV).to(torch.bfloat16)
     outs = []
     for policy in (0, 1):
-        L.call("vqx_set_gemm_tile", policy)
+        ops.set_kernel_policy(policy)
         y = torch.empty(N, k_out, device=DEV, dtype=torch.float32)
         if mode == "fwd":
             ops.conv_fwd(a, wp, y, T=T, cin=cin, cout=cout, ntaps=3, pad=1, bias=bias, res=res, out_f32=True)
@@ -703,7 +715,7 @@ def test_conv_tap_reuse_matches_im2col_and_fp64(mode, n_utt, T, cin, cout):
             ops.conv_dgrad(a, wp, y, T=T, cin=cout, cout=cin, ntaps=3, pad=1, bias=bias, res=res, out_f32=True)
         torch.cuda.synchronize()
         outs.append(y)
-    L.call("vqx_set_gemm_tile", 0)
+    ops.set_kernel_policy(0)
     ad = a.double().cpu().view(n_utt, T, k_in).permute(0, 2, 1)
     if mode == "fwd":
         ref = F.conv1d(ad, w.double().cpu(), padding=1)
@@ -741,7 +753,7 @@ def test_conv_tall_tap_reuse_matches_tap_reuse_and_fp64(mode, n_utt, T, cin, cou
     outs = []
     policies = [4, 2] + ([3] if N % 512 == 0 else [])
     for policy in policies:
-        L.call("vqx_set_gemm_tile", policy)
+        ops.set_kernel_policy(policy)
         y = torch.empty(N, k_out, device=DEV, dtype=torch.float32)
         y2 = torch.empty(N, k_out, device=DEV, dtype=torch.bfloat16)
         red = torch.full((N // 128, tn * 4 if mode == "fwd" else k_out), float("nan"), device=DEV)
@@ -754,7 +766,7 @@ def test_conv_tall_tap_reuse_matches_tap_reuse_and_fp64(mode, n_utt, T, cin, cou
             call(a, wp, y2, bias=bias, colsum=red, **kw)
         torch.cuda.synchronize()
         outs.append((y, y2, red))
-    L.call("vqx_set_gemm_tile", 0)
+    ops.set_kernel_policy(0)
     ad = a.double().cpu().view(n_utt, T, k_in).permute(0, 2, 1)
     ref = F.conv1d(ad, w.double().cpu(), padding=1) if mode == "fwd" else \
         F.conv_transpose1d(ad, w.double().cpu(), padding=1)
@@ -814,12 +826,12 @@ def test_wgrad_tap_reuse_matches_im2col_and_fp64(sign, n_utt, T, r_dim, c_dim, s
     outs = []
     # policy 0: the library's pick (tap reuse), 1: implicit im2col
     for policy in (0, 1):
-        L.call("vqx_set_gemm_tile", policy)
+        ops.set_kernel_policy(policy)
         slabs = torch.full((splits, r_dim, 3 * c_dim), float("nan"), device=DEV)
         ops.conv_wgrad(p, q, slabs, T=T, r_dim=r_dim, c_dim=c_dim, ntaps=3, pad=1, shift_sign=sign, splits=splits)
         torch.cuda.synchronize()
         outs.append(slabs.sum(0))
-    L.call("vqx_set_gemm_tile", 0)
+    ops.set_kernel_policy(0)
     pd = p.double().cpu().view(n_utt, T, r_dim)
     qd = q.double().cpu().view(n_utt, T, c_dim)
     ref = torch.zeros(r_dim, 3, c_dim, dtype=torch.float64)
@@ -854,14 +866,14 @@ def test_split_epilogue_with_narrow_residual(acc, B, T, tile):
     skip0 = torch.randn(N, S, device=DEV)
     outs = []
     for policy in ((0, 1) if tile == 0 else (tile,)):
-        L.call("vqx_set_gemm_tile", policy)
+        ops.set_kernel_policy(policy)
         skip = skip0.clone()
         y = torch.empty(N, C, device=DEV, dtype=torch.bfloat16)
         ops.conv_fwd(x, pack(w.float()).to(torch.bfloat16), y, T=T, cin=cin, cout=C + S, ntaps=1, pad=0, bias=bias,
                      res=res, out2=skip, split_col=C, out2_accumulate=acc)
         torch.cuda.synchronize()
         outs.append((y, skip))
-    L.call("vqx_set_gemm_tile", tile)
+    ops.set_kernel_policy(tile)
     y, skip = outs[0]
     full = x.double().cpu() @ w.double().cpu()[:, :, 0].t() + bias.double().cpu()
     assert relerr(y, full[:, :C] + res.double().cpu()) < 2e-2

@@ -1,7 +1,9 @@
 #!/bin/bash
-# A/B of environment knobs on the bench line, interleaved over two passes so
+# A/B of environment settings on the bench line, interleaved over two passes so
 # clock drift cancels: tools/gpu_ab_env.sh TAG "K1=a K2=b" "K1=c" ...
 # (the empty setting -- the defaults -- always runs first in each pass).
+# Engine schedule options go in as compact JSON, e.g. 'VQX_ENGINE={"slab_f32":true}'
+# (bench.py -> Model arch "engine"), a variant library as VQX_LIB=path.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp

@@ -15,7 +15,7 @@ from pathlib import Path
 import torch  # noqa: F401  (loads the HIP runtime first; see module docstring)
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libvqx.so"
-ABI_VERSION = 121  # include/vqx.h VQX_ABI_VERSION
+ABI_VERSION = 122  # include/vqx.h VQX_ABI_VERSION
 
 VQX_F32, VQX_BF16 = 0, 1
 PRO_NONE, PRO_LRELU, PRO_RELU, PRO_SCALE_RELU = 0, 1, 2, 3
@@ -39,7 +39,7 @@ class ConvArgs(ctypes.Structure):
         ("pro_scale", c_float), ("mask_slope", c_float), ("mask_scale", c_float),
         ("y2", c_void_p), ("ldy2", c_int32), ("epi_act", c_int32), ("colsum_part", c_void_p),
         ("stat_part", c_void_p), ("gn_groups", c_int32), ("gn_glu", c_int32),
-        ("gn_stat_tiles", c_void_p), ("gn_eps", c_float), ("dil", c_int32),
+        ("gn_stat_tiles", c_void_p), ("gn_eps", c_float), ("dil", c_int32), ("kernel_policy", c_int32),
     ]
 
 
@@ -49,7 +49,7 @@ class WgradArgs(ctypes.Structure):
         ("r_dim", c_int32), ("c_dim", c_int32), ("ntaps", c_int32), ("pad", c_int32),
         ("shift_sign", c_int32), ("ldp", c_int32), ("ldq", c_int32), ("dtype", c_int32),
         ("q_prologue", c_int32), ("splits", c_int32), ("pro_scale", c_float), ("dil", c_int32),
-        ("slab_dtype", c_int32),
+        ("slab_dtype", c_int32), ("kernel_policy", c_int32),
     ]
 
 
@@ -113,7 +113,6 @@ _SIGS = {
     "vqx_adam_hyper": [c_void_p, c_double, c_double, c_int32, c_double, c_double, c_double, c_void_p, c_void_p],
     "vqx_linear_batched_fwd": [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p],
     "vqx_linear_batched_bwd": [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p],
-    "vqx_set_gemm_tile": [c_int32],
     "vqx_wgrad_tiles": [c_int64, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
                         ctypes.POINTER(c_int32)],
     "vqx_vq_normalize": [c_void_p, c_int64, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -15,17 +15,19 @@ namespace vqx {
 // start/stop event pair that the runtime stamps on the kernel's own dispatch
 // packet, so the measured duration is the kernel's (no extra queue packets
 // between kernels).  Events come from a pool reused across probe sessions.
+// The probe state is per host thread (thread_local): a measurement session on
+// one thread never changes another thread's launches.
 struct ProbeRec {
   hipEvent_t start, stop;
   int info[5];  // dtype, mode, prologue, gen, epilogue kind
   double flops;
 };
-static bool g_probe_on = false;
-static bool g_probe_sel_on = false;  // record only launches whose info equals g_probe_sel
-static int g_probe_sel[5];
-static std::vector<ProbeRec> g_probe;
-static std::vector<std::pair<hipEvent_t, hipEvent_t>> g_event_pool;
-static size_t g_probe_used = 0;
+static thread_local bool g_probe_on = false;
+static thread_local bool g_probe_sel_on = false;  // record only launches whose info equals g_probe_sel
+static thread_local int g_probe_sel[5];
+static thread_local std::vector<ProbeRec> g_probe;
+static thread_local std::vector<std::pair<hipEvent_t, hipEvent_t>> g_event_pool;
+static thread_local size_t g_probe_used = 0;
 
 void gemm_launch(const void* fn, int grid, hipStream_t s, const GemmParams& P, const int info[5], double flops,
                  int block) {
@@ -60,15 +62,10 @@ void gemm_launch_args(const void* fn, int grid, hipStream_t s, void** args, cons
   (void)hipExtLaunchKernel(fn, dim3(grid), dim3(block), args, 0, s, ev.first, ev.second, 0);
 }
 
-// vqx_set_gemm_tile: 0 = automatic, 1 = implicit-im2col kernel only,
-// 2 / 3 = tap reuse through conv_tr8_kernel with 1 / 2 frame segments where it
-// applies, 4 = tap reuse through conv_tr_kernel only
-static int g_gemm_policy = 0;
-
 int cu_count() {
   int dev = 0, n = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
-  static int cached_dev = -1, cached = 0;  // one device per process in practice; re-query on a switch
+  static thread_local int cached_dev = -1, cached = 0;  // one device per thread in practice; re-query on a switch
   if (dev != cached_dev) {
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 0;
     cached_dev = dev;
@@ -77,26 +74,9 @@ int cu_count() {
   return cached;
 }
 
-bool three_per_cu(int grid) {
+bool three_per_cu(int grid, int policy) {
   const int cus = cu_count();
-  return g_gemm_policy == 0 && cus > 0 && grid > 2 * cus && grid <= 3 * cus;
-}
-
-bool tap_reuse_enabled() {
-  static const bool env_on = [] {
-    const char* e = getenv("VQX_TAP_REUSE");
-    return !(e && e[0] == '0');
-  }();
-  return env_on && g_gemm_policy != 1;
-}
-
-int tr8_policy() {
-  static const int pol = [] {
-    const char* e = getenv("VQX_TR8");  // 0 = off, 1/2 = SEGS, unset = automatic (-1)
-    return (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : -1;
-  }();
-  if (g_gemm_policy >= 2 && g_gemm_policy <= 4) return g_gemm_policy == 4 ? 0 : g_gemm_policy - 1;
-  return pol;
+  return policy == POL_AUTO && cus > 0 && grid > 2 * cus && grid <= 3 * cus;
 }
 
 static void launch_mode(GemmParams& P, int mode, int64_t rows, int extra_mult, bool bf16, bool gen, hipStream_t s) {
@@ -147,6 +127,7 @@ static int conv_prepare(const vqx_conv_args* a, int mode, GemmParams& P, bool& g
   }
   if ((epi & VQX_EPI_COLSUM) && !a->colsum_part) { set_error("vqx_conv: COLSUM needs colsum_part [ceil(n_rows/128)][cout]"); return -1; }
   if (!a->y || !aligned16(a->y)) { set_error("vqx_conv: y must be non-null and 16-byte aligned"); return -1; }
+  if (a->kernel_policy < POL_AUTO || a->kernel_policy > POL_TR128) { set_error("vqx_conv: kernel_policy %d not in 0..4", a->kernel_policy); return -1; }
 
   P = GemmParams{};
   P.a = a->x; P.b = a->w;
@@ -167,6 +148,7 @@ static int conv_prepare(const vqx_conv_args* a, int mode, GemmParams& P, bool& g
   P.colsum_part = a->colsum_part;
   P.stat_part = a->stat_part; P.gn_groups = a->gn_groups; P.gn_glu = a->gn_glu;
   P.gn_tiles = a->gn_stat_tiles; P.gn_eps = a->gn_eps;
+  P.policy = a->kernel_policy;
   if (P.gn_tiles && (mode != MODE_FWD || !(epi & VQX_EPI_GNADD) || a->T % 128 || a->cout % 128 ||
                      a->gn_groups != 1 || !a->gn_mean_rstd)) {
     set_error("vqx_conv: gn_stat_tiles needs FWD with GNADD, G = 1, T %% 128 == 0, cout %% 128 == 0 and gn_mean_rstd");
@@ -199,6 +181,7 @@ static int wgrad_prepare(const vqx_wgrad_args* a, GemmParams& P, bool& gen) {
   if (!aligned16(a->p) || !aligned16(a->q) || !a->slabs || !aligned16(a->slabs)) { set_error("vqx_conv1d_wgrad: bad pointers"); return -1; }
   if (a->shift_sign != 1 && a->shift_sign != -1) { set_error("vqx_conv1d_wgrad: shift_sign must be +-1"); return -1; }
   if (a->slab_dtype != VQX_F32 && !(a->slab_dtype == VQX_BF16 && a->dtype == VQX_BF16)) { set_error("vqx_conv1d_wgrad: slab_dtype %d (bf16 slabs need bf16 operands)", a->slab_dtype); return -1; }
+  if (a->kernel_policy < POL_AUTO || a->kernel_policy > POL_TR128) { set_error("vqx_conv1d_wgrad: kernel_policy %d not in 0..4", a->kernel_policy); return -1; }
   P = GemmParams{};
   P.a = a->p; P.b = a->q; P.n_rows = a->n_rows; P.T = a->T; P.lda = a->ldp; P.ldb = a->ldq;
   P.a_bytes = ((a->n_rows - 1) * (int64_t)a->ldp + a->r_dim) * es;
@@ -213,29 +196,16 @@ static int wgrad_prepare(const vqx_wgrad_args* a, GemmParams& P, bool& gen) {
   P.k_per_split = kps;
   P.y = a->slabs;
   P.slab_bf16 = a->slab_dtype == VQX_BF16;
+  P.policy = a->kernel_policy;
   const int bkv = a->dtype == VQX_BF16 ? 64 : 32;
   gen = (a->T % bkv) != 0 || (a->n_rows % bkv) != 0;
-  if (!gen && wgrad_tr_ok(a->n_rows, a->T, a->c_dim, a->ntaps, a->pad, dil, a->dtype == VQX_BF16, a->q_prologue)) {
+  if (!gen && wgrad_tr_ok(a->n_rows, a->T, a->c_dim, a->ntaps, a->pad, dil, a->dtype == VQX_BF16, a->q_prologue,
+                          a->kernel_policy)) {
     P.tap_reuse = 1;
     P.tiles_n = a->c_dim / 64;
   }
   return 0;
 }
-
-// fused DGRAD+WGRAD launches: 0 = off, 1 = 3-tap tap-reuse pairs only, 3 =
-// also the 1x1 pairs with DGRAD's workgroups first (default; env VQX_DUAL).
-// Measured (profiles/r02/dual_ab.txt): 3-tap pairs interleaved 3-8% faster
-// than two launches; 1x1 pairs in sequence 0.7% faster per step than two
-// launches (one ramp/tail less).  The interleaved and three-per-CU 1x1 forms
-// measured slower and were retired in round 3.
-int dual_policy() {
-  static const int pol = [] {
-    const char* e = getenv("VQX_DUAL");
-    return (e && (e[0] == '0' || e[0] == '1' || e[0] == '3')) ? e[0] - '0' : 3;
-  }();
-  return g_gemm_policy == 1 ? 0 : pol;
-}
-static bool dual_enabled() { return dual_policy() > 0; }
 
 }  // namespace vqx
 
@@ -265,7 +235,13 @@ extern "C" int vqx_conv1d_dgrad_wgrad(const vqx_conv_args* d, const vqx_wgrad_ar
   if (wgrad_prepare(w, PW, gw)) return -1;
   hipStream_t s = (hipStream_t)stream;
   const bool bf = d->dtype == VQX_BF16 && w->dtype == VQX_BF16;
-  if (bf && !gd && !gw && dual_enabled()) {
+  // fused DGRAD + WGRAD launches unless the call keeps every GEMM on the
+  // implicit-im2col kernels.  Measured (profiles/r02/dual_ab.txt): 3-tap pairs
+  // interleaved 3-8% faster than two launches; 1x1 pairs in sequence 0.7% off
+  // the step.  The interleaved and three-per-CU 1x1 forms measured slower and
+  // were retired in round 3; WGRAD-first 1x1 pairs with fewer splits in round 4
+  // (profiles/r04/slab_wfirst_ab.txt).
+  if (bf && !gd && !gw && d->kernel_policy != POL_IM2COL) {
     PD.tiles_m = (int)((d->n_rows + 127) / 128);
     PW.tiles_m = (PW.Mc + 127) / 128;
     if (launch_dual(PD, PD.tiles_m * PD.tiles_n, PW, PW.tiles_m * PW.tiles_n * PW.splits, s)) {
@@ -290,15 +266,9 @@ extern "C" int vqx_wgrad_tiles(int64_t n_rows, int32_t T, int32_t r_dim, int32_t
   const int bkv = bf16 ? 64 : 32;
   const bool gen = (T % bkv) != 0 || (n_rows % bkv) != 0;
   const int tm = (r_dim + 127) / 128;
-  if (!gen && wgrad_tr_ok(n_rows, T, c_dim, ntaps, pad, dil > 0 ? dil : 1, bf16, q_prologue))
+  if (!gen && wgrad_tr_ok(n_rows, T, c_dim, ntaps, pad, dil > 0 ? dil : 1, bf16, q_prologue, POL_AUTO))
     *tiles = tm * (c_dim / 64);
   else *tiles = tm * ((ntaps * c_dim + kBN - 1) / kBN);
-  return 0;
-}
-
-extern "C" int vqx_set_gemm_tile(int32_t policy) {
-  if (policy < 0 || policy > 4) { set_error("vqx_set_gemm_tile: policy %d not in 0..4", policy); return -1; }
-  g_gemm_policy = policy;
   return 0;
 }
 

@@ -14,8 +14,6 @@
 // ramp and one tail cover both.  Each workgroup runs the unchanged kernel body
 // (vqx_gemm_kernel.h conv_gemm_body / conv_tr_body / wgrad_tr_body) on its own
 // tile grid; the branch is uniform per workgroup.
-#include <stdlib.h>
-
 #include "vqx_gemm_inst.h"
 
 namespace vqx {
@@ -49,12 +47,8 @@ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 template <int EKD>
 __global__ __launch_bounds__(256, 2) void dual_k1_kernel(GemmParams PD, GemmParams PW, int nd, int nw, int ch) {
   __shared__ __attribute__((aligned(16))) char smem[conv_gemm_smem<bf16_t, 64, 2>()];
+  (void)ch;
   const int b = blockIdx.x;
-  if (ch < 0) {  // WGRAD's workgroups first
-    if (b < nw) conv_gemm_body<bf16_t, MODE_WGRAD, VQX_PRO_NONE, false, 64, 2, EK_NONE>(PW, b, nw, smem);
-    else conv_gemm_body<bf16_t, MODE_DGRAD, VQX_PRO_NONE, false, 64, 2, EKD>(PD, b - nw, nd, smem);
-    return;
-  }
   if (b < nd) conv_gemm_body<bf16_t, MODE_DGRAD, VQX_PRO_NONE, false, 64, 2, EKD>(PD, b, nd, smem);
   else conv_gemm_body<bf16_t, MODE_WGRAD, VQX_PRO_NONE, false, 64, 2, EK_NONE>(PW, b - nd, nw, smem);
 }
@@ -80,9 +74,10 @@ bool launch_dual(const GemmParams& PD, int nd, const GemmParams& PW, int nw, hip
       case EK_NONE: fn = (const void*)dual_tr_kernel<EK_NONE>; break;
       case EK_ELEM: fn = (const void*)dual_tr_kernel<EK_ELEM>; break;
       case EK_COLSUM: fn = (const void*)dual_tr_kernel<EK_COLSUM>; break;
+      case EK_GNBWD: fn = (const void*)dual_tr_kernel<EK_GNBWD>; break;
       default: return false;
     }
-  } else if (PD.ntaps == 1 && PW.ntaps == 1 && PW.tap_reuse == 0 && dual_policy() >= 3 && nd % 8 == 0) {
+  } else if (PD.ntaps == 1 && PW.ntaps == 1 && PW.tap_reuse == 0 && nd % 8 == 0) {
     kind = 3;
     switch (ekd) {
       case EK_NONE: fn = (const void*)dual_k1_kernel<EK_NONE>; break;
@@ -97,12 +92,7 @@ bool launch_dual(const GemmParams& PD, int nd, const GemmParams& PW, int nw, hip
   const double flops = 2.0 * (double)PD.n_rows * PD.Nc * PD.K + 2.0 * (double)PW.n_rows * PW.Mc * PW.Nc;
   // probe label: mode 3 = dual, prologue slot = kind (2: 3-tap, 3: 1x1 in sequence), gen = 5
   const int info[5] = {VQX_BF16, 3, kind, 5, ekd};
-  int chunk = 256;  // interleave period: blocks of each GEMM per group (profiles/r02/chunk_probe.txt)
-  static const bool k1_wfirst = [] {
-    const char* e = getenv("VQX_K1_WFIRST");
-    return e && e[0] == '1';
-  }();
-  if (kind == 3 && k1_wfirst && nw % 8 == 0) chunk = -1;
+  const int chunk = 256;  // interleave period: blocks of each GEMM per group (profiles/r02/chunk_probe.txt)
   GemmParams pd = PD, pw = PW;
   int a = nd, b = nw, c = chunk;
   void* args[] = {(void*)&pd, (void*)&pw, (void*)&a, (void*)&b, (void*)&c};

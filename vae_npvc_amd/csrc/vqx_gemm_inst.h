@@ -23,10 +23,12 @@ void gemm_launch_args(const void* fn, int grid, hipStream_t s, void** args, cons
 // (dual_k1_kernel / dual_tr_kernel) where an instance covers the pair;
 // false = not covered (the caller launches them separately)
 bool launch_dual(const GemmParams& PD, int nd, const GemmParams& PW, int nw, hipStream_t s);
-int dual_policy();  // vqx_gemm.hip: 0 off, 1 3-tap pairs, 3 3-tap and 1x1 pairs (1x1 in sequence) (env VQX_DUAL)
 
-// vqx_gemm.hip: tap-reuse kernel switch (env VQX_TAP_REUSE=0 turns it off, for A/B runs)
-bool tap_reuse_enabled();
+// Kernel policy of a call (vqx_conv_args.kernel_policy, include/vqx.h): 0
+// automatic, 1 implicit-im2col kernels only (no tap reuse, no fused
+// DGRAD + WGRAD launch), 2 / 3 the tall tap-reuse kernel with 256 / 512-frame
+// tiles wherever it applies, 4 the 128-frame tap-reuse kernel only.
+enum { POL_AUTO = 0, POL_IM2COL = 1, POL_TALL256 = 2, POL_TALL512 = 3, POL_TR128 = 4 };
 
 // conv_tr_kernel applies: bf16, no prologue, 3 taps / pad 1, 32-channel K
 // slices (16-channel slices when cin % 32 != 0, e.g. the 80-mel input conv),
@@ -34,28 +36,30 @@ bool tap_reuse_enabled();
 inline bool tap_reuse_ok(const GemmParams& P, bool bf16, bool gen) {
   return bf16 && P.pro == VQX_PRO_NONE && P.ntaps == 3 && P.pad == 1 && P.dil == 1 && P.kcin % 16 == 0 &&
          (!gen || P.kcin % 32 != 0) && P.K == 3 * P.kcin && P.T % 128 == 0 && P.n_rows % 128 == 0 &&
-         tap_reuse_enabled();
+         P.policy != POL_IM2COL;
 }
 
 // wgrad_tr_kernel applies: bf16, no prologue, 3 taps / pad 1, c_dim % 64 == 0,
 // 64-frame K-tiles inside one utterance
-inline bool wgrad_tr_ok(int64_t n_rows, int T, int c_dim, int ntaps, int pad, int dil, bool bf16, int pro) {
+inline bool wgrad_tr_ok(int64_t n_rows, int T, int c_dim, int ntaps, int pad, int dil, bool bf16, int pro,
+                        int policy) {
   return bf16 && pro == VQX_PRO_NONE && ntaps == 3 && pad == 1 && dil == 1 && c_dim % 64 == 0 && T % 64 == 0 &&
-         n_rows % 64 == 0 && tap_reuse_enabled();
+         n_rows % 64 == 0 && policy != POL_IM2COL;
 }
 
-// frame segments per conv_tr8_kernel tile (0 = use conv_tr_kernel).  Env
-// VQX_TR8=0/1/2 forces it.  By default the 512-frame tile where it still gives
-// every CU a workgroup (config 2: dec_in FWD, 57 vs 61 us in the step); the
-// 256-frame tile measured equal on enc FWD and 7-10% slower on both DGRADs
-// (profiles/r02/tr_lab.txt), so it is never picked automatically.
-int tr8_policy();
+// frame segments per conv_tr8_kernel tile (0 = use conv_tr_kernel).  Policy 2 /
+// 3 forces 256 / 512 frames, 4 none.  Automatically the 512-frame tile where it
+// still gives every CU a workgroup (config 2: dec_in FWD, 57 vs 61 us in the
+// step); the 256-frame tile measured equal on enc FWD and 7-10% slower on both
+// DGRADs (profiles/r02/tr_lab.txt), so it is never picked automatically.
 inline int tr8_segs(const GemmParams& P) {
   if (P.T % 256 || P.kcin % 32) return 0;
-  const int pol = tr8_policy();
   const int tn = (P.Nc + kBN - 1) / kBN;
-  if (pol == 0) return 0;
-  if (pol == 1 || pol == 2) return P.n_rows % (256 * pol) == 0 ? pol : 0;
+  if (P.policy == POL_TR128) return 0;
+  if (P.policy == POL_TALL256 || P.policy == POL_TALL512) {
+    const int segs = P.policy == POL_TALL256 ? 1 : 2;
+    return P.n_rows % (256 * segs) == 0 ? segs : 0;
+  }
   if (P.n_rows % 512 == 0 && (P.n_rows / 512) * tn >= 256) return 2;
   return 0;
 }
@@ -106,9 +110,9 @@ void dispatch_tr(const GemmParams& P, int grid, hipStream_t s) {
 
 // vqx_gemm.hip: compute units of the current device; true when a grid of
 // 2-per-CU conv_gemm_kernel workgroups needs more than one round but at most
-// 1.5 (automatic tile policy only)
+// 1.5 (automatic policy only)
 int cu_count();
-bool three_per_cu(int grid);
+bool three_per_cu(int grid, int policy);
 
 template <typename T, int MODE, int PRO, bool GEN, int EK>
 void launch_one(const GemmParams& P, int grid, hipStream_t s) {
@@ -119,7 +123,7 @@ void launch_one(const GemmParams& P, int grid, hipStream_t s) {
                 (EK == EK_NONE || EK == EK_ELEM || EK == EK_SPLIT)) {
     // gen = 4: conv_gemm3_kernel (32-deep K-tiles, three workgroups per CU);
     // measured on the 1x1 640-column res/skip layers only, so 1x1 only
-    if (P.ntaps == 1 && three_per_cu(grid)) {
+    if (P.ntaps == 1 && three_per_cu(grid, P.policy)) {
       const int info3[5] = {VQX_BF16, MODE, P.pro, 4, EK};
       gemm_launch((const void*)conv_gemm3_kernel<T, MODE, PRO, GEN, EK>, grid, s, P, info3, flops);
       return;

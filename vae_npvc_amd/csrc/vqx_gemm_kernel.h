@@ -93,6 +93,7 @@ struct GemmParams {
   int slab_bf16;   // WGRAD: slabs stored as bf16 (bf16 operands only)
   const float* gn_tiles;  // GNADD: merge mean/rstd from these GNSTATS tiles (G = 1) and write gn_mr
   float gn_eps;
+  int policy;      // host side: the call's kernel_policy (vqx_conv_args / vqx_wgrad_args)
 };
 
 template <typename T> struct Cfg;

@@ -38,7 +38,6 @@ reference's and the optimizer touches one contiguous buffer.
 """
 import bisect
 import math
-import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -127,6 +126,36 @@ def _tm(N):
     return (N + L.CONV_TILE_ROWS - 1) // L.CONV_TILE_ROWS
 
 
+@dataclass
+class EngineOptions:
+    """Schedule choices of the engine.  The defaults are the measured-best
+    configuration; A/B runs pass others through the model
+    config's `engine` mapping (Model(arch), arch["engine"] = {...}), never
+    through the environment.
+      fuse_gn          GroupNorm statistics from GEMM epilogue tiles (False:
+                       standalone statistics kernels)
+      enc_gn_finalize  encoder GroupNorm statistics through a separate finalize
+                       launch instead of the skip GEMM's in-launch merge
+      side_stream      conditioning linears and EMA statistics + codebook update
+                       on a second stream (measured 0.5-0.8% slower)
+      wgrad_wgs, wgrad_wgs_1x1, wgrad_wgs_solo
+                       workgroups per weight-gradient launch (the split-K
+                       factor) of the 3-tap layers, the 1x1 layers and the
+                       stage convs; wgrad_min_k: fewest frames per split
+      slab_f32         fp32 split-K slabs in bf16 runs (+3.3% step time,
+                       profiles/r04/slab_wfirst_ab.txt)
+      kernel_policy    include/vqx.h VQX_POLICY_* of every conv GEMM call"""
+    fuse_gn: bool = True
+    enc_gn_finalize: bool = False
+    side_stream: bool = False
+    wgrad_wgs: int = 256
+    wgrad_wgs_1x1: int = 512
+    wgrad_wgs_solo: int = 512
+    wgrad_min_k: int = 512
+    slab_f32: bool = False
+    kernel_policy: int = 0
+
+
 class _Stage:
     """Per-stage activation buffers of a Workspace."""
 
@@ -139,7 +168,7 @@ class Workspace:
         self.B, self.T, self.N = B, T, B * T
         e = lambda *s, dt=cd: torch.empty(*s, device=dev, dtype=dt)  # noqa: E731
         Z, S, Fo, mel, K = d["Z"], d["S"], d["F"], d["mel"], d["K"]
-        fuse_env = os.environ.get("VQX_FUSE_GN", "1") != "0"
+        fuse_opt = eng.opt.fuse_gn
         self.x = e(self.N, mel)
         # ---- encoder stages
         self.enc = []
@@ -156,7 +185,7 @@ class Workspace:
             sw.h = [[e(N, C) for _ in range(st.L)] for _ in range(nb)]
             sw.g = [[e(N, C) for _ in range(st.L - 1)] for _ in range(nb)]  # LeakyReLU(GN(h)) of inner layers
             sw.mr = [[e(B, 2, dt=F32) for _ in range(st.L)] for _ in range(nb)]
-            sw.fuse = Tc % 128 == 0 and C % 128 == 0 and fuse_env
+            sw.fuse = Tc % 128 == 0 and C % 128 == 0 and fuse_opt
             if train:
                 # colsum partials of dL/dc_j (the producing dgrad's COLSUM epilogue)
                 sw.cs = [e(_tm(N), C, dt=F32) for _ in range(nb + 1)]
@@ -197,7 +226,7 @@ class Workspace:
             sw.g = [e(N, C) for _ in range(nb)]
             sw.mr = [e(B, 4, dt=F32) for _ in range(nb)]
             sw.condbias = [e(B, 2 * C, dt=F32) for _ in range(nb)]
-            sw.fuse = Td % 128 == 0 and C % 128 == 0 and fuse_env
+            sw.fuse = Td % 128 == 0 and C % 128 == 0 and fuse_opt
             if train:
                 sw.dr = [e(N, C + S) for _ in range(2)] if nb else None   # [dL/dx | dL/dskip] ping-pong
                 sw.dx = e(N, C) if not nb else None                        # stages without blocks
@@ -244,7 +273,6 @@ class Workspace:
         self.dc_flat = [e(NCe) for _ in range(2)]   # encoder dL/dc ping-pong (viewed per stage)
         self.dh_flat = e(NCe)
         self.dy_flat = e(NCe)                       # inner-layer gradients (stack_layers > 1)
-        self.tmp_flat = e(NCe)
         self.dyemb = e(B, d["ydim"], dt=F32)
         self.cs_part = e(64 * max(Cmax, S + Cmax, mel, 1024), dt=F32)
         self.cs_skip = e(_tm(self.Nskip), S, dt=F32)  # dL/dskip
@@ -260,8 +288,9 @@ class Workspace:
 
 
 class VQVAEEngine:
-    def __init__(self, model, device, compute_dtype="fp32"):
+    def __init__(self, model, device, compute_dtype="fp32", options=None):
         self.m = model
+        self.opt = options if options is not None else EngineOptions()
         self.device = torch.device(device)
         self.cd = torch.bfloat16 if compute_dtype in ("bf16", "bfloat16") else F32
         self.dt = ops.dt_code(self.cd)
@@ -279,14 +308,14 @@ class VQVAEEngine:
         self._build_layers()
         self._ws = {}
         self.opt_ready = False
-        self._enc_gn_separate = os.environ.get("VQX_ENC_GN_FINALIZE") == "1"
+        self._enc_gn_separate = self.opt.enc_gn_finalize
         # optional side stream for the latency-bound work off the GEMM chain: the
         # speaker conditioning linears (needed only by the decoder) and the EMA
         # codebook statistics + update (needed only by the next step).  Measured
         # 0.5-0.8% slower end to end (profiles/r02/side_stream_ab.txt: the small
         # kernels squeeze into the GEMMs' single round of workgroups), so off by
-        # default; env VQX_SIDE_STREAM=1 turns it on
-        self._side_on = self.device.type == "cuda" and os.environ.get("VQX_SIDE_STREAM", "0") == "1"
+        # default (EngineOptions.side_stream)
+        self._side_on = self.device.type == "cuda" and self.opt.side_stream
         self._side = None
 
     # ------------------------------------------------------------ parameters
@@ -473,11 +502,10 @@ class VQVAEEngine:
         # workgroups for the 3-tap layers (dec conv_in 4 splits, enc k3 8) beat
         # 512: 5.43 vs 5.53 ms per step; 1x1 layers stay at 512, and so do the
         # stage convolutions, whose WGRAD runs alone (no DGRAD beside it).
-        wg_target = int(os.environ.get("VQX_WGRAD_WGS", "256"))  # A/B knobs: workgroups per wgrad launch
-        wg_1x1 = int(os.environ.get("VQX_WGRAD_WGS_1X1", "512"))  # ... for the 1x1 layers
-        wg_solo = int(os.environ.get("VQX_WGRAD_WGS_SOLO", "512"))  # ... for the stage convs (WGRAD alone)
+        o = self.opt  # workgroups per wgrad launch of the 3-tap / 1x1 layers / stage convs (WGRAD alone)
+        wg_target, wg_1x1, wg_solo = o.wgrad_wgs, o.wgrad_wgs_1x1, o.wgrad_wgs_solo
         solo = {id(st.conv) for st in self.enc_stages} | {id(st.conv) for st in self.dec_stages}
-        min_k = int(os.environ.get("VQX_WGRAD_MIN_K", "512"))  # frames per split at least (256: +0.4%, 1024: +1.9%)
+        min_k = o.wgrad_min_k  # frames per split at least (256: +0.4%, 1024: +1.9%)
         B_ref, T_ref = 64, 256
         rate = {}
         Tc = T_ref
@@ -516,7 +544,7 @@ class VQVAEEngine:
         # once, summed in fp32 by the weight-norm backward): half the bytes of the
         # split-K round trip.  The conditioning linears write dW directly (fp32).
         groups = self._bwd_groups()
-        bf_slabs = self.dt == L.VQX_BF16 and os.environ.get("VQX_SLAB_F32") != "1"  # env: fp32 slabs (A/B)
+        bf_slabs = self.dt == L.VQX_BF16 and not self.opt.slab_f32
         sdt = {id(Lr): (torch.bfloat16 if bf_slabs and Lr not in self.dec_cond else F32)
                for grp in groups for Lr in grp}
 
@@ -662,6 +690,7 @@ class VQVAEEngine:
     # ------------------------------------------------------------ conv helpers
     def fwd(self, Lr, x, y, T, **kw):
         """y = conv(x); T = frames per utterance of the input x."""
+        kw["policy"] = self.opt.kernel_policy
         if Lr.kind in (KIND_CONV, KIND_CONVT):
             ops.conv_fwd(x, Lr.wp, y, T=T, cin=Lr.cin, cout=Lr.cout, ntaps=Lr.k, pad=Lr.pad, dil=Lr.dil, **kw)
         elif Lr.kind == KIND_DOWN:
@@ -677,6 +706,7 @@ class VQVAEEngine:
 
     def dgrad(self, Lr, dy, dx, T, **kw):
         """dx = dL/d(input) from dy = dL/d(output); T = frames per utterance of dy."""
+        kw["policy"] = self.opt.kernel_policy
         if Lr.kind in (KIND_CONV, KIND_CONVT):
             ops.conv_dgrad(dy, Lr.wp, dx, T=T, cin=Lr.cout, cout=Lr.cin, ntaps=Lr.k,
                            pad=(Lr.k - 1) * Lr.dil - Lr.pad, dil=Lr.dil, **kw)
@@ -693,22 +723,23 @@ class VQVAEEngine:
 
     def wgrad(self, Lr, dy, x, T, pro=L.PRO_NONE, scale=1.0):
         """Weight-gradient slabs from dy (output gradient, T frames per utterance) and the input x."""
+        pol = self.opt.kernel_policy
         if Lr.kind == KIND_CONV:
             ops.conv_wgrad(dy, x, Lr.slab, T=T, r_dim=Lr.cout, c_dim=Lr.cin, ntaps=Lr.k, pad=Lr.pad, dil=Lr.dil,
-                           shift_sign=1, q_prologue=pro, pro_scale=scale, splits=Lr.splits)
+                           shift_sign=1, q_prologue=pro, pro_scale=scale, splits=Lr.splits, policy=pol)
             return
         assert pro == L.PRO_NONE
         if Lr.kind == KIND_CONVT:
             ops.conv_wgrad(x, dy, Lr.slab, T=T, r_dim=Lr.cin, c_dim=Lr.cout, ntaps=Lr.k, pad=Lr.pad, dil=Lr.dil,
-                           shift_sign=-1, splits=Lr.splits)
+                           shift_sign=-1, splits=Lr.splits, policy=pol)
         elif Lr.kind == KIND_DOWN:
             s = Lr.scale
             ops.conv_wgrad(dy, x.view(-1, s * Lr.cin), Lr.slab, T=T, r_dim=Lr.cout, c_dim=s * Lr.cin, ntaps=3, pad=1,
-                           shift_sign=1, splits=Lr.splits)
+                           shift_sign=1, splits=Lr.splits, policy=pol)
         else:
             s = Lr.scale
             ops.conv_wgrad(x, dy.view(-1, s * Lr.cout), Lr.slab, T=T // s, r_dim=Lr.cin, c_dim=s * Lr.cout, ntaps=3,
-                           pad=1, shift_sign=1, splits=Lr.splits)
+                           pad=1, shift_sign=1, splits=Lr.splits, policy=pol)
 
     def wgrad_dgrad(self, Lr, dy, x, dx, T, **kw):
         """self.wgrad(Lr, dy, x, T) then self.dgrad(Lr, dy, dx, T, **kw): for a plain
@@ -718,8 +749,10 @@ class VQVAEEngine:
             self.wgrad(Lr, dy, x, T)
             self.dgrad(Lr, dy, dx, T, **kw)
             return
-        dkw = dict(T=T, cin=Lr.cout, cout=Lr.cin, ntaps=Lr.k, pad=(Lr.k - 1) * Lr.dil - Lr.pad, dil=Lr.dil, **kw)
-        wkw = dict(T=T, ntaps=Lr.k, pad=Lr.pad, dil=Lr.dil, splits=Lr.splits)
+        pol = self.opt.kernel_policy
+        dkw = dict(T=T, cin=Lr.cout, cout=Lr.cin, ntaps=Lr.k, pad=(Lr.k - 1) * Lr.dil - Lr.pad, dil=Lr.dil, policy=pol,
+                   **kw)
+        wkw = dict(T=T, ntaps=Lr.k, pad=Lr.pad, dil=Lr.dil, splits=Lr.splits, policy=pol)
         if Lr.kind == KIND_CONV:  # as self.wgrad
             ops.conv_dgrad_wgrad(dy, Lr.wp, dx, dkw, dy, x, Lr.slab, dict(wkw, r_dim=Lr.cout, c_dim=Lr.cin, shift_sign=1))
         else:
@@ -935,7 +968,6 @@ class VQVAEEngine:
             st, sw = self.enc_stages[si], w.enc[si]
             T, N, C = sw.T, sw.N, sw.C
             dh = Workspace.view(w.dh_flat, N, C)
-            tmp = Workspace.view(w.tmp_flat, N, C)
             dy2 = Workspace.view(w.dy_flat, N, C)
             nb = len(st.blocks)
             # the producer of dL/dc_nb (output conv or next stage conv) fused GNBWD only when unfolded
@@ -947,6 +979,15 @@ class VQVAEEngine:
                 # cur = dL/dc_{j+1}, the gradient w.r.t. block j's output GN(h_L) + skip(c_j)
                 dy = cur
                 fused_here = top_fused if j == nb - 1 else True
+                # the skip conv first, with a plain epilogue: nxt = W_skip^T cur (+ dW_skip).  The
+                # stack's first conv then adds its masked data gradient to it in ITS epilogue, with
+                # the column sums and the previous block's GroupNorm-backward sums of the total: those
+                # HBM-bound epilogue reads run beside the 3-tap pair's long main loops instead of
+                # behind the 1x1 GEMM's short one
+                self.wgrad_dgrad(b.skip, cur, sw.c[j], nxt, T)
+                prod = dict(colsum=sw.cs[j])
+                if j > 0:
+                    prod.update(self._gnb(w, si, j - 1))
                 for l in reversed(range(st.L)):
                     Lr, gn = b.convs[l], b.gns[l]
                     cs_b = self._bview(w.colsum_b[l], B, C)
@@ -959,12 +1000,8 @@ class VQVAEEngine:
                     if l > 0:  # into LeakyReLU(GN(h_{l-1})): its derivative from the sign of the stored output
                         self.wgrad_dgrad(Lr, dh, src, dy2, T, mask=sw.g[j][l - 1], mask_slope=0.2)
                         dy = dy2
-                    else:
-                        self.wgrad_dgrad(Lr, dh, src, tmp, T, mask=sw.a[j], mask_slope=0.2)
-                prod = dict(colsum=sw.cs[j])
-                if j > 0:
-                    prod.update(self._gnb(w, si, j - 1))
-                self.wgrad_dgrad(b.skip, cur, sw.c[j], nxt, T, res=tmp, **prod)
+                    else:  # nxt += mask * W^T dh (read and written in place, element by element)
+                        self.wgrad_dgrad(Lr, dh, src, nxt, T, mask=sw.a[j], mask_slope=0.2, res=nxt, **prod)
                 # weight norms of the stack convs and skip + their biases and the GN affine
                 self._wn_bwd(w, b.key)
                 cur = nxt

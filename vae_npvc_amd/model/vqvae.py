@@ -15,7 +15,7 @@ import math
 import torch
 import torch.nn as nn
 
-from ..engine.step import VQVAEEngine
+from ..engine.step import EngineOptions, VQVAEEngine
 from .layers import Conditions, ResidualBlock, ResSkipBlock, WNConv1d
 from .resample import ResampleConv1d
 from .layers_vq import EMAVectorQuantizer, Jitter, VectorQuantizer
@@ -135,6 +135,8 @@ class Model(nn.Module):
         self.jitter = Jitter(probability=arch.get("jitter_p", 0.0))
         self.beta = arch.get("beta", 0.01)
         self.compute_dtype = arch.get("compute_dtype", "fp32")
+        # engine schedule options (engine/step.py EngineOptions; A/B runs only)
+        self.engine_options = EngineOptions(**arch.get("engine", {}))
         self._engine = None
 
     # ------------------------------------------------------------ engine
@@ -144,7 +146,7 @@ class Model(nn.Module):
             raise RuntimeError("vae_npvc_amd.Model runs only on the MI355X (HIP) path; move it with .cuda()")
         e = self._engine
         if e is None or e.device != dev or not e.params_intact():
-            e = self._engine = VQVAEEngine(self, dev, self.compute_dtype)
+            e = self._engine = VQVAEEngine(self, dev, self.compute_dtype, self.engine_options)
         return e
 
     # ------------------------------------------------------------ reference API

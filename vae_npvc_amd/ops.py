@@ -29,11 +29,41 @@ def _check_cuda(*ts):
             raise L.VqxError("libvqx ops need device tensors (the HIP kernels are the only implementation)")
 
 
+POLICY_AUTO, POLICY_IM2COL, POLICY_TALL256, POLICY_TALL512, POLICY_TR128 = 0, 1, 2, 3, 4  # include/vqx.h
+_policy = POLICY_AUTO
+
+
+def set_kernel_policy(policy):
+    """Policy for the conv GEMM calls that pass no `policy` (include/vqx.h
+    VQX_POLICY_*; for tests and A/B tools -- the library itself keeps no such
+    state: the policy travels in every call's arguments).  Returns the old one."""
+    global _policy
+    if policy not in (POLICY_AUTO, POLICY_IM2COL, POLICY_TALL256, POLICY_TALL512, POLICY_TR128):
+        raise ValueError(f"kernel policy {policy} not in 0..4")
+    prev, _policy = _policy, int(policy)
+    return prev
+
+
+class kernel_policy:
+    """with ops.kernel_policy(p): set_kernel_policy(p) for the block."""
+
+    def __init__(self, policy):
+        self.policy = policy
+
+    def __enter__(self):
+        self.prev = set_kernel_policy(self.policy)
+        return self
+
+    def __exit__(self, *exc):
+        set_kernel_policy(self.prev)
+        return False
+
+
 def conv_args(x, w, y, *, T, cin, cout, ntaps, pad, prologue=L.PRO_NONE, pro_scale=1.0, bias=None,
               rowbias=None, res=None, mask=None, mask_slope=0.0, mask_scale=1.0, gn_h=None, gn_mr=None,
               gn_gamma=None, gn_beta=None, out2=None, split_col=0, out2_accumulate=False, out_f32=False,
               act=None, y2=None, colsum=None, gn_stats=None, gn_bwd=None, gn_groups=1, gn_glu=False,
-              gn_tiles=None, gn_eps=1e-5, dil=1):
+              gn_tiles=None, gn_eps=1e-5, dil=1, policy=None):
     epi = 0
     if bias is not None:
         epi |= L.EPI_BIAS
@@ -64,6 +94,7 @@ def conv_args(x, w, y, *, T, cin, cout, ntaps, pad, prologue=L.PRO_NONE, pro_sca
     a.bias, a.rowbias, a.res, a.mask = ptr(bias), ptr(rowbias), ptr(res), ptr(mask)
     a.gn_h, a.gn_mean_rstd, a.gn_gamma, a.gn_beta, a.out2 = ptr(gn_h), ptr(gn_mr), ptr(gn_gamma), ptr(gn_beta), ptr(out2)
     a.n_rows, a.T, a.cin, a.cout, a.ntaps, a.pad, a.dil = x.shape[0], T, cin, cout, ntaps, pad, dil
+    a.kernel_policy = _policy if policy is None else policy
     a.ldx, a.ldy = x.stride(0), y.stride(0)
     a.ldres = res.stride(0) if res is not None else 0
     a.ldmask = mask.stride(0) if mask is not None else 0
@@ -192,8 +223,9 @@ def conv_dgrad(dy, w, dx, **kw):
 
 
 def wgrad_args(p, q, slabs, *, T, r_dim, c_dim, ntaps, pad, shift_sign=1, q_prologue=L.PRO_NONE, pro_scale=1.0,
-               splits=1, dil=1):
+               splits=1, dil=1, policy=None):
     a = L.WgradArgs()
+    a.kernel_policy = _policy if policy is None else policy
     a.p, a.q, a.slabs = ptr(p), ptr(q), ptr(slabs)
     a.n_rows, a.T, a.r_dim, a.c_dim, a.ntaps, a.pad, a.shift_sign = p.shape[0], T, r_dim, c_dim, ntaps, pad, shift_sign
     a.ldp, a.ldq = p.stride(0), q.stride(0)
