@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--reserve-cus", type=int, default=0,
                     help="run the step on a stream that leaves this many CUs idle (vqx_stream_create_cu_mask): "
                          "the cost of co-resident work such as RCCL's all-reduce kernels")
+    ap.add_argument("--grad-sync", default="overlap", choices=["overlap", "end"],
+                    help="N>1: gradient all-reduces beside the backward (default) or all after it")
     return ap.parse_args()
 
 
@@ -185,6 +187,7 @@ def main():
     cfg = yaml.safe_load(open(os.path.join(ROOT, "vae_npvc_amd", "conf", f"{a.config}.yaml")))
     cfg["compute_dtype"] = a.dtype
     cfg["batch_size"] = B_PER_GPU
+    cfg["grad_sync"] = a.grad_sync
     if os.environ.get("VQX_ENGINE"):  # A/B runs: engine schedule options as JSON (engine/step.py EngineOptions)
         cfg["engine"] = json.loads(os.environ["VQX_ENGINE"])
 
@@ -259,7 +262,8 @@ def main():
         # (Comm.finish) and the EMA-statistics all-reduce (codebook update)
         comm_out = {"bytes_per_step": round(allr[0][0]), "collectives_per_step": allr[0][1],
                     "grad_wait_ms": [round(r[2], 4) for r in allr], "ema_wait_ms": [round(r[3], 4) for r in allr],
-                    "bucket_bytes": comm.bucket * 4, "backend": comm.backend}
+                    "bucket_bytes": comm.bucket * 4, "backend": comm.backend,
+                    "grad_sync": "overlap" if comm.overlap else "end"}
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

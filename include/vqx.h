@@ -516,8 +516,8 @@ int vqx_probe_count(int64_t* n);
 int vqx_probe_read(int64_t i, int32_t* info5, double* flops, float* ms);
 
 /* A stream on all but `reserve_cus` of the current device's CUs
- * (hipExtStreamCreateWithCUMask; reserved CUs spread evenly over the CU
- * indices), for measuring what co-resident work such as RCCL's all-reduce
+ * (hipExtStreamCreateWithCUMask; mask bit i is CU i / 8 of XCD i % 8, so
+ * the top `reserve_cus` bits are cleared: reserve_cus / 8 per XCD), for measuring what co-resident work such as RCCL's all-reduce
  * kernels costs the step (bench.py --reserve-cus).  *cus_used = the CUs the
  * stream may use.  No reference counterpart (measurement only). */
 int vqx_stream_create_cu_mask(int32_t reserve_cus, vqx_stream_t* out, int32_t* cus_used);

@@ -65,7 +65,16 @@ def _comm_worker(rank, port, q):
         ok_stats = (nbytes, calls, grad_ms, ema_ms) == (1003 * 4, 18, 0, 0)
         comm.reset_stats()
         ok_stats = ok_stats and comm.stats() == (0, 0, 0, 0)
-        q.put((rank, torch.equal(flat, want) and ok_stats, s.tolist(), m.item()))
+        # grad_sync "end": runs held until finish(), adjacent ones merged (here out of
+        # order: 600-1000 then 0-600 -> one 1000-float run = 16 buckets), same values
+        late = Comm(bucket_bytes=64 * 4, overlap=False)
+        flat2 = torch.arange(1000, dtype=torch.float32) * (rank + 1)
+        late.grads_ready(flat2, 600, 1000)
+        late.grads_ready(flat2, 0, 600)
+        ok_late = late.stats()[1] == 0 and torch.equal(flat2, torch.arange(1000, dtype=torch.float32) * (rank + 1))
+        late.finish()
+        ok_late = ok_late and torch.equal(flat2, want) and late.stats()[:2] == (1000 * 4, 16) and not late.held
+        q.put((rank, torch.equal(flat, want) and ok_stats and ok_late, s.tolist(), m.item()))
         dist.destroy_process_group()
     except Exception as e:  # surface the failure to the parent
         q.put((rank, repr(e), None, None))

@@ -554,8 +554,7 @@ def test_gnbwd_epilogue_matches_standalone(glu, tile):
         assert relerr(a, b) < 2e-2, relerr(a, b)
 
 
-@pytest.mark.parametrize("case", ["k1_glu", "k1_res", "k1_plain", "tr_mask", "tr_convt", "gen", "tr_full", "k1_full",
-                                  "tr_gnbwd", "tr_gnbwd_full"])
+@pytest.mark.parametrize("case", ["k1_glu", "k1_res", "k1_plain", "tr_mask", "tr_convt", "gen", "tr_full", "k1_full"])
 def test_fused_dgrad_wgrad_equals_separate_launches(case):
     """vqx_conv1d_dgrad_wgrad (vqx_gemm_dual.hip: one launch interleaving a
     layer's data- and weight-gradient GEMMs) against vqx_conv1d_wgrad +
@@ -566,10 +565,7 @@ def test_fused_dgrad_wgrad_equals_separate_launches(case):
     default in-sequence, the interleaved and the three-per-CU form), the
     3-tap tap-reuse pair
     with the activation-derivative mask, the ConvTranspose form (shift -1,
-    residual + column sums), the encoder's first stack conv (mask, residual
-    = the skip conv's data gradient, column sums and the previous block's
-    GroupNorm-backward sums; engine/step.py encoder_bwd), and an im2col-only
-    layer (cin 80: two launches);
+    residual + column sums), and an im2col-only layer (cin 80: two launches);
     *_full at the bench size (64 x 256 frames: 512 + 512 workgroups, so the
     256-block interleaved groups are exercised)."""
     ops = _ops()
@@ -580,8 +576,7 @@ def test_fused_dgrad_wgrad_equals_separate_launches(case):
     N = B * T
     k = 3 if case.startswith("tr") else 1
     cfg = {"k1_glu": (640, 512), "k1_res": (512, 512), "k1_plain": (512, 768), "tr_mask": (1024, 512),
-           "tr_convt": (512, 1024), "gen": (80, 512), "tr_full": (1024, 512), "k1_full": (512, 512),
-           "tr_gnbwd": (512, 512), "tr_gnbwd_full": (512, 512)}[case]
+           "tr_convt": (512, 1024), "gen": (80, 512), "tr_full": (1024, 512), "k1_full": (512, 512)}[case]
     co, ci = cfg                                   # forward layer cout, cin
     dy = torch.randn(N, co, device=DEV).to(dt)
     x = torch.randn(N, ci, device=DEV).to(dt)
@@ -608,13 +603,6 @@ def test_fused_dgrad_wgrad_equals_separate_launches(case):
                      res=torch.randn(N, ci, device=DEV).to(dt))
     elif case in ("tr_mask", "tr_full"):
         extra = dict(mask=torch.randn(N, ci, device=DEV).to(dt), mask_slope=0.2)
-    elif case.startswith("tr_gnbwd"):
-        u = torch.randn(N, ci, device=DEV).to(dt)
-        mr = torch.empty(B, 1, 2, device=DEV)
-        ops.groupnorm_stats(u, T, 1, torch.empty(B * 24, device=DEV), mr)
-        extra = dict(mask=torch.randn(N, ci, device=DEV).to(dt), mask_slope=0.2, gn_h=u, gn_mr=mr,
-                     gn_gamma=torch.randn(ci, device=DEV), gn_beta=torch.randn(ci, device=DEV),
-                     res=torch.randn(N, ci, device=DEV).to(dt))
     elif case == "tr_convt":
         extra = dict(res=torch.randn(N, ci, device=DEV).to(dt))
     outs = []
@@ -623,10 +611,10 @@ def test_fused_dgrad_wgrad_equals_separate_launches(case):
         o = {"dx": torch.full((N, ci), float("nan"), device=DEV, dtype=dt),
              "slabs": torch.full(slab_shape, float("nan"), device=DEV, dtype=dt)}
         kw = dict(extra)
-        if case in ("k1_glu", "k1_res") or case.startswith("tr_gnbwd"):
+        if case in ("k1_glu", "k1_res"):
             o["gnb"] = torch.full((N // 128 * (ci // 128) * 4,), float("nan"), device=DEV)
             kw["gn_bwd"] = o["gnb"]
-        if case in ("k1_res", "tr_convt") or case.startswith("tr_gnbwd"):
+        if case in ("k1_res", "tr_convt"):
             o["cs"] = torch.full((N // 128, ci), float("nan"), device=DEV)
             kw["colsum"] = o["cs"]
         if fused_call[0]:

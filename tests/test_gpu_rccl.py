@@ -78,12 +78,12 @@ def _worker(port, q):
         meta, _ = load_fixture("step_vcc20")
         cfg = cfg_of("vcc20", compute_dtype="fp32")
         runs = []
-        for ddp in (False, True):
+        for ddp in (False, True, "end"):  # plain, all-reduce beside the backward, all after it
             tr = make_trainer(cfg, meta["wseed"])
             eng = tr.engine
             calls = []
             if ddp:
-                c2 = Comm()
+                c2 = Comm(overlap=ddp is True)
                 real = c2.grads_ready
 
                 def rec(flat_, lo, hi, _real=real):
@@ -124,13 +124,14 @@ def test_rccl_world1_comm_and_engine_step():
     assert out["avg_exact"] and out["gather_exact"]
     assert out["mean"] == [2.5, -1.0]
     assert out["sum"] == [7.0] * 7
-    plain, ddp = out["engine"]
-    assert ddp["p"] == plain["p"] and ddp["e"] == plain["e"]      # bit-identical weights and codebook
-    assert ddp["d"] == plain["d"]                                  # identical loss dicts
-    for calls in ddp["calls"]:                                     # every gradient reduced exactly once per step
-        covered = 0
-        for (lo, hi), nxt in zip(calls, calls[1:] + [(ddp["n"], None)]):
-            assert lo < hi <= nxt[0]
-            covered += hi - lo
-        assert covered == ddp["n"]
+    plain, ddp, late = out["engine"]
+    for d in (ddp, late):
+        assert d["p"] == plain["p"] and d["e"] == plain["e"]       # bit-identical weights and codebook
+        assert d["d"] == plain["d"]                                # identical loss dicts
+        for calls in d["calls"]:                                   # every gradient reduced exactly once per step
+            covered = 0
+            for (lo, hi), nxt in zip(calls, calls[1:] + [(d["n"], None)]):
+                assert lo < hi <= nxt[0]
+                covered += hi - lo
+            assert covered == d["n"]
     assert len(ddp["calls"][0]) > 3                                # reduced in several runs during the backward

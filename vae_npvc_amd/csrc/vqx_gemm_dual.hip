@@ -74,7 +74,6 @@ bool launch_dual(const GemmParams& PD, int nd, const GemmParams& PW, int nw, hip
       case EK_NONE: fn = (const void*)dual_tr_kernel<EK_NONE>; break;
       case EK_ELEM: fn = (const void*)dual_tr_kernel<EK_ELEM>; break;
       case EK_COLSUM: fn = (const void*)dual_tr_kernel<EK_COLSUM>; break;
-      case EK_GNBWD: fn = (const void*)dual_tr_kernel<EK_GNBWD>; break;
       default: return false;
     }
   } else if (PD.ntaps == 1 && PW.ntaps == 1 && PW.tap_reuse == 0 && nd % 8 == 0) {

@@ -331,10 +331,20 @@ __device__ __forceinline__ EpiOps epi_ops(const EpiRows* R) {
 // pass when the epilogue prefetches (PRE).
 struct EpiVec {
   float b[8], ga[8], be[8], gb[8], bb[8];
+  float mr[4];  // GNBWD: the tile's utterance's (mean, rstd) pairs, valid when mr_ok
+  bool mr_ok;
 };
 template <int EMASK>
-__device__ __forceinline__ void epi_vec_load(const GemmParams& P, int col, EpiVec& V) {
+__device__ __forceinline__ void epi_vec_load(const GemmParams& P, int col, EpiVec& V, int m0 = 0) {
   const int epi = P.epi & EMASK;
+  V.mr_ok = false;
+  if ((epi & VQX_EPI_GNBWD) && P.T % 128 == 0 && (P.gn_glu || P.gn_groups == 1)) {
+    // every row of a 128-row tile lies in utterance m0 / T: one load per tile
+    const int b = m0 / P.T, n = P.gn_glu ? 4 : 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) V.mr[i] = i < n ? P.gn_mr[b * n + i] : 0.f;
+    V.mr_ok = true;
+  }
   if (col >= P.Nc) return;
   if (epi & VQX_EPI_BIAS) ld8<float>(P.bias, col, V.b);
   if (epi & (VQX_EPI_GNADD | VQX_EPI_GNBWD)) {
@@ -444,9 +454,11 @@ __device__ __forceinline__ void gnbwd8(const GemmParams& P, int64_t row, int col
   float ua[8], ga[8];
   row_op<T>(o, EPR_GNH, P.gn_h, row * P.ldgn + col, ua);
   vec8<PRE>(V.ga, P.gn_gamma, col, ga);
+  const bool mr_pre = PRE && V.mr_ok;  // the tile's utterance's (mean, rstd), loaded once per tile
   if (!P.gn_glu) {
     const int grp = P.gn_groups == 1 ? 0 : col / (P.Nc / P.gn_groups);
-    const float m = P.gn_mr[(b * P.gn_groups + grp) * 2], r = P.gn_mr[(b * P.gn_groups + grp) * 2 + 1];
+    const float m = mr_pre ? V.mr[0] : P.gn_mr[(b * P.gn_groups + grp) * 2];
+    const float r = mr_pre ? V.mr[1] : P.gn_mr[(b * P.gn_groups + grp) * 2 + 1];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const float g = ga[e] * dy[e];
@@ -461,7 +473,8 @@ __device__ __forceinline__ void gnbwd8(const GemmParams& P, int64_t row, int col
   vec8<PRE>(V.gb, P.gn_gamma, col + half, gb);
   vec8<PRE>(V.be, P.gn_beta, col, ba);
   vec8<PRE>(V.bb, P.gn_beta, col + half, bb);
-  const float ma = P.gn_mr[b * 4], ra = P.gn_mr[b * 4 + 1], mb = P.gn_mr[b * 4 + 2], rb = P.gn_mr[b * 4 + 3];
+  const float ma = mr_pre ? V.mr[0] : P.gn_mr[b * 4], ra = mr_pre ? V.mr[1] : P.gn_mr[b * 4 + 1];
+  const float mb = mr_pre ? V.mr[2] : P.gn_mr[b * 4 + 2], rb = mr_pre ? V.mr[3] : P.gn_mr[b * 4 + 3];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const float xa = (ua[e] - ma) * ra, xb = (ub[e] - mb) * rb;
@@ -567,7 +580,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
   float mn = 0.f, mm = 0.f, mq = 0.f;                       // GNSTATS running (count, mean, M2)
   float gs[4] = {0.f, 0.f, 0.f, 0.f};                       // GNBWD sums
   EpiVec V;
-  if constexpr (PREVEC && MODE != MODE_WGRAD) epi_vec_load<EMASK>(P, n0 + ec, V);
+  if constexpr (PREVEC && MODE != MODE_WGRAD) epi_vec_load<EMASK>(P, n0 + ec, V, m0);
   __syncthreads();  // staging buffers are free
   // slab and pass are compile-time constants (static_for), so the prefetched
   // row operands R->r*[slab*4 + pass] are register-resident

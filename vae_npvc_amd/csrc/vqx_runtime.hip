@@ -33,8 +33,10 @@ extern "C" int vqx_version(void) { return VQX_ABI_VERSION; }
 // A compute stream restricted to all but `reserve_cus` of the device's CUs
 // (hipExtStreamCreateWithCUMask), for measuring what co-resident work (RCCL's
 // all-reduce kernels under data parallelism) costs the step: bench.py
-// --reserve-cus wraps it as a torch ExternalStream.  The reserved CUs are
-// spread evenly over the CU index space.
+// --reserve-cus wraps it as a torch ExternalStream.  Mask bit i is CU i / 8 of
+// XCD i % 8 (measured with tools/lab/cu_map.cpp, profiles/r04/cu_reserve.txt;
+// a mask that leaves an XCD no CU is ignored by the runtime), so clearing the
+// top `reserve_cus` bits takes reserve_cus / 8 CUs from every XCD.
 extern "C" int vqx_stream_create_cu_mask(int32_t reserve_cus, vqx_stream_t* out, int32_t* cus_used) {
   if (!out) { vqx::set_error("vqx_stream_create_cu_mask: null stream pointer"); return -1; }
   int dev = 0, n = 0;
@@ -48,8 +50,8 @@ extern "C" int vqx_stream_create_cu_mask(int32_t reserve_cus, vqx_stream_t* out,
   }
   std::vector<uint32_t> mask((n + 31) / 32, 0u);
   for (int i = 0; i < n; ++i) mask[i / 32] |= 1u << (i % 32);
-  for (int k = 0; k < reserve_cus; ++k) {  // evenly spaced indices
-    const int i = (int)(((int64_t)k * n) / reserve_cus);
+  for (int k = 0; k < reserve_cus; ++k) {  // the top bits: even over the XCDs
+    const int i = n - 1 - k;
     mask[i / 32] &= ~(1u << (i % 32));
   }
   hipStream_t s = nullptr;

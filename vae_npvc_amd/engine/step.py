@@ -273,6 +273,7 @@ class Workspace:
         self.dc_flat = [e(NCe) for _ in range(2)]   # encoder dL/dc ping-pong (viewed per stage)
         self.dh_flat = e(NCe)
         self.dy_flat = e(NCe)                       # inner-layer gradients (stack_layers > 1)
+        self.tmp_flat = e(NCe)
         self.dyemb = e(B, d["ydim"], dt=F32)
         self.cs_part = e(64 * max(Cmax, S + Cmax, mel, 1024), dt=F32)
         self.cs_skip = e(_tm(self.Nskip), S, dt=F32)  # dL/dskip
@@ -968,6 +969,7 @@ class VQVAEEngine:
             st, sw = self.enc_stages[si], w.enc[si]
             T, N, C = sw.T, sw.N, sw.C
             dh = Workspace.view(w.dh_flat, N, C)
+            tmp = Workspace.view(w.tmp_flat, N, C)
             dy2 = Workspace.view(w.dy_flat, N, C)
             nb = len(st.blocks)
             # the producer of dL/dc_nb (output conv or next stage conv) fused GNBWD only when unfolded
@@ -979,15 +981,6 @@ class VQVAEEngine:
                 # cur = dL/dc_{j+1}, the gradient w.r.t. block j's output GN(h_L) + skip(c_j)
                 dy = cur
                 fused_here = top_fused if j == nb - 1 else True
-                # the skip conv first, with a plain epilogue: nxt = W_skip^T cur (+ dW_skip).  The
-                # stack's first conv then adds its masked data gradient to it in ITS epilogue, with
-                # the column sums and the previous block's GroupNorm-backward sums of the total: those
-                # HBM-bound epilogue reads run beside the 3-tap pair's long main loops instead of
-                # behind the 1x1 GEMM's short one
-                self.wgrad_dgrad(b.skip, cur, sw.c[j], nxt, T)
-                prod = dict(colsum=sw.cs[j])
-                if j > 0:
-                    prod.update(self._gnb(w, si, j - 1))
                 for l in reversed(range(st.L)):
                     Lr, gn = b.convs[l], b.gns[l]
                     cs_b = self._bview(w.colsum_b[l], B, C)
@@ -1000,8 +993,17 @@ class VQVAEEngine:
                     if l > 0:  # into LeakyReLU(GN(h_{l-1})): its derivative from the sign of the stored output
                         self.wgrad_dgrad(Lr, dh, src, dy2, T, mask=sw.g[j][l - 1], mask_slope=0.2)
                         dy = dy2
-                    else:  # nxt += mask * W^T dh (read and written in place, element by element)
-                        self.wgrad_dgrad(Lr, dh, src, nxt, T, mask=sw.a[j], mask_slope=0.2, res=nxt, **prod)
+                    else:
+                        self.wgrad_dgrad(Lr, dh, src, tmp, T, mask=sw.a[j], mask_slope=0.2)
+                # the skip conv last, adding the stack's data gradient with the column sums and the
+                # previous block's GroupNorm-backward sums in its epilogue.  (Round 4: the skip conv
+                # first with a plain epilogue and those reads in the 3-tap DGRAD's epilogue instead
+                # measured +10 us per block: the 3-tap DGRAD runs two rounds of workgroups and pays
+                # the epilogue twice, profiles/r04/enc_bwd_order.txt.)
+                prod = dict(colsum=sw.cs[j])
+                if j > 0:
+                    prod.update(self._gnb(w, si, j - 1))
+                self.wgrad_dgrad(b.skip, cur, sw.c[j], nxt, T, res=tmp, **prod)
                 # weight norms of the stack convs and skip + their biases and the GN affine
                 self._wn_bwd(w, b.key)
                 cur = nxt
@@ -1062,11 +1064,10 @@ class VQVAEEngine:
                 ci, gn, rs = b.conv_in, b.gn, b.rs
                 nxt = sw.dr[k ^ 1]
                 # cur = [dL/dx_{j+1} | dL/dskip]
-                if sw.fuse:  # GLU + GroupNorm backward sums from the res/skip dgrad's epilogue
-                    self.wgrad_dgrad(rs, cur, sw.g[j], dg, T, gn_bwd=w.gnb_part, gn_h=sw.u[j], gn_mr=sw.mr[j],
-                                     gn_gamma=gn.weight, gn_beta=gn.bias, gn_groups=2, gn_glu=True)
-                else:
-                    self.wgrad_dgrad(rs, cur, sw.g[j], dg, T)
+                # (sw.fuse: GLU + GroupNorm backward sums from the res/skip dgrad's epilogue)
+                gkw = dict(gn_bwd=w.gnb_part, gn_h=sw.u[j], gn_mr=sw.mr[j], gn_gamma=gn.weight, gn_beta=gn.bias,
+                           gn_groups=2, gn_glu=True) if sw.fuse else {}
+                self.wgrad_dgrad(rs, cur, sw.g[j], dg, T, **gkw)
                 ops.gn_bwd(dg, sw.u[j], du, T, 2, True, sw.mr[j], gn.weight, gn.bias, w.gnb_part, sw.cs_all[j],
                            dg_b, db_b, nparts=self._gnb_parts(sw, C))
                 self.wgrad_dgrad(ci, du, sw.xs[j], nxt[:, :C], T, res=cur[:, :C], colsum=sw.cs[j])

@@ -19,6 +19,13 @@ Per step:
     rank draws the same CPU randperm(N_global); each fills the rows it owns,
     so the sum assembles exactly the global batch's z[perm[:K]].
 No other collective sits on the data path.
+
+Comm(overlap=False) (config `grad_sync: end`, bench.py --grad-sync end) holds
+the gradient runs back and issues them all in finish(), after the backward:
+RCCL's device kernel (248-256 VGPRs on gfx950) takes a GEMM workgroup slot on
+every CU it occupies, and the one-round GEMM grids lose 20-25% while it is
+resident (profiles/r04/cu_reserve.txt), so the switch trades that for the
+all-reduce's own time on the critical path.
 """
 import torch
 import torch.distributed as dist
@@ -35,8 +42,10 @@ def owned_rows(perm, rank_offset, n_local):
 
 
 class Comm:
-    def __init__(self, group=None, bucket_bytes=BUCKET_BYTES):
+    def __init__(self, group=None, bucket_bytes=BUCKET_BYTES, overlap=True):
         self.group = group
+        self.overlap = overlap  # False: gradient runs all-reduced in finish(), after the backward
+        self.held = []          # (lo, hi) runs held back when not overlapping
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.backend = dist.get_backend(group)
@@ -92,7 +101,14 @@ class Comm:
         return torch.cat(parts).to(t.device)
 
     def grads_ready(self, flat, lo, hi):
-        """Launch async mean all-reduces over flat[lo:hi] in buckets."""
+        """Launch async mean all-reduces over flat[lo:hi] in buckets (held
+        until finish() when not overlapping)."""
+        if not self.overlap:
+            self.held.append((flat, lo, hi))
+            return
+        self._launch(flat, lo, hi)
+
+    def _launch(self, flat, lo, hi):
         op = self._avg_op()
         for s in range(lo, hi, self.bucket):
             view = flat[s: min(hi, s + self.bucket)]
@@ -101,7 +117,19 @@ class Comm:
             self.pending.append((work, view))
 
     def finish(self):
-        """Make the current stream wait for every launched reduce."""
+        """Make the current stream wait for every launched reduce (first
+        launching the held runs, adjacent ones merged, when not overlapping)."""
+        if self.held:
+            runs = sorted(self.held, key=lambda r: r[1])
+            self.held = []
+            flat, lo, hi = runs[0]
+            for f, a, b in runs[1:]:
+                if f is flat and a == hi:
+                    hi = b
+                    continue
+                self._launch(flat, lo, hi)
+                flat, lo, hi = f, a, b
+            self._launch(flat, lo, hi)
         timed = self.timing and self.backend == "nccl" and self.pending
         if timed:  # one event pair around all the waits: the stream's total stall
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -112,6 +112,10 @@ class Trainer(object):
         lr_sched = config.get("lr_scheduler", None)
         lr_param = config.get("lr_param", {"step_size": 100000, "gamma": 0.5, "last_epoch": -1})
         self.scheduler_cfg = lr_param if lr_sched is not None else None
+        # gradient all-reduce beside the backward ("overlap") or after it ("end"); parallel/ddp.py
+        self.grad_sync = str(config.get("grad_sync", "overlap"))
+        if self.grad_sync not in ("overlap", "end"):
+            raise ValueError(f"grad_sync must be 'overlap' or 'end', not {self.grad_sync!r}")
 
         module = import_module(model_type[0], package=None)
         model_name = "Model" if len(model_type) < 2 else model_type[1]
@@ -130,7 +134,7 @@ class Trainer(object):
         self.engine = self.model.engine(self.device)
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             from ..parallel.ddp import Comm
-            self.engine.attach_comm(Comm())
+            self.engine.attach_comm(Comm(overlap=self.grad_sync == "overlap"))
             dist.broadcast(self.engine.flat_p, 0)
             for b in self.model.buffers():
                 dist.broadcast(b, 0)
