@@ -231,10 +231,10 @@ def test_bf16_bench_step_tracks_fp32_at_full_size():
     of the same engine on the same weights and batch (itself pinned to the
     reference's full-size run, test_fp32_full_size_step_matches_reference_golden):
     reconstruction loss within 1e-3, commitment loss within 2e-2, codebook
-    indices equal on >= 95% of frames (measured 96.3%: at step 1 the codebook
+    indices equal on >= 95% of frames (measured 96.4%: at step 1 the codebook
     is 512 of the batch's own encoder frames, so the ~0.5% bf16 difference of
     the encoder output flips near-ties), and per-parameter gradient norms
-    within 1e-2 median / 5e-2 worst (measured 2.2e-3 / 9.8e-3)."""
+    within 5e-3 median / 2e-2 worst (measured 6.3e-4 / 5.2e-3, round 4)."""
     from oracle.vqvae_cpu import seeded_batch
     from vae_npvc_amd import ops
     B, T = 64, 256
@@ -270,4 +270,49 @@ def test_bf16_bench_step_tracks_fp32_at_full_size():
     med, worst = errs[len(errs) // 2], errs[-1]
     print(f"full-size bf16 vs fp32: idx equal {same:.4f}; grad-norm rel err median {med:.3g} worst {worst:.3g}")
     assert same >= 0.95, same
-    assert med <= 1e-2 and worst <= 5e-2, (med, worst)
+    assert med <= 5e-3 and worst <= 2e-2, (med, worst)
+
+
+def test_bf16_split_k_slab_rounding_at_full_size():
+    """What the bf16 split-K slabs cost the bf16 step's weight gradients
+    (engine/step.py: each split's fp32 partial of a weight gradient rounded to
+    bf16 before the weight-norm backward sums the splits in fp32), at the bench
+    configuration (vcc20, 64 x 256 frames).  The same batch and weights run as
+    the fp32 step (the reference-pinned path), the bf16 step with bf16 slabs
+    (the default) and the bf16 step with fp32 slabs (EngineOptions.slab_f32).
+    Per parameter the relative error ||g - g_fp32|| / ||g_fp32|| of the whole
+    gradient tensor: the slabs' rounding must stay small against the error the
+    bf16 operands already carry (fp32 slabs), median and worst."""
+    from oracle.vqvae_cpu import seeded_batch
+    B, T = 64, 256
+    grads = {}
+    for tag, dt, eng in (("fp32", "fp32", {}), ("bf16", "bf16", {}), ("bf16_f32slab", "bf16", {"slab_f32": True})):
+        cfg = cfg_of("vcc20", compute_dtype=dt)
+        if eng:
+            cfg["engine"] = eng
+        tr = make_trainer(cfg, 31)
+        x, y = seeded_batch(cfg, B, T, 41)
+        torch.manual_seed(7)
+        np.random.seed(7)
+        tr.train_step((x.cuda(), y.cuda()))
+        grads[tag] = {n: tr.engine.g(p).detach().double().cpu() for n, p in tr.model.named_parameters()}
+        del tr
+        torch.cuda.empty_cache()
+    ref = grads["fp32"]
+    stats = {}
+    for tag in ("bf16", "bf16_f32slab"):
+        e = sorted(float((grads[tag][n] - g).norm() / g.norm()) for n, g in ref.items() if float(g.norm()) > 0)
+        stats[tag] = (e[len(e) // 2], e[-1])
+    (m16, w16), (m32, w32) = stats["bf16"], stats["bf16_f32slab"]
+    # the slabs' own share: bf16-slab vs fp32-slab gradients of the same bf16
+    # step, over the split-K conv weights (weight_v and the weight_g they feed)
+    e = sorted(float((grads["bf16"][n] - grads["bf16_f32slab"][n]).norm() / g.norm())
+               for n, g in ref.items() if float(g.norm()) > 0 and n.endswith(("weight_v", "weight_g")))
+    ms, ws = e[len(e) // 2], e[-1]
+    print(f"full-size bf16 gradient rel err vs fp32: bf16 slabs median {m16:.3g} worst {w16:.3g}; "
+          f"fp32 slabs median {m32:.3g} worst {w32:.3g}; conv weights, bf16 vs fp32 slabs: median {ms:.3g} "
+          f"worst {ws:.3g} over {len(e)}")
+    # measured: 0.0214 / 0.163 both ways (the bf16 operands' error); slab share <= 1.5e-3
+    assert m16 <= 3e-2 and w16 <= 2.5e-1, stats
+    assert abs(m16 - m32) <= 0.05 * m32 and abs(w16 - w32) <= 0.05 * w32, stats
+    assert ws <= 5e-3 and ms <= 0.1 * m32, (ms, ws, m32)
