@@ -177,3 +177,30 @@ def test_remove_weight_norm_bakes_every_conv_including_resampling():
     for base, w in before.items():
         assert torch.equal(params[base + ".weight"], w), base
         assert names.index(base + ".weight") == names.index(base + ".bias") + 1
+
+
+@pytest.mark.parametrize("name", ["vcc20_nown", "vcc20_multi_nown"])
+def test_no_weight_norm_convs_get_kaiming_init(name):
+    """use_weight_norm: false -- the reference's reset_parameters (vqvae.py:183,
+    210-217, 296) re-draws every Conv1d / ConvTranspose1d weight with
+    kaiming_normal_(nonlinearity='relu'): N(0, 2 / fan_in), torch's fan_in =
+    weight.size(1) * kernel (for ConvTranspose1d that is cout * k).  The
+    stride-1 and the resampling convs of both halves follow it; the biases keep
+    the default uniform.  Statistical check on every weight of >= 4096 values:
+    std within 8% of sqrt(2 / fan_in), mean within 4 standard errors of 0."""
+    from tests.helpers import cfg_of
+    from vae_npvc_amd.model.vqvae import Model
+    torch.manual_seed(3)
+    m = Model(cfg_of(name))
+    checked = 0
+    for n, p in m.named_parameters():
+        if not n.endswith(".weight") or p.dim() != 3 or p.numel() < 4096:
+            continue
+        fan_in = p.size(1) * p.size(2)
+        want = (2.0 / fan_in) ** 0.5
+        std, mean = float(p.detach().std()), float(p.detach().mean())
+        assert abs(std / want - 1) < 0.08, (n, std, want)
+        assert abs(mean) < 4 * want / p.numel() ** 0.5, (n, mean)
+        checked += 1
+    assert checked >= 10, checked
+    assert not any(n.endswith("weight_v") for n, _ in m.named_parameters())
