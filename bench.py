@@ -59,6 +59,8 @@ def parse():
                          "the cost of co-resident work such as RCCL's all-reduce kernels")
     ap.add_argument("--grad-sync", default="overlap", choices=["overlap", "end"],
                     help="N>1: gradient all-reduces beside the backward (default) or all after it")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N>1 process group (nccl = RCCL; gloo lets tests run several ranks on one GPU)")
     return ap.parse_args()
 
 
@@ -179,8 +181,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        local = local % torch.cuda.device_count()  # == local on a node with a GPU per rank
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())

@@ -149,3 +149,38 @@ def test_two_rank_tile_path_keeps_ranks_identical():
     for s in range(3):  # the EMA diagnostics are global statistics
         for k in ("entropy", "used_curr", "usage", "diff_emb"):
             assert ranks[0][3][s][k] == ranks[1][3][s][k], (s, k)
+
+
+@pytest.mark.timeout(600)
+def test_bench_two_ranks_reports_comm_block():
+    """bench.py's N > 1 path end to end on the box's one GPU: --gpus 2 launches
+    two ranks under torch.distributed.run (here with the gloo process group,
+    since RCCL refuses two ranks on one device), times the barrier-bracketed
+    steps as the max over ranks and prints the line with the `comm` block
+    (bytes all-reduced and collectives per step, per-rank waits, grad_sync),
+    for the all-reduce beside the backward and after it."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lines = {}
+    for mode in ("overlap", "end"):
+        cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+               "--dist-backend", "gloo", "--grad-sync", mode, "--no-cpu-baseline", "--fp32-steps", "0",
+               "--vq-reps", "0", "--no-probe"]
+        env = dict(os.environ)
+        env.pop("WORLD_SIZE", None)
+        r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=500)
+        assert r.returncode == 0, r.stderr[-3000:]
+        js = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        assert len(js) == 1, r.stdout[-2000:]
+        lines[mode] = json.loads(js[0])
+    for mode, d in lines.items():
+        assert d["n_gpus"] == 2 and d["steps"] == 3 and d["value"] > 0, d
+        c = d["comm"]
+        assert c["backend"] == "gloo" and c["grad_sync"] == mode, c
+        # every fp32 gradient once per step (31.3 M params) plus the EMA statistics bundle
+        assert 31_000_000 * 4 < c["bytes_per_step"] < 32_000_000 * 4 + (8 << 20), c
+        assert len(c["grad_wait_ms"]) == 2 and len(c["ema_wait_ms"]) == 2, c
+    assert lines["end"]["comm"]["bytes_per_step"] == lines["overlap"]["comm"]["bytes_per_step"]
+    assert lines["end"]["comm"]["collectives_per_step"] <= lines["overlap"]["comm"]["collectives_per_step"]
