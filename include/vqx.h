@@ -328,16 +328,16 @@ int vqx_logloss_fwd_bwd(const float* x_nct, const float* xhat, int32_t ldxh, int
  *                 (deterministic: 512-frame chunks sorted by code, segmented
  *                 sums, chunk tables reduced in order; pass NULL to skip, e.g.
  *                 eval / encode())
- * z [N][D] f32 (frame-major, D = 128), E [K][D] f32, K % 16 == 0, K <= 2048.
- * `partials` is a caller workspace of >= vqx_vq_workspace(N, K, bsum != NULL)
- * floats.
+ * z [N][D] f32 (frame-major, D = z_dim in {64, 128, 256}), E [K][D] f32,
+ * K % 16 == 0, K <= 2048.  `partials` is a caller workspace of
+ * >= vqx_vq_workspace(N, K, D, bsum != NULL) floats.
  */
 int vqx_vq_forward(const float* z, int64_t n_rows, int32_t D, const float* E, int32_t K,
                    int64_t* idx, float* zq, void* zq_c, int32_t zq_c_dtype, float* sqerr_out,
                    float* partials, float* bsum, float* bcnt, vqx_stream_t stream);
-/* Workspace (floats) vqx_vq_forward needs for N frames and K codes, with or
- * without the EMA statistics. */
-int vqx_vq_workspace(int64_t n_rows, int32_t K, int32_t with_stats, int64_t* floats);
+/* Workspace (floats) vqx_vq_forward needs for N frames and K codes of width
+ * D, with or without the EMA statistics (ABI 123: D added). */
+int vqx_vq_workspace(int64_t n_rows, int32_t K, int32_t D, int32_t with_stats, int64_t* floats);
 /* The EMA statistics part of vqx_vq_forward on its own (bsum = one-hot^T z,
  * bcnt = counts of idx; update_emb's onehot matmul, layers_vq.py:207-211),
  * for callers that run it on another stream than the distance kernel.
@@ -524,7 +524,7 @@ int vqx_stream_create_cu_mask(int32_t reserve_cus, vqx_stream_t* out, int32_t* c
 int vqx_stream_destroy(vqx_stream_t stream);
 
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
-#define VQX_ABI_VERSION 122
+#define VQX_ABI_VERSION 123
 int vqx_version(void);
 
 #ifdef __cplusplus

@@ -22,6 +22,8 @@ stored):
   * step_vcc20_radam      8 steps with optim_type RAdam (trainer/radam.py,
                           SURVEY §8f row 4); RAdam switches to the adaptive
                           update at step 6
+  * step_vcc20_z*         3 steps at codebook width z_dim 64 / 256, EMA and
+                          straight-through quantizers (--only-zdim)
   * step_vcc20_multi*     3 steps of the general Encoder/Decoder topology
                           (two resolution stages with strided resampling
                           convs, dilation 2**j, stack_layers 2, decoder
@@ -61,8 +63,8 @@ VARIANTS = {  # derived configs: base recipe + overrides
     "aishell3_plain": ("aishell3", {"use_ema": False}),
 }
 RADAM = {"vcc20_radam": ("vcc20", {"optim_type": "RAdam"})}
-from tests.helpers import MULTI, NOWN  # noqa: E402  (general topology; use_weight_norm false)
-VARIANTS_ALL = dict(VARIANTS, **RADAM, **MULTI, **NOWN)
+from tests.helpers import MULTI, NOWN, ZDIM  # noqa: E402  (general topology; no weight norm; z_dim)
+VARIANTS_ALL = dict(VARIANTS, **RADAM, **MULTI, **NOWN, **ZDIM)
 
 
 def load_cfg(name):
@@ -266,6 +268,11 @@ if __name__ == "__main__":
             step_fixture(name, B=4, T=128, steps=3, wseed=1401 + i, bseed=2401 + i, tseed=3401 + i, nseed=4401 + i,
                          out_prefix=f"step_{name}")
         sys.exit(0)
+    if "--only-zdim" in sys.argv:  # codebook widths 64 / 256 (EMA and straight-through quantizers)
+        for i, name in enumerate(ZDIM):
+            step_fixture(name, B=4, T=128, steps=3, wseed=1501 + i, bseed=2501 + i, tseed=3501 + i, nseed=4501 + i,
+                         out_prefix=f"step_{name}")
+        sys.exit(0)
     if "--only-plain" in sys.argv:  # just the §8f row-1 fixtures
         for i, name in enumerate(VARIANTS):
             step_fixture(name, B=4, T=128, steps=3, wseed=1101 + i, bseed=2101 + i, tseed=3101 + i,
@@ -286,6 +293,9 @@ if __name__ == "__main__":
                  out_prefix="step_vcc20_radam")
     for i, name in enumerate(NOWN):
         step_fixture(name, B=4, T=128, steps=3, wseed=1401 + i, bseed=2401 + i, tseed=3401 + i, nseed=4401 + i,
+                     out_prefix=f"step_{name}")
+    for i, name in enumerate(ZDIM):
+        step_fixture(name, B=4, T=128, steps=3, wseed=1501 + i, bseed=2501 + i, tseed=3501 + i, nseed=4501 + i,
                      out_prefix=f"step_{name}")
     for K in (128, 512, 1024):
         vq_fixture(K, 64, 256, 5000 + K, f"vq_K{K}")

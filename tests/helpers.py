@@ -39,9 +39,22 @@ NOWN = {"vcc20_nown": ("vcc20", _nown(_VCC20)),
         "vcc20_multi_nown": ("vcc20_multi", dict(_nown({"encoder": MULTI_ENC, "decoder": MULTI_DEC})))}
 
 
+def _zdim(base_cfg, z):
+    """Codebook width z_dim = z (layers_vq.py:166-173): the encoder's output
+    conv (z_channels) and the decoder's input (in_channels[0]) follow it."""
+    return {"z_dim": z, "encoder": dict(base_cfg["encoder"], z_channels=z),
+            "decoder": dict(base_cfg["decoder"], in_channels=[z])}
+
+
+# z_dim 64 / 256 (the VQ kernels' other widths; fixtures tests/golden/step_vcc20_z*)
+ZDIM = {"vcc20_z64": ("vcc20", _zdim(_VCC20, 64)), "vcc20_z256": ("vcc20", _zdim(_VCC20, 256)),
+        "vcc20_z64_plain": ("vcc20_z64", {"use_ema": False}),
+        "vcc20_z256_plain": ("vcc20_z256", {"use_ema": False})}
+
+
 def cfg_of(name, **over):
-    if name in NOWN:
-        base, mo = NOWN[name]
+    if name in NOWN or name in ZDIM:
+        base, mo = NOWN[name] if name in NOWN else ZDIM[name]
         cfg = cfg_of(base)
         cfg.update(mo)
     elif name in MULTI:

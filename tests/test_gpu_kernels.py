@@ -223,11 +223,15 @@ def test_weight_norm_pack_layouts(dtype):
             assert bool(((got - r16).abs() <= ulp).all()), (kind, cin, cout, k)
 
 
+@pytest.mark.parametrize("D", [64, 128, 256])
 @pytest.mark.parametrize("K", [128, 512, 1024])
-def test_vq_argmin_exact(K):
+def test_vq_argmin_exact(K, D):
+    """vqx_vq_forward at every built code width (vq_forward_kernel<D>):
+    indices equal torch's first-minimum argmin of the reference's distance
+    order, z_q the gathered codes, sqerr, counts and per-code sums."""
     ops = _ops()
     torch.manual_seed(3)
-    N, D = 4096, 128
+    N = 4096
     z = torch.randn(N, D)
     E = torch.randn(K, D)
     dist = (z.pow(2).sum(1, keepdim=True) + E.pow(2).sum(1)) - 2 * z @ E.t()
@@ -237,7 +241,7 @@ def test_vq_argmin_exact(K):
     zq = torch.empty(N, D, device=DEV)
     zqc = torch.empty(N, D, device=DEV, dtype=torch.bfloat16)
     sq = torch.zeros(1, device=DEV)
-    part = torch.empty(ops.vq_workspace(N, K, True), device=DEV)
+    part = torch.empty(ops.vq_workspace(N, K, True, D), device=DEV)
     bsum = torch.zeros(K, D, device=DEV)
     bcnt = torch.zeros(K, device=DEV)
     ops.vq_forward(zd, Ed, idx, zq, zqc, sq, part, bsum, bcnt)
@@ -252,9 +256,11 @@ def test_vq_argmin_exact(K):
     assert torch.allclose(bsum.cpu(), onehot.t() @ z, atol=1e-4, rtol=1e-5)
 
 
-@pytest.mark.parametrize("N,K,collapse", [(1000, 16, False), (777, 128, True), (16384, 512, True),
-                                          (5000, 1024, False), (3001, 2048, False), (33, 512, False)])
-def test_vq_ema_statistics_ragged_and_collapsed(N, K, collapse):
+@pytest.mark.parametrize("N,K,collapse,D", [(1000, 16, False, 128), (777, 128, True, 128), (16384, 512, True, 128),
+                                            (5000, 1024, False, 128), (3001, 2048, False, 128), (33, 512, False, 128),
+                                            (777, 128, True, 64), (3001, 2048, False, 64), (1000, 16, False, 256),
+                                            (5000, 1024, True, 256)])
+def test_vq_ema_statistics_ragged_and_collapsed(N, K, collapse, D):
     """EMA statistics of vqx_vq_forward (update_emb, layers_vq.py:207-211):
     bsum = onehot(idx)^T z and bcnt = code counts, accumulated (+=) into
     nonzero buffers, for ragged N (partial frame groups and chunks), every
@@ -262,14 +268,13 @@ def test_vq_ema_statistics_ragged_and_collapsed(N, K, collapse):
     pick 2 codes (the round-1 kernel's same-address atomic pile-up case)."""
     ops = _ops()
     torch.manual_seed(N + K)
-    D = 128
     z = torch.randn(N, D)
     E = torch.randn(K, D)
     if collapse:
         E[2:] += 50.0  # every frame is nearest to code 0 or 1
     ref = ((z.pow(2).sum(1, keepdim=True) + E.pow(2).sum(1)) - 2 * z @ E.t()).argmin(1)
     idx = torch.empty(N, dtype=torch.int64, device=DEV)
-    part = torch.empty(ops.vq_workspace(N, K, True), device=DEV)
+    part = torch.empty(ops.vq_workspace(N, K, True, D), device=DEV)
     bsum0, bcnt0 = torch.randn(K, D), torch.rand(K)
     bsum, bcnt = bsum0.to(DEV), bcnt0.to(DEV)
     sq = torch.zeros(1, device=DEV)
@@ -284,15 +289,15 @@ def test_vq_ema_statistics_ragged_and_collapsed(N, K, collapse):
         assert int((onehot.sum(0) > 0).sum()) <= 2
 
 
+@pytest.mark.parametrize("D", [64, 128, 256])
 @pytest.mark.parametrize("K", [16, 128, 512, 2048])
-def test_vq_stats_counts_equal_bincount_skewed(K):
+def test_vq_stats_counts_equal_bincount_skewed(K, D):
     """vq_stats_kernel's per-chunk code counts race-free (the count
     loop read keys[] while the sort's first pass could swap them): bcnt must
     equal torch.bincount exactly and bsum the per-code sums, over many 512-frame
     chunks, for skewed index streams (geometric code popularity, long runs of
     one code, a single code, ragged N), launched repeatedly."""
     ops = _ops()
-    D = 128
     g = torch.Generator().manual_seed(K)
     N = 64 * 512 + 37
     z = torch.randn(N, D, generator=g)
@@ -302,7 +307,7 @@ def test_vq_stats_counts_equal_bincount_skewed(K):
     mixed = torch.where(torch.rand(N, generator=g) < 0.9, torch.zeros(N, dtype=torch.int64),
                         torch.randint(0, K, (N,), generator=g))
     zd = z.to(DEV)
-    part = torch.empty(ops.vq_workspace(N, K, True), device=DEV)
+    part = torch.empty(ops.vq_workspace(N, K, True, D), device=DEV)
     for idx in (geo, runs, single, mixed):
         want_c = torch.bincount(idx, minlength=K).float()
         want_s = torch.zeros(K, D, dtype=torch.float64).index_add_(0, idx, z.double())

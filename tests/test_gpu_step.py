@@ -9,7 +9,8 @@ from tests.helpers import cfg_of, load_fixture, make_trainer, relclose
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("prefix", ["step_vcc20", "step_aishell3", "step_vcc20_nown", "step_vcc20_multi_nown"])
+@pytest.mark.parametrize("prefix", ["step_vcc20", "step_aishell3", "step_vcc20_nown", "step_vcc20_multi_nown",
+                                    "step_vcc20_z64", "step_vcc20_z256"])
 def test_fp32_train_steps_match_reference_golden(prefix):
     """fp32 mode.  Step 1: loss dict within 1e-4 relative (diff_emb: 1e-3 with a
     1e-6 absolute floor -- at step 1 every frame is its own code, so the
@@ -23,7 +24,9 @@ def test_fp32_train_steps_match_reference_golden(prefix):
     the commitment term (zq - z) (measured <= 2.1e-4 on aishell3 with
     jitter); EMA buffers within 1e-4.  The *_nown fixtures run use_weight_norm
     false (vqvae.py:179-180,290-293: plain `weight` parameters on every conv,
-    the multi-stage one including the strided resampling convs)."""
+    the multi-stage one including the strided resampling convs).  The
+    *_z64 / *_z256 fixtures run codebooks of width z_dim 64 and 256 (the VQ
+    kernels' vq_forward_kernel<D>, layers_vq.py:166-173)."""
     from oracle.vqvae_cpu import seeded_batch
     meta, arr = load_fixture(prefix)
     cfg = cfg_of(meta["config"], compute_dtype="fp32")
@@ -90,7 +93,8 @@ def test_fp32_radam_steps_match_reference_golden(tmp_path):
 
 PLAIN = {"vcc20_plain": ("vcc20", {"use_ema": False}),
          "vcc20_plain_nonorm": ("vcc20", {"use_ema": False, "embed_norm": False}),
-         "aishell3_plain": ("aishell3", {"use_ema": False})}
+         "aishell3_plain": ("aishell3", {"use_ema": False}),
+         "vcc20_z64_plain": ("vcc20_z64_plain", {}), "vcc20_z256_plain": ("vcc20_z256_plain", {})}
 
 
 @pytest.mark.parametrize("name", list(PLAIN))
@@ -120,8 +124,15 @@ def test_fp32_plain_vq_steps_match_reference_golden(name):
         for k, v in meta["detail"][s].items():
             # the perplexity is a count statistic over B*T = 512 frames: after an
             # Adam step, a near-tie frame or two may pick the other code, which
-            # moves it by O(1/512) while every loss still agrees to 1e-3
-            rt = 1e-4 if s == 0 else (2e-2 if k == "entropy" else 1e-3)
+            # moves it by O(1/512) while every loss still agrees to 1e-3.  At
+            # z_dim 64 / 256 the commitment loss after Adam steps drifts further
+            # (z64: 1.4e-4 at step 2, 2.4e-3 at step 3, with every code index
+            # and X like equal): the step-1 encoder gradients, small residuals
+            # through z/||z||, differ from the reference by <= 1.6e-4 (D=128:
+            # 4.4e-5) and Adam's m/sqrt(v) turns that into parameter moves
+            zdim = name.startswith("vcc20_z")
+            rt = 1e-4 if s == 0 else (2e-2 if k == "entropy" else 5e-3 if (zdim and k in ("VQ loss", "Total"))
+                                      else 1e-3)
             assert relclose(detail[k], v, rt), (s, k, detail[k], v)
         if s == 0:
             g = {n: eng.g(p) for n, p in tr.model.named_parameters()}

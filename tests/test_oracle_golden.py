@@ -44,7 +44,8 @@ def test_structure_matches_reference():
 
 FIXTURE_CFG = {"step_vcc20": ("vcc20", {}), "step_aishell3": ("aishell3", {}),
                "step_vcc20_radam": ("vcc20", {"optim_type": "RAdam"}), "step_vcc20_multi": ("vcc20_multi", {}),
-               "step_vcc20_nown": ("vcc20_nown", {}), "step_vcc20_multi_nown": ("vcc20_multi_nown", {})}
+               "step_vcc20_nown": ("vcc20_nown", {}), "step_vcc20_multi_nown": ("vcc20_multi_nown", {}),
+               "step_vcc20_z64": ("vcc20_z64", {}), "step_vcc20_z256": ("vcc20_z256", {})}
 
 
 @pytest.mark.parametrize("prefix", list(FIXTURE_CFG))
@@ -87,7 +88,8 @@ def test_oracle_train_steps_match_reference(prefix):
 PLAIN = {"vcc20_plain": ("vcc20", {"use_ema": False}),
          "vcc20_plain_nonorm": ("vcc20", {"use_ema": False, "embed_norm": False}),
          "aishell3_plain": ("aishell3", {"use_ema": False}),
-         "vcc20_multi_plain": ("vcc20_multi_plain", {})}
+         "vcc20_multi_plain": ("vcc20_multi_plain", {}),
+         "vcc20_z64_plain": ("vcc20_z64_plain", {}), "vcc20_z256_plain": ("vcc20_z256_plain", {})}
 
 
 def plain_cfg(name):

@@ -16,9 +16,11 @@
 
 namespace vqx {
 
-constexpr int VQ_D = 128;
+// Code widths D (= z_dim) the kernels are built for: 64, 128 (the BASELINE
+// configs) and 256; every vqx_vq_* entry point refuses any other.
+inline bool vq_d_ok(int D) { return D == 64 || D == 128 || D == 256; }
 // Workgroup geometry of vq_forward_kernel: VQ_FG groups of 16 frames x VQ_CS
-// code splits = 8 waves.  A wave keeps its 16 frames' z (16 x 128 f32) in
+// code splits = 8 waves.  A wave keeps its 16 frames' z (16 x D f32) in
 // registers as the A operand of v_mfma_f32_16x16x4_f32 and, per step, scores
 // them against VQ_SUB codes (one accumulator chain per 16 codes; the 40-cycle
 // dependent-MFMA latency is covered by the other waves of the SIMD).  The
@@ -31,10 +33,12 @@ constexpr int VQ_FG = 2;
 constexpr int VQ_CS = 4;
 constexpr int VQ_SUB = 16;
 constexpr int VQ_STEP = VQ_CS * VQ_SUB;            // 64 codes per LDS step
-constexpr int VQ_STEP_BYTES = VQ_STEP * VQ_D * 4;  // 32 KiB
 constexpr int VQ_THREADS = 64 * VQ_FG * VQ_CS;     // 512
 constexpr int VQ_FRAMES = 16 * VQ_FG;              // 32 frames per workgroup
-constexpr int VQ_STAGE = VQ_STEP_BYTES / 16 / VQ_THREADS;  // 16-B chunks staged per thread per step
+template <int D>
+constexpr int vq_step_bytes() { return VQ_STEP * D * 4; }  // 32 KiB at D = 128
+template <int D>
+constexpr int vq_stage() { return vq_step_bytes<D>() / 16 / VQ_THREADS; }  // 16-B chunks staged per thread per step
 
 // EMA statistics (vq_stats_kernel): frames per chunk and the per-code sum
 // slabs [chunks][K][D] + counts [chunks][K] that vq_stats_reduce_kernel sums
@@ -49,20 +53,23 @@ inline int vq_stats_chunks(int64_t N, int K) {
   return (int)((N + 511) / 512);  // VQ_CHUNK frames per chunk
 }
 inline int64_t vq_partials_floats(int64_t N) { return (N + VQ_FRAMES - 1) / VQ_FRAMES; }
-inline int64_t vq_workspace_floats(int64_t N, int K, bool stats) {
+inline int64_t vq_workspace_floats(int64_t N, int K, int D, bool stats) {
   int64_t f = (vq_partials_floats(N) + 63) & ~(int64_t)63;
-  if (stats) f += (int64_t)vq_stats_chunks(N, K) * K * (VQ_D + 1);
+  if (stats) f += (int64_t)vq_stats_chunks(N, K) * K * (D + 1);
   return f;
 }
 
-__global__ __launch_bounds__(VQ_THREADS, 4) void vq_forward_kernel(const float* __restrict__ z, int64_t N,
+// D = 256: a 128-KiB double-buffered step leaves one workgroup per CU
+template <int D>
+__global__ __launch_bounds__(VQ_THREADS, D == 256 ? 2 : 4) void vq_forward_kernel(const float* __restrict__ z, int64_t N,
                                                                    const float* __restrict__ E, int K,
                                                                    int64_t* __restrict__ idx_out,
                                                                    float* __restrict__ zq, void* __restrict__ zq_c,
                                                                    int zq_dt, float* __restrict__ partials) {
   // two code steps in LDS (double buffer) + their ||e||^2: one barrier per step,
-  // the next step's LDS writes issued beside this step's MFMAs.  64.5 KiB:
-  // two workgroups per CU.
+  // the next step's LDS writes issued beside this step's MFMAs.  64.5 KiB at
+  // D = 128: two workgroups per CU.
+  constexpr int VQ_D = D, VQ_STEP_BYTES = vq_step_bytes<D>(), VQ_STAGE = vq_stage<D>(), KB = D / 16;
   __shared__ __attribute__((aligned(16))) char smem[2 * VQ_STEP_BYTES];
   __shared__ float eeL[2][VQ_STEP];
   __shared__ float red[16];
@@ -74,17 +81,17 @@ __global__ __launch_bounds__(VQ_THREADS, 4) void vq_forward_kernel(const float* 
   const bool row_ok = my_row < N;
 
   const int nsteps = (K + VQ_STEP - 1) / VQ_STEP;
-  // Staging: thread t holds 4 consecutive 16-B chunks (64 B) of code t >> 3 of
-  // the step, loaded through one buffer descriptor over E (codes >= K read as
-  // zeros, no branches) one step ahead of its LDS write.  The 8 threads of a
-  // code also form its ||e||^2 (the 32 fmaf of each thread, then two quad-DPP
-  // and one half-row-mirror adds) into eeL, so the score loop needs one LDS
-  // read per code block.
-  static_assert(VQ_STAGE == 4 && VQ_STEP * 8 == VQ_THREADS, "staging layout");
+  // Staging: thread t holds VQ_STAGE consecutive 16-B chunks (D / 2 bytes) of
+  // code t >> 3 of the step, loaded through one buffer descriptor over E (codes
+  // >= K read as zeros, no branches) one step ahead of its LDS write.  The 8
+  // threads of a code also form its ||e||^2 (the D/8 fmaf of each thread, then
+  // two quad-DPP and one half-row-mirror adds) into eeL, so the score loop
+  // needs one LDS read per code block.
+  static_assert(VQ_STAGE * 8 * 16 == VQ_D * 4 && VQ_STEP * 8 == VQ_THREADS, "staging layout");
   const __amdgpu_buffer_rsrc_t rsE =
       __builtin_amdgcn_make_buffer_rsrc((void*)E, (short)0, (int)((int64_t)K * VQ_D * 4), 0x00020000);
   const int s_code = tid >> 3, s_part = tid & 7;
-  const unsigned s_off = (unsigned)(s_code * 512 + s_part * 64);
+  const unsigned s_off = (unsigned)(s_code * VQ_D * 4 + s_part * 16 * VQ_STAGE);
   f32x4_t stage[VQ_STAGE];
   auto load_step = [&](int st) {
     typedef float f4v __attribute__((ext_vector_type(4)));
@@ -95,14 +102,14 @@ __global__ __launch_bounds__(VQ_THREADS, 4) void vq_forward_kernel(const float* 
     }
   };
   auto lds_at = [&](int buf, int code, int ch) {
-    return smem + buf * VQ_STEP_BYTES + code * 512 + 16 * (ch ^ (code & 15));
+    return smem + buf * VQ_STEP_BYTES + code * (VQ_D * 4) + 16 * (ch ^ (code & 15));
   };
   // the staged step into buffer buf, its codes' squared norms into eeL[buf]
   auto write_step = [&](int buf) {
     float e2 = 0.f;
 #pragma unroll
     for (int j = 0; j < VQ_STAGE; ++j) {
-      *(f32x4_t*)lds_at(buf, s_code, 4 * s_part + j) = stage[j];
+      *(f32x4_t*)lds_at(buf, s_code, VQ_STAGE * s_part + j) = stage[j];
       e2 = fmaf(stage[j][0], stage[j][0], e2);
       e2 = fmaf(stage[j][1], stage[j][1], e2);
       e2 = fmaf(stage[j][2], stage[j][2], e2);
@@ -118,16 +125,16 @@ __global__ __launch_bounds__(VQ_THREADS, 4) void vq_forward_kernel(const float* 
 
   // z fragments: zf[kb] = z[my_row][16kb + 4q .. +3] (rows >= N read as zeros
   // through a descriptor that starts at this workgroup's first frame)
-  f32x4_t zf[8];
+  f32x4_t zf[KB];
   float zz = 0.f;
   const int64_t wg_row0 = (int64_t)blockIdx.x * VQ_FRAMES;
   int64_t z_rec = (N - wg_row0) * VQ_D * 4;
   if (z_rec > VQ_FRAMES * VQ_D * 4) z_rec = VQ_FRAMES * VQ_D * 4;
   const __amdgpu_buffer_rsrc_t rsZ =
       __builtin_amdgcn_make_buffer_rsrc((void*)(z + wg_row0 * VQ_D), (short)0, (int)z_rec, 0x00020000);
-  const unsigned z_off = (unsigned)((fg * 16 + j16) * 512 + 16 * q);
+  const unsigned z_off = (unsigned)((fg * 16 + j16) * (VQ_D * 4) + 16 * q);
 #pragma unroll
-  for (int kb = 0; kb < 8; ++kb) {
+  for (int kb = 0; kb < KB; ++kb) {
     typedef float f4v __attribute__((ext_vector_type(4)));
     const f4v u = __builtin_amdgcn_raw_buffer_load_b128(rsZ, (int)(z_off + 64 * kb), 0, 0);
     const f32x4_t v = {u[0], u[1], u[2], u[3]};
@@ -174,7 +181,7 @@ __global__ __launch_bounds__(VQ_THREADS, 4) void vq_forward_kernel(const float* 
       acc2[b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
-    for (int kb = 0; kb < 8; kb += 2) {
+    for (int kb = 0; kb < KB; kb += 2) {
       f32x4_t bf[NB], bg[NB];
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
@@ -245,16 +252,16 @@ __global__ __launch_bounds__(VQ_THREADS, 4) void vq_forward_kernel(const float* 
       if (q == 0) idx_out[my_row] = my_idx;
       // the code row's 8 loads all in flight before the first store (a
       // load-store pair per 16 dims paid one memory latency each)
-      f32x4_t ev[8];
+      f32x4_t ev[KB];
 #pragma unroll
-      for (int kb = 0; kb < 8; ++kb) ev[kb] = *(const f32x4_t*)(E + (int64_t)my_idx * VQ_D + 16 * kb + 4 * q);
+      for (int kb = 0; kb < KB; ++kb) ev[kb] = *(const f32x4_t*)(E + (int64_t)my_idx * VQ_D + 16 * kb + 4 * q);
       if (zq) {
 #pragma unroll
-        for (int kb = 0; kb < 8; ++kb) *(f32x4_t*)(zq + my_row * VQ_D + 16 * kb + 4 * q) = ev[kb];
+        for (int kb = 0; kb < KB; ++kb) *(f32x4_t*)(zq + my_row * VQ_D + 16 * kb + 4 * q) = ev[kb];
       }
       if (zq_c && zq_dt == VQX_BF16) {
 #pragma unroll
-        for (int kb = 0; kb < 8; ++kb) {
+        for (int kb = 0; kb < KB; ++kb) {
           uint2 pk;
           pk.x = pack_bf16x2(ev[kb][0], ev[kb][1]);
           pk.y = pack_bf16x2(ev[kb][2], ev[kb][3]);
@@ -262,10 +269,10 @@ __global__ __launch_bounds__(VQ_THREADS, 4) void vq_forward_kernel(const float* 
         }
       } else if (zq_c) {
 #pragma unroll
-        for (int kb = 0; kb < 8; ++kb) *(f32x4_t*)((float*)zq_c + my_row * VQ_D + 16 * kb + 4 * q) = ev[kb];
+        for (int kb = 0; kb < KB; ++kb) *(f32x4_t*)((float*)zq_c + my_row * VQ_D + 16 * kb + 4 * q) = ev[kb];
       }
 #pragma unroll
-      for (int kb = 0; kb < 8; ++kb)
+      for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
           const float df = __fsub_rn(ev[kb][m], zf[kb][m]);
@@ -290,7 +297,7 @@ __global__ __launch_bounds__(VQ_THREADS, 4) void vq_forward_kernel(const float* 
 constexpr int VQ_CHUNK = 512;
 
 template <int DSL>
-__global__ __launch_bounds__(256) void vq_stats_kernel(const float* __restrict__ z, int64_t N,
+__global__ __launch_bounds__(256) void vq_stats_kernel(const float* __restrict__ z, int64_t N, int VQ_D,
                                                        const int64_t* __restrict__ idx, int K, int64_t frames_per_chunk,
                                                        float* __restrict__ slab, float* __restrict__ cnt_slab) {
   constexpr int G = DSL / 4;             // 4-dim groups per slice
@@ -421,7 +428,8 @@ __global__ __launch_bounds__(256) void vq_stats_kernel(const float* __restrict__
 // loading a quarter of the chunks (independent loads), combined in order.
 __global__ __launch_bounds__(256) void vq_stats_reduce_kernel(const float* __restrict__ slab,
                                                               const float* __restrict__ cnt_slab, int chunks, int K,
-                                                              float* __restrict__ bsum, float* __restrict__ bcnt) {
+                                                              int VQ_D, float* __restrict__ bsum,
+                                                              float* __restrict__ bcnt) {
   __shared__ f32x4_t red[4][64];
   const int64_t total = (int64_t)K * VQ_D;
   const int col = threadIdx.x & 63, qg = threadIdx.x >> 6;
@@ -562,33 +570,33 @@ __global__ void commit_bwd_kernel(const float* __restrict__ z, const float* __re
 
 using namespace vqx;
 
-extern "C" int vqx_vq_workspace(int64_t n_rows, int32_t K, int32_t with_stats, int64_t* floats) {
-  if (n_rows <= 0 || K <= 0 || !floats) { set_error("vqx_vq_workspace: bad arguments"); return -1; }
-  *floats = vq_workspace_floats(n_rows, K, with_stats != 0);
+extern "C" int vqx_vq_workspace(int64_t n_rows, int32_t K, int32_t D, int32_t with_stats, int64_t* floats) {
+  if (n_rows <= 0 || K <= 0 || !floats || !vq_d_ok(D)) { set_error("vqx_vq_workspace: bad arguments"); return -1; }
+  *floats = vq_workspace_floats(n_rows, K, D, with_stats != 0);
   return 0;
 }
 
 template <int DSL>
-static void launch_vq_stats(const float* z, int64_t N, const int64_t* idx, int K, float* ws, float* bsum, float* bcnt,
-                            hipStream_t s) {
+static void launch_vq_stats(const float* z, int64_t N, int VQ_D, const int64_t* idx, int K, float* ws, float* bsum,
+                            float* bcnt, hipStream_t s) {
   const int chunks = vq_stats_chunks(N, K);
   const int64_t fpc = VQ_CHUNK;
   float* slab = ws + ((vq_partials_floats(N) + 63) & ~(int64_t)63);
   float* cnt_slab = slab + (int64_t)chunks * K * VQ_D;
   constexpr int R = 256 / (DSL / 4);
   const size_t lds = (size_t)K * DSL * 4 + VQ_CHUNK * 4 + 2 * R * 4 + (size_t)((K + 3) & ~3) * 4 + 2 * R * (DSL / 4) * 16;
-  hipLaunchKernelGGL(vq_stats_kernel<DSL>, dim3(chunks, VQ_D / DSL), dim3(256), lds, s, z, N, idx, K, fpc, slab,
+  hipLaunchKernelGGL(vq_stats_kernel<DSL>, dim3(chunks, VQ_D / DSL), dim3(256), lds, s, z, N, VQ_D, idx, K, fpc, slab,
                      cnt_slab);
   const int64_t total4 = (int64_t)K * VQ_D / 4;
   unsigned nb = (unsigned)((total4 + 63) / 64);
   if (nb * 256u < (unsigned)K) nb = (unsigned)((K + 255) / 256);
-  hipLaunchKernelGGL(vq_stats_reduce_kernel, dim3(nb), dim3(256), 0, s, slab, cnt_slab, chunks, K, bsum, bcnt);
+  hipLaunchKernelGGL(vq_stats_reduce_kernel, dim3(nb), dim3(256), 0, s, slab, cnt_slab, chunks, K, VQ_D, bsum, bcnt);
 }
 
 extern "C" int vqx_vq_forward(const float* z, int64_t n_rows, int32_t D, const float* E, int32_t K, int64_t* idx,
                               float* zq, void* zq_c, int32_t zq_c_dtype, float* sqerr_out, float* partials,
                               float* bsum, float* bcnt, vqx_stream_t stream) {
-  if (D != VQ_D) { set_error("vqx_vq_forward: only D=128 supported (got %d)", D); return -1; }
+  if (!vq_d_ok(D)) { set_error("vqx_vq_forward: D must be 64, 128 or 256 (got %d)", D); return -1; }
   if (K <= 0 || K % 16) { set_error("vqx_vq_forward: K=%d must be a positive multiple of 16", K); return -1; }
   if (bsum && K > 2048) { set_error("vqx_vq_forward: EMA statistics need K <= 2048 (got %d)", K); return -1; }
   if (n_rows <= 0 || !z || !E || !idx || !partials) { set_error("vqx_vq_forward: bad arguments"); return -1; }
@@ -596,15 +604,15 @@ extern "C" int vqx_vq_forward(const float* z, int64_t n_rows, int32_t D, const f
   if (((uintptr_t)z | (uintptr_t)E) & 15) { set_error("vqx_vq_forward: z/E must be 16-byte aligned"); return -1; }
   hipStream_t s = (hipStream_t)stream;
   const int grid = (int)vq_partials_floats(n_rows);
-  hipLaunchKernelGGL(vq_forward_kernel, dim3(grid), dim3(VQ_THREADS), 0, s, z, n_rows, E, K, idx, zq, zq_c,
-                     zq_c_dtype, partials);
+  auto* kfn = D == 64 ? vq_forward_kernel<64> : D == 128 ? vq_forward_kernel<128> : vq_forward_kernel<256>;
+  hipLaunchKernelGGL(kfn, dim3(grid), dim3(VQ_THREADS), 0, s, z, n_rows, E, K, idx, zq, zq_c, zq_c_dtype, partials);
   if (sqerr_out) hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(1024), 0, s, partials, grid, 1.0f, sqerr_out);
   if (bsum) {
     switch (vq_stats_dsl(K)) {
-      case 32: launch_vq_stats<32>(z, n_rows, idx, K, partials, bsum, bcnt, s); break;
-      case 16: launch_vq_stats<16>(z, n_rows, idx, K, partials, bsum, bcnt, s); break;
-      case 8: launch_vq_stats<8>(z, n_rows, idx, K, partials, bsum, bcnt, s); break;
-      default: launch_vq_stats<4>(z, n_rows, idx, K, partials, bsum, bcnt, s); break;
+      case 32: launch_vq_stats<32>(z, n_rows, D, idx, K, partials, bsum, bcnt, s); break;
+      case 16: launch_vq_stats<16>(z, n_rows, D, idx, K, partials, bsum, bcnt, s); break;
+      case 8: launch_vq_stats<8>(z, n_rows, D, idx, K, partials, bsum, bcnt, s); break;
+      default: launch_vq_stats<4>(z, n_rows, D, idx, K, partials, bsum, bcnt, s); break;
     }
   }
   return launch_status("vqx_vq_forward");
@@ -612,16 +620,16 @@ extern "C" int vqx_vq_forward(const float* z, int64_t n_rows, int32_t D, const f
 
 extern "C" int vqx_vq_stats(const float* z, int64_t n_rows, int32_t D, const int64_t* idx, int32_t K,
                             float* partials, float* bsum, float* bcnt, vqx_stream_t stream) {
-  if (D != VQ_D) { set_error("vqx_vq_stats: only D=128 supported (got %d)", D); return -1; }
+  if (!vq_d_ok(D)) { set_error("vqx_vq_stats: D must be 64, 128 or 256 (got %d)", D); return -1; }
   if (K <= 0 || K % 16 || K > 2048) { set_error("vqx_vq_stats: K=%d must be a multiple of 16 in [16, 2048]", K); return -1; }
   if (n_rows <= 0 || !z || !idx || !partials || !bsum || !bcnt) { set_error("vqx_vq_stats: bad arguments"); return -1; }
   if ((uintptr_t)z & 15) { set_error("vqx_vq_stats: z must be 16-byte aligned"); return -1; }
   hipStream_t s = (hipStream_t)stream;
   switch (vq_stats_dsl(K)) {
-    case 32: launch_vq_stats<32>(z, n_rows, idx, K, partials, bsum, bcnt, s); break;
-    case 16: launch_vq_stats<16>(z, n_rows, idx, K, partials, bsum, bcnt, s); break;
-    case 8: launch_vq_stats<8>(z, n_rows, idx, K, partials, bsum, bcnt, s); break;
-    default: launch_vq_stats<4>(z, n_rows, idx, K, partials, bsum, bcnt, s); break;
+    case 32: launch_vq_stats<32>(z, n_rows, D, idx, K, partials, bsum, bcnt, s); break;
+    case 16: launch_vq_stats<16>(z, n_rows, D, idx, K, partials, bsum, bcnt, s); break;
+    case 8: launch_vq_stats<8>(z, n_rows, D, idx, K, partials, bsum, bcnt, s); break;
+    default: launch_vq_stats<4>(z, n_rows, D, idx, K, partials, bsum, bcnt, s); break;
   }
   return launch_status("vqx_vq_stats");
 }
@@ -663,7 +671,7 @@ extern "C" int vqx_vq_commit_bwd(const float* z, const float* zq, int64_t count,
 
 // ===================================================================
 // Straight-through VectorQuantizer (use_ema: false; layers_vq.py:9-163,
-// reduction 'frame_mean', target_norm 1.0).  One wave per 128-wide row.
+// reduction 'frame_mean', target_norm 1.0).  One wave per D-wide row.
 // ===================================================================
 namespace {
 
@@ -673,41 +681,74 @@ __device__ __forceinline__ float wave_sum64(float v) {
   return v;
 }
 
+// PL = D/64 consecutive floats of a D-wide row per lane (one wave per row)
+template <int PL>
+struct RowPL {
+  float v[PL];
+  __device__ __forceinline__ void load(const float* p) {
+#pragma unroll
+    for (int i = 0; i < PL; ++i) v[i] = p[i];
+  }
+  __device__ __forceinline__ void store(float* p) const {
+#pragma unroll
+    for (int i = 0; i < PL; ++i) p[i] = v[i];
+  }
+  __device__ __forceinline__ float dot(const RowPL& o) const {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < PL; ++i) s += v[i] * o.v[i];
+    return s;
+  }
+};
+
 // Blocks [0, ceil(K/4)) renormalise the codebook rows, the rest the frames.
 //   codebook (embed_norm, layers_vq.py:28-33, then :99): E *= 1/||E|| in
 //     place, embn = (1.0*E)/||E||, e_len = ||E|| (after the in-place step);
 //   frames (:97): z_norm = (1.0*z)/||z||, z_len = ||z||, and the per-block
 //     sum of (z_norm - z)^2 (normalisation loss, :125-126).
+template <int PL>
 __global__ __launch_bounds__(256) void vq_normalize_kernel(const float* __restrict__ z, int64_t N, float* __restrict__ E,
                                                            int K, float* __restrict__ zn, float* __restrict__ zlen,
                                                            float* __restrict__ embn, float* __restrict__ elen,
                                                            float* __restrict__ part) {
+  constexpr int D = 64 * PL;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int kb = (K + 3) / 4;
   __shared__ float red[4];
   if ((int)blockIdx.x < kb) {
     const int k = blockIdx.x * 4 + w;
     if (k >= K) return;
-    float2 e = *(const float2*)(E + (int64_t)k * 128 + 2 * lane);
-    const float n1 = sqrtf(wave_sum64(e.x * e.x + e.y * e.y));
+    float* er = E + (int64_t)k * D + PL * lane;
+    RowPL<PL> e;
+    e.load(er);
+    const float n1 = sqrtf(wave_sum64(e.dot(e)));
     const float f = 1.0f / n1;
-    e.x *= f;
-    e.y *= f;
-    *(float2*)(E + (int64_t)k * 128 + 2 * lane) = e;
-    const float n2 = sqrtf(wave_sum64(e.x * e.x + e.y * e.y));
-    *(float2*)(embn + (int64_t)k * 128 + 2 * lane) = make_float2(e.x / n2, e.y / n2);
+#pragma unroll
+    for (int i = 0; i < PL; ++i) e.v[i] *= f;
+    e.store(er);
+    const float n2 = sqrtf(wave_sum64(e.dot(e)));
+    RowPL<PL> o;
+#pragma unroll
+    for (int i = 0; i < PL; ++i) o.v[i] = e.v[i] / n2;
+    o.store(embn + (int64_t)k * D + PL * lane);
     if (lane == 0) elen[k] = n2;
     return;
   }
   const int64_t n = (int64_t)(blockIdx.x - kb) * 4 + w;
   float l = 0.f;
   if (n < N) {
-    const float2 v = *(const float2*)(z + n * 128 + 2 * lane);
-    const float nz = sqrtf(wave_sum64(v.x * v.x + v.y * v.y));
-    const float2 u = make_float2(v.x / nz, v.y / nz);
-    *(float2*)(zn + n * 128 + 2 * lane) = u;
+    RowPL<PL> v, u;
+    v.load(z + n * D + PL * lane);
+    const float nz = sqrtf(wave_sum64(v.dot(v)));
+    float d2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < PL; ++i) {
+      u.v[i] = v.v[i] / nz;
+      d2 += (u.v[i] - v.v[i]) * (u.v[i] - v.v[i]);
+    }
+    u.store(zn + n * D + PL * lane);
     if (lane == 0) zlen[n] = nz;
-    l = wave_sum64((u.x - v.x) * (u.x - v.x) + (u.y - v.y) * (u.y - v.y));
+    l = wave_sum64(d2);
   }
   if (lane == 0) red[w] = l;
   __syncthreads();
@@ -736,7 +777,7 @@ __global__ __launch_bounds__(256) void vq_perplexity_kernel(const float* __restr
 // codes k: d = s*(cnt_k*emb_k - bsum_k) (= sum over the code's frames of
 //   2(zq - zn)/(B*T), z_qut), then dE = (d - emb (emb.d)) / e_len through
 //   emb = E/||E||, or dE = d without normalisation.
-template <typename T>
+template <typename T, int PL>
 __global__ __launch_bounds__(256) void vq_plain_bwd_kernel(const float* __restrict__ z, const float* __restrict__ zn,
                                                            const float* __restrict__ zlen, const float* __restrict__ zq,
                                                            const T* __restrict__ dzq, const int* __restrict__ src_t,
@@ -745,47 +786,53 @@ __global__ __launch_bounds__(256) void vq_plain_bwd_kernel(const float* __restri
                                                            const float* __restrict__ bcnt,
                                                            const float* __restrict__ emb, const float* __restrict__ elen,
                                                            int K, float* __restrict__ dE) {
+  constexpr int D = 64 * PL;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int kb = (K + 3) / 4;
   if ((int)blockIdx.x < kb) {
     const int k = blockIdx.x * 4 + w;
     if (k >= K) return;
-    const float2 e = *(const float2*)(emb + (int64_t)k * 128 + 2 * lane);
-    const float2 b = *(const float2*)(bsum + (int64_t)k * 128 + 2 * lane);
+    RowPL<PL> e, b, d;
+    e.load(emb + (int64_t)k * D + PL * lane);
+    b.load(bsum + (int64_t)k * D + PL * lane);
     const float c = bcnt[k];
-    float2 d = make_float2(s * (c * e.x - b.x), s * (c * e.y - b.y));
+#pragma unroll
+    for (int i = 0; i < PL; ++i) d.v[i] = s * (c * e.v[i] - b.v[i]);
     if (normalize) {
-      const float dot = wave_sum64(e.x * d.x + e.y * d.y);
+      const float dot = wave_sum64(e.dot(d));
       const float il = 1.0f / elen[k];
-      d = make_float2((d.x - e.x * dot) * il, (d.y - e.y * dot) * il);
+#pragma unroll
+      for (int i = 0; i < PL; ++i) d.v[i] = (d.v[i] - e.v[i] * dot) * il;
     }
-    *(float2*)(dE + (int64_t)k * 128 + 2 * lane) = d;
+    d.store(dE + (int64_t)k * D + PL * lane);
     return;
   }
   const int64_t n = (int64_t)(blockIdx.x - kb) * 4 + w;
   if (n >= N) return;
-  const int64_t o = n * 128 + 2 * lane;
-  const float2 u = *(const float2*)(zn + o);
-  const float2 q = *(const float2*)(zq + o);
-  float g0 = 0.f, g1 = 0.f;
+  const int64_t o = n * D + PL * lane;
+  RowPL<PL> u, q, g;
+  u.load(zn + o);
+  q.load(zq + o);
   const int t = (int)(n % Tn);
-  if (dzq && (!src_t || src_t[t] == t)) {
-    g0 = Elem<T>::ld(dzq, o);
-    g1 = Elem<T>::ld(dzq, o + 1);
-  }
+  const bool st = dzq && (!src_t || src_t[t] == t);
+#pragma unroll
+  for (int i = 0; i < PL; ++i) g.v[i] = st ? Elem<T>::ld(dzq, o + i) : 0.f;
   const float bs = beta * s;
-  float d0 = g0 + bs * (u.x - q.x), d1 = g1 + bs * (u.y - q.y);
+  RowPL<PL> d;
+#pragma unroll
+  for (int i = 0; i < PL; ++i) d.v[i] = g.v[i] + bs * (u.v[i] - q.v[i]);
   if (normalize) {
-    const float2 v = *(const float2*)(z + o);
-    d0 += bs * (u.x - v.x);
-    d1 += bs * (u.y - v.y);
-    const float dot = wave_sum64(u.x * d0 + u.y * d1);
+    RowPL<PL> v;
+    v.load(z + o);
+#pragma unroll
+    for (int i = 0; i < PL; ++i) d.v[i] += bs * (u.v[i] - v.v[i]);
+    const float dot = wave_sum64(u.dot(d));
     const float il = 1.0f / zlen[n];
-    d0 = (d0 - u.x * dot) * il - bs * (u.x - v.x);
-    d1 = (d1 - u.y * dot) * il - bs * (u.y - v.y);
+#pragma unroll
+    for (int i = 0; i < PL; ++i) d.v[i] = (d.v[i] - u.v[i] * dot) * il - bs * (u.v[i] - v.v[i]);
   }
-  Elem<T>::st(dz, o, d0);
-  Elem<T>::st(dz, o + 1, d1);
+#pragma unroll
+  for (int i = 0; i < PL; ++i) Elem<T>::st(dz, o + i, d.v[i]);
 }
 
 }  // namespace
@@ -793,7 +840,7 @@ __global__ __launch_bounds__(256) void vq_plain_bwd_kernel(const float* __restri
 extern "C" int vqx_vq_normalize(const float* z, int64_t n_rows, int32_t D, float* E, int32_t K, float* z_norm,
                                 float* z_len, float* emb_norm, float* e_len, float* partials, float* normloss_out,
                                 vqx_stream_t stream) {
-  if (D != 128) { set_error("vqx_vq_normalize: z_dim must be 128"); return -1; }
+  if (!vq_d_ok(D)) { set_error("vqx_vq_normalize: z_dim must be 64, 128 or 256 (got %d)", D); return -1; }
   if (!z || !E || !z_norm || !z_len || !emb_norm || !e_len || !partials || n_rows < 1 || K < 1) {
     set_error("vqx_vq_normalize: bad arguments");
     return -1;
@@ -801,8 +848,9 @@ extern "C" int vqx_vq_normalize(const float* z, int64_t n_rows, int32_t D, float
   hipStream_t s = (hipStream_t)stream;
   const int kb = (K + 3) / 4;
   const int64_t zb = (n_rows + 3) / 4;
-  hipLaunchKernelGGL(vq_normalize_kernel, dim3((unsigned)(kb + zb)), dim3(256), 0, s, z, n_rows, E, K, z_norm, z_len,
-                     emb_norm, e_len, partials);
+  auto* kfn = D == 64 ? vq_normalize_kernel<1> : D == 128 ? vq_normalize_kernel<2> : vq_normalize_kernel<4>;
+  hipLaunchKernelGGL(kfn, dim3((unsigned)(kb + zb)), dim3(256), 0, s, z, n_rows, E, K, z_norm, z_len, emb_norm, e_len,
+                     partials);
   if (normloss_out) hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(1024), 0, s, partials, (int)zb, 1.0f, normloss_out);
   return launch_status("vqx_vq_normalize");
 }
@@ -818,7 +866,7 @@ extern "C" int vqx_vq_plain_bwd(const float* z, const float* z_norm, const float
                                 int32_t normalize, float beta, float scale, void* dz, int32_t dtype, const float* bsum,
                                 const float* bcnt, const float* emb, const float* e_len, int32_t K, float* dE,
                                 vqx_stream_t stream) {
-  if (D != 128) { set_error("vqx_vq_plain_bwd: z_dim must be 128"); return -1; }
+  if (!vq_d_ok(D)) { set_error("vqx_vq_plain_bwd: z_dim must be 64, 128 or 256 (got %d)", D); return -1; }
   if (!z_norm || !zq || !dz || !bsum || !bcnt || !emb || !dE || T < 1 || n_rows < 1 || K < 1 ||
       (normalize && (!z || !z_len || !e_len))) {
     set_error("vqx_vq_plain_bwd: bad arguments");
@@ -827,13 +875,17 @@ extern "C" int vqx_vq_plain_bwd(const float* z, const float* z_norm, const float
   const int kb = (K + 3) / 4;
   const int64_t zb = (n_rows + 3) / 4;
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == VQX_BF16)
-    hipLaunchKernelGGL(vq_plain_bwd_kernel<bf16_t>, dim3((unsigned)(kb + zb)), dim3(256), 0, s, z, z_norm, z_len, zq,
-                       (const bf16_t*)dzq, src_t, T, n_rows, normalize, beta, scale, (bf16_t*)dz, bsum, bcnt, emb, e_len,
-                       K, dE);
-  else
-    hipLaunchKernelGGL(vq_plain_bwd_kernel<float>, dim3((unsigned)(kb + zb)), dim3(256), 0, s, z, z_norm, z_len, zq,
-                       (const float*)dzq, src_t, T, n_rows, normalize, beta, scale, (float*)dz, bsum, bcnt, emb, e_len,
-                       K, dE);
+  const dim3 grid((unsigned)(kb + zb));
+  if (dtype == VQX_BF16) {
+    auto* kfn = D == 64 ? vq_plain_bwd_kernel<bf16_t, 1> : D == 128 ? vq_plain_bwd_kernel<bf16_t, 2>
+                                                                    : vq_plain_bwd_kernel<bf16_t, 4>;
+    hipLaunchKernelGGL(kfn, grid, dim3(256), 0, s, z, z_norm, z_len, zq, (const bf16_t*)dzq, src_t, T, n_rows,
+                       normalize, beta, scale, (bf16_t*)dz, bsum, bcnt, emb, e_len, K, dE);
+  } else {
+    auto* kfn = D == 64 ? vq_plain_bwd_kernel<float, 1> : D == 128 ? vq_plain_bwd_kernel<float, 2>
+                                                                   : vq_plain_bwd_kernel<float, 4>;
+    hipLaunchKernelGGL(kfn, grid, dim3(256), 0, s, z, z_norm, z_len, zq, (const float*)dzq, src_t, T, n_rows,
+                       normalize, beta, scale, (float*)dz, bsum, bcnt, emb, e_len, K, dE);
+  }
   return launch_status("vqx_vq_plain_bwd");
 }

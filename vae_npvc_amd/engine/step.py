@@ -205,7 +205,7 @@ class Workspace:
             self.embn = e(K, Z, dt=F32)
             self.e_len = e(K, dt=F32)
             self.pv_part = e(Nz // 4 + 8, dt=F32)
-        self.vq_part = e(ops.vq_workspace(Nz, K, train or eng.plain), dt=F32)  # VQ partials (+ statistics slabs)
+        self.vq_part = e(ops.vq_workspace(Nz, K, train or eng.plain, Z), dt=F32)  # VQ partials (+ statistics slabs)
         # EMA statistics bundle (all-reduced as one buffer in data parallel)
         self.ema = e(K * Z + K + K * Z, dt=F32)
         self.bsum = self.ema[: K * Z].view(K, Z)
@@ -300,8 +300,8 @@ class VQVAEEngine:
         self.dims = d = dict(mel=enc.in_ch, Z=enc.z_ch, S=dec.skip_ch, F=dec.final_ch, cond=dec.cond_ch,
                              K=model.quantizer.z_num, ydim=model.embeds._embedding.weight.shape[1],
                              jitter_p=model.jitter.probability)
-        if d["Z"] != 128 or model.quantizer.z_dim != 128:  # Model's constructor refuses these already
-            raise NotImplementedError("the fused VQ kernel is built for z_dim = 128")
+        if d["Z"] not in (64, 128, 256) or model.quantizer.z_dim != d["Z"]:  # Model's constructor refuses these
+            raise NotImplementedError("the fused VQ kernels are built for z_dim 64, 128 or 256")
         # straight-through VectorQuantizer (use_ema: false)
         self.plain = not model.use_ema
         self.vq_normalize = bool(getattr(model.quantizer, "normalize", False)) if self.plain else False

@@ -121,10 +121,13 @@ class Model(nn.Module):
         self.decoder = Decoder(**arch["decoder"])
         self.use_ema = arch.get("use_ema", False)
         # the reference's quantizers take any z_dim (layers_vq.py:166-173); the
-        # fused VQ kernel (vqx_vq_forward) keeps a frame's 128 dims in registers
+        # fused VQ kernels (vqx_vq_forward) keep a frame's z_dim values in
+        # registers and are built for 64, 128 and 256; the encoder's output
+        # channels must equal z_dim, as the reference's quantizer needs
         z_dim, z_ch = arch.get("z_dim", 128), self.encoder.z_ch
-        if z_dim != 128 or z_ch != 128:
-            raise NotImplementedError(f"z_dim {z_dim} / encoder output {z_ch}: the HIP quantizer is built for 128")
+        if z_dim not in (64, 128, 256) or z_ch != z_dim:
+            raise NotImplementedError(f"z_dim {z_dim} / encoder output {z_ch}: the HIP quantizer is built for "
+                                      "z_dim 64, 128 or 256 with the encoder's output channels equal to it")
         if self.use_ema:
             self.quantizer = EMAVectorQuantizer(arch.get("z_num", 512), arch.get("z_dim", 128), arch.get("mu", 0.9),
                                                 reduction="frame_mean")

@@ -392,17 +392,18 @@ def logloss_fwd_bwd(x_nct, xhat, grad_scale, dxhat, loss_out, partials):
     return loss_out
 
 
-def vq_workspace(n_rows, K, stats):
-    """Floats of workspace vqx_vq_forward needs (with or without EMA statistics)."""
+def vq_workspace(n_rows, K, stats, D=128):
+    """Floats of workspace vqx_vq_forward needs for K codes of width D (with or
+    without EMA statistics)."""
     out = ctypes.c_int64()
-    call("vqx_vq_workspace", int(n_rows), int(K), int(bool(stats)), ctypes.byref(out))
+    call("vqx_vq_workspace", int(n_rows), int(K), int(D), int(bool(stats)), ctypes.byref(out))
     return out.value
 
 
 def vq_forward(z, E, idx, zq, zq_c, sqerr, partials=None, bsum=None, bcnt=None):
-    """partials: f32 workspace of >= vq_workspace(N, K, bsum is not None) floats (allocated if None)."""
+    """partials: f32 workspace of >= vq_workspace(N, K, bsum is not None, D) floats (allocated if None)."""
     N, D = z.shape
-    need = vq_workspace(N, E.shape[0], bsum is not None)
+    need = vq_workspace(N, E.shape[0], bsum is not None, D)
     if partials is None:
         partials = torch.empty(need, device=z.device, dtype=torch.float32)
     if partials.numel() < need:
@@ -416,7 +417,7 @@ def vq_stats(z, idx, K, partials, bsum, bcnt):
     """EMA statistics alone (vqx_vq_stats): bsum [K, D] = sum of the frames per
     code, bcnt [K] = counts; partials as vq_forward's workspace with stats."""
     N, D = z.shape
-    need = vq_workspace(N, K, True)
+    need = vq_workspace(N, K, True, D)
     if partials.numel() < need:
         raise ValueError(f"vq_stats: workspace {partials.numel()} < {need} floats")
     call("vqx_vq_stats", ptr(z), N, D, ptr(idx), K, ptr(partials), ptr(bsum), ptr(bcnt), stream_ptr())
