@@ -449,7 +449,7 @@ int vqx_radam_step(float* p, const float* g, float* m, float* v, int64_t n, cons
 
 /*
  * Straight-through VectorQuantizer (use_ema: false; layers_vq.py:9-163,
- * reduction 'frame_mean', target_norm 1.0, z_dim 128).
+ * reduction 'frame_mean', target_norm 1.0, z_dim 64, 128 or 256).
  * vqx_vq_normalize (embed_norm: true): the codebook parameter E [K][D] is
  *   renormalised in place (embed_norm(), :28-33) and emb_norm = E/||E||
  *   (:99), e_len = ||E|| after that step; z_norm = z/||z|| (:97), z_len =
