@@ -99,14 +99,14 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("prefix,dtype", [("step_vcc20", "fp32"), ("step_vcc20", "bf16"), ("step_aishell3", "fp32"),
-                                          ("step_vcc20_multi", "fp32")])
+                                          ("step_aishell3", "bf16"), ("step_vcc20_multi", "fp32")])
 def test_two_rank_engine_step_matches_reference_golden(prefix, dtype):
     """fp32: losses 1e-4 at step 1 and 1e-3 later, gradient norms 2e-3 (as the
     single-process golden test), parameters after 3 steps 1e-3.  bf16 (the
     bench dtype): losses 1e-2 (VQ loss 2e-2), gradient norms 5e-2, parameters 1e-2.
-    aishell3 (BASELINE config 4: 160 mel, K=128, skip 256, jitter 0.12) needs
-    the same numpy stream on every rank: each rank draws the single-process
-    jitter map.  vcc20_multi is the general topology (two stages, stride-2
+    aishell3 (BASELINE config 4: 160 mel, K=128, skip 256, jitter 0.12, bf16
+    as the config states) needs the same numpy stream on every rank: each
+    rank draws the single-process jitter map.  vcc20_multi is the general topology (two stages, stride-2
     resampling, dilation, stack_layers 2, kernel 5)."""
     from tests.helpers import load_fixture
     meta, _ = load_fixture(prefix)
