@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--splits", type=int, default=8)
     ap.add_argument("--rotate", type=int, default=1, help="cycle through R operand sets (R*~50 MB > MALL = cold)")
     ap.add_argument("--sweep-splits", default=None, help="comma list: time every wgrad shape at each split count")
+    ap.add_argument("--gnstats", action="store_true", help="fwd: GroupNorm statistics tiles in the epilogue (GNSTATS)")
     a = ap.parse_args()
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     B, T = 64, 256
@@ -58,11 +59,15 @@ def main():
         dxs = [torch.empty(N, cin, device=dev, dtype=dt) for _ in range(R)]
         slabs = torch.empty(splits, cout, k * cin, device=dev)
         bias = torch.zeros(cout, device=dev)
+        use_gst = a.gnstats and cout % 128 == 0  # GNSTATS tiles need 128-column groups
+        gst = torch.empty((N // 128) * ((cout + 127) // 128) * 4, device=dev) if use_gst else None
+        fkw = dict(gn_stats=gst, gn_groups=1) if use_gst else {}
 
         def fn(i):
             x, dy, y, dx = xs[i % R], dys[i % R], ys[i % R], dxs[i % R]
             if mode == "fwd":
-                ops.conv_fwd(x, w, y, T=T, cin=cin, cout=cout, ntaps=k, pad=(k - 1) // 2, prologue=pro, bias=bias)
+                ops.conv_fwd(x, w, y, T=T, cin=cin, cout=cout, ntaps=k, pad=(k - 1) // 2, prologue=pro, bias=bias,
+                             **fkw)
             elif mode == "dgrad":
                 ops.conv_dgrad(dy, w, dx, T=T, cin=cout, cout=cin, ntaps=k, pad=(k - 1) // 2)
             else:
