@@ -69,7 +69,7 @@ __global__ __launch_bounds__(VQ_THREADS, D == 256 ? 2 : 4) void vq_forward_kerne
   // two code steps in LDS (double buffer) + their ||e||^2: one barrier per step,
   // the next step's LDS writes issued beside this step's MFMAs.  64.5 KiB at
   // D = 128: two workgroups per CU.
-  constexpr int VQ_D = D, VQ_STEP_BYTES = vq_step_bytes<D>(), VQ_STAGE = vq_stage<D>(), KB = D / 16;
+  constexpr int VQ_STEP_BYTES = vq_step_bytes<D>(), VQ_STAGE = vq_stage<D>(), KB = D / 16;
   __shared__ __attribute__((aligned(16))) char smem[2 * VQ_STEP_BYTES];
   __shared__ float eeL[2][VQ_STEP];
   __shared__ float red[16];
@@ -87,11 +87,11 @@ __global__ __launch_bounds__(VQ_THREADS, D == 256 ? 2 : 4) void vq_forward_kerne
   // threads of a code also form its ||e||^2 (the D/8 fmaf of each thread, then
   // two quad-DPP and one half-row-mirror adds) into eeL, so the score loop
   // needs one LDS read per code block.
-  static_assert(VQ_STAGE * 8 * 16 == VQ_D * 4 && VQ_STEP * 8 == VQ_THREADS, "staging layout");
+  static_assert(VQ_STAGE * 8 * 16 == D * 4 && VQ_STEP * 8 == VQ_THREADS, "staging layout");
   const __amdgpu_buffer_rsrc_t rsE =
-      __builtin_amdgcn_make_buffer_rsrc((void*)E, (short)0, (int)((int64_t)K * VQ_D * 4), 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)E, (short)0, (int)((int64_t)K * D * 4), 0x00020000);
   const int s_code = tid >> 3, s_part = tid & 7;
-  const unsigned s_off = (unsigned)(s_code * VQ_D * 4 + s_part * 16 * VQ_STAGE);
+  const unsigned s_off = (unsigned)(s_code * D * 4 + s_part * 16 * VQ_STAGE);
   f32x4_t stage[VQ_STAGE];
   auto load_step = [&](int st) {
     typedef float f4v __attribute__((ext_vector_type(4)));
@@ -102,7 +102,7 @@ __global__ __launch_bounds__(VQ_THREADS, D == 256 ? 2 : 4) void vq_forward_kerne
     }
   };
   auto lds_at = [&](int buf, int code, int ch) {
-    return smem + buf * VQ_STEP_BYTES + code * (VQ_D * 4) + 16 * (ch ^ (code & 15));
+    return smem + buf * VQ_STEP_BYTES + code * (D * 4) + 16 * (ch ^ (code & 15));
   };
   // the staged step into buffer buf, its codes' squared norms into eeL[buf]
   auto write_step = [&](int buf) {
@@ -128,11 +128,11 @@ __global__ __launch_bounds__(VQ_THREADS, D == 256 ? 2 : 4) void vq_forward_kerne
   f32x4_t zf[KB];
   float zz = 0.f;
   const int64_t wg_row0 = (int64_t)blockIdx.x * VQ_FRAMES;
-  int64_t z_rec = (N - wg_row0) * VQ_D * 4;
-  if (z_rec > VQ_FRAMES * VQ_D * 4) z_rec = VQ_FRAMES * VQ_D * 4;
+  int64_t z_rec = (N - wg_row0) * D * 4;
+  if (z_rec > VQ_FRAMES * D * 4) z_rec = VQ_FRAMES * D * 4;
   const __amdgpu_buffer_rsrc_t rsZ =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(z + wg_row0 * VQ_D), (short)0, (int)z_rec, 0x00020000);
-  const unsigned z_off = (unsigned)((fg * 16 + j16) * (VQ_D * 4) + 16 * q);
+      __builtin_amdgcn_make_buffer_rsrc((void*)(z + wg_row0 * D), (short)0, (int)z_rec, 0x00020000);
+  const unsigned z_off = (unsigned)((fg * 16 + j16) * (D * 4) + 16 * q);
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb) {
     typedef float f4v __attribute__((ext_vector_type(4)));
@@ -254,10 +254,10 @@ __global__ __launch_bounds__(VQ_THREADS, D == 256 ? 2 : 4) void vq_forward_kerne
       // load-store pair per 16 dims paid one memory latency each)
       f32x4_t ev[KB];
 #pragma unroll
-      for (int kb = 0; kb < KB; ++kb) ev[kb] = *(const f32x4_t*)(E + (int64_t)my_idx * VQ_D + 16 * kb + 4 * q);
+      for (int kb = 0; kb < KB; ++kb) ev[kb] = *(const f32x4_t*)(E + (int64_t)my_idx * D + 16 * kb + 4 * q);
       if (zq) {
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb) *(f32x4_t*)(zq + my_row * VQ_D + 16 * kb + 4 * q) = ev[kb];
+        for (int kb = 0; kb < KB; ++kb) *(f32x4_t*)(zq + my_row * D + 16 * kb + 4 * q) = ev[kb];
       }
       if (zq_c && zq_dt == VQX_BF16) {
 #pragma unroll
@@ -265,11 +265,11 @@ __global__ __launch_bounds__(VQ_THREADS, D == 256 ? 2 : 4) void vq_forward_kerne
           uint2 pk;
           pk.x = pack_bf16x2(ev[kb][0], ev[kb][1]);
           pk.y = pack_bf16x2(ev[kb][2], ev[kb][3]);
-          *(uint2*)((bf16_t*)zq_c + my_row * VQ_D + 16 * kb + 4 * q) = pk;
+          *(uint2*)((bf16_t*)zq_c + my_row * D + 16 * kb + 4 * q) = pk;
         }
       } else if (zq_c) {
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb) *(f32x4_t*)((float*)zq_c + my_row * VQ_D + 16 * kb + 4 * q) = ev[kb];
+        for (int kb = 0; kb < KB; ++kb) *(f32x4_t*)((float*)zq_c + my_row * D + 16 * kb + 4 * q) = ev[kb];
       }
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb)
@@ -297,7 +297,7 @@ __global__ __launch_bounds__(VQ_THREADS, D == 256 ? 2 : 4) void vq_forward_kerne
 constexpr int VQ_CHUNK = 512;
 
 template <int DSL>
-__global__ __launch_bounds__(256) void vq_stats_kernel(const float* __restrict__ z, int64_t N, int VQ_D,
+__global__ __launch_bounds__(256) void vq_stats_kernel(const float* __restrict__ z, int64_t N, int D,
                                                        const int64_t* __restrict__ idx, int K, int64_t frames_per_chunk,
                                                        float* __restrict__ slab, float* __restrict__ cnt_slab) {
   constexpr int G = DSL / 4;             // 4-dim groups per slice
@@ -360,7 +360,7 @@ __global__ __launch_bounds__(256) void vq_stats_kernel(const float* __restrict__
   for (int u = 0; u < LEN; ++u) {
     const int key = keys[p0 + u];
     rc[u] = key == 0x7fffffff ? -1 : key >> 9;
-    rows[u] = *(const f32x4_t*)(z + (n0 + (rc[u] < 0 ? 0 : (key & 511))) * VQ_D + dd);
+    rows[u] = *(const f32x4_t*)(z + (n0 + (rc[u] < 0 ? 0 : (key & 511))) * D + dd);
   }
 #pragma unroll
   for (int u = 0; u < LEN; ++u)
@@ -414,10 +414,10 @@ __global__ __launch_bounds__(256) void vq_stats_kernel(const float* __restrict__
     if (kt >= 0) finish(kt, r, part[(r * 2 + 1) * G + g]);
   }
   __syncthreads();
-  float* out = slab + (int64_t)c * K * VQ_D + d0;
+  float* out = slab + (int64_t)c * K * D + d0;
   for (int i = tid; i < K * G; i += 256) {
     const int k = i / G, q = i % G;
-    *(f32x4_t*)(out + (int64_t)k * VQ_D + 4 * q) = *(const f32x4_t*)&acc[k * DSL + 4 * q];
+    *(f32x4_t*)(out + (int64_t)k * D + 4 * q) = *(const f32x4_t*)&acc[k * DSL + 4 * q];
   }
   if (counts)
     for (int i = tid; i < K; i += 256) cnt_slab[(int64_t)c * K + i] = (float)cnt[i];
@@ -428,10 +428,10 @@ __global__ __launch_bounds__(256) void vq_stats_kernel(const float* __restrict__
 // loading a quarter of the chunks (independent loads), combined in order.
 __global__ __launch_bounds__(256) void vq_stats_reduce_kernel(const float* __restrict__ slab,
                                                               const float* __restrict__ cnt_slab, int chunks, int K,
-                                                              int VQ_D, float* __restrict__ bsum,
+                                                              int D, float* __restrict__ bsum,
                                                               float* __restrict__ bcnt) {
   __shared__ f32x4_t red[4][64];
-  const int64_t total = (int64_t)K * VQ_D;
+  const int64_t total = (int64_t)K * D;
   const int col = threadIdx.x & 63, qg = threadIdx.x >> 6;
   const int64_t i4 = ((int64_t)blockIdx.x * 64 + col) * 4;
   const int per = (chunks + 3) / 4, c0 = qg * per, c1 = min(chunks, c0 + per);
@@ -577,20 +577,20 @@ extern "C" int vqx_vq_workspace(int64_t n_rows, int32_t K, int32_t D, int32_t wi
 }
 
 template <int DSL>
-static void launch_vq_stats(const float* z, int64_t N, int VQ_D, const int64_t* idx, int K, float* ws, float* bsum,
+static void launch_vq_stats(const float* z, int64_t N, int D, const int64_t* idx, int K, float* ws, float* bsum,
                             float* bcnt, hipStream_t s) {
   const int chunks = vq_stats_chunks(N, K);
   const int64_t fpc = VQ_CHUNK;
   float* slab = ws + ((vq_partials_floats(N) + 63) & ~(int64_t)63);
-  float* cnt_slab = slab + (int64_t)chunks * K * VQ_D;
+  float* cnt_slab = slab + (int64_t)chunks * K * D;
   constexpr int R = 256 / (DSL / 4);
   const size_t lds = (size_t)K * DSL * 4 + VQ_CHUNK * 4 + 2 * R * 4 + (size_t)((K + 3) & ~3) * 4 + 2 * R * (DSL / 4) * 16;
-  hipLaunchKernelGGL(vq_stats_kernel<DSL>, dim3(chunks, VQ_D / DSL), dim3(256), lds, s, z, N, VQ_D, idx, K, fpc, slab,
+  hipLaunchKernelGGL(vq_stats_kernel<DSL>, dim3(chunks, D / DSL), dim3(256), lds, s, z, N, D, idx, K, fpc, slab,
                      cnt_slab);
-  const int64_t total4 = (int64_t)K * VQ_D / 4;
+  const int64_t total4 = (int64_t)K * D / 4;
   unsigned nb = (unsigned)((total4 + 63) / 64);
   if (nb * 256u < (unsigned)K) nb = (unsigned)((K + 255) / 256);
-  hipLaunchKernelGGL(vq_stats_reduce_kernel, dim3(nb), dim3(256), 0, s, slab, cnt_slab, chunks, K, VQ_D, bsum, bcnt);
+  hipLaunchKernelGGL(vq_stats_reduce_kernel, dim3(nb), dim3(256), 0, s, slab, cnt_slab, chunks, K, D, bsum, bcnt);
 }
 
 extern "C" int vqx_vq_forward(const float* z, int64_t n_rows, int32_t D, const float* E, int32_t K, int64_t* idx,
