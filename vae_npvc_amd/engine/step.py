@@ -142,6 +142,12 @@ class EngineOptions:
                        workgroups per weight-gradient launch (the split-K
                        factor) of the 3-tap layers, the 1x1 layers and the
                        stage convs; wgrad_min_k: fewest frames per split
+      wn_bwd_batch     one process (no data parallelism): every backward
+                       group's weight-norm backward + bias reductions in one
+                       launch after the backward (each group's split-K slabs
+                       and partial sums kept in buffers of their own) instead
+                       of a launch per group; data parallel keeps the launch
+                       per group, whose all-reduce then overlaps the backward
       slab_f32         fp32 split-K slabs in bf16 runs (+3.3% step time,
                        profiles/r04/slab_wfirst_ab.txt)
       kernel_policy    include/vqx.h VQX_POLICY_* of every conv GEMM call"""
@@ -153,6 +159,7 @@ class EngineOptions:
     wgrad_wgs_solo: int = 512
     wgrad_min_k: int = 512
     slab_f32: bool = False
+    wn_bwd_batch: bool = True
     kernel_policy: int = 0
 
 
@@ -268,6 +275,18 @@ class Workspace:
         self.colsum_b = [e(B * 2 * Cmax, dt=F32) for _ in range(Lmax)]
         self.dgam_b = [e(B * 2 * Cmax, dt=F32) for _ in range(Lmax)]
         self.dbet_b = [e(B * 2 * Cmax, dt=F32) for _ in range(Lmax)]
+        # ... per block when the weight-norm backward is batched (EngineOptions.wn_bwd_batch):
+        # the column reductions then read them after the whole backward
+        self.blk_parts = {}
+        if eng.opt.wn_bwd_batch:
+            for si, st in enumerate(eng.enc_stages):
+                for j in range(len(st.blocks)):
+                    self.blk_parts[("enc", si, j)] = {k: [e(B * self.enc[si].C, dt=F32) for _ in range(st.L)]
+                                                      for k in ("colsum_b", "dgam_b", "dbet_b")}
+            for si, st in enumerate(eng.dec_stages):
+                for j in range(len(st.blocks)):
+                    self.blk_parts[("dec", si, j)] = {k: [e(B * 2 * self.dec[si].C, dt=F32)]
+                                                      for k in ("dgam_b", "dbet_b")}
         self.dz = e(Nz, Z)
         self.dzq = e(Nz, Z) if eng.plain else None  # decoder gradient w.r.t. its (jittered) input
         self.dc_flat = [e(NCe) for _ in range(2)]   # encoder dL/dc ping-pong (viewed per stage)
@@ -318,6 +337,8 @@ class VQVAEEngine:
         # default (EngineOptions.side_stream)
         self._side_on = self.device.type == "cuda" and self.opt.side_stream
         self._side = None
+        self._wn_active = False   # inside backward(): the weight-norm backward may be batched
+        self._wn_pending = set()
 
     # ------------------------------------------------------------ parameters
     def _flatten(self):
@@ -553,10 +574,16 @@ class VQVAEEngine:
             n = Lr.splits * Lr.rows * Lr.cols * (4 if sdt[id(Lr)] == F32 else 2)
             return (n + 255) // 256 * 256
 
-        arena = max(sum(nbytes(Lr) for Lr in grp) for grp in groups)
+        # batched weight-norm backward (EngineOptions.wn_bwd_batch): every group's
+        # slabs in a region of their own, all read by one launch after the backward
+        per_group = [sum(nbytes(Lr) for Lr in grp) for grp in groups]
+        arena = sum(per_group) if self.opt.wn_bwd_batch else max(per_group)
         self.arena = torch.empty(arena, device=self.device, dtype=torch.uint8)
-        for grp in groups:
-            off = 0
+        base = 0
+        for gi, grp in enumerate(groups):
+            off = base
+            if self.opt.wn_bwd_batch:
+                base += per_group[gi]
             for Lr in grp:
                 n = Lr.splits * Lr.rows * Lr.cols * (4 if sdt[id(Lr)] == F32 else 2)
                 Lr.slab = self.arena[off:off + n].view(sdt[id(Lr)]).view(Lr.splits, Lr.rows, Lr.cols)
@@ -620,8 +647,9 @@ class VQVAEEngine:
             sw = w.dec[si]
             C2 = 2 * sw.C
             nb = len(st.blocks)
-            dg_b, db_b = self._bview(w.dgam_b[0], B, C2), self._bview(w.dbet_b[0], B, C2)
             for j, b in enumerate(st.blocks):
+                dg_b = self._bview(self._blk(w, "dec", si, j, "dgam_b", 0), B, C2)
+                db_b = self._bview(self._blk(w, "dec", si, j, "dbet_b", 0), B, C2)
                 rb = g(b.rs.mod.bias)
                 # dL/dx_{j+1}: zero after the last block of the last stage (cs zeroed), else the
                 # colsums of the next block's / next stage conv's dgrad
@@ -648,14 +676,15 @@ class VQVAEEngine:
                                                                                               sw.cs[j + 1]),
                                                                           g(b.skip.mod.bias))]
                 for l, (Lr, gn) in enumerate(zip(b.convs, b.gns)):
-                    ent += [cr(self._bview(w.colsum_b[l], B, C), g(Lr.mod.bias)),
-                            cr(self._bview(w.dgam_b[l], B, C), g(gn.weight)),
-                            cr(self._bview(w.dbet_b[l], B, C), g(gn.bias))]
+                    ent += [cr(self._bview(self._blk(w, "enc", si, j, "colsum_b", l), B, C), g(Lr.mod.bias)),
+                            cr(self._bview(self._blk(w, "enc", si, j, "dgam_b", l), B, C), g(gn.weight)),
+                            cr(self._bview(self._blk(w, "enc", si, j, "dbet_b", l), B, C), g(gn.bias))]
                 t[b.key] = ent
             first_folded = not st.blocks and si + 1 < ne and self.enc_stages[si + 1].conv.kind == KIND_DOWN
             t[("enc_stage", si)] = [self._wn_entry(st.conv, True),
                                     cr(self._bias_partials(w, first_folded, sw.cs[0]), g(st.conv.mod.bias))]
         w.bwd_tables = {k: ops.wn_table(v) for k, v in t.items()}
+        w.bwd_table_all = ops.wn_table([e for v in t.values() for e in v])  # the batched launch
         # parameters whose gradients are final once a group's launch is done
         # (data parallel: their all-reduce is issued right then, parallel/ddp.py)
         w.bwd_params = {k: self._params_written([t_ for e in entries for t_ in (e.get("dv"), e.get("dg"))])
@@ -906,11 +935,35 @@ class VQVAEEngine:
         return src
 
     # ------------------------------------------------------------ backward
+    def _wn_batched(self):
+        return self.opt.wn_bwd_batch and self.comm is None and self._wn_active
+
     def _wn_bwd(self, w, key):
         """A backward group's weight-norm backward + bias/affine reductions;
-        its gradients are final afterwards (data parallel: reduce them now)."""
+        its gradients are final afterwards (data parallel: reduce them now).
+        Batched (one process): noted here, run for every group at once by
+        _wn_bwd_flush after the backward."""
+        if self._wn_batched():
+            self._wn_pending.add(key)
+            return
         ops.weight_norm_bwd(w.bwd_tables[key])
         self._grads_final(w.bwd_params[key])
+
+    def _wn_bwd_flush(self, w):
+        if not self._wn_batched():
+            return
+        if self._wn_pending != set(w.bwd_tables):  # every group's GEMMs ran (their slabs are final)
+            raise RuntimeError(f"batched weight-norm backward: groups {set(w.bwd_tables) - self._wn_pending} "
+                               "did not run")
+        ops.weight_norm_bwd(w.bwd_table_all)
+        self._wn_pending = set()
+
+    def _blk(self, w, side, si, j, kind, l):
+        """Partial-sum buffer `kind` of layer l of block j (encoder / decoder
+        stage si): the block's own when the weight-norm backward is batched,
+        else the workspace's shared one."""
+        parts = w.blk_parts.get((side, si, j))
+        return parts[kind][l] if parts is not None else getattr(w, kind)[l]
 
     def _gnb(self, w, si, j):
         """GNBWD epilogue arguments: the GEMM producing dL/dc_{j+1} of encoder
@@ -983,9 +1036,9 @@ class VQVAEEngine:
                 fused_here = top_fused if j == nb - 1 else True
                 for l in reversed(range(st.L)):
                     Lr, gn = b.convs[l], b.gns[l]
-                    cs_b = self._bview(w.colsum_b[l], B, C)
-                    dg_b = self._bview(w.dgam_b[l], B, C)
-                    db_b = self._bview(w.dbet_b[l], B, C)
+                    cs_b = self._bview(self._blk(w, "enc", si, j, "colsum_b", l), B, C)
+                    dg_b = self._bview(self._blk(w, "enc", si, j, "dgam_b", l), B, C)
+                    db_b = self._bview(self._blk(w, "enc", si, j, "dbet_b", l), B, C)
                     nparts = self._gnb_parts(sw, C, fused_here) if l == st.L - 1 else 0
                     ops.gn_bwd(dy, sw.h[j][l], dh, T, 1, False, sw.mr[j][l], gn.weight, gn.bias, w.gnb_part, cs_b,
                                dg_b, db_b, nparts=nparts)
@@ -1058,9 +1111,10 @@ class VQVAEEngine:
             C2 = 2 * C
             dg = Workspace.view(w.dg_flat, sw.N, C)
             du = Workspace.view(w.du_flat, sw.N, C2)
-            dg_b, db_b = (self._bview(t[0], B, C2) for t in (w.dgam_b, w.dbet_b))
             for j in reversed(range(len(st.blocks))):
                 b = st.blocks[j]
+                dg_b = self._bview(self._blk(w, "dec", si, j, "dgam_b", 0), B, C2)
+                db_b = self._bview(self._blk(w, "dec", si, j, "dbet_b", 0), B, C2)
                 ci, gn, rs = b.conv_in, b.gn, b.rs
                 nxt = sw.dr[k ^ 1]
                 # cur = [dL/dx_{j+1} | dL/dskip]
@@ -1266,14 +1320,20 @@ class VQVAEEngine:
         codebook) is flushed at the end."""
         if self.comm is not None:
             self._grads_reset()
-        if self.plain:
-            # straight-through: the encoder's gradient comes through the decoder
-            self.decoder_bwd(w)
-            self.vq_plain_backward(w)
-            self.encoder_bwd(w)
-        else:
-            self.encoder_bwd(w)
-            self.decoder_bwd(w)
+        self._wn_pending = set()
+        self._wn_active = True
+        try:
+            if self.plain:
+                # straight-through: the encoder's gradient comes through the decoder
+                self.decoder_bwd(w)
+                self.vq_plain_backward(w)
+                self.encoder_bwd(w)
+            else:
+                self.encoder_bwd(w)
+                self.decoder_bwd(w)
+            self._wn_bwd_flush(w)
+        finally:
+            self._wn_active = False
         if self.comm is not None:
             self._grads_final(range(len(self.params)), flush=True)
             self.comm.finish()
