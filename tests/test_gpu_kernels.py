@@ -183,6 +183,24 @@ def test_convtranspose_via_weight_norm_pack(dtype, tile):
     assert relerr(dwt, wr.grad) < TOL[dtype]
 
 
+def test_weight_norm_bwd_table_chunks():
+    """vqx_weight_norm_bwd over a table longer than one launch's layers
+    (kWnMaxL = 256, the host splits it into launches; the engine's batched
+    weight-norm backward runs ~150 entries at once): 600 column-reduction
+    entries of ragged shapes, each dst the ordered column sum of its src."""
+    ops = _ops()
+    torch.manual_seed(12)
+    srcs, dsts = [], []
+    for i in range(600):
+        rows, cols = 1 + (i * 7) % 40, 8 + (i * 13) % 120
+        srcs.append(torch.randn(rows, cols, device=DEV))
+        dsts.append(torch.full((cols,), float("nan"), device=DEV))
+    ops.weight_norm_bwd(ops.wn_table([ops.colreduce_entry(s_, d_) for s_, d_ in zip(srcs, dsts)]))
+    torch.cuda.synchronize()
+    for s_, d_ in zip(srcs, dsts):
+        assert relerr(d_, s_.double().sum(0)) < 1e-6
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_weight_norm_pack_layouts(dtype):
     """vqx_weight_norm_fwd over one table of mixed layers (the flat unit grid):

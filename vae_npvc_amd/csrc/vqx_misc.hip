@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256) void wn_norm_kernel(const vqx_wn_layer* __rest
 // The grid is flat over every layer's units (WnUnits: per-layer prefix), so
 // no workgroup of a small layer launches only to exit.
 constexpr int kWnRow = 4096;
-constexpr int kWnMaxL = 128;  // layers per pack launch (the host launches larger tables in chunks)
+constexpr int kWnMaxL = 256;  // layers per launch (the host launches larger tables in chunks; 1 KiB of kernel argument)
 struct WnUnits {
   int n;
   int off[kWnMaxL + 1];
