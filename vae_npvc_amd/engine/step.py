@@ -561,7 +561,9 @@ class VQVAEEngine:
             tiles = ops.wgrad_tiles(n, T_, r, c, k, pad, self.dt, dil=dil)
             wgs = wg_solo if id(Lr) in solo else wg_1x1 if Lr.k == 1 else wg_target
             Lr.splits = max(1, min(wgs // tiles, n // min_k))
-        # slab arena: one backward group's slabs at a time (kept L2/MALL-resident).
+        # slab arena: every group's slabs in a region of their own when the
+        # weight-norm backward is batched (EngineOptions.wn_bwd_batch), else one
+        # group's slabs at a time (reused group by group, L2/MALL-resident).
         # bf16 runs keep the conv slabs in bf16 (each split's fp32 partial rounded
         # once, summed in fp32 by the weight-norm backward): half the bytes of the
         # split-K round trip.  The conditioning linears write dW directly (fp32).
