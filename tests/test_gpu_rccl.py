@@ -11,7 +11,9 @@ device-tensor collectives before the driver's 8-GPU run.
   * the engine with the communicator attached (every collective of the step:
     initial broadcast, per-group gradient all-reduces, the EMA-statistics
     bundle, owned-rows assembly) equals the plain engine bit for bit over
-    three steps, and every gradient is reduced exactly once per step;
+    three steps, and every gradient is reduced exactly once per step -- with
+    the weight-norm backward batched every 5 groups (default), per group and
+    for all groups at once;
   * bin/train.py's nccl initialisation path from torchrun-style env
     (setup_distributed), world size 1.
 """
@@ -78,8 +80,10 @@ def _worker(port, q):
         meta, _ = load_fixture("step_vcc20")
         cfg = cfg_of("vcc20", compute_dtype="fp32")
         runs = []
-        for ddp in (False, True, "end"):  # plain, all-reduce beside the backward, all after it
-            tr = make_trainer(cfg, meta["wseed"])
+        # plain, all-reduce beside the backward (weight-norm backward batched every 5 groups, every
+        # group, all groups at once), all after it
+        for ddp, chunk in ((False, 5), (True, 5), ("end", 5), (True, 1), (True, 1000)):
+            tr = make_trainer(dict(cfg, engine={"wn_bwd_ddp_groups": chunk}), meta["wseed"])
             eng = tr.engine
             calls = []
             if ddp:
@@ -124,8 +128,8 @@ def test_rccl_world1_comm_and_engine_step():
     assert out["avg_exact"] and out["gather_exact"]
     assert out["mean"] == [2.5, -1.0]
     assert out["sum"] == [7.0] * 7
-    plain, ddp, late = out["engine"]
-    for d in (ddp, late):
+    plain, ddp, late, per_group, one = out["engine"]
+    for d in (ddp, late, per_group, one):
         assert d["p"] == plain["p"] and d["e"] == plain["e"]       # bit-identical weights and codebook
         assert d["d"] == plain["d"]                                # identical loss dicts
         for calls in d["calls"]:                                   # every gradient reduced exactly once per step
@@ -135,3 +139,4 @@ def test_rccl_world1_comm_and_engine_step():
                 covered += hi - lo
             assert covered == d["n"]
     assert len(ddp["calls"][0]) > 3                                # reduced in several runs during the backward
+    assert len(per_group["calls"][0]) > len(ddp["calls"][0]) > len(one["calls"][0])

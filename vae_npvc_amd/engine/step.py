@@ -142,12 +142,14 @@ class EngineOptions:
                        workgroups per weight-gradient launch (the split-K
                        factor) of the 3-tap layers, the 1x1 layers and the
                        stage convs; wgrad_min_k: fewest frames per split
-      wn_bwd_batch     one process (no data parallelism): every backward
-                       group's weight-norm backward + bias reductions in one
-                       launch after the backward (each group's split-K slabs
-                       and partial sums kept in buffers of their own) instead
-                       of a launch per group; data parallel keeps the launch
-                       per group, whose all-reduce then overlaps the backward
+      wn_bwd_batch     the backward groups' weight-norm backward + bias
+                       reductions batched (each group's split-K slabs and
+                       partial sums kept in buffers of their own): one process
+                       runs them all in one launch after the backward; data
+                       parallel runs them every wn_bwd_ddp_groups groups, so
+                       the all-reduce of each chunk's gradients still overlaps
+                       the rest of the backward
+      wn_bwd_ddp_groups  groups per batched launch under data parallelism
       slab_f32         fp32 split-K slabs in bf16 runs (+3.3% step time,
                        profiles/r04/slab_wfirst_ab.txt)
       kernel_policy    include/vqx.h VQX_POLICY_* of every conv GEMM call"""
@@ -160,6 +162,7 @@ class EngineOptions:
     wgrad_min_k: int = 512
     slab_f32: bool = False
     wn_bwd_batch: bool = True
+    wn_bwd_ddp_groups: int = 5
     kernel_policy: int = 0
 
 
@@ -338,7 +341,8 @@ class VQVAEEngine:
         self._side_on = self.device.type == "cuda" and self.opt.side_stream
         self._side = None
         self._wn_active = False   # inside backward(): the weight-norm backward may be batched
-        self._wn_pending = set()
+        self._wn_pending = []     # groups whose weight-norm backward is batched and not yet run
+        self._wn_done = set()     # ... and those already run in this backward
 
     # ------------------------------------------------------------ parameters
     def _flatten(self):
@@ -686,7 +690,8 @@ class VQVAEEngine:
             t[("enc_stage", si)] = [self._wn_entry(st.conv, True),
                                     cr(self._bias_partials(w, first_folded, sw.cs[0]), g(st.conv.mod.bias))]
         w.bwd_tables = {k: ops.wn_table(v) for k, v in t.items()}
-        w.bwd_table_all = ops.wn_table([e for v in t.values() for e in v])  # the batched launch
+        w.bwd_entries = t
+        w.bwd_table_cache = {}  # group sequence -> table of one batched launch (_wn_run)
         # parameters whose gradients are final once a group's launch is done
         # (data parallel: their all-reduce is issued right then, parallel/ddp.py)
         w.bwd_params = {k: self._params_written([t_ for e in entries for t_ in (e.get("dv"), e.get("dg"))])
@@ -938,27 +943,43 @@ class VQVAEEngine:
 
     # ------------------------------------------------------------ backward
     def _wn_batched(self):
-        return self.opt.wn_bwd_batch and self.comm is None and self._wn_active
+        return self.opt.wn_bwd_batch and self._wn_active
 
     def _wn_bwd(self, w, key):
         """A backward group's weight-norm backward + bias/affine reductions;
         its gradients are final afterwards (data parallel: reduce them now).
-        Batched (one process): noted here, run for every group at once by
-        _wn_bwd_flush after the backward."""
+        Batched: noted here and run with other groups' in one launch -- by
+        _wn_bwd_flush after the backward (one process), or every
+        wn_bwd_ddp_groups groups (data parallel, whose all-reduces start then)."""
         if self._wn_batched():
-            self._wn_pending.add(key)
+            self._wn_pending.append(key)
+            if self.comm is not None and len(self._wn_pending) >= max(1, self.opt.wn_bwd_ddp_groups):
+                self._wn_run(w)
             return
         ops.weight_norm_bwd(w.bwd_tables[key])
         self._grads_final(w.bwd_params[key])
 
+    def _wn_run(self, w):
+        """One launch for the pending groups (their tables concatenated, cached
+        per group sequence), then their gradients are final."""
+        keys = tuple(self._wn_pending)
+        self._wn_pending = []
+        if not keys:
+            return
+        tab = w.bwd_table_cache.get(keys)
+        if tab is None:
+            tab = w.bwd_table_cache[keys] = ops.wn_table([e for k in keys for e in w.bwd_entries[k]])
+        ops.weight_norm_bwd(tab)
+        self._wn_done.update(keys)
+        self._grads_final([i for k in keys for i in w.bwd_params[k]])
+
     def _wn_bwd_flush(self, w):
         if not self._wn_batched():
             return
-        if self._wn_pending != set(w.bwd_tables):  # every group's GEMMs ran (their slabs are final)
-            raise RuntimeError(f"batched weight-norm backward: groups {set(w.bwd_tables) - self._wn_pending} "
-                               "did not run")
-        ops.weight_norm_bwd(w.bwd_table_all)
-        self._wn_pending = set()
+        done = set(self._wn_pending) | self._wn_done
+        if done != set(w.bwd_tables):  # every group's GEMMs ran (their slabs are final)
+            raise RuntimeError(f"batched weight-norm backward: groups {set(w.bwd_tables) - done} did not run")
+        self._wn_run(w)
 
     def _blk(self, w, side, si, j, kind, l):
         """Partial-sum buffer `kind` of layer l of block j (encoder / decoder
@@ -1322,7 +1343,7 @@ class VQVAEEngine:
         codebook) is flushed at the end."""
         if self.comm is not None:
             self._grads_reset()
-        self._wn_pending = set()
+        self._wn_pending, self._wn_done = [], set()
         self._wn_active = True
         try:
             if self.plain:
