@@ -428,3 +428,25 @@ def test_side_stream_path_is_bit_identical():
     assert out[0][0] == out[1][0]
     assert torch.equal(out[0][1], out[1][1])
     assert torch.equal(out[0][2], out[1][2])
+
+
+@pytest.mark.parametrize("engine", [{"wn_bwd_sort": False}, {"wn_bwd_batch": False}])
+def test_weight_norm_backward_schedules_are_bit_identical(engine):
+    """The weight-norm backward's schedule options (engine/step.py
+    EngineOptions) move no bit: batched entries in group order instead of
+    heaviest first, or a launch per backward group with the slab arena reused, give the default
+    step's losses, weights and codebook exactly over 3 bf16 steps (every
+    table entry is an independent row or column reduction)."""
+    from oracle.vqvae_cpu import seeded_batch
+    out = []
+    for opts in ({}, engine):
+        cfg = cfg_of("vcc20", compute_dtype="bf16", engine=opts)
+        tr = make_trainer(cfg, 17)
+        torch.manual_seed(3)
+        np.random.seed(3)
+        dets = [dict(tr.train_step(tuple(t.cuda() for t in seeded_batch(cfg, 4, 128, 90 + s)))[1]) for s in range(3)]
+        torch.cuda.synchronize()
+        out.append((dets, tr.engine.flat_p.detach().clone(), tr.model.quantizer.embeddings.detach().clone()))
+    assert out[0][0] == out[1][0]
+    assert torch.equal(out[0][1], out[1][1])
+    assert torch.equal(out[0][2], out[1][2])

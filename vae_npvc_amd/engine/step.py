@@ -126,6 +126,24 @@ def _tm(N):
     return (N + L.CONV_TILE_ROWS - 1) // L.CONV_TILE_ROWS
 
 
+def _wn_block_bytes(e):
+    """Approximate HBM bytes one workgroup of vqx_weight_norm_bwd moves for a
+    table entry (csrc/vqx_misc.hip wn_bwd_kernel): a column-reduce block
+    reads 32 columns of every partial row; a row block reads the row's
+    split-K slabs and v and writes dv (four rows per block on the 1x1
+    wave-per-row path)."""
+    if e["kind"] == L.WN_COLREDUCE:
+        return e["cin"] * 32 * 4
+    rows_cout = e["kind"] in (0, L.WN_RESAMPLE)
+    other = e["cin"] if rows_cout else e["cout"]
+    cols = 3 * e.get("stride", 1) * other if e["kind"] in (L.WN_RESAMPLE, L.WN_RESAMPLE_T) else other * e["k"]
+    sl = e.get("slabs")
+    es = sl.element_size() if sl is not None else 4
+    b = cols * (e.get("splits", 1) * es + 8)
+    wave_rows = e["kind"] == 0 and e["k"] == 1 and e["cin"] <= 1024 and (e["cin"] // 4) * e.get("splits", 1) <= 256
+    return 4 * b if wave_rows else b
+
+
 @dataclass
 class EngineOptions:
     """Schedule choices of the engine.  The defaults are the measured-best
@@ -150,6 +168,9 @@ class EngineOptions:
                        the all-reduce of each chunk's gradients still overlaps
                        the rest of the backward
       wn_bwd_ddp_groups  groups per batched launch under data parallelism
+      wn_bwd_sort      a batched launch's entries ordered by bytes per
+                       workgroup, heaviest first (the last workgroups of the
+                       flat grid are then short ones)
       slab_f32         fp32 split-K slabs in bf16 runs (+3.3% step time,
                        profiles/r04/slab_wfirst_ab.txt)
       kernel_policy    include/vqx.h VQX_POLICY_* of every conv GEMM call"""
@@ -163,6 +184,7 @@ class EngineOptions:
     slab_f32: bool = False
     wn_bwd_batch: bool = True
     wn_bwd_ddp_groups: int = 5
+    wn_bwd_sort: bool = True
     kernel_policy: int = 0
 
 
@@ -968,7 +990,10 @@ class VQVAEEngine:
             return
         tab = w.bwd_table_cache.get(keys)
         if tab is None:
-            tab = w.bwd_table_cache[keys] = ops.wn_table([e for k in keys for e in w.bwd_entries[k]])
+            ents = [e for k in keys for e in w.bwd_entries[k]]
+            if self.opt.wn_bwd_sort:  # entries are independent: any order gives the same bits
+                ents.sort(key=_wn_block_bytes, reverse=True)
+            tab = w.bwd_table_cache[keys] = ops.wn_table(ents)
         ops.weight_norm_bwd(tab)
         self._wn_done.update(keys)
         self._grads_final([i for k in keys for i in w.bwd_params[k]])
