@@ -168,6 +168,9 @@ class EngineOptions:
                        the all-reduce of each chunk's gradients still overlaps
                        the rest of the backward
       wn_bwd_ddp_groups  groups per batched launch under data parallelism
+      lazy_stats       the step's loss statistics snapshotted on the device
+                       and copied to the host when first read (trainer/
+                       basic.py LazyLossDetail) instead of an eager D2H
       wn_bwd_sort      a batched launch's entries ordered by bytes per
                        workgroup, heaviest first (the last workgroups of the
                        flat grid are then short ones)
@@ -185,6 +188,7 @@ class EngineOptions:
     wn_bwd_batch: bool = True
     wn_bwd_ddp_groups: int = 5
     wn_bwd_sort: bool = True
+    lazy_stats: bool = True
     kernel_policy: int = 0
 
 
