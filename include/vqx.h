@@ -366,6 +366,14 @@ int vqx_vq_ema_update(float* emb_sum, float* emb_elem, float* E, const float* bs
 int vqx_gather_rows(const float* src, int32_t ld_src, const int64_t* rows, int32_t n_out,
                     int32_t D, float* out, vqx_stream_t stream);
 
+/* The same gather with the row indices in HOST memory (int32, read during
+ * the call and passed to the kernels by value, 512 rows a launch): no
+ * host-to-device copy on the stream.  Replaces the reference's
+ * `_z[torch.randperm(N)][:K]` indexing with a CPU permutation
+ * (layers_vq.py:197,213), whose index tensor torch copies to the device. */
+int vqx_gather_rows_host(const float* src, int32_t ld_src, const int32_t* rows, int32_t n_out,
+                         int32_t D, float* out, vqx_stream_t stream);
+
 /* Commitment-loss gradient (layers_vq.py:301 backward):
  *   dz[n][d] = scale * (z[n][d] - zq[n][d])  written in dtype. */
 int vqx_vq_commit_bwd(const float* z, const float* zq, int64_t count, float scale, void* dz,
@@ -524,7 +532,7 @@ int vqx_stream_create_cu_mask(int32_t reserve_cus, vqx_stream_t* out, int32_t* c
 int vqx_stream_destroy(vqx_stream_t stream);
 
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
-#define VQX_ABI_VERSION 123
+#define VQX_ABI_VERSION 124
 int vqx_version(void);
 
 #ifdef __cplusplus

@@ -1018,3 +1018,23 @@ def test_colsum_matches_fp64_and_accumulates(dtype, n, C, ld):
     torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=tol)
     ops.colsum(x, part, out, accumulate=True, C=C)
     torch.testing.assert_close(out.double(), 2 * ref, rtol=1e-5, atol=2 * tol)
+
+
+@pytest.mark.parametrize("K,N", [(512, 16384), (1024, 300), (7, 5)])
+def test_gather_rows_host_indices_equal_device_indices(K, N):
+    """vqx_gather_rows_host (row ids in host memory, passed to the kernels by
+    value, 512 a launch) writes exactly what vqx_gather_rows does with the
+    same ids on the device, including -1 (zero rows: another rank's frames)
+    and K above one launch's 512 rows."""
+    from vae_npvc_amd import ops
+    g = torch.Generator().manual_seed(K + N)
+    D = 128
+    src = torch.randn(N, D, generator=g).cuda()
+    rows = torch.randint(-1, N, (K,), generator=g)
+    a = torch.full((K, D), 7.0, device="cuda")
+    b = torch.full((K, D), 9.0, device="cuda")
+    ops.gather_rows(src, rows.cuda(), a)
+    ops.gather_rows_host(src, rows.to(torch.int32), b)
+    assert torch.equal(a, b)
+    ref = torch.where((rows >= 0)[:, None], src.cpu()[rows.clamp_min(0)], torch.zeros(1))
+    assert torch.equal(b.cpu(), ref)

@@ -14,6 +14,8 @@
 // a lowest-index tie-break across lanes), matching torch.argmin.
 #include "vqx_common.h"
 
+#include <cstring>
+
 namespace vqx {
 
 // Code widths D (= z_dim) the kernels are built for: 64, 128 (the BASELINE
@@ -559,6 +561,19 @@ __global__ void gather_rows_kernel(const float* __restrict__ src, int ld, const 
   for (int d = threadIdx.x; d < D; d += blockDim.x) out[(int64_t)i * D + d] = (r >= 0) ? src[r * ld + d] : 0.f;
 }
 
+// row indices passed by value (vqx_gather_rows_host): kernel arguments, no copy on the stream
+constexpr int kGatherArgRows = 512;
+struct GatherIdx {
+  int32_t idx[kGatherArgRows];
+};
+__global__ void gather_rows_arg_kernel(const float* __restrict__ src, int ld, GatherIdx R, int n_out, int D,
+                                       float* __restrict__ out) {
+  const int i = blockIdx.x;
+  if (i >= n_out) return;
+  const int64_t r = R.idx[i];
+  for (int d = threadIdx.x; d < D; d += blockDim.x) out[(int64_t)i * D + d] = (r >= 0) ? src[r * ld + d] : 0.f;
+}
+
 template <typename T>
 __global__ void commit_bwd_kernel(const float* __restrict__ z, const float* __restrict__ zq, int64_t n, float scale,
                                   T* __restrict__ dz) {
@@ -654,6 +669,19 @@ extern "C" int vqx_gather_rows(const float* src, int32_t ld_src, const int64_t* 
   hipLaunchKernelGGL(gather_rows_kernel, dim3(n_out), dim3(128), 0, (hipStream_t)stream, src, ld_src, rows, n_out, D,
                      out);
   return launch_status("vqx_gather_rows");
+}
+
+extern "C" int vqx_gather_rows_host(const float* src, int32_t ld_src, const int32_t* rows, int32_t n_out, int32_t D,
+                                    float* out, vqx_stream_t stream) {
+  if (n_out <= 0 || D <= 0 || !rows) { set_error("vqx_gather_rows_host: bad arguments"); return -1; }
+  for (int i0 = 0; i0 < n_out; i0 += kGatherArgRows) {
+    GatherIdx R;
+    const int n = std::min(kGatherArgRows, n_out - i0);
+    memcpy(R.idx, rows + i0, sizeof(int32_t) * n);
+    hipLaunchKernelGGL(gather_rows_arg_kernel, dim3(n), dim3(128), 0, (hipStream_t)stream, src, ld_src, R, n, D,
+                       out + (int64_t)i0 * D);
+  }
+  return launch_status("vqx_gather_rows_host");
 }
 
 extern "C" int vqx_vq_commit_bwd(const float* z, const float* zq, int64_t count, float scale, void* dz, int32_t dtype,

@@ -919,12 +919,14 @@ class VQVAEEngine:
     # ------------------------------------------------------------ quantizer host logic
     def _perm_rows(self, n, K, rank_offset=0, n_local=None):
         """torch.randperm(n)[:K] on the CPU generator (layers_vq.py:197,213),
-        mapped to local row ids (-1 = row owned by another rank)."""
+        mapped to local row ids (-1 = row owned by another rank): a host int32
+        tensor for ops.gather_rows_host, which passes it to the kernel by
+        value (a host-to-device copy on the stream idled it ~5.5 us)."""
         perm = torch.randperm(n)[:K]
         if n_local is not None:
             from ..parallel.ddp import owned_rows
             perm = owned_rows(perm, rank_offset, n_local)
-        return perm.pin_memory().to(self.device, non_blocking=True)
+        return perm.to(torch.int32)
 
     def _tile_rows(self, w):
         """N < K path of _tile (layers_vq.py:183-190): repeat z with N(0, 0.01/sqrt(D))
@@ -1231,7 +1233,7 @@ class VQVAEEngine:
             q.embeddings.copy_(rows)
         else:
             perm = self._perm_rows(w.Nz * self.world, K, self.rank * w.Nz, w.Nz if self.comm is not None else None)
-            ops.gather_rows(w.z, perm, q.embeddings)
+            ops.gather_rows_host(w.z, perm, q.embeddings)
             if self.comm is not None:
                 self.comm.all_reduce_sum(q.embeddings)
         ops.convert_2d(q.embeddings, q.emb_sum)
@@ -1299,7 +1301,7 @@ class VQVAEEngine:
             w.rand_rows.copy_(rows)
         else:
             perm = self._perm_rows(w.Nz * self.world, K, self.rank * w.Nz, w.Nz if self.comm is not None else None)
-            ops.gather_rows(w.z, perm, w.rand_rows)
+            ops.gather_rows_host(w.z, perm, w.rand_rows)
 
     def _ema_apply(self, w):
         q = self.m.quantizer

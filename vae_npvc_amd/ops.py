@@ -438,6 +438,16 @@ def gather_rows(src, rows, out):
     return out
 
 
+def gather_rows_host(src, rows, out):
+    """out[i] = src[rows[i]] (zero rows for negative ids) with `rows` a host
+    int32 tensor passed to the kernels by value (no copy on the stream)."""
+    rows = rows.to(torch.int32).contiguous()
+    assert rows.device.type == "cpu" and rows.numel() == out.shape[0]
+    call("vqx_gather_rows_host", ptr(src), src.stride(0), rows.data_ptr(), out.shape[0], out.shape[1], ptr(out),
+         stream_ptr())
+    return out
+
+
 def vq_commit_bwd(z, zq, scale, dz):
     call("vqx_vq_commit_bwd", ptr(z), ptr(zq), z.numel(), scale, ptr(dz), dt_code(dz.dtype), stream_ptr())
     return dz
