@@ -16,6 +16,11 @@ stored):
   * vq_tile.npz/.json     the N < K tiling path (layers_vq.py:183-190)
   * jitter.json           Jitter.forward neighbour map (layers_vq.py:353-379)
   * full_step.npz/.json   2 steps at the config-2 size B=64 x T=256
+  * full_step_vcc20_b512  2 steps at B=512 x T=256 (--only-big): config 3's
+                          global batch (8 ranks x 64 x 256), pinning the
+                          single-process engine and the 8-rank data-parallel
+                          engine at config 3's real partition (≈22 GB of
+                          RAM for the reference's CPU autograd)
   * step_<cfg>_plain*     3 steps with the straight-through VectorQuantizer
                           (use_ema: false; embed_norm true / false; aishell3
                           with jitter_p 0.12), SURVEY §8f row 1
@@ -122,7 +127,9 @@ def summarize(t, n=16):
     return dict(norm=float(t.norm()), sum=float(t.sum()), head=[float(v) for v in t[:n]])
 
 
-def step_fixture(name, B, T, steps, wseed, bseed, tseed, nseed, out_prefix, keep_idx=True):
+def step_fixture(name, B, T, steps, wseed, bseed, tseed, nseed, out_prefix, keep_idx=True, compact=False):
+    """compact (the B=512 fixture): xhat slice of the first 64 utterances only,
+    top-2 gaps as float16 (the tests only ask whether a gap is < 1e-4)."""
     cfg = load_cfg(name)
     sd = seeded_state_dict(cfg, wseed)
     model = ref_model(cfg, sd)
@@ -148,7 +155,7 @@ def step_fixture(name, B, T, steps, wseed, bseed, tseed, nseed, out_prefix, keep
         meta["xhat"][str(s)] = summarize(xhat)
         if s == 0:
             meta["grads"] = {k: summarize(g) for k, g in grads.items()}
-            arrays["xhat0_slice"] = xhat[:, :, :16].numpy().astype(np.float32)
+            arrays["xhat0_slice"] = xhat[:64 if compact else B, :, :16].numpy().astype(np.float32)
         q = model.quantizer
         meta[f"embeddings{s}"] = summarize(q.embeddings)
         if not ema:
@@ -156,7 +163,7 @@ def step_fixture(name, B, T, steps, wseed, bseed, tseed, nseed, out_prefix, keep
         c = rec.calls[-1]
         if keep_idx:
             arrays[f"idx{s}"] = c["idx"].numpy().astype(np.int16)
-            arrays[f"gap{s}"] = c["gap"].numpy().astype(np.float32)
+            arrays[f"gap{s}"] = c["gap"].numpy().astype(np.float16 if compact else np.float32)
         arrays[f"emb_elem{s}"] = q.emb_elem.detach().numpy().astype(np.float32)
         meta[f"emb_sum{s}"] = summarize(q.emb_sum)
     meta["params_after"] = {k: summarize(p, 8) for k, p in model.named_parameters()}
@@ -272,6 +279,10 @@ if __name__ == "__main__":
         for i, name in enumerate(ZDIM):
             step_fixture(name, B=4, T=128, steps=3, wseed=1501 + i, bseed=2501 + i, tseed=3501 + i, nseed=4501 + i,
                          out_prefix=f"step_{name}")
+        sys.exit(0)
+    if "--only-big" in sys.argv:  # config 3's data-parallel global batch (8 x 64 x 256)
+        step_fixture("vcc20", B=512, T=256, steps=2, wseed=1004, bseed=2004, tseed=3004, nseed=4004,
+                     out_prefix="full_step_vcc20_b512", compact=True)
         sys.exit(0)
     if "--only-plain" in sys.argv:  # just the §8f row-1 fixtures
         for i, name in enumerate(VARIANTS):

@@ -105,11 +105,8 @@ def test_wgrad_tiles_reports_the_kernel_the_library_picks():
     """vqx_wgrad_tiles is host-only (no GPU): 3-tap pad-1 bf16 layers with
     T % 64 == 0 and c_dim % 64 == 0 get the tap-reuse tiling (128 r x 3 taps x
     64 c), everything else 128 x 128 tiles of the (tap, channel) columns."""
-    import os
     from vae_npvc_amd import _lib as L
     from vae_npvc_amd import ops
-    if os.environ.get("VQX_TAP_REUSE") == "0":
-        pytest.skip("tap reuse disabled in this environment")
     N, T = 64 * 256, 256
     assert ops.wgrad_tiles(N, T, 512, 512, 3, 1, L.VQX_BF16) == 4 * 8
     assert ops.wgrad_tiles(N, T, 512, 1024, 3, 1, L.VQX_BF16) == 4 * 16

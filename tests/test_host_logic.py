@@ -121,6 +121,24 @@ def test_train_step_advances_under_reference_loop(monkeypatch):
     assert tr2.train_step(batch)[0] == 22  # iteration=None counts the same way
 
 
+def test_resume_counter_restored_or_reference(monkeypatch, tmp_path):
+    """load_checkpoint restores the iteration counter by default; with
+    `reference_resume_counter` it only returns it, as the reference's
+    (trainer/basic.py:117-121), whose next train_step then returns 1."""
+    import vae_npvc_amd.trainer.basic as tb
+    ckpt = tmp_path / "c.pt"
+    torch.save({"model": {}, "optimizer": {}, "iteration": 40}, ckpt)
+    batch = (torch.zeros(1, 2, 3), torch.zeros(1, 1, dtype=torch.int64))
+    for ref_mode, expect in ((False, 41), (True, 1)):
+        tr = _loop_trainer(monkeypatch)
+        tr.engine = SimpleNamespace(train_step=lambda x, y: SimpleNamespace(stats=None), params_intact=lambda: True)
+        tr.model = SimpleNamespace(training=True, load_state_dict=lambda sd: None, _engine=tr.engine)
+        tr.optimizer = SimpleNamespace(load_state_dict=lambda sd: None)
+        tr.reference_resume_counter = ref_mode
+        assert tr.load_checkpoint(str(ckpt)) == 40
+        assert tr.train_step(batch, iteration=41)[0] == expect
+
+
 def test_load_state_dict_resizes_plain_codebook():
     """vqvae.py:106-119: a straight-through-VQ checkpoint with another codebook
     size rebuilds the quantizer at the checkpoint's shape and loads."""

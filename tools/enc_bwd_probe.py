@@ -46,7 +46,7 @@ if __name__ == "__main__" and not os.environ.get("PROBE_STATS") and not os.envir
         c = copy.deepcopy(base)
         c["encoder"]["stacks"] = [stacks]
         try:
-            run(c, f"vcc20 fp32 encoder stacks={stacks} fuse_gn={os.environ.get('VQX_FUSE_GN', '1')}")
+            run(c, f"vcc20 fp32 encoder stacks={stacks}")
         except Exception as e:  # noqa: BLE001
             print(f"== stacks={stacks}: {e!r}")
 

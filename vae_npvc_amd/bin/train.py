@@ -112,7 +112,7 @@ def train(args):
     config = yaml.safe_load(open(args.config))  # host only: the process group comes before any GPU call
     # rank 0 alone validates at a checkpoint while the others wait in a barrier:
     # a long validation set needs more than torch's default collective timeout
-    world, rank, backend = setup_distributed(getattr(args, "backend", None), config.get("dist_timeout_s", 7200))
+    world, rank, backend = setup_distributed(getattr(args, "backend", None), config.get("dist_timeout_s"))
     ddp = world > 1
     output_dir = args.output_dir
     checkpoint_path = args.checkpoint

@@ -673,7 +673,10 @@ extern "C" int vqx_gather_rows(const float* src, int32_t ld_src, const int64_t* 
 
 extern "C" int vqx_gather_rows_host(const float* src, int32_t ld_src, const int32_t* rows, int32_t n_out, int32_t D,
                                     float* out, vqx_stream_t stream) {
-  if (n_out <= 0 || D <= 0 || !rows) { set_error("vqx_gather_rows_host: bad arguments"); return -1; }
+  if (n_out <= 0 || D <= 0 || !rows || !src || !out || ld_src < D) {
+    set_error("vqx_gather_rows_host: bad arguments");
+    return -1;
+  }
   for (int i0 = 0; i0 < n_out; i0 += kGatherArgRows) {
     GatherIdx R;
     const int n = std::min(kGatherArgRows, n_out - i0);

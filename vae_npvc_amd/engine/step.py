@@ -391,7 +391,9 @@ class VQVAEEngine:
         self._p0_ptr = params[0].data_ptr()
         enc_ids = {id(p) for p in self.m.encoder.parameters()}
         self.enc_end = sum(p.numel() for p in params if id(p) in enc_ids)
-        assert all(id(p) in enc_ids for p in params[: len(enc_ids)]), 'encoder parameters must come first'
+        if not all(id(p) in enc_ids for p in params[: len(enc_ids)]):
+            raise ValueError("the encoder's parameters must come first in model.parameters() "
+                             "(the flat gradient buffer is all-reduced encoder-first)")
 
     def params_intact(self):
         return self.params[0].data_ptr() == self._p0_ptr and all(
@@ -791,7 +793,8 @@ class VQVAEEngine:
             ops.conv_wgrad(dy, x, Lr.slab, T=T, r_dim=Lr.cout, c_dim=Lr.cin, ntaps=Lr.k, pad=Lr.pad, dil=Lr.dil,
                            shift_sign=1, q_prologue=pro, pro_scale=scale, splits=Lr.splits, policy=pol)
             return
-        assert pro == L.PRO_NONE
+        if pro != L.PRO_NONE:
+            raise ValueError(f"weight-gradient prologue {pro} is defined for plain convs only (layer kind {Lr.kind})")
         if Lr.kind == KIND_CONVT:
             ops.conv_wgrad(x, dy, Lr.slab, T=T, r_dim=Lr.cin, c_dim=Lr.cout, ntaps=Lr.k, pad=Lr.pad, dil=Lr.dil,
                            shift_sign=-1, splits=Lr.splits, policy=pol)
@@ -1431,7 +1434,8 @@ class VQVAEEngine:
         """One full training step (trainer/basic.py:55-79): forward, backward,
         clip, Adam, StepLR, EMA codebook update.  Returns the device stats
         vector [x_loss, sqerr, -, -, entropy, used_curr, usage, diff_emb]."""
-        assert self.opt_ready, "init_optimizer() first"
+        if not self.opt_ready:
+            raise RuntimeError("init_optimizer() first")
         w = self.forward_train(x, y)
         self.backward(w)
         self.optimizer_step()

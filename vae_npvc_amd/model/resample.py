@@ -117,7 +117,8 @@ class _ResampleFn(torch.autograd.Function):
             raise L.VqxError("ResampleConv1d runs on the MI355X only (libvqx); move it with .cuda()")
         B, C, T = x.shape
         s, cd, dev = mod.scale, mod.cd, x.device
-        assert C == mod.cin
+        if C != mod.cin:
+            raise ValueError(f"ResampleConv1d: input has {C} channels, the layer takes {mod.cin}")
         R, FC = mod.rows, mod.fold_c
         wp = torch.empty(R, 3 * s * FC, device=dev, dtype=cd)
         norm = torch.empty(R, device=dev, dtype=F32)

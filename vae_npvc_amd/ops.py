@@ -428,7 +428,8 @@ def vq_ema_update(emb_sum, emb_elem, E, bsum, bcnt, rand_rows, mu, threshold, di
     K, D = E.shape
     if partials is None:
         partials = torch.empty((K * D + 1023) // 1024, device=E.device, dtype=torch.float32)
-    assert partials.numel() >= (K * D + 1023) // 1024
+    if partials.numel() < (K * D + 1023) // 1024:
+        raise ValueError(f"vq_ema_update: workspace {partials.numel()} < {(K * D + 1023) // 1024} floats")
     call("vqx_vq_ema_update", ptr(emb_sum), ptr(emb_elem), ptr(E), ptr(bsum), ptr(bcnt), ptr(rand_rows), K, D,
          mu, threshold, ptr(diag), ptr(partials), stream_ptr())
 
@@ -441,8 +442,14 @@ def gather_rows(src, rows, out):
 def gather_rows_host(src, rows, out):
     """out[i] = src[rows[i]] (zero rows for negative ids) with `rows` a host
     int32 tensor passed to the kernels by value (no copy on the stream)."""
+    _check_cuda(src, out)
+    if rows.device.type != "cpu" or rows.numel() != out.shape[0]:
+        raise ValueError("gather_rows_host: rows must be a host tensor of out.shape[0] ids")
+    if not out.is_contiguous() or out.dim() != 2 or out.shape[1] > src.shape[1] or src.stride(1) != 1:
+        raise ValueError("gather_rows_host: out must be contiguous [n, D] with D <= src's row width")
+    if rows.numel() and (int(rows.max()) >= src.shape[0] or int(rows.min()) < -1):
+        raise ValueError(f"gather_rows_host: row ids must lie in [-1, {src.shape[0]})")
     rows = rows.to(torch.int32).contiguous()
-    assert rows.device.type == "cpu" and rows.numel() == out.shape[0]
     call("vqx_gather_rows_host", ptr(src), src.stride(0), rows.data_ptr(), out.shape[0], out.shape[1], ptr(out),
          stream_ptr())
     return out

@@ -133,6 +133,12 @@ class Trainer(object):
         self.grad_sync = str(config.get("grad_sync", "overlap"))
         if self.grad_sync not in ("overlap", "end"):
             raise ValueError(f"grad_sync must be 'overlap' or 'end', not {self.grad_sync!r}")
+        # load_checkpoint restores the iteration counter (a resumed run continues at
+        # checkpoint + 1).  The reference's load_checkpoint returns the checkpoint's
+        # iteration without restoring its counter (trainer/basic.py:117-121), so its
+        # first train_step after a resume returns 1 and bin/train.py's loop restarts
+        # counting there; `reference_resume_counter: true` keeps that behaviour.
+        self.reference_resume_counter = bool(config.get("reference_resume_counter", False))
 
         module = import_module(model_type[0], package=None)
         model_name = "Model" if len(model_type) < 2 else model_type[1]
@@ -163,7 +169,9 @@ class Trainer(object):
                                    kind=self.optim_kind)
 
     def train_step(self, input, iteration=None):
-        assert self.model.training
+        if not self.model.training:
+            raise RuntimeError("train_step needs the model in training mode (valid_step restores it; "
+                               "call model.train() after a manual model.eval())")
         x, y = input
         x = x.to(self.device, non_blocking=True).float().contiguous()
         y = y.to(self.device, non_blocking=True)
@@ -172,7 +180,8 @@ class Trainer(object):
         # trainer's own counter advances (bin/train.py:126 feeds the returned
         # value back in).  The reference's iteration=None branch raises
         # (None + 1); here it counts the same way.  load_checkpoint restores
-        # the counter, so a resumed run continues at checkpoint + 1.
+        # the counter, so a resumed run continues at checkpoint + 1 (unless
+        # reference_resume_counter: the reference's restart at 1).
         self.iteration += 1
         return self.iteration, LazyLossDetail(self.engine, w, w.stats)
 
@@ -206,5 +215,6 @@ class Trainer(object):
         if self.model._engine is not self.engine or not self.engine.params_intact():
             self._setup_engine()  # the codebook was resized (Model.load_state_dict, vqvae.py:106-119)
         self.optimizer.load_state_dict(data["optimizer"])
-        self.iteration = int(data["iteration"])
-        return self.iteration
+        if not self.reference_resume_counter:
+            self.iteration = int(data["iteration"])
+        return int(data["iteration"])
