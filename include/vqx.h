@@ -139,6 +139,8 @@ typedef struct vqx_conv_args {
 #define VQX_POLICY_TALL256 2
 #define VQX_POLICY_TALL512 3
 #define VQX_POLICY_TR128 4
+#define VQX_POLICY_K1_3PCU 5  /* ABI 125: as AUTO, but every bf16 1x1 FWD and DGRAD+WGRAD on the
+                                 three-workgroups-per-CU kernels (one round with spare slots) */
 
 int vqx_conv1d_fwd(const vqx_conv_args* a, vqx_stream_t stream);
 int vqx_conv1d_dgrad(const vqx_conv_args* a, vqx_stream_t stream);
@@ -225,8 +227,27 @@ typedef struct vqx_wn_layer {
  * replays without host work). */
 int vqx_weight_norm_fwd(const vqx_wn_layer* layers_host, const vqx_wn_layer* layers_dev,
                         int32_t n_layers, vqx_stream_t stream);
+/* The same with flags (ABI 125): VQX_WNF_NORMS_READY skips the ConvTranspose
+ * row norms (kind 1): vqx_adam_step_wn has written them for the current v. */
+#define VQX_WNF_NORMS_READY 1
+int vqx_weight_norm_fwd_flags(const vqx_wn_layer* layers_host, const vqx_wn_layer* layers_dev,
+                              int32_t n_layers, int32_t flags, vqx_stream_t stream);
 int vqx_weight_norm_bwd(const vqx_wn_layer* layers_host, const vqx_wn_layer* layers_dev,
                         int32_t n_layers, vqx_stream_t stream);
+/* The same launch, also leaving the sum of squares of every gradient value it
+ * writes (dv, dg, column reductions) as per-wave partials in
+ * sq_partials[0 .. count) (ABI 125; count from vqx_weight_norm_bwd_partials):
+ * the global gradient norm of clip_grad_norm_ (trainer/basic.py:63-67)
+ * without re-reading the 125 MB gradient.  vqx_sq_norm_finish then sums the
+ * partials and g^2 over the flat ranges [off, off+len) the weight-norm
+ * backward does not write (ranges: int64 pairs, device memory), each in a
+ * fixed order, into out[0] -- what vqx_grad_sq_norm computes, summed in
+ * another order. */
+int vqx_weight_norm_bwd_partials(const vqx_wn_layer* layers_host, int32_t n_layers, int64_t* count);
+int vqx_weight_norm_bwd_sq(const vqx_wn_layer* layers_host, const vqx_wn_layer* layers_dev,
+                           int32_t n_layers, float* sq_partials, int64_t sq_capacity, vqx_stream_t stream);
+int vqx_sq_norm_finish(const float* partials, int64_t n_partials, const float* g, const int64_t* ranges,
+                       int32_t n_ranges, float* scratch /* >= 64 floats */, float* out, vqx_stream_t stream);
 
 /*
  * GroupNorm statistics (nn.GroupNorm, layers.py:154 (G=1), layers.py:201
@@ -439,6 +460,22 @@ int vqx_adam_hyper(int64_t* step, double lr0, double gamma, int32_t step_size, d
                    double beta2, double eps, float* hyper, vqx_stream_t stream);
 int vqx_adam_step(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper,
                   const float* sumsq, float max_norm, vqx_stream_t stream);
+/* adam_step with the next forward's weight-norm preparation fused in (ABI
+ * 125; replaces the per-step torch weight_norm recomputation of
+ * w = g*v/||v||, vqvae.py:203-208 / 329-334, that vqx_weight_norm_fwd does
+ * otherwise).  rows: weight-normed convs (vqx_wn_layer with v, g pointing into
+ * p; kind 0 needs w_packed) whose rows of v and gains g this launch updates,
+ * writing norm[o] = ||v_o|| of the updated row and, for kind 0, the packed
+ * weights -- bit for bit what vqx_weight_norm_fwd computes from the updated
+ * parameters; kind 1 (ConvT) rows get their norms, to be packed by
+ * vqx_weight_norm_fwd_flags(VQX_WNF_NORMS_READY).  segs: (offset, length)
+ * int64 pairs covering every other element of p (host and device copies);
+ * rows + segs must cover [0, n) exactly.  The update of every element is
+ * adam_step's, bit for bit.  At most 128 layers and 128 segments. */
+int vqx_adam_step_wn(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper,
+                     const float* sumsq, float max_norm, const vqx_wn_layer* rows_host,
+                     const vqx_wn_layer* rows_dev, int32_t n_layers, const int64_t* segs_host,
+                     const int64_t* segs_dev, int32_t n_segs, vqx_stream_t stream);
 
 /* RAdam, optim_type: RAdam (replaces trainer/radam.py:5-78 RAdam.step, built
  * by trainer/basic.py:30-34 with betas (0.5, 0.999), weight_decay 0).
@@ -501,7 +538,8 @@ int vqx_convert_2d(const void* src, int32_t ld_src, int32_t src_dtype, void* dst
  * per tile, two 4-wave K groups per tile), the rest one group per 128 x 128
  * tile.  Callers size `splits` (and the slab buffer) from it. */
 int vqx_wgrad_tiles(int64_t n_rows, int32_t T, int32_t r_dim, int32_t c_dim, int32_t ntaps, int32_t pad,
-                    int32_t dil, int32_t dtype, int32_t q_prologue, int32_t* tiles);
+                    int32_t dil, int32_t dtype, int32_t q_prologue, int32_t kernel_policy /* ABI 125 */,
+                    int32_t* tiles);
 
 /* Thread-local description of the last failure. */
 const char* vqx_last_error(void);
@@ -532,7 +570,7 @@ int vqx_stream_create_cu_mask(int32_t reserve_cus, vqx_stream_t* out, int32_t* c
 int vqx_stream_destroy(vqx_stream_t stream);
 
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
-#define VQX_ABI_VERSION 124
+#define VQX_ABI_VERSION 125
 int vqx_version(void);
 
 #ifdef __cplusplus

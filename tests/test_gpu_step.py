@@ -430,21 +430,156 @@ def test_side_stream_path_is_bit_identical():
     assert torch.equal(out[0][2], out[1][2])
 
 
+def _named_cfg(name, **over):
+    """cfg_of plus the straight-through variant `vcc20_plain` (use_ema: false)."""
+    if name == "vcc20_plain":
+        return cfg_of("vcc20", use_ema=False, **over)
+    return cfg_of(name, **over)
+
+
+@pytest.mark.parametrize("name", ["vcc20", "vcc20_plain", "vcc20_multi", "vcc20_nown"])
 @pytest.mark.parametrize("engine", [{"wn_bwd_sort": False}, {"wn_bwd_batch": False}])
-def test_weight_norm_backward_schedules_are_bit_identical(engine):
+def test_weight_norm_backward_schedules_are_bit_identical(engine, name):
     """The weight-norm backward's schedule options (engine/step.py
     EngineOptions) move no bit: batched entries in group order instead of
     heaviest first, or a launch per backward group with the slab arena reused, give the default
     step's losses, weights and codebook exactly over 3 bf16 steps (every
-    table entry is an independent row or column reduction)."""
+    table entry is an independent row or column reduction).  Each partial-sum
+    buffer must belong to one group for that to hold, so the straight-through
+    path (decoder, then VQ, then encoder), the two-stage topology (folded
+    column sums) and the configuration without weight norm are covered too.
+    Both arms take the gradient norm by re-reading the gradient
+    (fuse_grad_norm off): the fused norm's partials follow the launch's entry
+    order, which is what the options change."""
     from oracle.vqvae_cpu import seeded_batch
     out = []
     for opts in ({}, engine):
-        cfg = cfg_of("vcc20", compute_dtype="bf16", engine=opts)
+        cfg = _named_cfg(name, compute_dtype="bf16", engine=dict(opts, fuse_grad_norm=False))
         tr = make_trainer(cfg, 17)
         torch.manual_seed(3)
         np.random.seed(3)
         dets = [dict(tr.train_step(tuple(t.cuda() for t in seeded_batch(cfg, 4, 128, 90 + s)))[1]) for s in range(3)]
+        torch.cuda.synchronize()
+        out.append((dets, tr.engine.flat_p.detach().clone(), tr.model.quantizer.embeddings.detach().clone()))
+    assert out[0][0] == out[1][0]
+    assert torch.equal(out[0][1], out[1][1])
+    assert torch.equal(out[0][2], out[1][2])
+
+
+@pytest.mark.parametrize("name,dtype", [("vcc20", "bf16"), ("vcc20", "fp32"), ("vcc20_plain", "fp32"),
+                                        ("vcc20_multi_nown", "fp32"), ("aishell3", "bf16")])
+def test_fused_gradient_norm_equals_rereading_the_gradient(name, dtype):
+    """fuse_grad_norm (the default in one process): the clip's global norm
+    comes from sum-of-squares partials the batched weight-norm backward leaves
+    as it writes the gradients, plus g^2 over the parameters it does not write
+    (speaker embedding, straight-through codebook, ...).  Against the float64
+    sum of squares of the step's whole flat gradient: 1e-5 relative (an fp32
+    sum in another order); and three steps with it equal three steps re-reading
+    the gradient (vqx_grad_sq_norm) within 1e-5 of the parameter norm (1e-3
+    for aishell3 in bf16, whose jitter and bf16 roundings amplify the
+    difference through codebook near-ties)."""
+    from oracle.vqvae_cpu import seeded_batch
+    out = []
+    for fuse in (True, False):
+        cfg = _named_cfg(name, compute_dtype=dtype, engine={"fuse_grad_norm": fuse})
+        tr = make_trainer(cfg, 23)
+        torch.manual_seed(4)
+        np.random.seed(4)
+        for s in range(3):
+            tr.train_step(tuple(t.cuda() for t in seeded_batch(cfg, 4, 128, 70 + s)))
+            if s == 0:
+                torch.cuda.synchronize()
+                ref = float((tr.engine.flat_g.double() ** 2).sum())
+                got = float(tr.engine.sumsq.item())
+                assert abs(got - ref) <= 1e-5 * ref, (fuse, got, ref)
+        torch.cuda.synchronize()
+        out.append(tr.engine.flat_p.detach().double().clone())
+    d = float((out[0] - out[1]).norm() / out[1].norm())
+    # fp32: 1e-5 (measured <= 1.3e-6).  aishell3 bf16 (jitter): an fp32-rounding change of the clip
+    # coefficient moves bf16 roundings of the next steps' activations and with
+    # them codebook near-ties, so three steps drift apart at the 1e-4 level
+    assert d <= (1e-5 if dtype == "fp32" or name == "vcc20" else 1e-3), d
+
+
+@pytest.mark.parametrize("name,dtype", [("vcc20", "bf16"), ("vcc20", "fp32"), ("aishell3", "bf16"),
+                                        ("vcc20_multi", "fp32"), ("vcc20_nown", "bf16")])
+def test_fused_adam_weight_norm_preparation_is_bit_identical(name, dtype):
+    """fuse_adam_wn (the default): Adam updates weight_v row by row, writes
+    each row's norm of the updated v and, for Conv1d layers, the next
+    forward's packed w = g*v/||v||; the forward then packs only the
+    ConvTranspose layers.  Over three steps the parameters, both Adam moments,
+    the losses, and -- after one more pack_weights -- every layer's packed
+    weights and row norms equal the separate Adam + weight-norm passes bit for
+    bit (vcc20: Conv1d + ConvT rows; the two-stage topology adds resampling
+    convs, which keep the separate pack; without weight norm nothing fuses)."""
+    from oracle.vqvae_cpu import seeded_batch
+    out = []
+    for fuse in (True, False):
+        cfg = cfg_of(name, compute_dtype=dtype, engine={"fuse_adam_wn": fuse})
+        tr = make_trainer(cfg, 29)
+        eng = tr.engine
+        torch.manual_seed(5)
+        np.random.seed(5)
+        dets = [dict(tr.train_step(tuple(t.cuda() for t in seeded_batch(cfg, 4, 128, 50 + s)))[1]) for s in range(3)]
+        if fuse and name != "vcc20_nown":
+            assert eng._adam_wn is not None and eng._packed_version == eng._param_version()
+        eng.pack_weights()
+        torch.cuda.synchronize()
+        out.append((dets, eng.flat_p.clone(), eng.exp_avg.clone(), eng.exp_avg_sq.clone(),
+                    [Lr.wp.clone() for Lr in eng.convs],
+                    [Lr.norm.clone() for Lr in eng.convs if getattr(Lr.mod, "has_weight_norm", True)]))
+    a, b = out
+    assert a[0] == b[0]
+    for x, y in zip(a[1:4], b[1:4]):
+        assert torch.equal(x, y)
+    for i, (x, y) in enumerate(zip(a[4], b[4])):
+        assert torch.equal(x, y), ("packed", i)
+    for i, (x, y) in enumerate(zip(a[5], b[5])):
+        assert torch.equal(x, y), ("norm", i)
+
+
+def test_fused_adam_packing_follows_external_parameter_edits():
+    """Packed weights written by the fused Adam are used only while the
+    parameters are the ones it wrote (flat_p's version counter): an in-place
+    edit between steps (load_state_dict, a manual copy_) makes the next forward
+    pack every layer again, as without the fusion."""
+    from oracle.vqvae_cpu import seeded_batch
+    cfg = cfg_of("vcc20", compute_dtype="bf16")
+    tr = make_trainer(cfg, 31)
+    eng = tr.engine
+    torch.manual_seed(6)
+    np.random.seed(6)
+    tr.train_step(tuple(t.cuda() for t in seeded_batch(cfg, 4, 128, 60)))
+    assert eng._packed_version == eng._param_version()
+    Lr = eng.convs[1]
+    with torch.no_grad():
+        Lr.mod.weight_v.mul_(0.5)  # w = g*v/||v|| is invariant to scaling v, its norm is not
+    assert eng._packed_version != eng._param_version()
+    eng.pack_weights()
+    torch.cuda.synchronize()
+    v = Lr.mod.weight_v.detach().double()
+    ref = v.reshape(v.shape[0], -1).norm(dim=1).float()
+    assert torch.allclose(Lr.norm, ref.to(Lr.norm.device), rtol=1e-6, atol=0), "norms not recomputed"
+    tr.train_step(tuple(t.cuda() for t in seeded_batch(cfg, 4, 128, 61)))
+    assert eng._packed_version == eng._param_version()
+    tr.model.load_state_dict(tr.model.state_dict())  # Model.load_state_dict invalidates explicitly too
+    assert eng._packed_version is None
+
+
+@pytest.mark.parametrize("name", ["vcc20", "aishell3"])
+def test_three_per_cu_1x1_policy_is_bit_identical(name):
+    """kernel_policy 5 (VQX_POLICY_K1_3PCU): every bf16 1x1 FWD and DGRAD+WGRAD
+    on the three-workgroups-per-CU kernels (32-deep K-tiles in a 3-deep ring)
+    -- the same MFMA sequence over K, so three bf16 steps give the default
+    policy's losses, weights and codebook bit for bit."""
+    from oracle.vqvae_cpu import seeded_batch
+    out = []
+    for pol in (0, 5):
+        cfg = cfg_of(name, compute_dtype="bf16", engine={"kernel_policy": pol})
+        tr = make_trainer(cfg, 37)
+        torch.manual_seed(8)
+        np.random.seed(8)
+        dets = [dict(tr.train_step(tuple(t.cuda() for t in seeded_batch(cfg, 4, 256, 40 + s)))[1]) for s in range(3)]
         torch.cuda.synchronize()
         out.append((dets, tr.engine.flat_p.detach().clone(), tr.model.quantizer.embeddings.detach().clone()))
     assert out[0][0] == out[1][0]

@@ -15,7 +15,7 @@ from pathlib import Path
 import torch  # noqa: F401  (loads the HIP runtime first; see module docstring)
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libvqx.so"
-ABI_VERSION = 124  # include/vqx.h VQX_ABI_VERSION
+ABI_VERSION = 125  # include/vqx.h VQX_ABI_VERSION
 
 VQX_F32, VQX_BF16 = 0, 1
 PRO_NONE, PRO_LRELU, PRO_RELU, PRO_SCALE_RELU = 0, 1, 2, 3
@@ -79,6 +79,12 @@ _SIGS = {
                                c_void_p],
     "vqx_weight_norm_fwd": [c_void_p, c_void_p, c_int32, c_void_p],
     "vqx_weight_norm_bwd": [c_void_p, c_void_p, c_int32, c_void_p],
+    "vqx_weight_norm_fwd_flags": [c_void_p, c_void_p, c_int32, c_int32, c_void_p],
+    "vqx_adam_step_wn": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_float, c_void_p,
+                         c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_void_p],
+    "vqx_weight_norm_bwd_partials": [c_void_p, c_int32, c_void_p],
+    "vqx_weight_norm_bwd_sq": [c_void_p, c_void_p, c_int32, c_void_p, c_int64, c_void_p],
+    "vqx_sq_norm_finish": [c_void_p, c_int64, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p],
     "vqx_groupnorm_stats": [c_void_p, c_int32, c_int32, c_int64, c_int32, c_int32, c_int32, c_float, c_void_p,
                             c_void_p, c_void_p],
     "vqx_gn_lrelu_fwd": [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int64, c_int32, c_int32, c_void_p,
@@ -114,7 +120,7 @@ _SIGS = {
     "vqx_adam_hyper": [c_void_p, c_double, c_double, c_int32, c_double, c_double, c_double, c_void_p, c_void_p],
     "vqx_linear_batched_fwd": [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p],
     "vqx_linear_batched_bwd": [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p],
-    "vqx_wgrad_tiles": [c_int64, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
+    "vqx_wgrad_tiles": [c_int64, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
                         ctypes.POINTER(c_int32)],
     "vqx_vq_normalize": [c_void_p, c_int64, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p, c_void_p],

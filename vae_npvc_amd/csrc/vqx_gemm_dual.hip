@@ -53,6 +53,18 @@ __global__ __launch_bounds__(256, 2) void dual_k1_kernel(GemmParams PD, GemmPara
   else conv_gemm_body<bf16_t, MODE_WGRAD, VQX_PRO_NONE, false, 64, 2, EK_NONE>(PW, b - nd, nw, smem);
 }
 
+// the same, three workgroups per CU (32-deep K-tiles in a 3-deep ring, 48 KiB
+// of LDS): kernel policy POL_K1_3PCU.  The DGRAD round then leaves a third of
+// the slots free, which the WGRAD workgroups (or co-resident kernels) take.
+template <int EKD>
+__global__ __launch_bounds__(256, 3) void dual_k1_3_kernel(GemmParams PD, GemmParams PW, int nd, int nw, int ch) {
+  __shared__ __attribute__((aligned(16))) char smem[conv_gemm_smem<bf16_t, 32, 3>()];
+  (void)ch;
+  const int b = blockIdx.x;
+  if (b < nd) conv_gemm_body<bf16_t, MODE_DGRAD, VQX_PRO_NONE, false, 32, 3, EKD>(PD, b, nd, smem);
+  else conv_gemm_body<bf16_t, MODE_WGRAD, VQX_PRO_NONE, false, 32, 3, EK_NONE>(PW, b - nd, nw, smem);
+}
+
 // 3-tap layer: conv_tr_kernel DGRAD (epilogue kind EKD) + wgrad_tr_kernel
 template <int EKD>
 __global__ __launch_bounds__(256, 2) void dual_tr_kernel(GemmParams PD, GemmParams PW, int nd, int nw, int ch) {
@@ -78,18 +90,29 @@ bool launch_dual(const GemmParams& PD, int nd, const GemmParams& PW, int nw, hip
     }
   } else if (PD.ntaps == 1 && PW.ntaps == 1 && PW.tap_reuse == 0 && nd % 8 == 0) {
     kind = 3;
-    switch (ekd) {
-      case EK_NONE: fn = (const void*)dual_k1_kernel<EK_NONE>; break;
-      case EK_ELEM: fn = (const void*)dual_k1_kernel<EK_ELEM>; break;
-      case EK_COLSUM: fn = (const void*)dual_k1_kernel<EK_COLSUM>; break;
-      case EK_GNBWD: fn = (const void*)dual_k1_kernel<EK_GNBWD>; break;
-      default: return false;
+    if (PD.policy == POL_K1_3PCU) {
+      kind = 4;
+      switch (ekd) {
+        case EK_NONE: fn = (const void*)dual_k1_3_kernel<EK_NONE>; break;
+        case EK_ELEM: fn = (const void*)dual_k1_3_kernel<EK_ELEM>; break;
+        case EK_COLSUM: fn = (const void*)dual_k1_3_kernel<EK_COLSUM>; break;
+        case EK_GNBWD: fn = (const void*)dual_k1_3_kernel<EK_GNBWD>; break;
+        default: return false;
+      }
+    } else {
+      switch (ekd) {
+        case EK_NONE: fn = (const void*)dual_k1_kernel<EK_NONE>; break;
+        case EK_ELEM: fn = (const void*)dual_k1_kernel<EK_ELEM>; break;
+        case EK_COLSUM: fn = (const void*)dual_k1_kernel<EK_COLSUM>; break;
+        case EK_GNBWD: fn = (const void*)dual_k1_kernel<EK_GNBWD>; break;
+        default: return false;
+      }
     }
   } else {
     return false;
   }
   const double flops = 2.0 * (double)PD.n_rows * PD.Nc * PD.K + 2.0 * (double)PW.n_rows * PW.Mc * PW.Nc;
-  // probe label: mode 3 = dual, prologue slot = kind (2: 3-tap, 3: 1x1 in sequence), gen = 5
+  // probe label: mode 3 = dual, prologue slot = kind (2: 3-tap, 3: 1x1 in sequence, 4: 1x1 three per CU), gen = 5
   const int info[5] = {VQX_BF16, 3, kind, 5, ekd};
   const int chunk = 256;  // interleave period: blocks of each GEMM per group (profiles/r02/chunk_probe.txt)
   GemmParams pd = PD, pw = PW;

@@ -18,32 +18,37 @@ constexpr float kLog2Pi = 1.8378770664093453f;  // log(2*pi), layers.py:8
 // o = ci, effective tap j' = k-1-j.  Packed effective weight:
 // wp[co][j*cin + ci].
 // Row norms of the ConvTranspose layers (rows = cin, contiguous cout*k):
-// one wave per row, 4 rows per block.  Conv1d layers get theirs in the pack.
+// one 256-thread block per row, thread t the elements 4t + 1024u + (0..3)
+// summed in u order as fmaf(x0, x0, fmaf(x1, x1, fmaf(x2, x2, fmaf(x3, x3, s)))),
+// then the block sum: the order adam_wn_kernel uses, so both give the same
+// bits.  Conv1d layers get theirs in the pack.
 __global__ __launch_bounds__(256) void wn_norm_kernel(const vqx_wn_layer* __restrict__ L, int n_layers) {
   const vqx_wn_layer& l = L[blockIdx.y];
   if (l.kind != 1 || !l.g) return;
-  const int o = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int o = blockIdx.x;
   if (o >= l.cin) return;
+  __shared__ float red[16];
   const int cols = l.cout * l.k;
   const float* v = l.v + (int64_t)o * cols;
   float s = 0.f;
   if ((cols & 3) == 0 && (((uintptr_t)v) & 15) == 0 && cols <= 4096) {
-    // the lane's 16-B loads all in flight before the first add (a runtime
-    // loop of load + add paid one memory latency per iteration)
-    f32x4_t xv[16];
+    // the thread's 16-B loads all in flight before the first add
+    f32x4_t xv[4];
 #pragma unroll
-    for (int u = 0; u < 16; ++u)
-      xv[u] = 256 * u < cols ? *(const f32x4_t*)(v + min(lane * 4 + 256 * u, cols - 4)) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < 4; ++u)
+      xv[u] = 1024 * u < cols ? *(const f32x4_t*)(v + min((int)threadIdx.x * 4 + 1024 * u, cols - 4))
+                              : f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
+    for (int u = 0; u < 4; ++u) {
       const f32x4_t x = xv[u];
-      if (lane * 4 + 256 * u < cols) s = fmaf(x[0], x[0], fmaf(x[1], x[1], fmaf(x[2], x[2], fmaf(x[3], x[3], s))));
+      if ((int)threadIdx.x * 4 + 1024 * u < cols)
+        s = fmaf(x[0], x[0], fmaf(x[1], x[1], fmaf(x[2], x[2], fmaf(x[3], x[3], s))));
     }
   } else {
-    for (int i = lane; i < cols; i += 64) s = fmaf(v[i], v[i], s);
+    for (int i = threadIdx.x; i < cols; i += 256) s = fmaf(v[i], v[i], s);
   }
-  s = wave_sum(s);
-  if (lane == 0) l.norm[o] = sqrtf(s);
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) l.norm[o] = sqrtf(s);
 }
 
 // Pack w = g*v/||v|| into the effective-conv layout wp[co][j][ci].
@@ -83,7 +88,7 @@ __global__ __launch_bounds__(256) void wn_pack_kernel(const vqx_wn_layer* __rest
   const vqx_wn_layer& l = L[lo];
   const int unit = (int)blockIdx.x - U.off[lo];
   const int K = l.k, cin = l.cin, cout = l.cout;
-  __shared__ float buf[kWnBuf];
+  __shared__ __attribute__((aligned(16))) float buf[kWnBuf];
   __shared__ float red[16];
   if (l.kind == VQX_WN_RESAMPLE || l.kind == VQX_WN_RESAMPLE_T) {
     // strided conv (include/vqx.h): row r of v, norm, then the folded 3-tap row
@@ -159,16 +164,37 @@ __global__ __launch_bounds__(256) void wn_pack_kernel(const vqx_wn_layer* __rest
     float s = 0.f;
     // the row's loads all in flight before the first use (a load + use per
     // iteration of a runtime-bound loop paid one memory latency each)
-    float xr[kWnRow / 256];
+    if ((cols & 3) == 0 && (((uintptr_t)v) & 15) == 0) {
+      // 16-B partition: thread t holds elements 4t + 1024u + (0..3), summed in
+      // u order as fmaf(x0, x0, fmaf(x1, x1, fmaf(x2, x2, fmaf(x3, x3, s)))):
+      // the order adam_wn_kernel uses for the row norms it writes, so both give
+      // the same bits
+      f32x4_t xv[kWnRow / 1024];
 #pragma unroll
-    for (int u = 0; u < kWnRow / 256; ++u)
-      xr[u] = 256 * u < cols ? v[min((int)threadIdx.x + 256 * u, cols - 1)] : 0.f;
+      for (int u = 0; u < kWnRow / 1024; ++u)
+        xv[u] = 1024 * u < cols ? *(const f32x4_t*)(v + min((int)threadIdx.x * 4 + 1024 * u, cols - 4))
+                                : f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < kWnRow / 256; ++u) {
-      const int i = threadIdx.x + 256 * u;
-      if (i < cols) {
-        buf[i] = xr[u];
-        s = fmaf(xr[u], xr[u], s);
+      for (int u = 0; u < kWnRow / 1024; ++u) {
+        const int i = (int)threadIdx.x * 4 + 1024 * u;
+        if (i < cols) {
+          const f32x4_t x = xv[u];
+          *(f32x4_t*)(buf + i) = x;
+          s = fmaf(x[0], x[0], fmaf(x[1], x[1], fmaf(x[2], x[2], fmaf(x[3], x[3], s))));
+        }
+      }
+    } else {
+      float xr[kWnRow / 256];
+#pragma unroll
+      for (int u = 0; u < kWnRow / 256; ++u)
+        xr[u] = 256 * u < cols ? v[min((int)threadIdx.x + 256 * u, cols - 1)] : 0.f;
+#pragma unroll
+      for (int u = 0; u < kWnRow / 256; ++u) {
+        const int i = threadIdx.x + 256 * u;
+        if (i < cols) {
+          buf[i] = xr[u];
+          s = fmaf(xr[u], xr[u], s);
+        }
       }
     }
     s = block_sum(s, red);  // includes the barriers that publish buf
@@ -341,7 +367,16 @@ constexpr int kWnWaveX4 = 4;   // 16-B column groups per lane on the wave-per-ro
 __host__ __device__ inline bool wn_bwd_wave_rows(const vqx_wn_layer& l) {
   return l.kind == 0 && l.k == 1 && l.cin <= 64 * 4 * kWnWaveX4 && (l.cin / 4) * l.splits <= 64 * kWnNF;
 }
-__global__ __launch_bounds__(kWnThreads) void wn_bwd_kernel(const vqx_wn_layer* __restrict__ L, WnUnits U) {
+// sq (optional, vqx_weight_norm_bwd_sq): every wave of block b stores the sum of
+// squares of the gradient values it wrote at sq[4*b + wave] (0 if none): the
+// global gradient norm's partial sums without re-reading the gradient.
+__device__ __forceinline__ void wn_sq_store(float* sq, float q) {
+  if (!sq) return;
+  q = wave_sum(q);
+  if ((threadIdx.x & 63) == 0) sq[(int64_t)blockIdx.x * (kWnThreads / 64) + (threadIdx.x >> 6)] = q;
+}
+__global__ __launch_bounds__(kWnThreads) void wn_bwd_kernel(const vqx_wn_layer* __restrict__ L, WnUnits U,
+                                                            float* __restrict__ sq) {
   int lo = 0, hi = U.n - 1;  // the layer owning this block
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
@@ -373,12 +408,15 @@ __global__ __launch_bounds__(kWnThreads) void wn_bwd_kernel(const vqx_wn_layer* 
     }
     crs[g][cl] = a;
     __syncthreads();
+    float q2 = 0.f;
     if (g == 0 && c < l.cout) {
       float t = 0.f;
 #pragma unroll
       for (int q = 0; q < RG; ++q) t += crs[q][cl];
       l.dv[c] = t;
+      q2 = t * t;
     }
+    wn_sq_store(sq, q2);
     return;
   }
   if (wn_bwd_wave_rows(l)) {
@@ -386,7 +424,10 @@ __global__ __launch_bounds__(kWnThreads) void wn_bwd_kernel(const vqx_wn_layer* 
     // linears: 128 columns, dW written directly): one wave per row, the row's
     // sums held in registers, wave reductions only (no LDS, no barriers)
     const int o = unit * (kWnThreads / 64) + (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (o >= l.cout) return;
+    if (o >= l.cout) {
+      wn_sq_store(sq, 0.f);
+      return;
+    }
     const int cols = l.cin, nx4 = cols / 4;
     const int64_t ss = (int64_t)l.cout * cols, srow = (int64_t)o * cols;
     const bool sbf = l.slab_dtype == VQX_BF16;
@@ -404,30 +445,44 @@ __global__ __launch_bounds__(kWnThreads) void wn_bwd_kernel(const vqx_wn_layer* 
         dot = fmaf(sm[u][0], vv[u][0], fmaf(sm[u][1], vv[u][1], fmaf(sm[u][2], vv[u][2], fmaf(sm[u][3], vv[u][3], dot))));
       }
     }
+    float q2 = 0.f;
     if (!l.g) {
 #pragma unroll
       for (int u = 0; u < kWnWaveX4; ++u)
-        if (lane + 64 * u < nx4) *(f32x4_t*)(dv + 4 * (lane + 64 * u)) = sm[u];
+        if (lane + 64 * u < nx4) {
+          *(f32x4_t*)(dv + 4 * (lane + 64 * u)) = sm[u];
+          q2 = fmaf(sm[u][0], sm[u][0], fmaf(sm[u][1], sm[u][1], fmaf(sm[u][2], sm[u][2], fmaf(sm[u][3], sm[u][3], q2))));
+        }
+      wn_sq_store(sq, q2);
       return;
     }
     dot = wave_sum(dot);
     const float nrm = l.norm[o];
     const float dg = dot / nrm;
-    if (lane == 0) l.dg[o] = dg;
+    if (lane == 0) {
+      l.dg[o] = dg;
+      q2 = dg * dg;
+    }
     const float sc = l.g[o] / nrm, t = dg / nrm;
 #pragma unroll
     for (int u = 0; u < kWnWaveX4; ++u)
-      if (lane + 64 * u < nx4)
-        *(f32x4_t*)(dv + 4 * (lane + 64 * u)) =
-            f32x4_t{sc * (sm[u][0] - vv[u][0] * t), sc * (sm[u][1] - vv[u][1] * t), sc * (sm[u][2] - vv[u][2] * t),
-                    sc * (sm[u][3] - vv[u][3] * t)};
+      if (lane + 64 * u < nx4) {
+        const f32x4_t r = {sc * (sm[u][0] - vv[u][0] * t), sc * (sm[u][1] - vv[u][1] * t),
+                           sc * (sm[u][2] - vv[u][2] * t), sc * (sm[u][3] - vv[u][3] * t)};
+        *(f32x4_t*)(dv + 4 * (lane + 64 * u)) = r;
+        q2 = fmaf(r[0], r[0], fmaf(r[1], r[1], fmaf(r[2], r[2], fmaf(r[3], r[3], q2))));
+      }
+    wn_sq_store(sq, q2);
     return;
   }
   const bool rsm = l.kind == VQX_WN_RESAMPLE || l.kind == VQX_WN_RESAMPLE_T;
   const bool row_is_cout = l.kind == 0 || l.kind == VQX_WN_RESAMPLE;
   const int rows = row_is_cout ? l.cout : l.cin;
   const int o = unit;
-  if (o >= rows) return;
+  if (o >= rows) {
+    wn_sq_store(sq, 0.f);
+    return;
+  }
   const int other = row_is_cout ? l.cin : l.cout;  // multiple of 4 (host-checked)
   const int K = l.k;
   const int cols = other * K;
@@ -512,8 +567,13 @@ __global__ __launch_bounds__(kWnThreads) void wn_bwd_kernel(const vqx_wn_layer* 
   }
   __syncthreads();
   float* dv = l.dv + (int64_t)o * cols;
+  float q2 = 0.f;
   if (!l.g) {  // plain weight (weight norm removed): dv is the weight gradient itself
-    for (int i = threadIdx.x; i < cols; i += blockDim.x) dv[i] = dw[i];
+    for (int i = threadIdx.x; i < cols; i += blockDim.x) {
+      dv[i] = dw[i];
+      q2 = fmaf(dw[i], dw[i], q2);
+    }
+    wn_sq_store(sq, q2);
     return;
   }
   float dot = 0.f;
@@ -526,13 +586,21 @@ __global__ __launch_bounds__(kWnThreads) void wn_bwd_kernel(const vqx_wn_layer* 
   const float nrm = l.norm[o];
   const float gg = l.g[o];
   const float dg = dot / nrm;
-  if (threadIdx.x == 0) l.dg[o] = dg;
+  if (threadIdx.x == 0) {
+    l.dg[o] = dg;
+    q2 = dg * dg;
+  }
   const float sc = gg / nrm, t = dg / nrm;
 #pragma unroll
   for (int u = 0; u < kWnVRegs; ++u) {
     const int i = threadIdx.x + u * kWnThreads;
-    if (i < cols) dv[i] = sc * (dw[i] - vr[u] * t);
+    if (i < cols) {
+      const float r = sc * (dw[i] - vr[u] * t);
+      dv[i] = r;
+      q2 = fmaf(r, r, q2);
+    }
   }
+  wn_sq_store(sq, q2);
 }
 
 // --------------------------------------------------------------- groupnorm
@@ -1629,6 +1697,40 @@ __global__ __launch_bounds__(256) void sqnorm_partial_kernel(const float* __rest
   if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
 
+// The global gradient norm from the weight-norm backward's partials
+// (vqx_weight_norm_bwd_sq) and g^2 over the ranges [off, off+len) it did not
+// write: kSqBlocks blocks each sum a fixed strided share of both into
+// scratch[b], then one block adds the kSqBlocks values in order into out[0].
+// Deterministic (fixed assignment and order).
+constexpr int kSqBlocks = 64;
+__global__ __launch_bounds__(256) void sq_partial_sum_kernel(const float* __restrict__ part, int64_t np,
+                                                             const float* __restrict__ g,
+                                                             const int64_t* __restrict__ rng, int nr,
+                                                             float* __restrict__ scratch) {
+  __shared__ float red[16];
+  const int64_t stride = (int64_t)kSqBlocks * 256;
+  float s = 0.f;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * stride < np; i += 4 * stride) {  // four loads in flight
+    const float a = part[i], b = part[i + stride], c = part[i + 2 * stride], d = part[i + 3 * stride];
+    s += a;
+    s += b;
+    s += c;
+    s += d;
+  }
+  for (; i < np; i += stride) s += part[i];
+  for (int r = 0; r < nr; ++r) {
+    const int64_t off = rng[2 * r], len = rng[2 * r + 1];
+    for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < len; j += stride) s = fmaf(g[off + j], g[off + j], s);
+  }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) scratch[blockIdx.x] = s;
+}
+__global__ __launch_bounds__(64) void sq_final_kernel(const float* __restrict__ scratch, float* __restrict__ out) {
+  const float s = wave_sum(scratch[threadIdx.x]);
+  if (threadIdx.x == 0) out[0] = s;
+}
+
 __global__ void adam_hyper_kernel(int64_t* __restrict__ step, double lr0, double gamma, int step_size, double b1,
                                   double b2, double eps, float* __restrict__ hyper) {
   const int64_t t = step[0] + 1;
@@ -1759,6 +1861,243 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   }
 }
 
+// Adam with the next forward's weight-norm preparation fused in
+// (vqx_adam_step_wn).  Blocks [0, row_off[n_layers]) own the rows of the
+// weight-normed convs in the table: each updates its rows of v = weight_v
+// and their gains weight_g[o] (adam_elem, the bits of adam_kernel), reduces
+// ||v_o|| of the NEW row in the canonical order of the pack (kind 0, k > 1:
+// 256-thread block, thread t the elements 4t + 1024u + (0..3); kind 0 k = 1
+// and kind 1: a wave per row, lane l the elements 4l + 256u + (0..3); nested
+// fmaf of the four, then block / wave sums), stores it in norm[o] and, for
+// kind 0 (Conv1d), writes the packed w = g*v/||v|| exactly as wn_pack_kernel
+// would from the same parameters.  The remaining blocks update the flat
+// segments (start, len) of everything else, 4096 elements a block.
+constexpr int kAdamMaxL = 128, kAdamMaxS = 128;
+struct AdamWnPlan {
+  int n_layers, n_segs;
+  int row_off[kAdamMaxL + 1];  // block prefix of the row layers
+  int seg_blk[kAdamMaxS + 1];  // block prefix of the flat segments (after the row blocks)
+};
+__host__ __device__ inline int adam_wn_units(const vqx_wn_layer& l) {
+  return l.kind == 1 ? l.cin : l.k > 1 ? l.cout : (l.cout + 3) / 4;
+}
+struct AdamHyper {
+  float coef, step_size, bc2s, w, b2, omb2, eps;
+};
+__device__ __forceinline__ AdamHyper adam_hyper_load(const float* hyper, const float* sumsq, float max_norm) {
+  AdamHyper h;
+  h.coef = 1.f;
+  if (max_norm > 0.f && sumsq) {
+    const float tn = sqrtf(sumsq[0]);
+    h.coef = max_norm / (tn + 1e-6f);
+    h.coef = h.coef < 1.f ? h.coef : 1.f;
+  }
+  h.step_size = hyper[1];
+  h.bc2s = hyper[2];
+  h.w = hyper[4];
+  h.b2 = hyper[5];
+  h.omb2 = hyper[6];
+  h.eps = hyper[7];
+  return h;
+}
+__device__ __forceinline__ f32x4_t adam4(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                         float* __restrict__ v, int64_t i, const AdamHyper& h) {
+  f32x4_t pv = *(const f32x4_t*)(p + i), gv = *(const f32x4_t*)(g + i);
+  f32x4_t mv = *(const f32x4_t*)(m + i), vv = *(const f32x4_t*)(v + i);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float pi = pv[e], mi = mv[e], vi = vv[e];
+    adam_elem(pi, __fmul_rn(gv[e], h.coef), mi, vi, h.w, h.b2, h.omb2, h.bc2s, h.eps, h.step_size);
+    pv[e] = pi;
+    mv[e] = mi;
+    vv[e] = vi;
+  }
+  *(f32x4_t*)(p + i) = pv;
+  *(f32x4_t*)(m + i) = mv;
+  *(f32x4_t*)(v + i) = vv;
+  return pv;
+}
+__device__ __forceinline__ float adam1(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                       float* __restrict__ v, int64_t i, const AdamHyper& h) {
+  float pi = p[i], mi = m[i], vi = v[i];
+  adam_elem(pi, __fmul_rn(g[i], h.coef), mi, vi, h.w, h.b2, h.omb2, h.bc2s, h.eps, h.step_size);
+  p[i] = pi;
+  m[i] = mi;
+  v[i] = vi;
+  return pi;
+}
+__device__ __forceinline__ float sq4(const f32x4_t x, float s) {
+  return fmaf(x[0], x[0], fmaf(x[1], x[1], fmaf(x[2], x[2], fmaf(x[3], x[3], s))));
+}
+
+__global__ __launch_bounds__(256, 4) void adam_wn_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                      float* __restrict__ m, float* __restrict__ v,
+                                                      const float* __restrict__ hyper,
+                                                      const float* __restrict__ sumsq, float max_norm,
+                                                      const vqx_wn_layer* __restrict__ L,
+                                                      const int64_t* __restrict__ segs, AdamWnPlan P) {
+  const AdamHyper h = adam_hyper_load(hyper, sumsq, max_norm);
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (b >= P.row_off[P.n_layers]) {  // flat segment chunk: 4096 elements
+    int lo = 0, hi = P.n_segs - 1;
+    const int rb = b - P.row_off[P.n_layers];
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (P.seg_blk[mid] <= rb) lo = mid; else hi = mid - 1;
+    }
+    const int64_t s0 = segs[2 * lo], len = segs[2 * lo + 1];
+    const int64_t c0 = (int64_t)(rb - P.seg_blk[lo]) * 4096;
+    if ((s0 & 3) == 0 && (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t j = c0 + (int64_t)threadIdx.x * 4 + 1024 * u;
+        if (j + 4 <= len) {
+          adam4(p, g, m, v, s0 + j, h);
+        } else {
+          for (int64_t e = j; e < len && e < j + 4; ++e) adam1(p, g, m, v, s0 + e, h);
+        }
+      }
+    } else {
+      for (int64_t j = c0 + threadIdx.x; j < len && j < c0 + 4096; j += 256) adam1(p, g, m, v, s0 + j, h);
+    }
+    return;
+  }
+  int lo = 0, hi = P.n_layers - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (P.row_off[mid] <= b) lo = mid; else hi = mid - 1;
+  }
+  const vqx_wn_layer& l = L[lo];
+  const int unit = b - P.row_off[lo];
+  const int K = l.k, cin = l.cin, cout = l.cout;
+  const int64_t voff = l.v - p, goff = l.g - p;
+  if (l.kind == 1 || K > 1) {
+    // one row per 256-thread block: Conv1d row co (packed [co][j*cin + ci]
+    // through LDS) or ConvT row ci (norm only); every load of the thread's
+    // elements is issued before the first update
+    __shared__ __attribute__((aligned(16))) float buf[kWnRow];
+    __shared__ float red[16];
+    __shared__ float gnew;
+    const int o = unit;
+    const int cols = l.kind == 1 ? cout * K : cin * K;
+    const int64_t r0 = voff + (int64_t)o * cols;
+    constexpr int U = kWnRow / 1024, UC = 2;  // UC 16-B groups' loads in flight at a time (register budget)
+    float s = 0.f;
+#pragma unroll
+    for (int u0 = 0; u0 < U; u0 += UC) {
+      f32x4_t pv[UC], gv[UC], mv[UC], vv[UC];
+#pragma unroll
+      for (int uu = 0; uu < UC; ++uu) {
+        const int i = (int)threadIdx.x * 4 + 1024 * (u0 + uu);
+        if (i < cols) {
+          pv[uu] = *(const f32x4_t*)(p + r0 + i);
+          gv[uu] = *(const f32x4_t*)(g + r0 + i);
+          mv[uu] = *(const f32x4_t*)(m + r0 + i);
+          vv[uu] = *(const f32x4_t*)(v + r0 + i);
+        }
+      }
+#pragma unroll
+      for (int uu = 0; uu < UC; ++uu) {
+        const int i = (int)threadIdx.x * 4 + 1024 * (u0 + uu);
+        if (i < cols) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float pi = pv[uu][e], mi = mv[uu][e], vi = vv[uu][e];
+            adam_elem(pi, __fmul_rn(gv[uu][e], h.coef), mi, vi, h.w, h.b2, h.omb2, h.bc2s, h.eps, h.step_size);
+            pv[uu][e] = pi;
+            mv[uu][e] = mi;
+            vv[uu][e] = vi;
+          }
+          *(f32x4_t*)(p + r0 + i) = pv[uu];
+          *(f32x4_t*)(m + r0 + i) = mv[uu];
+          *(f32x4_t*)(v + r0 + i) = vv[uu];
+          if (l.kind == 0) *(f32x4_t*)(buf + i) = pv[uu];
+          s = sq4(pv[uu], s);
+        }
+      }
+    }
+    if (threadIdx.x == 0) gnew = adam1(p, g, m, v, goff + o, h);
+    s = block_sum(s, red);  // its barriers publish buf and gnew
+    const float nrm = sqrtf(s);
+    if (threadIdx.x == 0) l.norm[o] = nrm;
+    if (l.kind == 1) return;
+    const int co = o;
+    const float sc = gnew / nrm;
+    bf16_t* wb = (bf16_t*)l.w_packed + (int64_t)co * cols;
+    if (l.dtype == VQX_BF16 && (cin & 3) == 0 && (((uintptr_t)wb) & 7) == 0) {
+      for (int e = threadIdx.x * 4; e < cols; e += 1024) {  // 4 consecutive ci of one tap, 8 B a lane
+        const int j = e / cin, ci = e - j * cin;
+        const float* bb = buf + ci * K + j;
+        *(uint2*)(wb + e) = make_uint2(pack_bf16x2(bb[0] * sc, bb[K] * sc), pack_bf16x2(bb[2 * K] * sc, bb[3 * K] * sc));
+      }
+      return;
+    }
+    for (int e = threadIdx.x; e < cols; e += 256) {
+      const int j = e / cin, ci = e - j * cin;
+      st_dt(l.w_packed, (int64_t)co * cols + e, buf[ci * K + j] * sc, l.dtype);
+    }
+    return;
+  }
+  // a wave per row: kind 0 k = 1 (row co of cin, packed = the row scaled)
+  const int o = unit * 4 + wv;
+  if (o >= cout) return;
+  const int cols = cin;
+  const int64_t r0 = voff + (int64_t)o * cols;
+  float s = 0.f;
+  {
+    f32x4_t xs[2], gv[2], mv[2], vv[2];  // cols <= 512
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {  // every load first
+      const int i = lane * 4 + 256 * u;
+      if (i < cols) {
+        xs[u] = *(const f32x4_t*)(p + r0 + i);
+        gv[u] = *(const f32x4_t*)(g + r0 + i);
+        mv[u] = *(const f32x4_t*)(m + r0 + i);
+        vv[u] = *(const f32x4_t*)(v + r0 + i);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = lane * 4 + 256 * u;
+      if (i < cols) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float pi = xs[u][e], mi = mv[u][e], vi = vv[u][e];
+          adam_elem(pi, __fmul_rn(gv[u][e], h.coef), mi, vi, h.w, h.b2, h.omb2, h.bc2s, h.eps, h.step_size);
+          xs[u][e] = pi;
+          mv[u][e] = mi;
+          vv[u][e] = vi;
+        }
+        *(f32x4_t*)(p + r0 + i) = xs[u];
+        *(f32x4_t*)(m + r0 + i) = mv[u];
+        *(f32x4_t*)(v + r0 + i) = vv[u];
+        s = sq4(xs[u], s);
+      }
+    }
+    float gn = 0.f;
+    if (lane == 0) gn = adam1(p, g, m, v, goff + o, h);
+    gn = __shfl(gn, 0, 64);
+    s = wave_sum(s);
+    const float nrm = sqrtf(s);
+    if (lane == 0) l.norm[o] = nrm;
+    const float sc = gn / nrm;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = lane * 4 + 256 * u;
+      if (i < cols) {
+        const f32x4_t x = xs[u];
+        if (l.dtype == VQX_BF16) {
+          *(uint2*)((bf16_t*)l.w_packed + (int64_t)o * cols + i) =
+              make_uint2(pack_bf16x2(x[0] * sc, x[1] * sc), pack_bf16x2(x[2] * sc, x[3] * sc));
+        } else {
+          *(f32x4_t*)((float*)l.w_packed + (int64_t)o * cols + i) = f32x4_t{x[0] * sc, x[1] * sc, x[2] * sc, x[3] * sc};
+        }
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void scale_act_2d_kernel(const void* __restrict__ src, int lds, int sdt,
                                                            void* __restrict__ dst, int ldd, int ddt, int64_t rows,
                                                            int cols, float scale, int act) {
@@ -1795,8 +2134,8 @@ static int grid_for(int64_t n, int block = 256, int cap = 8192) {
   return (int)(g > cap ? cap : g);
 }
 
-extern "C" int vqx_weight_norm_fwd(const vqx_wn_layer* lh, const vqx_wn_layer* ld, int32_t n_layers,
-                                   vqx_stream_t stream) {
+static int wn_fwd_launch(const vqx_wn_layer* lh, const vqx_wn_layer* ld, int32_t n_layers, int32_t flags,
+                         vqx_stream_t stream) {
   if (!lh || !ld || n_layers <= 0) { set_error("vqx_weight_norm_fwd: bad tables"); return -1; }
   int max_rows = 1;
   int64_t max_el = 1;
@@ -1820,7 +2159,8 @@ extern "C" int vqx_weight_norm_fwd(const vqx_wn_layer* lh, const vqx_wn_layer* l
   (void)max_el;
   (void)max_rows;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(wn_norm_kernel, dim3((max_t_rows + 3) / 4, n_layers), dim3(256), 0, s, ld, n_layers);
+  if (!(flags & VQX_WNF_NORMS_READY))
+    hipLaunchKernelGGL(wn_norm_kernel, dim3(max_t_rows, n_layers), dim3(256), 0, s, ld, n_layers);
   for (int i0 = 0; i0 < n_layers; i0 += kWnMaxL) {  // flat grid over the layers' units, kWnMaxL layers a launch
     WnUnits U;
     U.n = n_layers - i0 < kWnMaxL ? n_layers - i0 : kWnMaxL;
@@ -1831,9 +2171,39 @@ extern "C" int vqx_weight_norm_fwd(const vqx_wn_layer* lh, const vqx_wn_layer* l
   return launch_status("vqx_weight_norm_fwd");
 }
 
-extern "C" int vqx_weight_norm_bwd(const vqx_wn_layer* lh, const vqx_wn_layer* ld, int32_t n_layers,
+extern "C" int vqx_weight_norm_fwd(const vqx_wn_layer* lh, const vqx_wn_layer* ld, int32_t n_layers,
                                    vqx_stream_t stream) {
+  return wn_fwd_launch(lh, ld, n_layers, 0, stream);
+}
+
+extern "C" int vqx_weight_norm_fwd_flags(const vqx_wn_layer* lh, const vqx_wn_layer* ld, int32_t n_layers,
+                                         int32_t flags, vqx_stream_t stream) {
+  return wn_fwd_launch(lh, ld, n_layers, flags, stream);
+}
+
+static int wn_bwd_units(const vqx_wn_layer& l) {
+  return l.kind == VQX_WN_COLREDUCE ? (l.cout + kWnCrCols - 1) / kWnCrCols
+         : wn_bwd_wave_rows(l)       ? (l.cout + kWnThreads / 64 - 1) / (kWnThreads / 64)
+         : (l.kind == 0 || l.kind == VQX_WN_RESAMPLE) ? l.cout
+                                                      : l.cin;
+}
+
+extern "C" int vqx_weight_norm_bwd_partials(const vqx_wn_layer* lh, int32_t n_layers, int64_t* count) {
+  if (!lh || n_layers <= 0 || !count) { set_error("vqx_weight_norm_bwd_partials: bad arguments"); return -1; }
+  int64_t b = 0;
+  for (int i = 0; i < n_layers; ++i) b += wn_bwd_units(lh[i]);
+  *count = b * (kWnThreads / 64);
+  return 0;
+}
+
+static int wn_bwd_launch(const vqx_wn_layer* lh, const vqx_wn_layer* ld, int32_t n_layers, float* sq,
+                         int64_t sq_capacity, vqx_stream_t stream) {
   if (!lh || !ld || n_layers <= 0) { set_error("vqx_weight_norm_bwd: bad tables"); return -1; }
+  if (sq) {
+    int64_t need = 0;
+    vqx_weight_norm_bwd_partials(lh, n_layers, &need);
+    if (sq_capacity < need) { set_error("vqx_weight_norm_bwd_sq: %lld partials < %lld", (long long)sq_capacity, (long long)need); return -1; }
+  }
   int max_rows = 1;
   for (int i = 0; i < n_layers; ++i) {
     const vqx_wn_layer& l = lh[i];
@@ -1859,17 +2229,36 @@ extern "C" int vqx_weight_norm_bwd(const vqx_wn_layer* lh, const vqx_wn_layer* l
     WnUnits U;
     U.n = n_layers - i0 < kWnMaxL ? n_layers - i0 : kWnMaxL;
     U.off[0] = 0;
-    for (int i = 0; i < U.n; ++i) {
-      const vqx_wn_layer& l = lh[i0 + i];
-      const int units = l.kind == VQX_WN_COLREDUCE ? (l.cout + kWnCrCols - 1) / kWnCrCols
-                        : wn_bwd_wave_rows(l) ? (l.cout + kWnThreads / 64 - 1) / (kWnThreads / 64)
-                        : (l.kind == 0 || l.kind == VQX_WN_RESAMPLE) ? l.cout : l.cin;
-      U.off[i + 1] = U.off[i] + units;
-    }
+    for (int i = 0; i < U.n; ++i) U.off[i + 1] = U.off[i] + wn_bwd_units(lh[i0 + i]);
     if (U.off[U.n] > 0)
-      hipLaunchKernelGGL(wn_bwd_kernel, dim3(U.off[U.n]), dim3(kWnThreads), 0, (hipStream_t)stream, ld + i0, U);
+      hipLaunchKernelGGL(wn_bwd_kernel, dim3(U.off[U.n]), dim3(kWnThreads), 0, (hipStream_t)stream, ld + i0, U, sq);
+    if (sq) sq += (int64_t)U.off[U.n] * (kWnThreads / 64);
   }
   return launch_status("vqx_weight_norm_bwd");
+}
+
+extern "C" int vqx_weight_norm_bwd(const vqx_wn_layer* lh, const vqx_wn_layer* ld, int32_t n_layers,
+                                   vqx_stream_t stream) {
+  return wn_bwd_launch(lh, ld, n_layers, nullptr, 0, stream);
+}
+
+extern "C" int vqx_weight_norm_bwd_sq(const vqx_wn_layer* lh, const vqx_wn_layer* ld, int32_t n_layers,
+                                      float* sq_partials, int64_t sq_capacity, vqx_stream_t stream) {
+  if (!sq_partials) { set_error("vqx_weight_norm_bwd_sq: null partials"); return -1; }
+  return wn_bwd_launch(lh, ld, n_layers, sq_partials, sq_capacity, stream);
+}
+
+extern "C" int vqx_sq_norm_finish(const float* partials, int64_t n_partials, const float* g, const int64_t* ranges,
+                                  int32_t n_ranges, float* scratch, float* out, vqx_stream_t stream) {
+  if (n_partials < 0 || n_ranges < 0 || !out || !scratch || (n_partials && !partials) || (n_ranges && (!ranges || !g))) {
+    set_error("vqx_sq_norm_finish: bad arguments");
+    return -1;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(sq_partial_sum_kernel, dim3(kSqBlocks), dim3(256), 0, s, partials, n_partials, g, ranges, n_ranges,
+                     scratch);
+  hipLaunchKernelGGL(sq_final_kernel, dim3(1), dim3(64), 0, s, scratch, out);
+  return launch_status("vqx_sq_norm_finish");
 }
 
 extern "C" int vqx_groupnorm_stats(const void* x, int32_t ldx, int32_t dtype, int64_t n_rows, int32_t T, int32_t C,
@@ -2117,6 +2506,51 @@ extern "C" int vqx_adam_step(float* p, const float* g, float* m, float* v, int64
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for((n + 3) / 4, 256, 4096)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
                      hyper, sumsq, max_norm);
   return launch_status("vqx_adam_step");
+}
+
+extern "C" int vqx_adam_step_wn(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper,
+                                const float* sumsq, float max_norm, const vqx_wn_layer* rows_host,
+                                const vqx_wn_layer* rows_dev, int32_t n_layers, const int64_t* segs_host,
+                                const int64_t* segs_dev, int32_t n_segs, vqx_stream_t stream) {
+  if (!p || !g || !m || !v || !hyper || n_layers < 0 || n_segs < 0 || n_layers > kAdamMaxL || n_segs > kAdamMaxS ||
+      (n_layers && (!rows_host || !rows_dev)) || (n_segs && (!segs_host || !segs_dev))) {
+    set_error("vqx_adam_step_wn: bad arguments (at most %d layers and %d segments)", kAdamMaxL, kAdamMaxS);
+    return -1;
+  }
+  AdamWnPlan P;
+  P.n_layers = n_layers;
+  P.n_segs = n_segs;
+  P.row_off[0] = 0;
+  int64_t covered = 0;
+  for (int i = 0; i < n_layers; ++i) {
+    const vqx_wn_layer& l = rows_host[i];
+    const bool k3 = l.kind == 0 && l.k > 1;
+    const int cols = l.kind == 0 ? l.cin * l.k : l.cout * l.k;
+    const int rows = l.kind == 0 ? l.cout : l.cin;
+    const int64_t vo = l.v - p, go = l.g - p;
+    const bool ok = (l.kind == 0 || l.kind == 1) && l.g && l.norm && (l.kind == 1 || l.w_packed) && l.k >= 1 &&
+                    cols % 4 == 0 && cols <= (k3 || l.kind == 1 ? kWnRow : 512) && vo >= 0 && vo % 4 == 0 &&
+                    vo + (int64_t)rows * cols <= n && go >= 0 && go + rows <= n &&
+                    (l.dtype == VQX_BF16 || l.dtype == VQX_F32) &&
+                    (l.kind == 1 || k3 ||
+                     ((((uintptr_t)l.w_packed) & 15) == 0 && (l.cin * (l.dtype == VQX_BF16 ? 2 : 4)) % 16 == 0));
+    if (!ok) { set_error("vqx_adam_step_wn: layer %d cannot take the fused weight-norm preparation", i); return -1; }
+    P.row_off[i + 1] = P.row_off[i] + adam_wn_units(l);
+    covered += (int64_t)rows * cols + rows;
+  }
+  P.seg_blk[0] = 0;
+  for (int i = 0; i < n_segs; ++i) {
+    const int64_t s0 = segs_host[2 * i], len = segs_host[2 * i + 1];
+    if (s0 < 0 || len < 0 || s0 + len > n) { set_error("vqx_adam_step_wn: segment %d out of range", i); return -1; }
+    P.seg_blk[i + 1] = P.seg_blk[i] + (int)((len + 4095) / 4096);
+    covered += len;
+  }
+  if (covered != n) { set_error("vqx_adam_step_wn: rows + segments cover %lld of %lld elements", (long long)covered, (long long)n); return -1; }
+  const int grid = P.row_off[n_layers] + P.seg_blk[n_segs];
+  if (grid > 0)
+    hipLaunchKernelGGL(adam_wn_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, p, g, m, v, hyper, sumsq,
+                       max_norm, rows_dev, segs_dev, P);
+  return launch_status("vqx_adam_step_wn");
 }
 
 extern "C" int vqx_radam_hyper(int64_t* step, double lr0, double gamma, int32_t step_size, double beta1,

@@ -176,7 +176,18 @@ class EngineOptions:
                        flat grid are then short ones)
       slab_f32         fp32 split-K slabs in bf16 runs (+3.3% step time,
                        profiles/r04/slab_wfirst_ab.txt)
-      kernel_policy    include/vqx.h VQX_POLICY_* of every conv GEMM call"""
+      fuse_grad_norm   one process, batched weight-norm backward: the global
+                       gradient norm of the clip from sum-of-squares partials
+                       the weight-norm backward leaves as it writes the
+                       gradients (plus the few parameters it does not write),
+                       instead of a pass re-reading the 125 MB gradient
+      fuse_adam_wn     Adam writes the next forward's weight-norm row norms and
+                       Conv1d packed weights as it updates weight_v / weight_g
+                       (vqx_adam_step_wn); the forward then packs only the
+                       ConvTranspose layers
+      kernel_policy    include/vqx.h VQX_POLICY_* of every conv GEMM call (5:
+                       the 1x1 layers on three-workgroups-per-CU kernels,
+                       which leave slots for co-resident RCCL kernels)"""
     fuse_gn: bool = True
     enc_gn_finalize: bool = False
     side_stream: bool = False
@@ -189,6 +200,8 @@ class EngineOptions:
     wn_bwd_ddp_groups: int = 5
     wn_bwd_sort: bool = True
     lazy_stats: bool = True
+    fuse_grad_norm: bool = True
+    fuse_adam_wn: bool = True
     kernel_policy: int = 0
 
 
@@ -369,6 +382,10 @@ class VQVAEEngine:
         self._wn_active = False   # inside backward(): the weight-norm backward may be batched
         self._wn_pending = []     # groups whose weight-norm backward is batched and not yet run
         self._wn_done = set()     # ... and those already run in this backward
+        self._sq_plan_ready = None  # gradient-norm partials of this backward (fuse_grad_norm)
+        # fused Adam + weight-norm preparation (fuse_adam_wn): its plan, and the
+        # flat_p version the packed weights / norms it wrote belong to
+        self._adam_wn, self._adam_wn_built, self._packed_version = None, False, None
 
     # ------------------------------------------------------------ parameters
     def _flatten(self):
@@ -590,7 +607,7 @@ class VQVAEEngine:
             else:
                 r, c = (Lr.cin, Lr.cout) if Lr.kind == KIND_CONVT else (Lr.cout, Lr.cin)
                 n, T_, k, pad, dil = B_ref * To, To, Lr.k, Lr.pad, Lr.dil
-            tiles = ops.wgrad_tiles(n, T_, r, c, k, pad, self.dt, dil=dil)
+            tiles = ops.wgrad_tiles(n, T_, r, c, k, pad, self.dt, dil=dil, policy=self.opt.kernel_policy)
             wgs = wg_solo if id(Lr) in solo else wg_1x1 if Lr.k == 1 else wg_target
             Lr.splits = max(1, min(wgs // tiles, n // min_k))
         # slab arena: every group's slabs in a region of their own when the
@@ -656,6 +673,7 @@ class VQVAEEngine:
     def refresh_tables(self):
         """Rebuild descriptor tables (after remove_weight_norm or a re-flatten)."""
         self.wn_fwd_table = ops.wn_table([self._wn_entry(Lr, bwd=False) for Lr in self.convs])
+        self._adam_wn, self._adam_wn_built, self._packed_version = None, False, None
         for (_, _, train), w in self._ws.items():
             if train:
                 self._build_bwd_tables(w)
@@ -720,6 +738,7 @@ class VQVAEEngine:
         w.bwd_tables = {k: ops.wn_table(v) for k, v in t.items()}
         w.bwd_entries = t
         w.bwd_table_cache = {}  # group sequence -> table of one batched launch (_wn_run)
+        w.bwd_sq_cache = {}     # ... and its gradient-norm plan (_sq_plan)
         # parameters whose gradients are final once a group's launch is done
         # (data parallel: their all-reduce is issued right then, parallel/ddp.py)
         w.bwd_params = {k: self._params_written([t_ for e in entries for t_ in (e.get("dv"), e.get("dg"))])
@@ -829,7 +848,14 @@ class VQVAEEngine:
 
     # ------------------------------------------------------------ forward
     def pack_weights(self):
-        ops.weight_norm_fwd(self.wn_fwd_table)
+        plan = self._adam_wn
+        if plan is not None and self._packed_version == self._param_version():
+            # the last optimizer step packed the Conv1d layers and wrote every
+            # ConvT row norm for the current parameters (vqx_adam_step_wn)
+            if plan[2] is not None:
+                ops.weight_norm_fwd(plan[2], flags=plan[3])
+        else:
+            ops.weight_norm_fwd(self.wn_fwd_table)
         for st in self.dec_stages:
             if st.conv.kind == KIND_UP:  # the up-sampler's bias, once per folded frame
                 s = st.conv.scale
@@ -1003,9 +1029,45 @@ class VQVAEEngine:
             if self.opt.wn_bwd_sort:  # entries are independent: any order gives the same bits
                 ents.sort(key=_wn_block_bytes, reverse=True)
             tab = w.bwd_table_cache[keys] = ops.wn_table(ents)
-        ops.weight_norm_bwd(tab)
+            w.bwd_sq_cache[keys] = self._sq_plan(tab, ents)
+        plan = w.bwd_sq_cache.get(keys) if (self.comm is None and self.opt.fuse_grad_norm) else None
+        if plan is not None:
+            ops.weight_norm_bwd(tab, sq_partials=plan[0])
+            self._sq_plan_ready = plan
+        else:
+            ops.weight_norm_bwd(tab)
         self._wn_done.update(keys)
         self._grads_final([i for k in keys for i in w.bwd_params[k]])
+
+    def _sq_plan(self, tab, ents):
+        """Gradient-norm plan of one batched weight-norm backward launch:
+        (partials buffer, int64 [n, 2] device ranges of the flat gradient the
+        launch does not write).  None when its writes overlap (an element would
+        be counted twice) -- the step then re-reads the gradient instead."""
+        base = self.flat_g.data_ptr()
+        iv = []
+        for e in ents:
+            for k in ("dv", "dg"):
+                t = e.get(k)
+                if t is None or t.numel() == 0:
+                    continue
+                lo = (t.data_ptr() - base) // 4
+                if not t.is_contiguous() or lo < 0 or lo + t.numel() > self.n_params:
+                    return None
+                iv.append((lo, lo + t.numel()))
+        iv.sort()
+        rest, cur = [], 0
+        for lo, hi in iv:
+            if lo < cur:
+                return None
+            if lo > cur:
+                rest.append((cur, lo - cur))
+            cur = hi
+        if cur < self.n_params:
+            rest.append((cur, self.n_params - cur))
+        parts = torch.zeros(max(1, ops.weight_norm_bwd_partials(tab)), device=self.device, dtype=F32)
+        rng = torch.tensor(rest, dtype=torch.int64).view(-1, 2).to(self.device) if rest else None
+        return parts, rng
 
     def _wn_bwd_flush(self, w):
         if not self._wn_batched():
@@ -1378,6 +1440,7 @@ class VQVAEEngine:
         if self.comm is not None:
             self._grads_reset()
         self._wn_pending, self._wn_done = [], set()
+        self._sq_plan_ready = None
         self._wn_active = True
         try:
             if self.plain:
@@ -1416,8 +1479,12 @@ class VQVAEEngine:
         self.opt_ready = True
 
     def optimizer_step(self):
+        plan, self._sq_plan_ready = self._sq_plan_ready, None
         if self.max_grad_norm > 0:
-            ops.grad_sq_norm(self.flat_g, self.norm_part, self.sumsq)
+            if plan is not None:  # partials from this step's weight-norm backward
+                ops.sq_norm_finish(plan[0], self.flat_g, plan[1], self.sumsq, self.norm_part)
+            else:
+                ops.grad_sq_norm(self.flat_g, self.norm_part, self.sumsq)
         sumsq = self.sumsq if self.max_grad_norm > 0 else None
         if self.opt_kind == "radam":
             ops.radam_hyper(self.opt_step, self.lr0, self.sched_gamma, self.sched_step, self.betas[0], self.betas[1],
@@ -1427,8 +1494,82 @@ class VQVAEEngine:
             return
         ops.adam_hyper(self.opt_step, self.lr0, self.sched_gamma, self.sched_step, self.betas[0], self.betas[1],
                        self.eps, self.hyper)
+        if not self._adam_wn_built:
+            self._adam_wn = self._adam_wn_plan() if self.opt.fuse_adam_wn else None
+            self._adam_wn_built = True
+        if self._adam_wn is not None:
+            rows, segs = self._adam_wn[0], self._adam_wn[1]
+            ops.adam_step_wn(self.flat_p, self.flat_g, self.exp_avg, self.exp_avg_sq, self.hyper, sumsq,
+                             float(self.max_grad_norm), rows, segs)
+            self._packed_version = self._param_version()
+            return
         ops.adam_step(self.flat_p, self.flat_g, self.exp_avg, self.exp_avg_sq, self.hyper, sumsq,
                       float(self.max_grad_norm))
+
+    def _param_version(self):
+        """Sum of the version counters of flat_p and of every parameter: any
+        in-place torch op on them (copy_, mul_, load_state_dict, a broadcast)
+        changes it; the HIP kernels' writes do not.  Edits through `.data`
+        bypass version counters: call invalidate_packed() after those."""
+        return self.flat_p._version + sum(p._version for p in self.params)
+
+    def invalidate_packed(self):
+        """The next forward packs every layer from the parameters (fuse_adam_wn)."""
+        self._packed_version = None
+
+    def _adam_wn_plan(self):
+        """(rows table, flat segments, forward table of what is left to pack,
+        its flags) for vqx_adam_step_wn, or None when the model has nothing it
+        can take.  Rows: the weight-normed Conv1d (kind 0) and, when every one
+        of them qualifies, ConvTranspose (kind 1) layers whose rows fit the
+        kernel's partitions (include/vqx.h)."""
+        base, esz = self.flat_p.data_ptr(), (2 if self.cd == torch.bfloat16 else 4)
+        ents = [self._wn_entry(Lr, bwd=False) for Lr in self.convs]
+
+        def ok(e):
+            if e["g"] is None or e["kind"] not in (0, 1):
+                return False
+            vo = (e["v"].data_ptr() - base) // 4
+            if vo % 4 or (e["v"].data_ptr() - base) % 4:
+                return False
+            if e["kind"] == 1:
+                return (e["cout"] * e["k"]) % 4 == 0 and e["cout"] * e["k"] <= 4096
+            cols = e["cin"] * e["k"]
+            if cols % 4:
+                return False
+            if e["k"] > 1:
+                return cols <= 4096
+            return e["cin"] <= 512 and (e["cin"] * esz) % 16 == 0 and e["w_packed"].data_ptr() % 16 == 0
+
+        conv0 = [e for e in ents if e["kind"] == 0 and ok(e)]
+        convt = [e for e in ents if e["kind"] == 1]
+        convt = convt if convt and all(ok(e) for e in convt) else []
+        rows = conv0 + convt
+        if not rows or len(rows) > 128:
+            return None
+        iv = []
+        for e in rows:
+            for t in (e["v"], e["g"]):
+                lo = (t.data_ptr() - base) // 4
+                iv.append((lo, lo + t.numel()))
+        iv.sort()
+        segs, cur = [], 0
+        for lo, hi in iv:
+            if lo < cur:
+                return None
+            if lo > cur:
+                segs.append((cur, lo - cur))
+            cur = hi
+        if cur < self.n_params:
+            segs.append((cur, self.n_params - cur))
+        if len(segs) > 128:
+            return None
+        packed = {id(e["w_packed"]) for e in conv0}
+        rest = [e for e in ents if id(e["w_packed"]) not in packed]
+        sh = torch.tensor(segs, dtype=torch.int64).view(-1, 2)
+        sd = sh.to(self.device) if segs else sh
+        flags = ops.WNF_NORMS_READY if convt else 0
+        return ops.wn_table(rows), (sh, sd), (ops.wn_table(rest) if rest else None), flags
 
     def train_step(self, x, y):
         """One full training step (trainer/basic.py:55-79): forward, backward,

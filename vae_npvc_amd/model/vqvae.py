@@ -211,7 +211,10 @@ class Model(nn.Module):
                 self.quantizer = VectorQuantizer(want[0], want[1], normalize=self.quantizer.normalize,
                                                  reduction=self.quantizer.reduction).to(dev)
                 self._engine = None
-        return super().load_state_dict(state_dict, strict=strict)
+        out = super().load_state_dict(state_dict, strict=strict)
+        if self._engine is not None:
+            self._engine.invalidate_packed()
+        return out
 
 
 LOG_2PI = math.log(2.0 * math.pi)

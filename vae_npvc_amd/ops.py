@@ -29,7 +29,7 @@ def _check_cuda(*ts):
             raise L.VqxError("libvqx ops need device tensors (the HIP kernels are the only implementation)")
 
 
-POLICY_AUTO, POLICY_IM2COL, POLICY_TALL256, POLICY_TALL512, POLICY_TR128 = 0, 1, 2, 3, 4  # include/vqx.h
+POLICY_AUTO, POLICY_IM2COL, POLICY_TALL256, POLICY_TALL512, POLICY_TR128, POLICY_K1_3PCU = 0, 1, 2, 3, 4, 5  # vqx.h
 _policy = POLICY_AUTO
 
 
@@ -38,8 +38,8 @@ def set_kernel_policy(policy):
     VQX_POLICY_*; for tests and A/B tools -- the library itself keeps no such
     state: the policy travels in every call's arguments).  Returns the old one."""
     global _policy
-    if policy not in (POLICY_AUTO, POLICY_IM2COL, POLICY_TALL256, POLICY_TALL512, POLICY_TR128):
-        raise ValueError(f"kernel policy {policy} not in 0..4")
+    if policy not in (POLICY_AUTO, POLICY_IM2COL, POLICY_TALL256, POLICY_TALL512, POLICY_TR128, POLICY_K1_3PCU):
+        raise ValueError(f"kernel policy {policy} not in 0..5")
     prev, _policy = _policy, int(policy)
     return prev
 
@@ -263,10 +263,11 @@ def conv_dgrad_wgrad(dy, w, dx, dgrad_kw, p, q, slabs, wgrad_kw):
     return bool(fused.value)
 
 
-def wgrad_tiles(n_rows, T, r_dim, c_dim, ntaps, pad, dtype, q_prologue=L.PRO_NONE, dil=1):
-    """Output tiles per split of the weight-gradient kernel conv_wgrad would launch."""
+def wgrad_tiles(n_rows, T, r_dim, c_dim, ntaps, pad, dtype, q_prologue=L.PRO_NONE, dil=1, policy=POLICY_AUTO):
+    """Output tiles per split of the weight-gradient kernel conv_wgrad would
+    launch under kernel policy `policy`."""
     t = ctypes.c_int32()
-    call("vqx_wgrad_tiles", n_rows, T, r_dim, c_dim, ntaps, pad, dil, dtype, q_prologue, ctypes.byref(t))
+    call("vqx_wgrad_tiles", n_rows, T, r_dim, c_dim, ntaps, pad, dil, dtype, q_prologue, policy, ctypes.byref(t))
     return t.value
 
 
@@ -316,14 +317,51 @@ def linear_batched_bwd(table, c, B, I, O, dc, partials=None):
     call("vqx_linear_batched_bwd", dev.data_ptr(), len(arr), ptr(c), B, I, O, ptr(dc), ptr(partials), stream_ptr())
 
 
-def weight_norm_fwd(table):
-    arr, dev = table
-    call("vqx_weight_norm_fwd", ctypes.addressof(arr), dev.data_ptr(), len(arr), stream_ptr())
+WNF_NORMS_READY = 1  # include/vqx.h VQX_WNF_NORMS_READY
 
 
-def weight_norm_bwd(table):
+def weight_norm_fwd(table, flags=0):
     arr, dev = table
-    call("vqx_weight_norm_bwd", ctypes.addressof(arr), dev.data_ptr(), len(arr), stream_ptr())
+    if flags:
+        call("vqx_weight_norm_fwd_flags", ctypes.addressof(arr), dev.data_ptr(), len(arr), flags, stream_ptr())
+    else:
+        call("vqx_weight_norm_fwd", ctypes.addressof(arr), dev.data_ptr(), len(arr), stream_ptr())
+
+
+def weight_norm_bwd(table, sq_partials=None):
+    """sq_partials: also leave the sum of squares of every written gradient
+    value as per-wave partials there (weight_norm_bwd_partials(table) floats)."""
+    arr, dev = table
+    if sq_partials is None:
+        call("vqx_weight_norm_bwd", ctypes.addressof(arr), dev.data_ptr(), len(arr), stream_ptr())
+        return
+    _check_cuda(sq_partials)
+    call("vqx_weight_norm_bwd_sq", ctypes.addressof(arr), dev.data_ptr(), len(arr), ptr(sq_partials),
+         sq_partials.numel(), stream_ptr())
+
+
+def weight_norm_bwd_partials(table):
+    """Number of sum-of-squares partials weight_norm_bwd(table, sq) writes."""
+    arr, _ = table
+    n = ctypes.c_int64(0)
+    call("vqx_weight_norm_bwd_partials", ctypes.addressof(arr), len(arr), ctypes.byref(n))
+    return n.value
+
+
+def sq_norm_finish(partials, g, ranges, out, scratch):
+    """out[0] = sum(partials) + sum over ranges (int64 [n, 2] device tensor of
+    (offset, length) into g) of g^2, in a fixed order; scratch >= 64 floats."""
+    _check_cuda(partials, g, out, scratch)
+    if scratch.numel() < 64:
+        raise ValueError("sq_norm_finish: scratch needs 64 floats")
+    nr = 0 if ranges is None else ranges.shape[0]
+    if nr:
+        _check_cuda(ranges)
+        if ranges.dtype != torch.int64 or ranges.dim() != 2 or ranges.shape[1] != 2:
+            raise ValueError("sq_norm_finish: ranges must be an int64 [n, 2] tensor")
+    call("vqx_sq_norm_finish", ptr(partials), partials.numel(), ptr(g), ptr(ranges) if nr else None, nr, ptr(scratch),
+         ptr(out), stream_ptr())
+    return out
 
 
 def groupnorm_stats(x, T, G, partials, mean_rstd, eps=1e-5):
@@ -504,6 +542,17 @@ def adam_step(p, g, m, v, hyper, sumsq, max_norm):
 
 def radam_hyper(step, lr0, gamma, step_size, beta1, beta2, eps, hyper):
     call("vqx_radam_hyper", ptr(step), lr0, gamma, step_size, beta1, beta2, eps, ptr(hyper), stream_ptr())
+
+
+def adam_step_wn(p, g, m, v, hyper, sumsq, max_norm, rows_table, segs):
+    """adam_step plus the next forward's weight-norm preparation of the rows
+    in `rows_table` (wn_table of weight-normed convs); `segs` = (host int64
+    [n, 2] tensor, its device copy) of the other flat ranges."""
+    arr, dev = rows_table
+    sh, sd = segs
+    call("vqx_adam_step_wn", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), ptr(hyper), ptr(sumsq), max_norm,
+         ctypes.addressof(arr), dev.data_ptr(), len(arr), sh.data_ptr() if sh.numel() else None,
+         ptr(sd) if sh.numel() else None, sh.shape[0], stream_ptr())
 
 
 def radam_step(p, g, m, v, hyper, sumsq, max_norm):
