@@ -139,8 +139,9 @@ typedef struct vqx_conv_args {
 #define VQX_POLICY_TALL256 2
 #define VQX_POLICY_TALL512 3
 #define VQX_POLICY_TR128 4
-#define VQX_POLICY_K1_3PCU 5  /* ABI 125: as AUTO, but every bf16 1x1 FWD and DGRAD+WGRAD on the
-                                 three-workgroups-per-CU kernels (one round with spare slots) */
+#define VQX_POLICY_K1_2PCU 5  /* ABI 125: as AUTO, but the bf16 1x1 FWD and DGRAD+WGRAD on the
+                                 two-workgroups-per-CU kernels (AUTO: three per CU, one round
+                                 with spare slots, since round 5) */
 
 int vqx_conv1d_fwd(const vqx_conv_args* a, vqx_stream_t stream);
 int vqx_conv1d_dgrad(const vqx_conv_args* a, vqx_stream_t stream);

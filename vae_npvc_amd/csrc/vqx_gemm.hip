@@ -76,8 +76,8 @@ int cu_count() {
 
 bool three_per_cu(int grid, int policy) {
   const int cus = cu_count();
-  if (policy == POL_K1_3PCU) return cus > 0 && grid <= 3 * cus;
-  return policy == POL_AUTO && cus > 0 && grid > 2 * cus && grid <= 3 * cus;
+  if (policy == POL_AUTO) return cus > 0 && grid <= 3 * cus;
+  return policy == POL_K1_2PCU && cus > 0 && grid > 2 * cus && grid <= 3 * cus;
 }
 
 static void launch_mode(GemmParams& P, int mode, int64_t rows, int extra_mult, bool bf16, bool gen, hipStream_t s) {
@@ -128,7 +128,7 @@ static int conv_prepare(const vqx_conv_args* a, int mode, GemmParams& P, bool& g
   }
   if ((epi & VQX_EPI_COLSUM) && !a->colsum_part) { set_error("vqx_conv: COLSUM needs colsum_part [ceil(n_rows/128)][cout]"); return -1; }
   if (!a->y || !aligned16(a->y)) { set_error("vqx_conv: y must be non-null and 16-byte aligned"); return -1; }
-  if (a->kernel_policy < POL_AUTO || a->kernel_policy > POL_K1_3PCU) { set_error("vqx_conv: kernel_policy %d not in 0..5", a->kernel_policy); return -1; }
+  if (a->kernel_policy < POL_AUTO || a->kernel_policy > POL_K1_2PCU) { set_error("vqx_conv: kernel_policy %d not in 0..5", a->kernel_policy); return -1; }
 
   P = GemmParams{};
   P.a = a->x; P.b = a->w;
@@ -182,7 +182,7 @@ static int wgrad_prepare(const vqx_wgrad_args* a, GemmParams& P, bool& gen) {
   if (!aligned16(a->p) || !aligned16(a->q) || !a->slabs || !aligned16(a->slabs)) { set_error("vqx_conv1d_wgrad: bad pointers"); return -1; }
   if (a->shift_sign != 1 && a->shift_sign != -1) { set_error("vqx_conv1d_wgrad: shift_sign must be +-1"); return -1; }
   if (a->slab_dtype != VQX_F32 && !(a->slab_dtype == VQX_BF16 && a->dtype == VQX_BF16)) { set_error("vqx_conv1d_wgrad: slab_dtype %d (bf16 slabs need bf16 operands)", a->slab_dtype); return -1; }
-  if (a->kernel_policy < POL_AUTO || a->kernel_policy > POL_K1_3PCU) { set_error("vqx_conv1d_wgrad: kernel_policy %d not in 0..5", a->kernel_policy); return -1; }
+  if (a->kernel_policy < POL_AUTO || a->kernel_policy > POL_K1_2PCU) { set_error("vqx_conv1d_wgrad: kernel_policy %d not in 0..5", a->kernel_policy); return -1; }
   P = GemmParams{};
   P.a = a->p; P.b = a->q; P.n_rows = a->n_rows; P.T = a->T; P.lda = a->ldp; P.ldb = a->ldq;
   P.a_bytes = ((a->n_rows - 1) * (int64_t)a->ldp + a->r_dim) * es;
@@ -260,7 +260,7 @@ extern "C" int vqx_conv1d_dgrad_wgrad(const vqx_conv_args* d, const vqx_wgrad_ar
 extern "C" int vqx_wgrad_tiles(int64_t n_rows, int32_t T, int32_t r_dim, int32_t c_dim, int32_t ntaps, int32_t pad,
                                int32_t dil, int32_t dtype, int32_t q_prologue, int32_t policy, int32_t* tiles) {
   if (!tiles || n_rows <= 0 || T <= 0 || r_dim <= 0 || c_dim <= 0 || ntaps < 1 || ntaps > 8 || policy < POL_AUTO ||
-      policy > POL_K1_3PCU) {
+      policy > POL_K1_2PCU) {
     set_error("vqx_wgrad_tiles: bad arguments");
     return -1;
   }

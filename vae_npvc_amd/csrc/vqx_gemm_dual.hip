@@ -54,8 +54,9 @@ __global__ __launch_bounds__(256, 2) void dual_k1_kernel(GemmParams PD, GemmPara
 }
 
 // the same, three workgroups per CU (32-deep K-tiles in a 3-deep ring, 48 KiB
-// of LDS): kernel policy POL_K1_3PCU.  The DGRAD round then leaves a third of
-// the slots free, which the WGRAD workgroups (or co-resident kernels) take.
+// of LDS): the automatic choice (POL_K1_2PCU keeps the two-per-CU kernel).
+// The DGRAD round leaves a third of the slots free, which the WGRAD
+// workgroups (or co-resident kernels) take at once.
 template <int EKD>
 __global__ __launch_bounds__(256, 3) void dual_k1_3_kernel(GemmParams PD, GemmParams PW, int nd, int nw, int ch) {
   __shared__ __attribute__((aligned(16))) char smem[conv_gemm_smem<bf16_t, 32, 3>()];
@@ -90,7 +91,7 @@ bool launch_dual(const GemmParams& PD, int nd, const GemmParams& PW, int nw, hip
     }
   } else if (PD.ntaps == 1 && PW.ntaps == 1 && PW.tap_reuse == 0 && nd % 8 == 0) {
     kind = 3;
-    if (PD.policy == POL_K1_3PCU) {
+    if (PD.policy == POL_AUTO) {
       kind = 4;
       switch (ekd) {
         case EK_NONE: fn = (const void*)dual_k1_3_kernel<EK_NONE>; break;

@@ -28,11 +28,12 @@ bool launch_dual(const GemmParams& PD, int nd, const GemmParams& PW, int nw, hip
 // automatic, 1 implicit-im2col kernels only (no tap reuse, no fused
 // DGRAD + WGRAD launch), 2 / 3 the tall tap-reuse kernel with 256 / 512-frame
 // tiles wherever it applies, 4 the 128-frame tap-reuse kernel only, 5 as
-// automatic but every bf16 1x1 FWD / DGRAD+WGRAD on the three-workgroups-per-CU
-// kernels (a grid of up to 3 x CUs then runs in one round with a third of the
-// slots spare: co-resident work, e.g. RCCL's kernels, takes no slot a tile
-// needs).
-enum { POL_AUTO = 0, POL_IM2COL = 1, POL_TALL256 = 2, POL_TALL512 = 3, POL_TR128 = 4, POL_K1_3PCU = 5 };
+// automatic but the bf16 1x1 FWD / DGRAD+WGRAD on the two-workgroups-per-CU
+// kernels (the round-4 choice).  Automatically a 1x1 grid of up to 3 x CUs
+// tiles runs on the three-workgroups-per-CU kernels: one round with a third of
+// the slots spare, which the fused WGRAD workgroups (and co-resident kernels,
+// e.g. RCCL's) take (profiles/r05/policy_ab.txt: step -1.4%).
+enum { POL_AUTO = 0, POL_IM2COL = 1, POL_TALL256 = 2, POL_TALL512 = 3, POL_TR128 = 4, POL_K1_2PCU = 5 };
 
 // conv_tr_kernel applies: bf16, no prologue, 3 taps / pad 1, 32-channel K
 // slices (16-channel slices when cin % 32 != 0, e.g. the 80-mel input conv),
@@ -113,8 +114,8 @@ void dispatch_tr(const GemmParams& P, int grid, hipStream_t s) {
 }
 
 // vqx_gemm.hip: compute units of the current device; true when a grid of
-// 2-per-CU conv_gemm_kernel workgroups needs more than one round but at most
-// 1.5 (automatic policy), or fits one round of three per CU (POL_K1_3PCU)
+// three per CU fits one round (automatic policy), or a grid of 2-per-CU
+// workgroups needs more than one round but at most 1.5 (POL_K1_2PCU)
 int cu_count();
 bool three_per_cu(int grid, int policy);
 
@@ -124,7 +125,10 @@ void launch_one(const GemmParams& P, int grid, hipStream_t s) {
   const double flops = MODE == MODE_WGRAD ? 2.0 * (double)P.n_rows * P.Mc * P.Nc
                                           : 2.0 * (double)P.n_rows * P.Nc * P.K;
   if constexpr (sizeof(T) == 2 && !GEN && MODE != MODE_WGRAD && PRO == VQX_PRO_NONE &&
-                (EK == EK_NONE || EK == EK_ELEM || EK == EK_SPLIT || EK == EK_GNADD)) {
+                (EK == EK_NONE || EK == EK_ELEM || EK == EK_SPLIT)) {
+    // (not GNADD: its prefetched epilogue operands need the registers of the
+    // two-per-CU kernel -- the encoder skip FWD ran 32.9 vs 27.6 us three per CU,
+    // profiles/r05/rocprof_summary_gnadd3.txt)
     // gen = 4: conv_gemm3_kernel (32-deep K-tiles, three workgroups per CU);
     // measured on the 1x1 640-column res/skip layers only, so 1x1 only
     if (P.ntaps == 1 && three_per_cu(grid, P.policy)) {

@@ -186,8 +186,8 @@ class EngineOptions:
                        (vqx_adam_step_wn); the forward then packs only the
                        ConvTranspose layers
       kernel_policy    include/vqx.h VQX_POLICY_* of every conv GEMM call (5:
-                       the 1x1 layers on three-workgroups-per-CU kernels,
-                       which leave slots for co-resident RCCL kernels)"""
+                       the 1x1 layers on the two-workgroups-per-CU kernels
+                       of round 4; automatic: three per CU)"""
     fuse_gn: bool = True
     enc_gn_finalize: bool = False
     side_stream: bool = False

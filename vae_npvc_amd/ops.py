@@ -29,7 +29,7 @@ def _check_cuda(*ts):
             raise L.VqxError("libvqx ops need device tensors (the HIP kernels are the only implementation)")
 
 
-POLICY_AUTO, POLICY_IM2COL, POLICY_TALL256, POLICY_TALL512, POLICY_TR128, POLICY_K1_3PCU = 0, 1, 2, 3, 4, 5  # vqx.h
+POLICY_AUTO, POLICY_IM2COL, POLICY_TALL256, POLICY_TALL512, POLICY_TR128, POLICY_K1_2PCU = 0, 1, 2, 3, 4, 5  # vqx.h
 _policy = POLICY_AUTO
 
 
@@ -38,7 +38,7 @@ def set_kernel_policy(policy):
     VQX_POLICY_*; for tests and A/B tools -- the library itself keeps no such
     state: the policy travels in every call's arguments).  Returns the old one."""
     global _policy
-    if policy not in (POLICY_AUTO, POLICY_IM2COL, POLICY_TALL256, POLICY_TALL512, POLICY_TR128, POLICY_K1_3PCU):
+    if policy not in (POLICY_AUTO, POLICY_IM2COL, POLICY_TALL256, POLICY_TALL512, POLICY_TR128, POLICY_K1_2PCU):
         raise ValueError(f"kernel policy {policy} not in 0..5")
     prev, _policy = _policy, int(policy)
     return prev
