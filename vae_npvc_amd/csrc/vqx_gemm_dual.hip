@@ -58,12 +58,13 @@ __global__ __launch_bounds__(256, 2) void dual_k1_kernel(GemmParams PD, GemmPara
 // The DGRAD round leaves a third of the slots free, which the WGRAD
 // workgroups (or co-resident kernels) take at once.
 template <int EKD>
-__global__ __launch_bounds__(256, 3) void dual_k1_3_kernel(GemmParams PD, GemmParams PW, int nd, int nw, int ch) {
-  __shared__ __attribute__((aligned(16))) char smem[conv_gemm_smem<bf16_t, 32, 3>()];
+__global__ __launch_bounds__(256, VQX_K1_OCC) void dual_k1_3_kernel(GemmParams PD, GemmParams PW, int nd, int nw,
+                                                                     int ch) {
+  __shared__ __attribute__((aligned(16))) char smem[conv_gemm_smem<bf16_t, VQX_K1_BK, VQX_K1_NST>()];
   (void)ch;
   const int b = blockIdx.x;
-  if (b < nd) conv_gemm_body<bf16_t, MODE_DGRAD, VQX_PRO_NONE, false, 32, 3, EKD>(PD, b, nd, smem);
-  else conv_gemm_body<bf16_t, MODE_WGRAD, VQX_PRO_NONE, false, 32, 3, EK_NONE>(PW, b - nd, nw, smem);
+  if (b < nd) conv_gemm_body<bf16_t, MODE_DGRAD, VQX_PRO_NONE, false, VQX_K1_BK, VQX_K1_NST, EKD>(PD, b, nd, smem);
+  else conv_gemm_body<bf16_t, MODE_WGRAD, VQX_PRO_NONE, false, VQX_K1_BK, VQX_K1_NST, EK_NONE>(PW, b - nd, nw, smem);
 }
 
 // 3-tap layer: conv_tr_kernel DGRAD (epilogue kind EKD) + wgrad_tr_kernel

@@ -574,7 +574,10 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
   constexpr int EP_LD = kBN + 4;  // floats; +4 keeps the b128 writes conflict-free
   constexpr int EROWS = 16 * SUB;  // rows per pass
   float* ep = (float*)smem;                 // [64][EP_LD]
-  float* csr = (float*)(smem + 36864);      // COLSUM reduction [EROWS][kBN]
+  // the GroupNorm / COLSUM reductions of a slab run after its row passes and
+  // their barrier, when ep is dead until the next slab's writes (behind the
+  // reductions' own closing barrier): they share its LDS
+  float* csr = (float*)smem;                // [EROWS][kBN]
   const int er = tid >> 4, ec = (tid & 15) * 8;
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // COLSUM accumulators
   float mn = 0.f, mm = 0.f, mq = 0.f;                       // GNSTATS running (count, mean, M2)
@@ -713,8 +716,11 @@ __device__ __forceinline__ void tile_epilogue(const GemmParams& P, f32x16_t (&ac
 //   BK=32, NST=4: 64 KiB, three 16-KiB K-tiles in flight (bf16 default).
 // Two 4-wave workgroups per CU either way.
 // LDS bytes of conv_gemm_body: the NST-deep ring of A+B K-tiles (>= the epilogue's 44 KiB)
+constexpr int kEpiBytes = 64 * (kBN + 4) * 4;  // tile_epilogue's LDS: one 64-row slab of the tile (33 KiB)
 template <typename T, int BK, int NST>
-__host__ __device__ constexpr int conv_gemm_smem() { return NST * 2 * 128 * BK * (int)sizeof(T); }
+__host__ __device__ constexpr int conv_gemm_smem() {
+  return NST * 2 * 128 * BK * (int)sizeof(T) > kEpiBytes ? NST * 2 * 128 * BK * (int)sizeof(T) : kEpiBytes;
+}
 
 // The kernel body as a device function of (bid, nwg) = (this workgroup's
 // index, workgroup count) of its own tile grid, on the caller's LDS, so that
@@ -730,9 +736,9 @@ __device__ __forceinline__ void conv_gemm_body(const GemmParams& P, int bid, int
   constexpr int PW = OP_BYTES / 1024 / 4;     // pieces per wave per operand
   constexpr int A_BYTES = OP_BYTES, STAGE = 2 * OP_BYTES;
   constexpr int NP = 2 * PW;                  // DMA pieces per wave per K-tile
-  static_assert(NST * STAGE >= 45056, "epilogue staging needs 44 KiB of LDS");
+  static_assert(conv_gemm_smem<T, BK, NST>() >= kEpiBytes, "epilogue staging needs 33 KiB of LDS");
   static_assert(BK % (16 / ES * 2) == 0 || ES == 4, "BK");
-  static_assert(conv_gemm_smem<T, BK, NST>() == NST * STAGE, "LDS");
+  static_assert(conv_gemm_smem<T, BK, NST>() >= NST * STAGE, "LDS");
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1102,10 +1108,22 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams P) {
 // <= 168 VGPRs) for 1x1 layers whose tile count lies between one and 1.5
 // rounds of the two-per-CU kernel (config 2: the decoder's 512 -> 640
 // res/skip conv, 640 tiles, which ran as a full round plus a quarter round).
+// The 1x1 pipeline shape of the many-workgroups kernels (conv_gemm3_kernel,
+// dual_k1_3_kernel): K-tile depth, ring depth and workgroups per CU.  Lab
+// builds override them (build.py -D) for same-box A/Bs through VQX_LIB.
+#ifndef VQX_K1_BK
+#define VQX_K1_BK 32
+#endif
+#ifndef VQX_K1_NST
+#define VQX_K1_NST 3
+#endif
+#ifndef VQX_K1_OCC
+#define VQX_K1_OCC 3
+#endif
 template <typename T, int MODE, int PRO, bool GEN, int EK>
-__global__ __launch_bounds__(256, 3) void conv_gemm3_kernel(GemmParams P) {
-  __shared__ __attribute__((aligned(16))) char smem[conv_gemm_smem<T, 32, 3>()];
-  conv_gemm_body<T, MODE, PRO, GEN, 32, 3, EK>(P, blockIdx.x, gridDim.x, smem);
+__global__ __launch_bounds__(256, VQX_K1_OCC) void conv_gemm3_kernel(GemmParams P) {
+  __shared__ __attribute__((aligned(16))) char smem[conv_gemm_smem<T, VQX_K1_BK, VQX_K1_NST>()];
+  conv_gemm_body<T, MODE, PRO, GEN, VQX_K1_BK, VQX_K1_NST, EK>(P, blockIdx.x, gridDim.x, smem);
 }
 
 
