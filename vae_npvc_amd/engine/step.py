@@ -192,7 +192,7 @@ class EngineOptions:
     enc_gn_finalize: bool = False
     side_stream: bool = False
     wgrad_wgs: int = 256
-    wgrad_wgs_1x1: int = 512
+    wgrad_wgs_1x1: int = 256
     wgrad_wgs_solo: int = 512
     wgrad_min_k: int = 512
     slab_f32: bool = False
@@ -571,8 +571,12 @@ class VQVAEEngine:
         # Round 3 (profiles/r03/wgs_ab.txt): with the 3-tap WGRAD inside the fused
         # DGRAD+WGRAD launch (512 DGRAD workgroups of its own), 256 split-K
         # workgroups for the 3-tap layers (dec conv_in 4 splits, enc k3 8) beat
-        # 512: 5.43 vs 5.53 ms per step; 1x1 layers stay at 512, and so do the
-        # stage convolutions, whose WGRAD runs alone (no DGRAD beside it).
+        # 512: 5.43 vs 5.53 ms per step; the stage convolutions, whose WGRAD
+        # runs alone (no DGRAD beside it), stay at 512.  Round 5
+        # (profiles/r05/wgs_ab.txt): with the 1x1 DGRAD + WGRAD launch three
+        # workgroups per CU, 256 for the 1x1 layers (16 splits, half the slab
+        # bytes) beat 512 by 1.4%: the 512 DGRAD + 256 WGRAD workgroups are one
+        # round of three per CU; 192 +0.9%, 128 +5%, 384 +2%.
         o = self.opt  # workgroups per wgrad launch of the 3-tap / 1x1 layers / stage convs (WGRAD alone)
         wg_target, wg_1x1, wg_solo = o.wgrad_wgs, o.wgrad_wgs_1x1, o.wgrad_wgs_solo
         solo = {id(st.conv) for st in self.enc_stages} | {id(st.conv) for st in self.dec_stages}
