@@ -128,7 +128,8 @@ void launch_one(const GemmParams& P, int grid, hipStream_t s) {
                 (EK == EK_NONE || EK == EK_ELEM || EK == EK_SPLIT)) {
     // (not GNADD: its prefetched epilogue operands need the registers of the
     // two-per-CU kernel -- the encoder skip FWD ran 32.9 vs 27.6 us three per CU,
-    // profiles/r05/rocprof_summary_gnadd3.txt)
+    // profiles/r05/rocprof_summary_gnadd3.txt, and 27.7 vs 25.2 us three per CU
+    // without the prefetch, profiles/r05/k1_pipeline_ab.txt)
     // gen = 4: conv_gemm3_kernel (32-deep K-tiles, three workgroups per CU);
     // measured on the 1x1 640-column res/skip layers only, so 1x1 only
     if (P.ntaps == 1 && three_per_cu(grid, P.policy)) {
