@@ -248,7 +248,7 @@ int vqx_weight_norm_bwd_partials(const vqx_wn_layer* layers_host, int32_t n_laye
 int vqx_weight_norm_bwd_sq(const vqx_wn_layer* layers_host, const vqx_wn_layer* layers_dev,
                            int32_t n_layers, float* sq_partials, int64_t sq_capacity, vqx_stream_t stream);
 int vqx_sq_norm_finish(const float* partials, int64_t n_partials, const float* g, const int64_t* ranges,
-                       int32_t n_ranges, float* scratch /* >= 64 floats */, float* out, vqx_stream_t stream);
+                       int32_t n_ranges, float* scratch /* >= 256 floats */, float* out, vqx_stream_t stream);
 
 /*
  * GroupNorm statistics (nn.GroupNorm, layers.py:154 (G=1), layers.py:201

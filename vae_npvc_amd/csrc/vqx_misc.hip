@@ -1702,7 +1702,7 @@ __global__ __launch_bounds__(256) void sqnorm_partial_kernel(const float* __rest
 // write: kSqBlocks blocks each sum a fixed strided share of both into
 // scratch[b], then one block adds the kSqBlocks values in order into out[0].
 // Deterministic (fixed assignment and order).
-constexpr int kSqBlocks = 64;
+constexpr int kSqBlocks = 256;  // one per CU: 64 left the pass at 9.6 us, latency-bound
 __global__ __launch_bounds__(256) void sq_partial_sum_kernel(const float* __restrict__ part, int64_t np,
                                                              const float* __restrict__ g,
                                                              const int64_t* __restrict__ rng, int nr,
@@ -1726,8 +1726,9 @@ __global__ __launch_bounds__(256) void sq_partial_sum_kernel(const float* __rest
   s = block_sum(s, red);
   if (threadIdx.x == 0) scratch[blockIdx.x] = s;
 }
-__global__ __launch_bounds__(64) void sq_final_kernel(const float* __restrict__ scratch, float* __restrict__ out) {
-  const float s = wave_sum(scratch[threadIdx.x]);
+__global__ __launch_bounds__(kSqBlocks) void sq_final_kernel(const float* __restrict__ scratch, float* __restrict__ out) {
+  __shared__ float red[16];
+  const float s = block_sum(scratch[threadIdx.x], red);
   if (threadIdx.x == 0) out[0] = s;
 }
 
@@ -2257,7 +2258,7 @@ extern "C" int vqx_sq_norm_finish(const float* partials, int64_t n_partials, con
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(sq_partial_sum_kernel, dim3(kSqBlocks), dim3(256), 0, s, partials, n_partials, g, ranges, n_ranges,
                      scratch);
-  hipLaunchKernelGGL(sq_final_kernel, dim3(1), dim3(64), 0, s, scratch, out);
+  hipLaunchKernelGGL(sq_final_kernel, dim3(1), dim3(kSqBlocks), 0, s, scratch, out);
   return launch_status("vqx_sq_norm_finish");
 }
 

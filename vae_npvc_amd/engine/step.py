@@ -306,7 +306,11 @@ class Workspace:
         if not train:
             return
         NCe = max([sw.N * sw.C for sw in self.enc] + [1])
-        self.dxhat = e(self.N, Fo)
+        if eng.fin2_pad is not None:  # zero columns up to the padded K of the output conv's DGRAD
+            self.dxhat_pad = torch.zeros(self.N, eng.fin2_pad[0], device=dev, dtype=cd)
+            self.dxhat = self.dxhat_pad[:, :Fo]
+        else:
+            self.dxhat = self.dxhat_pad = e(self.N, Fo)
         self.df1 = e(self.Nskip, S)
         NCd = max([sw.N * sw.C for sw in self.dec] + [1])
         self.dg_flat = e(NCd)
@@ -545,6 +549,19 @@ class VQVAEEngine:
         self.skip_stage = with_blocks[0]
         self.fin1 = self._mk(m.decoder.final_layer[1], "decoder.final_layer.1")
         self.fin2 = self._mk(m.decoder.final_layer[3], "decoder.final_layer.3")
+        # The output conv's DGRAD has K = final_channels (80 mel), off the
+        # 64-deep K-tiles: the generic-tile kernel ran it 22 us.  Its packed
+        # weight gets zero rows up to a multiple of 64 (the pack and Adam write
+        # only the real rows) and dL/dxhat zero columns (Workspace.dxhat_pad),
+        # so the DGRAD runs on the regular tiles; everything else sees the
+        # real rows and columns.
+        f2 = self.fin2
+        Fp = -(-f2.cout // 64) * 64
+        self.fin2_pad = None
+        if Fp != f2.cout and f2.kind == KIND_CONV and f2.k == 1 and not m.decoder.final_layer[3].transposed:
+            full = torch.zeros(Fp, f2.cin, device=self.device, dtype=f2.wp.dtype)
+            f2.wp = full[:f2.cout]
+            self.fin2_pad = (Fp, full)
         self.dec_blocks = [b for st in self.dec_stages for b in st.blocks]
         self.dec_cond = [b.cond for b in self.dec_blocks]
         # speaker-conditioning linears grouped by output width (one batched launch per group)
@@ -1209,7 +1226,16 @@ class VQVAEEngine:
         dxhat = w.dxhat
         ns = len(self.dec_stages)
         self.bias_grad(f2, dxhat, w)
-        self.wgrad_dgrad(f2, dxhat, w.f1, w.df1, w.T, mask=w.f1, mask_slope=0.0, colsum=w.cs_f1)
+        if self.fin2_pad is not None:
+            Fp, wfull = self.fin2_pad
+            pol = self.opt.kernel_policy
+            ops.conv_dgrad_wgrad(w.dxhat_pad, wfull, w.df1,
+                                 dict(T=w.T, cin=Fp, cout=f2.cin, ntaps=1, pad=0, dil=1, policy=pol, mask=w.f1,
+                                      mask_slope=0.0, colsum=w.cs_f1),
+                                 dxhat, w.f1, f2.slab, dict(T=w.T, ntaps=1, pad=0, dil=1, splits=f2.splits, policy=pol,
+                                                            r_dim=f2.cout, c_dim=f2.cin, shift_sign=1))
+        else:
+            self.wgrad_dgrad(f2, dxhat, w.f1, w.df1, w.T, mask=w.f1, mask_slope=0.0, colsum=w.cs_f1)
         s = math.sqrt(1.0 / self.n_dec_layers)
         # dL/dskip (identical for every block) -> tail columns of every [dx | dskip] buffer
         lst = ns - 1

@@ -350,10 +350,10 @@ def weight_norm_bwd_partials(table):
 
 def sq_norm_finish(partials, g, ranges, out, scratch):
     """out[0] = sum(partials) + sum over ranges (int64 [n, 2] device tensor of
-    (offset, length) into g) of g^2, in a fixed order; scratch >= 64 floats."""
+    (offset, length) into g) of g^2, in a fixed order; scratch >= 256 floats."""
     _check_cuda(partials, g, out, scratch)
-    if scratch.numel() < 64:
-        raise ValueError("sq_norm_finish: scratch needs 64 floats")
+    if scratch.numel() < 256:
+        raise ValueError("sq_norm_finish: scratch needs 256 floats")
     nr = 0 if ranges is None else ranges.shape[0]
     if nr:
         _check_cuda(ranges)
