@@ -36,10 +36,13 @@ for k, v in agg.items():
         continue
     res[k] = {"dispatches": len(f), "read_bytes_per_launch": sum(f) / len(f), "write_bytes_per_launch": sum(w) / len(w),
               "hbm_bytes_per_launch": sum(f) / len(f) + sum(w) / len(w)}
-adam = res.get("vqx::adam_kernel")
+adam = res.get("vqx::adam_kernel") or res.get("vqx::adam_wn_kernel")
 calib = None
 if adam:
-    calib = {"adam_expected_read": 16.0 * n_params, "adam_expected_write": 12.0 * n_params,
+    # adam_wn_kernel (round 5) also writes the Conv1d packed weights (2 B per weight in bf16)
+    # and the row norms: its reads are the same 16 B per parameter, its writes 12 B + those
+    calib = {"kernel": "vqx::adam_kernel" if "vqx::adam_kernel" in res else "vqx::adam_wn_kernel",
+             "adam_expected_read": 16.0 * n_params, "adam_expected_write_min": 12.0 * n_params,
              "adam_measured_read": adam["read_bytes_per_launch"], "adam_measured_write": adam["write_bytes_per_launch"]}
 json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), bench.py --no-probe",
            "correction": "read = 2 x FETCH_SIZE (gfx950 wide-read half count); KiB -> bytes",

@@ -1,5 +1,5 @@
 """Per-kernel time per bf16 training step from a rocprofv3 kernel trace of bench.py:
-steps are the windows between consecutive adam_kernel launches; windows holding
+steps are the windows between consecutive adam_kernel / adam_wn_kernel launches; windows holding
 fp32 GEMMs (the bench's fp32 leg) or more than one step's launches are skipped.
 python tools/trace_steps.py TRACE_CSV [TOP]"""
 import csv
@@ -8,7 +8,7 @@ from collections import defaultdict
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 top = int(sys.argv[2]) if len(sys.argv) > 2 else 40
-ad = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("vqx::adam_kernel")]
+ad = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith(("vqx::adam_kernel", "vqx::adam_wn_kernel"))]
 wins = []
 for a, b in zip(ad[:-1], ad[1:]):
     seg = rows[a:b]
