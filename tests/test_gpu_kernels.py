@@ -894,11 +894,12 @@ def test_split_epilogue_with_narrow_residual(acc, B, T, tile):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("B,T", [(3, 256), (2, 128), (1, 384)])
+@pytest.mark.parametrize("B,T", [(3, 256), (2, 128), (1, 384), (1, 2048)])
 def test_gn_glu_fwd_tiles_equals_finalize_then_glu(dtype, B, T):
     """vqx_gn_glu_fwd_tiles (statistics merged from the GEMM's GNSTATS tiles
     inside the GLU launch) = vqx_gn_finalize_tiles + vqx_gn_glu_fwd, bit for
-    bit, including the mean/rstd it writes for the backward."""
+    bit, including the mean/rstd it writes for the backward.  T = 2048 has 64
+    tiles per group: the merge reads them from memory instead of shuffling."""
     ops = _ops()
     torch.manual_seed(9)
     cin, cout = 512, 1024

@@ -690,12 +690,14 @@ __global__ void gn_finalize_tiles_kernel(const float* __restrict__ part, int B, 
 template <typename T> struct Vec;
 template <> struct Vec<bf16_t> {
   static constexpr int N = 8;
-  __device__ static __forceinline__ void load(const bf16_t* p, float* f) {
-    const uint4 u = *(const uint4*)p;
+  typedef uint4 raw_t;  // the 16-B chunk as loaded (cvt: to floats where they are used)
+  __device__ static __forceinline__ raw_t ld(const bf16_t* p) { return *(const uint4*)p; }
+  __device__ static __forceinline__ void cvt(const raw_t& u, float* f) {
     const unsigned w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) { f[2 * i] = __uint_as_float(w[i] << 16); f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u); }
   }
+  __device__ static __forceinline__ void load(const bf16_t* p, float* f) { cvt(ld(p), f); }
   __device__ static __forceinline__ void store(bf16_t* p, const float* f) {
     unsigned w[4];
 #pragma unroll
@@ -705,10 +707,10 @@ template <> struct Vec<bf16_t> {
 };
 template <> struct Vec<float> {
   static constexpr int N = 4;
-  __device__ static __forceinline__ void load(const float* p, float* f) {
-    const f32x4_t v = *(const f32x4_t*)p;
-    f[0] = v[0]; f[1] = v[1]; f[2] = v[2]; f[3] = v[3];
-  }
+  typedef f32x4_t raw_t;
+  __device__ static __forceinline__ raw_t ld(const float* p) { return *(const f32x4_t*)p; }
+  __device__ static __forceinline__ void cvt(const raw_t& v, float* f) { f[0] = v[0]; f[1] = v[1]; f[2] = v[2]; f[3] = v[3]; }
+  __device__ static __forceinline__ void load(const float* p, float* f) { cvt(ld(p), f); }
   __device__ static __forceinline__ void store(float* p, const float* f) {
     f32x4_t v = {f[0], f[1], f[2], f[3]};
     *(f32x4_t*)p = v;
@@ -850,11 +852,13 @@ __global__ __launch_bounds__(256) void gn_bwd_reduce_vec_kernel(const T* __restr
 constexpr int kGnApplyRG = 32, kGnApplyW = 4;
 template <typename T> struct Vec4;
 template <> struct Vec4<bf16_t> {
-  __device__ static __forceinline__ void load(const bf16_t* p, float* f) {
-    const uint2 u = *(const uint2*)p;
+  typedef uint2 raw_t;
+  __device__ static __forceinline__ raw_t ld(const bf16_t* p) { return *(const uint2*)p; }
+  __device__ static __forceinline__ void cvt(const raw_t& u, float* f) {
     f[0] = __uint_as_float(u.x << 16); f[1] = __uint_as_float(u.x & 0xffff0000u);
     f[2] = __uint_as_float(u.y << 16); f[3] = __uint_as_float(u.y & 0xffff0000u);
   }
+  __device__ static __forceinline__ void load(const bf16_t* p, float* f) { cvt(ld(p), f); }
   __device__ static __forceinline__ void store(bf16_t* p, const float* f) {
     *(uint2*)p = make_uint2(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]));
   }
@@ -888,26 +892,52 @@ __global__ __launch_bounds__(512) void gn_bwd_apply_vec_kernel(const T* __restri
   const int c = ch * W;
   const float* mr4 = mr + (int64_t)b * G * 2;
   const int ng = glu ? 2 : 1;
+  const int lane = threadIdx.x & 63;
+  // The utterance's partials, one part per lane (nparts <= 64), loaded first,
+  // then gamma / beta and the first two rows; every wave then sums the
+  // partials in part order through shuffles (no LDS, no barrier), so the sum
+  // waits on the partial loads only and runs under the rows' flight.  (The
+  // LDS-staged sum behind a barrier waited on every load in flight.)
+  const bool shfl_sum = nparts <= 64;
+  float q0 = 0.f, q1 = 0.f, q2 = 0.f, q3 = 0.f;
+  if (shfl_sum && lane < nparts) {
+    const float* o = part + ((int64_t)b * nparts + lane) * pstride;
+    q0 = o[0];
+    q1 = o[1];
+    if (glu) { q2 = o[2]; q3 = o[3]; }
+  }
+  float ga[W], ba[W], gb[W], bb[W];
+  const int cc = active ? c : 0;  // inactive lanes load chunk 0 and discard it (no branch to join)
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    ga[i] = gamma[cc + i];
+    ba[i] = beta[cc + i];
+    gb[i] = glu ? gamma[cc + half + i] : 0.f;
+    bb[i] = glu ? beta[cc + half + i] : 0.f;
+  }
+  // the first row pair as raw chunks (rows clamped into the utterance), converted after the sums
+  typedef typename Vec4<T>::raw_t raw_t;
+  const int64_t nb0 = (int64_t)b * T_;
+  const int64_t n0c = nb0 + min(rg, T_ - 1), n1c = nb0 + min(rg + RG, T_ - 1);
+  const raw_t pg0 = Vec4<T>::ld(dy + n0c * lddy + cc), pa0 = Vec4<T>::ld(u + n0c * ldu + cc);
+  const raw_t pg1 = Vec4<T>::ld(dy + n1c * lddy + cc), pa1 = Vec4<T>::ld(u + n1c * ldu + cc);
+  raw_t pb0{}, pb1{};
+  if (glu) {
+    pb0 = Vec4<T>::ld(u + n0c * ldu + cc + half);
+    pb1 = Vec4<T>::ld(u + n1c * ldu + cc + half);
+  }
   float m1a = 0.f, m2a = 0.f, m1b = 0.f, m2b = 0.f;
   {
     const int cg = C / G;
     const float M = (float)T_ * (float)cg;
     float S1a = 0.f, S2a = 0.f, S1b = 0.f, S2b = 0.f;
-    // the utterance's partials staged through LDS by one load per thread, then
-    // summed by every thread in part order (a runtime loop of loads + adds
-    // paid one memory latency per part)
-    constexpr int kMaxP = 64;
-    __shared__ float sp[kMaxP][4];
-    if (nparts <= kMaxP) {
-      if ((int)threadIdx.x < 4 * nparts) {
-        const int q = threadIdx.x >> 2, k = threadIdx.x & 3;
-        sp[q][k] = (k < 2 || glu) ? part[((int64_t)b * nparts + q) * pstride + k] : 0.f;
-      }
-      __syncthreads();
+    // two loops: a global load inside the shuffle loop would make every
+    // iteration wait on all loads in flight
+    if (shfl_sum) {
       for (int q = 0; q < nparts; ++q) {
-        S1a += sp[q][0];
-        S2a += sp[q][1];
-        if (glu) { S1b += sp[q][2]; S2b += sp[q][3]; }
+        S1a += __shfl(q0, q, 64);
+        S2a += __shfl(q1, q, 64);
+        if (glu) { S1b += __shfl(q2, q, 64); S2b += __shfl(q3, q, 64); }
       }
     } else {
       for (int q = 0; q < nparts; ++q) {
@@ -918,14 +948,6 @@ __global__ __launch_bounds__(512) void gn_bwd_apply_vec_kernel(const T* __restri
       }
     }
     m1a = S1a / M; m2a = S2a / M; m1b = S1b / M; m2b = S2b / M;
-  }
-  float ga[W], ba[W], gb[W], bb[W];
-#pragma unroll
-  for (int i = 0; i < W; ++i) {
-    ga[i] = active ? gamma[c + i] : 0.f;
-    ba[i] = active ? beta[c + i] : 0.f;
-    gb[i] = active && glu ? gamma[c + half + i] : 0.f;
-    bb[i] = active && glu ? beta[c + half + i] : 0.f;
   }
   float a_du[2][W], a_dg[2][W], a_db[2][W];
 #pragma unroll
@@ -957,19 +979,29 @@ __global__ __launch_bounds__(512) void gn_bwd_apply_vec_kernel(const T* __restri
   };
   if (active) {
     int r = rg;
-    for (; r + RG < T_; r += 2 * RG) {
-      const int64_t n0 = (int64_t)b * T_ + r, n1 = n0 + RG;
-      float g0[W], ua0[W], ub0[W], g1[W], ua1[W], ub1[W];
-      gn_row_load<T>(dy, lddy, u, ldu, n0, c, half, glu, g0, ua0, ub0);
-      gn_row_load<T>(dy, lddy, u, ldu, n1, c, half, glu, g1, ua1, ub1);
-      row(n0, g0, ua0, ub0);
-      row(n1, g1, ua1, ub1);
-    }
-    if (r < T_) {
-      const int64_t n0 = (int64_t)b * T_ + r;
-      float g0[W], ua0[W], ub0[W];
-      gn_row_load<T>(dy, lddy, u, ldu, n0, c, half, glu, g0, ua0, ub0);
-      row(n0, g0, ua0, ub0);
+    float g0[W], ua0[W], ub0[W], g1[W], ua1[W], ub1[W];
+    if (r + RG < T_) {  // the preloaded pair
+      Vec4<T>::cvt(pg0, g0); Vec4<T>::cvt(pa0, ua0);
+      Vec4<T>::cvt(pg1, g1); Vec4<T>::cvt(pa1, ua1);
+      if (glu) { Vec4<T>::cvt(pb0, ub0); Vec4<T>::cvt(pb1, ub1); }
+      row(nb0 + r, g0, ua0, ub0);
+      row(nb0 + r + RG, g1, ua1, ub1);
+      for (r += 2 * RG; r + RG < T_; r += 2 * RG) {
+        const int64_t n0 = nb0 + r, n1 = n0 + RG;
+        gn_row_load<T>(dy, lddy, u, ldu, n0, c, half, glu, g0, ua0, ub0);
+        gn_row_load<T>(dy, lddy, u, ldu, n1, c, half, glu, g1, ua1, ub1);
+        row(n0, g0, ua0, ub0);
+        row(n1, g1, ua1, ub1);
+      }
+      if (r < T_) {
+        const int64_t n0 = nb0 + r;
+        gn_row_load<T>(dy, lddy, u, ldu, n0, c, half, glu, g0, ua0, ub0);
+        row(n0, g0, ua0, ub0);
+      }
+    } else if (r < T_) {  // one row: the preloaded first
+      Vec4<T>::cvt(pg0, g0); Vec4<T>::cvt(pa0, ua0);
+      if (glu) Vec4<T>::cvt(pb0, ub0);
+      row(nb0 + r, g0, ua0, ub0);
     }
   }
   __shared__ float lds[RG][16][2 * W];
@@ -1011,61 +1043,94 @@ __global__ __launch_bounds__(256) void gn_glu_fwd_vec_kernel(const T* __restrict
   constexpr int V = Vec<T>::N;
   const int ch = threadIdx.x % cpr, rs = threadIdx.x / cpr, nrs = 256 / cpr;
   const int c = ch * V;
-  __shared__ float smr[4];
-  if (tiles) {
-    // statistics of this block's utterance (T % fpb == 0: the fpb frames share
-    // one) merged from the producing GEMM's GNSTATS tiles, as
-    // gn_finalize_tiles_kernel does; the utterance's first block stores them
-    const int b0 = blockIdx.x * fpb / T_, rg = T_ / 128, ntn = 2 * half / 128, tpg = ntn / 2;
-    // the utterance's tiles staged through LDS by one thread each (a serial
-    // merge loop over global loads paid one memory latency per tile), then
-    // merged by threads 0 / 1 in the same order
-    constexpr int kMaxTl = 64;
-    __shared__ float tl[2 * kMaxTl][3];
-    const int nt = rg * tpg;
-    const bool staged = nt <= kMaxTl;
-    if (staged) {
-      if ((int)threadIdx.x < 2 * nt) {
-        const int gi = threadIdx.x / nt, k = threadIdx.x - gi * nt, r = k / tpg, t = k - r * tpg;
-        const float* o = tiles + ((int64_t)(b0 * rg + r) * ntn + gi * tpg + t) * 4;
-        tl[threadIdx.x][0] = o[0];
-        tl[threadIdx.x][1] = o[1];
-        tl[threadIdx.x][2] = o[2];
-      }
-      __syncthreads();
-    }
-    if (threadIdx.x < 2) {
-      const int gi = threadIdx.x;
-      double n = 0.0, mean = 0.0, m2 = 0.0;
-      for (int r = 0; r < rg; ++r)
-        for (int t = 0; t < tpg; ++t) {
-          const float* o = staged ? tl[gi * nt + r * tpg + t]
-                                  : tiles + ((int64_t)(b0 * rg + r) * ntn + gi * tpg + t) * 4;
-          const double nb = o[0];
-          if (nb == 0.0) continue;
-          const double d = (double)o[1] - mean;
-          const double nn = n + nb;
-          mean += d * nb / nn;
-          m2 += (double)o[2] + d * d * n * nb / nn;
-          n = nn;
-        }
-      const float var = n > 0.0 ? (float)(m2 / n) : 0.f;
-      smr[2 * gi] = (float)mean;
-      smr[2 * gi + 1] = 1.0f / sqrtf(var + eps);
-      if ((blockIdx.x * fpb) % T_ == 0) {
-        mr_out[4 * b0 + 2 * gi] = smr[2 * gi];
-        mr_out[4 * b0 + 2 * gi + 1] = smr[2 * gi + 1];
-      }
-    }
-    __syncthreads();
+  const int lane = threadIdx.x & 63;
+  // In-launch statistics (tiles != null): this block's utterance (T % fpb == 0:
+  // the fpb frames share one) merged from the producing GEMM's GNSTATS tiles,
+  // as gn_finalize_tiles_kernel does, by wave 0: lane k loads tile k (group
+  // k / nt), then the tiles are merged in order through shuffles, lane parity
+  // choosing the group, in double, and lanes 0 / 1 leave the result in LDS
+  // behind a barrier fenced for LDS only.  The tile loads go out first, then
+  // gamma / beta and the first rows: the merge waits on the tile loads only
+  // and the barrier on the merge, with the rows in flight.  (Round 5:
+  // __syncthreads' fence waits on every load in flight, so the merge behind
+  // it cost 2.6 us of a 13.2 us launch against the precomputed-statistics
+  // path; the merge in every wave cost as much in f64 issue.)
+  const int b0 = blockIdx.x * fpb / T_, rg = T_ / 128, ntn = 2 * half / 128, tpg = ntn / 2, nt = rg * tpg;
+  const bool shfl_merge = 2 * nt <= 64;  // every tile in one lane
+  float tl0 = 0.f, tl1 = 0.f, tl2 = 0.f;
+  if (tiles && shfl_merge && (int)threadIdx.x < 2 * nt) {
+    const int gi = lane / nt, k = lane - gi * nt, r = k / tpg, t = k - r * tpg;
+    const float* o = tiles + ((int64_t)(b0 * rg + r) * ntn + gi * tpg + t) * 4;
+    tl0 = o[0];
+    tl1 = o[1];
+    tl2 = o[2];
   }
   float ga[V], ba[V], gb[V], bb[V];
 #pragma unroll
   for (int i = 0; i < V; ++i) { ga[i] = gamma[c + i]; ba[i] = beta[c + i]; gb[i] = gamma[c + half + i]; bb[i] = beta[c + half + i]; }
+  // two rows' loads in flight before the math of either; the first pair's
+  // raw chunks are converted after the merge, so it does not wait on them
+  typedef typename Vec<T>::raw_t raw_t;
+  const int rend = min(n_rows, blockIdx.x * fpb + fpb);
+  int r = blockIdx.x * fpb + rs;
+  const bool pair = r + nrs < rend, one = r < rend;
+  // clamped rows (every block holds at least one): the loads need no branch,
+  // whose join would wait on them
+  const int r0c = one ? r : rend - 1, r1c = pair ? r + nrs : r0c;
+  const raw_t qa0 = Vec<T>::ld(u + (int64_t)r0c * ldu + c), qb0 = Vec<T>::ld(u + (int64_t)r0c * ldu + c + half);
+  const raw_t qa1 = Vec<T>::ld(u + (int64_t)r1c * ldu + c), qb1 = Vec<T>::ld(u + (int64_t)r1c * ldu + c + half);
+  float s_ma = 0.f, s_ra = 0.f, s_mb = 0.f, s_rb = 0.f;  // mean / rstd of groups a and b (tiles path)
+  __shared__ float smr[4];
+  if (tiles && threadIdx.x < 64) {
+    const int gi = lane & 1;
+    double n = 0.0, mean = 0.0, m2 = 0.0;
+    auto merge = [&](float o0, float o1, float o2) {
+      const double nb = o0;
+      if (nb == 0.0) return;
+      const double d = (double)o1 - mean;
+      const double nn = n + nb;
+      mean += d * nb / nn;
+      m2 += (double)o2 + d * d * n * nb / nn;
+      n = nn;
+    };
+    // two loops: a global load inside the shuffle loop would make every
+    // iteration wait on all loads in flight
+    if (shfl_merge) {
+      for (int k = 0; k < nt; ++k) {
+        const int src = gi * nt + k;
+        merge(__shfl(tl0, src, 64), __shfl(tl1, src, 64), __shfl(tl2, src, 64));
+      }
+    } else {
+      for (int rr = 0; rr < rg; ++rr)
+        for (int t = 0; t < tpg; ++t) {
+          const float* o = tiles + ((int64_t)(b0 * rg + rr) * ntn + gi * tpg + t) * 4;
+          merge(o[0], o[1], o[2]);
+        }
+    }
+    const float var = n > 0.0 ? (float)(m2 / n) : 0.f;
+    const float mf = (float)mean, rf = 1.0f / sqrtf(var + eps);
+    if (threadIdx.x < 2) {
+      smr[2 * gi] = mf;
+      smr[2 * gi + 1] = rf;
+      if ((blockIdx.x * fpb) % T_ == 0) {  // the utterance's first block stores them
+        mr_out[4 * b0 + 2 * gi] = mf;
+        mr_out[4 * b0 + 2 * gi + 1] = rf;
+      }
+    }
+  }
+  if (tiles) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    s_ma = smr[0];
+    s_ra = smr[1];
+    s_mb = smr[2];
+    s_rb = smr[3];
+  }
   auto row = [&](int r, const float* ua, const float* ub) {
     const int b = r / T_;
     float ma, ra, mb, rb;
-    if (tiles) { ma = smr[0]; ra = smr[1]; mb = smr[2]; rb = smr[3]; }
+    if (tiles) { ma = s_ma; ra = s_ra; mb = s_mb; rb = s_rb; }
     else { ma = mr[4 * b + 0]; ra = mr[4 * b + 1]; mb = mr[4 * b + 2]; rb = mr[4 * b + 3]; }
     float o[V];
 #pragma unroll
@@ -1074,11 +1139,16 @@ __global__ __launch_bounds__(256) void gn_glu_fwd_vec_kernel(const T* __restrict
              fsigmoid<sizeof(T) == 2>((ub[i] - mb) * rb * gb[i] + bb[i]);
     Vec<T>::store(g + (int64_t)r * ldg + c, o);
   };
-  // two rows' loads in flight before the math of either
-  const int rend = min(n_rows, blockIdx.x * fpb + fpb);
-  int r = blockIdx.x * fpb + rs;
-  for (; r + nrs < rend; r += 2 * nrs) {
-    float ua0[V], ub0[V], ua1[V], ub1[V];
+  if (!one) return;
+  float ua0[V], ub0[V], ua1[V], ub1[V];
+  Vec<T>::cvt(qa0, ua0);
+  Vec<T>::cvt(qb0, ub0);
+  row(r, ua0, ub0);
+  if (!pair) return;
+  Vec<T>::cvt(qa1, ua1);
+  Vec<T>::cvt(qb1, ub1);
+  row(r + nrs, ua1, ub1);
+  for (r += 2 * nrs; r + nrs < rend; r += 2 * nrs) {
     Vec<T>::load(u + (int64_t)r * ldu + c, ua0);
     Vec<T>::load(u + (int64_t)r * ldu + c + half, ub0);
     Vec<T>::load(u + (int64_t)(r + nrs) * ldu + c, ua1);
@@ -1087,7 +1157,6 @@ __global__ __launch_bounds__(256) void gn_glu_fwd_vec_kernel(const T* __restrict
     row(r + nrs, ua1, ub1);
   }
   if (r < rend) {
-    float ua0[V], ub0[V];
     Vec<T>::load(u + (int64_t)r * ldu + c, ua0);
     Vec<T>::load(u + (int64_t)r * ldu + c + half, ub0);
     row(r, ua0, ub0);
