@@ -894,10 +894,10 @@ __global__ __launch_bounds__(512) void gn_bwd_apply_vec_kernel(const T* __restri
   const int ng = glu ? 2 : 1;
   const int lane = threadIdx.x & 63;
   // The utterance's partials, one part per lane (nparts <= 64), loaded first,
-  // then gamma / beta and the first two rows; every wave then sums the
-  // partials in part order through shuffles (no LDS, no barrier), so the sum
-  // waits on the partial loads only and runs under the rows' flight.  (The
-  // LDS-staged sum behind a barrier waited on every load in flight.)
+  // then gamma / beta and the first two rows as raw chunks; every wave then
+  // sums the partials in part order through shuffles (no LDS, no barrier), so
+  // the sum waits on the partial loads only and runs under the rows' flight.
+  // (The LDS-staged sum ran before any row load was issued.)
   const bool shfl_sum = nparts <= 64;
   float q0 = 0.f, q1 = 0.f, q2 = 0.f, q3 = 0.f;
   if (shfl_sum && lane < nparts) {
@@ -1049,12 +1049,14 @@ __global__ __launch_bounds__(256) void gn_glu_fwd_vec_kernel(const T* __restrict
   // as gn_finalize_tiles_kernel does, by wave 0: lane k loads tile k (group
   // k / nt), then the tiles are merged in order through shuffles, lane parity
   // choosing the group, in double, and lanes 0 / 1 leave the result in LDS
-  // behind a barrier fenced for LDS only.  The tile loads go out first, then
-  // gamma / beta and the first rows: the merge waits on the tile loads only
-  // and the barrier on the merge, with the rows in flight.  (Round 5:
-  // __syncthreads' fence waits on every load in flight, so the merge behind
-  // it cost 2.6 us of a 13.2 us launch against the precomputed-statistics
-  // path; the merge in every wave cost as much in f64 issue.)
+  // for the barrier.  The tile loads go out first, then gamma / beta and the
+  // first rows as raw chunks: the merge waits on the tile loads only (vmcnt
+  // counts in issue order) and the barrier (an LDS wait on gfx950) on the
+  // merge, with the rows in flight.  (Round 5: with the rows loaded after the
+  // barrier, as program order had them, the merge cost 2.6 us of a 13.2 us
+  // launch against the precomputed-statistics path; loads converted as they
+  // are issued would wait right there.  The merge in every wave, without the
+  // barrier, cost as much in f64 issue as it saved.)
   const int b0 = blockIdx.x * fpb / T_, rg = T_ / 128, ntn = 2 * half / 128, tpg = ntn / 2, nt = rg * tpg;
   const bool shfl_merge = 2 * nt <= 64;  // every tile in one lane
   float tl0 = 0.f, tl1 = 0.f, tl2 = 0.f;
@@ -1119,9 +1121,7 @@ __global__ __launch_bounds__(256) void gn_glu_fwd_vec_kernel(const T* __restrict
     }
   }
   if (tiles) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    __syncthreads();  // (waits on LDS only: the rows' loads stay in flight)
     s_ma = smr[0];
     s_ra = smr[1];
     s_mb = smr[2];
