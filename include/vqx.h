@@ -319,6 +319,16 @@ int vqx_colsum(const void* x, int32_t ldx, int32_t dtype, int64_t n_rows, int32_
                float* partials /* >= 64*C */, float* out, int32_t accumulate, vqx_stream_t stream);
 
 /*
+ * The first level of vqx_colsum alone (ABI 126): partials[p][c] = the sum of
+ * row part p of column c, p < vqx_colsum_parts(n_rows, C, dtype) <= 64.  The
+ * caller reduces them later, e.g. as a VQX_WN_COLREDUCE entry of the batched
+ * weight-norm backward (a conv bias gradient without a launch of its own).
+ */
+int vqx_colsum_parts(int64_t n_rows, int32_t C, int32_t dtype, int32_t* nparts);
+int vqx_colsum_partials(const void* x, int32_t ldx, int32_t dtype, int64_t n_rows, int32_t C,
+                        float* partials /* >= nparts * C */, vqx_stream_t stream);
+
+/*
  * Frame-major copy of the (B, C, T) input batch, with dtype conversion
  * (the reference's z.transpose(1,2).contiguous(), layers_vq.py:274-276).
  */
@@ -400,6 +410,14 @@ int vqx_gather_rows_host(const float* src, int32_t ld_src, const int32_t* rows, 
  *   dz[n][d] = scale * (z[n][d] - zq[n][d])  written in dtype. */
 int vqx_vq_commit_bwd(const float* z, const float* zq, int64_t count, float scale, void* dz,
                       int32_t dtype, vqx_stream_t stream);
+/* The same over [n_rows][D] rows, plus the column sums of the dz it stores
+ * (ABI 126): partials[p][d] = sum of dz[n][d] over the rows n of part p (rows
+ * n_rows*p/P .. n_rows*(p+1)/P, P = VQX_COMMIT_PARTS; empty parts write 0),
+ * the first level of the bias gradient of the conv producing z.  D % 4 == 0,
+ * D <= 1024. */
+#define VQX_COMMIT_PARTS 256
+int vqx_vq_commit_bwd_cs(const float* z, const float* zq, int64_t n_rows, int32_t D, float scale, void* dz,
+                         int32_t dtype, float* partials /* [VQX_COMMIT_PARTS][D] */, vqx_stream_t stream);
 
 /* Jitter (layers_vq.py:353-379): y[b][t][:] = x[b][src_t[t]][:]. */
 int vqx_time_gather(const void* x, void* y, int32_t B, int32_t T, int32_t C, const int32_t* src_t,
@@ -571,7 +589,7 @@ int vqx_stream_create_cu_mask(int32_t reserve_cus, vqx_stream_t* out, int32_t* c
 int vqx_stream_destroy(vqx_stream_t stream);
 
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
-#define VQX_ABI_VERSION 125
+#define VQX_ABI_VERSION 126
 int vqx_version(void);
 
 #ifdef __cplusplus

@@ -1021,6 +1021,52 @@ def test_colsum_matches_fp64_and_accumulates(dtype, n, C, ld):
     torch.testing.assert_close(out.double(), 2 * ref, rtol=1e-5, atol=2 * tol)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n,C,ld", [(16384, 80, 80), (16384, 128, 128), (777, 128, 192), (65, 8, 8), (5, 80, 80)])
+def test_colsum_partials_sum_to_colsum(dtype, n, C, ld):
+    """vqx_colsum_partials (ABI 126: the first level alone, for a bias gradient
+    reduced by the weight-norm backward's column reduce) equals vqx_colsum's
+    two levels up to summation order."""
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(n + 3 * C)
+    x = torch.randn(n, ld, generator=g).to(DEV, dtype)[:, :C]
+    npart = ops.colsum_parts(n, C, dtype)
+    assert 1 <= npart <= 64
+    part = torch.empty(npart, C, device=DEV)
+    ops.colsum_partials(x, part)
+    ref = x.double().sum(0)
+    tol = 1e-5 * (n ** 0.5) + 1e-5
+    torch.testing.assert_close(part.double().sum(0), ref, rtol=1e-5, atol=tol)
+    with pytest.raises(ValueError):
+        ops.colsum_partials(x, torch.empty(npart + 1, C, device=DEV))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("N,D", [(16384, 128), (16384, 64), (1000, 256), (100, 128)])
+def test_commit_bwd_with_column_sums(dtype, N, D):
+    """vqx_vq_commit_bwd_cs writes the same dz as vqx_vq_commit_bwd, bit for
+    bit, and per row part the column sums of the stored dz (the encoder output
+    conv's bias gradient); parts past N rows (N < 256) are zero."""
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(N + D)
+    z, zq = (torch.randn(N, D, generator=g).to(DEV) for _ in range(2))
+    scale = 2.0 * 0.25 / N
+    dz1 = torch.empty(N, D, device=DEV, dtype=dtype)
+    dz2 = torch.empty_like(dz1)
+    part = torch.full((ops.COMMIT_PARTS, D), float("nan"), device=DEV)
+    ops.vq_commit_bwd(z, zq, scale, dz1)
+    ops.vq_commit_bwd_cs(z, zq, scale, dz2, part)
+    torch.cuda.synchronize()
+    assert torch.equal(dz1, dz2)
+    assert torch.isfinite(part).all()
+    P = ops.COMMIT_PARTS
+    for p in (0, P // 2, P - 1):
+        r0, r1 = N * p // P, N * (p + 1) // P
+        ref = dz1[r0:r1].double().sum(0)
+        torch.testing.assert_close(part[p].double(), ref, rtol=1e-5, atol=1e-6 * scale * max(1, r1 - r0))
+    torch.testing.assert_close(part.double().sum(0), dz1.double().sum(0), rtol=1e-5, atol=1e-5 * scale * N ** 0.5)
+
+
 @pytest.mark.parametrize("K,N", [(512, 16384), (1024, 300), (7, 5)])
 def test_gather_rows_host_indices_equal_device_indices(K, N):
     """vqx_gather_rows_host (row ids in host memory, passed to the kernels by

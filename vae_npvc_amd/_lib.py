@@ -15,7 +15,7 @@ from pathlib import Path
 import torch  # noqa: F401  (loads the HIP runtime first; see module docstring)
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libvqx.so"
-ABI_VERSION = 125  # include/vqx.h VQX_ABI_VERSION
+ABI_VERSION = 126  # include/vqx.h VQX_ABI_VERSION
 
 VQX_F32, VQX_BF16 = 0, 1
 PRO_NONE, PRO_LRELU, PRO_RELU, PRO_SCALE_RELU = 0, 1, 2, 3
@@ -98,6 +98,8 @@ _SIGS = {
                    c_void_p],
     "vqx_gn_finalize_tiles": [c_void_p, c_int64, c_int32, c_int32, c_int32, c_float, c_void_p, c_void_p],
     "vqx_colsum": [c_void_p, c_int32, c_int32, c_int64, c_int32, c_void_p, c_void_p, c_int32, c_void_p],
+    "vqx_colsum_parts": [c_int64, c_int32, c_int32, c_void_p],
+    "vqx_colsum_partials": [c_void_p, c_int32, c_int32, c_int64, c_int32, c_void_p, c_void_p],
     "vqx_nct_to_ntc": [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_int32, c_int32, c_void_p],
     "vqx_ntc_to_nct": [c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p],
     "vqx_logloss_fwd_bwd": [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_float, c_void_p, c_int32,
@@ -111,6 +113,7 @@ _SIGS = {
     "vqx_gather_rows": [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_void_p, c_void_p],
     "vqx_gather_rows_host": [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_void_p, c_void_p],
     "vqx_vq_commit_bwd": [c_void_p, c_void_p, c_int64, c_float, c_void_p, c_int32, c_void_p],
+    "vqx_vq_commit_bwd_cs": [c_void_p, c_void_p, c_int64, c_int32, c_float, c_void_p, c_int32, c_void_p, c_void_p],
     "vqx_time_gather": [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_int32, c_void_p],
     "vqx_embedding_fwd": [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p],
     "vqx_embedding_bwd": [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p],

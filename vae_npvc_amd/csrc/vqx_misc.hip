@@ -2449,17 +2449,8 @@ extern "C" int vqx_gn_bwd(const void* dy, int32_t lddy, const void* u, int32_t l
   return launch_status("vqx_gn_bwd");
 }
 
-extern "C" int vqx_colsum(const void* x, int32_t ldx, int32_t dtype, int64_t n_rows, int32_t C, float* partials,
-                          float* out, int32_t accumulate, vqx_stream_t stream) {
-  if (n_rows <= 0 || C <= 0) { set_error("vqx_colsum: bad shape"); return -1; }
-  hipStream_t s = (hipStream_t)stream;
-  if (n_rows <= 64) {
-    if (dtype == VQX_BF16)
-      hipLaunchKernelGGL(colsum_small_kernel<bf16_t>, dim3((C + 63) / 64), dim3(256), 0, s, (const bf16_t*)x, ldx, n_rows, C, out, accumulate);
-    else
-      hipLaunchKernelGGL(colsum_small_kernel<float>, dim3((C + 63) / 64), dim3(256), 0, s, (const float*)x, ldx, n_rows, C, out, accumulate);
-    return launch_status("vqx_colsum");
-  }
+// row parts of the first colsum level and the vector kernel's lanes per row group
+static int colsum_geometry(int64_t n_rows, int C, int dtype, int* lanes) {
   const int V = dtype == VQX_BF16 ? 8 : 4;
   int L = 1;  // lanes per row group in the vector kernel: pow2 >= C/V, <= 32
   while (L < 32 && L * V < C) L <<= 1;
@@ -2468,6 +2459,14 @@ extern "C" int vqx_colsum(const void* x, int32_t ldx, int32_t dtype, int64_t n_r
   if (nparts > 64) nparts = 64;
   if (nparts > n_rows / 8) nparts = (int)(n_rows / 8);
   if (nparts < 1) nparts = 1;
+  if (lanes) *lanes = L;
+  return nparts;
+}
+
+// first level: partials[p][c] over nparts row parts
+static void colsum_partials_launch(const void* x, int ldx, int dtype, int64_t n_rows, int C, int nparts, int L,
+                                   float* partials, hipStream_t s) {
+  const int V = dtype == VQX_BF16 ? 8 : 4;
   const bool vec = (C % V == 0) && (ldx % V == 0) && (((uintptr_t)x & 15) == 0);
   if (vec) {
     const int nch = C / V;
@@ -2480,6 +2479,37 @@ extern "C" int vqx_colsum(const void* x, int32_t ldx, int32_t dtype, int64_t n_r
   } else {
     hipLaunchKernelGGL(colsum_partial_kernel<float>, dim3((C + 63) / 64, nparts), dim3(256), 0, s, (const float*)x, ldx, n_rows, C, nparts, partials);
   }
+}
+
+extern "C" int vqx_colsum_parts(int64_t n_rows, int32_t C, int32_t dtype, int32_t* nparts) {
+  if (n_rows <= 0 || C <= 0 || !nparts) { set_error("vqx_colsum_parts: bad arguments"); return -1; }
+  *nparts = colsum_geometry(n_rows, C, dtype, nullptr);
+  return 0;
+}
+
+extern "C" int vqx_colsum_partials(const void* x, int32_t ldx, int32_t dtype, int64_t n_rows, int32_t C,
+                                   float* partials, vqx_stream_t stream) {
+  if (!x || !partials || n_rows <= 0 || C <= 0 || ldx < C) { set_error("vqx_colsum_partials: bad arguments"); return -1; }
+  int L = 1;
+  const int nparts = colsum_geometry(n_rows, C, dtype, &L);
+  colsum_partials_launch(x, ldx, dtype, n_rows, C, nparts, L, partials, (hipStream_t)stream);
+  return launch_status("vqx_colsum_partials");
+}
+
+extern "C" int vqx_colsum(const void* x, int32_t ldx, int32_t dtype, int64_t n_rows, int32_t C, float* partials,
+                          float* out, int32_t accumulate, vqx_stream_t stream) {
+  if (n_rows <= 0 || C <= 0) { set_error("vqx_colsum: bad shape"); return -1; }
+  hipStream_t s = (hipStream_t)stream;
+  if (n_rows <= 64) {
+    if (dtype == VQX_BF16)
+      hipLaunchKernelGGL(colsum_small_kernel<bf16_t>, dim3((C + 63) / 64), dim3(256), 0, s, (const bf16_t*)x, ldx, n_rows, C, out, accumulate);
+    else
+      hipLaunchKernelGGL(colsum_small_kernel<float>, dim3((C + 63) / 64), dim3(256), 0, s, (const float*)x, ldx, n_rows, C, out, accumulate);
+    return launch_status("vqx_colsum");
+  }
+  int L = 1;
+  const int nparts = colsum_geometry(n_rows, C, dtype, &L);
+  colsum_partials_launch(x, ldx, dtype, n_rows, C, nparts, L, partials, s);
   hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 3) / 4), dim3(256), 0, s, partials, nparts, C, out, accumulate);
   return launch_status("vqx_colsum");
 }

@@ -581,6 +581,62 @@ __global__ void commit_bwd_kernel(const float* __restrict__ z, const float* __re
     Elem<T>::st(dz, i, scale * __fsub_rn(z[i], zq[i]));
 }
 
+// commit_bwd with the column sums of the stored dz: block p = row part p,
+// thread = (4-column chunk, row group); rows of a group four at a time (their
+// loads in flight together), the groups' sums added in order through LDS.
+template <typename T>
+__global__ __launch_bounds__(256) void commit_bwd_cs_kernel(const float* __restrict__ z, const float* __restrict__ zq,
+                                                            int64_t n_rows, int D, float scale, T* __restrict__ dz,
+                                                            float* __restrict__ part) {
+  const int cpr = D / 4, R = 256 / cpr;
+  const int ch = threadIdx.x % cpr, rg = threadIdx.x / cpr;
+  const int p = blockIdx.x;
+  const int64_t r0 = n_rows * p / VQX_COMMIT_PARTS, r1 = n_rows * (p + 1) / VQX_COMMIT_PARTS;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  auto one = [&](const f32x4_t& a, const f32x4_t& b, int64_t r) {
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = scale * __fsub_rn(a[k], b[k]);
+    if constexpr (sizeof(T) == 2) {
+      uint2 pk;
+      pk.x = pack_bf16x2(v[0], v[1]);
+      pk.y = pack_bf16x2(v[2], v[3]);
+      *(uint2*)(dz + r * D + 4 * ch) = pk;
+      // the column sums are of the values stored
+      v[0] = __uint_as_float(pk.x << 16); v[1] = __uint_as_float(pk.x & 0xffff0000u);
+      v[2] = __uint_as_float(pk.y << 16); v[3] = __uint_as_float(pk.y & 0xffff0000u);
+    } else {
+      *(f32x4_t*)(dz + r * D + 4 * ch) = f32x4_t{v[0], v[1], v[2], v[3]};
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s[k] += v[k];
+  };
+  if (rg < R) {
+    int64_t r = r0 + rg;
+    for (; r + 3 * R < r1; r += 4 * R) {
+      f32x4_t a[4], b[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[u] = *(const f32x4_t*)(z + (r + u * R) * D + 4 * ch);
+        b[u] = *(const f32x4_t*)(zq + (r + u * R) * D + 4 * ch);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) one(a[u], b[u], r + u * R);
+    }
+    for (; r < r1; r += R) one(*(const f32x4_t*)(z + r * D + 4 * ch), *(const f32x4_t*)(zq + r * D + 4 * ch), r);
+  }
+  __shared__ float lds[256 * 4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) lds[threadIdx.x * 4 + k] = s[k];
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += 256) {
+    const int cc = c >> 2, k = c & 3;
+    float t = 0.f;
+    for (int q = 0; q < R; ++q) t += lds[(q * cpr + cc) * 4 + k];
+    part[(int64_t)p * D + c] = t;
+  }
+}
+
 }  // namespace vqx
 
 using namespace vqx;
@@ -685,6 +741,22 @@ extern "C" int vqx_gather_rows_host(const float* src, int32_t ld_src, const int3
                        out + (int64_t)i0 * D);
   }
   return launch_status("vqx_gather_rows_host");
+}
+
+extern "C" int vqx_vq_commit_bwd_cs(const float* z, const float* zq, int64_t n_rows, int32_t D, float scale, void* dz,
+                                    int32_t dtype, float* partials, vqx_stream_t stream) {
+  if (!z || !zq || !dz || !partials || n_rows <= 0 || D <= 0 || D % 4 || D > 1024 || 256 % (D / 4) ||
+      (((uintptr_t)z | (uintptr_t)zq | (uintptr_t)dz) & 7)) {
+    set_error("vqx_vq_commit_bwd_cs: bad arguments (D %% 4 == 0, D / 4 dividing 256, aligned rows)");
+    return -1;
+  }
+  if (dtype == VQX_BF16)
+    hipLaunchKernelGGL(commit_bwd_cs_kernel<bf16_t>, dim3(VQX_COMMIT_PARTS), dim3(256), 0, (hipStream_t)stream, z, zq,
+                       n_rows, D, scale, (bf16_t*)dz, partials);
+  else
+    hipLaunchKernelGGL(commit_bwd_cs_kernel<float>, dim3(VQX_COMMIT_PARTS), dim3(256), 0, (hipStream_t)stream, z, zq,
+                       n_rows, D, scale, (float*)dz, partials);
+  return launch_status("vqx_vq_commit_bwd_cs");
 }
 
 extern "C" int vqx_vq_commit_bwd(const float* z, const float* zq, int64_t count, float scale, void* dz, int32_t dtype,

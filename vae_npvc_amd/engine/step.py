@@ -280,6 +280,9 @@ class Workspace:
                 sw.dr = [e(N, C + S) for _ in range(2)] if nb else None   # [dL/dx | dL/dskip] ping-pong
                 sw.dx = e(N, C) if not nb else None                        # stages without blocks
                 sw.cs = [e(_tm(N), C, dt=F32) for _ in range(nb + 1)]     # colsum partials of dL/dx_j
+                # dL/dx_nb of the last stage is zero and no kernel writes its partials: zeroed
+                # here once, not every step (earlier stages' are overwritten by the next stage's dgrad)
+                sw.cs[-1].zero_()
                 sw.cs_all = [e(B, 2 * C, dt=F32) for _ in range(nb)]      # per-utterance colsums of du
             self.dec.append(sw)
         if Td != T:
@@ -343,6 +346,10 @@ class Workspace:
         self.cs_part = e(64 * max(Cmax, S + Cmax, mel, 1024), dt=F32)
         self.cs_skip = e(_tm(self.Nskip), S, dt=F32)  # dL/dskip
         self.cs_f1 = e(_tm(self.Nskip), S, dt=F32)    # dL/d(final conv 1 output)
+        # bias-gradient row-part sums of the encoder output conv (from dL/dz) and of the
+        # output conv (from dL/dxhat), reduced by their group's weight-norm backward launch
+        self.cs_eo = torch.zeros(ops.COMMIT_PARTS, Z, device=dev, dtype=F32)  # rows past colsum_parts stay 0
+        self.cs_f2 = e(ops.colsum_parts(self.N, Fo, cd), Fo, dt=F32)
         self.lin_part = e(max(len(g) * ((O + 63) // 64) for O, g in eng.cond_groups.items()) * B * d["ydim"]
                           if eng.cond_groups else 1, dt=F32)  # split-K partials of d(embedding)
         eng._build_bwd_tables(self)
@@ -714,7 +721,7 @@ class VQVAEEngine:
         cr = ops.colreduce_entry
         t = {}
         t["fin"] = [self._wn_entry(self.fin1, True), self._wn_entry(self.fin2, True),
-                    cr(w.cs_f1, g(self.fin1.mod.bias))]
+                    cr(w.cs_f1, g(self.fin1.mod.bias)), cr(w.cs_f2, g(self.fin2.mod.bias))]
         ns = len(self.dec_stages)
         for si, st in enumerate(self.dec_stages):
             sw = w.dec[si]
@@ -734,7 +741,7 @@ class VQVAEEngine:
             t[("dec_stage", si)] = [self._wn_entry(st.conv, True),
                                     cr(self._bias_partials(w, first_folded, sw.cs[0]), g(st.conv.mod.bias))]
         t["cond"] = [self._wn_entry(Lr, True) for Lr in self.dec_cond]
-        t["enc_out"] = [self._wn_entry(self.enc_out, True)]
+        t["enc_out"] = [self._wn_entry(self.enc_out, True), cr(w.cs_eo, g(self.enc_out.mod.bias))]
         ne = len(self.enc_stages)
         for si, st in enumerate(self.enc_stages):
             sw = w.enc[si]
@@ -864,8 +871,15 @@ class VQVAEEngine:
         else:
             ops.conv_dgrad_wgrad(dy, Lr.wp, dx, dkw, x, dy, Lr.slab, dict(wkw, r_dim=Lr.cin, c_dim=Lr.cout, shift_sign=-1))
 
-    def bias_grad(self, Lr, dy, w):
-        ops.colsum(dy, w.cs_part, self.g(Lr.mod.bias))
+    def bias_grad(self, part, dy, zero_tail=False):
+        """First level of a conv bias gradient (the column sums of dy) into the
+        first colsum_parts rows of `part` (the rest must be zero: `zero_tail`
+        clears them); its group's weight-norm backward launch adds the rows (a
+        VQX_WN_COLREDUCE entry, _build_bwd_tables)."""
+        n = ops.colsum_parts(dy.shape[0], dy.shape[1], dy.dtype)
+        ops.colsum_partials(dy, part[:n])
+        if zero_tail and n < part.shape[0]:
+            ops.zero_(part[n:])
 
     # ------------------------------------------------------------ forward
     def pack_weights(self):
@@ -1145,14 +1159,19 @@ class VQVAEEngine:
         [B*T_z, Z] f32) replaces that source: parity tests feed the same
         well-conditioned dL/dz to this path and to autograd of the oracle."""
         B = w.B
-        if dz is not None:
-            ops.convert_2d(dz, w.dz)
-        elif not self.plain:  # EMA: the commitment term is the encoder's only gradient
-            ops.vq_commit_bwd(w.z, w.zq, 2.0 * self.m.beta * grad_scale / w.Nz, w.dz)
+        # the encoder output conv's bias gradient: column sums of dL/dz into the rows of
+        # w.cs_eo, added by the "enc_out" group's weight-norm backward
+        if dz is None and not self.plain:  # EMA: the commitment term is the encoder's only gradient
+            ops.vq_commit_bwd_cs(w.z, w.zq, 2.0 * self.m.beta * grad_scale / w.Nz, w.dz, w.cs_eo)
+            w.cs_eo_full = True  # every row written (allocated zero: the other path needs no clear until then)
+        else:
+            if dz is not None:
+                ops.convert_2d(dz, w.dz)
+            self.bias_grad(w.cs_eo, w.dz, zero_tail=getattr(w, "cs_eo_full", False))
+            w.cs_eo_full = False
         eo = self.enc_out
         ne = len(self.enc_stages)
         last = w.enc[-1]
-        self.bias_grad(eo, w.dz, w)
         k = 0
         cur = self._enc_cur(w, ne - 1, k)
         self.wgrad_dgrad(eo, w.dz, last.a[-1], cur, last.T, mask=last.a[-1], mask_slope=0.2,
@@ -1225,7 +1244,7 @@ class VQVAEEngine:
         f1, f2 = self.fin1, self.fin2
         dxhat = w.dxhat
         ns = len(self.dec_stages)
-        self.bias_grad(f2, dxhat, w)
+        self.bias_grad(w.cs_f2, dxhat)
         if self.fin2_pad is not None:
             Fp, wfull = self.fin2_pad
             pol = self.opt.kernel_policy
@@ -1251,7 +1270,7 @@ class VQVAEEngine:
                         continue
                     ops.convert_2d(cur[:, sw.C:], w.dec[si].dr[q][:, w.dec[si].C:])
         ops.convert_2d(None, cur, cols=sw.C)  # dL/dx at the decoder output is 0: the last residual is unused
-        ops.zero_(sw.cs[-1])                   # ... and so are its bias-gradient partials
+        # (its bias-gradient partials sw.cs[-1] are zero since the workspace was allocated)
         self._wn_bwd(w, "fin")
         cur_x = cur[:, :sw.C]
         for si in reversed(range(ns)):

@@ -410,6 +410,24 @@ def colsum(x, partials, out, accumulate=False, C=None):
     return out
 
 
+def colsum_parts(n_rows, C, dtype):
+    """Row parts colsum_partials writes for an [n_rows, C] input of `dtype`."""
+    n = ctypes.c_int32()
+    call("vqx_colsum_parts", int(n_rows), int(C), dt_code(dtype), ctypes.byref(n))
+    return n.value
+
+
+def colsum_partials(x, partials):
+    """partials[p][c] = sum over row part p of x[:, c] (the first level of colsum);
+    `partials` is f32 [colsum_parts(...), C], to be reduced later (colreduce_entry)."""
+    _check_cuda(x, partials)
+    n, C = x.shape
+    if tuple(partials.shape) != (colsum_parts(n, C, x.dtype), C) or not partials.is_contiguous():
+        raise ValueError(f"colsum_partials: partials {tuple(partials.shape)} != ({colsum_parts(n, C, x.dtype)}, {C})")
+    call("vqx_colsum_partials", ptr(x), x.stride(0), dt_code(x.dtype), n, C, ptr(partials), stream_ptr())
+    return partials
+
+
 def nct_to_ntc(x_nct, y):
     B, C, T = x_nct.shape
     call("vqx_nct_to_ntc", ptr(x_nct), B, C, T, ptr(y), y.stride(0), dt_code(y.dtype), stream_ptr())
@@ -495,6 +513,22 @@ def gather_rows_host(src, rows, out):
 
 def vq_commit_bwd(z, zq, scale, dz):
     call("vqx_vq_commit_bwd", ptr(z), ptr(zq), z.numel(), scale, ptr(dz), dt_code(dz.dtype), stream_ptr())
+    return dz
+
+
+COMMIT_PARTS = 256  # vqx.h VQX_COMMIT_PARTS
+
+
+def vq_commit_bwd_cs(z, zq, scale, dz, partials):
+    """vq_commit_bwd plus partials[p][d] = column sums of the stored dz over row part p
+    (COMMIT_PARTS parts; the first level of the bias gradient of the conv producing z)."""
+    _check_cuda(z, zq, dz, partials)
+    N, D = z.shape
+    if tuple(partials.shape) != (COMMIT_PARTS, D) or not partials.is_contiguous() or tuple(dz.shape) != (N, D) \
+            or not (z.is_contiguous() and zq.is_contiguous() and dz.is_contiguous()):
+        raise ValueError("vq_commit_bwd_cs: contiguous z/zq/dz [N, D] and partials [COMMIT_PARTS, D] expected")
+    call("vqx_vq_commit_bwd_cs", ptr(z), ptr(zq), N, D, scale, ptr(dz), dt_code(dz.dtype), ptr(partials),
+         stream_ptr())
     return dz
 
 
