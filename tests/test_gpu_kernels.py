@@ -1022,6 +1022,34 @@ def test_colsum_matches_fp64_and_accumulates(dtype, n, C, ld):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,C,T,ldx", [(64, 80, 256, 80), (3, 80, 100, 128), (2, 7, 33, 7), (1, 80, 1, 80)])
+def test_logloss_matches_torch(dtype, B, C, T, ldx):
+    """vqx_logloss_fwd_bwd (log_loss, layers.py:283-296): the loss sum and
+    dL/dxhat = (xhat - x) * grad_scale, on the 64-frame LDS-tile path (C % 4
+    == 0, padded dxhat rows, ragged last tile) and the flat path (C = 7)."""
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(B * C + T)
+    x = torch.randn(B, C, T, generator=g).to(DEV)
+    xh_full = torch.randn(B * T, ldx, generator=g).to(DEV)
+    xh = xh_full[:, :C]
+    dx_full = torch.full((B * T, ldx), 7.0, device=DEV, dtype=dtype)
+    dx = dx_full[:, :C]
+    loss = torch.zeros(1, device=DEV)
+    part = torch.empty(1024, device=DEV)
+    gs = 1.0 / (B * T)
+    ops.logloss_fwd_bwd(x, xh, gs, dx, loss, part)
+    torch.cuda.synchronize()
+    d = xh.double().cpu() - x.double().cpu().transpose(1, 2).reshape(B * T, C)
+    want = (0.5 * (np.log(2 * np.pi) + d * d)).sum() / (B * T)
+    assert abs(loss.item() - want.item()) <= 1e-5 * abs(want.item())
+    d32 = xh.cpu() - x.cpu().transpose(1, 2).reshape(B * T, C)  # the kernel's f32 difference and scaling
+    torch.testing.assert_close(dx.float().cpu(), (d32 * torch.tensor(gs, dtype=torch.float32)).to(dtype).float(),
+                               rtol=0, atol=0)
+    if ldx > C:
+        assert (dx_full[:, C:] == 7.0).all()  # padding columns untouched
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("n,C,ld", [(16384, 80, 80), (16384, 128, 128), (777, 128, 192), (65, 8, 8), (5, 80, 80)])
 def test_colsum_partials_sum_to_colsum(dtype, n, C, ld):
     """vqx_colsum_partials (ABI 126: the first level alone, for a bias gradient

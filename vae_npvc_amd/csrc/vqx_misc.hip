@@ -1338,6 +1338,45 @@ __global__ __launch_bounds__(256) void logloss_kernel(const float* __restrict__ 
   if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
 
+// The same over (utterance, 64-frame tile) blocks: the tile of x (C channels
+// x 64 frames, NCT) is read row by row (coalesced) into LDS, then xhat (f32)
+// and dx move as whole 4-channel chunks of their frame-major rows (C % 4 ==
+// 0), each chunk's channels taken from the LDS tile.  (The flat kernel above
+// reads x with a stride of T floats between neighbouring lanes.)
+constexpr int kLlTile = 64;
+template <typename T>
+__global__ __launch_bounds__(256) void logloss_tile_kernel(const float* __restrict__ x, const float* __restrict__ xh,
+                                                           int ldxh, int C, int T_, float gscale, T* __restrict__ dx,
+                                                           int lddx, float* __restrict__ part) {
+  extern __shared__ float xs[];  // [C][kLlTile + 1]
+  __shared__ float red[16];
+  const int b = blockIdx.y, t0 = blockIdx.x * kLlTile;
+  const int nt = min(kLlTile, T_ - t0);
+  const float* xb = x + (int64_t)b * C * T_ + t0;
+  for (int e = threadIdx.x; e < C * kLlTile; e += 256) {
+    const int c = e / kLlTile, t = e - c * kLlTile;
+    xs[c * (kLlTile + 1) + t] = t < nt ? xb[(int64_t)c * T_ + t] : 0.f;
+  }
+  __syncthreads();
+  const int cpr = C / 4;  // chunks per frame row
+  const int64_t n0 = (int64_t)b * T_ + t0;
+  float s = 0.f;
+  for (int q = threadIdx.x; q < nt * cpr; q += 256) {
+    const int t = q / cpr, c0 = (q - t * cpr) * 4;
+    const f32x4_t h = *(const f32x4_t*)(xh + (n0 + t) * ldxh + c0);
+    float o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float d = h[k] - xs[(c0 + k) * (kLlTile + 1) + t];
+      s += 0.5f * (kLog2Pi + d * d);
+      o[k] = d * gscale;
+    }
+    if (dx) Vec4<T>::store(dx + (n0 + t) * lddx + c0, o);
+  }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) part[blockIdx.y * gridDim.x + blockIdx.x] = s;
+}
+
 __global__ void sum_partials_scale_kernel(const float* __restrict__ p, int n, float scale, float* __restrict__ out) {
   __shared__ float red[16];
   float s = 0.f;
@@ -2539,12 +2578,25 @@ extern "C" int vqx_logloss_fwd_bwd(const float* x, const float* xhat, int32_t ld
                                    float* partials, vqx_stream_t stream) {
   const int64_t total = (int64_t)B * C * T;
   if (total <= 0 || total >= (1LL << 31)) { set_error("vqx_logloss_fwd_bwd: B*C*T must be in [1, 2^31)"); return -1; }
-  const int grid = grid_for(total, 256, 1024);
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == VQX_BF16)
-    hipLaunchKernelGGL(logloss_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, x, xhat, ldxh, B, C, T, grad_scale, (bf16_t*)dxhat, lddx, partials);
-  else
-    hipLaunchKernelGGL(logloss_kernel<float>, dim3(grid), dim3(256), 0, s, x, xhat, ldxh, B, C, T, grad_scale, (float*)dxhat, lddx, partials);
+  const int tiles = (T + kLlTile - 1) / kLlTile;
+  const uintptr_t dx_align = dtype == VQX_BF16 ? 7 : 15;  // 4-element chunks: 8-B bf16 / 16-B f32 stores
+  int grid;
+  if (C % 4 == 0 && ldxh % 4 == 0 && (!dxhat || lddx % 4 == 0) && C <= 256 && (int64_t)tiles * B <= 1024 &&
+      ((uintptr_t)xhat & 15) == 0 && (!dxhat || ((uintptr_t)dxhat & dx_align) == 0)) {
+    grid = tiles * B;  // partials: at most 1024 (the caller's buffer)
+    const size_t lds = (size_t)C * (kLlTile + 1) * sizeof(float);
+    if (dtype == VQX_BF16)
+      hipLaunchKernelGGL(logloss_tile_kernel<bf16_t>, dim3(tiles, B), dim3(256), lds, s, x, xhat, ldxh, C, T, grad_scale, (bf16_t*)dxhat, lddx, partials);
+    else
+      hipLaunchKernelGGL(logloss_tile_kernel<float>, dim3(tiles, B), dim3(256), lds, s, x, xhat, ldxh, C, T, grad_scale, (float*)dxhat, lddx, partials);
+  } else {
+    grid = grid_for(total, 256, 1024);
+    if (dtype == VQX_BF16)
+      hipLaunchKernelGGL(logloss_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, x, xhat, ldxh, B, C, T, grad_scale, (bf16_t*)dxhat, lddx, partials);
+    else
+      hipLaunchKernelGGL(logloss_kernel<float>, dim3(grid), dim3(256), 0, s, x, xhat, ldxh, B, C, T, grad_scale, (float*)dxhat, lddx, partials);
+  }
   hipLaunchKernelGGL(sum_partials_scale_kernel, dim3(1), dim3(1024), 0, s, partials, grid, 1.0f / ((float)B * (float)T), loss_out);
   return launch_status("vqx_logloss_fwd_bwd");
 }
