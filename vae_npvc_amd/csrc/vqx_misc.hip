@@ -1615,131 +1615,144 @@ __global__ __launch_bounds__(256) void linear_batched_bwd_x_kernel(const vqx_lin
   }
 }
 
-// ---- speaker-conditioning fast path: I = 128 inputs, B <= 64 rows, O % 32 == 0
-// (every recipe: cond dim 128).  One workgroup per (32 output channels,
-// layer) holds all of c (64 x 128) and the layer's 32 x 128 weight slice in
-// LDS and multiplies them in one pass: one global round trip instead of one
-// per 64-wide K tile, and 2x the workgroups of the tiled kernels above.  The
-// summation orders are those of the tiled kernels (i, resp. b, ascending), so
-// the results are bit-identical to them.
-constexpr int kCondI = 128, kCondB = 64, kCondO = 32;
+// ---- speaker-conditioning fast path: I = 128 inputs, B <= 64 rows, O % 64 == 0
+// (every recipe: cond dim 128).  fp32 MFMA (v_mfma_f32_16x16x4f32, the
+// reference's fp32): a workgroup is 4 waves x 16 output channels of one
+// layer; the operands go straight from memory into the MFMA lane layout.  The
+// K index is permuted so each lane's operands are contiguous: in step s, lane
+// group q takes k = 32q + s (forward, K = I = 128) or b = 16q + s (weight
+// gradient, K = B <= 64).  (Round 5: the LDS-blocked VALU kernels these
+// replace took 11-12 us a launch, bound by three LDS reads per eight FMAs;
+// the tiled kernels above, for other shapes, sum in a different order.)
+constexpr int kCondI = 128, kCondB = 64, kCondO = 64;
 
-// out_l[b][o] = bias_l[o] + sum_i c[b][i] W_l[o][i]; grid (O/32, n)
+// out_l[b][o] = bias_l[o] + sum_i c[b][i] W_l[o][i]; grid (O/64, n)
 __global__ __launch_bounds__(256) void linear_cond_fwd_kernel(const vqx_linear_layer* __restrict__ L,
                                                               const float* __restrict__ c, int B, int O) {
   const vqx_linear_layer& l = L[blockIdx.y];
-  const float* __restrict__ W = l.W;
-  const float* __restrict__ bias = l.bias;
-  float* __restrict__ out = l.out;
-  const int o0 = blockIdx.x * kCondO;
-  __shared__ __attribute__((aligned(16))) float cs[kCondB][kCondI + 4];  // [b][i]
-  __shared__ __attribute__((aligned(16))) float wt[kCondI][kCondO + 4];  // [i][o]
-  const int t = threadIdx.x;
-  const int b = t >> 2, oq = (t & 3) * 8;
-  // all operand loads in flight at once (rows b >= B read row B-1 and are
-  // zeroed at the LDS write), the bias with them
-  constexpr int NC = kCondB * kCondI / 4 / 256, NW = kCondO * kCondI / 4 / 256;
-  f32x4_t cv[NC], wv[NW];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int q = lane >> 4, j = lane & 15;
+  const int o0 = blockIdx.x * kCondO + w * 16;
+  // B operand (k = 32q + s, n = j): W[o0 + j][32q .. 32q + 31]
+  f32x4_t wb[8];
+  const float* wr = l.W + (int64_t)(o0 + j) * kCondI + 32 * q;
 #pragma unroll
-  for (int u = 0; u < NC; ++u) {
-    const int e = t + 256 * u, r = e / (kCondI / 4), i4 = e % (kCondI / 4);
-    cv[u] = *(const f32x4_t*)(c + (int64_t)min(r, B - 1) * kCondI + 4 * i4);
-  }
+  for (int u = 0; u < 8; ++u) wb[u] = *(const f32x4_t*)(wr + 4 * u);
+  const float bj = l.bias ? l.bias[o0 + j] : 0.f;
+  for (int rt = 0; rt * 16 < B; ++rt) {
+    // A operand (m = j, k = 32q + s): c[row][32q .. 32q + 31]; rows >= B read row B-1, not stored
+    const float* cr = c + (int64_t)min(rt * 16 + j, B - 1) * kCondI + 32 * q;
+    f32x4_t ca[8];
 #pragma unroll
-  for (int u = 0; u < NW; ++u) {
-    const int e = t + 256 * u, r = e / (kCondI / 4), i4 = e % (kCondI / 4);
-    wv[u] = *(const f32x4_t*)(W + (int64_t)(o0 + r) * kCondI + 4 * i4);
-  }
-  float bj[8];
+    for (int u = 0; u < 8; ++u) ca[u] = *(const f32x4_t*)(cr + 4 * u);
+    f32x4_t acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int j = 0; j < 8; ++j) bj[j] = bias ? bias[o0 + oq + j] : 0.f;
+    for (int u = 0; u < 8; ++u) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[u][0], wb[u][0], acc, 0, 0, 0);
+      acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[u][1], wb[u][1], acc2, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[u][2], wb[u][2], acc, 0, 0, 0);
+      acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[u][3], wb[u][3], acc2, 0, 0, 0);
+    }
+    // D[m = 4q + r][n = j]
 #pragma unroll
-  for (int u = 0; u < NC; ++u) {
-    const int e = t + 256 * u, r = e / (kCondI / 4), i4 = e % (kCondI / 4);
-    const f32x4_t z = {0.f, 0.f, 0.f, 0.f};
-    *(f32x4_t*)&cs[r][4 * i4] = r < B ? cv[u] : z;
-  }
-#pragma unroll
-  for (int u = 0; u < NW; ++u) {
-    const int e = t + 256 * u, r = e / (kCondI / 4), i4 = e % (kCondI / 4);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) wt[4 * i4 + k][r] = wv[u][k];
-  }
-  __syncthreads();
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-  for (int i = 0; i < kCondI; ++i) {
-    const float x = cs[b][i];
-    const f32x4_t w0 = *(const f32x4_t*)&wt[i][oq], w1 = *(const f32x4_t*)&wt[i][oq + 4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      acc[k] = fmaf(x, w0[k], acc[k]);
-      acc[4 + k] = fmaf(x, w1[k], acc[4 + k]);
+    for (int r = 0; r < 4; ++r) {
+      const int b = rt * 16 + 4 * q + r;
+      if (b < B) l.out[(int64_t)b * O + o0 + j] = (acc[r] + acc2[r]) + bj;
     }
   }
-  if (b >= B) return;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) out[(int64_t)b * O + o0 + oq + j] = acc[j] + bj[j];
 }
 
-// dW_l[o][i] = sum_b dout_l[b][o] c[b][i], dbias_l[o] = sum_b dout_l[b][o]; grid (O/32, n)
+// dW_l[o][i] = sum_b dout_l[b][o] c[b][i], dbias_l[o] = sum_b dout_l[b][o]; grid (O/64, n)
 __global__ __launch_bounds__(256) void linear_cond_bwd_w_kernel(const vqx_linear_layer* __restrict__ L,
                                                                 const float* __restrict__ c, int B, int O) {
   const vqx_linear_layer& l = L[blockIdx.y];
-  const float* __restrict__ dout = l.dout;
-  const int o0 = blockIdx.x * kCondO;
-  __shared__ __attribute__((aligned(16))) float cs[kCondB][kCondI + 4];  // [b][i]
-  __shared__ float ds[kCondB][kCondO + 1];                               // [b][o]
-  const int t = threadIdx.x;
-  // all operand loads in flight at once (rows b >= B read row B-1 and are
-  // zeroed at the LDS write)
-  constexpr int NC = kCondB * kCondI / 4 / 256, ND = kCondB * kCondO / 256;
+  __shared__ float cs[kCondB][kCondI];  // c, rows >= B zero
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int q = lane >> 4, j = lane & 15;
+  const int o0 = blockIdx.x * kCondO + w * 16;
+  // A operand (m = j, k = b = 16q + s): dout[16q + s][o0 + j], zero past B
+  float da[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const int b = 16 * q + s;
+    da[s] = l.dout[(int64_t)min(b, B - 1) * O + o0 + j];
+  }
+  constexpr int NC = kCondB * kCondI / 4 / 256;
   f32x4_t cv[NC];
-  float dv[ND];
 #pragma unroll
   for (int u = 0; u < NC; ++u) {
-    const int e = t + 256 * u, r = e / (kCondI / 4), i4 = e % (kCondI / 4);
+    const int e = threadIdx.x + 256 * u, r = e / (kCondI / 4), i4 = e % (kCondI / 4);
     cv[u] = *(const f32x4_t*)(c + (int64_t)min(r, B - 1) * kCondI + 4 * i4);
   }
 #pragma unroll
-  for (int u = 0; u < ND; ++u) {
-    const int e = t + 256 * u, r = e / kCondO, q = e % kCondO;
-    dv[u] = dout[(int64_t)min(r, B - 1) * O + o0 + q];
-  }
-#pragma unroll
   for (int u = 0; u < NC; ++u) {
-    const int e = t + 256 * u, r = e / (kCondI / 4), i4 = e % (kCondI / 4);
+    const int e = threadIdx.x + 256 * u, r = e / (kCondI / 4), i4 = e % (kCondI / 4);
     const f32x4_t z = {0.f, 0.f, 0.f, 0.f};
     *(f32x4_t*)&cs[r][4 * i4] = r < B ? cv[u] : z;
   }
+  // dbias: the lane's 16 rows in order, then the four lane groups (q) in order
+  float db = 0.f;
 #pragma unroll
-  for (int u = 0; u < ND; ++u) {
-    const int e = t + 256 * u, r = e / kCondO, q = e % kCondO;
-    ds[r][q] = r < B ? dv[u] : 0.f;
+  for (int s = 0; s < 16; ++s) {
+    if (16 * q + s >= B) da[s] = 0.f;
+    db += da[s];
+  }
+  {
+    const float d1 = __shfl(db, j + 16, 64), d2 = __shfl(db, j + 32, 64), d3 = __shfl(db, j + 48, 64);
+    if (q == 0 && l.dbias) l.dbias[o0 + j] = ((db + d1) + d2) + d3;
   }
   __syncthreads();
-  const int ol = t >> 3, ic = (t & 7) * 16;
-  float acc[16], db = 0.f;
+  for (int it = 0; it < kCondI / 16; ++it) {
+    // B operand (k = b = 16q + s, n = j): c[16q + s][16 it + j]
+    f32x4_t acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
-#pragma unroll 4
-  for (int b = 0; b < kCondB; ++b) {
-    const float d = ds[b][ol];
-    db += d;
+    for (int s = 0; s < 16; s += 2) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(da[s], cs[16 * q + s][16 * it + j], acc, 0, 0, 0);
+      acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(da[s + 1], cs[16 * q + s + 1][16 * it + j], acc2, 0, 0, 0);
+    }
+    // D[m = 4q + r][n = j]: dW[o0 + 4q + r][16 it + j]
 #pragma unroll
-    for (int j = 0; j < 16; j += 4) {
-      const f32x4_t x = *(const f32x4_t*)&cs[b][ic + j];
-      acc[j] = fmaf(d, x[0], acc[j]);
-      acc[j + 1] = fmaf(d, x[1], acc[j + 1]);
-      acc[j + 2] = fmaf(d, x[2], acc[j + 2]);
-      acc[j + 3] = fmaf(d, x[3], acc[j + 3]);
+    for (int r = 0; r < 4; ++r) l.dW[(int64_t)(o0 + 4 * q + r) * kCondI + 16 * it + j] = acc[r] + acc2[r];
+  }
+}
+
+// dc partials: part[l * (O/64) + oc][b][i] = sum over the chunk's 64 outputs o
+// of dout_l[b][o] W_l[o][i] (k = o = o0 + 16q + s); sum_slices_wide_kernel adds
+// the slices in order.  Wave w covers inputs 32w .. 32w + 31.  grid (O/64, n)
+__global__ __launch_bounds__(256) void linear_cond_bwd_x_kernel(const vqx_linear_layer* __restrict__ L, int B, int O,
+                                                                float* __restrict__ part) {
+  const vqx_linear_layer& l = L[blockIdx.y];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int q = lane >> 4, j = lane & 15;
+  const int o0 = blockIdx.x * kCondO;
+  const int64_t slice = (int64_t)blockIdx.y * (O / kCondO) + blockIdx.x;
+  // B operand (k = 16q + s, n = j) of the wave's two 16-input tiles
+  float wv[2][16];
+#pragma unroll
+  for (int it = 0; it < 2; ++it)
+#pragma unroll
+    for (int s = 0; s < 16; ++s) wv[it][s] = l.W[(int64_t)(o0 + 16 * q + s) * kCondI + 32 * w + 16 * it + j];
+  for (int rt = 0; rt * 16 < B; ++rt) {
+    // A operand (m = j, k = 16q + s): dout[row][o0 + 16q + s]; rows >= B read row B-1, not stored
+    const float* dr = l.dout + (int64_t)min(rt * 16 + j, B - 1) * O + o0 + 16 * q;
+    float da[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) da[s] = dr[s];
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 16; s += 2) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(da[s], wv[it][s], acc, 0, 0, 0);
+        acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(da[s + 1], wv[it][s + 1], acc2, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b = rt * 16 + 4 * q + r;
+        if (b < B) part[(slice * B + b) * kCondI + 32 * w + 16 * it + j] = acc[r] + acc2[r];
+      }
     }
   }
-  const int o = o0 + ol;
-  float* dw = l.dW + (int64_t)o * kCondI + ic;
-#pragma unroll
-  for (int j = 0; j < 16; j += 4) *(f32x4_t*)(dw + j) = f32x4_t{acc[j], acc[j + 1], acc[j + 2], acc[j + 3]};
-  if ((t & 7) == 0 && l.dbias) l.dbias[o] = db;
 }
 
 // dc[e] = sum_p part[p][e] in a fixed order: each of the 4 waves of a
@@ -2766,8 +2779,11 @@ extern "C" int vqx_linear_batched_bwd(const vqx_linear_layer* table_dev, int32_t
     hipLaunchKernelGGL(linear_batched_bwd_w_kernel, dim3(nO, n, (I + kLT - 1) / kLT), dim3(256), 0, s,
                        table_dev, c, B, I, O);
   if (dc) {
-    hipLaunchKernelGGL(linear_batched_bwd_x_kernel, dim3(nO, n, ((B + kLT - 1) / kLT) * ((I + kLT - 1) / kLT)),
-                       dim3(256), 0, s, table_dev, B, I, O, partials);
+    if (I == kCondI && B <= kCondB && O % kCondO == 0 && kCondO == kLT)  // same slice count (nO per layer)
+      hipLaunchKernelGGL(linear_cond_bwd_x_kernel, dim3(O / kCondO, n), dim3(256), 0, s, table_dev, B, O, partials);
+    else
+      hipLaunchKernelGGL(linear_batched_bwd_x_kernel, dim3(nO, n, ((B + kLT - 1) / kLT) * ((I + kLT - 1) / kLT)),
+                         dim3(256), 0, s, table_dev, B, I, O, partials);
     const int64_t ne = (int64_t)B * I;
     hipLaunchKernelGGL(sum_slices_wide_kernel, dim3((unsigned)((ne + 63) / 64)), dim3(256), 0, s, partials, n * nO, ne,
                        dc);
