@@ -485,7 +485,7 @@ def test_linear_batched_and_colreduce():
     assert L.WN_COLREDUCE == 2
 
 
-@pytest.mark.parametrize("B", [64, 13])
+@pytest.mark.parametrize("B", [64, 13, 200])
 def test_linear_cond_fast_path_equals_tiled_kernels(B):
     """The fp32-MFMA conditioning kernels (I = 128, B <= 64, 16-B aligned c;
     vqx_misc.hip linear_cond_*) and the 64x64-tiled kernels the same call
@@ -520,6 +520,21 @@ def test_linear_cond_fast_path_equals_tiled_kernels(B):
         assert relerr(dc, sum(d["dout"].double() @ d["W"].double() for d in lay)) < 1e-6
     (la, dca), (lb, dcb) = runs
     assert torch.equal(dca, dcb)  # the data gradient takes the same kernels either way
+    # a row's forward output and data gradient do not depend on the batch around it
+    # (data-parallel ranks against one process on the global batch)
+    if B == 200:
+        sub = runs[0][0]
+        cs = c0[:64].clone()
+        lay64 = [dict(W=d["W"], bias=d["bias"], out=torch.empty(64, O, device=DEV), dout=d["dout"][:64].clone(),
+                      dW=torch.empty(O, I, device=DEV), dbias=torch.empty(O, device=DEV)) for d in sub]
+        tab = ops.linear_table(lay64)
+        dc64 = torch.empty(64, I, device=DEV)
+        ops.linear_batched_fwd(tab, cs, 64, I, O)
+        ops.linear_batched_bwd(tab, cs, 64, I, O, dc64)
+        torch.cuda.synchronize()
+        for d, d64 in zip(sub, lay64):
+            assert torch.equal(d["out"][:64], d64["out"])
+        assert torch.equal(dca[:64], dc64)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

@@ -1615,8 +1615,10 @@ __global__ __launch_bounds__(256) void linear_batched_bwd_x_kernel(const vqx_lin
   }
 }
 
-// ---- speaker-conditioning fast path: I = 128 inputs, B <= 64 rows, O % 64 == 0
-// (every recipe: cond dim 128).  fp32 MFMA (v_mfma_f32_16x16x4f32, the
+// ---- speaker-conditioning fast path: I = 128 inputs, O % 64 == 0 (every
+// recipe: cond dim 128); any B for the forward and the data gradient (their
+// per-row results do not depend on B: data-parallel ranks and one process on
+// the global batch agree row by row), B <= 64 for the weight gradient.  fp32 MFMA (v_mfma_f32_16x16x4f32, the
 // reference's fp32): a workgroup is 4 waves x 16 output channels of one
 // layer; the operands go straight from memory into the MFMA lane layout.  The
 // K index is permuted so each lane's operands are contiguous: in step s, lane
@@ -2758,7 +2760,7 @@ extern "C" int vqx_scale_act_2d(const void* src, int32_t ld_src, int32_t src_dty
 extern "C" int vqx_linear_batched_fwd(const vqx_linear_layer* table_dev, int32_t n, const float* c, int32_t B,
                                       int32_t I, int32_t O, vqx_stream_t stream) {
   if (!table_dev || n < 1 || !c || B < 1 || I < 1 || O < 1) { set_error("vqx_linear_batched_fwd: bad arguments"); return -1; }
-  if (I == kCondI && B <= kCondB && O % kCondO == 0 && ((uintptr_t)c & 15) == 0)
+  if (I == kCondI && O % kCondO == 0 && ((uintptr_t)c & 15) == 0)  // any B: 16-row tiles in turn
     hipLaunchKernelGGL(linear_cond_fwd_kernel, dim3(O / kCondO, n), dim3(256), 0, (hipStream_t)stream, table_dev, c, B,
                        O);
   else
@@ -2779,7 +2781,8 @@ extern "C" int vqx_linear_batched_bwd(const vqx_linear_layer* table_dev, int32_t
     hipLaunchKernelGGL(linear_batched_bwd_w_kernel, dim3(nO, n, (I + kLT - 1) / kLT), dim3(256), 0, s,
                        table_dev, c, B, I, O);
   if (dc) {
-    if (I == kCondI && B <= kCondB && O % kCondO == 0 && kCondO == kLT)  // same slice count (nO per layer)
+    // any B (16-row tiles in turn), nO slices per layer as the tiled kernel: a row's dc does not depend on B
+    if (I == kCondI && O % kCondO == 0 && kCondO == kLT)
       hipLaunchKernelGGL(linear_cond_bwd_x_kernel, dim3(O / kCondO, n), dim3(256), 0, s, table_dev, B, O, partials);
     else
       hipLaunchKernelGGL(linear_batched_bwd_x_kernel, dim3(nO, n, ((B + kLT - 1) / kLT) * ((I + kLT - 1) / kLT)),
