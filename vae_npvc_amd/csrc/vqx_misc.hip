@@ -1353,25 +1353,49 @@ __global__ __launch_bounds__(256) void logloss_tile_kernel(const float* __restri
   const int b = blockIdx.y, t0 = blockIdx.x * kLlTile;
   const int nt = min(kLlTile, T_ - t0);
   const float* xb = x + (int64_t)b * C * T_ + t0;
-  for (int e = threadIdx.x; e < C * kLlTile; e += 256) {
-    const int c = e / kLlTile, t = e - c * kLlTile;
-    xs[c * (kLlTile + 1) + t] = t < nt ? xb[(int64_t)c * T_ + t] : 0.f;
+  // loads batched U at a time (clamped addresses, no branch), then their LDS writes:
+  // a load-store pair per element paid one memory latency each
+  constexpr int U = 16;
+  for (int e0 = threadIdx.x; e0 < C * kLlTile; e0 += 256 * U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = min(e0 + 256 * u, C * kLlTile - 1), c = e / kLlTile, t = min(e - c * kLlTile, nt - 1);
+      v[u] = xb[(int64_t)c * T_ + t];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + 256 * u, c = e / kLlTile, t = e - c * kLlTile;
+      if (e < C * kLlTile) xs[c * (kLlTile + 1) + t] = t < nt ? v[u] : 0.f;
+    }
   }
   __syncthreads();
   const int cpr = C / 4;  // chunks per frame row
   const int64_t n0 = (int64_t)b * T_ + t0;
+  const int nq = nt * cpr;
   float s = 0.f;
-  for (int q = threadIdx.x; q < nt * cpr; q += 256) {
-    const int t = q / cpr, c0 = (q - t * cpr) * 4;
-    const f32x4_t h = *(const f32x4_t*)(xh + (n0 + t) * ldxh + c0);
-    float o[4];
+  constexpr int U2 = 8;
+  for (int q0 = threadIdx.x; q0 < nq; q0 += 256 * U2) {
+    f32x4_t h[U2];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float d = h[k] - xs[(c0 + k) * (kLlTile + 1) + t];
-      s += 0.5f * (kLog2Pi + d * d);
-      o[k] = d * gscale;
+    for (int u = 0; u < U2; ++u) {
+      const int qq = min(q0 + 256 * u, nq - 1), t = qq / cpr, c0 = (qq - t * cpr) * 4;
+      h[u] = *(const f32x4_t*)(xh + (n0 + t) * ldxh + c0);
     }
-    if (dx) Vec4<T>::store(dx + (n0 + t) * lddx + c0, o);
+#pragma unroll
+    for (int u = 0; u < U2; ++u) {
+      const int q = q0 + 256 * u;
+      if (q >= nq) break;
+      const int t = q / cpr, c0 = (q - t * cpr) * 4;
+      float o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float d = h[u][k] - xs[(c0 + k) * (kLlTile + 1) + t];
+        s += 0.5f * (kLog2Pi + d * d);
+        o[k] = d * gscale;
+      }
+      if (dx) Vec4<T>::store(dx + (n0 + t) * lddx + c0, o);
+    }
   }
   s = block_sum(s, red);
   if (threadIdx.x == 0) part[blockIdx.y * gridDim.x + blockIdx.x] = s;
