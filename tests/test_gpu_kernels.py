@@ -369,6 +369,28 @@ def test_conv_fwd_act_epilogues(dtype, act, tile):
     assert torch.equal(y3, y2)
 
 
+@pytest.mark.parametrize("dt_in", [torch.float32, torch.bfloat16, None])
+@pytest.mark.parametrize("dt_out", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rows,cols,lds,ldd", [(16384, 512, 1024, 1024), (300, 128, 128, 136), (7, 13, 13, 20),
+                                               (1, 4096, 4096, 4096)])
+def test_convert_2d_paths(dt_in, dt_out, rows, cols, lds, ldd):
+    """vqx_convert_2d (strided copy with dtype conversion; src None = zero
+    fill) on the 8-element chunk path (cols and both leading dimensions
+    multiples of 8) and the element path; the destination's padding columns
+    are untouched."""
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(rows + cols)
+    src = None if dt_in is None else torch.randn(rows, lds, generator=g).to(DEV, dt_in)[:, :cols]
+    dst_full = torch.full((rows, ldd), 3.0, device=DEV, dtype=dt_out)
+    dst = dst_full[:, :cols]
+    ops.convert_2d(src, dst)
+    torch.cuda.synchronize()
+    want = torch.zeros(rows, cols, device=DEV, dtype=dt_out) if src is None else src.to(dt_out)
+    assert torch.equal(dst, want)
+    if ldd > cols:
+        assert (dst_full[:, cols:] == 3.0).all()
+
+
 @pytest.mark.parametrize("dt_out", [torch.float32, torch.bfloat16])
 def test_scale_act_2d(dt_out):
     ops = _ops()

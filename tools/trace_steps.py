@@ -3,6 +3,7 @@ steps are the windows between consecutive adam_kernel / adam_wn_kernel launches;
 fp32 GEMMs (the bench's fp32 leg) or more than one step's launches are skipped.
 python tools/trace_steps.py TRACE_CSV [TOP]"""
 import csv
+import re
 import sys
 from collections import defaultdict
 
@@ -12,7 +13,7 @@ ad = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith(("vqx::adam_k
 wins = []
 for a, b in zip(ad[:-1], ad[1:]):
     seg = rows[a:b]
-    if any("<float" in r["Kernel_Name"] for r in seg):
+    if any(re.search(r"(conv|dual|wgrad)\w*<float", r["Kernel_Name"]) for r in seg):  # fp32 GEMMs
         continue
     wins.append(seg)
 n = {len(w) for w in wins}

@@ -2272,6 +2272,61 @@ __global__ __launch_bounds__(256) void convert_2d_kernel(const void* __restrict_
   }
 }
 
+// convert_2d / scale_act_2d on 8-element chunks (cols, both leading
+// dimensions multiples of 8, 16-B aligned rows): 16-B bf16 / 2 x 16-B f32
+// accesses, four chunks' loads in flight per thread, 32-bit chunk indexing
+// (the element kernels above divide 64-bit indices and move 2-4 B a lane).
+template <typename S> struct Chunk8;
+template <> struct Chunk8<float> {
+  __device__ static __forceinline__ void ld(const float* p, float* f) {
+    const f32x4_t a = *(const f32x4_t*)p, b = *(const f32x4_t*)(p + 4);
+    f[0] = a[0]; f[1] = a[1]; f[2] = a[2]; f[3] = a[3]; f[4] = b[0]; f[5] = b[1]; f[6] = b[2]; f[7] = b[3];
+  }
+  __device__ static __forceinline__ void st(float* p, const float* f) {
+    *(f32x4_t*)p = f32x4_t{f[0], f[1], f[2], f[3]};
+    *(f32x4_t*)(p + 4) = f32x4_t{f[4], f[5], f[6], f[7]};
+  }
+};
+template <> struct Chunk8<bf16_t> {
+  __device__ static __forceinline__ void ld(const bf16_t* p, float* f) { Vec<bf16_t>::load(p, f); }
+  __device__ static __forceinline__ void st(bf16_t* p, const float* f) { Vec<bf16_t>::store(p, f); }
+};
+template <typename S, typename D, bool ZERO>
+__global__ __launch_bounds__(256) void map8_kernel(const S* __restrict__ src, int lds, D* __restrict__ dst, int ldd,
+                                                   int n8, int cpr, float scale, int act) {
+  constexpr int U = 4;
+  const int stride = gridDim.x * 256;
+  for (int q0 = blockIdx.x * 256 + threadIdx.x; q0 < n8; q0 += U * stride) {
+    float v[U][8];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = min(q0 + u * stride, n8 - 1), r = q / cpr, c = (q - r * cpr) * 8;
+      if constexpr (ZERO) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[u][k] = 0.f;
+      } else {
+        Chunk8<S>::ld(src + (int64_t)r * lds + c, v[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = q0 + u * stride;
+      if (q >= n8) break;
+      const int r = q / cpr, c = (q - r * cpr) * 8;
+      if (!ZERO) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float x = scale * v[u][k];
+          if (act == VQX_PRO_RELU) x = x > 0.f ? x : 0.f;
+          else if (act == VQX_PRO_LRELU) x = x > 0.f ? x : 0.2f * x;
+          v[u][k] = x;
+        }
+      }
+      Chunk8<D>::st(dst + (int64_t)r * ldd + c, v[u]);
+    }
+  }
+}
+
 }  // namespace vqx
 
 using namespace vqx;
@@ -2762,10 +2817,36 @@ extern "C" int vqx_radam_step(float* p, const float* g, float* m, float* v, int6
   return launch_status("vqx_radam_step");
 }
 
+// the 8-element chunk path when the shapes allow it (see map8_kernel); false: not taken
+static bool map8_launch(const void* src, int32_t lds, int32_t sdt, void* dst, int32_t ldd, int32_t ddt, int64_t rows,
+                        int32_t cols, float scale, int32_t act, hipStream_t s) {
+  if (cols % 8 || ldd % 8 || (src && lds % 8) || rows * cols / 8 >= (int64_t)1 << 31 ||
+      ((uintptr_t)dst & 15) || ((uintptr_t)src & 15))
+    return false;
+  const int n8 = (int)(rows * cols / 8), cpr = cols / 8;
+  const int grid = grid_for(n8, 256, 2048);
+  const bool sb = sdt == VQX_BF16, db = ddt == VQX_BF16;
+  if (!src) {
+    if (db) hipLaunchKernelGGL((map8_kernel<float, bf16_t, true>), dim3(grid), dim3(256), 0, s, nullptr, 0, (bf16_t*)dst, ldd, n8, cpr, 1.f, 0);
+    else hipLaunchKernelGGL((map8_kernel<float, float, true>), dim3(grid), dim3(256), 0, s, nullptr, 0, (float*)dst, ldd, n8, cpr, 1.f, 0);
+  } else if (sb && db) {
+    hipLaunchKernelGGL((map8_kernel<bf16_t, bf16_t, false>), dim3(grid), dim3(256), 0, s, (const bf16_t*)src, lds, (bf16_t*)dst, ldd, n8, cpr, scale, act);
+  } else if (sb) {
+    hipLaunchKernelGGL((map8_kernel<bf16_t, float, false>), dim3(grid), dim3(256), 0, s, (const bf16_t*)src, lds, (float*)dst, ldd, n8, cpr, scale, act);
+  } else if (db) {
+    hipLaunchKernelGGL((map8_kernel<float, bf16_t, false>), dim3(grid), dim3(256), 0, s, (const float*)src, lds, (bf16_t*)dst, ldd, n8, cpr, scale, act);
+  } else {
+    hipLaunchKernelGGL((map8_kernel<float, float, false>), dim3(grid), dim3(256), 0, s, (const float*)src, lds, (float*)dst, ldd, n8, cpr, scale, act);
+  }
+  return true;
+}
+
 extern "C" int vqx_convert_2d(const void* src, int32_t ld_src, int32_t src_dtype, void* dst, int32_t ld_dst,
                               int32_t dst_dtype, int64_t rows, int32_t cols, vqx_stream_t stream) {
   if (rows <= 0 || cols <= 0) return 0;
   if (!dst) { set_error("vqx_convert_2d: null dst"); return -1; }
+  if (map8_launch(src, ld_src, src_dtype, dst, ld_dst, dst_dtype, rows, cols, 1.f, VQX_PRO_NONE, (hipStream_t)stream))
+    return launch_status("vqx_convert_2d");
   hipLaunchKernelGGL(convert_2d_kernel, dim3(grid_for(rows * cols, 256, 8192)), dim3(256), 0, (hipStream_t)stream,
                      src, ld_src, src_dtype, dst, ld_dst, dst_dtype, rows, cols);
   return launch_status("vqx_convert_2d");
@@ -2776,6 +2857,8 @@ extern "C" int vqx_scale_act_2d(const void* src, int32_t ld_src, int32_t src_dty
                                 vqx_stream_t stream) {
   if (rows <= 0 || cols <= 0) return 0;
   if (!dst || !src) { set_error("vqx_scale_act_2d: null pointer"); return -1; }
+  if (map8_launch(src, ld_src, src_dtype, dst, ld_dst, dst_dtype, rows, cols, scale, act, (hipStream_t)stream))
+    return launch_status("vqx_scale_act_2d");
   hipLaunchKernelGGL(scale_act_2d_kernel, dim3(grid_for(rows * cols, 256, 8192)), dim3(256), 0, (hipStream_t)stream,
                      src, ld_src, src_dtype, dst, ld_dst, dst_dtype, rows, cols, scale, act);
   return launch_status("vqx_scale_act_2d");

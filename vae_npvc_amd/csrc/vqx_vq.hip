@@ -496,16 +496,34 @@ __global__ __launch_bounds__(256) void vq_ema_elem_kernel(float* __restrict__ em
                                                           float one_minus_mu, float thr, float* __restrict__ part) {
   __shared__ float red[16];
   const int i0 = blockIdx.x * kEmaElems;
+  const int n = K * D;
   float dsq = 0.f;
-  for (int i = i0 + threadIdx.x; i < min(K * D, i0 + kEmaElems); i += blockDim.x) {
-    const int k = i / D;
-    const float s = __fadd_rn(__fmul_rn(mu, emb_sum[i]), __fmul_rn(one_minus_mu, bsum[i]));
-    const float el = __fadd_rn(__fmul_rn(mu, emb_elem[k]), __fmul_rn(one_minus_mu, bcnt[k]));
+  // the thread's elements' loads all issued first (clamped indices), then the
+  // math in element order: a load-use loop paid one memory latency per element
+  constexpr int U = kEmaElems / 256;
+  static_assert(U * 256 == kEmaElems, "elements per thread");
+  float es[U], bs[U], ee[U], bc[U], rr[U], eo[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = min(i0 + (int)threadIdx.x + 256 * u, n - 1), k = i / D;
+    es[u] = emb_sum[i];
+    bs[u] = bsum[i];
+    ee[u] = emb_elem[k];
+    bc[u] = bcnt[k];
+    rr[u] = rand_rows[i];
+    eo[u] = E[i];
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = i0 + (int)threadIdx.x + 256 * u;
+    if (i >= n) break;
+    const float s = __fadd_rn(__fmul_rn(mu, es[u]), __fmul_rn(one_minus_mu, bs[u]));
+    const float el = __fadd_rn(__fmul_rn(mu, ee[u]), __fmul_rn(one_minus_mu, bc[u]));
     emb_sum[i] = s;
-    const float u = (el >= thr) ? 1.f : 0.f;
+    const float uu = (el >= thr) ? 1.f : 0.f;
     // usage*(sum/elem) + (1-usage)*rand, evaluated like the reference
-    const float newe = __fadd_rn(__fmul_rn(u, __fdiv_rn(s, el)), __fmul_rn(1.f - u, rand_rows[i]));
-    const float diff = __fsub_rn(newe, E[i]);
+    const float newe = __fadd_rn(__fmul_rn(uu, __fdiv_rn(s, el)), __fmul_rn(1.f - uu, rr[u]));
+    const float diff = __fsub_rn(newe, eo[u]);
     dsq = fmaf(diff, diff, dsq);
     E[i] = newe;
   }
