@@ -429,6 +429,12 @@ int vqx_embedding_fwd(const float* weight, const int64_t* ids, int32_t B, int32_
                       vqx_stream_t stream);
 int vqx_embedding_bwd(const float* dout, const int64_t* ids, int32_t B, int32_t D, float* dweight,
                       vqx_stream_t stream);
+/* The dense weight gradient in one pass (ABI 126): every row r < n_rows of
+ * dweight is written, dweight[r] (+)= sum over b with ids[b] == r of dout[b]
+ * in batch order (0 for ids absent from the batch; accumulate = 1 adds).  No
+ * zero-fill launch before it.  B <= 1024. */
+int vqx_embedding_bwd_rows(const float* dout, const int64_t* ids, int32_t B, int32_t D, int32_t n_rows,
+                           float* dweight, int32_t accumulate, vqx_stream_t stream);
 
 /* Small dense GEMM for the time-constant conv_cond term (vqvae.py:309-312):
  * out[b][o] = sum_i W[o][i] * c[b][i] + bias[o]   (f32, W from weight norm

@@ -1063,6 +1063,28 @@ def test_colsum_matches_fp64_and_accumulates(dtype, n, C, ld):
     torch.testing.assert_close(out.double(), 2 * ref, rtol=1e-5, atol=2 * tol)
 
 
+@pytest.mark.parametrize("B,n_rows", [(64, 100), (64, 3), (5, 40)])
+def test_embedding_bwd_rows(B, n_rows):
+    """vqx_embedding_bwd_rows (ABI 126): every row of the dense gradient
+    written (ids absent from the batch give 0, no zero fill before it), equal
+    to zero fill + vqx_embedding_bwd bit for bit (batch-order sums), and
+    accumulate = 1 adds."""
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(B + n_rows)
+    D = 128
+    dout = torch.randn(B, D, generator=g).to(DEV)
+    ids = torch.randint(0, n_rows, (B,), generator=g).to(DEV)
+    ref = torch.zeros(n_rows, D, device=DEV)
+    ops.embedding_bwd(dout, ids, ref)
+    got = torch.full((n_rows, D), float("nan"), device=DEV)
+    ops.embedding_bwd_rows(dout, ids, got)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    ops.embedding_bwd_rows(dout, ids, got, accumulate=True)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref + ref)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("B,C,T,ldx", [(64, 80, 256, 80), (3, 80, 100, 128), (2, 7, 33, 7), (1, 80, 1, 80)])
 def test_logloss_matches_torch(dtype, B, C, T, ldx):

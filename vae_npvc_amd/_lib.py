@@ -117,6 +117,7 @@ _SIGS = {
     "vqx_time_gather": [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_int32, c_void_p],
     "vqx_embedding_fwd": [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p],
     "vqx_embedding_bwd": [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p],
+    "vqx_embedding_bwd_rows": [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_int32, c_void_p],
     "vqx_linear_f32": [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p],
     "vqx_linear_bwd_f32": [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p],
     "vqx_grad_sq_norm": [c_void_p, c_int64, c_void_p, c_void_p, c_void_p],

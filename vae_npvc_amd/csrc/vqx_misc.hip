@@ -1443,6 +1443,26 @@ __global__ void embedding_bwd_kernel(const float* __restrict__ dout, const int64
   }
 }
 
+// vqx_embedding_bwd_rows: block r = embedding row r; the batch's ids staged in
+// LDS, every thread scans them in batch order and adds the matching rows of
+// dout (one or two per id in a batch: a short load chain, not B serial loads)
+constexpr int kEmbMaxB = 1024;
+__global__ __launch_bounds__(256) void embedding_bwd_rows_kernel(const float* __restrict__ dout,
+                                                                 const int64_t* __restrict__ ids, int B, int D,
+                                                                 float* __restrict__ dw, int accumulate) {
+  __shared__ int sid[kEmbMaxB];
+  const int r = blockIdx.x;
+  for (int q = threadIdx.x; q < B; q += blockDim.x) sid[q] = (int)ids[q];
+  __syncthreads();
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float s = 0.f;
+    for (int q = 0; q < B; ++q)
+      if (sid[q] == r) s += dout[(int64_t)q * D + d];
+    float* o = dw + (int64_t)r * D + d;
+    *o = accumulate ? *o + s : s;
+  }
+}
+
 __global__ void linear_fwd_kernel(const float* __restrict__ c, const float* __restrict__ W, const float* __restrict__ bias,
                                   int B, int I, int O, float* __restrict__ out) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2716,6 +2736,17 @@ extern "C" int vqx_embedding_bwd(const float* dout, const int64_t* ids, int32_t 
                                  vqx_stream_t stream) {
   hipLaunchKernelGGL(embedding_bwd_kernel, dim3(B), dim3(128), 0, (hipStream_t)stream, dout, ids, B, D, dweight);
   return launch_status("vqx_embedding_bwd");
+}
+
+extern "C" int vqx_embedding_bwd_rows(const float* dout, const int64_t* ids, int32_t B, int32_t D, int32_t n_rows,
+                                      float* dweight, int32_t accumulate, vqx_stream_t stream) {
+  if (!dout || !ids || !dweight || B < 1 || B > kEmbMaxB || D < 1 || n_rows < 1) {
+    set_error("vqx_embedding_bwd_rows: bad arguments (1 <= B <= %d)", kEmbMaxB);
+    return -1;
+  }
+  hipLaunchKernelGGL(embedding_bwd_rows_kernel, dim3(n_rows), dim3(D >= 256 ? 256 : ((D + 63) / 64) * 64), 0,
+                     (hipStream_t)stream, dout, ids, B, D, dweight, accumulate);
+  return launch_status("vqx_embedding_bwd_rows");
 }
 
 extern "C" int vqx_linear_f32(const float* c, const float* W, const float* bias, int32_t B, int32_t I, int32_t O,

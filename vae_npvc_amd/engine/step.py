@@ -1326,10 +1326,11 @@ class VQVAEEngine:
                 self._wn_bwd(w, ("dec_stage", 0))
         # speaker conditioning of all blocks: dW, bias and d(embedding), per output width
         emb_g = self.g(self.m.embeds._embedding.weight)
-        ops.zero_(emb_g)
-        for O, blocks in self.cond_groups.items():
+        if not self.cond_groups:  # the embedding feeds nothing: its gradient is zero
+            ops.zero_(emb_g)
+        for gi, (O, blocks) in enumerate(self.cond_groups.items()):
             ops.linear_batched_bwd(w.cond_tables[O], w.yemb, B, blocks[0].cond.cin, O, w.dyemb, w.lin_part)
-            ops.embedding_bwd(w.dyemb, w.y_dev, emb_g)
+            ops.embedding_bwd_rows(w.dyemb, w.y_dev, emb_g, accumulate=gi > 0)  # every row written: no zero fill
         self._wn_bwd_cond(w)
 
     def _wn_bwd_cond(self, w):

@@ -547,6 +547,17 @@ def embedding_bwd(dout, ids, dweight):
     return dweight
 
 
+def embedding_bwd_rows(dout, ids, dweight, accumulate=False):
+    """Every row of dweight: (+)= the sum of dout's rows whose id is that row, in
+    batch order (0 where absent); no zero fill needed before it."""
+    _check_cuda(dout, ids, dweight)
+    if ids.dtype != torch.int64 or not (dout.is_contiguous() and dweight.is_contiguous()):
+        raise ValueError("embedding_bwd_rows: int64 ids, contiguous dout / dweight")
+    call("vqx_embedding_bwd_rows", ptr(dout), ptr(ids), ids.numel(), dweight.shape[1], dweight.shape[0], ptr(dweight),
+         int(accumulate), stream_ptr())
+    return dweight
+
+
 def linear_f32(c, W, bias, out):
     B, I = c.shape
     O = W.shape[0]
