@@ -1876,19 +1876,41 @@ __global__ __launch_bounds__(256) void sq_partial_sum_kernel(const float* __rest
                                                              float* __restrict__ scratch) {
   __shared__ float red[16];
   const int64_t stride = (int64_t)kSqBlocks * 256;
-  float s = 0.f;
-  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  for (; i + 3 * stride < np; i += 4 * stride) {  // four loads in flight
-    const float a = part[i], b = part[i + stride], c = part[i + 2 * stride], d = part[i + 3 * stride];
-    s += a;
-    s += b;
-    s += c;
-    s += d;
+  const int64_t j0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  // the first ranges' bounds load beside the partials (one latency, not one per range)
+  constexpr int kR = 8;
+  int64_t ro[kR], rl[kR];
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
+    const int rr = min(r, max(nr - 1, 0));
+    ro[r] = nr ? rng[2 * rr] : 0;
+    rl[r] = r < nr ? rng[2 * rr + 1] : 0;
   }
-  for (; i < np; i += stride) s += part[i];
-  for (int r = 0; r < nr; ++r) {
+  float s = 0.f;
+  // partials four at a time, clamped loads (no tail loop of single loads), added in index order
+  for (int64_t i = j0; i < np; i += 4 * stride) {
+    float t[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) t[u] = part[min(i + u * stride, np - 1)];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i + u * stride < np) s += t[u];
+  }
+  // each range's first element of this thread loaded together, then the ranges in order
+  float gv[kR];
+  if (nr > 0) {  // (g may be null without ranges)
+#pragma unroll
+    for (int r = 0; r < kR; ++r) gv[r] = g[ro[r] + min(j0, max(rl[r] - 1, (int64_t)0))];
+  }
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
+    if (r >= nr) break;
+    if (j0 < rl[r]) s = fmaf(gv[r], gv[r], s);
+    for (int64_t j = j0 + stride; j < rl[r]; j += stride) s = fmaf(g[ro[r] + j], g[ro[r] + j], s);
+  }
+  for (int r = kR; r < nr; ++r) {
     const int64_t off = rng[2 * r], len = rng[2 * r + 1];
-    for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < len; j += stride) s = fmaf(g[off + j], g[off + j], s);
+    for (int64_t j = j0; j < len; j += stride) s = fmaf(g[off + j], g[off + j], s);
   }
   s = block_sum(s, red);
   if (threadIdx.x == 0) scratch[blockIdx.x] = s;

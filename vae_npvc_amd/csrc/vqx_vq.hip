@@ -531,42 +531,55 @@ __global__ __launch_bounds__(256) void vq_ema_elem_kernel(float* __restrict__ em
   if (threadIdx.x == 0) part[blockIdx.x] = dsq;
 }
 
+// N block sums at once (one pair of barriers): each value's waves added in
+// wave order, as block_sum does
+template <int N>
+__device__ __forceinline__ void block_sum_n(float (&v)[N], float (*scratch)[16]) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] = wave_sum(v[k]);
+  __syncthreads();
+  if (l == 0) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) scratch[k][w] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    float t = 0.f;
+    for (int i = 0; i < nw; ++i) t += scratch[k][i];
+    v[k] = t;
+  }
+}
+
 __global__ __launch_bounds__(1024) void vq_ema_final_kernel(float* __restrict__ emb_elem,
                                                             const float* __restrict__ bcnt, int K, int D, float mu,
                                                             float one_minus_mu, float thr,
                                                             const float* __restrict__ part, int nparts,
                                                             float* __restrict__ diag) {
-  __shared__ float red[16];
-  float dsq = 0.f;
-  for (int b = threadIdx.x; b < nparts; b += blockDim.x) dsq += part[b];
-  dsq = block_sum(dsq, red);
-  __syncthreads();
-  float total = 0.f;
-  for (int k = threadIdx.x; k < K; k += blockDim.x) total += bcnt[k];
-  total = block_sum(total, red);
-  __syncthreads();
-  float ent = 0.f, used = 0.f, usage = 0.f;
+  __shared__ float red[3][16];
+  float a[2] = {0.f, 0.f};  // sum of squared codebook moves, total count
+  for (int b = threadIdx.x; b < nparts; b += blockDim.x) a[0] += part[b];
+  for (int k = threadIdx.x; k < K; k += blockDim.x) a[1] += bcnt[k];
+  block_sum_n<2>(a, red);
+  const float dsq = a[0], total = a[1];
+  float e[3] = {0.f, 0.f, 0.f};  // entropy term, codes used this step, codes in use after the update
   for (int k = threadIdx.x; k < K; k += blockDim.x) {
     const float c = bcnt[k];
     const float p = c / total;
-    ent += p * logf(p + 1e-8f);
-    used += (c >= thr) ? 1.f : 0.f;
+    e[0] += p * logf(p + 1e-8f);
+    e[1] += (c >= thr) ? 1.f : 0.f;
     const float el = __fadd_rn(__fmul_rn(mu, emb_elem[k]), __fmul_rn(one_minus_mu, c));
-    usage += (el >= thr) ? 1.f : 0.f;
+    e[2] += (el >= thr) ? 1.f : 0.f;
   }
-  __syncthreads();
-  ent = block_sum(ent, red);
-  __syncthreads();
-  used = block_sum(used, red);
-  __syncthreads();
-  usage = block_sum(usage, red);
-  __syncthreads();
+  __syncthreads();  // red is rewritten
+  block_sum_n<3>(e, red);
   for (int k = threadIdx.x; k < K; k += blockDim.x)
     emb_elem[k] = __fadd_rn(__fmul_rn(mu, emb_elem[k]), __fmul_rn(one_minus_mu, bcnt[k]));
   if (threadIdx.x == 0) {
-    diag[0] = expf(-ent);
-    diag[1] = used;
-    diag[2] = usage;
+    diag[0] = expf(-e[0]);
+    diag[1] = e[1];
+    diag[2] = e[2];
     diag[3] = sqrtf(dsq) / sqrtf((float)K * (float)D);
   }
 }
