@@ -459,6 +459,14 @@ int vqx_linear_batched_fwd(const vqx_linear_layer* table_dev, int32_t n, const f
                            int32_t I, int32_t O, vqx_stream_t stream);
 int vqx_linear_batched_bwd(const vqx_linear_layer* table_dev, int32_t n, const float* c, int32_t B,
                            int32_t I, int32_t O, float* dc, float* partials, vqx_stream_t stream);
+/* The same with c[b] = emb[ids[b]] (ABI 126): the embedding lookup
+ * (vqx_embedding_fwd) folded into the operand loads, for I = 128, B <= 64,
+ * O % 64 == 0 and a 16-B aligned table (anything else: an error). */
+int vqx_linear_batched_fwd_ids(const vqx_linear_layer* table_dev, int32_t n, const float* emb,
+                               const int64_t* ids, int32_t B, int32_t I, int32_t O, vqx_stream_t stream);
+int vqx_linear_batched_bwd_ids(const vqx_linear_layer* table_dev, int32_t n, const float* emb,
+                               const int64_t* ids, int32_t B, int32_t I, int32_t O, float* dc, float* partials,
+                               vqx_stream_t stream);
 
 int vqx_linear_f32(const float* c, const float* W, const float* bias, int32_t B, int32_t I,
                    int32_t O, float* out, vqx_stream_t stream);

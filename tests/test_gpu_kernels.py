@@ -1113,6 +1113,43 @@ def test_logloss_matches_torch(dtype, B, C, T, ldx):
         assert (dx_full[:, C:] == 7.0).all()  # padding columns untouched
 
 
+@pytest.mark.parametrize("B", [64, 13])
+def test_linear_cond_ids_equal_lookup_then_linear(B):
+    """vqx_linear_batched_fwd_ids / _bwd_ids (ABI 126: rows of the embedding
+    table read in the operand loads) = vqx_embedding_fwd + the plain batched
+    calls, bit for bit (the same kernels on the same rows)."""
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(40 + B)
+    n, I, O, n_spk = 10, 128, 1024, 100
+    emb = torch.randn(n_spk, I, generator=g).to(DEV)
+    ids = torch.randint(0, n_spk, (B,), generator=g).to(DEV)
+    runs = []
+    for use_ids in (False, True):
+        gg = torch.Generator(device="cpu").manual_seed(3)
+        lay = [dict(W=(torch.randn(O, I, generator=gg) / I ** 0.5).to(DEV), bias=torch.randn(O, generator=gg).to(DEV),
+                    out=torch.empty(B, O, device=DEV), dout=torch.randn(B, O, generator=gg).to(DEV),
+                    dW=torch.empty(O, I, device=DEV), dbias=torch.empty(O, device=DEV)) for _ in range(n)]
+        tab = ops.linear_table(lay)
+        dc = torch.empty(B, I, device=DEV)
+        part = torch.empty(n * (O // 64) * B * I, device=DEV)
+        if use_ids:
+            assert ops.linear_ids_ok(B, I, O, emb)
+            ops.linear_batched_fwd_ids(tab, emb, ids, B, I, O)
+            ops.linear_batched_bwd_ids(tab, emb, ids, B, I, O, dc, part)
+        else:
+            c = torch.empty(B, I, device=DEV)
+            ops.embedding_fwd(emb, ids, c)
+            ops.linear_batched_fwd(tab, c, B, I, O)
+            ops.linear_batched_bwd(tab, c, B, I, O, dc, part)
+        torch.cuda.synchronize()
+        runs.append((lay, dc))
+    (la, dca), (lb, dcb) = runs
+    for a, b in zip(la, lb):
+        for k in ("out", "dW", "dbias"):
+            assert torch.equal(a[k], b[k]), k
+    assert torch.equal(dca, dcb)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("n,C,ld", [(16384, 80, 80), (16384, 128, 128), (777, 128, 192), (65, 8, 8), (5, 80, 80)])
 def test_colsum_partials_sum_to_colsum(dtype, n, C, ld):

@@ -124,6 +124,9 @@ _SIGS = {
     "vqx_adam_hyper": [c_void_p, c_double, c_double, c_int32, c_double, c_double, c_double, c_void_p, c_void_p],
     "vqx_linear_batched_fwd": [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p],
     "vqx_linear_batched_bwd": [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p],
+    "vqx_linear_batched_fwd_ids": [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p],
+    "vqx_linear_batched_bwd_ids": [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p,
+                                   c_void_p, c_void_p],
     "vqx_wgrad_tiles": [c_int64, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
                         ctypes.POINTER(c_int32)],
     "vqx_vq_normalize": [c_void_p, c_int64, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,

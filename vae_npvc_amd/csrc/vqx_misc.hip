@@ -1673,8 +1673,11 @@ __global__ __launch_bounds__(256) void linear_batched_bwd_x_kernel(const vqx_lin
 constexpr int kCondI = 128, kCondB = 64, kCondO = 64;
 
 // out_l[b][o] = bias_l[o] + sum_i c[b][i] W_l[o][i]; grid (O/64, n)
+// ids != null: row b of c is row ids[b] of c (the embedding table: the lookup
+// folded into the operand loads, vqx_linear_batched_fwd_ids)
 __global__ __launch_bounds__(256) void linear_cond_fwd_kernel(const vqx_linear_layer* __restrict__ L,
-                                                              const float* __restrict__ c, int B, int O) {
+                                                              const float* __restrict__ c,
+                                                              const int64_t* __restrict__ ids, int B, int O) {
   const vqx_linear_layer& l = L[blockIdx.y];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int q = lane >> 4, j = lane & 15;
@@ -1687,7 +1690,8 @@ __global__ __launch_bounds__(256) void linear_cond_fwd_kernel(const vqx_linear_l
   const float bj = l.bias ? l.bias[o0 + j] : 0.f;
   for (int rt = 0; rt * 16 < B; ++rt) {
     // A operand (m = j, k = 32q + s): c[row][32q .. 32q + 31]; rows >= B read row B-1, not stored
-    const float* cr = c + (int64_t)min(rt * 16 + j, B - 1) * kCondI + 32 * q;
+    const int row = min(rt * 16 + j, B - 1);
+    const float* cr = c + (ids ? ids[row] : (int64_t)row) * kCondI + 32 * q;
     f32x4_t ca[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) ca[u] = *(const f32x4_t*)(cr + 4 * u);
@@ -1710,7 +1714,8 @@ __global__ __launch_bounds__(256) void linear_cond_fwd_kernel(const vqx_linear_l
 
 // dW_l[o][i] = sum_b dout_l[b][o] c[b][i], dbias_l[o] = sum_b dout_l[b][o]; grid (O/64, n)
 __global__ __launch_bounds__(256) void linear_cond_bwd_w_kernel(const vqx_linear_layer* __restrict__ L,
-                                                                const float* __restrict__ c, int B, int O) {
+                                                                const float* __restrict__ c,
+                                                                const int64_t* __restrict__ ids, int B, int O) {
   const vqx_linear_layer& l = L[blockIdx.y];
   __shared__ float cs[kCondB][kCondI];  // c, rows >= B zero
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1728,7 +1733,8 @@ __global__ __launch_bounds__(256) void linear_cond_bwd_w_kernel(const vqx_linear
 #pragma unroll
   for (int u = 0; u < NC; ++u) {
     const int e = threadIdx.x + 256 * u, r = e / (kCondI / 4), i4 = e % (kCondI / 4);
-    cv[u] = *(const f32x4_t*)(c + (int64_t)min(r, B - 1) * kCondI + 4 * i4);
+    const int row = min(r, B - 1);
+    cv[u] = *(const f32x4_t*)(c + (ids ? ids[row] : (int64_t)row) * kCondI + 4 * i4);
   }
 #pragma unroll
   for (int u = 0; u < NC; ++u) {
@@ -2921,8 +2927,8 @@ extern "C" int vqx_linear_batched_fwd(const vqx_linear_layer* table_dev, int32_t
                                       int32_t I, int32_t O, vqx_stream_t stream) {
   if (!table_dev || n < 1 || !c || B < 1 || I < 1 || O < 1) { set_error("vqx_linear_batched_fwd: bad arguments"); return -1; }
   if (I == kCondI && O % kCondO == 0 && ((uintptr_t)c & 15) == 0)  // any B: 16-row tiles in turn
-    hipLaunchKernelGGL(linear_cond_fwd_kernel, dim3(O / kCondO, n), dim3(256), 0, (hipStream_t)stream, table_dev, c, B,
-                       O);
+    hipLaunchKernelGGL(linear_cond_fwd_kernel, dim3(O / kCondO, n), dim3(256), 0, (hipStream_t)stream, table_dev, c,
+                       (const int64_t*)nullptr, B, O);
   else
     hipLaunchKernelGGL(linear_batched_fwd_kernel, dim3((O + kLT - 1) / kLT, n, (B + kLT - 1) / kLT), dim3(256), 0,
                        (hipStream_t)stream, table_dev, c, B, I, O);
@@ -2936,7 +2942,8 @@ extern "C" int vqx_linear_batched_bwd(const vqx_linear_layer* table_dev, int32_t
   hipStream_t s = (hipStream_t)stream;
   const int nO = (O + kLT - 1) / kLT;
   if (I == kCondI && B <= kCondB && O % kCondO == 0 && ((uintptr_t)c & 15) == 0)
-    hipLaunchKernelGGL(linear_cond_bwd_w_kernel, dim3(O / kCondO, n), dim3(256), 0, s, table_dev, c, B, O);
+    hipLaunchKernelGGL(linear_cond_bwd_w_kernel, dim3(O / kCondO, n), dim3(256), 0, s, table_dev, c,
+                       (const int64_t*)nullptr, B, O);
   else
     hipLaunchKernelGGL(linear_batched_bwd_w_kernel, dim3(nO, n, (I + kLT - 1) / kLT), dim3(256), 0, s,
                        table_dev, c, B, I, O);
@@ -2952,6 +2959,39 @@ extern "C" int vqx_linear_batched_bwd(const vqx_linear_layer* table_dev, int32_t
                        dc);
   }
   return launch_status("vqx_linear_batched_bwd");
+}
+
+static bool linear_ids_ok(const vqx_linear_layer* t, int n, const float* emb, const int64_t* ids, int B, int I, int O,
+                          const char* who) {
+  if (!t || n < 1 || !emb || !ids || B < 1 || B > kCondB || I != kCondI || O % kCondO || ((uintptr_t)emb & 15)) {
+    set_error("%s: needs I = %d, 1 <= B <= %d, O %% %d == 0 and a 16-B aligned table", who, kCondI, kCondB, kCondO);
+    return false;
+  }
+  return true;
+}
+
+extern "C" int vqx_linear_batched_fwd_ids(const vqx_linear_layer* table_dev, int32_t n, const float* emb,
+                                          const int64_t* ids, int32_t B, int32_t I, int32_t O, vqx_stream_t stream) {
+  if (!linear_ids_ok(table_dev, n, emb, ids, B, I, O, "vqx_linear_batched_fwd_ids")) return -1;
+  hipLaunchKernelGGL(linear_cond_fwd_kernel, dim3(O / kCondO, n), dim3(256), 0, (hipStream_t)stream, table_dev, emb, ids,
+                     B, O);
+  return launch_status("vqx_linear_batched_fwd_ids");
+}
+
+extern "C" int vqx_linear_batched_bwd_ids(const vqx_linear_layer* table_dev, int32_t n, const float* emb,
+                                          const int64_t* ids, int32_t B, int32_t I, int32_t O, float* dc,
+                                          float* partials, vqx_stream_t stream) {
+  if (!linear_ids_ok(table_dev, n, emb, ids, B, I, O, "vqx_linear_batched_bwd_ids")) return -1;
+  if (dc && !partials) { set_error("vqx_linear_batched_bwd_ids: dc needs partials [n*O/64][B][I]"); return -1; }
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(linear_cond_bwd_w_kernel, dim3(O / kCondO, n), dim3(256), 0, s, table_dev, emb, ids, B, O);
+  if (dc) {
+    hipLaunchKernelGGL(linear_cond_bwd_x_kernel, dim3(O / kCondO, n), dim3(256), 0, s, table_dev, B, O, partials);
+    const int64_t ne = (int64_t)B * I;
+    hipLaunchKernelGGL(sum_slices_wide_kernel, dim3((unsigned)((ne + 63) / 64)), dim3(256), 0, s, partials,
+                       n * (O / kCondO), ne, dc);
+  }
+  return launch_status("vqx_linear_batched_bwd_ids");
 }
 
 extern "C" int vqx_gn_finalize_tiles(const float* parts, int64_t n_rows, int32_t T, int32_t C, int32_t G, float eps,

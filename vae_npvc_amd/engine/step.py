@@ -913,8 +913,22 @@ class VQVAEEngine:
         side.wait_stream(torch.cuda.current_stream())
         return side
 
+    def _cond_ids(self, w, ids):
+        """The conditioning linears read their input rows straight from the
+        embedding table (linear_batched_*_ids: no lookup launch) for this batch."""
+        emb = self.m.embeds._embedding.weight
+        return (getattr(w, "cond_tables", None) is not None and bool(self.cond_groups) and ids.dtype == torch.int64
+                and all(ops.linear_ids_ok(w.B, blocks[0].cond.cin, O, emb) for O, blocks in self.cond_groups.items()))
+
     def embed_and_cond(self, w, y):
-        ops.embedding_fwd(self.m.embeds._embedding.weight, y.reshape(-1), w.yemb)
+        ids = y.reshape(-1)
+        emb = self.m.embeds._embedding.weight
+        w.cond_ids_mode = self._cond_ids(w, ids)
+        if w.cond_ids_mode:
+            for O, blocks in self.cond_groups.items():
+                ops.linear_batched_fwd_ids(w.cond_tables[O], emb, ids, w.B, blocks[0].cond.cin, O)
+            return
+        ops.embedding_fwd(emb, ids, w.yemb)
         tabs = getattr(w, "cond_tables", None)
         for O, blocks in self.cond_groups.items():
             if tabs is not None:
@@ -1329,7 +1343,11 @@ class VQVAEEngine:
         if not self.cond_groups:  # the embedding feeds nothing: its gradient is zero
             ops.zero_(emb_g)
         for gi, (O, blocks) in enumerate(self.cond_groups.items()):
-            ops.linear_batched_bwd(w.cond_tables[O], w.yemb, B, blocks[0].cond.cin, O, w.dyemb, w.lin_part)
+            if getattr(w, "cond_ids_mode", False):
+                ops.linear_batched_bwd_ids(w.cond_tables[O], self.m.embeds._embedding.weight, w.y_dev, B,
+                                           blocks[0].cond.cin, O, w.dyemb, w.lin_part)
+            else:
+                ops.linear_batched_bwd(w.cond_tables[O], w.yemb, B, blocks[0].cond.cin, O, w.dyemb, w.lin_part)
             ops.embedding_bwd_rows(w.dyemb, w.y_dev, emb_g, accumulate=gi > 0)  # every row written: no zero fill
         self._wn_bwd_cond(w)
 

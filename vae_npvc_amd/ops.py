@@ -309,6 +309,29 @@ def linear_batched_fwd(table, c, B, I, O):
     call("vqx_linear_batched_fwd", dev.data_ptr(), len(arr), ptr(c), B, I, O, stream_ptr())
 
 
+def linear_ids_ok(B, I, O, emb):
+    """Whether linear_batched_*_ids take this shape (vqx.h: I = 128, B <= 64, O % 64 == 0, aligned table)."""
+    return I == 128 and 1 <= B <= 64 and O % 64 == 0 and emb.data_ptr() % 16 == 0
+
+
+def linear_batched_fwd_ids(table, emb, ids, B, I, O):
+    """linear_batched_fwd with c[b] = emb[ids[b]] (the embedding lookup in the operand loads)."""
+    arr, dev = table
+    _check_cuda(emb, ids)
+    if ids.dtype != torch.int64 or ids.numel() != B:
+        raise ValueError("linear_batched_fwd_ids: B int64 ids")
+    call("vqx_linear_batched_fwd_ids", dev.data_ptr(), len(arr), ptr(emb), ptr(ids), B, I, O, stream_ptr())
+
+
+def linear_batched_bwd_ids(table, emb, ids, B, I, O, dc, partials):
+    arr, dev = table
+    _check_cuda(emb, ids)
+    if ids.dtype != torch.int64 or ids.numel() != B:
+        raise ValueError("linear_batched_bwd_ids: B int64 ids")
+    call("vqx_linear_batched_bwd_ids", dev.data_ptr(), len(arr), ptr(emb), ptr(ids), B, I, O, ptr(dc), ptr(partials),
+         stream_ptr())
+
+
 def linear_batched_bwd(table, c, B, I, O, dc, partials=None):
     """partials: f32 workspace of >= len(table) * ceil(O/64) * B * I (allocated if None)."""
     arr, dev = table
