@@ -249,6 +249,12 @@ int vqx_weight_norm_bwd_sq(const vqx_wn_layer* layers_host, const vqx_wn_layer* 
                            int32_t n_layers, float* sq_partials, int64_t sq_capacity, vqx_stream_t stream);
 int vqx_sq_norm_finish(const float* partials, int64_t n_partials, const float* g, const int64_t* ranges,
                        int32_t n_ranges, float* scratch /* >= 256 floats */, float* out, vqx_stream_t stream);
+/* vqx_sq_norm_finish followed by vqx_adam_hyper (same arguments, same
+ * results) with the second folded into the finish's last launch (ABI 126). */
+int vqx_sq_norm_finish_adam(const float* partials, int64_t n_partials, const float* g, const int64_t* ranges,
+                            int32_t n_ranges, float* scratch, float* out, int64_t* step, double lr0, double gamma,
+                            int32_t step_size, double beta1, double beta2, double eps, float* hyper,
+                            vqx_stream_t stream);
 
 /*
  * GroupNorm statistics (nn.GroupNorm, layers.py:154 (G=1), layers.py:201

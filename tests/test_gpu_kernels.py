@@ -1113,6 +1113,35 @@ def test_logloss_matches_torch(dtype, B, C, T, ldx):
         assert (dx_full[:, C:] == 7.0).all()  # padding columns untouched
 
 
+def test_sq_norm_finish_adam_equals_finish_then_hyper():
+    """vqx_sq_norm_finish_adam (ABI 126) = vqx_sq_norm_finish + vqx_adam_hyper,
+    bit for bit: the norm, the per-step scalars (StepLR decay at step 4) and the
+    step counter, advanced once per call."""
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(12)
+    part = torch.randn(110_000, generator=g).abs().to(DEV)
+    flat = torch.randn(300_000, generator=g).to(DEV)
+    rng = torch.tensor([[1000, 5000], [200_000, 70_000]], dtype=torch.int64).to(DEV)
+    outs = []
+    for fused in (False, True):
+        step = torch.zeros(1, dtype=torch.int64, device=DEV)
+        hyper = torch.zeros(16, device=DEV)
+        out, scratch = torch.zeros(1, device=DEV), torch.zeros(256, device=DEV)
+        hist = []
+        for _ in range(5):
+            if fused:
+                ops.sq_norm_finish_adam(part, flat, rng, out, scratch, step, 2e-4, 0.5, 4, 0.9, 0.999, 1e-8, hyper)
+            else:
+                ops.sq_norm_finish(part, flat, rng, out, scratch)
+                ops.adam_hyper(step, 2e-4, 0.5, 4, 0.9, 0.999, 1e-8, hyper)
+            hist.append((out.clone(), hyper.clone(), step.clone()))
+        torch.cuda.synchronize()
+        outs.append(hist)
+    for (o1, h1, s1), (o2, h2, s2) in zip(*outs):
+        assert torch.equal(o1, o2) and torch.equal(h1, h2) and torch.equal(s1, s2)
+    assert int(outs[1][-1][2]) == 5
+
+
 @pytest.mark.parametrize("B", [64, 13])
 def test_linear_cond_ids_equal_lookup_then_linear(B):
     """vqx_linear_batched_fwd_ids / _bwd_ids (ABI 126: rows of the embedding

@@ -85,6 +85,8 @@ _SIGS = {
     "vqx_weight_norm_bwd_partials": [c_void_p, c_int32, c_void_p],
     "vqx_weight_norm_bwd_sq": [c_void_p, c_void_p, c_int32, c_void_p, c_int64, c_void_p],
     "vqx_sq_norm_finish": [c_void_p, c_int64, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p],
+    "vqx_sq_norm_finish_adam": [c_void_p, c_int64, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p,
+                                c_double, c_double, c_int32, c_double, c_double, c_double, c_void_p, c_void_p],
     "vqx_groupnorm_stats": [c_void_p, c_int32, c_int32, c_int64, c_int32, c_int32, c_int32, c_float, c_void_p,
                             c_void_p, c_void_p],
     "vqx_gn_lrelu_fwd": [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int64, c_int32, c_int32, c_void_p,

@@ -1921,14 +1921,10 @@ __global__ __launch_bounds__(256) void sq_partial_sum_kernel(const float* __rest
   s = block_sum(s, red);
   if (threadIdx.x == 0) scratch[blockIdx.x] = s;
 }
-__global__ __launch_bounds__(kSqBlocks) void sq_final_kernel(const float* __restrict__ scratch, float* __restrict__ out) {
-  __shared__ float red[16];
-  const float s = block_sum(scratch[threadIdx.x], red);
-  if (threadIdx.x == 0) out[0] = s;
-}
-
-__global__ void adam_hyper_kernel(int64_t* __restrict__ step, double lr0, double gamma, int step_size, double b1,
-                                  double b2, double eps, float* __restrict__ hyper) {
+// Adam's per-step scalars (StepLR'd lr, bias corrections) from the device step
+// counter, which it advances; one thread
+__device__ __forceinline__ void adam_hyper_eval(int64_t* __restrict__ step, double lr0, double gamma, int step_size,
+                                                double b1, double b2, double eps, float* __restrict__ hyper) {
   const int64_t t = step[0] + 1;
   step[0] = t;
   const double lr = lr0 * pow(gamma, (double)((t - 1) / step_size));
@@ -1942,6 +1938,29 @@ __global__ void adam_hyper_kernel(int64_t* __restrict__ step, double lr0, double
   hyper[5] = (float)b2;
   hyper[6] = (float)(1.0 - b2);
   hyper[7] = (float)eps;
+}
+
+__global__ void adam_hyper_kernel(int64_t* __restrict__ step, double lr0, double gamma, int step_size, double b1,
+                                  double b2, double eps, float* __restrict__ hyper) {
+  adam_hyper_eval(step, lr0, gamma, step_size, b1, b2, eps, hyper);
+}
+
+// the second level of vqx_sq_norm_finish; with hyper != null (vqx_sq_norm_finish_adam)
+// thread 0 also evaluates Adam's per-step scalars: one launch fewer
+struct AdamHyperArgs {
+  int64_t* step;
+  double lr0, gamma, b1, b2, eps;
+  int step_size;
+  float* hyper;
+};
+__global__ __launch_bounds__(kSqBlocks) void sq_final_kernel(const float* __restrict__ scratch, float* __restrict__ out,
+                                                             AdamHyperArgs H) {
+  __shared__ float red[16];
+  const float s = block_sum(scratch[threadIdx.x], red);
+  if (threadIdx.x == 0) {
+    out[0] = s;
+    if (H.hyper) adam_hyper_eval(H.step, H.lr0, H.gamma, H.step_size, H.b1, H.b2, H.eps, H.hyper);
+  }
 }
 
 // RAdam (trainer/radam.py:15-78): rectification decided once per step on the
@@ -2508,8 +2527,25 @@ extern "C" int vqx_sq_norm_finish(const float* partials, int64_t n_partials, con
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(sq_partial_sum_kernel, dim3(kSqBlocks), dim3(256), 0, s, partials, n_partials, g, ranges, n_ranges,
                      scratch);
-  hipLaunchKernelGGL(sq_final_kernel, dim3(1), dim3(kSqBlocks), 0, s, scratch, out);
+  hipLaunchKernelGGL(sq_final_kernel, dim3(1), dim3(kSqBlocks), 0, s, scratch, out, AdamHyperArgs{});
   return launch_status("vqx_sq_norm_finish");
+}
+
+extern "C" int vqx_sq_norm_finish_adam(const float* partials, int64_t n_partials, const float* g,
+                                       const int64_t* ranges, int32_t n_ranges, float* scratch, float* out,
+                                       int64_t* step, double lr0, double gamma, int32_t step_size, double beta1,
+                                       double beta2, double eps, float* hyper, vqx_stream_t stream) {
+  if (n_partials < 0 || n_ranges < 0 || !out || !scratch || (n_partials && !partials) || (n_ranges && (!ranges || !g)) ||
+      !step || !hyper || step_size < 1) {
+    set_error("vqx_sq_norm_finish_adam: bad arguments");
+    return -1;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(sq_partial_sum_kernel, dim3(kSqBlocks), dim3(256), 0, s, partials, n_partials, g, ranges, n_ranges,
+                     scratch);
+  hipLaunchKernelGGL(sq_final_kernel, dim3(1), dim3(kSqBlocks), 0, s, scratch, out,
+                     AdamHyperArgs{step, lr0, gamma, beta1, beta2, eps, step_size, hyper});
+  return launch_status("vqx_sq_norm_finish_adam");
 }
 
 extern "C" int vqx_groupnorm_stats(const void* x, int32_t ldx, int32_t dtype, int64_t n_rows, int32_t T, int32_t C,

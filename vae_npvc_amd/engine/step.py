@@ -1548,8 +1548,14 @@ class VQVAEEngine:
 
     def optimizer_step(self):
         plan, self._sq_plan_ready = self._sq_plan_ready, None
+        hyper_done = False
         if self.max_grad_norm > 0:
-            if plan is not None:  # partials from this step's weight-norm backward
+            if plan is not None and self.opt_kind != "radam":  # + Adam's per-step scalars in the same launch
+                ops.sq_norm_finish_adam(plan[0], self.flat_g, plan[1], self.sumsq, self.norm_part, self.opt_step,
+                                        self.lr0, self.sched_gamma, self.sched_step, self.betas[0], self.betas[1],
+                                        self.eps, self.hyper)
+                hyper_done = True
+            elif plan is not None:  # partials from this step's weight-norm backward
                 ops.sq_norm_finish(plan[0], self.flat_g, plan[1], self.sumsq, self.norm_part)
             else:
                 ops.grad_sq_norm(self.flat_g, self.norm_part, self.sumsq)
@@ -1560,8 +1566,9 @@ class VQVAEEngine:
             ops.radam_step(self.flat_p, self.flat_g, self.exp_avg, self.exp_avg_sq, self.hyper, sumsq,
                            float(self.max_grad_norm))
             return
-        ops.adam_hyper(self.opt_step, self.lr0, self.sched_gamma, self.sched_step, self.betas[0], self.betas[1],
-                       self.eps, self.hyper)
+        if not hyper_done:
+            ops.adam_hyper(self.opt_step, self.lr0, self.sched_gamma, self.sched_step, self.betas[0], self.betas[1],
+                           self.eps, self.hyper)
         if not self._adam_wn_built:
             self._adam_wn = self._adam_wn_plan() if self.opt.fuse_adam_wn else None
             self._adam_wn_built = True

@@ -387,6 +387,21 @@ def sq_norm_finish(partials, g, ranges, out, scratch):
     return out
 
 
+def sq_norm_finish_adam(partials, g, ranges, out, scratch, step, lr0, gamma, step_size, beta1, beta2, eps, hyper):
+    """sq_norm_finish then adam_hyper, the second in the finish's last launch."""
+    _check_cuda(partials, g, out, scratch, step, hyper)
+    if scratch.numel() < 256:
+        raise ValueError("sq_norm_finish_adam: scratch needs 256 floats")
+    nr = 0 if ranges is None else ranges.shape[0]
+    if nr:
+        _check_cuda(ranges)
+        if ranges.dtype != torch.int64 or ranges.dim() != 2 or ranges.shape[1] != 2:
+            raise ValueError("sq_norm_finish_adam: ranges must be an int64 [n, 2] tensor")
+    call("vqx_sq_norm_finish_adam", ptr(partials), partials.numel(), ptr(g), ptr(ranges) if nr else None, nr,
+         ptr(scratch), ptr(out), ptr(step), lr0, gamma, step_size, beta1, beta2, eps, ptr(hyper), stream_ptr())
+    return out
+
+
 def groupnorm_stats(x, T, G, partials, mean_rstd, eps=1e-5):
     call("vqx_groupnorm_stats", ptr(x), x.stride(0), dt_code(x.dtype), x.shape[0], T, x.shape[1], G, eps,
          ptr(partials), ptr(mean_rstd), stream_ptr())
