@@ -397,6 +397,11 @@ int vqx_vq_stats(const float* z, int64_t n_rows, int32_t D, const int64_t* idx, 
 int vqx_vq_ema_update(float* emb_sum, float* emb_elem, float* E, const float* bsum,
                       const float* bcnt, const float* rand_rows, int32_t K, int32_t D, float mu,
                       float threshold, float* diag, float* partials, vqx_stream_t stream);
+/* The same, and bsum / bcnt are zero afterwards (ABI 126): the next step's
+ * vqx_vq_forward accumulates into them without a zero-fill launch. */
+int vqx_vq_ema_update_clear(float* emb_sum, float* emb_elem, float* E, float* bsum, float* bcnt,
+                            const float* rand_rows, int32_t K, int32_t D, float mu, float threshold, float* diag,
+                            float* partials, vqx_stream_t stream);
 
 /* out[i][:] = src[rows[i]][:] for i < n_out  (f32, row length D).  rows are
  * int64 indices; negative indices write zero rows (rows owned by another

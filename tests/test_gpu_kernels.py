@@ -1113,6 +1113,31 @@ def test_logloss_matches_torch(dtype, B, C, T, ldx):
         assert (dx_full[:, C:] == 7.0).all()  # padding columns untouched
 
 
+def test_ema_update_clear_equals_update_and_zeroes_the_statistics():
+    """vqx_vq_ema_update_clear (ABI 126) = vqx_vq_ema_update bit for bit
+    (codebook, EMA buffers, diagnostics), with bsum / bcnt zero afterwards."""
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(21)
+    K, D = 512, 128
+    base = dict(emb_sum=torch.randn(K, D, generator=g), emb_elem=torch.rand(K, generator=g) * 3,
+                E=torch.randn(K, D, generator=g), bsum=torch.randn(K, D, generator=g),
+                bcnt=torch.randint(0, 5, (K,), generator=g).float(), rand=torch.randn(K, D, generator=g))
+    res = []
+    for clear in (False, True):
+        t = {k: v.clone().to(DEV) for k, v in base.items()}
+        diag = torch.zeros(4, device=DEV)
+        ops.vq_ema_update(t["emb_sum"], t["emb_elem"], t["E"], t["bsum"], t["bcnt"], t["rand"], 0.99, 1.0, diag,
+                          clear=clear)
+        torch.cuda.synchronize()
+        res.append((t, diag))
+    (a, da), (b, db) = res
+    for k in ("emb_sum", "emb_elem", "E"):
+        assert torch.equal(a[k], b[k]), k
+    assert torch.equal(da, db)
+    assert torch.equal(a["bsum"], base["bsum"].to(DEV)) and torch.equal(a["bcnt"], base["bcnt"].to(DEV))
+    assert not b["bsum"].any() and not b["bcnt"].any()
+
+
 def test_sq_norm_finish_adam_equals_finish_then_hyper():
     """vqx_sq_norm_finish_adam (ABI 126) = vqx_sq_norm_finish + vqx_adam_hyper,
     bit for bit: the norm, the per-step scalars (StepLR decay at step 4) and the

@@ -112,6 +112,8 @@ _SIGS = {
     "vqx_vq_stats": [c_void_p, c_int64, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p],
     "vqx_vq_ema_update": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_float,
                           c_float, c_void_p, c_void_p, c_void_p],
+    "vqx_vq_ema_update_clear": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_float,
+                                c_float, c_void_p, c_void_p, c_void_p],
     "vqx_gather_rows": [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_void_p, c_void_p],
     "vqx_gather_rows_host": [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_void_p, c_void_p],
     "vqx_vq_commit_bwd": [c_void_p, c_void_p, c_int64, c_float, c_void_p, c_int32, c_void_p],

@@ -493,7 +493,8 @@ __global__ __launch_bounds__(256) void vq_ema_elem_kernel(float* __restrict__ em
                                                           const float* __restrict__ bsum,
                                                           const float* __restrict__ bcnt,
                                                           const float* __restrict__ rand_rows, int K, int D, float mu,
-                                                          float one_minus_mu, float thr, float* __restrict__ part) {
+                                                          float one_minus_mu, float thr, float* __restrict__ part,
+                                                          float* __restrict__ clear_sum) {
   __shared__ float red[16];
   const int i0 = blockIdx.x * kEmaElems;
   const int n = K * D;
@@ -520,6 +521,7 @@ __global__ __launch_bounds__(256) void vq_ema_elem_kernel(float* __restrict__ em
     const float s = __fadd_rn(__fmul_rn(mu, es[u]), __fmul_rn(one_minus_mu, bs[u]));
     const float el = __fadd_rn(__fmul_rn(mu, ee[u]), __fmul_rn(one_minus_mu, bc[u]));
     emb_sum[i] = s;
+    if (clear_sum) clear_sum[i] = 0.f;  // consumed: zero for the next step's accumulation
     const float uu = (el >= thr) ? 1.f : 0.f;
     // usage*(sum/elem) + (1-usage)*rand, evaluated like the reference
     const float newe = __fadd_rn(__fmul_rn(uu, __fdiv_rn(s, el)), __fmul_rn(1.f - uu, rr[u]));
@@ -556,7 +558,7 @@ __global__ __launch_bounds__(1024) void vq_ema_final_kernel(float* __restrict__ 
                                                             const float* __restrict__ bcnt, int K, int D, float mu,
                                                             float one_minus_mu, float thr,
                                                             const float* __restrict__ part, int nparts,
-                                                            float* __restrict__ diag) {
+                                                            float* __restrict__ diag, float* __restrict__ clear_cnt) {
   __shared__ float red[3][16];
   float a[2] = {0.f, 0.f};  // sum of squared codebook moves, total count
   for (int b = threadIdx.x; b < nparts; b += blockDim.x) a[0] += part[b];
@@ -574,8 +576,10 @@ __global__ __launch_bounds__(1024) void vq_ema_final_kernel(float* __restrict__ 
   }
   __syncthreads();  // red is rewritten
   block_sum_n<3>(e, red);
-  for (int k = threadIdx.x; k < K; k += blockDim.x)
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
     emb_elem[k] = __fadd_rn(__fmul_rn(mu, emb_elem[k]), __fmul_rn(one_minus_mu, bcnt[k]));
+    if (clear_cnt) clear_cnt[k] = 0.f;  // this thread's every read of bcnt[k] is done (and the element kernel's)
+  }
   if (threadIdx.x == 0) {
     diag[0] = expf(-e[0]);
     diag[1] = e[1];
@@ -736,18 +740,31 @@ extern "C" int vqx_vq_stats(const float* z, int64_t n_rows, int32_t D, const int
   return launch_status("vqx_vq_stats");
 }
 
-extern "C" int vqx_vq_ema_update(float* emb_sum, float* emb_elem, float* E, const float* bsum, const float* bcnt,
-                                 const float* rand_rows, int32_t K, int32_t D, float mu, float threshold, float* diag,
-                                 float* partials, vqx_stream_t stream) {
+static int ema_update(float* emb_sum, float* emb_elem, float* E, const float* bsum, const float* bcnt,
+                      const float* rand_rows, int32_t K, int32_t D, float mu, float threshold, float* diag,
+                      float* partials, bool clear, vqx_stream_t stream) {
   if (K <= 0 || D <= 0 || !partials) { set_error("vqx_vq_ema_update: bad K/D or no partials"); return -1; }
   const float omm = (float)(1.0 - (double)mu);  // (1. - mu) in double, as the reference's Python float
   const int nb = (K * D + kEmaElems - 1) / kEmaElems;
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(vq_ema_elem_kernel, dim3(nb), dim3(256), 0, s, emb_sum, emb_elem, E, bsum, bcnt, rand_rows, K,
-                     D, mu, omm, threshold, partials);
+                     D, mu, omm, threshold, partials, clear ? (float*)bsum : nullptr);
   hipLaunchKernelGGL(vq_ema_final_kernel, dim3(1), dim3(1024), 0, s, emb_elem, bcnt, K, D, mu, omm, threshold,
-                     partials, nb, diag);
+                     partials, nb, diag, clear ? (float*)bcnt : nullptr);
   return launch_status("vqx_vq_ema_update");
+}
+
+extern "C" int vqx_vq_ema_update(float* emb_sum, float* emb_elem, float* E, const float* bsum, const float* bcnt,
+                                 const float* rand_rows, int32_t K, int32_t D, float mu, float threshold, float* diag,
+                                 float* partials, vqx_stream_t stream) {
+  return ema_update(emb_sum, emb_elem, E, bsum, bcnt, rand_rows, K, D, mu, threshold, diag, partials, false, stream);
+}
+
+extern "C" int vqx_vq_ema_update_clear(float* emb_sum, float* emb_elem, float* E, float* bsum, float* bcnt,
+                                       const float* rand_rows, int32_t K, int32_t D, float mu, float threshold,
+                                       float* diag, float* partials, vqx_stream_t stream) {
+  if (!bsum || !bcnt) { set_error("vqx_vq_ema_update_clear: null statistics"); return -1; }
+  return ema_update(emb_sum, emb_elem, E, bsum, bcnt, rand_rows, K, D, mu, threshold, diag, partials, true, stream);
 }
 
 extern "C" int vqx_gather_rows(const float* src, int32_t ld_src, const int64_t* rows, int32_t n_out, int32_t D,

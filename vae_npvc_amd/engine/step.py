@@ -1419,7 +1419,9 @@ class VQVAEEngine:
                 self._ema_apply(w)
             w.ev_ema = side.record_event()
             return
-        ops.zero_(w.ema)
+        if not getattr(w, "ema_clean", False):  # bsum / bcnt not left zero by the last update (rand_rows: overwritten)
+            ops.zero_(w.ema)
+        w.ema_clean = False
         ops.vq_forward(w.z, q.embeddings, w.idx, w.zq, w.zq_c, w.stats[1:2], w.vq_part, w.bsum, w.bcnt)
         self._ema_rows(w, K)
         if self.comm is not None:
@@ -1437,9 +1439,12 @@ class VQVAEEngine:
             ops.gather_rows_host(w.z, perm, w.rand_rows)
 
     def _ema_apply(self, w):
+        """The EMA update; it leaves bsum / bcnt zero (clear=True), so the next
+        step's accumulation needs no zero fill of the statistics."""
         q = self.m.quantizer
         ops.vq_ema_update(q.emb_sum, q.emb_elem, q.embeddings, w.bsum, w.bcnt, w.rand_rows, q.mu, q.threshold,
-                          w.stats[4:8], w.ema_part)
+                          w.stats[4:8], w.ema_part, clear=True)
+        w.ema_clean = True
 
     def vq_ema_update(self, w):
         """End of the step: apply the EMA update (or, when it ran on the side

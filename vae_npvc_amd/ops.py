@@ -517,14 +517,15 @@ def vq_stats(z, idx, K, partials, bsum, bcnt):
     call("vqx_vq_stats", ptr(z), N, D, ptr(idx), K, ptr(partials), ptr(bsum), ptr(bcnt), stream_ptr())
 
 
-def vq_ema_update(emb_sum, emb_elem, E, bsum, bcnt, rand_rows, mu, threshold, diag, partials=None):
-    """partials: workspace of ceil(K*D/1024) floats (allocated here if None)."""
+def vq_ema_update(emb_sum, emb_elem, E, bsum, bcnt, rand_rows, mu, threshold, diag, partials=None, clear=False):
+    """partials: workspace of ceil(K*D/1024) floats (allocated here if None);
+    clear: bsum / bcnt are zero afterwards (vqx_vq_ema_update_clear)."""
     K, D = E.shape
     if partials is None:
         partials = torch.empty((K * D + 1023) // 1024, device=E.device, dtype=torch.float32)
     if partials.numel() < (K * D + 1023) // 1024:
         raise ValueError(f"vq_ema_update: workspace {partials.numel()} < {(K * D + 1023) // 1024} floats")
-    call("vqx_vq_ema_update", ptr(emb_sum), ptr(emb_elem), ptr(E), ptr(bsum), ptr(bcnt), ptr(rand_rows), K, D,
+    call("vqx_vq_ema_update_clear" if clear else "vqx_vq_ema_update", ptr(emb_sum), ptr(emb_elem), ptr(E), ptr(bsum), ptr(bcnt), ptr(rand_rows), K, D,
          mu, threshold, ptr(diag), ptr(partials), stream_ptr())
 
 
