@@ -353,6 +353,14 @@ int vqx_ntc_to_nct(const void* y, int32_t ldy, int32_t dtype, int32_t B, int32_t
 int vqx_logloss_fwd_bwd(const float* x_nct, const float* xhat, int32_t ldxh, int32_t B, int32_t C,
                         int32_t T, float grad_scale, void* dxhat, int32_t lddx, int32_t dtype,
                         float* loss_out, float* partials, vqx_stream_t stream);
+/* The same, and in its final sum launch also extra_out[0] = the sum of
+ * extra_partials[0 .. n_extra) in the order vqx_vq_forward sums its
+ * commitment partials (ABI 126: the VQ kernel then runs with sqerr_out NULL,
+ * one launch fewer). */
+int vqx_logloss_fwd_bwd_x(const float* x, const float* xhat, int32_t ldxh, int32_t B, int32_t C, int32_t T,
+                          float grad_scale, void* dxhat, int32_t lddx, int32_t dtype, float* loss_out,
+                          float* partials, const float* extra_partials, int32_t n_extra, float* extra_out,
+                          vqx_stream_t stream);
 
 /*
  * EMA vector-quantizer forward (EMAVectorQuantizer.forward,

@@ -1113,6 +1113,32 @@ def test_logloss_matches_torch(dtype, B, C, T, ldx):
         assert (dx_full[:, C:] == 7.0).all()  # padding columns untouched
 
 
+def test_logloss_x_sums_the_vq_partials_like_the_vq_kernel():
+    """vqx_logloss_fwd_bwd_x (ABI 126) = vqx_logloss_fwd_bwd plus, in its final
+    launch, the VQ commitment sum that vqx_vq_forward computes itself with
+    sqerr_out set, bit for bit."""
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(5)
+    N, D, K = 16384, 128, 512
+    z = torch.randn(N, D, generator=g).to(DEV)
+    E = torch.randn(K, D, generator=g).to(DEV)
+    idx = torch.empty(N, dtype=torch.int64, device=DEV)
+    part = torch.empty(ops.vq_workspace(N, K, False), device=DEV)
+    sq_ref = torch.zeros(1, device=DEV)
+    ops.vq_forward(z, E, idx, None, None, sq_ref, part)
+    B, C, T = 64, 80, 256
+    x = torch.randn(B, C, T, generator=g).to(DEV)
+    xh = torch.randn(B * T, C, generator=g).to(DEV)
+    dx1, dx2 = (torch.empty(B * T, C, device=DEV, dtype=torch.bfloat16) for _ in range(2))
+    l1, l2, sq = torch.zeros(1, device=DEV), torch.zeros(1, device=DEV), torch.zeros(1, device=DEV)
+    lp = torch.empty(1024, device=DEV)
+    ops.logloss_fwd_bwd(x, xh, 1.0 / (B * T), dx1, l1, lp)
+    n = (N + ops.VQ_FRAMES - 1) // ops.VQ_FRAMES
+    ops.logloss_fwd_bwd_x(x, xh, 1.0 / (B * T), dx2, l2, lp, part[:n], sq)
+    torch.cuda.synchronize()
+    assert torch.equal(l1, l2) and torch.equal(dx1, dx2) and torch.equal(sq, sq_ref)
+
+
 def test_ema_update_clear_equals_update_and_zeroes_the_statistics():
     """vqx_vq_ema_update_clear (ABI 126) = vqx_vq_ema_update bit for bit
     (codebook, EMA buffers, diagnostics), with bsum / bcnt zero afterwards."""

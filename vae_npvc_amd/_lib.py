@@ -106,6 +106,8 @@ _SIGS = {
     "vqx_ntc_to_nct": [c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p],
     "vqx_logloss_fwd_bwd": [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_float, c_void_p, c_int32,
                             c_int32, c_void_p, c_void_p, c_void_p],
+    "vqx_logloss_fwd_bwd_x": [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_float, c_void_p, c_int32,
+                              c_int32, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p],
     "vqx_vq_forward": [c_void_p, c_int64, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_int32,
                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "vqx_vq_workspace": [c_int64, c_int32, c_int32, c_int32, c_void_p],

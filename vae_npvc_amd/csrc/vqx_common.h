@@ -97,6 +97,27 @@ __device__ __forceinline__ float block_sum(float v, float* scratch /* >= 16 floa
   return s;
 }
 
+// N block sums at once (one pair of barriers): each value's waves added in
+// wave order, as block_sum does
+template <int N>
+__device__ __forceinline__ void block_sum_n(float (&v)[N], float (*scratch)[16]) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] = wave_sum(v[k]);
+  __syncthreads();
+  if (l == 0) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) scratch[k][w] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    float t = 0.f;
+    for (int i = 0; i < nw; ++i) t += scratch[k][i];
+    v[k] = t;
+  }
+}
+
 // Bijective XCD-aware remap of a linear block id (guide §5 "XCD swizzle must
 // be bijective"): blocks b and b+8 share an XCD, so give each XCD group a
 // contiguous range of logical tiles.

@@ -1409,6 +1409,21 @@ __global__ void sum_partials_scale_kernel(const float* __restrict__ p, int n, fl
   if (threadIdx.x == 0) out[0] = s * scale;
 }
 
+// two such sums in one launch (the log-loss total and another partial set, e.g.
+// the VQ kernel's commitment partials): each as sum_partials_scale_kernel sums it
+__global__ void sum_partials2_kernel(const float* __restrict__ p, int n, float scale, float* __restrict__ out,
+                                     const float* __restrict__ p2, int n2, float scale2, float* __restrict__ out2) {
+  __shared__ float red[2][16];
+  float v[2] = {0.f, 0.f};
+  for (int i = threadIdx.x; i < n; i += blockDim.x) v[0] += p[i];
+  for (int i = threadIdx.x; i < n2; i += blockDim.x) v[1] += p2[i];
+  block_sum_n<2>(v, red);
+  if (threadIdx.x == 0) {
+    out[0] = v[0] * scale;
+    out2[0] = v[1] * scale2;
+  }
+}
+
 // ------------------------------------------------------------ small kernels
 template <typename T>
 __global__ void time_gather_kernel(const T* __restrict__ x, T* __restrict__ y, int B, int T_, int C,
@@ -2751,9 +2766,9 @@ extern "C" int vqx_ntc_to_nct(const void* y, int32_t ldy, int32_t dtype, int32_t
   return launch_status("vqx_ntc_to_nct");
 }
 
-extern "C" int vqx_logloss_fwd_bwd(const float* x, const float* xhat, int32_t ldxh, int32_t B, int32_t C, int32_t T,
-                                   float grad_scale, void* dxhat, int32_t lddx, int32_t dtype, float* loss_out,
-                                   float* partials, vqx_stream_t stream) {
+static int logloss_impl(const float* x, const float* xhat, int32_t ldxh, int32_t B, int32_t C, int32_t T,
+                        float grad_scale, void* dxhat, int32_t lddx, int32_t dtype, float* loss_out, float* partials,
+                        const float* extra_parts, int32_t n_extra, float* extra_out, vqx_stream_t stream) {
   const int64_t total = (int64_t)B * C * T;
   if (total <= 0 || total >= (1LL << 31)) { set_error("vqx_logloss_fwd_bwd: B*C*T must be in [1, 2^31)"); return -1; }
   hipStream_t s = (hipStream_t)stream;
@@ -2775,8 +2790,31 @@ extern "C" int vqx_logloss_fwd_bwd(const float* x, const float* xhat, int32_t ld
     else
       hipLaunchKernelGGL(logloss_kernel<float>, dim3(grid), dim3(256), 0, s, x, xhat, ldxh, B, C, T, grad_scale, (float*)dxhat, lddx, partials);
   }
-  hipLaunchKernelGGL(sum_partials_scale_kernel, dim3(1), dim3(1024), 0, s, partials, grid, 1.0f / ((float)B * (float)T), loss_out);
+  if (extra_parts)
+    hipLaunchKernelGGL(sum_partials2_kernel, dim3(1), dim3(1024), 0, s, partials, grid, 1.0f / ((float)B * (float)T),
+                       loss_out, extra_parts, n_extra, 1.0f, extra_out);
+  else
+    hipLaunchKernelGGL(sum_partials_scale_kernel, dim3(1), dim3(1024), 0, s, partials, grid, 1.0f / ((float)B * (float)T), loss_out);
   return launch_status("vqx_logloss_fwd_bwd");
+}
+
+extern "C" int vqx_logloss_fwd_bwd(const float* x, const float* xhat, int32_t ldxh, int32_t B, int32_t C, int32_t T,
+                                   float grad_scale, void* dxhat, int32_t lddx, int32_t dtype, float* loss_out,
+                                   float* partials, vqx_stream_t stream) {
+  return logloss_impl(x, xhat, ldxh, B, C, T, grad_scale, dxhat, lddx, dtype, loss_out, partials, nullptr, 0, nullptr,
+                      stream);
+}
+
+extern "C" int vqx_logloss_fwd_bwd_x(const float* x, const float* xhat, int32_t ldxh, int32_t B, int32_t C, int32_t T,
+                                     float grad_scale, void* dxhat, int32_t lddx, int32_t dtype, float* loss_out,
+                                     float* partials, const float* extra_partials, int32_t n_extra, float* extra_out,
+                                     vqx_stream_t stream) {
+  if (!extra_partials || !extra_out || n_extra < 1) {
+    set_error("vqx_logloss_fwd_bwd_x: needs extra partials and their output");
+    return -1;
+  }
+  return logloss_impl(x, xhat, ldxh, B, C, T, grad_scale, dxhat, lddx, dtype, loss_out, partials, extra_partials,
+                      n_extra, extra_out, stream);
 }
 
 extern "C" int vqx_time_gather(const void* x, void* y, int32_t B, int32_t T, int32_t C, const int32_t* src_t,

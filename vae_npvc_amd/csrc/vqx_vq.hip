@@ -533,27 +533,6 @@ __global__ __launch_bounds__(256) void vq_ema_elem_kernel(float* __restrict__ em
   if (threadIdx.x == 0) part[blockIdx.x] = dsq;
 }
 
-// N block sums at once (one pair of barriers): each value's waves added in
-// wave order, as block_sum does
-template <int N>
-__device__ __forceinline__ void block_sum_n(float (&v)[N], float (*scratch)[16]) {
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
-#pragma unroll
-  for (int k = 0; k < N; ++k) v[k] = wave_sum(v[k]);
-  __syncthreads();
-  if (l == 0) {
-#pragma unroll
-    for (int k = 0; k < N; ++k) scratch[k][w] = v[k];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < N; ++k) {
-    float t = 0.f;
-    for (int i = 0; i < nw; ++i) t += scratch[k][i];
-    v[k] = t;
-  }
-}
-
 __global__ __launch_bounds__(1024) void vq_ema_final_kernel(float* __restrict__ emb_elem,
                                                             const float* __restrict__ bcnt, int K, int D, float mu,
                                                             float one_minus_mu, float thr,

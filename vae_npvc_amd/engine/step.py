@@ -1422,7 +1422,9 @@ class VQVAEEngine:
         if not getattr(w, "ema_clean", False):  # bsum / bcnt not left zero by the last update (rand_rows: overwritten)
             ops.zero_(w.ema)
         w.ema_clean = False
-        ops.vq_forward(w.z, q.embeddings, w.idx, w.zq, w.zq_c, w.stats[1:2], w.vq_part, w.bsum, w.bcnt)
+        # the commitment partials' sum (stats[1]) is left to the log-loss launch (train_forward)
+        ops.vq_forward(w.z, q.embeddings, w.idx, w.zq, w.zq_c, None, w.vq_part, w.bsum, w.bcnt)
+        w.vq_sum_pending = (w.Nz + ops.VQ_FRAMES - 1) // ops.VQ_FRAMES
         self._ema_rows(w, K)
         if self.comm is not None:
             self._ema_work = self.comm.all_reduce_sum(w.ema, async_op=True)
@@ -1502,7 +1504,13 @@ class VQVAEEngine:
         if w.ev_cond is not None:
             torch.cuda.current_stream().wait_event(w.ev_cond)
         self.decoder_fwd(w, w.zq_in)
-        ops.logloss_fwd_bwd(x, w.xhat, 1.0 / (B * T), w.dxhat, w.stats[0:1], w.loss_part)
+        n_vq = getattr(w, "vq_sum_pending", 0)
+        if n_vq:  # the VQ commitment partials summed in the log-loss's final launch
+            ops.logloss_fwd_bwd_x(x, w.xhat, 1.0 / (B * T), w.dxhat, w.stats[0:1], w.loss_part, w.vq_part[:n_vq],
+                                  w.stats[1:2])
+            w.vq_sum_pending = 0
+        else:
+            ops.logloss_fwd_bwd(x, w.xhat, 1.0 / (B * T), w.dxhat, w.stats[0:1], w.loss_part)
         return w
 
     def backward(self, w, grad_loss=None):

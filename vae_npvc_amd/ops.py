@@ -486,6 +486,20 @@ def logloss_fwd_bwd(x_nct, xhat, grad_scale, dxhat, loss_out, partials):
     return loss_out
 
 
+def logloss_fwd_bwd_x(x_nct, xhat, grad_scale, dxhat, loss_out, partials, extra_partials, extra_out):
+    """logloss_fwd_bwd, and extra_out[0] = the sum of extra_partials in the same
+    final launch (the VQ kernel's commitment partials: VQ_FRAMES frames each)."""
+    B, C, T = x_nct.shape
+    _check_cuda(extra_partials, extra_out)
+    call("vqx_logloss_fwd_bwd_x", ptr(x_nct), ptr(xhat), xhat.stride(0), B, C, T, grad_scale, ptr(dxhat),
+         dxhat.stride(0) if dxhat is not None else 0, dt_code(dxhat.dtype) if dxhat is not None else 0,
+         ptr(loss_out), ptr(partials), ptr(extra_partials), extra_partials.numel(), ptr(extra_out), stream_ptr())
+    return loss_out
+
+
+VQ_FRAMES = 32  # frames per commitment partial of vqx_vq_forward (vqx_vq.hip VQ_FRAMES)
+
+
 def vq_workspace(n_rows, K, stats, D=128):
     """Floats of workspace vqx_vq_forward needs for K codes of width D (with or
     without EMA statistics)."""
