@@ -494,14 +494,25 @@ __global__ __launch_bounds__(kWnThreads) void wn_bwd_kernel(const vqx_wn_layer* 
   const int64_t srow = (int64_t)o * scols;  // element offset of this row in split 0
   const int splits = l.splits;
   const bool sbf = l.slab_dtype == VQX_BF16;
-  // the row of v, loaded before the slabs so both latencies overlap (cols <= 4096, 256 threads)
-  float vr[kWnVRegs];
+  // the row of v, loaded before the slabs so both latencies overlap (cols <= 4096,
+  // 256 threads): thread t holds the 4-element chunks c = t + 256u, 16-B loads
+  // when the row is 16-B aligned (cols % 4 == 0: the data path moves a quarter
+  // of the lane requests of element loads; this kernel's TD is ~90% busy)
+  constexpr int kV4 = kWnVRegs / 4;
+  f32x4_t vr4[kV4];
   const float* vrow = l.v + (int64_t)o * cols;
-  {
+  float* dv = l.dv + (int64_t)o * cols;
+  const bool al16 = ((((uintptr_t)vrow) | ((uintptr_t)dv)) & 15) == 0;
 #pragma unroll
-    for (int u = 0; u < kWnVRegs; ++u) {
-      const int i = threadIdx.x + u * kWnThreads;
-      vr[u] = (l.g && i < cols) ? vrow[i] : 0.f;
+  for (int u = 0; u < kV4; ++u) {
+    const int i = 4 * ((int)threadIdx.x + u * kWnThreads);
+    vr4[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    if (l.g && i < cols) {
+      if (al16) {
+        vr4[u] = *(const f32x4_t*)(vrow + i);
+      } else {
+        vr4[u] = f32x4_t{vrow[i], vrow[i + 1], vrow[i + 2], vrow[i + 3]};
+      }
     }
   }
   // Thread t sums the splits g, g+G, ... of column group x4 = t % nx4 (G = the
@@ -566,21 +577,38 @@ __global__ __launch_bounds__(kWnThreads) void wn_bwd_kernel(const vqx_wn_layer* 
     }
   }
   __syncthreads();
-  float* dv = l.dv + (int64_t)o * cols;
   float q2 = 0.f;
+  auto store4 = [&](int i, const f32x4_t& r) {
+    if (al16) {
+      *(f32x4_t*)(dv + i) = r;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) dv[i + k] = r[k];
+    }
+  };
   if (!l.g) {  // plain weight (weight norm removed): dv is the weight gradient itself
-    for (int i = threadIdx.x; i < cols; i += blockDim.x) {
-      dv[i] = dw[i];
-      q2 = fmaf(dw[i], dw[i], q2);
+#pragma unroll
+    for (int u = 0; u < kV4; ++u) {
+      const int i = 4 * ((int)threadIdx.x + u * kWnThreads);
+      if (i < cols) {
+        const f32x4_t r = *(const f32x4_t*)(dw + i);
+        store4(i, r);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q2 = fmaf(r[k], r[k], q2);
+      }
     }
     wn_sq_store(sq, q2);
     return;
   }
   float dot = 0.f;
 #pragma unroll
-  for (int u = 0; u < kWnVRegs; ++u) {
-    const int i = threadIdx.x + u * kWnThreads;
-    if (i < cols) dot = fmaf(dw[i], vr[u], dot);
+  for (int u = 0; u < kV4; ++u) {
+    const int i = 4 * ((int)threadIdx.x + u * kWnThreads);
+    if (i < cols) {
+      const f32x4_t d4 = *(const f32x4_t*)(dw + i);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) dot = fmaf(d4[k], vr4[u][k], dot);
+    }
   }
   dot = block_sum(dot, red);
   const float nrm = l.norm[o];
@@ -592,12 +620,17 @@ __global__ __launch_bounds__(kWnThreads) void wn_bwd_kernel(const vqx_wn_layer* 
   }
   const float sc = gg / nrm, t = dg / nrm;
 #pragma unroll
-  for (int u = 0; u < kWnVRegs; ++u) {
-    const int i = threadIdx.x + u * kWnThreads;
+  for (int u = 0; u < kV4; ++u) {
+    const int i = 4 * ((int)threadIdx.x + u * kWnThreads);
     if (i < cols) {
-      const float r = sc * (dw[i] - vr[u] * t);
-      dv[i] = r;
-      q2 = fmaf(r, r, q2);
+      const f32x4_t d4 = *(const f32x4_t*)(dw + i);
+      f32x4_t r;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        r[k] = sc * (d4[k] - vr4[u][k] * t);
+        q2 = fmaf(r[k], r[k], q2);
+      }
+      store4(i, r);
     }
   }
   wn_sq_store(sq, q2);
