@@ -582,6 +582,12 @@ int vqx_scale_act_2d(const void* src, int32_t ld_src, int32_t src_dtype, void* d
  * and the residual/skip gradient buffers of the backward. */
 int vqx_convert_2d(const void* src, int32_t ld_src, int32_t src_dtype, void* dst, int32_t ld_dst,
                    int32_t dst_dtype, int64_t rows, int32_t cols, vqx_stream_t stream);
+/* convert_2d(src, dst) and, in the same launch, zero_dst[r][c] = 0 for r <
+ * zero_rows, c < zero_cols (dst's dtype; ABI 126: the decoder backward's
+ * dL/dskip copy and the zero dL/dx at the decoder output in one launch). */
+int vqx_convert_2d_zero2(const void* src, int32_t ld_src, int32_t src_dtype, void* dst, int32_t ld_dst,
+                         int32_t dst_dtype, int64_t rows, int32_t cols, void* zero_dst, int32_t ld_zero,
+                         int64_t zero_rows, int32_t zero_cols, vqx_stream_t stream);
 
 /* Work units per split of the weight-gradient kernel that vqx_conv1d_wgrad
  * would launch for these arguments, one unit = one 4-wave group (two per CU

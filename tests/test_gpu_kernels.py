@@ -391,6 +391,23 @@ def test_convert_2d_paths(dt_in, dt_out, rows, cols, lds, ldd):
         assert (dst_full[:, cols:] == 3.0).all()
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rows,C,S", [(16384, 512, 256), (16384, 256, 256), (9, 13, 7)])
+def test_convert_2d_zero2(dt, rows, C, S):
+    """vqx_convert_2d_zero2 (ABI 126): dst = src and zero_dst = 0 in one launch
+    (chunk path) or two (widths not multiples of 8), in the layout of the
+    decoder's [dL/dx (C) | dL/dskip (S)] buffers."""
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(rows + C)
+    a = torch.randn(rows, C + S, generator=g).to(DEV, dt)
+    b = torch.full((rows, C + S), 5.0, device=DEV, dtype=dt)
+    want = a[:, C:].clone()
+    ops.convert_2d_zero2(a[:, C:], b[:, C:], a[:, :C])
+    torch.cuda.synchronize()
+    assert torch.equal(b[:, C:], want) and (b[:, :C] == 5.0).all()
+    assert not a[:, :C].any() and torch.equal(a[:, C:], want)
+
+
 @pytest.mark.parametrize("dt_out", [torch.float32, torch.bfloat16])
 def test_scale_act_2d(dt_out):
     ops = _ops()

@@ -2406,38 +2406,48 @@ template <> struct Chunk8<bf16_t> {
   __device__ static __forceinline__ void ld(const bf16_t* p, float* f) { Vec<bf16_t>::load(p, f); }
   __device__ static __forceinline__ void st(bf16_t* p, const float* f) { Vec<bf16_t>::store(p, f); }
 };
+// zdst (optional): a second matrix (n8z chunks, cprz per row) set to zero in the
+// same launch (vqx_convert_2d_zero2): chunk indices past n8 address it
 template <typename S, typename D, bool ZERO>
 __global__ __launch_bounds__(256) void map8_kernel(const S* __restrict__ src, int lds, D* __restrict__ dst, int ldd,
-                                                   int n8, int cpr, float scale, int act) {
+                                                   int n8, int cpr, float scale, int act, D* __restrict__ zdst,
+                                                   int ldz, int n8z, int cprz) {
   constexpr int U = 4;
   const int stride = gridDim.x * 256;
-  for (int q0 = blockIdx.x * 256 + threadIdx.x; q0 < n8; q0 += U * stride) {
+  const int total = n8 + n8z;
+  for (int q0 = blockIdx.x * 256 + threadIdx.x; q0 < total; q0 += U * stride) {
     float v[U][8];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int q = min(q0 + u * stride, n8 - 1), r = q / cpr, c = (q - r * cpr) * 8;
-      if constexpr (ZERO) {
+      const int q = q0 + u * stride;
+      if (ZERO || q >= n8) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[u][k] = 0.f;
       } else {
+        const int r = q / cpr, c = (q - r * cpr) * 8;
         Chunk8<S>::ld(src + (int64_t)r * lds + c, v[u]);
       }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int q = q0 + u * stride;
-      if (q >= n8) break;
-      const int r = q / cpr, c = (q - r * cpr) * 8;
-      if (!ZERO) {
+      if (q >= total) break;
+      if (q < n8) {
+        const int r = q / cpr, c = (q - r * cpr) * 8;
+        if (!ZERO) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          float x = scale * v[u][k];
-          if (act == VQX_PRO_RELU) x = x > 0.f ? x : 0.f;
-          else if (act == VQX_PRO_LRELU) x = x > 0.f ? x : 0.2f * x;
-          v[u][k] = x;
+          for (int k = 0; k < 8; ++k) {
+            float x = scale * v[u][k];
+            if (act == VQX_PRO_RELU) x = x > 0.f ? x : 0.f;
+            else if (act == VQX_PRO_LRELU) x = x > 0.f ? x : 0.2f * x;
+            v[u][k] = x;
+          }
         }
+        Chunk8<D>::st(dst + (int64_t)r * ldd + c, v[u]);
+      } else {
+        const int qz = q - n8, r = qz / cprz, c = (qz - r * cprz) * 8;
+        Chunk8<D>::st(zdst + (int64_t)r * ldz + c, v[u]);  // zeros
       }
-      Chunk8<D>::st(dst + (int64_t)r * ldd + c, v[u]);
     }
   }
 }
@@ -2985,24 +2995,26 @@ extern "C" int vqx_radam_step(float* p, const float* g, float* m, float* v, int6
 
 // the 8-element chunk path when the shapes allow it (see map8_kernel); false: not taken
 static bool map8_launch(const void* src, int32_t lds, int32_t sdt, void* dst, int32_t ldd, int32_t ddt, int64_t rows,
-                        int32_t cols, float scale, int32_t act, hipStream_t s) {
-  if (cols % 8 || ldd % 8 || (src && lds % 8) || rows * cols / 8 >= (int64_t)1 << 31 ||
-      ((uintptr_t)dst & 15) || ((uintptr_t)src & 15))
+                        int32_t cols, float scale, int32_t act, hipStream_t s, void* zdst = nullptr, int32_t ldz = 0,
+                        int64_t zrows = 0, int32_t zcols = 0) {
+  if (cols % 8 || ldd % 8 || (src && lds % 8) || (rows * cols + zrows * zcols) / 8 >= (int64_t)1 << 31 ||
+      ((uintptr_t)dst & 15) || ((uintptr_t)src & 15) || (zdst && (zcols % 8 || ldz % 8 || ((uintptr_t)zdst & 15))))
     return false;
   const int n8 = (int)(rows * cols / 8), cpr = cols / 8;
-  const int grid = grid_for(n8, 256, 2048);
+  const int n8z = zdst ? (int)(zrows * zcols / 8) : 0, cprz = zdst ? zcols / 8 : 1;
+  const int grid = grid_for(n8 + n8z, 256, 2048);
   const bool sb = sdt == VQX_BF16, db = ddt == VQX_BF16;
   if (!src) {
-    if (db) hipLaunchKernelGGL((map8_kernel<float, bf16_t, true>), dim3(grid), dim3(256), 0, s, nullptr, 0, (bf16_t*)dst, ldd, n8, cpr, 1.f, 0);
-    else hipLaunchKernelGGL((map8_kernel<float, float, true>), dim3(grid), dim3(256), 0, s, nullptr, 0, (float*)dst, ldd, n8, cpr, 1.f, 0);
+    if (db) hipLaunchKernelGGL((map8_kernel<float, bf16_t, true>), dim3(grid), dim3(256), 0, s, nullptr, 0, (bf16_t*)dst, ldd, n8, cpr, 1.f, 0, (bf16_t*)zdst, ldz, n8z, cprz);
+    else hipLaunchKernelGGL((map8_kernel<float, float, true>), dim3(grid), dim3(256), 0, s, nullptr, 0, (float*)dst, ldd, n8, cpr, 1.f, 0, (float*)zdst, ldz, n8z, cprz);
   } else if (sb && db) {
-    hipLaunchKernelGGL((map8_kernel<bf16_t, bf16_t, false>), dim3(grid), dim3(256), 0, s, (const bf16_t*)src, lds, (bf16_t*)dst, ldd, n8, cpr, scale, act);
+    hipLaunchKernelGGL((map8_kernel<bf16_t, bf16_t, false>), dim3(grid), dim3(256), 0, s, (const bf16_t*)src, lds, (bf16_t*)dst, ldd, n8, cpr, scale, act, (bf16_t*)zdst, ldz, n8z, cprz);
   } else if (sb) {
-    hipLaunchKernelGGL((map8_kernel<bf16_t, float, false>), dim3(grid), dim3(256), 0, s, (const bf16_t*)src, lds, (float*)dst, ldd, n8, cpr, scale, act);
+    hipLaunchKernelGGL((map8_kernel<bf16_t, float, false>), dim3(grid), dim3(256), 0, s, (const bf16_t*)src, lds, (float*)dst, ldd, n8, cpr, scale, act, (float*)zdst, ldz, n8z, cprz);
   } else if (db) {
-    hipLaunchKernelGGL((map8_kernel<float, bf16_t, false>), dim3(grid), dim3(256), 0, s, (const float*)src, lds, (bf16_t*)dst, ldd, n8, cpr, scale, act);
+    hipLaunchKernelGGL((map8_kernel<float, bf16_t, false>), dim3(grid), dim3(256), 0, s, (const float*)src, lds, (bf16_t*)dst, ldd, n8, cpr, scale, act, (bf16_t*)zdst, ldz, n8z, cprz);
   } else {
-    hipLaunchKernelGGL((map8_kernel<float, float, false>), dim3(grid), dim3(256), 0, s, (const float*)src, lds, (float*)dst, ldd, n8, cpr, scale, act);
+    hipLaunchKernelGGL((map8_kernel<float, float, false>), dim3(grid), dim3(256), 0, s, (const float*)src, lds, (float*)dst, ldd, n8, cpr, scale, act, (float*)zdst, ldz, n8z, cprz);
   }
   return true;
 }
@@ -3016,6 +3028,21 @@ extern "C" int vqx_convert_2d(const void* src, int32_t ld_src, int32_t src_dtype
   hipLaunchKernelGGL(convert_2d_kernel, dim3(grid_for(rows * cols, 256, 8192)), dim3(256), 0, (hipStream_t)stream,
                      src, ld_src, src_dtype, dst, ld_dst, dst_dtype, rows, cols);
   return launch_status("vqx_convert_2d");
+}
+
+extern "C" int vqx_convert_2d_zero2(const void* src, int32_t ld_src, int32_t src_dtype, void* dst, int32_t ld_dst,
+                                    int32_t dst_dtype, int64_t rows, int32_t cols, void* zero_dst, int32_t ld_zero,
+                                    int64_t zero_rows, int32_t zero_cols, vqx_stream_t stream) {
+  if (rows <= 0 || cols <= 0 || zero_rows < 0 || zero_cols < 0) { set_error("vqx_convert_2d_zero2: bad shape"); return -1; }
+  if (!dst || (!zero_dst && zero_rows * zero_cols)) { set_error("vqx_convert_2d_zero2: null dst"); return -1; }
+  hipStream_t s = (hipStream_t)stream;
+  if (map8_launch(src, ld_src, src_dtype, dst, ld_dst, dst_dtype, rows, cols, 1.f, VQX_PRO_NONE, s, zero_dst, ld_zero,
+                  zero_rows, zero_cols))
+    return launch_status("vqx_convert_2d_zero2");
+  // unaligned shapes: the two element passes
+  const int rc1 = vqx_convert_2d(src, ld_src, src_dtype, dst, ld_dst, dst_dtype, rows, cols, stream);
+  if (rc1 || !zero_rows || !zero_cols) return rc1;
+  return vqx_convert_2d(nullptr, 0, 0, zero_dst, ld_zero, dst_dtype, zero_rows, zero_cols, stream);
 }
 
 extern "C" int vqx_scale_act_2d(const void* src, int32_t ld_src, int32_t src_dtype, void* dst, int32_t ld_dst,

@@ -1277,13 +1277,15 @@ class VQVAEEngine:
         cur = sw.dr[k]
         self.wgrad_dgrad(f1, w.df1, w.a_skip, cur[:, sw.C:], w.T, mask=w.a_skip, mask_slope=0.0, mask_scale=s,
                          colsum=w.cs_skip)
-        for si in range(ns):
-            if self.dec_stages[si].blocks:
-                for q in range(2):
-                    if si == lst and q == k:
-                        continue
-                    ops.convert_2d(cur[:, sw.C:], w.dec[si].dr[q][:, w.dec[si].C:])
-        ops.convert_2d(None, cur, cols=sw.C)  # dL/dx at the decoder output is 0: the last residual is unused
+        targets = [w.dec[si].dr[q][:, w.dec[si].C:] for si in range(ns) if self.dec_stages[si].blocks
+                   for q in range(2) if not (si == lst and q == k)]
+        if len(targets) == 1:
+            # the copy and the zero dL/dx at the decoder output (the last residual is unused) in one pass
+            ops.convert_2d_zero2(cur[:, sw.C:], targets[0], cur[:, :sw.C])
+        else:
+            for t in targets:
+                ops.convert_2d(cur[:, sw.C:], t)
+            ops.convert_2d(None, cur, cols=sw.C)  # dL/dx at the decoder output is 0: the last residual is unused
         # (its bias-gradient partials sw.cs[-1] are zero since the workspace was allocated)
         self._wn_bwd(w, "fin")
         cur_x = cur[:, :sw.C]

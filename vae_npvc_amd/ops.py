@@ -668,6 +668,17 @@ def convert_2d(src, dst, rows=None, cols=None):
     return dst
 
 
+def convert_2d_zero2(src, dst, zero_dst):
+    """dst = src (dtype-converting, strided) and zero_dst = 0 (dst's dtype), one launch."""
+    _check_cuda(src, dst, zero_dst)
+    if tuple(src.shape) != tuple(dst.shape) or zero_dst.dtype != dst.dtype or zero_dst.dim() != 2:
+        raise ValueError("convert_2d_zero2: src and dst must share a shape, zero_dst dst's dtype")
+    call("vqx_convert_2d_zero2", ptr(src), src.stride(0), dt_code(src.dtype), ptr(dst), dst.stride(0),
+         dt_code(dst.dtype), dst.shape[0], dst.shape[1], ptr(zero_dst), zero_dst.stride(0), zero_dst.shape[0],
+         zero_dst.shape[1], stream_ptr())
+    return dst
+
+
 def zero_(t):
     """Zero a contiguous f32/bf16 device tensor with the native fill."""
     flat = t.view(1, -1)
