@@ -448,15 +448,16 @@ def test_dgrad_colsum_partials(n_utt, T, tile):
                                                         (1, 512, 1024, 3, 8, True), (0, 512, 512, 3, 16, True),
                                                         (0, 80, 128, 1, 3, True), (1, 128, 80, 5, 1, True),
                                                         (0, 256, 64, 1, 7, False), (0, 1024, 128, 1, 1, True),
-                                                        (0, 77, 1000, 1, 1, True)])
+                                                        (0, 77, 1000, 1, 1, True), (0, 77, 200, 1, 2, True)])
 def test_weight_norm_bwd_reduces_slabs_like_torch(sdt, kind, rows, other, k, splits, wn):
     """vqx_weight_norm_bwd (wn_bwd_kernel): sums the split-K slabs (fp32 or
     bf16) in a fixed order, maps them to v's layout (Conv1d rows cout: x =
     j*cin + ci; ConvTranspose1d rows cin: x = j'*cout + co, tap k-1-j') and
     forms the weight-norm gradients dv, dg of torch._weight_norm(v, g, 0);
     1x1 rows split their 25-32 slabs over thread groups, wide rows do not;
-    short 1x1 rows with little split work (<= 1024 columns, e.g. the
-    speaker-conditioning linears' 1024 x 128, one slab) take one wave per row;
+    short 1x1 rows with little split work (<= 256 columns, e.g. the
+    speaker-conditioning linears' 1024 x 128, one slab) take one wave per row,
+    longer ones (77 x 1000) the row-block path;
     a plain weight (weight norm removed) gets dW itself."""
     ops = _ops()
     from vae_npvc_amd import _lib as L

@@ -361,8 +361,13 @@ __device__ __forceinline__ f32x4_t slab_sum(const void* slabs, int64_t p, int64_
 // so the block -- not the grid -- must carry the loads in flight.
 constexpr int kWnVRegs = 4096 / kWnThreads;  // v row values per thread (row length <= 4096)
 constexpr int kWnCrCols = 32;  // columns per column-reduce block
-constexpr int kWnWaveX4 = 4;   // 16-B column groups per lane on the wave-per-row path (rows <= 1024 columns)
-// wave-per-row path: Conv1d 1x1 rows of <= 1024 columns whose split sums are
+// 16-B column groups per lane on the wave-per-row path (rows <= 256 columns:
+// the conditioning linears' 128).  Four (rows <= 1024) cost the whole kernel
+// 86 VGPRs, i.e. five waves per SIMD and 5/8 of the slab loads in flight; one
+// keeps it at 64 VGPRs, eight waves per SIMD (157.4 -> 136.8 us a step,
+// profiles/r05/wn_bwd_vec_ab.txt).
+constexpr int kWnWaveX4 = 1;
+// wave-per-row path: Conv1d 1x1 rows of <= 256 columns whose split sums are
 // at most one round of loads per lane
 __host__ __device__ inline bool wn_bwd_wave_rows(const vqx_wn_layer& l) {
   return l.kind == 0 && l.k == 1 && l.cin <= 64 * 4 * kWnWaveX4 && (l.cin / 4) * l.splits <= 64 * kWnNF;

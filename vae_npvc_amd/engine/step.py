@@ -140,7 +140,7 @@ def _wn_block_bytes(e):
     sl = e.get("slabs")
     es = sl.element_size() if sl is not None else 4
     b = cols * (e.get("splits", 1) * es + 8)
-    wave_rows = e["kind"] == 0 and e["k"] == 1 and e["cin"] <= 1024 and (e["cin"] // 4) * e.get("splits", 1) <= 256
+    wave_rows = e["kind"] == 0 and e["k"] == 1 and e["cin"] <= 256 and (e["cin"] // 4) * e.get("splits", 1) <= 256
     return 4 * b if wave_rows else b
 
 
