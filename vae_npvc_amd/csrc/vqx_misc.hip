@@ -350,6 +350,50 @@ __device__ __forceinline__ f32x4_t slab_sum(const void* slabs, int64_t p, int64_
   }
   return acc;
 }
+// slab_sum<true> (splits 0, 1, ... in order) of two column groups at once,
+// p0 and p1: twice the loads in flight.  Buffer loads through one descriptor
+// over the slabs (slab bytes < 2^31, caller-checked): a VGPR offset per
+// column and the split's offset in an SGPR, where flat loads would hold a
+// 64-bit address per load (84 VGPRs: five waves per SIMD instead of eight).
+__device__ __forceinline__ void slab_sum2_bf(const void* slabs, int sbytes, int64_t p0, int64_t p1, int64_t ss,
+                                             int splits, f32x4_t& a0, f32x4_t& a1) {
+  typedef int i32x2_t __attribute__((ext_vector_type(2)));
+  auto cvt = [](i32x2_t u) -> f32x4_t {
+    return {__uint_as_float((unsigned)u[0] << 16), __uint_as_float((unsigned)u[0] & 0xffff0000u),
+            __uint_as_float((unsigned)u[1] << 16), __uint_as_float((unsigned)u[1] & 0xffff0000u)};
+  };
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)slabs, (short)0, sbytes, 0x00020000);
+  const int v0 = (int)(p0 * 2), v1 = (int)(p1 * 2), sstep = (int)(ss * 2);
+  a0 = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  a1 = a0;
+  int sp = 0;
+  for (; sp + kWnNF - 1 < splits; sp += kWnNF) {
+    i32x2_t t0[kWnNF], t1[kWnNF];
+#pragma unroll
+    for (int u = 0; u < kWnNF; ++u) {
+      t0[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, v0, (sp + u) * sstep, 0);
+      t1[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, v1, (sp + u) * sstep, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kWnNF; ++u) {
+      a0 += cvt(t0[u]);
+      a1 += cvt(t1[u]);
+    }
+  }
+  i32x2_t t0[kWnNF], t1[kWnNF];
+#pragma unroll
+  for (int u = 0; u < kWnNF - 1; ++u)
+    if (sp + u < splits) {
+      t0[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, v0, (sp + u) * sstep, 0);
+      t1[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, v1, (sp + u) * sstep, 0);
+    }
+#pragma unroll
+  for (int u = 0; u < kWnNF - 1; ++u)
+    if (sp + u < splits) {
+      a0 += cvt(t0[u]);
+      a1 += cvt(t1[u]);
+    }
+}
 
 // Backward per weight-norm row o.  slabs[s][o][x] with x = j*cin+ci (Conv1d,
 // row co) or x = j'*cout+co (ConvT, row ci); dW of the effective conv.
@@ -530,17 +574,8 @@ __global__ __launch_bounds__(kWnThreads) void wn_bwd_kernel(const vqx_wn_layer* 
   const int G = nx4 >= (int)blockDim.x ? 1 : min(splits, (int)blockDim.x / nx4);
   const int gidx = threadIdx.x / nx4;  // split group (G == 1: every thread is group 0)
   f32x4_t* part = (f32x4_t*)dw;        // [G][nx4] partials (G > 1 only: nx4 * G <= kWnThreads -> <= 16 KiB)
-  // G == 1: x4 = t, t + 256, ...;  G > 1: the one group x4 = t % nx4 (threads with gidx >= G idle)
-  const int x4_0 = G == 1 ? (int)threadIdx.x : ((int)threadIdx.x % nx4 + (gidx < G ? 0 : nx4));
-  for (int x4 = x4_0; x4 < nx4; x4 += (G == 1 ? (int)blockDim.x : nx4)) {
-    const int64_t p = srow + 4 * x4;
-    const int sp0 = G > 1 ? gidx : 0, step = G > 1 ? G : 1;
-    const f32x4_t sum = sbf ? slab_sum<true>(l.slabs, p, slab_stride, sp0, step, splits)
-                            : slab_sum<false>(l.slabs, p, slab_stride, sp0, step, splits);
-    if (G > 1) {
-      part[gidx * nx4 + x4] = sum;
-      continue;
-    }
+  // slab column x -> dw[v index] (4 consecutive columns share the mapping)
+  auto scatter = [&](int x4, const f32x4_t& sum) {
     const int x = 4 * x4;
     if (rsm) {  // slab col x = m*S*C + q*C + c -> v index c*K + S*(m-1) + q + pad (4 c's share m, q)
       const int m = x / SC, rem = x - m * SC, q = rem / other, c = rem - q * other;
@@ -549,13 +584,37 @@ __global__ __launch_bounds__(kWnThreads) void wn_bwd_kernel(const vqx_wn_layer* 
 #pragma unroll
         for (int e = 0; e < 4; ++e) dw[(c + e) * K + j] = sum[e];
       }
-      continue;
+      return;
     }
     // slab col x = j*other + c  -> v index c*K + (kind==0 ? j : K-1-j)
     const int j = x / other, c = x - j * other;
     const int jj = l.kind == 0 ? j : K - 1 - j;
 #pragma unroll
     for (int e = 0; e < 4; ++e) dw[(c + e) * K + jj] = sum[e];
+  };
+  const int64_t sbytes = (int64_t)splits * slab_stride * 2;
+  if (G == 1 && sbf && sbytes < ((int64_t)1 << 31)) {
+    // bf16 slabs: column groups x4 and x4 + 256 summed together (the 3-tap
+    // rows have 384-768 groups and 4-8 splits: one pass of 8-16 loads)
+    for (int x4 = threadIdx.x; x4 < nx4; x4 += 2 * kWnThreads) {
+      const int x4b = x4 + kWnThreads;
+      const bool hb = x4b < nx4;
+      f32x4_t s0, s1;
+      slab_sum2_bf(l.slabs, (int)sbytes, srow + 4 * x4, srow + 4 * (hb ? x4b : x4), slab_stride, splits, s0, s1);
+      scatter(x4, s0);
+      if (hb) scatter(x4b, s1);
+    }
+  } else {
+    // G == 1: x4 = t, t + 256, ...;  G > 1: the one group x4 = t % nx4 (threads with gidx >= G idle)
+    const int x4_0 = G == 1 ? (int)threadIdx.x : ((int)threadIdx.x % nx4 + (gidx < G ? 0 : nx4));
+    for (int x4 = x4_0; x4 < nx4; x4 += (G == 1 ? (int)blockDim.x : nx4)) {
+      const int64_t p = srow + 4 * x4;
+      const int sp0 = G > 1 ? gidx : 0, step = G > 1 ? G : 1;
+      const f32x4_t sum = sbf ? slab_sum<true>(l.slabs, p, slab_stride, sp0, step, splits)
+                              : slab_sum<false>(l.slabs, p, slab_stride, sp0, step, splits);
+      if (G > 1) part[gidx * nx4 + x4] = sum;
+      else scatter(x4, sum);
+    }
   }
   if (G > 1) {  // add the split groups' partials in group order, then scatter as above
     __syncthreads();
@@ -564,22 +623,7 @@ __global__ __launch_bounds__(kWnThreads) void wn_bwd_kernel(const vqx_wn_layer* 
     if (x4 < nx4)
       for (int g = 0; g < G; ++g) sum += part[g * nx4 + x4];
     __syncthreads();  // dw doubles as the partial buffer
-    if (x4 < nx4) {
-      const int x = 4 * x4;
-      if (rsm) {
-        const int m = x / SC, rem = x - m * SC, q = rem / other, c = rem - q * other;
-        const int j = S * (m - 1) + q + l.pad;
-        if (j >= 0 && j < K) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) dw[(c + e) * K + j] = sum[e];
-        }
-      } else {
-        const int j = x / other, c = x - j * other;
-        const int jj = l.kind == 0 ? j : K - 1 - j;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) dw[(c + e) * K + jj] = sum[e];
-      }
-    }
+    if (x4 < nx4) scatter(x4, sum);
   }
   __syncthreads();
   float q2 = 0.f;
