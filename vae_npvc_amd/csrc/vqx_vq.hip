@@ -45,8 +45,11 @@ constexpr int vq_stage() { return vq_step_bytes<D>() / 16 / VQ_THREADS; }  // 16
 // EMA statistics (vq_stats_kernel): frames per chunk and the per-code sum
 // slabs [chunks][K][D] + counts [chunks][K] that vq_stats_reduce_kernel sums
 // in chunk order.
+#ifndef VQX_VQ_STATS_DSL_MAX  // widest dim slice (lab builds narrow it: more workgroups per chunk)
+#define VQX_VQ_STATS_DSL_MAX 32
+#endif
 __host__ __device__ constexpr int vq_stats_dsl(int K) {  // dims per LDS slice: K * (dsl + 1) * 4 B + ~10 KiB <= 64 KiB
-  int d = 32;  // <= 32: a thread holds VQ_CHUNK * dsl / 1024 sorted rows in registers
+  int d = VQX_VQ_STATS_DSL_MAX;  // <= 32: a thread holds VQ_CHUNK * dsl / 1024 sorted rows in registers
   while (d > 4 && K * (d + 1) > 13824) d >>= 1;
   return d;
 }
