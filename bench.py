@@ -61,6 +61,8 @@ def parse():
                          "the cost of co-resident work such as RCCL's all-reduce kernels")
     ap.add_argument("--grad-sync", default="overlap", choices=["overlap", "end"],
                     help="N>1: gradient all-reduces beside the backward (default) or all after it")
+    ap.add_argument("--no-read-loss", dest="read_loss", action="store_false",
+                    help="skip the second timed loop that reads loss_detail every step (ms_per_step_read_loss)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 process group (nccl = RCCL; gloo lets tests run several ranks on one GPU)")
     return ap.parse_args()
@@ -157,6 +159,34 @@ def time_fp32(cfg, steps, dev):
     flops = FLOP_PER_FRAME * B_PER_GPU * T_FRAMES
     return {"value": round(B_PER_GPU * T_FRAMES / dt, 1), "unit": "mel-frames/s", "ms_per_step": round(1e3 * dt, 3),
             "steps": steps, "dtype": "fp32", "step_mfma_frac": round(flops / dt / PEAK_F32, 4)}
+
+
+def time_read_loss(tr, xs, ys, steps, world):
+    """ms per step of the timed loop with the step's loss dict read on the host
+    after every step, as the reference's training loop does
+    (/root/reference/vae_npvc/bin/train.py:128-132: train_log[key].append(val)
+    for every key, every iteration); max over ranks."""
+    n = len(xs)
+    for i in range(2):
+        dict(tr.train_step((xs[i % n], ys[i % n]))[1])
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    log = {}
+    t0 = time.perf_counter()
+    for i in range(steps):
+        _, det = tr.train_step((xs[i % n], ys[i % n]))
+        for k, v in det.items():
+            log.setdefault(k, []).append(v)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=torch.device("cuda", torch.cuda.current_device()))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+    return 1e3 * el / steps
 
 
 def committed_traffic(symbol):
@@ -256,6 +286,10 @@ def main():
     if probe is not None:
         probe.select(None)
     elapsed = t1 - t0
+    # the same loop as a recipe runs it: the reference's bin/train.py:128-132
+    # appends every loss_detail value every iteration, so each step ends in a
+    # host read of the step's statistics (one device sync per step)
+    read_ms = time_read_loss(tr, xs, ys, a.steps, world) if a.read_loss else None
     comm_out = None
     if comm is not None:
         comm.timing = False
@@ -306,6 +340,8 @@ def main():
         "metric": "mel-frames/sec/GPU VQ-VAE train step (80-dim mel, batch=64x256f) at 1/2/4/8 GPUs",
         "value": round(value, 1), "unit": "mel-frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "ms_per_step_read_loss": None if read_ms is None else round(read_ms, 3),
+        "read_loss_overhead": None if read_ms is None else round(read_ms / ms - 1.0, 4),
         "dtype": a.dtype, "data": "synthetic (N(0,1) 80-mel, random speaker ids; seeded random-init weights)",
         "config": {"workload": f"{a.config} VQ-VAE (K={cfg['z_num']}, {mel}-mel), {B_PER_GPU}x{T_FRAMES} frames per GPU",
                    "global_batch": B_PER_GPU * world, "seq_len": T_FRAMES, "parallelism": f"dp{world}"},

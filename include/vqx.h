@@ -167,9 +167,26 @@ typedef struct vqx_wgrad_args {
                          rounded once to bf16, half the slab bytes written here and read by
                          vqx_weight_norm_bwd, which sums them in fp32 */
   int32_t kernel_policy; /* VQX_POLICY_* (ABI 122); IM2COL: no tap-reuse weight-gradient kernel */
+  /* In-launch ordered split-K reduction (ABI 127, optional: NULL = off).  With
+   * fixup_dw set, the split that finishes an output tile last (one agent-scope
+   * counter per tile) sums every split's slab of that tile in split order
+   * 0, 1, ... in fp32 -- the order vqx_weight_norm_bwd sums slabs -- and
+   * stores the fp32 weight gradient fixup_dw [r_dim][ntaps*c_dim]; a
+   * weight-norm backward table entry then reads it as one fp32 "slab"
+   * (splits 1), bit for bit the gradient it would have formed from the
+   * slabs.  The slabs are still written (write-through, for the last split to
+   * read).  fixup_counters: vqx_wgrad_tiles(...) uint32 counters, zero before
+   * the first call and left zero by every call.  Needs the 3-tap tap-reuse
+   * weight-gradient kernel and bf16 slabs (vqx_wgrad_fixup_ok). */
+  float* fixup_dw;
+  uint32_t* fixup_counters;
 } vqx_wgrad_args;
 
 int vqx_conv1d_wgrad(const vqx_wgrad_args* a, vqx_stream_t stream);
+/* *ok = 1 when a weight gradient of this shape takes the in-launch split-K
+ * reduction (fixup_dw), else 0 (ABI 127). */
+int vqx_wgrad_fixup_ok(int64_t n_rows, int32_t T, int32_t r_dim, int32_t c_dim, int32_t ntaps, int32_t pad, int32_t dil,
+                       int32_t dtype, int32_t slab_dtype, int32_t q_prologue, int32_t policy, int32_t* ok);
 
 /*
  * One layer's data gradient (d, as vqx_conv1d_dgrad) and weight gradient (w,
@@ -451,7 +468,8 @@ int vqx_embedding_bwd(const float* dout, const int64_t* ids, int32_t B, int32_t 
 /* The dense weight gradient in one pass (ABI 126): every row r < n_rows of
  * dweight is written, dweight[r] (+)= sum over b with ids[b] == r of dout[b]
  * in batch order (0 for ids absent from the batch; accumulate = 1 adds).  No
- * zero-fill launch before it.  B <= 1024. */
+ * zero-fill launch before it.  Any B (round 6): ids are staged 1024 at a
+ * time, each chunk's sum added to the row in chunk order. */
 int vqx_embedding_bwd_rows(const float* dout, const int64_t* ids, int32_t B, int32_t D, int32_t n_rows,
                            float* dweight, int32_t accumulate, vqx_stream_t stream);
 
@@ -522,8 +540,9 @@ int vqx_adam_step(float* p, const float* g, float* m, float* v, int64_t n, const
  * parameters; kind 1 (ConvT) rows get their norms, to be packed by
  * vqx_weight_norm_fwd_flags(VQX_WNF_NORMS_READY).  segs: (offset, length)
  * int64 pairs covering every other element of p (host and device copies);
- * rows + segs must cover [0, n) exactly.  The update of every element is
- * adam_step's, bit for bit.  At most 128 layers and 128 segments. */
+ * rows + segs must cover [0, n) exactly: the host rejects overlapping ranges
+ * (round 6) and p, g, m, v that are not 16-B aligned.  The update of every
+ * element is adam_step's, bit for bit.  At most 128 layers and 128 segments. */
 int vqx_adam_step_wn(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper,
                      const float* sumsq, float max_norm, const vqx_wn_layer* rows_host,
                      const vqx_wn_layer* rows_dev, int32_t n_layers, const int64_t* segs_host,
@@ -628,7 +647,7 @@ int vqx_stream_create_cu_mask(int32_t reserve_cus, vqx_stream_t* out, int32_t* c
 int vqx_stream_destroy(vqx_stream_t stream);
 
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
-#define VQX_ABI_VERSION 126
+#define VQX_ABI_VERSION 127
 int vqx_version(void);
 
 #ifdef __cplusplus

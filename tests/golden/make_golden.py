@@ -29,6 +29,9 @@ stored):
                           update at step 6
   * step_vcc20_z*         3 steps at codebook width z_dim 64 / 256, EMA and
                           straight-through quantizers (--only-zdim)
+  * encode_<cfg>          Model.encode ids + top-2 gaps and Model.decode of
+                          them, eval mode, odd lengths (--only-encode), the
+                          inference path of bin/extract_bnf.py (§8f row 3)
   * step_vcc20_multi*     3 steps of the general Encoder/Decoder topology
                           (two resolution stages with strided resampling
                           convs, dilation 2**j, stack_layers 2, decoder
@@ -206,6 +209,46 @@ def vq_fixture(K, N_B, N_T, seed, out_prefix):
     print(f"[golden] {out_prefix}: loss={meta['enc_loss']:.6f} detail={meta['detail']} min_gap={meta['min_gap']:.3g}")
 
 
+def encode_fixture(name, wseed, eseed, bseed, shapes, out_prefix):
+    """Inference: the reference's Model.encode
+    (vqvae.py:45-52 -> layers_vq.py:236-252, the path of bin/extract_bnf.py:
+    47-69) in eval mode on a trained-shape codebook, at odd utterance lengths:
+    the ids, the top-2 relative distance gap of every frame (computed from the
+    reference encoder's z with the reference's distance formula), and the
+    reference's Model.decode of those ids (vqvae.py:55-60)."""
+    cfg = load_cfg(name)
+    sd = seeded_state_dict(cfg, wseed)
+    rng = np.random.Generator(np.random.PCG64(eseed))
+    sd["quantizer.emb_init"] = torch.tensor(True)
+    sd["quantizer.embeddings"] = torch.from_numpy(
+        (rng.standard_normal((cfg["z_num"], cfg["z_dim"])) * 0.3).astype(np.float32))
+    m = ref_model(cfg, sd)
+    m.eval()
+    arrays, meta = {}, dict(config=name, wseed=wseed, eseed=eseed, bseed=bseed, shapes=[list(s) for s in shapes],
+                            cases=[])
+    with torch.no_grad():
+        for i, (B, T) in enumerate(shapes):
+            x, y = seeded_batch(cfg, B, T, bseed + i)
+            ids = m.encode(x)
+            z = m.encoder(x)
+            zf = z.transpose(1, 2).contiguous().view(-1, z.shape[1])
+            E = m.quantizer.embeddings
+            dist = (torch.sum(zf.pow(2), dim=1, keepdim=True) + torch.sum(E.pow(2), dim=1)) - 2 * torch.matmul(zf, E.t())
+            top2 = torch.topk(dist, 2, dim=1, largest=False).values
+            gap = (top2[:, 1] - top2[:, 0]) / top2[:, 1].abs().clamp_min(1e-30)
+            assert torch.equal(torch.argmin(dist, dim=1), ids.reshape(-1))
+            xhat = m.decode((ids, y))
+            arrays[f"ids{i}"] = ids.reshape(-1).numpy().astype(np.int16)
+            arrays[f"gap{i}"] = gap.numpy().astype(np.float32)
+            arrays[f"xhat_head{i}"] = xhat.reshape(-1)[:256].numpy().astype(np.float32)
+            meta["cases"].append(dict(B=B, T=T, xhat=summarize(xhat), n_gap_lt_1e4=int((gap < 1e-4).sum()),
+                                      min_gap=float(gap.min())))
+    np.savez_compressed(HERE / f"{out_prefix}.npz", **arrays)
+    json.dump(meta, open(HERE / f"{out_prefix}.json", "w"), indent=1)
+    print(f"[golden] {out_prefix}: " + ", ".join(f"{c['B']}x{c['T']} min_gap={c['min_gap']:.3g} "
+                                                 f"<1e-4: {c['n_gap_lt_1e4']}" for c in meta["cases"]))
+
+
 def vq_tile_fixture(seed, out_prefix):
     """N < K: init_emb and update_emb tile z with N(0, (0.01/sqrt(D))^2) noise."""
     from vae_npvc.model.layers_vq import EMAVectorQuantizer
@@ -283,6 +326,11 @@ if __name__ == "__main__":
     if "--only-big" in sys.argv:  # config 3's data-parallel global batch (8 x 64 x 256)
         step_fixture("vcc20", B=512, T=256, steps=2, wseed=1004, bseed=2004, tseed=3004, nseed=4004,
                      out_prefix="full_step_vcc20_b512", compact=True)
+        sys.exit(0)
+    if "--only-encode" in sys.argv:  # §8f row 3: Model.encode / decode in eval mode (round 6)
+        for i, name in enumerate(CFGS):
+            encode_fixture(name, wseed=1601 + i, eseed=1701 + i, bseed=1801 + 10 * i,
+                           shapes=[(2, 333), (1, 129), (3, 97)], out_prefix=f"encode_{name}")
         sys.exit(0)
     if "--only-plain" in sys.argv:  # just the §8f row-1 fixtures
         for i, name in enumerate(VARIANTS):

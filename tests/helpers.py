@@ -115,3 +115,32 @@ def grad_errors(grads, ref):
         g = grads[n].detach().double().cpu()
         out.append((float((g - r).norm() / r.norm().clamp_min(1e-30)), n))
     return sorted(out)
+
+
+NEAR_TIE = 1e-4  # a frame's top-2 relative distance gap below this is a near-tie (the training tests' bar)
+
+
+def oracle_encode_gaps(orc, x):
+    """(ids, top-2 relative gaps) of the oracle's Model.encode on x: the
+    near-tie measure of the golden fixtures (make_golden.py Recorder), per frame
+    in (utterance, time) order."""
+    z = orc.encoder(x)
+    zf = z.transpose(1, 2).contiguous().view(-1, z.shape[1])
+    if orc.use_ema:
+        E = orc.embeddings
+    else:
+        E = orc._plain_codebook(in_place=False)
+        if orc.normalize:
+            zf = zf / zf.norm(dim=1, keepdim=True)
+    dist = orc.distances(zf, E)
+    top2 = torch.topk(dist, 2, dim=1, largest=False).values
+    gap = (top2[:, 1] - top2[:, 0]) / top2[:, 1].abs().clamp_min(1e-30)
+    return torch.argmin(dist, dim=1).numpy(), gap.numpy()
+
+
+def assert_ids_near_tie_exact(got, want, gap, what=""):
+    """Every id that differs from the reference's sits at a reference near-tie."""
+    got, want, gap = np.asarray(got).reshape(-1), np.asarray(want).reshape(-1), np.asarray(gap).reshape(-1)
+    mism = got != want
+    assert (gap[mism] < NEAR_TIE).all(), (what, int(mism.sum()), gap[mism][gap[mism] >= NEAR_TIE][:8])
+    return int(mism.sum())

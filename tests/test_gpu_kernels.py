@@ -1103,6 +1103,47 @@ def test_embedding_bwd_rows(B, n_rows):
     assert torch.equal(got, ref + ref)
 
 
+@pytest.mark.parametrize("B,n_rows", [(2500, 7), (1025, 300)])
+def test_embedding_bwd_rows_above_one_lds_chunk(B, n_rows):
+    """Round 6: batches above the kernel's 1024 staged ids run in
+    LDS-sized chunks instead of being refused; each row = its ids' dout rows
+    summed (float64 reference, fp32 rounding bar)."""
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(B)
+    D = 128
+    dout = torch.randn(B, D, generator=g)
+    ids = torch.randint(0, n_rows, (B,), generator=g)
+    ref = torch.zeros(n_rows, D, dtype=torch.float64).index_add_(0, ids, dout.double())
+    got = torch.full((n_rows, D), float("nan"), device=DEV)
+    ops.embedding_bwd_rows(dout.to(DEV), ids.to(DEV), got)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(got.double().cpu(), ref, rtol=1e-5, atol=1e-4)
+
+
+def test_guard_canaries_catch_an_out_of_extent_write():
+    """vae_npvc_amd/debug.py: a kernel writing one row past a guarded buffer is
+    reported by the post-call check with the entry point and the buffer (host
+    extent checks off, so the write reaches the device), and a write inside
+    the buffer passes."""
+    from vae_npvc_amd import debug
+    ops = _ops()
+    gs = debug.GuardSet(DEV)
+    buf = gs.empty(64, 32, dtype=torch.float32, label="probe buffer")
+    other = gs.zeros(16, dtype=torch.float32, label="neighbour")
+    debug.install(gs)
+    try:
+        ops.zero_(buf)  # inside: passes the check
+        assert gs.checks >= 1
+        over = torch.as_strided(buf, (65, 32), (32, 1))  # one row into the tail guard
+        ops.set_debug_checks(False)
+        with pytest.raises(AssertionError, match=r"vqx_convert_2d.*probe buffer \(tail guard: 128 bytes"):
+            ops.convert_2d(None, over)
+        assert torch.equal(other.cpu(), torch.zeros(16))
+    finally:
+        debug.uninstall(gs)
+    assert not ops._debug
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("B,C,T,ldx", [(64, 80, 256, 80), (3, 80, 100, 128), (2, 7, 33, 7), (1, 80, 1, 80)])
 def test_logloss_matches_torch(dtype, B, C, T, ldx):
@@ -1312,3 +1353,46 @@ def test_gather_rows_host_indices_equal_device_indices(K, N):
     assert torch.equal(a, b)
     ref = torch.where((rows >= 0)[:, None], src.cpu()[rows.clamp_min(0)], torch.zeros(1))
     assert torch.equal(b.cpu(), ref)
+
+
+@pytest.mark.parametrize("r,c,shift,splits,B,T", [(512, 512, 1, 8, 8, 256), (512, 1024, -1, 4, 8, 256),
+                                                  (256, 512, 1, 5, 3, 128), (128, 64, -1, 3, 2, 64)])
+def test_wgrad_in_launch_split_k_reduction(r, c, shift, splits, B, T):
+    """vqx_wgrad_args.fixup_dw (ABI 127): the last split of each tile sums the
+    bf16 slabs of its tile in split order in fp32 inside the launch.  fixup_dw
+    equals that sum formed from the slabs afterwards (acc = 0, acc += slab s:
+    the weight-norm backward's order) bit for bit; the slabs equal those of a
+    call without the reduction; the tile counters are left zero, so a second
+    call (and the fused DGRAD + WGRAD launch) gives the same bits."""
+    ops = _ops()
+    from vae_npvc_amd import _lib as L
+    g = torch.Generator(device="cpu").manual_seed(r + c + splits)
+    N = B * T
+    p = torch.randn(N, r, generator=g).to(DEV, torch.bfloat16)
+    q = torch.randn(N, c, generator=g).to(DEV, torch.bfloat16)
+    assert ops.wgrad_fixup_ok(N, T, r, c, 3, 1, L.VQX_BF16, L.VQX_BF16)
+    assert not ops.wgrad_fixup_ok(N, T, r, c, 3, 1, L.VQX_BF16, L.VQX_F32)
+    kw = dict(T=T, r_dim=r, c_dim=c, ntaps=3, pad=1, shift_sign=shift, splits=splits)
+    ref_slabs = torch.empty(splits, r, 3 * c, device=DEV, dtype=torch.bfloat16)
+    ops.conv_wgrad(p, q, ref_slabs, **kw)
+    acc = torch.zeros(r, 3 * c, device=DEV)
+    for s in range(splits):
+        acc += ref_slabs[s].float()
+    cnt = torch.zeros(((r + 127) // 128) * (c // 64 + 1), device=DEV, dtype=torch.int32)
+    for it in range(2):
+        slabs = torch.full((splits, r, 3 * c), float("nan"), device=DEV, dtype=torch.bfloat16)
+        dw = torch.full((r, 3 * c), float("nan"), device=DEV)
+        ops.conv_wgrad(p, q, slabs, fixup_dw=dw, fixup_counters=cnt, **kw)
+        torch.cuda.synchronize()
+        assert torch.equal(slabs, ref_slabs), it
+        assert torch.equal(dw, acc), (it, float((dw - acc).abs().max()))
+        assert int(cnt.abs().sum()) == 0
+    # the fused DGRAD + WGRAD launch (3-tap interleaved kernel) takes the same path
+    if shift == 1:
+        wt = (torch.randn(r, c, 3, generator=g) / (3 * c) ** 0.5).to(DEV, torch.bfloat16)
+        dx = torch.empty(N, c, device=DEV, dtype=torch.bfloat16)
+        dw2 = torch.full((r, 3 * c), float("nan"), device=DEV)
+        fused = ops.conv_dgrad_wgrad(p, pack(wt), dx, dict(T=T, cin=r, cout=c, ntaps=3, pad=1), p, q, slabs,
+                                     dict(kw, fixup_dw=dw2, fixup_counters=cnt))
+        torch.cuda.synchronize()
+        assert torch.equal(dw2, acc) and int(cnt.abs().sum()) == 0, fused

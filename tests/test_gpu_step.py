@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 import torch
 
-from tests.helpers import cfg_of, load_fixture, make_trainer, relclose
+from tests.helpers import assert_ids_near_tie_exact, cfg_of, load_fixture, make_trainer, oracle_encode_gaps, relclose
 
 pytestmark = pytest.mark.gpu
 
@@ -369,8 +369,9 @@ def test_inference_encode_decode_match_oracle():
     x, y = seeded_batch(cfg, 1, 333, 7)  # odd utterance length, B=1 (decode.py path)
     with torch.no_grad():
         idx = m.encode(x.cuda()).cpu()
-        idx_ref = orc.encode(x)
-        assert (idx == idx_ref).float().mean() > 0.99
+        idx_ref, gap = oracle_encode_gaps(orc, x)
+        assert_ids_near_tie_exact(idx.numpy(), idx_ref, gap, "encode")  # every mismatch at an oracle near-tie
+        idx_ref = torch.from_numpy(idx_ref).view_as(idx)
         xo = m.decode((idx_ref.cuda(), y.cuda())).cpu()
         xr = orc.decode(idx_ref, y)
         assert ((xo - xr).norm() / xr.norm()) < 1e-4
@@ -586,3 +587,36 @@ def test_three_per_cu_1x1_policy_is_bit_identical(name):
     assert out[0][0] == out[1][0]
     assert torch.equal(out[0][1], out[1][1])
     assert torch.equal(out[0][2], out[1][2])
+
+
+@pytest.mark.parametrize("name,B,T", [("vcc20", 64, 256), ("aishell3", 4, 128), ("vcc20_multi", 4, 128)])
+def test_in_launch_split_k_reduction_is_bit_identical(name, B, T):
+    """EngineOptions.wgrad_fixup (round 6): the 3-tap layers' bf16 split-K
+    slabs summed inside the weight-gradient launch by each tile's last split
+    (ABI 127 fixup_dw), the weight-norm backward reading one fp32 gradient per
+    layer.  Over three bf16 steps (vcc20 at the bench's 64 x 256; aishell3;
+    the two-stage topology, whose strided stage convs keep the slabs) the
+    losses, gradients, parameters and both Adam moments equal the slab path
+    bit for bit, and the layers that took it are reported."""
+    from oracle.vqvae_cpu import seeded_batch
+    out = []
+    for fix in (True, False):
+        cfg = cfg_of(name, compute_dtype="bf16", engine={"wgrad_fixup": fix})
+        tr = make_trainer(cfg, 37)
+        eng = tr.engine
+        torch.manual_seed(8)
+        np.random.seed(8)
+        dets = []
+        for s in range(3):
+            dets.append(dict(tr.train_step(tuple(t.cuda() for t in seeded_batch(cfg, B, T, 70 + s)))[1]))
+            if s == 0:
+                g0 = eng.flat_g.clone()
+        torch.cuda.synchronize()
+        n_fix = len(eng._ws[(B, T, True)].fix)
+        out.append((dets, g0, eng.flat_p.clone(), eng.exp_avg.clone(), eng.exp_avg_sq.clone(), n_fix))
+    a, b = out
+    print(f"{name}: {a[5]} layers reduced in-launch")
+    assert a[5] > 0 and b[5] == 0
+    assert a[0] == b[0]
+    for i, (x, y) in enumerate(zip(a[1:5], b[1:5])):
+        assert torch.equal(x, y), i

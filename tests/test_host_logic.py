@@ -222,3 +222,40 @@ def test_no_weight_norm_convs_get_kaiming_init(name):
         checked += 1
     assert checked >= 10, checked
     assert not any(n.endswith("weight_v") for n, _ in m.named_parameters())
+
+
+def test_debug_extent_checks_refuse_short_buffers():
+    """ops.set_debug_checks: a pointer argument whose buffer is shorter than the
+    span the kernel would touch raises before any launch (host-side; CPU
+    tensors suffice, no library call is made)."""
+    from vae_npvc_amd import _lib as L
+    from vae_npvc_amd import ops
+    prev = ops.set_debug_checks(True)
+    try:
+        N, C = 256, 64
+        x, w = torch.empty(N, C), torch.empty(C, 3 * C)
+        ops.conv_args(x, w, torch.empty(N, C), T=128, cin=C, cout=C, ntaps=3, pad=1)  # exact sizes pass
+        with pytest.raises(L.VqxError, match="conv y"):
+            ops.conv_args(x, w, torch.empty(N - 1, C), T=128, cin=C, cout=C, ntaps=3, pad=1)
+        with pytest.raises(L.VqxError, match="conv colsum_part"):
+            ops.conv_args(x, w, torch.empty(N, C), T=128, cin=C, cout=C, ntaps=3, pad=1,
+                          colsum=torch.empty(N // 128 - 1, C))
+        big = torch.empty(N, 2 * C)  # a column view: its rows stride over the whole buffer
+        ops.conv_args(x, w, big[:, C:], T=128, cin=C, cout=C, ntaps=3, pad=1)
+        with pytest.raises(L.VqxError, match="conv y2"):
+            ops.conv_args(x, w, big[:, :C], T=128, cin=C, cout=C, ntaps=3, pad=1, y2=big[1:, C:])
+        with pytest.raises(L.VqxError, match="wgrad slabs"):
+            ops.wgrad_args(x, x, torch.empty(4, C, 3 * C - 1), T=128, r_dim=C, c_dim=C, ntaps=3, pad=1, splits=4)
+        # the guarded allocations' logical end (debug.py): the tail guard is not the buffer's
+        raw = torch.empty(4096 + 4 * N + 4096, dtype=torch.uint8)
+        ops._logical_end[raw.untyped_storage().data_ptr()] = 4096 + 4 * N
+        try:
+            t = raw[4096:4096 + 4 * N].view(torch.float32)
+            ops._span(t, N, "guarded")
+            with pytest.raises(L.VqxError, match="guarded"):
+                ops._span(t, N + 1, "guarded")
+        finally:
+            ops._logical_end.pop(raw.untyped_storage().data_ptr(), None)
+    finally:
+        ops.set_debug_checks(prev)
+    ops.conv_args(x, w, torch.empty(N - 1, C), T=128, cin=C, cout=C, ntaps=3, pad=1)  # off: no check

@@ -15,7 +15,7 @@ from pathlib import Path
 import torch  # noqa: F401  (loads the HIP runtime first; see module docstring)
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libvqx.so"
-ABI_VERSION = 126  # include/vqx.h VQX_ABI_VERSION
+ABI_VERSION = 127  # include/vqx.h VQX_ABI_VERSION
 
 VQX_F32, VQX_BF16 = 0, 1
 PRO_NONE, PRO_LRELU, PRO_RELU, PRO_SCALE_RELU = 0, 1, 2, 3
@@ -49,7 +49,7 @@ class WgradArgs(ctypes.Structure):
         ("r_dim", c_int32), ("c_dim", c_int32), ("ntaps", c_int32), ("pad", c_int32),
         ("shift_sign", c_int32), ("ldp", c_int32), ("ldq", c_int32), ("dtype", c_int32),
         ("q_prologue", c_int32), ("splits", c_int32), ("pro_scale", c_float), ("dil", c_int32),
-        ("slab_dtype", c_int32), ("kernel_policy", c_int32),
+        ("slab_dtype", c_int32), ("kernel_policy", c_int32), ("fixup_dw", c_void_p), ("fixup_counters", c_void_p),
     ]
 
 
@@ -135,6 +135,8 @@ _SIGS = {
                                    c_void_p, c_void_p],
     "vqx_wgrad_tiles": [c_int64, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
                         ctypes.POINTER(c_int32)],
+    "vqx_wgrad_fixup_ok": [c_int64, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
+                           c_int32, ctypes.POINTER(c_int32)],
     "vqx_vq_normalize": [c_void_p, c_int64, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p, c_void_p],
     "vqx_vq_perplexity": [c_void_p, c_int32, c_int64, c_void_p, c_void_p],
@@ -192,12 +194,23 @@ def load(path: os.PathLike = None):
     return lib
 
 
+_post_call = None  # debug.py's guard check (EngineOptions.debug_checks); None in normal runs
+
+
+def set_post_call(fn):
+    """fn(name) after every successful entry point (None removes it)."""
+    global _post_call
+    _post_call = fn
+
+
 def call(name: str, *args):
     """Invoke an entry point and turn a non-zero status into VqxError."""
     lib = load()
     rc = getattr(lib, name)(*args)
     if rc != 0:
         raise VqxError(f"{name} failed ({rc}): {lib.vqx_last_error().decode(errors='replace')}")
+    if _post_call is not None:
+        _post_call(name)
     return rc
 
 

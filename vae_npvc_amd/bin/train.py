@@ -46,6 +46,9 @@ from torch.utils.data import DataLoader
 from ..dataset.sampler import ShardSampler
 
 
+DIST_TIMEOUT_S = 7200  # multi-rank default: rank 0's checkpoint validation while the others wait
+
+
 def setup_distributed(backend=None, timeout_s=None):
     """Initialise the process group from torchrun's environment (before any
     other GPU call) and select GPU LOCAL_RANK.  Returns (world, rank, backend)
@@ -112,7 +115,10 @@ def train(args):
     config = yaml.safe_load(open(args.config))  # host only: the process group comes before any GPU call
     # rank 0 alone validates at a checkpoint while the others wait in a barrier:
     # a long validation set needs more than torch's default collective timeout
-    world, rank, backend = setup_distributed(getattr(args, "backend", None), config.get("dist_timeout_s"))
+    # (about 10 min for NCCL), so multi-rank runs default to DIST_TIMEOUT_S
+    # unless the config sets dist_timeout_s (null keeps torch's default)
+    timeout_s = config.get("dist_timeout_s", DIST_TIMEOUT_S if int(os.environ.get("WORLD_SIZE", "1")) > 1 else None)
+    world, rank, backend = setup_distributed(getattr(args, "backend", None), timeout_s)
     ddp = world > 1
     output_dir = args.output_dir
     checkpoint_path = args.checkpoint

@@ -205,6 +205,13 @@ static int wgrad_prepare(const vqx_wgrad_args* a, GemmParams& P, bool& gen) {
     P.tap_reuse = 1;
     P.tiles_n = a->c_dim / 64;
   }
+  if (a->fixup_dw) {  // in-launch ordered split-K reduction (ABI 127)
+    if (!P.tap_reuse || !P.slab_bf16) { set_error("vqx_conv1d_wgrad: fixup_dw needs the 3-tap tap-reuse kernel and bf16 slabs (vqx_wgrad_fixup_ok)"); return -1; }
+    if (!aligned16(a->fixup_dw) || !a->fixup_counters) { set_error("vqx_conv1d_wgrad: fixup_dw must be 16-B aligned, fixup_counters non-null"); return -1; }
+    if ((int64_t)a->splits * P.Mc * P.Nc * 2 > 0x7fffffffLL) { set_error("vqx_conv1d_wgrad: fixup slabs larger than 2 GiB"); return -1; }
+    P.fix_dw = a->fixup_dw;
+    P.fix_cnt = a->fixup_counters;
+  }
   return 0;
 }
 
@@ -271,6 +278,20 @@ extern "C" int vqx_wgrad_tiles(int64_t n_rows, int32_t T, int32_t r_dim, int32_t
   if (!gen && wgrad_tr_ok(n_rows, T, c_dim, ntaps, pad, dil > 0 ? dil : 1, bf16, q_prologue, policy))
     *tiles = tm * (c_dim / 64);
   else *tiles = tm * ((ntaps * c_dim + kBN - 1) / kBN);
+  return 0;
+}
+
+extern "C" int vqx_wgrad_fixup_ok(int64_t n_rows, int32_t T, int32_t r_dim, int32_t c_dim, int32_t ntaps, int32_t pad,
+                                  int32_t dil, int32_t dtype, int32_t slab_dtype, int32_t q_prologue, int32_t policy,
+                                  int32_t* ok) {
+  if (!ok || n_rows <= 0 || T <= 0 || r_dim <= 0 || c_dim <= 0 || ntaps < 1 || ntaps > 8) {
+    set_error("vqx_wgrad_fixup_ok: bad arguments");
+    return -1;
+  }
+  const bool bf16 = dtype == VQX_BF16;
+  const bool gen = (T % 64) != 0 || (n_rows % 64) != 0;
+  *ok = (bf16 && slab_dtype == VQX_BF16 && !gen &&
+         wgrad_tr_ok(n_rows, T, c_dim, ntaps, pad, dil > 0 ? dil : 1, bf16, q_prologue, policy)) ? 1 : 0;
   return 0;
 }
 

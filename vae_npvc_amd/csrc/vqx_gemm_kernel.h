@@ -94,6 +94,8 @@ struct GemmParams {
   const float* gn_tiles;  // GNADD: merge mean/rstd from these GNSTATS tiles (G = 1) and write gn_mr
   float gn_eps;
   int policy;      // host side: the call's kernel_policy (vqx_conv_args / vqx_wgrad_args)
+  float* fix_dw;           // WGRAD (tap reuse, bf16 slabs): in-launch split-K reduction target, or null
+  unsigned* fix_cnt;       // ... its per-tile arrival counters (left zero)
 };
 
 template <typename T> struct Cfg;
@@ -1526,6 +1528,86 @@ __global__ __launch_bounds__(512, 1) void conv_tr8_kernel(GemmParams P) {
 // shift.
 __device__ __forceinline__ int q_off128(int row, int ch) { return row * 128 + 16 * (ch ^ (((row >> 1) & 1) << 2)); }
 
+// In-launch ordered split-K reduction of one weight-gradient tile (ABI 127,
+// vqx_wgrad_args.fixup_dw).  Every split has stored its bf16 partial of the
+// tile write-through (sc1); each storing wave waits for its stores, the
+// workgroup barrier joins them, and one lane adds to the tile's agent-scope
+// counter.  The split whose add returns splits-1 is the last: it reads every
+// split's partial of the tile with sc1 loads (the hand-off of
+// MI355X_MICROARCH.md "inter-workgroup visibility", table row 1: write-through
+// 16-B stores, one counter add per storing workgroup, the last adder told by
+// the value its add returned, the other waves loading after a barrier),
+// sums them in split order 0, 1, ... in fp32 exactly as
+// vqx_weight_norm_bwd's slab_sum2_bf does (acc = 0, acc += split s), stores
+// the fp32 gradient and resets the counter for the next call.  No workgroup
+// waits for another, so the grid needs no co-residency.
+constexpr int kCpolSc1 = 16;  // buffer cache policy bit sc1 (gfx950)
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4_t bf16x4_lo(const u32x4_t& u) {
+  return f32x4_t{__uint_as_float(u[0] << 16), __uint_as_float(u[0] & 0xffff0000u), __uint_as_float(u[1] << 16),
+                 __uint_as_float(u[1] & 0xffff0000u)};
+}
+__device__ __forceinline__ f32x4_t bf16x4_hi(const u32x4_t& u) {
+  return f32x4_t{__uint_as_float(u[2] << 16), __uint_as_float(u[2] & 0xffff0000u), __uint_as_float(u[3] << 16),
+                 __uint_as_float(u[3] & 0xffff0000u)};
+}
+__device__ __forceinline__ void wgrad_tile_fixup(const GemmParams& P, int tmn, int r0, int c0,
+                                              __amdgpu_buffer_rsrc_t rsY, char* smem) {
+  constexpr int NT = 256;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores have left
+  __syncthreads();                                   // ... and every other wave's
+  int* flag = (int*)smem;
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(P.fix_cnt + tmn, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = (int)old;
+  }
+  __syncthreads();
+  if (*flag != P.splits - 1) return;  // uniform per workgroup
+  if (threadIdx.x == 0) __hip_atomic_store(P.fix_cnt + tmn, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int tid = threadIdx.x;
+  const int64_t ss2 = (int64_t)P.Mc * P.Nc * 2;  // bytes per split
+  const int S = P.splits;
+  // chunk (j, pass): row r0 + pass*32 + tid/8, columns j*cdim + c0 + (tid%8)*8 .. +7
+  // (the slab store's lane map); two chunks per round, all their splits' loads in flight
+  for (int it = 0; it < 12; it += 2) {
+    int64_t at[2];
+    bool ok[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = it + u, j = c >> 2, pass = c & 3;
+      const int r = r0 + pass * (NT / 8) + (tid >> 3), cc = c0 + (tid & 7) * 8;
+      ok[u] = r < P.Mc && cc < P.cdim;
+      at[u] = (int64_t)r * P.Nc + j * P.cdim + cc;
+    }
+    f32x4_t a0[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    f32x4_t a1[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    for (int s0 = 0; s0 < S; s0 += 8) {
+      u32x4_t v[2][8];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (ok[u] && s0 + k < S)
+            v[u][k] = __builtin_amdgcn_raw_buffer_load_b128(rsY, (int)(at[u] * 2), (int)((s0 + k) * ss2), kCpolSc1);
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (ok[u] && s0 + k < S) {
+            a0[u] += bf16x4_lo(v[u][k]);
+            a1[u] += bf16x4_hi(v[u][k]);
+          }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (ok[u]) {
+        float* o = P.fix_dw + at[u];
+        *(f32x4_t*)o = a0[u];
+        *(f32x4_t*)(o + 4) = a1[u];
+      }
+  }
+}
+
 // LDS bytes of wgrad_tr_body: two 25-KiB stages, at least the slab-store
 // staging (128 x 68 floats)
 __host__ __device__ constexpr int wgrad_tr_smem() { return 2 * 25600 > 128 * 68 * 4 ? 2 * 25600 : 128 * 68 * 4; }
@@ -1669,6 +1751,8 @@ __device__ __forceinline__ void wgrad_tr_body(const GemmParams& P, int bid, int 
   // slab store, one tap at a time through LDS: rows of 64 channels, 8 lanes x 8 floats each
   float* ep = (float*)smem;
   const int64_t slab0 = (int64_t)split * P.Mc * P.Nc;
+  const __amdgpu_buffer_rsrc_t rsY =
+      __builtin_amdgcn_make_buffer_rsrc(P.y, (short)0, (int)((int64_t)P.splits * P.Mc * P.Nc * 2), 0x00020000);
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     __syncthreads();
@@ -1688,7 +1772,11 @@ __device__ __forceinline__ void wgrad_tr_body(const GemmParams& P, int bid, int 
         const f32x4_t lo = *(const f32x4_t*)(ep + lr * EP_LD + lc);
         const f32x4_t hi = *(const f32x4_t*)(ep + lr * EP_LD + lc + 4);
         const int64_t at = slab0 + (int64_t)r * P.Nc + j * P.cdim + cc;
-        if (P.slab_bf16) {
+        if (P.slab_bf16 && P.fix_dw) {  // write-through (sc1): the tile's last split reads it in this launch
+          const u32x4_t u = {pack_bf16x2(lo[0], lo[1]), pack_bf16x2(lo[2], lo[3]), pack_bf16x2(hi[0], hi[1]),
+                             pack_bf16x2(hi[2], hi[3])};
+          __builtin_amdgcn_raw_buffer_store_b128(u, rsY, (int)(at * 2), 0, kCpolSc1);
+        } else if (P.slab_bf16) {
           const float v8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           st8<bf16_t>(P.y, at, v8);
         } else {
@@ -1699,6 +1787,7 @@ __device__ __forceinline__ void wgrad_tr_body(const GemmParams& P, int bid, int 
       }
     }
   }
+  if (P.fix_dw) wgrad_tile_fixup(P, tmn, r0, c0, rsY, smem);
 }
 
 template <int EK>

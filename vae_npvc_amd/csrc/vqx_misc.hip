@@ -1549,14 +1549,20 @@ __global__ __launch_bounds__(256) void embedding_bwd_rows_kernel(const float* __
                                                                  float* __restrict__ dw, int accumulate) {
   __shared__ int sid[kEmbMaxB];
   const int r = blockIdx.x;
-  for (int q = threadIdx.x; q < B; q += blockDim.x) sid[q] = (int)ids[q];
-  __syncthreads();
-  for (int d = threadIdx.x; d < D; d += blockDim.x) {
-    float s = 0.f;
-    for (int q = 0; q < B; ++q)
-      if (sid[q] == r) s += dout[(int64_t)q * D + d];
-    float* o = dw + (int64_t)r * D + d;
-    *o = accumulate ? *o + s : s;
+  // batches above kEmbMaxB ids run in LDS-sized chunks (each chunk's sum added
+  // to the row in chunk order; one chunk for B <= kEmbMaxB, as before)
+  for (int q0 = 0; q0 < B; q0 += kEmbMaxB) {
+    const int nq = min(kEmbMaxB, B - q0);
+    __syncthreads();
+    for (int q = threadIdx.x; q < nq; q += blockDim.x) sid[q] = (int)ids[q0 + q];
+    __syncthreads();
+    for (int d = threadIdx.x; d < D; d += blockDim.x) {
+      float s = 0.f;
+      for (int q = 0; q < nq; ++q)
+        if (sid[q] == r) s += dout[(int64_t)(q0 + q) * D + d];
+      float* o = dw + (int64_t)r * D + d;
+      *o = (accumulate || q0 > 0) ? *o + s : s;
+    }
   }
 }
 
@@ -2934,8 +2940,8 @@ extern "C" int vqx_embedding_bwd(const float* dout, const int64_t* ids, int32_t 
 
 extern "C" int vqx_embedding_bwd_rows(const float* dout, const int64_t* ids, int32_t B, int32_t D, int32_t n_rows,
                                       float* dweight, int32_t accumulate, vqx_stream_t stream) {
-  if (!dout || !ids || !dweight || B < 1 || B > kEmbMaxB || D < 1 || n_rows < 1) {
-    set_error("vqx_embedding_bwd_rows: bad arguments (1 <= B <= %d)", kEmbMaxB);
+  if (!dout || !ids || !dweight || B < 1 || D < 1 || n_rows < 1) {
+    set_error("vqx_embedding_bwd_rows: bad arguments");
     return -1;
   }
   hipLaunchKernelGGL(embedding_bwd_rows_kernel, dim3(n_rows), dim3(D >= 256 ? 256 : ((D + 63) / 64) * 64), 0,
@@ -2988,11 +2994,21 @@ extern "C" int vqx_adam_step_wn(float* p, const float* g, float* m, float* v, in
     set_error("vqx_adam_step_wn: bad arguments (at most %d layers and %d segments)", kAdamMaxL, kAdamMaxS);
     return -1;
   }
+  // the row path moves 16-B vectors of p, g, m, v (the segment path checks its own alignment)
+  if ((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m) | ((uintptr_t)v)) & 15) {
+    set_error("vqx_adam_step_wn: p, g, m and v must be 16-B aligned");
+    return -1;
+  }
   AdamWnPlan P;
   P.n_layers = n_layers;
   P.n_segs = n_segs;
   P.row_off[0] = 0;
   int64_t covered = 0;
+  // every interval the launch updates (v and g rows of each layer, the flat
+  // segments), to check that they do not overlap (with the coverage count
+  // below: exactly once each of the n elements)
+  int64_t iv[2 * (2 * kAdamMaxL + kAdamMaxS)];
+  int niv = 0;
   for (int i = 0; i < n_layers; ++i) {
     const vqx_wn_layer& l = rows_host[i];
     const bool k3 = l.kind == 0 && l.k > 1;
@@ -3008,6 +3024,8 @@ extern "C" int vqx_adam_step_wn(float* p, const float* g, float* m, float* v, in
     if (!ok) { set_error("vqx_adam_step_wn: layer %d cannot take the fused weight-norm preparation", i); return -1; }
     P.row_off[i + 1] = P.row_off[i] + adam_wn_units(l);
     covered += (int64_t)rows * cols + rows;
+    iv[2 * niv] = vo; iv[2 * niv + 1] = vo + (int64_t)rows * cols; ++niv;
+    iv[2 * niv] = go; iv[2 * niv + 1] = go + rows; ++niv;
   }
   P.seg_blk[0] = 0;
   for (int i = 0; i < n_segs; ++i) {
@@ -3015,7 +3033,20 @@ extern "C" int vqx_adam_step_wn(float* p, const float* g, float* m, float* v, in
     if (s0 < 0 || len < 0 || s0 + len > n) { set_error("vqx_adam_step_wn: segment %d out of range", i); return -1; }
     P.seg_blk[i + 1] = P.seg_blk[i] + (int)((len + 4095) / 4096);
     covered += len;
+    if (len > 0) { iv[2 * niv] = s0; iv[2 * niv + 1] = s0 + len; ++niv; }
   }
+  // insertion sort by start (at most 2 * 128 + 128 intervals), then adjacent overlap test
+  for (int i = 1; i < niv; ++i)
+    for (int j = i; j > 0 && iv[2 * j] < iv[2 * (j - 1)]; --j) {
+      const int64_t a0 = iv[2 * j], a1 = iv[2 * j + 1];
+      iv[2 * j] = iv[2 * (j - 1)]; iv[2 * j + 1] = iv[2 * (j - 1) + 1];
+      iv[2 * (j - 1)] = a0; iv[2 * (j - 1) + 1] = a1;
+    }
+  for (int i = 1; i < niv; ++i)
+    if (iv[2 * i] < iv[2 * (i - 1) + 1]) {
+      set_error("vqx_adam_step_wn: updated ranges overlap at element %lld", (long long)iv[2 * i]);
+      return -1;
+    }
   if (covered != n) { set_error("vqx_adam_step_wn: rows + segments cover %lld of %lld elements", (long long)covered, (long long)n); return -1; }
   const int grid = P.row_off[n_layers] + P.seg_blk[n_segs];
   if (grid > 0)

@@ -70,6 +70,8 @@ class ConvLayer:
     norm: torch.Tensor = None   # ||v_o||
     slab: torch.Tensor = None   # wgrad partials [splits, rows, cols]
     splits: int = 1
+    fix_dw: torch.Tensor = None   # wgrad_fixup: the in-launch reduced fp32 weight gradient [rows, cols]
+    fix_cnt: torch.Tensor = None  # ... and its per-tile arrival counters
     btile: torch.Tensor = None  # kind 4: bias tiled over the s folded frames [s*cout]
 
     @property
@@ -187,7 +189,16 @@ class EngineOptions:
                        ConvTranspose layers
       kernel_policy    include/vqx.h VQX_POLICY_* of every conv GEMM call (5:
                        the 1x1 layers on the two-workgroups-per-CU kernels
-                       of round 4; automatic: three per CU)"""
+                       of round 4; automatic: three per CU)
+      wgrad_fixup      the 3-tap layers' split-K weight-gradient slabs summed
+                       inside the GEMM launch by the last split of each tile
+                       (vqx_wgrad_args.fixup_dw, ABI 127): the weight-norm
+                       backward then reads one fp32 gradient instead of the
+                       bf16 slabs; bit-identical results
+      debug_checks     out-of-extent write detection (vae_npvc_amd/debug.py):
+                       every engine buffer between guard canaries checked
+                       after every libvqx call, and host extent checks of
+                       every pointer argument; slow, for audits only"""
     fuse_gn: bool = True
     enc_gn_finalize: bool = False
     side_stream: bool = False
@@ -203,6 +214,8 @@ class EngineOptions:
     fuse_grad_norm: bool = True
     fuse_adam_wn: bool = True
     kernel_policy: int = 0
+    debug_checks: bool = False
+    wgrad_fixup: bool = False
 
 
 class _Stage:
@@ -215,7 +228,7 @@ class Workspace:
     def __init__(self, eng, B, T, train=True):
         d, cd, dev = eng.dims, eng.cd, eng.device
         self.B, self.T, self.N = B, T, B * T
-        e = lambda *s, dt=cd: torch.empty(*s, device=dev, dtype=dt)  # noqa: E731
+        e = lambda *s, dt=cd: eng._empty(*s, dtype=dt)  # noqa: E731
         Z, S, Fo, mel, K = d["Z"], d["S"], d["F"], d["mel"], d["K"]
         fuse_opt = eng.opt.fuse_gn
         self.x = e(self.N, mel)
@@ -298,7 +311,7 @@ class Workspace:
         self.xhat = e(self.N, Fo, dt=F32)
         self.xhat_nct = e(B, Fo, T, dt=F32)
         # scalars: 0 x_loss, 1 sqerr, 4..7 EMA diagnostics
-        self.stats = torch.zeros(8, device=dev, dtype=F32)
+        self.stats = eng._zeros(8, dtype=F32)
         # GroupNorm partials written by GEMM epilogues (GNSTATS / GNBWD tiles:
         # [N/128][column tile][4]) when T and the group widths are multiples of 128
         Cmax = max([sw.C for sw in self.enc] + [2 * sw.C for sw in self.dec] + [1])
@@ -310,7 +323,7 @@ class Workspace:
             return
         NCe = max([sw.N * sw.C for sw in self.enc] + [1])
         if eng.fin2_pad is not None:  # zero columns up to the padded K of the output conv's DGRAD
-            self.dxhat_pad = torch.zeros(self.N, eng.fin2_pad[0], device=dev, dtype=cd)
+            self.dxhat_pad = eng._zeros(self.N, eng.fin2_pad[0], dtype=cd)
             self.dxhat = self.dxhat_pad[:, :Fo]
         else:
             self.dxhat = self.dxhat_pad = e(self.N, Fo)
@@ -348,7 +361,7 @@ class Workspace:
         self.cs_f1 = e(_tm(self.Nskip), S, dt=F32)    # dL/d(final conv 1 output)
         # bias-gradient row-part sums of the encoder output conv (from dL/dz) and of the
         # output conv (from dL/dxhat), reduced by their group's weight-norm backward launch
-        self.cs_eo = torch.zeros(ops.COMMIT_PARTS, Z, device=dev, dtype=F32)  # rows past colsum_parts stay 0
+        self.cs_eo = eng._zeros(ops.COMMIT_PARTS, Z, dtype=F32)  # rows past colsum_parts stay 0
         self.cs_f2 = e(ops.colsum_parts(self.N, Fo, cd), Fo, dt=F32)
         self.lin_part = e(max(len(g) * ((O + 63) // 64) for O, g in eng.cond_groups.items()) * B * d["ydim"]
                           if eng.cond_groups else 1, dt=F32)  # split-K partials of d(embedding)
@@ -368,6 +381,14 @@ class VQVAEEngine:
         self.cd = torch.bfloat16 if compute_dtype in ("bf16", "bfloat16") else F32
         self.dt = ops.dt_code(self.cd)
         L.load()
+        self._guards = None
+        if self.opt.debug_checks:
+            from .. import debug
+            self._guards = debug.GuardSet(self.device)
+            ops.set_debug_checks(True)
+            debug.install(self._guards)
+            import weakref
+            weakref.finalize(self, debug.uninstall, self._guards)
         enc, dec = model.encoder, model.decoder
         self.dims = d = dict(mel=enc.in_ch, Z=enc.z_ch, S=dec.skip_ch, F=dec.final_ch, cond=dec.cond_ch,
                              K=model.quantizer.z_num, ydim=model.embeds._embedding.weight.shape[1],
@@ -378,6 +399,8 @@ class VQVAEEngine:
         self.plain = not model.use_ema
         self.vq_normalize = bool(getattr(model.quantizer, "normalize", False)) if self.plain else False
         self._flatten()
+        if self._guards is not None:
+            self._adopt_buffers()
         self._build_layers()
         self._ws = {}
         self.opt_ready = False
@@ -398,13 +421,34 @@ class VQVAEEngine:
         # flat_p version the packed weights / norms it wrote belong to
         self._adam_wn, self._adam_wn_built, self._packed_version = None, False, None
 
+    # ------------------------------------------------------------ allocation
+    def _empty(self, *shape, dtype=F32):
+        """Every engine buffer comes from here (guarded under debug_checks)."""
+        if self._guards is not None:
+            return self._guards.empty(*shape, dtype=dtype, label=f"{dtype} {tuple(shape)}")
+        return torch.empty(*shape, device=self.device, dtype=dtype)
+
+    def _zeros(self, *shape, dtype=F32):
+        t = self._empty(*shape, dtype=dtype)
+        t.zero_()
+        return t
+
+    def _adopt_buffers(self):
+        """debug_checks: the quantizer's EMA buffers (written by the EMA update)
+        moved between guards too."""
+        q = self.m.quantizer
+        for name in ("emb_sum", "emb_elem", "embeddings"):
+            t = getattr(q, name, None)
+            if isinstance(t, torch.Tensor) and t.device == self.device and name in q._buffers:
+                q._buffers[name] = self._guards.adopt(t, f"quantizer.{name}")
+
     # ------------------------------------------------------------ parameters
     def _flatten(self):
         params = list(self.m.parameters())
         self.params = params
         total = sum(p.numel() for p in params)
-        self.flat_p = torch.empty(total, device=self.device, dtype=F32)
-        self.flat_g = torch.zeros(total, device=self.device, dtype=F32)
+        self.flat_p = self._empty(total, dtype=F32)
+        self.flat_g = self._zeros(total, dtype=F32)
         self.gviews = {}
         off = 0
         with torch.no_grad():
@@ -495,9 +539,9 @@ class VQVAEEngine:
         if isinstance(mod, ResampleConv1d):
             Lr = ConvLayer(mod, name, KIND_UP if mod.transposed else KIND_DOWN, mod.cin, mod.cout, 3, 1, 1,
                            mod.scale)
-            Lr.wp = torch.empty(Lr.rows, Lr.cols, device=dev, dtype=dtype or self.cd)
+            Lr.wp = self._empty(Lr.rows, Lr.cols, dtype=dtype or self.cd)
             if Lr.kind == KIND_UP:
-                Lr.btile = torch.empty(mod.scale * mod.cout, device=dev, dtype=F32)
+                Lr.btile = self._empty(mod.scale * mod.cout, dtype=F32)
         else:
             kind = KIND_CONVT if mod.transposed else KIND_CONV
             dil = getattr(mod, "dilation", 1)
@@ -505,8 +549,8 @@ class VQVAEEngine:
             if 2 * pad != (mod.k - 1) * dil:
                 raise NotImplementedError(f"{name}: asymmetric padding (the output length would change)")
             Lr = ConvLayer(mod, name, kind, mod.cin, mod.cout, mod.k, pad, dil)
-            Lr.wp = torch.empty(Lr.cout, Lr.k * Lr.cin, device=dev, dtype=dtype or self.cd)
-        Lr.norm = torch.empty(Lr.rows, device=dev, dtype=F32)
+            Lr.wp = self._empty(Lr.cout, Lr.k * Lr.cin, dtype=dtype or self.cd)
+        Lr.norm = self._empty(Lr.rows, dtype=F32)
         return Lr
 
     def _build_layers(self):
@@ -566,7 +610,7 @@ class VQVAEEngine:
         Fp = -(-f2.cout // 64) * 64
         self.fin2_pad = None
         if Fp != f2.cout and f2.kind == KIND_CONV and f2.k == 1 and not m.decoder.final_layer[3].transposed:
-            full = torch.zeros(Fp, f2.cin, device=self.device, dtype=f2.wp.dtype)
+            full = self._zeros(Fp, f2.cin, dtype=f2.wp.dtype)
             f2.wp = full[:f2.cout]
             self.fin2_pad = (Fp, full)
         self.dec_blocks = [b for st in self.dec_stages for b in st.blocks]
@@ -657,7 +701,7 @@ class VQVAEEngine:
         # slabs in a region of their own, all read by one launch after the backward
         per_group = [sum(nbytes(Lr) for Lr in grp) for grp in groups]
         arena = sum(per_group) if self.opt.wn_bwd_batch else max(per_group)
-        self.arena = torch.empty(arena, device=self.device, dtype=torch.uint8)
+        self.arena = self._empty(arena, dtype=torch.uint8)
         base = 0
         for gi, grp in enumerate(groups):
             off = base
@@ -669,6 +713,15 @@ class VQVAEEngine:
                 off += nbytes(Lr)
         self.wn_fwd_table = ops.wn_table([self._wn_entry(Lr, bwd=False) for Lr in self.convs])
         self.groups = groups
+        # in-launch split-K reduction of the 3-tap weight gradients (EngineOptions.wgrad_fixup):
+        # an fp32 gradient buffer and tile counters per candidate layer; whether a call takes it
+        # depends on the workspace's frames (Workspace.fix, _build_bwd_tables)
+        if self.opt.wgrad_fixup and bf_slabs:
+            for grp in groups:
+                for Lr in grp:
+                    if Lr.kind in (KIND_CONV, KIND_CONVT) and Lr.k == 3 and Lr.splits > 1:
+                        Lr.fix_dw = self._empty(Lr.rows, Lr.cols, dtype=F32)
+                        Lr.fix_cnt = self._zeros(((Lr.rows + 127) // 128) * (Lr.cols // 64 + 1), dtype=torch.int32)
 
     def _bwd_groups(self):
         gr = [[self.fin1, self.fin2]]
@@ -681,7 +734,7 @@ class VQVAEEngine:
             gr += [[st.conv]]
         return gr
 
-    def _wn_entry(self, Lr, bwd):
+    def _wn_entry(self, Lr, bwd, fix=False):
         mod = Lr.mod
         if Lr.kind in (KIND_DOWN, KIND_UP):
             wn = mod.has_weight_norm
@@ -696,6 +749,8 @@ class VQVAEEngine:
         if bwd:
             v = e["v"]
             e.update(dv=self.g(v), dg=self.g(mod.weight_g) if wn else None, slabs=Lr.slab)
+            if fix:  # the GEMM launch left the reduced fp32 gradient: one "slab"
+                e.update(slabs=Lr.fix_dw.view(1, Lr.rows, Lr.cols), splits=1)
         return e
 
     def refresh_tables(self):
@@ -712,6 +767,27 @@ class VQVAEEngine:
         (resampling) GEMM whose epilogue cannot sum unfolded columns."""
         return buf[:1] if producer_folded else buf
 
+    def _fixup_layers(self, w):
+        """{id(layer)} of the 3-tap layers whose weight gradient takes the
+        in-launch split-K reduction at this workspace's frames."""
+        on = set()
+        pol, sdt = self.opt.kernel_policy, L.VQX_BF16
+        for si, st in enumerate(self.enc_stages):
+            sw = w.enc[si]
+            for b in st.blocks:
+                for Lr in b.convs:
+                    if Lr.fix_dw is not None and Lr.kind == KIND_CONV and ops.wgrad_fixup_ok(
+                            sw.N, sw.T, Lr.cout, Lr.cin, Lr.k, Lr.pad, self.dt, sdt, dil=Lr.dil, policy=pol):
+                        on.add(id(Lr))
+        for si, st in enumerate(self.dec_stages):
+            sw = w.dec[si]
+            for b in st.blocks:
+                Lr = b.conv_in
+                if Lr.fix_dw is not None and Lr.kind == KIND_CONVT and ops.wgrad_fixup_ok(
+                        sw.N, sw.T, Lr.cin, Lr.cout, Lr.k, Lr.pad, self.dt, sdt, dil=Lr.dil, policy=pol):
+                    on.add(id(Lr))
+        return on
+
     def _build_bwd_tables(self, w):
         """Per-workspace backward tables: each group's weight-norm backward plus
         the column reductions of the bias / GroupNorm-affine partials that are
@@ -719,8 +795,13 @@ class VQVAEEngine:
         B, S = w.B, self.dims["S"]
         g = self.g
         cr = ops.colreduce_entry
+        w.fix = self._fixup_layers(w) if self.opt.wgrad_fixup else set()
+
+        def wb(Lr):  # a layer's backward entry (its reduced fp32 gradient when w.fix has it)
+            return self._wn_entry(Lr, True, fix=id(Lr) in w.fix)
+
         t = {}
-        t["fin"] = [self._wn_entry(self.fin1, True), self._wn_entry(self.fin2, True),
+        t["fin"] = [wb(self.fin1), wb(self.fin2),
                     cr(w.cs_f1, g(self.fin1.mod.bias)), cr(w.cs_f2, g(self.fin2.mod.bias))]
         ns = len(self.dec_stages)
         for si, st in enumerate(self.dec_stages):
@@ -734,14 +815,14 @@ class VQVAEEngine:
                 # dL/dx_{j+1}: zero after the last block of the last stage (cs zeroed), else the
                 # colsums of the next block's / next stage conv's dgrad
                 nxt_folded = (j == nb - 1 and si + 1 < ns and self.dec_stages[si + 1].conv.kind == KIND_UP)
-                t[b.key] = [self._wn_entry(b.conv_in, True), self._wn_entry(b.rs, True),
+                t[b.key] = [wb(b.conv_in), wb(b.rs),
                             cr(self._bias_partials(w, nxt_folded, sw.cs[j + 1]), rb[:sw.C]), cr(w.cs_skip, rb[sw.C:]),
                             cr(sw.cs_all[j], g(b.conv_in.mod.bias)), cr(dg_b, g(b.gn.weight)), cr(db_b, g(b.gn.bias))]
             first_folded = not st.blocks and si + 1 < ns and self.dec_stages[si + 1].conv.kind == KIND_UP
-            t[("dec_stage", si)] = [self._wn_entry(st.conv, True),
+            t[("dec_stage", si)] = [wb(st.conv),
                                     cr(self._bias_partials(w, first_folded, sw.cs[0]), g(st.conv.mod.bias))]
-        t["cond"] = [self._wn_entry(Lr, True) for Lr in self.dec_cond]
-        t["enc_out"] = [self._wn_entry(self.enc_out, True), cr(w.cs_eo, g(self.enc_out.mod.bias))]
+        t["cond"] = [wb(Lr) for Lr in self.dec_cond]
+        t["enc_out"] = [wb(self.enc_out), cr(w.cs_eo, g(self.enc_out.mod.bias))]
         ne = len(self.enc_stages)
         for si, st in enumerate(self.enc_stages):
             sw = w.enc[si]
@@ -751,17 +832,15 @@ class VQVAEEngine:
                 # dL/dc_{j+1} comes from the next block's skip dgrad, the next stage conv's
                 # dgrad (folded when it down-samples) or the output conv's dgrad
                 nxt_folded = j == nb - 1 and si + 1 < ne and self.enc_stages[si + 1].conv.kind == KIND_DOWN
-                ent = [self._wn_entry(Lr, True) for Lr in b.convs] + [self._wn_entry(b.skip, True),
-                                                                       cr(self._bias_partials(w, nxt_folded,
-                                                                                              sw.cs[j + 1]),
-                                                                          g(b.skip.mod.bias))]
+                ent = [wb(Lr) for Lr in b.convs] + [wb(b.skip), cr(self._bias_partials(w, nxt_folded, sw.cs[j + 1]),
+                                                                    g(b.skip.mod.bias))]
                 for l, (Lr, gn) in enumerate(zip(b.convs, b.gns)):
                     ent += [cr(self._bview(self._blk(w, "enc", si, j, "colsum_b", l), B, C), g(Lr.mod.bias)),
                             cr(self._bview(self._blk(w, "enc", si, j, "dgam_b", l), B, C), g(gn.weight)),
                             cr(self._bview(self._blk(w, "enc", si, j, "dbet_b", l), B, C), g(gn.bias))]
                 t[b.key] = ent
             first_folded = not st.blocks and si + 1 < ne and self.enc_stages[si + 1].conv.kind == KIND_DOWN
-            t[("enc_stage", si)] = [self._wn_entry(st.conv, True),
+            t[("enc_stage", si)] = [wb(st.conv),
                                     cr(self._bias_partials(w, first_folded, sw.cs[0]), g(st.conv.mod.bias))]
         w.bwd_tables = {k: ops.wn_table(v) for k, v in t.items()}
         w.bwd_entries = t
@@ -833,8 +912,12 @@ class VQVAEEngine:
             ops.conv_fwd(dy.view(-1, s * Lr.cout), Lr.wp, dx, T=T // s, cin=s * Lr.cout, cout=Lr.cin, ntaps=3,
                          pad=1, **kw)
 
+    _fix_now = frozenset()  # the current backward's workspace's Workspace.fix
+
     def wgrad(self, Lr, dy, x, T, pro=L.PRO_NONE, scale=1.0):
         """Weight-gradient slabs from dy (output gradient, T frames per utterance) and the input x."""
+        if id(Lr) in self._fix_now:
+            raise RuntimeError(f"{Lr.name}: the in-launch split-K reduction runs through wgrad_dgrad only")
         pol = self.opt.kernel_policy
         if Lr.kind == KIND_CONV:
             ops.conv_wgrad(dy, x, Lr.slab, T=T, r_dim=Lr.cout, c_dim=Lr.cin, ntaps=Lr.k, pad=Lr.pad, dil=Lr.dil,
@@ -866,6 +949,8 @@ class VQVAEEngine:
         dkw = dict(T=T, cin=Lr.cout, cout=Lr.cin, ntaps=Lr.k, pad=(Lr.k - 1) * Lr.dil - Lr.pad, dil=Lr.dil, policy=pol,
                    **kw)
         wkw = dict(T=T, ntaps=Lr.k, pad=Lr.pad, dil=Lr.dil, splits=Lr.splits, policy=pol)
+        if id(Lr) in self._fix_now:  # the in-launch split-K reduction (EngineOptions.wgrad_fixup)
+            wkw.update(fixup_dw=Lr.fix_dw, fixup_counters=Lr.fix_cnt)
         if Lr.kind == KIND_CONV:  # as self.wgrad
             ops.conv_dgrad_wgrad(dy, Lr.wp, dx, dkw, dy, x, Lr.slab, dict(wkw, r_dim=Lr.cout, c_dim=Lr.cin, shift_sign=1))
         else:
@@ -889,6 +974,8 @@ class VQVAEEngine:
             # ConvT row norm for the current parameters (vqx_adam_step_wn)
             if plan[2] is not None:
                 ops.weight_norm_fwd(plan[2], flags=plan[3])
+            if self._guards is not None:  # debug_checks: the packed weights must be those of the parameters
+                self._check_packed()
         else:
             ops.weight_norm_fwd(self.wn_fwd_table)
         for st in self.dec_stages:
@@ -1114,7 +1201,7 @@ class VQVAEEngine:
             cur = hi
         if cur < self.n_params:
             rest.append((cur, self.n_params - cur))
-        parts = torch.zeros(max(1, ops.weight_norm_bwd_partials(tab)), device=self.device, dtype=F32)
+        parts = self._zeros(max(1, ops.weight_norm_bwd_partials(tab)), dtype=F32)
         rng = torch.tensor(rest, dtype=torch.int64).view(-1, 2).to(self.device) if rest else None
         return parts, rng
 
@@ -1459,6 +1546,13 @@ class VQVAEEngine:
             torch.cuda.current_stream().wait_event(w.ev_ema)
             w.ev_ema = None
             return
+        if getattr(w, "ema_applied", False):  # already run at the end of the forward
+            w.ema_applied = False
+            return
+        self._ema_finish(w)
+
+    def _ema_finish(self, w):
+        """Wait for the EMA bundle's all-reduce (data parallel), then update."""
         if getattr(self, "_ema_work", None) is not None:
             self.comm.wait(self._ema_work, "ema")
             self._ema_work = None
@@ -1513,7 +1607,29 @@ class VQVAEEngine:
             w.vq_sum_pending = 0
         else:
             ops.logloss_fwd_bwd(x, w.xhat, 1.0 / (B * T), w.dxhat, w.stats[0:1], w.loss_part)
+        # Round 6: the EMA codebook update here, where the reference runs it
+        # (inside the forward, layers_vq.py:295-296; the backward reads no
+        # codebook in EMA mode), so every loss statistic is final at the end of
+        # the forward: snapshot them and mark the point with an event
+        # (trainer/basic.py LazyLossDetail reads them without waiting for the
+        # backward).  The side-stream schedule keeps its end-of-step join.
+        w.stats_snap = None
+        if not self._side_on:
+            if not self.plain:
+                self._ema_finish(w)
+                w.ema_applied = True
+            if self.opt.lazy_stats:
+                w.stats_snap = torch.empty_like(w.stats)
+                ops.convert_2d(w.stats.view(1, -1), w.stats_snap.view(1, -1))
+                w.stats_snap_ev = torch.cuda.Event()
+                w.stats_snap_ev.record()
         return w
+
+    def transfer_stream(self):
+        """Stream for the host reads of the step statistics (LazyLossDetail)."""
+        if getattr(self, "_xfer", None) is None:
+            self._xfer = torch.cuda.Stream(device=self.device)
+        return self._xfer
 
     def backward(self, w, grad_loss=None):
         """Data parallel: every backward group's gradients are all-reduced as
@@ -1525,6 +1641,7 @@ class VQVAEEngine:
         self._wn_pending, self._wn_done = [], set()
         self._sq_plan_ready = None
         self._wn_active = True
+        self._fix_now = getattr(w, "fix", frozenset())
         try:
             if self.plain:
                 # straight-through: the encoder's gradient comes through the decoder
@@ -1537,6 +1654,7 @@ class VQVAEEngine:
             self._wn_bwd_flush(w)
         finally:
             self._wn_active = False
+            self._fix_now = frozenset()
         if self.comm is not None:
             self._grads_final(range(len(self.params)), flush=True)
             self.comm.finish()
@@ -1550,12 +1668,12 @@ class VQVAEEngine:
             raise ValueError(f"unknown optimizer {kind!r}")
         self.opt_kind = kind
         dev = self.device
-        self.exp_avg = torch.zeros(self.n_params, device=dev, dtype=F32)
-        self.exp_avg_sq = torch.zeros(self.n_params, device=dev, dtype=F32)
-        self.opt_step = torch.zeros(1, device=dev, dtype=torch.int64)
-        self.hyper = torch.zeros(16, device=dev, dtype=F32)
-        self.sumsq = torch.zeros(1, device=dev, dtype=F32)
-        self.norm_part = torch.zeros(1024, device=dev, dtype=F32)
+        self.exp_avg = self._zeros(self.n_params, dtype=F32)
+        self.exp_avg_sq = self._zeros(self.n_params, dtype=F32)
+        self.opt_step = self._zeros(1, dtype=torch.int64)
+        self.hyper = self._zeros(16, dtype=F32)
+        self.sumsq = self._zeros(1, dtype=F32)
+        self.norm_part = self._zeros(1024, dtype=F32)
         self.lr0, self.betas, self.eps, self.max_grad_norm = lr, betas, eps, max_grad_norm
         self.sched_step = sched_step or (1 << 30)
         self.sched_gamma = sched_gamma
@@ -1604,8 +1722,22 @@ class VQVAEEngine:
         return self.flat_p._version + sum(p._version for p in self.params)
 
     def invalidate_packed(self):
-        """The next forward packs every layer from the parameters (fuse_adam_wn)."""
+        """The next forward packs every layer from the parameters (fuse_adam_wn).
+        Called by Model.load_state_dict and after the Trainer's initial
+        broadcast; any other write to the parameters that bypasses torch's
+        version counters (.data, raw kernels, collectives) must call it too --
+        EngineOptions.debug_checks verifies it at every forward."""
         self._packed_version = None
+
+    def _check_packed(self):
+        """debug_checks: the packed weights and row norms the fused Adam left
+        equal a full weight-norm pack of the current parameters."""
+        before = [(Lr.wp.clone(), Lr.norm.clone()) for Lr in self.convs]
+        ops.weight_norm_fwd(self.wn_fwd_table)
+        for Lr, (wp, nm) in zip(self.convs, before):
+            if not (torch.equal(wp, Lr.wp) and torch.equal(nm, Lr.norm)):
+                raise RuntimeError(f"{Lr.name}: packed weights are stale (parameters written without "
+                                   "invalidate_packed())")
 
     def _adam_wn_plan(self):
         """(rows table, flat segments, forward table of what is left to pack,

@@ -29,6 +29,56 @@ def _check_cuda(*ts):
             raise L.VqxError("libvqx ops need device tensors (the HIP kernels are the only implementation)")
 
 
+# ---- host extent checks (debug mode; vae_npvc_amd/debug.py)
+_debug = False
+_logical_end = {}  # guarded allocations: storage data_ptr -> bytes of the storage that belong to the buffer
+
+
+def set_debug_checks(on):
+    """Check every pointer argument's span against its tensor's storage before
+    the calls below (off by default: a few microseconds of host time per call).
+    Returns the previous setting."""
+    global _debug
+    prev, _debug = _debug, bool(on)
+    return prev
+
+
+def _span(t, elems, what):
+    """`t` must hold `elems` elements from its data pointer on."""
+    if not _debug or t is None or elems <= 0:
+        return
+    st = t.untyped_storage()
+    end = _logical_end.get(st.data_ptr(), st.nbytes())
+    avail = (end - t.storage_offset() * t.element_size()) // t.element_size()
+    if elems > avail:
+        raise L.VqxError(f"extent check: {what} needs {elems} elements from its pointer, its buffer holds {avail}")
+
+
+def _rows(t, rows, ld, cols, what):
+    if rows > 0 and t is not None:
+        _span(t, (rows - 1) * ld + cols, what)
+
+
+def _conv_extents(x, w, y, a, bias, rowbias, res, mask, out2, y2, colsum, stats, tiles, gn_h, gn_mr):
+    n, cout, cin = a.n_rows, a.cout, a.cin
+    split = a.split_col if out2 is not None else 0
+    tm = (n + 127) // 128
+    _rows(x, n, a.ldx, cin, "conv x")
+    _span(w, cout * a.ntaps * cin, "conv w")
+    _rows(y, n, a.ldy, split or cout, "conv y")
+    _span(bias, cout, "conv bias")
+    _span(rowbias, (n // max(1, a.T)) * cout, "conv rowbias")
+    _rows(res, n, a.ldres, split or cout, "conv res")
+    _rows(mask, n, a.ldmask, cout, "conv mask")
+    _rows(out2, n, a.ldo2, cout - split, "conv out2")
+    _rows(y2, n, a.ldy2, cout, "conv y2")
+    _span(colsum, tm * cout, "conv colsum_part")
+    _span(stats, (n // 128) * ((cout + 127) // 128) * 4, "conv stat_part")
+    _span(tiles, (n // 128) * ((cout + 127) // 128) * 4, "conv gn_stat_tiles")
+    _rows(gn_h, n, a.ldgn, cout * (2 if a.gn_glu else 1), "conv gn_h")
+    _span(gn_mr, (n // max(1, a.T)) * 2 * max(1, a.gn_groups), "conv gn_mean_rstd")
+
+
 POLICY_AUTO, POLICY_IM2COL, POLICY_TALL256, POLICY_TALL512, POLICY_TR128, POLICY_K1_2PCU = 0, 1, 2, 3, 4, 5  # vqx.h
 _policy = POLICY_AUTO
 
@@ -110,6 +160,9 @@ def conv_args(x, w, y, *, T, cin, cout, ntaps, pad, prologue=L.PRO_NONE, pro_sca
     a.gn_stat_tiles, a.gn_eps = ptr(gn_tiles), gn_eps
     a.stat_part = ptr(gn_stats if gn_stats is not None else gn_bwd)
     a.gn_groups, a.gn_glu = gn_groups, int(gn_glu)
+    if _debug:
+        _conv_extents(x, w, y, a, bias, rowbias, res, mask, out2, y2, colsum,
+                      gn_stats if gn_stats is not None else gn_bwd, gn_tiles, gn_h, gn_mr)
     return a
 
 
@@ -223,7 +276,7 @@ def conv_dgrad(dy, w, dx, **kw):
 
 
 def wgrad_args(p, q, slabs, *, T, r_dim, c_dim, ntaps, pad, shift_sign=1, q_prologue=L.PRO_NONE, pro_scale=1.0,
-               splits=1, dil=1, policy=None):
+               splits=1, dil=1, policy=None, fixup_dw=None, fixup_counters=None):
     a = L.WgradArgs()
     a.kernel_policy = _policy if policy is None else policy
     a.p, a.q, a.slabs = ptr(p), ptr(q), ptr(slabs)
@@ -231,6 +284,12 @@ def wgrad_args(p, q, slabs, *, T, r_dim, c_dim, ntaps, pad, shift_sign=1, q_prol
     a.ldp, a.ldq = p.stride(0), q.stride(0)
     a.dtype, a.q_prologue, a.splits, a.pro_scale, a.dil = dt_code(p.dtype), q_prologue, splits, pro_scale, dil
     a.slab_dtype = dt_code(slabs.dtype)
+    a.fixup_dw, a.fixup_counters = ptr(fixup_dw), ptr(fixup_counters)
+    if _debug:
+        _span(fixup_dw, r_dim * ntaps * c_dim, "wgrad fixup_dw")
+        _rows(p, a.n_rows, a.ldp, r_dim, "wgrad p")
+        _rows(q, a.n_rows, a.ldq, c_dim, "wgrad q")
+        _span(slabs, splits * r_dim * ntaps * c_dim, "wgrad slabs")
     return a
 
 
@@ -271,6 +330,33 @@ def wgrad_tiles(n_rows, T, r_dim, c_dim, ntaps, pad, dtype, q_prologue=L.PRO_NON
     return t.value
 
 
+def _wn_extents(d):
+    """Spans of one weight-norm table entry (include/vqx.h vqx_wn_layer)."""
+    kind, cout, cin, k, s = d["kind"], d["cout"], d["cin"], d["k"], d.get("stride", 1) or 1
+    if kind == L.WN_COLREDUCE:
+        _span(d.get("v"), cin * cout, "colreduce src")
+        _span(d.get("dv"), cout, "colreduce dst")
+        return
+    rows = cin if kind in (1, L.WN_RESAMPLE_T) else cout
+    cols = (3 * s * cin if kind == L.WN_RESAMPLE else 3 * s * cout if kind == L.WN_RESAMPLE_T
+            else (cout if kind == 1 else cin) * k)
+    for key in ("v", "dv"):
+        _span(d.get(key), cout * cin * k, f"weight-norm {key}")
+    for key in ("g", "dg", "norm"):
+        _span(d.get(key), rows, f"weight-norm {key}")
+    _span(d.get("w_packed"), rows * cols, "weight-norm w_packed")
+    _span(d.get("slabs"), d.get("splits", 1) * rows * cols, "weight-norm slabs")
+
+
+def wgrad_fixup_ok(n_rows, T, r_dim, c_dim, ntaps, pad, dtype, slab_dtype, q_prologue=L.PRO_NONE, dil=1,
+                   policy=POLICY_AUTO):
+    """Whether conv_wgrad of this shape takes the in-launch split-K reduction (fixup_dw, ABI 127)."""
+    ok = ctypes.c_int32()
+    call("vqx_wgrad_fixup_ok", n_rows, T, r_dim, c_dim, ntaps, pad, dil, dtype, slab_dtype, q_prologue, policy,
+         ctypes.byref(ok))
+    return bool(ok.value)
+
+
 def wn_table(layers):
     """Pack a list of dicts into a ctypes WNLayer array (host copy) and a device byte tensor copy."""
     arr = (L.WNLayer * len(layers))()
@@ -283,6 +369,8 @@ def wn_table(layers):
         e.stride, e.pad = d.get("stride", 0), d.get("pad", 0)
         sl = d.get("slabs")
         e.slab_dtype = dt_code(sl.dtype) if sl is not None else L.VQX_F32
+        if _debug:
+            _wn_extents(d)
     raw = bytes(arr)
     dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to("cuda")
     return arr, dev
@@ -300,12 +388,29 @@ def linear_table(layers):
     for i, d in enumerate(layers):
         for k in ("W", "bias", "out", "dout", "dW", "dbias"):
             setattr(arr[i], k, ptr(d.get(k)))
+    arr.ents = layers  # the tensors behind the pointers (debug extent checks)
     dev = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to("cuda")
     return arr, dev
 
 
+def _linear_extents(arr, B, I, O, dc=None, partials=None):
+    if not _debug:
+        return
+    for d in arr.ents:
+        _span(d.get("W"), O * I, "linear W")
+        _span(d.get("dW"), O * I, "linear dW")
+        for key in ("bias", "dbias"):
+            _span(d.get(key), O, f"linear {key}")
+        for key in ("out", "dout"):
+            _span(d.get(key), B * O, f"linear {key}")
+    _span(dc, B * I, "linear dc")
+    _span(partials, len(arr) * ((O + 63) // 64) * B * I, "linear partials")
+
+
 def linear_batched_fwd(table, c, B, I, O):
     arr, dev = table
+    _linear_extents(arr, B, I, O)
+    _span(c, B * I, "linear c")
     call("vqx_linear_batched_fwd", dev.data_ptr(), len(arr), ptr(c), B, I, O, stream_ptr())
 
 
@@ -320,6 +425,7 @@ def linear_batched_fwd_ids(table, emb, ids, B, I, O):
     _check_cuda(emb, ids)
     if ids.dtype != torch.int64 or ids.numel() != B:
         raise ValueError("linear_batched_fwd_ids: B int64 ids")
+    _linear_extents(arr, B, I, O)
     call("vqx_linear_batched_fwd_ids", dev.data_ptr(), len(arr), ptr(emb), ptr(ids), B, I, O, stream_ptr())
 
 
@@ -328,6 +434,7 @@ def linear_batched_bwd_ids(table, emb, ids, B, I, O, dc, partials):
     _check_cuda(emb, ids)
     if ids.dtype != torch.int64 or ids.numel() != B:
         raise ValueError("linear_batched_bwd_ids: B int64 ids")
+    _linear_extents(arr, B, I, O, dc, partials)
     call("vqx_linear_batched_bwd_ids", dev.data_ptr(), len(arr), ptr(emb), ptr(ids), B, I, O, ptr(dc), ptr(partials),
          stream_ptr())
 
@@ -337,6 +444,8 @@ def linear_batched_bwd(table, c, B, I, O, dc, partials=None):
     arr, dev = table
     if dc is not None and partials is None:
         partials = torch.empty(len(arr) * ((O + 63) // 64) * B * I, device=c.device, dtype=torch.float32)
+    _linear_extents(arr, B, I, O, dc, partials)
+    _span(c, B * I, "linear c")
     call("vqx_linear_batched_bwd", dev.data_ptr(), len(arr), ptr(c), B, I, O, ptr(dc), ptr(partials), stream_ptr())
 
 
@@ -359,6 +468,8 @@ def weight_norm_bwd(table, sq_partials=None):
         call("vqx_weight_norm_bwd", ctypes.addressof(arr), dev.data_ptr(), len(arr), stream_ptr())
         return
     _check_cuda(sq_partials)
+    if _debug:
+        _span(sq_partials, weight_norm_bwd_partials(table), "weight-norm sq partials")
     call("vqx_weight_norm_bwd_sq", ctypes.addressof(arr), dev.data_ptr(), len(arr), ptr(sq_partials),
          sq_partials.numel(), stream_ptr())
 
@@ -516,6 +627,11 @@ def vq_forward(z, E, idx, zq, zq_c, sqerr, partials=None, bsum=None, bcnt=None):
         partials = torch.empty(need, device=z.device, dtype=torch.float32)
     if partials.numel() < need:
         raise ValueError(f"vq_forward: workspace {partials.numel()} < {need} floats")
+    if _debug:
+        K = E.shape[0]
+        for t, n, what in ((idx, N, "idx"), (zq, N * D, "zq"), (zq_c, N * D, "zq_c"), (bsum, K * D, "bsum"),
+                           (bcnt, K, "bcnt"), (E, K * D, "codebook")):
+            _span(t, n, f"vq_forward {what}")
     call("vqx_vq_forward", ptr(z), N, D, ptr(E), E.shape[0], ptr(idx), ptr(zq), ptr(zq_c),
          dt_code(zq_c.dtype) if zq_c is not None else 0, ptr(sqerr), ptr(partials), ptr(bsum), ptr(bcnt),
          stream_ptr())
@@ -539,6 +655,10 @@ def vq_ema_update(emb_sum, emb_elem, E, bsum, bcnt, rand_rows, mu, threshold, di
         partials = torch.empty((K * D + 1023) // 1024, device=E.device, dtype=torch.float32)
     if partials.numel() < (K * D + 1023) // 1024:
         raise ValueError(f"vq_ema_update: workspace {partials.numel()} < {(K * D + 1023) // 1024} floats")
+    if _debug:
+        for t, n, what in ((emb_sum, K * D, "emb_sum"), (emb_elem, K, "emb_elem"), (bsum, K * D, "bsum"),
+                           (bcnt, K, "bcnt"), (rand_rows, K * D, "rand_rows"), (diag, 4, "diag")):
+            _span(t, n, f"vq_ema_update {what}")
     call("vqx_vq_ema_update_clear" if clear else "vqx_vq_ema_update", ptr(emb_sum), ptr(emb_elem), ptr(E), ptr(bsum), ptr(bcnt), ptr(rand_rows), K, D,
          mu, threshold, ptr(diag), ptr(partials), stream_ptr())
 
@@ -606,6 +726,8 @@ def embedding_bwd_rows(dout, ids, dweight, accumulate=False):
     _check_cuda(dout, ids, dweight)
     if ids.dtype != torch.int64 or not (dout.is_contiguous() and dweight.is_contiguous()):
         raise ValueError("embedding_bwd_rows: int64 ids, contiguous dout / dweight")
+    _span(dout, ids.numel() * dweight.shape[1], "embedding dout")
+    _span(ids, ids.numel(), "embedding ids")
     call("vqx_embedding_bwd_rows", ptr(dout), ptr(ids), ids.numel(), dweight.shape[1], dweight.shape[0], ptr(dweight),
          int(accumulate), stream_ptr())
     return dweight

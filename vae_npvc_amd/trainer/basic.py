@@ -26,20 +26,35 @@ class LazyLossDetail(Mapping):
     """loss_detail dict of one step (instead of the reference's 7 .item()
     syncs, vqvae.py:85-87 and layers_vq.py:229-232).  The step's statistics
     are snapshotted on the device by a kernel (the next step overwrites
-    them) and copied to the host only when a value is first read, which
-    waits for the work queued up to that read.  An eager asynchronous D2H
-    per step (EngineOptions.lazy_stats false) held the compute stream
-    ~10 us after the runtime copy even when nothing read the values."""
+    them) and copied to the host only when a value is first read.  An eager
+    asynchronous D2H per step (EngineOptions.lazy_stats false) held the
+    compute stream ~10 us after the runtime copy even when nothing read the
+    values.
+
+    Round 6: every statistic is final at the end of the forward (the EMA
+    update runs there, where the reference runs it, layers_vq.py:295-296), so
+    the engine snapshots them right after the log-loss launch and records an
+    event (VQVAEEngine.forward_train).  A read copies the snapshot on a
+    transfer stream ordered after that event only, so it waits for the
+    forward, not for the backward and optimizer queued behind it: a loop that
+    reads every step (the reference's bin/train.py:128-132) enqueues the next
+    step while the GPU still runs this one's backward."""
 
     def __init__(self, engine, w, stats_dev):
         self._eng, self._w = engine, w
         self._d = None
-        if engine.opt.lazy_stats:
-            self._snap = torch.empty_like(stats_dev)
+        self._ev = None
+        snap = getattr(w, "stats_snap", None)
+        if engine.opt.lazy_stats and snap is not None:
+            self._snap, self._snap_ev = snap, w.stats_snap_ev   # taken mid-step by the engine
+            w.stats_snap = None
+            self._host = None
+        elif engine.opt.lazy_stats:
+            self._snap, self._snap_ev = torch.empty_like(stats_dev), None
             ops.convert_2d(stats_dev.view(1, -1), self._snap.view(1, -1))
-            self._host = self._ev = None
+            self._host = None
         else:
-            self._snap = None
+            self._snap = self._snap_ev = None
             self._host = torch.empty(stats_dev.shape, dtype=stats_dev.dtype, pin_memory=True)
             self._host.copy_(stats_dev, non_blocking=True)
             self._ev = torch.cuda.Event()
@@ -47,7 +62,16 @@ class LazyLossDetail(Mapping):
 
     def _get(self):
         if self._d is None:
-            if self._snap is not None:
+            if self._snap is not None and self._snap_ev is not None:
+                xfer = self._eng.transfer_stream()
+                xfer.wait_event(self._snap_ev)
+                host = torch.empty(self._snap.shape, dtype=self._snap.dtype, pin_memory=True)
+                with torch.cuda.stream(xfer):
+                    host.copy_(self._snap, non_blocking=True)
+                    self._snap.record_stream(xfer)
+                xfer.synchronize()
+                self._snap = None
+            elif self._snap is not None:
                 host = self._snap.cpu()
                 self._snap = None
             else:
@@ -161,6 +185,7 @@ class Trainer(object):
             dist.broadcast(self.engine.flat_p, 0)
             for b in self.model.buffers():
                 dist.broadcast(b, 0)
+            self.engine.invalidate_packed()  # the parameters were rewritten outside the fused Adam
         sp = self.scheduler_cfg or {}
         self.engine.init_optimizer(self.learning_rate, betas=(0.5, 0.999), eps=1e-8,
                                    max_grad_norm=float(self.max_grad_norm),
