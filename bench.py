@@ -286,10 +286,6 @@ def main():
     if probe is not None:
         probe.select(None)
     elapsed = t1 - t0
-    # the same loop as a recipe runs it: the reference's bin/train.py:128-132
-    # appends every loss_detail value every iteration, so each step ends in a
-    # host read of the step's statistics (one device sync per step)
-    read_ms = time_read_loss(tr, xs, ys, a.steps, world) if a.read_loss else None
     comm_out = None
     if comm is not None:
         comm.timing = False
@@ -311,6 +307,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     detail = dict(det)
+    # the same loop as a recipe runs it: the reference's bin/train.py:128-132
+    # appends every loss_detail value every iteration, so each step ends in a
+    # host read of the step's statistics (one device sync per step)
+    read_ms = time_read_loss(tr, xs, ys, a.steps, world) if a.read_loss else None
     if world > 1 and world != a.gpus and rank == 0:
         print(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}; reporting n_gpus={world}", file=sys.stderr)
     frames = B_PER_GPU * T_FRAMES * world * a.steps

@@ -1356,7 +1356,8 @@ def test_gather_rows_host_indices_equal_device_indices(K, N):
 
 
 @pytest.mark.parametrize("r,c,shift,splits,B,T", [(512, 512, 1, 8, 8, 256), (512, 1024, -1, 4, 8, 256),
-                                                  (256, 512, 1, 5, 3, 128), (128, 64, -1, 3, 2, 64)])
+                                                  (256, 512, 1, 5, 3, 128), (128, 64, -1, 3, 2, 64),
+                                                  (256, 128, 1, 6, 4, 128), (128, 256, -1, 7, 2, 256)])
 def test_wgrad_in_launch_split_k_reduction(r, c, shift, splits, B, T):
     """vqx_wgrad_args.fixup_dw (ABI 127): the last split of each tile sums the
     bf16 slabs of its tile in split order in fp32 inside the launch.  fixup_dw
@@ -1375,9 +1376,16 @@ def test_wgrad_in_launch_split_k_reduction(r, c, shift, splits, B, T):
     kw = dict(T=T, r_dim=r, c_dim=c, ntaps=3, pad=1, shift_sign=shift, splits=splits)
     ref_slabs = torch.empty(splits, r, 3 * c, device=DEV, dtype=torch.bfloat16)
     ops.conv_wgrad(p, q, ref_slabs, **kw)
+    # the weight-norm backward's order (vqx_misc.hip wn_bwd_kernel, 256-thread blocks): one
+    # sequential sum for rows of >= 256 four-column groups, else G interleaved split groups
+    nx4 = 3 * c // 4
+    G = 1 if nx4 >= 256 else min(splits, 256 // nx4)
     acc = torch.zeros(r, 3 * c, device=DEV)
-    for s in range(splits):
-        acc += ref_slabs[s].float()
+    for gi in range(G):
+        part = torch.zeros(r, 3 * c, device=DEV)
+        for s in range(gi, splits, G):
+            part += ref_slabs[s].float()
+        acc += part
     cnt = torch.zeros(((r + 127) // 128) * (c // 64 + 1), device=DEV, dtype=torch.int32)
     for it in range(2):
         slabs = torch.full((splits, r, 3 * c), float("nan"), device=DEV, dtype=torch.bfloat16)

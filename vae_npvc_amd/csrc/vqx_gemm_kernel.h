@@ -1537,8 +1537,8 @@ __device__ __forceinline__ int q_off128(int row, int ch) { return row * 128 + 16
 // MI355X_MICROARCH.md "inter-workgroup visibility", table row 1: write-through
 // 16-B stores, one counter add per storing workgroup, the last adder told by
 // the value its add returned, the other waves loading after a barrier),
-// sums them in split order 0, 1, ... in fp32 exactly as
-// vqx_weight_norm_bwd's slab_sum2_bf does (acc = 0, acc += split s), stores
+// sums them in fp32 in the order vqx_weight_norm_bwd would (acc = 0, acc +=
+// split s in order, or its interleaved split groups for short rows), stores
 // the fp32 gradient and resets the counter for the next call.  No workgroup
 // waits for another, so the grid needs no co-residency.
 constexpr int kCpolSc1 = 16;  // buffer cache policy bit sc1 (gfx950)
@@ -1567,6 +1567,12 @@ __device__ __forceinline__ void wgrad_tile_fixup(const GemmParams& P, int tmn, i
   const int tid = threadIdx.x;
   const int64_t ss2 = (int64_t)P.Mc * P.Nc * 2;  // bytes per split
   const int S = P.splits;
+  // vqx_weight_norm_bwd's summation order for a row of Nc columns: one
+  // sequential sum over the splits when the row has >= 256 four-column groups,
+  // else G = min(S, 256 / groups) interleaved split groups added in group order
+  // (wn_bwd_kernel, 256-thread blocks: vqx_misc.hip kWnThreads)
+  const int nx4 = P.Nc / 4;
+  const int G = nx4 >= 256 ? 1 : (S < 256 / nx4 ? S : 256 / nx4);
   // chunk (j, pass): row r0 + pass*32 + tid/8, columns j*cdim + c0 + (tid%8)*8 .. +7
   // (the slab store's lane map); two chunks per round, all their splits' loads in flight
   for (int it = 0; it < 12; it += 2) {
@@ -1579,31 +1585,41 @@ __device__ __forceinline__ void wgrad_tile_fixup(const GemmParams& P, int tmn, i
       ok[u] = r < P.Mc && cc < P.cdim;
       at[u] = (int64_t)r * P.Nc + j * P.cdim + cc;
     }
-    f32x4_t a0[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    f32x4_t a1[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    for (int s0 = 0; s0 < S; s0 += 8) {
-      u32x4_t v[2][8];
+    f32x4_t t0[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    f32x4_t t1[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    for (int gi = 0; gi < G; ++gi) {  // split group gi: splits gi, gi+G, ... in order
+      f32x4_t a0[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      f32x4_t a1[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      for (int s0 = gi; s0 < S; s0 += 8 * G) {
+        u32x4_t v[2][8];
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+        for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (ok[u] && s0 + k < S)
-            v[u][k] = __builtin_amdgcn_raw_buffer_load_b128(rsY, (int)(at[u] * 2), (int)((s0 + k) * ss2), kCpolSc1);
+          for (int k = 0; k < 8; ++k)
+            if (ok[u] && s0 + k * G < S)
+              v[u][k] = __builtin_amdgcn_raw_buffer_load_b128(rsY, (int)(at[u] * 2), (int)((s0 + k * G) * ss2),
+                                                              kCpolSc1);
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+        for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (ok[u] && s0 + k < S) {
-            a0[u] += bf16x4_lo(v[u][k]);
-            a1[u] += bf16x4_hi(v[u][k]);
-          }
+          for (int k = 0; k < 8; ++k)
+            if (ok[u] && s0 + k * G < S) {
+              a0[u] += bf16x4_lo(v[u][k]);
+              a1[u] += bf16x4_hi(v[u][k]);
+            }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {  // G == 1: 0 + a == a exactly (a sum from +0 is never -0)
+        t0[u] += a0[u];
+        t1[u] += a1[u];
+      }
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u)
       if (ok[u]) {
         float* o = P.fix_dw + at[u];
-        *(f32x4_t*)o = a0[u];
-        *(f32x4_t*)(o + 4) = a1[u];
+        *(f32x4_t*)o = t0[u];
+        *(f32x4_t*)(o + 4) = t1[u];
       }
   }
 }

@@ -306,6 +306,7 @@ __global__ __launch_bounds__(256) void wn_pack_kernel(const vqx_wn_layer* __rest
 #endif
 constexpr int kWnNF = VQX_WN_NF;
 constexpr int kWnThreads = VQX_WN_THREADS;
+static_assert(kWnThreads == 256, "vqx_gemm_kernel.h wgrad_tile_fixup reproduces the split grouping of 256-thread blocks");
 template <bool BF>
 __device__ __forceinline__ f32x4_t slab_sum(const void* slabs, int64_t p, int64_t ss, int sp0, int step, int splits) {
   typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
