@@ -69,9 +69,27 @@ inline int tr8_segs(const GemmParams& P) {
   return 0;
 }
 
+// Lab switch (build.py -D VQX_TR_FWD_LAB=n; 0 in the library): the automatic
+// 3-tap FWD on the tall 256-frame kernel with a 3-deep (1) or 2-deep (2) ring
+// of 32-channel stages instead of conv_tr_kernel's 128-frame tiles.
+#ifndef VQX_TR_FWD_LAB
+#define VQX_TR_FWD_LAB 0
+#endif
+
 template <int MODE, int EK>
 void launch_tr(const GemmParams& P, int grid, hipStream_t s) {
   const double flops = 2.0 * (double)P.n_rows * P.Nc * P.K;
+  if constexpr (MODE == MODE_FWD && VQX_TR_FWD_LAB != 0) {
+    if (P.policy == POL_AUTO && tr8_segs(P) == 0 && P.T % 256 == 0 && P.n_rows % 256 == 0 && P.kcin % 32 == 0) {
+      GemmParams Q = P;
+      Q.tiles_m = (int)(P.n_rows / 256);
+      const int info8[5] = {VQX_BF16, MODE, 1, 3, EK};
+      const void* fn = VQX_TR_FWD_LAB == 1 ? (const void*)conv_tr8_kernel<MODE, EK, 1, 32, 3>
+                                           : (const void*)conv_tr8_kernel<MODE, EK, 1, 32, 2>;
+      gemm_launch(fn, Q.tiles_m * Q.tiles_n, s, Q, info8, flops, 512);
+      return;
+    }
+  }
   if (const int segs = tr8_segs(P)) {
     GemmParams Q = P;
     Q.tiles_m = (int)(P.n_rows / (256 * segs));

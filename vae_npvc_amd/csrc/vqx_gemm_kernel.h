@@ -1337,11 +1337,11 @@ __global__ __launch_bounds__(256, 2) void conv_tr_kernel(GemmParams P) {
 // each group runs tile_epilogue on its quadrants in its own 44 KiB of LDS.
 // BKC = channels per stage: 32 (2-deep ring) or 16 (4-deep ring, two stages
 // in flight behind counted vmcnt waits: the same LDS, twice the prefetch distance).
-template <int MODE, int EK, int SEGS, int BKC = 32>
+template <int MODE, int EK, int SEGS, int BKC = 32, int NST_ = (BKC == 32 ? 2 : 4)>
 __global__ __launch_bounds__(512, 1) void conv_tr8_kernel(GemmParams P) {
   using T = bf16_t;
   constexpr int ES = 2, EPC = 8, KCH = BKC * ES / 16;  // 16-B chunks per K-major row
-  constexpr int NST = BKC == 32 ? 2 : 4;
+  constexpr int NST = NST_;  // ring depth: NST-1 stages in flight behind the one multiplied
   constexpr int SROWS = 258;                         // staged frames per segment
   constexpr int AROWS = SEGS * SROWS;
   constexpr int A_PIECES = (AROWS * BKC * ES + 1023) / 1024;

@@ -195,6 +195,10 @@ class EngineOptions:
                        (vqx_wgrad_args.fixup_dw, ABI 127): the weight-norm
                        backward then reads one fp32 gradient instead of the
                        bf16 slabs; bit-identical results
+      early_stats      (lazy_stats) the loss statistics snapshotted at the end
+                       of the forward, where they are final, so a host read
+                       waits for the forward only (False: at the end of the
+                       step, the read waits for the whole step)
       debug_checks     out-of-extent write detection (vae_npvc_amd/debug.py):
                        every engine buffer between guard canaries checked
                        after every libvqx call, and host extent checks of
@@ -216,6 +220,7 @@ class EngineOptions:
     kernel_policy: int = 0
     debug_checks: bool = False
     wgrad_fixup: bool = False
+    early_stats: bool = True
 
 
 class _Stage:
@@ -1618,7 +1623,7 @@ class VQVAEEngine:
             if not self.plain:
                 self._ema_finish(w)
                 w.ema_applied = True
-            if self.opt.lazy_stats:
+            if self.opt.lazy_stats and self.opt.early_stats:
                 w.stats_snap = torch.empty_like(w.stats)
                 ops.convert_2d(w.stats.view(1, -1), w.stats_snap.view(1, -1))
                 w.stats_snap_ev = torch.cuda.Event()
