@@ -646,6 +646,22 @@ int vqx_probe_read(int64_t i, int32_t* info5, double* flops, float* ms);
 int vqx_stream_create_cu_mask(int32_t reserve_cus, vqx_stream_t* out, int32_t* cus_used);
 int vqx_stream_destroy(vqx_stream_t stream);
 
+/* Host mailbox for the step statistics (ABI 127; replaces the loss .item()
+ * reads of vqvae.py:85-87 / layers_vq.py:229-232 with one stream-ordered
+ * publish the host polls).  vqx_mailbox_create allocates `slots` slots of
+ * `floats` (<= 64) f32 values in mapped, coherent pinned host memory: layout
+ * [slots] uint32 sequence numbers, then [slots][floats] values, zeroed; *host
+ * is the host view, *dev the device pointer of the same bytes.
+ * vqx_mailbox_publish (one 64-thread workgroup on `stream`) copies src[0..n)
+ * into slot `slot` (and into dev_copy, a device buffer, when non-NULL), then,
+ * behind a system-scope release, stores `seq` as the slot's sequence number:
+ * a host that reads the number equal to seq reads that step's values.  No
+ * marker or copy enters the stream. */
+int vqx_mailbox_create(int32_t slots, int32_t floats, void** host, void** dev);
+int vqx_mailbox_destroy(void* host);
+int vqx_mailbox_publish(const float* src, int32_t n, float* dev_copy, void* box_dev, int32_t slot, int32_t slots,
+                        int32_t floats, uint32_t seq, vqx_stream_t stream);
+
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
 #define VQX_ABI_VERSION 127
 int vqx_version(void);

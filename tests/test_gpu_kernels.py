@@ -1404,3 +1404,33 @@ def test_wgrad_in_launch_split_k_reduction(r, c, shift, splits, B, T):
                                      dict(kw, fixup_dw=dw2, fixup_counters=cnt))
         torch.cuda.synchronize()
         assert torch.equal(dw2, acc) and int(cnt.abs().sum()) == 0, fused
+
+
+def test_host_mailbox_publishes_in_stream_order():
+    """vqx_mailbox_* (ABI 127): values published on the stream arrive in the
+    host slot with the step's sequence number, behind earlier work on the same
+    stream; a slot reused by a later publish reports LookupError (the reader
+    then takes the device copy); many publishes in flight keep their order."""
+    ops = _ops()
+    mb = ops.Mailbox(slots=4, floats=16)
+    x = torch.arange(8, device=DEV, dtype=torch.float32)
+    big = torch.randn(4096, 4096, device=DEV)
+    for _ in range(3):  # queue some work ahead of the publish
+        big = big @ big.t() * 1e-3
+    copy = torch.empty(8, device=DEV)
+    seq, slot = mb.publish(x + big[0, 0] * 0, copy)
+    got = None
+    for _ in range(10_000_000):
+        got = mb.try_read(seq, slot, 8)
+        if got is not None:
+            break
+    assert got is not None and np.array_equal(got, np.arange(8, dtype=np.float32)), got
+    torch.cuda.synchronize()
+    assert torch.equal(copy, x)
+    pubs = [mb.publish(x + k) for k in range(6)]  # slots wrap: the first two are reused
+    torch.cuda.synchronize()
+    with pytest.raises(LookupError):
+        mb.try_read(*pubs[0], 8)
+    for k in (4, 5):
+        s, sl = pubs[k]
+        assert np.array_equal(mb.try_read(s, sl, 8), np.arange(8, dtype=np.float32) + k)

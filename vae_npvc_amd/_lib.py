@@ -144,6 +144,10 @@ _SIGS = {
                          c_int32, c_float, c_float, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_int32, c_void_p, c_void_p],
     "vqx_stream_create_cu_mask": [c_int32, ctypes.POINTER(c_void_p), ctypes.POINTER(c_int32)],
+    "vqx_mailbox_create": [c_int32, c_int32, ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p)],
+    "vqx_mailbox_destroy": [c_void_p],
+    "vqx_mailbox_publish": [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_int32, ctypes.c_uint32,
+                            c_void_p],
     "vqx_stream_destroy": [c_void_p],
     "vqx_probe_enable": [c_int32],
     "vqx_probe_select": [c_void_p],

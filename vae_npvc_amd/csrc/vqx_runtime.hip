@@ -2,6 +2,7 @@
 #include <hip/hip_ext.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <string.h>
 
 #include <vector>
 
@@ -72,4 +73,76 @@ extern "C" int vqx_stream_destroy(vqx_stream_t stream) {
     return -2;
   }
   return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Host mailbox for the step statistics (round 6).  A recipe loop reads the
+// step's loss values on the host every step (reference bin/train.py:128-132).
+// Reading them through an event or a copy puts a marker packet on the compute
+// stream, and each such marker idles the stream ~6 us while the next kernel
+// waits for it.  Instead the snapshot kernel writes the values straight into
+// mapped, coherent pinned host memory and then a per-slot sequence number
+// behind a system-scope release; the host polls the number.  Nothing but a
+// one-workgroup kernel enters the stream.
+struct MailboxHeader {
+  int32_t slots, floats;
+};
+
+extern "C" int vqx_mailbox_create(int32_t slots, int32_t floats, void** host, void** dev) {
+  if (slots < 1 || floats < 1 || floats > 64 || !host || !dev) {
+    vqx::set_error("vqx_mailbox_create: 1 <= floats <= 64 per slot, slots >= 1");
+    return -1;
+  }
+  // [slots] uint32 sequence numbers, then [slots][floats] f32 values
+  const size_t bytes = (size_t)slots * 4 + (size_t)slots * floats * 4;
+  void* h = nullptr;
+  hipError_t e = hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e != hipSuccess) { vqx::set_error("hipHostMalloc: %s", hipGetErrorString(e)); return -2; }
+  memset(h, 0, bytes);
+  void* d = nullptr;
+  e = hipHostGetDevicePointer(&d, h, 0);
+  if (e != hipSuccess) {
+    (void)hipHostFree(h);
+    vqx::set_error("hipHostGetDevicePointer: %s", hipGetErrorString(e));
+    return -2;
+  }
+  *host = h;
+  *dev = d;
+  return 0;
+}
+
+extern "C" int vqx_mailbox_destroy(void* host) {
+  const hipError_t e = hipHostFree(host);
+  if (e != hipSuccess) { vqx::set_error("hipHostFree: %s", hipGetErrorString(e)); return -2; }
+  return 0;
+}
+
+namespace vqx {
+// values first (system-scope stores), then every thread's stores released to
+// the system before lane 0 of the one wave stores the sequence number
+__global__ __launch_bounds__(64) void mailbox_publish_kernel(const float* __restrict__ src, int n, float* dev_copy,
+                                                             float* box, uint32_t* seqp, uint32_t seq) {
+  const int t = threadIdx.x;
+  if (t < n) {
+    const float v = src[t];
+    if (dev_copy) dev_copy[t] = v;
+    __hip_atomic_store(box + t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the values before the number
+  __syncthreads();
+  if (t == 0) __hip_atomic_store(seqp, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+}  // namespace vqx
+
+extern "C" int vqx_mailbox_publish(const float* src, int32_t n, float* dev_copy, void* box_dev, int32_t slot,
+                                   int32_t slots, int32_t floats, uint32_t seq, vqx_stream_t stream) {
+  if (!src || !box_dev || n < 1 || n > floats || floats > 64 || slot < 0 || slot >= slots) {
+    vqx::set_error("vqx_mailbox_publish: bad arguments");
+    return -1;
+  }
+  uint32_t* seqp = (uint32_t*)box_dev + slot;
+  float* box = (float*)((uint32_t*)box_dev + slots) + (size_t)slot * floats;
+  hipLaunchKernelGGL(vqx::mailbox_publish_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, src, n, dev_copy, box,
+                     seqp, seq);
+  return vqx::launch_status("vqx_mailbox_publish");
 }

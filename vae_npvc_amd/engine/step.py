@@ -425,6 +425,7 @@ class VQVAEEngine:
         # fused Adam + weight-norm preparation (fuse_adam_wn): its plan, and the
         # flat_p version the packed weights / norms it wrote belong to
         self._adam_wn, self._adam_wn_built, self._packed_version = None, False, None
+        self._mailbox = None  # host mailbox of the step statistics (early_stats)
 
     # ------------------------------------------------------------ allocation
     def _empty(self, *shape, dtype=F32):
@@ -1624,17 +1625,16 @@ class VQVAEEngine:
                 self._ema_finish(w)
                 w.ema_applied = True
             if self.opt.lazy_stats and self.opt.early_stats:
-                w.stats_snap = torch.empty_like(w.stats)
-                ops.convert_2d(w.stats.view(1, -1), w.stats_snap.view(1, -1))
-                w.stats_snap_ev = torch.cuda.Event()
-                w.stats_snap_ev.record()
+                # published into a host mailbox (ops.Mailbox, vqx_mailbox_publish): the
+                # host polls a sequence number, so no event marker enters the stream
+                # (a recorded event idled it ~6 us at every step)
+                if self._mailbox is None:
+                    self._mailbox = ops.Mailbox(64, 16)
+                snap = torch.empty_like(w.stats)  # the device copy, for reads after the slot was reused
+                seq, slot = self._mailbox.publish(w.stats, snap)
+                w.stats_snap = (self._mailbox, seq, slot, snap, torch.cuda.current_stream())
         return w
 
-    def transfer_stream(self):
-        """Stream for the host reads of the step statistics (LazyLossDetail)."""
-        if getattr(self, "_xfer", None) is None:
-            self._xfer = torch.cuda.Stream(device=self.device)
-        return self._xfer
 
     def backward(self, w, grad_loss=None):
         """Data parallel: every backward group's gradients are all-reduced as

@@ -844,3 +844,58 @@ def cu_masked_stream(reserve_cus):
 
 def release_stream(stream):
     call("vqx_stream_destroy", ctypes.c_void_p(stream.cuda_stream))
+
+
+class Mailbox:
+    """Host mailbox for small per-step statistics (vqx_mailbox_*): `slots`
+    slots of `floats` f32 values in mapped pinned host memory, each with a
+    sequence number the publishing kernel stores last (system-scope release).
+    publish() enqueues the copy on the current stream; read(seq, slot) polls
+    the slot's number on the host -- no event, no copy on the stream."""
+
+    def __init__(self, slots=64, floats=16):
+        import numpy as np
+        self.slots, self.floats = int(slots), int(floats)
+        h, d = ctypes.c_void_p(), ctypes.c_void_p()
+        call("vqx_mailbox_create", self.slots, self.floats, ctypes.byref(h), ctypes.byref(d))
+        self._host, self._dev = h.value, d.value
+        n = self.slots + self.slots * self.floats
+        buf = (ctypes.c_uint32 * n).from_address(self._host)
+        self._seq = np.frombuffer(buf, dtype=np.uint32, count=self.slots)
+        self._val = np.frombuffer(buf, dtype=np.float32, count=self.slots * self.floats,
+                                  offset=4 * self.slots).reshape(self.slots, self.floats)
+        self._next = 1
+
+    def publish(self, src, dev_copy=None):
+        """Publish src (f32 device tensor, <= floats values) as the next
+        sequence number; returns (seq, slot)."""
+        _check_cuda(src, dev_copy)
+        n = src.numel()
+        if n > self.floats or not src.is_contiguous() or src.dtype != torch.float32:
+            raise ValueError(f"Mailbox.publish: contiguous f32 tensor of <= {self.floats} values")
+        seq, self._next = self._next, self._next + 1
+        slot = seq % self.slots
+        call("vqx_mailbox_publish", ptr(src), n, ptr(dev_copy), self._dev, slot, self.slots, self.floats, seq,
+             stream_ptr())
+        return seq, slot
+
+    def try_read(self, seq, slot, n):
+        """The values of `seq` once published (None while pending); raises
+        LookupError when the slot has been reused by a later step."""
+        s = int(self._seq[slot])
+        if s < seq:
+            return None
+        if s > seq:
+            raise LookupError("mailbox slot reused")
+        v = self._val[slot, :n].copy()
+        if int(self._seq[slot]) != seq:  # overwritten while copying
+            raise LookupError("mailbox slot reused")
+        return v
+
+    def __del__(self):
+        try:
+            if getattr(self, "_host", None):
+                L.load().vqx_mailbox_destroy(ctypes.c_void_p(self._host))
+                self._host = None
+        except Exception:
+            pass

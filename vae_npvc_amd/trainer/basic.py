@@ -33,22 +33,24 @@ class LazyLossDetail(Mapping):
 
     Round 6: every statistic is final at the end of the forward (the EMA
     update runs there, where the reference runs it, layers_vq.py:295-296), so
-    the engine snapshots them right after the log-loss launch and records an
-    event (VQVAEEngine.forward_train).  A read copies the snapshot on a
-    transfer stream ordered after that event only, so it waits for the
-    forward, not for the backward and optimizer queued behind it: a loop that
-    reads every step (the reference's bin/train.py:128-132) enqueues the next
-    step while the GPU still runs this one's backward."""
+    the engine publishes them right after the log-loss launch into a host
+    mailbox (ops.Mailbox: mapped pinned memory, a sequence number stored
+    behind a system-scope release; VQVAEEngine.forward_train).  A read polls
+    that number, so it waits for the forward, not for the backward and
+    optimizer queued behind it: a loop that reads every step (the reference's
+    bin/train.py:128-132) enqueues the next step while the GPU still runs
+    this one's backward.  No event or copy enters the stream."""
 
     def __init__(self, engine, w, stats_dev):
         self._eng, self._w = engine, w
         self._d = None
         self._ev = None
-        snap = getattr(w, "stats_snap", None)
-        if engine.opt.lazy_stats and snap is not None:
-            self._snap, self._snap_ev = snap, w.stats_snap_ev   # taken mid-step by the engine
+        pub = getattr(w, "stats_snap", None)
+        self._pub = None
+        if engine.opt.lazy_stats and pub is not None:
+            self._pub = pub          # published mid-step into the engine's host mailbox
             w.stats_snap = None
-            self._host = None
+            self._snap = self._snap_ev = self._host = None
         elif engine.opt.lazy_stats:
             self._snap, self._snap_ev = torch.empty_like(stats_dev), None
             ops.convert_2d(stats_dev.view(1, -1), self._snap.view(1, -1))
@@ -60,17 +62,32 @@ class LazyLossDetail(Mapping):
             self._ev = torch.cuda.Event()
             self._ev.record()
 
+    def _read_mailbox(self):
+        """Poll the mailbox slot until the step's values are there; a slot
+        already reused by a later step, or a stream that has finished without
+        the values arriving, falls back to the device copy."""
+        mb, seq, slot, snap, stream = self._pub
+        self._pub = None
+        spins = 0
+        while True:
+            try:
+                v = mb.try_read(seq, slot, snap.numel())
+            except LookupError:
+                return snap.cpu()
+            if v is not None:
+                return torch.from_numpy(v)
+            spins += 1
+            if spins % 4096 == 0 and stream.query():  # the stream finished: one last look, then the copy
+                try:
+                    v = mb.try_read(seq, slot, snap.numel())
+                except LookupError:
+                    v = None
+                return torch.from_numpy(v) if v is not None else snap.cpu()
+
     def _get(self):
         if self._d is None:
-            if self._snap is not None and self._snap_ev is not None:
-                xfer = self._eng.transfer_stream()
-                xfer.wait_event(self._snap_ev)
-                host = torch.empty(self._snap.shape, dtype=self._snap.dtype, pin_memory=True)
-                with torch.cuda.stream(xfer):
-                    host.copy_(self._snap, non_blocking=True)
-                    self._snap.record_stream(xfer)
-                xfer.synchronize()
-                self._snap = None
+            if self._pub is not None:
+                host = self._read_mailbox()
             elif self._snap is not None:
                 host = self._snap.cpu()
                 self._snap = None
