@@ -378,6 +378,13 @@ int vqx_logloss_fwd_bwd_x(const float* x, const float* xhat, int32_t ldxh, int32
                           float grad_scale, void* dxhat, int32_t lddx, int32_t dtype, float* loss_out,
                           float* partials, const float* extra_partials, int32_t n_extra, float* extra_out,
                           vqx_stream_t stream);
+/* The same without the final sum launch (ABI 128): the per-workgroup
+ * partials only, their count in *n_parts (at most 1024); the total is
+ * (1/(B*T)) * their sum in the order vqx_logloss_fwd_bwd adds them
+ * (vqx_vq_ema_update_close sums them so). */
+int vqx_logloss_parts(const float* x, const float* xhat, int32_t ldxh, int32_t B, int32_t C, int32_t T,
+                      float grad_scale, void* dxhat, int32_t lddx, int32_t dtype, float* partials, int32_t* n_parts,
+                      vqx_stream_t stream);
 
 /*
  * EMA vector-quantizer forward (EMAVectorQuantizer.forward,
@@ -416,7 +423,9 @@ int vqx_vq_stats(const float* z, int64_t n_rows, int32_t D, const int64_t* idx, 
  *   E        = usage ? emb_sum/emb_elem : rand_rows
  *   diag[0..3] = {entropy (perplexity of bcnt), used_curr, usage, diff_emb}
  * rand_rows [K][D] are the rows z[perm[:K]] gathered by vqx_gather_rows.
- * partials: workspace of ceil(K*D/1024) floats.  Deterministic (fixed
+ * partials: workspace of ceil(K*D/1024) + 1 words, the last a counter that
+ * must be zero before the first call (each call leaves it zero; ABI 128: one
+ * launch, its last workgroup runs the per-code pass).  Deterministic (fixed
  * summation order).
  */
 int vqx_vq_ema_update(float* emb_sum, float* emb_elem, float* E, const float* bsum,
@@ -427,6 +436,31 @@ int vqx_vq_ema_update(float* emb_sum, float* emb_elem, float* E, const float* bs
 int vqx_vq_ema_update_clear(float* emb_sum, float* emb_elem, float* E, float* bsum, float* bcnt,
                             const float* rand_rows, int32_t K, int32_t D, float mu, float threshold, float* diag,
                             float* partials, vqx_stream_t stream);
+/* vqx_vq_ema_update_clear that also closes the training step's forward in
+ * its last workgroup (ABI 128), the work of two one-workgroup launches:
+ *   out[i][0] = scale[i] * (parts[i][0] + ... + parts[i][n[i]-1]), i < 2
+ *     (parts[i] NULL: none), summed in the order of vqx_logloss_fwd_bwd_x's
+ *     final launch (the log-loss total from vqx_logloss_parts' partials with
+ *     scale 1/(B*T); the commitment sum from vqx_vq_forward's partials);
+ *   then, with pub_box != NULL, pub_src[0 .. pub_n) published into mailbox
+ *     slot pub_slot with number pub_seq as vqx_mailbox_publish does, after
+ *     the sums and diag are stored (pub_src may hold them).
+ * The values equal those of the separate launches bit for bit. */
+typedef struct {
+  const float* parts[2];
+  int32_t n[2];
+  float scale[2];
+  float* out[2];
+  const float* pub_src;
+  int32_t pub_n;
+  float* pub_copy;     /* device copy of the published values, or NULL */
+  void* pub_box;       /* vqx_mailbox_create's device pointer, or NULL */
+  int32_t pub_slot, pub_slots, pub_floats;
+  uint32_t pub_seq;
+} vqx_step_close;
+int vqx_vq_ema_update_close(float* emb_sum, float* emb_elem, float* E, float* bsum, float* bcnt,
+                            const float* rand_rows, int32_t K, int32_t D, float mu, float threshold, float* diag,
+                            float* partials, const vqx_step_close* close, vqx_stream_t stream);
 
 /* out[i][:] = src[rows[i]][:] for i < n_out  (f32, row length D).  rows are
  * int64 indices; negative indices write zero rows (rows owned by another
@@ -501,6 +535,20 @@ int vqx_linear_batched_bwd(const vqx_linear_layer* table_dev, int32_t n, const f
  * O % 64 == 0 and a 16-B aligned table (anything else: an error). */
 int vqx_linear_batched_fwd_ids(const vqx_linear_layer* table_dev, int32_t n, const float* emb,
                                const int64_t* ids, int32_t B, int32_t I, int32_t O, vqx_stream_t stream);
+/* The training step's prologue as one launch (ABI 128): the three
+ * independent jobs a step begins with --
+ *   vqx_linear_batched_fwd_ids(cond_table_dev, n_cond, emb, ids, B, I, O)
+ *     (the speaker conditioning, vqvae.py decoder inputs),
+ *   vqx_nct_to_ntc(x_nct, xB, C, T, y, ldy, y_dtype) (the input's layout) and
+ *   vqx_weight_norm_fwd_flags(wn_host, wn_dev, n_wn, VQX_WNF_NORMS_READY)
+ *     (the ConvTranspose packs; their row norms must be current) --
+ * with the three calls' results bit for bit, in one grid.  A job is skipped
+ * with n_cond = 0, x_nct = NULL or n_wn = 0; n_wn <= 256; the conditioning
+ * job has vqx_linear_batched_fwd_ids's limits (anything else: an error). */
+int vqx_step_prologue(const vqx_wn_layer* wn_host, const vqx_wn_layer* wn_dev, int32_t n_wn,
+                      const vqx_linear_layer* cond_table_dev, int32_t n_cond, const float* emb,
+                      const int64_t* ids, int32_t B, int32_t I, int32_t O, const float* x_nct, int32_t xB,
+                      int32_t C, int32_t T, void* y, int32_t ldy, int32_t y_dtype, vqx_stream_t stream);
 int vqx_linear_batched_bwd_ids(const vqx_linear_layer* table_dev, int32_t n, const float* emb,
                                const int64_t* ids, int32_t B, int32_t I, int32_t O, float* dc, float* partials,
                                vqx_stream_t stream);
@@ -663,7 +711,7 @@ int vqx_mailbox_publish(const float* src, int32_t n, float* dev_copy, void* box_
                         int32_t floats, uint32_t seq, vqx_stream_t stream);
 
 /* ABI version (major*100 + minor); VQX_ABI_VERSION is what this header describes. */
-#define VQX_ABI_VERSION 127
+#define VQX_ABI_VERSION 128
 int vqx_version(void);
 
 #ifdef __cplusplus

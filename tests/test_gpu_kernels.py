@@ -1434,3 +1434,118 @@ def test_host_mailbox_publishes_in_stream_order():
     for k in (4, 5):
         s, sl = pubs[k]
         assert np.array_equal(mb.try_read(s, sl, 8), np.arange(8, dtype=np.float32) + k)
+
+
+@pytest.mark.parametrize("jobs", ["all", "wn", "cond", "x", "cond+x"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_step_prologue_equals_the_three_launches(jobs, dtype):
+    """vqx_step_prologue (ABI 128: ConvT packs + conditioning linears + input
+    transpose in one grid) = vqx_weight_norm_fwd_flags(NORMS_READY) +
+    vqx_linear_batched_fwd_ids + vqx_nct_to_ntc, bit for bit, for any subset
+    of the jobs (mixed-kind pack table, ragged transpose tiles, B < 16)."""
+    ops = _ops()
+    specs = [(1, 512, 1024, 3), (1, 100, 70, 3), (0, 512, 640, 1), (0, 96, 80, 5), (1, 64, 48, 5)]
+    B, I, O, n, n_spk, C, T = 13, 128, 1024, 7, 50, 80, 200
+    runs = []
+    for fused in (False, True):
+        g = torch.Generator(device="cpu").manual_seed(77)
+        ents = []
+        for kind, cin, cout, k in specs:
+            shape = (cout, cin, k) if kind == 0 else (cin, cout, k)
+            v = torch.randn(*shape, generator=g).to(DEV)
+            rows = shape[0]
+            ents.append(dict(v=v, g=(torch.rand(rows, generator=g) + 0.5).to(DEV),
+                             w_packed=torch.zeros(cout, k * cin, device=DEV, dtype=dtype),
+                             norm=torch.zeros(rows, device=DEV), kind=kind, cout=cout, cin=cin, k=k,
+                             dtype=ops.dt_code(dtype)))
+        wt = ops.wn_table(ents)
+        ops.weight_norm_fwd(wt)  # the row norms current (what vqx_adam_step_wn leaves)
+        for e in ents:
+            e["w_packed"].zero_()
+        emb = torch.randn(n_spk, I, generator=g).to(DEV)
+        ids = torch.randint(0, n_spk, (B,), generator=g).to(DEV)
+        lay = [dict(W=(torch.randn(O, I, generator=g) / I ** 0.5).to(DEV), bias=torch.randn(O, generator=g).to(DEV),
+                    out=torch.zeros(B, O, device=DEV), dout=torch.zeros(B, O, device=DEV),
+                    dW=torch.zeros(O, I, device=DEV), dbias=torch.zeros(O, device=DEV)) for _ in range(n)]
+        tab = ops.linear_table(lay)
+        x = torch.randn(B, C, T, generator=g).to(DEV)
+        y = torch.zeros(B * T, 96, device=DEV, dtype=dtype)  # ld > C
+        do_wn, do_c, do_x = jobs in ("all", "wn"), jobs in ("all", "cond", "cond+x"), jobs in ("all", "x", "cond+x")
+        if fused:
+            ops.step_prologue(wt if do_wn else None, (tab, emb, ids, B, I, O) if do_c else None,
+                              x if do_x else None, y if do_x else None)
+        else:
+            if do_wn:
+                ops.weight_norm_fwd(wt, flags=ops.WNF_NORMS_READY)
+            if do_c:
+                ops.linear_batched_fwd_ids(tab, emb, ids, B, I, O)
+            if do_x:
+                ops.nct_to_ntc(x, y)
+        torch.cuda.synchronize()
+        runs.append(([e["w_packed"] for e in ents] + [e["norm"] for e in ents] + [l_["out"] for l_ in lay], y))
+    (ta, ya), (tb, yb) = runs
+    for a, b in zip(ta, tb):
+        assert torch.equal(a, b)
+    assert torch.equal(ya, yb)
+    if jobs in ("all", "x", "cond+x"):
+        assert bool(ya.abs().sum() > 0)
+
+
+@pytest.mark.parametrize("n_vq", [0, 512])
+def test_ema_update_close_equals_the_separate_launches(n_vq):
+    """vqx_vq_ema_update_close (ABI 128) = vqx_logloss_fwd_bwd(_x)'s sums +
+    vqx_vq_ema_update_clear + vqx_mailbox_publish, bit for bit: the loss and
+    commitment sums, codebook, EMA buffers, diagnostics (the 1024-thread sums
+    formed by four virtual threads per thread) and the published values, with
+    the arrival counter left zero for the next call."""
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(23)
+    K, D, B, C, T = 512, 64, 8, 80, 200
+    base = dict(emb_sum=torch.randn(K, D, generator=g), emb_elem=torch.rand(K, generator=g) * 3,
+                E=torch.randn(K, D, generator=g), bsum=torch.randn(K, D, generator=g),
+                bcnt=torch.randint(0, 5, (K,), generator=g).float(), rand=torch.randn(K, D, generator=g))
+    x = torch.randn(B, C, T, generator=g).to(DEV)
+    xhat = torch.randn(B * T, C, generator=g).to(DEV)
+    vq_part = torch.rand(max(n_vq, 1), generator=g).to(DEV)
+    mb = ops.Mailbox(slots=4, floats=16)
+    res = []
+    for fused in (False, True):
+        t = {k: v.clone().to(DEV) for k, v in base.items()}
+        stats = torch.zeros(8, device=DEV)
+        dx = torch.empty(B * T, C, device=DEV)
+        lp = torch.zeros(1024, device=DEV)
+        part = torch.zeros(ops.ema_workspace(K, D), device=DEV)
+        copy = torch.zeros(8, device=DEV)
+        for rep in range(2):  # the second call checks the counter was left zero
+            t["bsum"].copy_(base["bsum"])  # (the first call cleared them)
+            t["bcnt"].copy_(base["bcnt"])
+            if fused:
+                n = ops.logloss_parts(x, xhat, 1.0 / (B * T), dx, lp)
+                sums = [(lp[:n], float(np.float32(1.0) / (np.float32(B) * np.float32(T))), stats[0:1])]
+                if n_vq:
+                    sums.append((vq_part[:n_vq], 1.0, stats[1:2]))
+                seq, slot = ops.vq_ema_update(t["emb_sum"], t["emb_elem"], t["E"], t["bsum"], t["bcnt"], t["rand"],
+                                              0.99, 1.0, stats[4:8], part, clear=True, sums=sums,
+                                              publish=(mb, stats, copy))
+            else:
+                if n_vq:
+                    ops.logloss_fwd_bwd_x(x, xhat, 1.0 / (B * T), dx, stats[0:1], lp, vq_part[:n_vq], stats[1:2])
+                else:
+                    ops.logloss_fwd_bwd(x, xhat, 1.0 / (B * T), dx, stats[0:1], lp)
+                ops.vq_ema_update(t["emb_sum"], t["emb_elem"], t["E"], t["bsum"], t["bcnt"], t["rand"], 0.99, 1.0,
+                                  stats[4:8], part, clear=True)
+                seq, slot = mb.publish(stats, copy)
+        torch.cuda.synchronize()
+        got = None
+        for _ in range(1_000_000):
+            got = mb.try_read(seq, slot, 8)
+            if got is not None:
+                break
+        res.append((t, stats.clone(), copy.clone(), got, part[-1].item()))
+    (a, sa, ca, ga, za), (b, sb, cb, gb, zb) = res
+    for k in ("emb_sum", "emb_elem", "E", "bsum", "bcnt"):
+        assert torch.equal(a[k], b[k]), k
+    assert torch.equal(sa, sb), (sa, sb)
+    assert torch.equal(ca, cb) and torch.equal(cb, sb)
+    assert np.array_equal(ga, gb) and np.array_equal(gb, sb.cpu().numpy())
+    assert za == 0.0 and zb == 0.0

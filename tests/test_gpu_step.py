@@ -620,3 +620,56 @@ def test_in_launch_split_k_reduction_is_bit_identical(name, B, T):
     assert a[0] == b[0]
     for i, (x, y) in enumerate(zip(a[1:5], b[1:5])):
         assert torch.equal(x, y), i
+
+
+@pytest.mark.parametrize("name,dtype", [("vcc20", "bf16"), ("aishell3", "bf16"), ("vcc20", "fp32"),
+                                        ("vcc20_multi", "bf16")])
+def test_fused_step_prologue_is_bit_identical(name, dtype):
+    """EngineOptions.fused_prologue (the default, round 6): from the second
+    step on (the first packs every layer) the ConvT packs, conditioning linears
+    and input transpose run as one launch (vqx_step_prologue).  Three steps
+    give the same losses, parameters, Adam moments and codebook as the three
+    launches bit for bit (vcc20_multi: 64-wide conditioning, which keeps its
+    own launches, and the up-sampler's bias tile after the launch)."""
+    from oracle.vqvae_cpu import seeded_batch
+    out = []
+    for fused in (True, False):
+        cfg = cfg_of(name, compute_dtype=dtype, engine={"fused_prologue": fused})
+        tr = make_trainer(cfg, 41)
+        eng = tr.engine
+        torch.manual_seed(9)
+        np.random.seed(9)
+        dets = [dict(tr.train_step(tuple(t.cuda() for t in seeded_batch(cfg, 4, 128, 80 + s)))[1]) for s in range(3)]
+        torch.cuda.synchronize()
+        out.append((dets, eng.flat_p.clone(), eng.exp_avg.clone(), eng.exp_avg_sq.clone(),
+                    tr.model.quantizer.embeddings.detach().clone(), getattr(eng, "n_fused_prologue", 0)))
+    a, b = out
+    print(f"{name}/{dtype}: {a[5]} fused prologues")
+    assert b[5] == 0 and a[5] == 2
+    assert a[0] == b[0]
+    for i, (x, y) in enumerate(zip(a[1:5], b[1:5])):
+        assert torch.equal(x, y), i
+
+
+@pytest.mark.parametrize("name,dtype", [("vcc20", "bf16"), ("aishell3", "fp32")])
+def test_fused_step_close_is_bit_identical(name, dtype):
+    """EngineOptions.fused_close (the default, round 6): the log-loss and
+    commitment sums and the statistics' mailbox publish in the EMA update's
+    last workgroup.  Three steps give the same losses (read through the
+    mailbox), parameters, Adam moments and codebook as the separate launches."""
+    from oracle.vqvae_cpu import seeded_batch
+    out = []
+    for fused in (True, False):
+        cfg = cfg_of(name, compute_dtype=dtype, engine={"fused_close": fused})
+        tr = make_trainer(cfg, 43)
+        eng = tr.engine
+        torch.manual_seed(10)
+        np.random.seed(10)
+        dets = [dict(tr.train_step(tuple(t.cuda() for t in seeded_batch(cfg, 4, 128, 90 + s)))[1]) for s in range(3)]
+        torch.cuda.synchronize()
+        out.append((dets, eng.flat_p.clone(), eng.exp_avg.clone(), eng.exp_avg_sq.clone(),
+                    tr.model.quantizer.embeddings.detach().clone()))
+    a, b = out
+    assert a[0] == b[0]
+    for i, (x, y) in enumerate(zip(a[1:5], b[1:5])):
+        assert torch.equal(x, y), i

@@ -15,7 +15,7 @@ from pathlib import Path
 import torch  # noqa: F401  (loads the HIP runtime first; see module docstring)
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libvqx.so"
-ABI_VERSION = 127  # include/vqx.h VQX_ABI_VERSION
+ABI_VERSION = 128  # include/vqx.h VQX_ABI_VERSION
 
 VQX_F32, VQX_BF16 = 0, 1
 PRO_NONE, PRO_LRELU, PRO_RELU, PRO_SCALE_RELU = 0, 1, 2, 3
@@ -67,6 +67,12 @@ class LinearLayer(ctypes.Structure):
                 ("dbias", c_void_p)]
 
 
+class StepClose(ctypes.Structure):  # include/vqx.h vqx_step_close
+    _fields_ = [("parts", c_void_p * 2), ("n", c_int32 * 2), ("scale", c_float * 2), ("out", c_void_p * 2),
+                ("pub_src", c_void_p), ("pub_n", c_int32), ("pub_copy", c_void_p), ("pub_box", c_void_p),
+                ("pub_slot", c_int32), ("pub_slots", c_int32), ("pub_floats", c_int32), ("pub_seq", ctypes.c_uint32)]
+
+
 WN_COLREDUCE = 2
 WN_RESAMPLE, WN_RESAMPLE_T = 3, 4  # strided Conv1d / ConvTranspose1d (include/vqx.h)
 
@@ -108,6 +114,8 @@ _SIGS = {
                             c_int32, c_void_p, c_void_p, c_void_p],
     "vqx_logloss_fwd_bwd_x": [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_float, c_void_p, c_int32,
                               c_int32, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p],
+    "vqx_logloss_parts": [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_float, c_void_p, c_int32, c_int32,
+                          c_void_p, c_void_p, c_void_p],
     "vqx_vq_forward": [c_void_p, c_int64, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_int32,
                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "vqx_vq_workspace": [c_int64, c_int32, c_int32, c_int32, c_void_p],
@@ -116,6 +124,8 @@ _SIGS = {
                           c_float, c_void_p, c_void_p, c_void_p],
     "vqx_vq_ema_update_clear": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_float,
                                 c_float, c_void_p, c_void_p, c_void_p],
+    "vqx_vq_ema_update_close": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_float,
+                                c_float, c_void_p, c_void_p, c_void_p, c_void_p],
     "vqx_gather_rows": [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_void_p, c_void_p],
     "vqx_gather_rows_host": [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_void_p, c_void_p],
     "vqx_vq_commit_bwd": [c_void_p, c_void_p, c_int64, c_float, c_void_p, c_int32, c_void_p],
@@ -131,6 +141,8 @@ _SIGS = {
     "vqx_linear_batched_fwd": [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p],
     "vqx_linear_batched_bwd": [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p],
     "vqx_linear_batched_fwd_ids": [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p],
+    "vqx_step_prologue": [c_void_p, c_void_p, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32,
+                          c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_int32, c_int32, c_void_p],
     "vqx_linear_batched_bwd_ids": [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p,
                                    c_void_p, c_void_p],
     "vqx_wgrad_tiles": [c_int64, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,

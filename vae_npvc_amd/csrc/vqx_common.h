@@ -118,6 +118,59 @@ __device__ __forceinline__ void block_sum_n(float (&v)[N], float (*scratch)[16])
   }
 }
 
+// N block sums as a block of NV * blockDim.x threads computes them with
+// block_sum_n (the same bits): thread t holds the values of virtual threads
+// t + j*blockDim.x (j < NV), whose virtual wave is w + j*waves; the virtual
+// waves' sums are added in order.  NV * waves <= 16.
+template <int N, int NV>
+__device__ __forceinline__ void block_sum_nv(float (&v)[N][NV], float (*scratch)[16], float (&out)[N]) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int k = 0; k < N; ++k)
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v[k][j] = wave_sum(v[k][j]);
+  __syncthreads();
+  if (l == 0) {
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+#pragma unroll
+      for (int j = 0; j < NV; ++j) scratch[k][w + j * nw] = v[k][j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    float t = 0.f;
+    for (int i = 0; i < nw * NV; ++i) t += scratch[k][i];
+    out[k] = t;
+  }
+}
+
+// Last-arriver hand-off between the workgroups of one launch (MI355X_MICROARCH.md
+// "inter-workgroup visibility", table row 1): every workgroup stores the words
+// it hands off with st_agent (sc1 stores), then calls arrive_last: each wave
+// waits for its stores, the barrier joins them, one lane adds to the
+// agent-scope counter, and the workgroup whose add returned n-1 (told to its
+// waves through LDS) gets true, resets the counter for the next launch and
+// reads the words with ld_agent (sc1 loads).  No workgroup waits for another.
+__device__ __forceinline__ void st_agent(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_agent(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool arrive_last(unsigned* counter, unsigned n) {
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == n - 1;
+    if (old == n - 1) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return last != 0;
+}
+
 // Bijective XCD-aware remap of a linear block id (guide §5 "XCD swizzle must
 // be bijective"): blocks b and b+8 share an XCD, so give each XCD group a
 // contiguous range of logical tiles.

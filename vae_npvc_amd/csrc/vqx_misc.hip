@@ -79,17 +79,18 @@ __host__ __device__ inline int wn_pack_units(const vqx_wn_layer& l) {
   if (l.kind == 0) return l.k == 1 ? (l.cout + 3) / 4 : l.cout;
   return ((l.cin + 63) / 64) * ((l.cout + wn_tco(l.k) - 1) / wn_tco(l.k));
 }
-__global__ __launch_bounds__(256) void wn_pack_kernel(const vqx_wn_layer* __restrict__ L, WnUnits U) {
-  int lo = 0, hi = U.n - 1;  // the layer owning this block: largest li with off[li] <= blockIdx.x
+// one unit of the flat grid (bid: the block's index in it); buf = kWnBuf
+// floats of LDS (16-B aligned), red = 16
+__device__ __forceinline__ void wn_pack_block(const vqx_wn_layer* __restrict__ L, const WnUnits& U, int bid,
+                                              float* __restrict__ buf, float* __restrict__ red) {
+  int lo = 0, hi = U.n - 1;  // the layer owning this block: largest li with off[li] <= bid
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
-    if (U.off[mid] <= (int)blockIdx.x) lo = mid; else hi = mid - 1;
+    if (U.off[mid] <= bid) lo = mid; else hi = mid - 1;
   }
   const vqx_wn_layer& l = L[lo];
-  const int unit = (int)blockIdx.x - U.off[lo];
+  const int unit = bid - U.off[lo];
   const int K = l.k, cin = l.cin, cout = l.cout;
-  __shared__ __attribute__((aligned(16))) float buf[kWnBuf];
-  __shared__ float red[16];
   if (l.kind == VQX_WN_RESAMPLE || l.kind == VQX_WN_RESAMPLE_T) {
     // strided conv (include/vqx.h): row r of v, norm, then the folded 3-tap row
     // w_packed[r][m][q*C + c] = w[r][c][S*(m-1) + q + pad]
@@ -293,6 +294,11 @@ __global__ __launch_bounds__(256) void wn_pack_kernel(const vqx_wn_layer* __rest
         st_dt(l.w_packed, ((int64_t)co * K + j) * cin + ci, buf[(cl * K + (K - 1 - j)) * 65 + r], l.dtype);
     }
   }
+}
+__global__ __launch_bounds__(256) void wn_pack_kernel(const vqx_wn_layer* __restrict__ L, WnUnits U) {
+  __shared__ __attribute__((aligned(16))) float buf[kWnBuf];
+  __shared__ float red[16];
+  wn_pack_block(L, U, (int)blockIdx.x, buf, red);
 }
 
 // Sum over splits sp0, sp0+step, ... < splits of the 4 slab values at element
@@ -932,7 +938,10 @@ __global__ __launch_bounds__(256) void gn_bwd_reduce_vec_kernel(const T* __restr
 // in one of 32 row groups and loads two rows before the math of either: the
 // kernel is bound by the loads in flight per CU, and 4 channels a thread keep
 // it at ~100 VGPRs (8 channels: 176, two waves per SIMD).
-constexpr int kGnApplyRG = 32, kGnApplyW = 4;
+#ifndef VQX_GN_NR  // rows in flight per thread in gn_bwd_apply_vec_kernel
+#define VQX_GN_NR 2
+#endif
+constexpr int kGnApplyRG = 32, kGnApplyW = 4, kGnApplyNR = VQX_GN_NR;
 template <typename T> struct Vec4;
 template <> struct Vec4<bf16_t> {
   typedef uint2 raw_t;
@@ -947,14 +956,6 @@ template <> struct Vec4<bf16_t> {
   }
 };
 template <> struct Vec4<float> : Vec<float> {};
-template <typename T>
-__device__ __forceinline__ void gn_row_load(const T* dy, int lddy, const T* u, int ldu, int64_t n, int c, int half,
-                                            bool glu, float (&g)[kGnApplyW], float (&ua)[kGnApplyW],
-                                            float (&ub)[kGnApplyW]) {
-  Vec4<T>::load(dy + n * lddy + c, g);
-  Vec4<T>::load(u + n * ldu + c, ua);
-  if (glu) Vec4<T>::load(u + n * ldu + c + half, ub);
-}
 template <typename T, bool GLU>
 __global__ __launch_bounds__(512) void gn_bwd_apply_vec_kernel(const T* __restrict__ dy, int lddy,
                                                                const T* __restrict__ u, int ldu, T* __restrict__ du,
@@ -998,17 +999,21 @@ __global__ __launch_bounds__(512) void gn_bwd_apply_vec_kernel(const T* __restri
     gb[i] = glu ? gamma[cc + half + i] : 0.f;
     bb[i] = glu ? beta[cc + half + i] : 0.f;
   }
-  // the first row pair as raw chunks (rows clamped into the utterance), converted after the sums
+  // the first NR rows as raw chunks (rows clamped into the utterance), converted after the sums
   typedef typename Vec4<T>::raw_t raw_t;
+  constexpr int NR = kGnApplyNR;
   const int64_t nb0 = (int64_t)b * T_;
-  const int64_t n0c = nb0 + min(rg, T_ - 1), n1c = nb0 + min(rg + RG, T_ - 1);
-  const raw_t pg0 = Vec4<T>::ld(dy + n0c * lddy + cc), pa0 = Vec4<T>::ld(u + n0c * ldu + cc);
-  const raw_t pg1 = Vec4<T>::ld(dy + n1c * lddy + cc), pa1 = Vec4<T>::ld(u + n1c * ldu + cc);
-  raw_t pb0{}, pb1{};
-  if (glu) {
-    pb0 = Vec4<T>::ld(u + n0c * ldu + cc + half);
-    pb1 = Vec4<T>::ld(u + n1c * ldu + cc + half);
-  }
+  raw_t pg[NR], pa[NR], pb[NR];
+  auto load_rows = [&](int r) {
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const int64_t nc = nb0 + min(r + k * RG, T_ - 1);
+      pg[k] = Vec4<T>::ld(dy + nc * lddy + cc);
+      pa[k] = Vec4<T>::ld(u + nc * ldu + cc);
+      pb[k] = glu ? Vec4<T>::ld(u + nc * ldu + cc + half) : raw_t{};
+    }
+  };
+  load_rows(rg);
   float m1a = 0.f, m2a = 0.f, m1b = 0.f, m2b = 0.f;
   {
     const int cg = C / G;
@@ -1061,30 +1066,20 @@ __global__ __launch_bounds__(512) void gn_bwd_apply_vec_kernel(const T* __restri
     }
   };
   if (active) {
-    int r = rg;
-    float g0[W], ua0[W], ub0[W], g1[W], ua1[W], ub1[W];
-    if (r + RG < T_) {  // the preloaded pair
-      Vec4<T>::cvt(pg0, g0); Vec4<T>::cvt(pa0, ua0);
-      Vec4<T>::cvt(pg1, g1); Vec4<T>::cvt(pa1, ua1);
-      if (glu) { Vec4<T>::cvt(pb0, ub0); Vec4<T>::cvt(pb1, ub1); }
-      row(nb0 + r, g0, ua0, ub0);
-      row(nb0 + r + RG, g1, ua1, ub1);
-      for (r += 2 * RG; r + RG < T_; r += 2 * RG) {
-        const int64_t n0 = nb0 + r, n1 = n0 + RG;
-        gn_row_load<T>(dy, lddy, u, ldu, n0, c, half, glu, g0, ua0, ub0);
-        gn_row_load<T>(dy, lddy, u, ldu, n1, c, half, glu, g1, ua1, ub1);
-        row(n0, g0, ua0, ub0);
-        row(n1, g1, ua1, ub1);
+    // NR rows in flight, processed in row order (the column sums' order does
+    // not depend on NR)
+    for (int r = rg; r < T_; r += NR * RG) {
+      if (r != rg) load_rows(r);
+#pragma unroll
+      for (int k = 0; k < NR; ++k) {
+        if (r + k * RG < T_) {
+          float g0[W], ua0[W], ub0[W];
+          Vec4<T>::cvt(pg[k], g0);
+          Vec4<T>::cvt(pa[k], ua0);
+          if (glu) Vec4<T>::cvt(pb[k], ub0);
+          row(nb0 + r + k * RG, g0, ua0, ub0);
+        }
       }
-      if (r < T_) {
-        const int64_t n0 = nb0 + r;
-        gn_row_load<T>(dy, lddy, u, ldu, n0, c, half, glu, g0, ua0, ub0);
-        row(n0, g0, ua0, ub0);
-      }
-    } else if (r < T_) {  // one row: the preloaded first
-      Vec4<T>::cvt(pg0, g0); Vec4<T>::cvt(pa0, ua0);
-      if (glu) Vec4<T>::cvt(pb0, ub0);
-      row(nb0 + r, g0, ua0, ub0);
     }
   }
   __shared__ float lds[RG][16][2 * W];
@@ -1366,11 +1361,11 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restri
 }
 
 // ------------------------------------------------------------------ layout
+// one 32 x 32 tile (bx over T, by over C, b the batch row); tile: LDS
 template <typename T>
-__global__ void nct_to_ntc_kernel(const float* __restrict__ x, int B, int C, int T_, T* __restrict__ y, int ldy) {
-  __shared__ float tile[32][33];
-  const int b = blockIdx.z;
-  const int t0 = blockIdx.x * 32, c0 = blockIdx.y * 32;
+__device__ __forceinline__ void nct_to_ntc_tile(const float* __restrict__ x, int C, int T_, T* __restrict__ y, int ldy,
+                                                int bx, int by, int b, float (*tile)[33]) {
+  const int t0 = bx * 32, c0 = by * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 8 rows per pass
   for (int i = ty; i < 32; i += 8) {
     const int c = c0 + i, t = t0 + tx;
@@ -1381,6 +1376,11 @@ __global__ void nct_to_ntc_kernel(const float* __restrict__ x, int B, int C, int
     const int t = t0 + i, c = c0 + tx;
     if (c < C && t < T_) Elem<T>::st(y, ((int64_t)b * T_ + t) * ldy + c, tile[tx][i]);
   }
+}
+template <typename T>
+__global__ void nct_to_ntc_kernel(const float* __restrict__ x, int B, int C, int T_, T* __restrict__ y, int ldy) {
+  __shared__ float tile[32][33];
+  nct_to_ntc_tile<T>(x, C, T_, y, ldy, blockIdx.x, blockIdx.y, blockIdx.z, tile);
 }
 
 template <typename T>
@@ -1779,13 +1779,13 @@ constexpr int kCondI = 128, kCondB = 64, kCondO = 64;
 // out_l[b][o] = bias_l[o] + sum_i c[b][i] W_l[o][i]; grid (O/64, n)
 // ids != null: row b of c is row ids[b] of c (the embedding table: the lookup
 // folded into the operand loads, vqx_linear_batched_fwd_ids)
-__global__ __launch_bounds__(256) void linear_cond_fwd_kernel(const vqx_linear_layer* __restrict__ L,
-                                                              const float* __restrict__ c,
-                                                              const int64_t* __restrict__ ids, int B, int O) {
-  const vqx_linear_layer& l = L[blockIdx.y];
+__device__ __forceinline__ void linear_cond_fwd_block(const vqx_linear_layer* __restrict__ L,
+                                                      const float* __restrict__ c, const int64_t* __restrict__ ids,
+                                                      int B, int O, int bx, int layer) {
+  const vqx_linear_layer& l = L[layer];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int q = lane >> 4, j = lane & 15;
-  const int o0 = blockIdx.x * kCondO + w * 16;
+  const int o0 = bx * kCondO + w * 16;
   // B operand (k = 32q + s, n = j): W[o0 + j][32q .. 32q + 31]
   f32x4_t wb[8];
   const float* wr = l.W + (int64_t)(o0 + j) * kCondI + 32 * q;
@@ -1814,6 +1814,40 @@ __global__ __launch_bounds__(256) void linear_cond_fwd_kernel(const vqx_linear_l
       if (b < B) l.out[(int64_t)b * O + o0 + j] = (acc[r] + acc2[r]) + bj;
     }
   }
+}
+__global__ __launch_bounds__(256) void linear_cond_fwd_kernel(const vqx_linear_layer* __restrict__ L,
+                                                              const float* __restrict__ c,
+                                                              const int64_t* __restrict__ ids, int B, int O) {
+  linear_cond_fwd_block(L, c, ids, B, O, blockIdx.x, blockIdx.y);
+}
+
+// The training step's prologue in one launch (vqx_step_prologue): the
+// conditioning linears (n_cond x O/64 blocks, latency-bound MFMA chains:
+// first, so they start first), the input transpose (32 x 32 tiles), then the
+// weight-norm pack units -- three independent jobs that ran as three
+// launches in turn (11 + 5 + 22 us).  Each block runs the body of the
+// launch it replaces, so the results are those launches' bits.
+template <typename T>
+__global__ __launch_bounds__(256) void step_prologue_kernel(const vqx_wn_layer* __restrict__ WL, WnUnits U,
+                                                            const vqx_linear_layer* __restrict__ CL, int n_cond_blocks,
+                                                            int cond_bx, const float* __restrict__ emb,
+                                                            const int64_t* __restrict__ ids, int B, int O,
+                                                            const float* __restrict__ x, int C, int T_, int tx_bx,
+                                                            int tx_by, int n_tx_blocks, T* __restrict__ y, int ldy) {
+  __shared__ __attribute__((aligned(16))) float buf[kWnBuf];
+  __shared__ float red[16];
+  int bid = (int)blockIdx.x;
+  if (bid < n_cond_blocks) {
+    linear_cond_fwd_block(CL, emb, ids, B, O, bid % cond_bx, bid / cond_bx);
+    return;
+  }
+  bid -= n_cond_blocks;
+  if (bid < n_tx_blocks) {
+    const int r = bid / tx_bx;
+    nct_to_ntc_tile<T>(x, C, T_, y, ldy, bid - r * tx_bx, r % tx_by, r / tx_by, (float(*)[33])buf);
+    return;
+  }
+  wn_pack_block(WL, U, bid - n_tx_blocks, buf, red);
 }
 
 // dW_l[o][i] = sum_b dout_l[b][o] c[b][i], dbias_l[o] = sum_b dout_l[b][o]; grid (O/64, n)
@@ -2518,30 +2552,27 @@ static int grid_for(int64_t n, int block = 256, int cap = 8192) {
   return (int)(g > cap ? cap : g);
 }
 
-static int wn_fwd_launch(const vqx_wn_layer* lh, const vqx_wn_layer* ld, int32_t n_layers, int32_t flags,
-                         vqx_stream_t stream) {
-  if (!lh || !ld || n_layers <= 0) { set_error("vqx_weight_norm_fwd: bad tables"); return -1; }
-  int max_rows = 1;
-  int64_t max_el = 1;
-  for (int i = 0; i < n_layers; ++i) {
-    const vqx_wn_layer& l = lh[i];
-    if (l.kind != 0 && l.kind != 1 && l.kind != VQX_WN_RESAMPLE && l.kind != VQX_WN_RESAMPLE_T) { set_error("vqx_weight_norm_fwd: layer %d bad kind", i); return -1; }
-    if (l.kind >= VQX_WN_RESAMPLE && !(l.stride >= 1 && l.pad >= 0 && l.pad <= l.stride && l.k - 1 - l.pad < 2 * l.stride)) { set_error("vqx_weight_norm_fwd: layer %d: resampling conv needs 0 <= pad <= stride and k-1-pad < 2*stride", i); return -1; }
-    const int rows = (l.kind == 0 || l.kind == VQX_WN_RESAMPLE) ? l.cout : l.cin;
-    max_rows = rows > max_rows ? rows : max_rows;
-    const int64_t el = (int64_t)l.cout * l.cin * l.k;
-    max_el = el > max_el ? el : max_el;
-  }
+// the pack kernel's limits on a host table; returns the most ConvT rows (the
+// norm pre-pass's grid) or -1 with the error set
+static int wn_fwd_check(const vqx_wn_layer* lh, int32_t n_layers, const char* who) {
   int max_t_rows = 1;
   for (int i = 0; i < n_layers; ++i) {
     const vqx_wn_layer& l = lh[i];
+    if (l.kind != 0 && l.kind != 1 && l.kind != VQX_WN_RESAMPLE && l.kind != VQX_WN_RESAMPLE_T) { set_error("%s: layer %d bad kind", who, i); return -1; }
+    if (l.kind >= VQX_WN_RESAMPLE && !(l.stride >= 1 && l.pad >= 0 && l.pad <= l.stride && l.k - 1 - l.pad < 2 * l.stride)) { set_error("%s: layer %d: resampling conv needs 0 <= pad <= stride and k-1-pad < 2*stride", who, i); return -1; }
     const bool rsm = l.kind >= VQX_WN_RESAMPLE;
     const bool row_is_cout = l.kind == 0 || l.kind == VQX_WN_RESAMPLE;
-    if ((row_is_cout ? l.cin : l.cout) * l.k > kWnRow || (!rsm && l.k > 64)) { set_error("vqx_weight_norm_fwd: layer %d row too long", i); return -1; }
+    if ((row_is_cout ? l.cin : l.cout) * l.k > kWnRow || (!rsm && l.k > 64)) { set_error("%s: layer %d row too long", who, i); return -1; }
     if (l.kind == 1) max_t_rows = l.cin > max_t_rows ? l.cin : max_t_rows;
   }
-  (void)max_el;
-  (void)max_rows;
+  return max_t_rows;
+}
+
+static int wn_fwd_launch(const vqx_wn_layer* lh, const vqx_wn_layer* ld, int32_t n_layers, int32_t flags,
+                         vqx_stream_t stream) {
+  if (!lh || !ld || n_layers <= 0) { set_error("vqx_weight_norm_fwd: bad tables"); return -1; }
+  const int max_t_rows = wn_fwd_check(lh, n_layers, "vqx_weight_norm_fwd");
+  if (max_t_rows < 0) return -1;
   hipStream_t s = (hipStream_t)stream;
   if (!(flags & VQX_WNF_NORMS_READY))
     hipLaunchKernelGGL(wn_norm_kernel, dim3(max_t_rows, n_layers), dim3(256), 0, s, ld, n_layers);
@@ -2865,9 +2896,11 @@ extern "C" int vqx_ntc_to_nct(const void* y, int32_t ldy, int32_t dtype, int32_t
   return launch_status("vqx_ntc_to_nct");
 }
 
+// loss_out == NULL: the partials only (their count in *n_parts), summed by the caller's later launch
 static int logloss_impl(const float* x, const float* xhat, int32_t ldxh, int32_t B, int32_t C, int32_t T,
                         float grad_scale, void* dxhat, int32_t lddx, int32_t dtype, float* loss_out, float* partials,
-                        const float* extra_parts, int32_t n_extra, float* extra_out, vqx_stream_t stream) {
+                        const float* extra_parts, int32_t n_extra, float* extra_out, vqx_stream_t stream,
+                        int32_t* n_parts = nullptr) {
   const int64_t total = (int64_t)B * C * T;
   if (total <= 0 || total >= (1LL << 31)) { set_error("vqx_logloss_fwd_bwd: B*C*T must be in [1, 2^31)"); return -1; }
   hipStream_t s = (hipStream_t)stream;
@@ -2889,6 +2922,8 @@ static int logloss_impl(const float* x, const float* xhat, int32_t ldxh, int32_t
     else
       hipLaunchKernelGGL(logloss_kernel<float>, dim3(grid), dim3(256), 0, s, x, xhat, ldxh, B, C, T, grad_scale, (float*)dxhat, lddx, partials);
   }
+  if (n_parts) *n_parts = grid;
+  if (!loss_out) return launch_status("vqx_logloss_parts");
   if (extra_parts)
     hipLaunchKernelGGL(sum_partials2_kernel, dim3(1), dim3(1024), 0, s, partials, grid, 1.0f / ((float)B * (float)T),
                        loss_out, extra_parts, n_extra, 1.0f, extra_out);
@@ -2902,6 +2937,14 @@ extern "C" int vqx_logloss_fwd_bwd(const float* x, const float* xhat, int32_t ld
                                    float* partials, vqx_stream_t stream) {
   return logloss_impl(x, xhat, ldxh, B, C, T, grad_scale, dxhat, lddx, dtype, loss_out, partials, nullptr, 0, nullptr,
                       stream);
+}
+
+extern "C" int vqx_logloss_parts(const float* x, const float* xhat, int32_t ldxh, int32_t B, int32_t C, int32_t T,
+                                 float grad_scale, void* dxhat, int32_t lddx, int32_t dtype, float* partials,
+                                 int32_t* n_parts, vqx_stream_t stream) {
+  if (!partials || !n_parts) { set_error("vqx_logloss_parts: needs partials and n_parts"); return -1; }
+  return logloss_impl(x, xhat, ldxh, B, C, T, grad_scale, dxhat, lddx, dtype, nullptr, partials, nullptr, 0, nullptr,
+                      stream, n_parts);
 }
 
 extern "C" int vqx_logloss_fwd_bwd_x(const float* x, const float* xhat, int32_t ldxh, int32_t B, int32_t C, int32_t T,
@@ -3191,6 +3234,37 @@ extern "C" int vqx_linear_batched_fwd_ids(const vqx_linear_layer* table_dev, int
   hipLaunchKernelGGL(linear_cond_fwd_kernel, dim3(O / kCondO, n), dim3(256), 0, (hipStream_t)stream, table_dev, emb, ids,
                      B, O);
   return launch_status("vqx_linear_batched_fwd_ids");
+}
+
+extern "C" int vqx_step_prologue(const vqx_wn_layer* wn_host, const vqx_wn_layer* wn_dev, int32_t n_wn,
+                                 const vqx_linear_layer* cond_table_dev, int32_t n_cond, const float* emb,
+                                 const int64_t* ids, int32_t B, int32_t I, int32_t O, const float* x_nct, int32_t xB,
+                                 int32_t C, int32_t T, void* y, int32_t ldy, int32_t y_dtype, vqx_stream_t stream) {
+  WnUnits U;
+  U.n = 0;
+  U.off[0] = 0;
+  if (n_wn < 0 || n_wn > kWnMaxL || (n_wn && (!wn_host || !wn_dev))) { set_error("vqx_step_prologue: 0 <= n_wn <= %d layers with both tables", kWnMaxL); return -1; }
+  if (n_wn) {
+    if (wn_fwd_check(wn_host, n_wn, "vqx_step_prologue") < 0) return -1;
+    U.n = n_wn;
+    for (int i = 0; i < n_wn; ++i) U.off[i + 1] = U.off[i] + wn_pack_units(wn_host[i]);
+  }
+  if (n_cond < 0 || (n_cond && !linear_ids_ok(cond_table_dev, n_cond, emb, ids, B, I, O, "vqx_step_prologue"))) return -1;
+  if (x_nct && (xB < 1 || C < 1 || T < 1 || !y || ldy < C || (y_dtype != VQX_F32 && y_dtype != VQX_BF16))) { set_error("vqx_step_prologue: bad transpose arguments"); return -1; }
+  const int cond_bx = n_cond ? O / kCondO : 1, n_cond_blocks = n_cond * (n_cond ? O / kCondO : 0);
+  const int tx_bx = x_nct ? (T + 31) / 32 : 1, tx_by = x_nct ? (C + 31) / 32 : 1;
+  const int64_t n_tx = x_nct ? (int64_t)tx_bx * tx_by * xB : 0;
+  const int64_t grid = n_cond_blocks + n_tx + U.off[U.n];
+  if (grid > INT32_MAX) { set_error("vqx_step_prologue: grid too large"); return -1; }
+  if (grid == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (y_dtype == VQX_BF16)
+    hipLaunchKernelGGL(step_prologue_kernel<bf16_t>, dim3((unsigned)grid), dim3(256), 0, s, wn_dev, U, cond_table_dev,
+                       n_cond_blocks, cond_bx, emb, ids, B, O, x_nct, C, T, tx_bx, tx_by, (int)n_tx, (bf16_t*)y, ldy);
+  else
+    hipLaunchKernelGGL(step_prologue_kernel<float>, dim3((unsigned)grid), dim3(256), 0, s, wn_dev, U, cond_table_dev,
+                       n_cond_blocks, cond_bx, emb, ids, B, O, x_nct, C, T, tx_bx, tx_by, (int)n_tx, (float*)y, ldy);
+  return launch_status("vqx_step_prologue");
 }
 
 extern "C" int vqx_linear_batched_bwd_ids(const vqx_linear_layer* table_dev, int32_t n, const float* emb,

@@ -484,20 +484,117 @@ __global__ void sum_partials_kernel(const float* __restrict__ p, int n, float sc
 }
 
 // EMA codebook update, one workgroup (layers_vq.py:203-233).
-// EMA update in two launches: the K*D elementwise update over many workgroups
+// EMA update in one launch: the K*D elementwise update over many workgroups
 // (one exact division per element; a single workgroup took ~48 us), each
-// writing its squared-difference partial; then one workgroup for the per-code
-// terms, the emb_elem update and the diagnostics, summing the partials in a
-// fixed order (deterministic).
-constexpr int kEmaElems = 1024;  // elements per workgroup of vq_ema_elem_kernel
+// storing its squared-difference partial; the last workgroup to finish
+// (arrive_last, counter after the partials) then runs the per-code terms, the
+// emb_elem update and the diagnostics, summing the partials in a fixed order
+// (deterministic).  Round 6: the per-code pass was a second, one-workgroup
+// launch (1024 threads; ~5 us).
+constexpr int kEmaElems = 1024;  // elements per workgroup of vq_ema_kernel
 
-__global__ __launch_bounds__(256) void vq_ema_elem_kernel(float* __restrict__ emb_sum,
-                                                          const float* __restrict__ emb_elem, float* __restrict__ E,
-                                                          const float* __restrict__ bsum,
-                                                          const float* __restrict__ bcnt,
-                                                          const float* __restrict__ rand_rows, int K, int D, float mu,
-                                                          float one_minus_mu, float thr, float* __restrict__ part,
-                                                          float* __restrict__ clear_sum) {
+// The step's closing work in the last workgroup (vqx_vq_ema_update_close):
+// up to two fixed-order sums (the log-loss total and the commitment sum that
+// sum_partials2_kernel computed) and the mailbox publish of the statistics
+// (mailbox_publish_kernel, vqx_runtime.hip).
+struct CloseArgs {
+  const float* parts[2];
+  int n[2];
+  float scale[2];
+  float* out[2];
+  const float* pub_src;
+  int pub_n;
+  float* pub_copy;
+  float* pub_box;     // the slot's values (mapped host memory)
+  uint32_t* pub_seqp;  // the slot's sequence number
+  uint32_t pub_seq;
+};
+
+// The per-code pass and the closing work in one 256-thread workgroup.  Every
+// sum is the one the 1024-thread launches it replaces formed (block_sum_nv:
+// four virtual threads per thread), so the diagnostics and the loss sums keep
+// their bits.
+constexpr int kEmaNV = 4;  // 1024 / 256
+__device__ __forceinline__ void ema_final_block(float* emb_elem, const float* bcnt, int K, int D, float mu,
+                                                float one_minus_mu, float thr, const float* __restrict__ part,
+                                                int nparts, float* __restrict__ diag, float* clear_cnt,
+                                                const CloseArgs& C) {
+  __shared__ float red[3][16];
+  constexpr int NV = kEmaNV;
+  const int nt = blockDim.x, vt = NV * nt;
+  if (C.parts[0] || C.parts[1]) {  // sum_partials2_kernel: thread-strided sums, then the block sum
+    float v[2][NV], o[2];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int t = threadIdx.x + j * nt;
+      v[0][j] = v[1][j] = 0.f;
+      for (int i = t; i < C.n[0]; i += vt) v[0][j] += C.parts[0][i];
+      for (int i = t; i < C.n[1]; i += vt) v[1][j] += C.parts[1][i];
+    }
+    block_sum_nv<2, NV>(v, red, o);
+    if (threadIdx.x == 0) {
+      if (C.out[0]) C.out[0][0] = o[0] * C.scale[0];
+      if (C.out[1]) C.out[1][0] = o[1] * C.scale[1];
+    }
+    __syncthreads();  // red is rewritten
+  }
+  float a[2][NV], ao[2];  // sum of squared codebook moves, total count
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int t = threadIdx.x + j * nt;
+    a[0][j] = a[1][j] = 0.f;
+    for (int b = t; b < nparts; b += vt) a[0][j] += ld_agent(part + b);
+    for (int k = t; k < K; k += vt) a[1][j] += bcnt[k];
+  }
+  block_sum_nv<2, NV>(a, red, ao);
+  const float dsq = ao[0], total = ao[1];
+  float e[3][NV], eo[3];  // entropy term, codes used this step, codes in use after the update
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int t = threadIdx.x + j * nt;
+    e[0][j] = e[1][j] = e[2][j] = 0.f;
+    for (int k = t; k < K; k += vt) {
+      const float c = bcnt[k];
+      const float p = c / total;
+      e[0][j] += p * logf(p + 1e-8f);
+      e[1][j] += (c >= thr) ? 1.f : 0.f;
+      const float el = __fadd_rn(__fmul_rn(mu, emb_elem[k]), __fmul_rn(one_minus_mu, c));
+      e[2][j] += (el >= thr) ? 1.f : 0.f;
+    }
+  }
+  __syncthreads();  // red is rewritten
+  block_sum_nv<3, NV>(e, red, eo);
+  for (int k = threadIdx.x; k < K; k += nt) {
+    emb_elem[k] = __fadd_rn(__fmul_rn(mu, emb_elem[k]), __fmul_rn(one_minus_mu, bcnt[k]));
+    if (clear_cnt) clear_cnt[k] = 0.f;  // every workgroup's reads of bcnt[k] are done (all arrived)
+  }
+  if (threadIdx.x == 0) {
+    diag[0] = expf(-eo[0]);
+    diag[1] = eo[1];
+    diag[2] = eo[2];
+    diag[3] = sqrtf(dsq) / sqrtf((float)K * (float)D);
+  }
+  if (!C.pub_seqp) return;
+  __syncthreads();  // thread 0's statistics (diag, sums) are in pub_src
+  const int t = threadIdx.x;
+  if (t < C.pub_n) {
+    const float v = C.pub_src[t];
+    if (C.pub_copy) C.pub_copy[t] = v;
+    __hip_atomic_store(C.pub_box + t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the values before the number
+  __syncthreads();
+  if (t == 0) __hip_atomic_store(C.pub_seqp, C.pub_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// emb_elem is read by every workgroup and rewritten by the last one, after
+// all have arrived (so not __restrict__)
+__global__ __launch_bounds__(256) void vq_ema_kernel(float* __restrict__ emb_sum, float* emb_elem,
+                                                     float* __restrict__ E, const float* __restrict__ bsum,
+                                                     const float* bcnt, const float* __restrict__ rand_rows, int K,
+                                                     int D, float mu, float one_minus_mu, float thr,
+                                                     float* __restrict__ part, float* clear_sum,
+                                                     float* __restrict__ diag, float* clear_cnt, CloseArgs C) {
   __shared__ float red[16];
   const int i0 = blockIdx.x * kEmaElems;
   const int n = K * D;
@@ -533,41 +630,9 @@ __global__ __launch_bounds__(256) void vq_ema_elem_kernel(float* __restrict__ em
     E[i] = newe;
   }
   dsq = block_sum(dsq, red);
-  if (threadIdx.x == 0) part[blockIdx.x] = dsq;
-}
-
-__global__ __launch_bounds__(1024) void vq_ema_final_kernel(float* __restrict__ emb_elem,
-                                                            const float* __restrict__ bcnt, int K, int D, float mu,
-                                                            float one_minus_mu, float thr,
-                                                            const float* __restrict__ part, int nparts,
-                                                            float* __restrict__ diag, float* __restrict__ clear_cnt) {
-  __shared__ float red[3][16];
-  float a[2] = {0.f, 0.f};  // sum of squared codebook moves, total count
-  for (int b = threadIdx.x; b < nparts; b += blockDim.x) a[0] += part[b];
-  for (int k = threadIdx.x; k < K; k += blockDim.x) a[1] += bcnt[k];
-  block_sum_n<2>(a, red);
-  const float dsq = a[0], total = a[1];
-  float e[3] = {0.f, 0.f, 0.f};  // entropy term, codes used this step, codes in use after the update
-  for (int k = threadIdx.x; k < K; k += blockDim.x) {
-    const float c = bcnt[k];
-    const float p = c / total;
-    e[0] += p * logf(p + 1e-8f);
-    e[1] += (c >= thr) ? 1.f : 0.f;
-    const float el = __fadd_rn(__fmul_rn(mu, emb_elem[k]), __fmul_rn(one_minus_mu, c));
-    e[2] += (el >= thr) ? 1.f : 0.f;
-  }
-  __syncthreads();  // red is rewritten
-  block_sum_n<3>(e, red);
-  for (int k = threadIdx.x; k < K; k += blockDim.x) {
-    emb_elem[k] = __fadd_rn(__fmul_rn(mu, emb_elem[k]), __fmul_rn(one_minus_mu, bcnt[k]));
-    if (clear_cnt) clear_cnt[k] = 0.f;  // this thread's every read of bcnt[k] is done (and the element kernel's)
-  }
-  if (threadIdx.x == 0) {
-    diag[0] = expf(-e[0]);
-    diag[1] = e[1];
-    diag[2] = e[2];
-    diag[3] = sqrtf(dsq) / sqrtf((float)K * (float)D);
-  }
+  if (threadIdx.x == 0) st_agent(part + blockIdx.x, dsq);
+  if (!arrive_last((unsigned*)(part + gridDim.x), gridDim.x)) return;
+  ema_final_block(emb_elem, bcnt, K, D, mu, one_minus_mu, thr, part, gridDim.x, diag, clear_cnt, C);
 }
 
 __global__ void gather_rows_kernel(const float* __restrict__ src, int ld, const int64_t* __restrict__ rows,
@@ -724,29 +789,61 @@ extern "C" int vqx_vq_stats(const float* z, int64_t n_rows, int32_t D, const int
 
 static int ema_update(float* emb_sum, float* emb_elem, float* E, const float* bsum, const float* bcnt,
                       const float* rand_rows, int32_t K, int32_t D, float mu, float threshold, float* diag,
-                      float* partials, bool clear, vqx_stream_t stream) {
-  if (K <= 0 || D <= 0 || !partials) { set_error("vqx_vq_ema_update: bad K/D or no partials"); return -1; }
+                      float* partials, bool clear, const vqx_step_close* close, vqx_stream_t stream) {
+  if (K <= 0 || D <= 0 || !partials || !diag) { set_error("vqx_vq_ema_update: bad K/D, no partials or no diag"); return -1; }
+  CloseArgs C{};
+  if (close) {
+    for (int i = 0; i < 2; ++i) {
+      if (close->parts[i] && (close->n[i] < 0 || !close->out[i])) { set_error("vqx_vq_ema_update_close: sum %d needs n >= 0 and an output", i); return -1; }
+      C.parts[i] = close->parts[i];
+      C.n[i] = close->parts[i] ? close->n[i] : 0;
+      C.scale[i] = close->scale[i];
+      C.out[i] = close->parts[i] ? close->out[i] : nullptr;
+    }
+    if (close->pub_box) {
+      const int n = close->pub_n, slots = close->pub_slots, fl = close->pub_floats, slot = close->pub_slot;
+      if (!close->pub_src || n < 1 || n > fl || fl > 64 || slot < 0 || slot >= slots) {
+        set_error("vqx_vq_ema_update_close: bad mailbox arguments");
+        return -1;
+      }
+      C.pub_src = close->pub_src;
+      C.pub_n = n;
+      C.pub_copy = close->pub_copy;
+      C.pub_seqp = (uint32_t*)close->pub_box + slot;
+      C.pub_box = (float*)((uint32_t*)close->pub_box + slots) + (size_t)slot * fl;
+      C.pub_seq = close->pub_seq;
+    }
+  }
   const float omm = (float)(1.0 - (double)mu);  // (1. - mu) in double, as the reference's Python float
   const int nb = (K * D + kEmaElems - 1) / kEmaElems;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(vq_ema_elem_kernel, dim3(nb), dim3(256), 0, s, emb_sum, emb_elem, E, bsum, bcnt, rand_rows, K,
-                     D, mu, omm, threshold, partials, clear ? (float*)bsum : nullptr);
-  hipLaunchKernelGGL(vq_ema_final_kernel, dim3(1), dim3(1024), 0, s, emb_elem, bcnt, K, D, mu, omm, threshold,
-                     partials, nb, diag, clear ? (float*)bcnt : nullptr);
+  hipLaunchKernelGGL(vq_ema_kernel, dim3(nb), dim3(256), 0, s, emb_sum, emb_elem, E, bsum, bcnt, rand_rows, K, D, mu,
+                     omm, threshold, partials, clear ? (float*)bsum : nullptr, diag, clear ? (float*)bcnt : nullptr, C);
   return launch_status("vqx_vq_ema_update");
 }
 
 extern "C" int vqx_vq_ema_update(float* emb_sum, float* emb_elem, float* E, const float* bsum, const float* bcnt,
                                  const float* rand_rows, int32_t K, int32_t D, float mu, float threshold, float* diag,
                                  float* partials, vqx_stream_t stream) {
-  return ema_update(emb_sum, emb_elem, E, bsum, bcnt, rand_rows, K, D, mu, threshold, diag, partials, false, stream);
+  return ema_update(emb_sum, emb_elem, E, bsum, bcnt, rand_rows, K, D, mu, threshold, diag, partials, false, nullptr,
+                    stream);
 }
 
 extern "C" int vqx_vq_ema_update_clear(float* emb_sum, float* emb_elem, float* E, float* bsum, float* bcnt,
                                        const float* rand_rows, int32_t K, int32_t D, float mu, float threshold,
                                        float* diag, float* partials, vqx_stream_t stream) {
   if (!bsum || !bcnt) { set_error("vqx_vq_ema_update_clear: null statistics"); return -1; }
-  return ema_update(emb_sum, emb_elem, E, bsum, bcnt, rand_rows, K, D, mu, threshold, diag, partials, true, stream);
+  return ema_update(emb_sum, emb_elem, E, bsum, bcnt, rand_rows, K, D, mu, threshold, diag, partials, true, nullptr,
+                    stream);
+}
+
+extern "C" int vqx_vq_ema_update_close(float* emb_sum, float* emb_elem, float* E, float* bsum, float* bcnt,
+                                       const float* rand_rows, int32_t K, int32_t D, float mu, float threshold,
+                                       float* diag, float* partials, const vqx_step_close* close,
+                                       vqx_stream_t stream) {
+  if (!close) { set_error("vqx_vq_ema_update_close: null close arguments"); return -1; }
+  return ema_update(emb_sum, emb_elem, E, bsum, bcnt, rand_rows, K, D, mu, threshold, diag, partials, true, close,
+                    stream);
 }
 
 extern "C" int vqx_gather_rows(const float* src, int32_t ld_src, const int64_t* rows, int32_t n_out, int32_t D,

@@ -202,7 +202,17 @@ class EngineOptions:
       debug_checks     out-of-extent write detection (vae_npvc_amd/debug.py):
                        every engine buffer between guard canaries checked
                        after every libvqx call, and host extent checks of
-                       every pointer argument; slow, for audits only"""
+                       every pointer argument; slow, for audits only
+      fused_prologue   the training forward's three independent first jobs
+                       (ConvT weight packs, conditioning linears, input
+                       transpose) as one launch (vqx_step_prologue) when the
+                       last optimizer step left the row norms current; the
+                       same bits as the three launches
+      fused_close      the forward's closing work -- the log-loss and
+                       commitment sums, the step statistics' mailbox publish --
+                       in the EMA update's last workgroup
+                       (vqx_vq_ema_update_close): two one-workgroup launches
+                       fewer, the same bits"""
     fuse_gn: bool = True
     enc_gn_finalize: bool = False
     side_stream: bool = False
@@ -221,6 +231,8 @@ class EngineOptions:
     debug_checks: bool = False
     wgrad_fixup: bool = False
     early_stats: bool = True
+    fused_prologue: bool = True
+    fused_close: bool = True
 
 
 class _Stage:
@@ -278,7 +290,7 @@ class Workspace:
         self.bsum = self.ema[: K * Z].view(K, Z)
         self.bcnt = self.ema[K * Z: K * Z + K]
         self.rand_rows = self.ema[K * Z + K:].view(K, Z)
-        self.ema_part = e((K * Z + 1023) // 1024, dt=F32)  # vqx_vq_ema_update workspace
+        self.ema_part = eng._zeros(ops.ema_workspace(K, Z), dtype=F32)  # vqx_vq_ema_update workspace (+ counter)
         self.yemb = e(B, d["ydim"], dt=F32)
         # ---- decoder stages
         self.dec = []
@@ -984,6 +996,9 @@ class VQVAEEngine:
                 self._check_packed()
         else:
             ops.weight_norm_fwd(self.wn_fwd_table)
+        self._up_bias()
+
+    def _up_bias(self):
         for st in self.dec_stages:
             if st.conv.kind == KIND_UP:  # the up-sampler's bias, once per folded frame
                 s = st.conv.scale
@@ -1030,8 +1045,33 @@ class VQVAEEngine:
                 for b in blocks:
                     ops.linear_f32(w.yemb, b.cond.wp, b.cond.mod.bias, w.dec[b.key[1]].condbias[b.key[2]])
 
-    def encoder_fwd(self, w, x_nct):
-        ops.nct_to_ntc(x_nct, w.x)
+    def _fused_prologue(self, w, x):
+        """pack_weights + embed_and_cond + the encoder's input transpose as one
+        launch (ops.step_prologue) when the shapes allow; False: nothing done."""
+        plan = self._adam_wn
+        if (not self.opt.fused_prologue or self._side_on or plan is None
+                or self._packed_version != self._param_version() or not x.is_contiguous()):
+            return False
+        if plan[2] is not None and (len(plan[2][0]) > 256 or not (plan[3] & ops.WNF_NORMS_READY
+                                                                  or all(e.kind != 1 for e in plan[2][0]))):
+            return False  # the launch skips the ConvT norm pre-pass
+        cond = None
+        if len(self.cond_groups) == 1 and self._cond_ids(w, w.y_dev):
+            (O, blocks), = self.cond_groups.items()
+            w.cond_ids_mode = True
+            cond = (w.cond_tables[O], self.m.embeds._embedding.weight, w.y_dev, w.B, blocks[0].cond.cin, O)
+        else:  # several widths or a conditioning input the launch does not take: its own launches
+            self.embed_and_cond(w, w.y_dev)
+        ops.step_prologue(plan[2], cond, x, w.x)
+        self._up_bias()
+        if self._guards is not None:
+            self._check_packed()
+        self.n_fused_prologue = getattr(self, "n_fused_prologue", 0) + 1
+        return True
+
+    def encoder_fwd(self, w, x_nct, transposed=False):
+        if not transposed:
+            ops.nct_to_ntc(x_nct, w.x)
         inp, T_in = w.x, w.T
         for si, st in enumerate(self.enc_stages):
             sw = w.enc[si]
@@ -1535,13 +1575,14 @@ class VQVAEEngine:
             perm = self._perm_rows(w.Nz * self.world, K, self.rank * w.Nz, w.Nz if self.comm is not None else None)
             ops.gather_rows_host(w.z, perm, w.rand_rows)
 
-    def _ema_apply(self, w):
+    def _ema_apply(self, w, sums=(), publish=None):
         """The EMA update; it leaves bsum / bcnt zero (clear=True), so the next
         step's accumulation needs no zero fill of the statistics."""
         q = self.m.quantizer
-        ops.vq_ema_update(q.emb_sum, q.emb_elem, q.embeddings, w.bsum, w.bcnt, w.rand_rows, q.mu, q.threshold,
-                          w.stats[4:8], w.ema_part, clear=True)
+        res = ops.vq_ema_update(q.emb_sum, q.emb_elem, q.embeddings, w.bsum, w.bcnt, w.rand_rows, q.mu, q.threshold,
+                                w.stats[4:8], w.ema_part, clear=True, sums=sums, publish=publish)
         w.ema_clean = True
+        return res
 
     def vq_ema_update(self, w):
         """End of the step: apply the EMA update (or, when it ran on the side
@@ -1557,12 +1598,13 @@ class VQVAEEngine:
             return
         self._ema_finish(w)
 
-    def _ema_finish(self, w):
-        """Wait for the EMA bundle's all-reduce (data parallel), then update."""
+    def _ema_finish(self, w, sums=(), publish=None):
+        """Wait for the EMA bundle's all-reduce (data parallel), then update
+        (sums / publish: ops.vq_ema_update's closing work; returns its (seq, slot))."""
         if getattr(self, "_ema_work", None) is not None:
             self.comm.wait(self._ema_work, "ema")
             self._ema_work = None
-        self._ema_apply(w)
+        return self._ema_apply(w, sums, publish)
 
     # ------------------------------------------------------------ full step
     world, rank, comm = 1, 0, None
@@ -1584,16 +1626,18 @@ class VQVAEEngine:
         w = self.ws(B, T, train=True)
         w.y_dev = y.reshape(-1)
         w.x_nct = x
-        self.pack_weights()
         w.ev_cond = None
-        if self._side_on:  # the conditioning row biases are first read by the decoder
-            side = self._fork()
-            with torch.cuda.stream(side):
+        fused = self._fused_prologue(w, x)
+        if not fused:
+            self.pack_weights()
+            if self._side_on:  # the conditioning row biases are first read by the decoder
+                side = self._fork()
+                with torch.cuda.stream(side):
+                    self.embed_and_cond(w, w.y_dev)
+                w.ev_cond = side.record_event()
+            else:
                 self.embed_and_cond(w, w.y_dev)
-            w.ev_cond = side.record_event()
-        else:
-            self.embed_and_cond(w, w.y_dev)
-        self.encoder_fwd(w, x)
+        self.encoder_fwd(w, x, transposed=fused)
         self.vq_forward_train(w)
         w.zq_in = w.zq_c
         w.jittered = False
@@ -1607,7 +1651,18 @@ class VQVAEEngine:
             torch.cuda.current_stream().wait_event(w.ev_cond)
         self.decoder_fwd(w, w.zq_in)
         n_vq = getattr(w, "vq_sum_pending", 0)
-        if n_vq:  # the VQ commitment partials summed in the log-loss's final launch
+        close = self.opt.fused_close and not self._side_on and not self.plain
+        sums = ()
+        if close:
+            # the log-loss partials (and the VQ commitment partials) summed in the
+            # EMA update's last workgroup (vqx_vq_ema_update_close), as the
+            # log-loss's final launch would: the same scale, in float32
+            n_l = ops.logloss_parts(x, w.xhat, 1.0 / (B * T), w.dxhat, w.loss_part)
+            sums = [(w.loss_part[:n_l], float(np.float32(1.0) / (np.float32(B) * np.float32(T))), w.stats[0:1])]
+            if n_vq:
+                sums.append((w.vq_part[:n_vq], 1.0, w.stats[1:2]))
+            w.vq_sum_pending = 0
+        elif n_vq:  # the VQ commitment partials summed in the log-loss's final launch
             ops.logloss_fwd_bwd_x(x, w.xhat, 1.0 / (B * T), w.dxhat, w.stats[0:1], w.loss_part, w.vq_part[:n_vq],
                                   w.stats[1:2])
             w.vq_sum_pending = 0
@@ -1621,17 +1676,25 @@ class VQVAEEngine:
         # backward).  The side-stream schedule keeps its end-of-step join.
         w.stats_snap = None
         if not self._side_on:
-            if not self.plain:
-                self._ema_finish(w)
-                w.ema_applied = True
-            if self.opt.lazy_stats and self.opt.early_stats:
-                # published into a host mailbox (ops.Mailbox, vqx_mailbox_publish): the
-                # host polls a sequence number, so no event marker enters the stream
-                # (a recorded event idled it ~6 us at every step)
+            publish = self.opt.lazy_stats and self.opt.early_stats
+            if publish:
+                # published into a host mailbox (ops.Mailbox): the host polls a
+                # sequence number, so no event marker enters the stream (a
+                # recorded event idled it ~6 us at every step)
                 if self._mailbox is None:
                     self._mailbox = ops.Mailbox(64, 16)
                 snap = torch.empty_like(w.stats)  # the device copy, for reads after the slot was reused
-                seq, slot = self._mailbox.publish(w.stats, snap)
+            if close:  # the sums and the publish in the EMA update's last workgroup
+                seq, slot = self._ema_finish(w, sums=sums, publish=(self._mailbox, w.stats, snap) if publish else None) \
+                    or (None, None)
+                w.ema_applied = True
+            else:
+                if not self.plain:
+                    self._ema_finish(w)
+                    w.ema_applied = True
+                if publish:
+                    seq, slot = self._mailbox.publish(w.stats, snap)  # vqx_mailbox_publish
+            if publish:
                 w.stats_snap = (self._mailbox, seq, slot, snap, torch.cuda.current_stream())
         return w
 

@@ -583,6 +583,32 @@ def nct_to_ntc(x_nct, y):
     return y
 
 
+def step_prologue(wn_table=None, cond=None, x_nct=None, y=None):
+    """One launch for weight_norm_fwd(wn_table, flags=WNF_NORMS_READY),
+    linear_batched_fwd_ids(*cond) and nct_to_ntc(x_nct, y), with their bits
+    (vqx_step_prologue).  cond = (table, emb, ids, B, I, O); any job may be None."""
+    wh, wd, nw = None, 0, 0
+    if wn_table is not None:
+        arr, dev = wn_table
+        wh, wd, nw = ctypes.addressof(arr), dev.data_ptr(), len(arr)
+    cd, nc, emb_p, ids_p, B, I, O = 0, 0, 0, 0, 0, 0, 0
+    if cond is not None:
+        (arr, dev), emb, ids, B, I, O = cond
+        _check_cuda(emb, ids)
+        if ids.dtype != torch.int64 or ids.numel() != B:
+            raise ValueError("step_prologue: B int64 ids")
+        _linear_extents(arr, B, I, O)
+        cd, nc, emb_p, ids_p = dev.data_ptr(), len(arr), ptr(emb), ptr(ids)
+    xp, xB, C, T, yp, ldy, ydt = 0, 0, 0, 0, 0, 0, 0
+    if x_nct is not None:
+        _check_cuda(x_nct, y)
+        xB, C, T = x_nct.shape
+        if not x_nct.is_contiguous() or y.dim() != 2 or y.shape[0] != xB * T or y.shape[1] < C or y.stride(1) != 1:
+            raise ValueError(f"step_prologue: x {tuple(x_nct.shape)} into y {tuple(y.shape)}")
+        xp, yp, ldy, ydt = ptr(x_nct), ptr(y), y.stride(0), dt_code(y.dtype)
+    call("vqx_step_prologue", wh, wd, nw, cd, nc, emb_p, ids_p, B, I, O, xp, xB, C, T, yp, ldy, ydt, stream_ptr())
+
+
 def ntc_to_nct(y, x_nct):
     B, C, T = x_nct.shape
     call("vqx_ntc_to_nct", ptr(y), y.stride(0), dt_code(y.dtype), B, C, T, ptr(x_nct), stream_ptr())
@@ -595,6 +621,19 @@ def logloss_fwd_bwd(x_nct, xhat, grad_scale, dxhat, loss_out, partials):
          dxhat.stride(0) if dxhat is not None else 0, dt_code(dxhat.dtype) if dxhat is not None else 0,
          ptr(loss_out), ptr(partials), stream_ptr())
     return loss_out
+
+
+def logloss_parts(x_nct, xhat, grad_scale, dxhat, partials):
+    """logloss_fwd_bwd without its final sum launch: the per-workgroup partials
+    only; returns their count (vq_ema_update(close=...) sums them)."""
+    B, C, T = x_nct.shape
+    n = ctypes.c_int32(0)
+    call("vqx_logloss_parts", ptr(x_nct), ptr(xhat), xhat.stride(0), B, C, T, grad_scale, ptr(dxhat),
+         dxhat.stride(0) if dxhat is not None else 0, dt_code(dxhat.dtype) if dxhat is not None else 0,
+         ptr(partials), ctypes.byref(n), stream_ptr())
+    if n.value > partials.numel():
+        raise L.VqxError(f"logloss_parts: {n.value} partials written into a buffer of {partials.numel()}")
+    return n.value
 
 
 def logloss_fwd_bwd_x(x_nct, xhat, grad_scale, dxhat, loss_out, partials, extra_partials, extra_out):
@@ -647,20 +686,52 @@ def vq_stats(z, idx, K, partials, bsum, bcnt):
     call("vqx_vq_stats", ptr(z), N, D, ptr(idx), K, ptr(partials), ptr(bsum), ptr(bcnt), stream_ptr())
 
 
-def vq_ema_update(emb_sum, emb_elem, E, bsum, bcnt, rand_rows, mu, threshold, diag, partials=None, clear=False):
-    """partials: workspace of ceil(K*D/1024) floats (allocated here if None);
-    clear: bsum / bcnt are zero afterwards (vqx_vq_ema_update_clear)."""
+def ema_workspace(K, D):
+    """Floats of vq_ema_update's workspace: the per-workgroup partials and the arrival counter."""
+    return (K * D + 1023) // 1024 + 1
+
+
+def vq_ema_update(emb_sum, emb_elem, E, bsum, bcnt, rand_rows, mu, threshold, diag, partials=None, clear=False,
+                  sums=(), publish=None):
+    """partials: workspace of ceil(K*D/1024) + 1 floats, zero-initialised once
+    (the last word is an arrival counter each call leaves zero; allocated here
+    if None); clear: bsum / bcnt are zero afterwards (vqx_vq_ema_update_clear).
+    sums: up to two (parts, scale, out) -- out[0] = scale * sum(parts) in the
+    last workgroup; publish: (mailbox, src, dev_copy) -- src published into the
+    Mailbox after them (vqx_vq_ema_update_close, which implies clear).  Returns
+    publish's (seq, slot), else None."""
     K, D = E.shape
+    need = ema_workspace(K, D)
     if partials is None:
-        partials = torch.empty((K * D + 1023) // 1024, device=E.device, dtype=torch.float32)
-    if partials.numel() < (K * D + 1023) // 1024:
-        raise ValueError(f"vq_ema_update: workspace {partials.numel()} < {(K * D + 1023) // 1024} floats")
+        partials = torch.zeros(need, device=E.device, dtype=torch.float32)
+    if partials.numel() < need:
+        raise ValueError(f"vq_ema_update: workspace {partials.numel()} < {need} floats")
     if _debug:
         for t, n, what in ((emb_sum, K * D, "emb_sum"), (emb_elem, K, "emb_elem"), (bsum, K * D, "bsum"),
                            (bcnt, K, "bcnt"), (rand_rows, K * D, "rand_rows"), (diag, 4, "diag")):
             _span(t, n, f"vq_ema_update {what}")
-    call("vqx_vq_ema_update_clear" if clear else "vqx_vq_ema_update", ptr(emb_sum), ptr(emb_elem), ptr(E), ptr(bsum), ptr(bcnt), ptr(rand_rows), K, D,
-         mu, threshold, ptr(diag), ptr(partials), stream_ptr())
+    if not sums and publish is None:
+        call("vqx_vq_ema_update_clear" if clear else "vqx_vq_ema_update", ptr(emb_sum), ptr(emb_elem), ptr(E), ptr(bsum),
+             ptr(bcnt), ptr(rand_rows), K, D, mu, threshold, ptr(diag), ptr(partials), stream_ptr())
+        return None
+    if not clear or len(sums) > 2:
+        raise ValueError("vq_ema_update: sums / publish need clear=True and at most two sums")
+    c = L.StepClose()
+    for i, (parts, scale, out) in enumerate(sums):
+        _check_cuda(parts, out)
+        c.parts[i], c.n[i], c.scale[i], c.out[i] = ptr(parts), parts.numel(), float(scale), ptr(out)
+    res = None
+    if publish is not None:
+        mb, src, copy = publish
+        _check_cuda(src, copy)
+        if src.numel() > mb.floats or not src.is_contiguous() or src.dtype != torch.float32:
+            raise ValueError(f"vq_ema_update: publish a contiguous f32 tensor of <= {mb.floats} values")
+        seq, slot = res = mb.reserve()
+        c.pub_src, c.pub_n, c.pub_copy, c.pub_box = ptr(src), src.numel(), ptr(copy), mb._dev
+        c.pub_slot, c.pub_slots, c.pub_floats, c.pub_seq = slot, mb.slots, mb.floats, seq
+    call("vqx_vq_ema_update_close", ptr(emb_sum), ptr(emb_elem), ptr(E), ptr(bsum), ptr(bcnt), ptr(rand_rows), K, D,
+         mu, threshold, ptr(diag), ptr(partials), ctypes.addressof(c), stream_ptr())
+    return res
 
 
 def gather_rows(src, rows, out):
@@ -873,11 +944,16 @@ class Mailbox:
         n = src.numel()
         if n > self.floats or not src.is_contiguous() or src.dtype != torch.float32:
             raise ValueError(f"Mailbox.publish: contiguous f32 tensor of <= {self.floats} values")
-        seq, self._next = self._next, self._next + 1
-        slot = seq % self.slots
+        seq, slot = self.reserve()
         call("vqx_mailbox_publish", ptr(src), n, ptr(dev_copy), self._dev, slot, self.slots, self.floats, seq,
              stream_ptr())
         return seq, slot
+
+    def reserve(self):
+        """The next (seq, slot), for a launch that publishes itself
+        (vq_ema_update(publish=...))."""
+        seq, self._next = self._next, self._next + 1
+        return seq, seq % self.slots
 
     def try_read(self, seq, slot, n):
         """The values of `seq` once published (None while pending); raises
