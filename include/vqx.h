@@ -444,7 +444,12 @@ int vqx_vq_ema_update_clear(float* emb_sum, float* emb_elem, float* E, float* bs
  *     scale 1/(B*T); the commitment sum from vqx_vq_forward's partials);
  *   then, with pub_box != NULL, pub_src[0 .. pub_n) published into mailbox
  *     slot pub_slot with number pub_seq as vqx_mailbox_publish does, after
- *     the sums and diag are stored (pub_src may hold them).
+ *     the sums and diag are stored (pub_src may hold them);
+ *   with rows_src != NULL, the dead-code rows read straight from it: row k of
+ *     rand_rows is rows_src[rows_host[k] * rows_ld ..] (a zero row for a
+ *     negative index; rows_host: n_rows == K <= 512 host int32 indices, copied
+ *     into the launch's arguments; rand_rows is then not read and may be
+ *     NULL): vqx_gather_rows_host folded in.
  * The values equal those of the separate launches bit for bit. */
 typedef struct {
   const float* parts[2];
@@ -457,6 +462,9 @@ typedef struct {
   void* pub_box;       /* vqx_mailbox_create's device pointer, or NULL */
   int32_t pub_slot, pub_slots, pub_floats;
   uint32_t pub_seq;
+  const float* rows_src;   /* z, or NULL: rand_rows as given */
+  int32_t rows_ld, n_rows;
+  const int32_t* rows_host;
 } vqx_step_close;
 int vqx_vq_ema_update_close(float* emb_sum, float* emb_elem, float* E, float* bsum, float* bcnt,
                             const float* rand_rows, int32_t K, int32_t D, float mu, float threshold, float* diag,

@@ -1491,13 +1491,15 @@ def test_step_prologue_equals_the_three_launches(jobs, dtype):
         assert bool(ya.abs().sum() > 0)
 
 
-@pytest.mark.parametrize("n_vq", [0, 512])
-def test_ema_update_close_equals_the_separate_launches(n_vq):
+@pytest.mark.parametrize("n_vq,rows", [(0, False), (512, False), (512, True)])
+def test_ema_update_close_equals_the_separate_launches(n_vq, rows):
     """vqx_vq_ema_update_close (ABI 128) = vqx_logloss_fwd_bwd(_x)'s sums +
     vqx_vq_ema_update_clear + vqx_mailbox_publish, bit for bit: the loss and
     commitment sums, codebook, EMA buffers, diagnostics (the 1024-thread sums
     formed by four virtual threads per thread) and the published values, with
-    the arrival counter left zero for the next call."""
+    the arrival counter left zero for the next call; rows: the dead-code rows
+    read from z inside the launch = vqx_gather_rows_host first (negative
+    indices: zero rows)."""
     ops = _ops()
     g = torch.Generator(device="cpu").manual_seed(23)
     K, D, B, C, T = 512, 64, 8, 80, 200
@@ -1507,6 +1509,9 @@ def test_ema_update_close_equals_the_separate_launches(n_vq):
     x = torch.randn(B, C, T, generator=g).to(DEV)
     xhat = torch.randn(B * T, C, generator=g).to(DEV)
     vq_part = torch.rand(max(n_vq, 1), generator=g).to(DEV)
+    z = torch.randn(3000, D, generator=g).to(DEV)
+    perm = torch.randperm(3000, generator=g)[:K].to(torch.int32)
+    perm[::7] = -1
     mb = ops.Mailbox(slots=4, floats=16)
     res = []
     for fused in (False, True):
@@ -1526,12 +1531,14 @@ def test_ema_update_close_equals_the_separate_launches(n_vq):
                     sums.append((vq_part[:n_vq], 1.0, stats[1:2]))
                 seq, slot = ops.vq_ema_update(t["emb_sum"], t["emb_elem"], t["E"], t["bsum"], t["bcnt"], t["rand"],
                                               0.99, 1.0, stats[4:8], part, clear=True, sums=sums,
-                                              publish=(mb, stats, copy))
+                                              publish=(mb, stats, copy), rows=(z, perm) if rows else None)
             else:
                 if n_vq:
                     ops.logloss_fwd_bwd_x(x, xhat, 1.0 / (B * T), dx, stats[0:1], lp, vq_part[:n_vq], stats[1:2])
                 else:
                     ops.logloss_fwd_bwd(x, xhat, 1.0 / (B * T), dx, stats[0:1], lp)
+                if rows:
+                    ops.gather_rows_host(z, perm, t["rand"])
                 ops.vq_ema_update(t["emb_sum"], t["emb_elem"], t["E"], t["bsum"], t["bcnt"], t["rand"], 0.99, 1.0,
                                   stats[4:8], part, clear=True)
                 seq, slot = mb.publish(stats, copy)

@@ -70,7 +70,8 @@ class LinearLayer(ctypes.Structure):
 class StepClose(ctypes.Structure):  # include/vqx.h vqx_step_close
     _fields_ = [("parts", c_void_p * 2), ("n", c_int32 * 2), ("scale", c_float * 2), ("out", c_void_p * 2),
                 ("pub_src", c_void_p), ("pub_n", c_int32), ("pub_copy", c_void_p), ("pub_box", c_void_p),
-                ("pub_slot", c_int32), ("pub_slots", c_int32), ("pub_floats", c_int32), ("pub_seq", ctypes.c_uint32)]
+                ("pub_slot", c_int32), ("pub_slots", c_int32), ("pub_floats", c_int32), ("pub_seq", ctypes.c_uint32),
+                ("rows_src", c_void_p), ("rows_ld", c_int32), ("n_rows", c_int32), ("rows_host", c_void_p)]
 
 
 WN_COLREDUCE = 2

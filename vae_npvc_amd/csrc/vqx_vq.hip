@@ -493,6 +493,12 @@ __global__ void sum_partials_kernel(const float* __restrict__ p, int n, float sc
 // launch (1024 threads; ~5 us).
 constexpr int kEmaElems = 1024;  // elements per workgroup of vq_ema_kernel
 
+// row indices passed by value (vqx_gather_rows_host): kernel arguments, no copy on the stream
+constexpr int kGatherArgRows = 512;
+struct GatherIdx {
+  int32_t idx[kGatherArgRows];
+};
+
 // The step's closing work in the last workgroup (vqx_vq_ema_update_close):
 // up to two fixed-order sums (the log-loss total and the commitment sum that
 // sum_partials2_kernel computed) and the mailbox publish of the statistics
@@ -594,7 +600,8 @@ __global__ __launch_bounds__(256) void vq_ema_kernel(float* __restrict__ emb_sum
                                                      const float* bcnt, const float* __restrict__ rand_rows, int K,
                                                      int D, float mu, float one_minus_mu, float thr,
                                                      float* __restrict__ part, float* clear_sum,
-                                                     float* __restrict__ diag, float* clear_cnt, CloseArgs C) {
+                                                     float* __restrict__ diag, float* clear_cnt, CloseArgs C,
+                                                     const float* __restrict__ rsrc, int rld, GatherIdx R) {
   __shared__ float red[16];
   const int i0 = blockIdx.x * kEmaElems;
   const int n = K * D;
@@ -611,7 +618,12 @@ __global__ __launch_bounds__(256) void vq_ema_kernel(float* __restrict__ emb_sum
     bs[u] = bsum[i];
     ee[u] = emb_elem[k];
     bc[u] = bcnt[k];
-    rr[u] = rand_rows[i];
+    if (rsrc) {  // the dead-code row straight from z (vqx_step_close.rows_src; negative: a zero row)
+      const int r = R.idx[k];
+      rr[u] = r >= 0 ? rsrc[(int64_t)r * rld + (i - k * D)] : 0.f;
+    } else {
+      rr[u] = rand_rows[i];
+    }
     eo[u] = E[i];
   }
 #pragma unroll
@@ -643,11 +655,6 @@ __global__ void gather_rows_kernel(const float* __restrict__ src, int ld, const 
   for (int d = threadIdx.x; d < D; d += blockDim.x) out[(int64_t)i * D + d] = (r >= 0) ? src[r * ld + d] : 0.f;
 }
 
-// row indices passed by value (vqx_gather_rows_host): kernel arguments, no copy on the stream
-constexpr int kGatherArgRows = 512;
-struct GatherIdx {
-  int32_t idx[kGatherArgRows];
-};
 __global__ void gather_rows_arg_kernel(const float* __restrict__ src, int ld, GatherIdx R, int n_out, int D,
                                        float* __restrict__ out) {
   const int i = blockIdx.x;
@@ -792,6 +799,21 @@ static int ema_update(float* emb_sum, float* emb_elem, float* E, const float* bs
                       float* partials, bool clear, const vqx_step_close* close, vqx_stream_t stream) {
   if (K <= 0 || D <= 0 || !partials || !diag) { set_error("vqx_vq_ema_update: bad K/D, no partials or no diag"); return -1; }
   CloseArgs C{};
+  GatherIdx R;
+  const float* rsrc = nullptr;
+  int rld = 0;
+  if (close && close->rows_src) {
+    if (close->n_rows != K || K > kGatherArgRows || !close->rows_host || close->rows_ld < D) {
+      set_error("vqx_vq_ema_update_close: rows_src needs n_rows == K <= %d host indices and ld >= D", kGatherArgRows);
+      return -1;
+    }
+    for (int i = 0; i < K; ++i) R.idx[i] = close->rows_host[i];
+    rsrc = close->rows_src;
+    rld = close->rows_ld;
+  } else if (!rand_rows) {
+    set_error("vqx_vq_ema_update: no rand_rows");
+    return -1;
+  }
   if (close) {
     for (int i = 0; i < 2; ++i) {
       if (close->parts[i] && (close->n[i] < 0 || !close->out[i])) { set_error("vqx_vq_ema_update_close: sum %d needs n >= 0 and an output", i); return -1; }
@@ -818,7 +840,8 @@ static int ema_update(float* emb_sum, float* emb_elem, float* E, const float* bs
   const int nb = (K * D + kEmaElems - 1) / kEmaElems;
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(vq_ema_kernel, dim3(nb), dim3(256), 0, s, emb_sum, emb_elem, E, bsum, bcnt, rand_rows, K, D, mu,
-                     omm, threshold, partials, clear ? (float*)bsum : nullptr, diag, clear ? (float*)bcnt : nullptr, C);
+                     omm, threshold, partials, clear ? (float*)bsum : nullptr, diag, clear ? (float*)bcnt : nullptr, C,
+                     rsrc, rld, R);
   return launch_status("vqx_vq_ema_update");
 }
 

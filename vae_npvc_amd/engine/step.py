@@ -1560,12 +1560,17 @@ class VQVAEEngine:
         # the commitment partials' sum (stats[1]) is left to the log-loss launch (train_forward)
         ops.vq_forward(w.z, q.embeddings, w.idx, w.zq, w.zq_c, None, w.vq_part, w.bsum, w.bcnt)
         w.vq_sum_pending = (w.Nz + ops.VQ_FRAMES - 1) // ops.VQ_FRAMES
-        self._ema_rows(w, K)
+        # one process with the fused close: the rows are read from z inside the EMA launch
+        self._ema_rows(w, K, defer=self.opt.fused_close and self.comm is None and K <= 512)
         if self.comm is not None:
             self._ema_work = self.comm.all_reduce_sum(w.ema, async_op=True)
 
-    def _ema_rows(self, w, K):
-        """rand_rows for dead-code replacement: z[randperm(N)[:K]] (update_emb, layers_vq.py:212-213)."""
+    def _ema_rows(self, w, K, defer=False):
+        """rand_rows for dead-code replacement: z[randperm(N)[:K]] (update_emb,
+        layers_vq.py:212-213).  defer: the permutation is drawn here (the CPU
+        generator's order) and kept in w.ema_perm for the EMA launch to read the
+        rows from z itself (vqx_step_close.rows_src)."""
+        w.ema_perm = None
         if w.Nz * self.world < K:
             rows = self._tile_rows(w)
             if self.rank != 0:  # every rank holds the same rows; the EMA bundle is SUM-reduced
@@ -1573,14 +1578,20 @@ class VQVAEEngine:
             w.rand_rows.copy_(rows)
         else:
             perm = self._perm_rows(w.Nz * self.world, K, self.rank * w.Nz, w.Nz if self.comm is not None else None)
+            if defer:
+                w.ema_perm = perm
+                return
             ops.gather_rows_host(w.z, perm, w.rand_rows)
 
     def _ema_apply(self, w, sums=(), publish=None):
         """The EMA update; it leaves bsum / bcnt zero (clear=True), so the next
         step's accumulation needs no zero fill of the statistics."""
         q = self.m.quantizer
+        perm = getattr(w, "ema_perm", None)
         res = ops.vq_ema_update(q.emb_sum, q.emb_elem, q.embeddings, w.bsum, w.bcnt, w.rand_rows, q.mu, q.threshold,
-                                w.stats[4:8], w.ema_part, clear=True, sums=sums, publish=publish)
+                                w.stats[4:8], w.ema_part, clear=True, sums=sums, publish=publish,
+                                rows=(w.z, perm) if perm is not None else None)
+        w.ema_perm = None
         w.ema_clean = True
         return res
 

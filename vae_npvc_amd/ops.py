@@ -692,14 +692,15 @@ def ema_workspace(K, D):
 
 
 def vq_ema_update(emb_sum, emb_elem, E, bsum, bcnt, rand_rows, mu, threshold, diag, partials=None, clear=False,
-                  sums=(), publish=None):
+                  sums=(), publish=None, rows=None):
     """partials: workspace of ceil(K*D/1024) + 1 floats, zero-initialised once
     (the last word is an arrival counter each call leaves zero; allocated here
     if None); clear: bsum / bcnt are zero afterwards (vqx_vq_ema_update_clear).
     sums: up to two (parts, scale, out) -- out[0] = scale * sum(parts) in the
     last workgroup; publish: (mailbox, src, dev_copy) -- src published into the
-    Mailbox after them (vqx_vq_ema_update_close, which implies clear).  Returns
-    publish's (seq, slot), else None."""
+    Mailbox after them; rows: (src, host int32 indices) -- rand_rows read as
+    src[indices] inside the launch (rand_rows unused) (vqx_vq_ema_update_close,
+    which implies clear).  Returns publish's (seq, slot), else None."""
     K, D = E.shape
     need = ema_workspace(K, D)
     if partials is None:
@@ -710,7 +711,7 @@ def vq_ema_update(emb_sum, emb_elem, E, bsum, bcnt, rand_rows, mu, threshold, di
         for t, n, what in ((emb_sum, K * D, "emb_sum"), (emb_elem, K, "emb_elem"), (bsum, K * D, "bsum"),
                            (bcnt, K, "bcnt"), (rand_rows, K * D, "rand_rows"), (diag, 4, "diag")):
             _span(t, n, f"vq_ema_update {what}")
-    if not sums and publish is None:
+    if not sums and publish is None and rows is None:
         call("vqx_vq_ema_update_clear" if clear else "vqx_vq_ema_update", ptr(emb_sum), ptr(emb_elem), ptr(E), ptr(bsum),
              ptr(bcnt), ptr(rand_rows), K, D, mu, threshold, ptr(diag), ptr(partials), stream_ptr())
         return None
@@ -729,6 +730,12 @@ def vq_ema_update(emb_sum, emb_elem, E, bsum, bcnt, rand_rows, mu, threshold, di
         seq, slot = res = mb.reserve()
         c.pub_src, c.pub_n, c.pub_copy, c.pub_box = ptr(src), src.numel(), ptr(copy), mb._dev
         c.pub_slot, c.pub_slots, c.pub_floats, c.pub_seq = slot, mb.slots, mb.floats, seq
+    if rows is not None:
+        src, idx = rows
+        _check_cuda(src)
+        if idx.dtype != torch.int32 or idx.is_cuda or idx.numel() != K or not idx.is_contiguous() or src.shape[1] != D:
+            raise ValueError("vq_ema_update: rows = (src [n, D] device, K host int32 indices)")
+        c.rows_src, c.rows_ld, c.n_rows, c.rows_host = ptr(src), src.stride(0), K, idx.data_ptr()
     call("vqx_vq_ema_update_close", ptr(emb_sum), ptr(emb_elem), ptr(E), ptr(bsum), ptr(bcnt), ptr(rand_rows), K, D,
          mu, threshold, ptr(diag), ptr(partials), ctypes.addressof(c), stream_ptr())
     return res
