@@ -1851,14 +1851,14 @@ __global__ __launch_bounds__(256) void step_prologue_kernel(const vqx_wn_layer* 
 }
 
 // dW_l[o][i] = sum_b dout_l[b][o] c[b][i], dbias_l[o] = sum_b dout_l[b][o]; grid (O/64, n)
-__global__ __launch_bounds__(256) void linear_cond_bwd_w_kernel(const vqx_linear_layer* __restrict__ L,
-                                                                const float* __restrict__ c,
-                                                                const int64_t* __restrict__ ids, int B, int O) {
-  const vqx_linear_layer& l = L[blockIdx.y];
-  __shared__ float cs[kCondB][kCondI];  // c, rows >= B zero
+// one workgroup (bx = output chunk, layer); cs: kCondB x kCondI floats of LDS (c, rows >= B zero)
+__device__ __forceinline__ void linear_cond_bwd_w_block(const vqx_linear_layer* __restrict__ L,
+                                                        const float* __restrict__ c, const int64_t* __restrict__ ids,
+                                                        int B, int O, int bx, int layer, float (*cs)[kCondI]) {
+  const vqx_linear_layer& l = L[layer];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int q = lane >> 4, j = lane & 15;
-  const int o0 = blockIdx.x * kCondO + w * 16;
+  const int o0 = bx * kCondO + w * 16;
   // A operand (m = j, k = b = 16q + s): dout[16q + s][o0 + j], zero past B
   float da[16];
 #pragma unroll
@@ -1905,17 +1905,23 @@ __global__ __launch_bounds__(256) void linear_cond_bwd_w_kernel(const vqx_linear
     for (int r = 0; r < 4; ++r) l.dW[(int64_t)(o0 + 4 * q + r) * kCondI + 16 * it + j] = acc[r] + acc2[r];
   }
 }
+__global__ __launch_bounds__(256) void linear_cond_bwd_w_kernel(const vqx_linear_layer* __restrict__ L,
+                                                                const float* __restrict__ c,
+                                                                const int64_t* __restrict__ ids, int B, int O) {
+  __shared__ float cs[kCondB][kCondI];
+  linear_cond_bwd_w_block(L, c, ids, B, O, blockIdx.x, blockIdx.y, cs);
+}
 
 // dc partials: part[l * (O/64) + oc][b][i] = sum over the chunk's 64 outputs o
 // of dout_l[b][o] W_l[o][i] (k = o = o0 + 16q + s); sum_slices_wide_kernel adds
 // the slices in order.  Wave w covers inputs 32w .. 32w + 31.  grid (O/64, n)
-__global__ __launch_bounds__(256) void linear_cond_bwd_x_kernel(const vqx_linear_layer* __restrict__ L, int B, int O,
-                                                                float* __restrict__ part) {
-  const vqx_linear_layer& l = L[blockIdx.y];
+__device__ __forceinline__ void linear_cond_bwd_x_block(const vqx_linear_layer* __restrict__ L, int B, int O,
+                                                        float* __restrict__ part, int bx, int layer) {
+  const vqx_linear_layer& l = L[layer];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int q = lane >> 4, j = lane & 15;
-  const int o0 = blockIdx.x * kCondO;
-  const int64_t slice = (int64_t)blockIdx.y * (O / kCondO) + blockIdx.x;
+  const int o0 = bx * kCondO;
+  const int64_t slice = (int64_t)layer * (O / kCondO) + bx;
   // B operand (k = 16q + s, n = j) of the wave's two 16-input tiles
   float wv[2][16];
 #pragma unroll
@@ -1943,6 +1949,19 @@ __global__ __launch_bounds__(256) void linear_cond_bwd_x_kernel(const vqx_linear
       }
     }
   }
+}
+__global__ __launch_bounds__(256) void linear_cond_bwd_x_kernel(const vqx_linear_layer* __restrict__ L, int B, int O,
+                                                                float* __restrict__ part) {
+  linear_cond_bwd_x_block(L, B, O, part, blockIdx.x, blockIdx.y);
+}
+// both in one grid (O/64, 2n): layers' dW / dbias in y < n, their dc slices in y >= n
+__global__ __launch_bounds__(256) void linear_cond_bwd_kernel(const vqx_linear_layer* __restrict__ L,
+                                                              const float* __restrict__ c,
+                                                              const int64_t* __restrict__ ids, int B, int O, int n,
+                                                              float* __restrict__ part) {
+  __shared__ float cs[kCondB][kCondI];
+  if ((int)blockIdx.y < n) linear_cond_bwd_w_block(L, c, ids, B, O, blockIdx.x, blockIdx.y, cs);
+  else linear_cond_bwd_x_block(L, B, O, part, blockIdx.x, blockIdx.y - n);
 }
 
 // dc[e] = sum_p part[p][e] in a fixed order: each of the 4 waves of a
@@ -3273,9 +3292,11 @@ extern "C" int vqx_linear_batched_bwd_ids(const vqx_linear_layer* table_dev, int
   if (!linear_ids_ok(table_dev, n, emb, ids, B, I, O, "vqx_linear_batched_bwd_ids")) return -1;
   if (dc && !partials) { set_error("vqx_linear_batched_bwd_ids: dc needs partials [n*O/64][B][I]"); return -1; }
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(linear_cond_bwd_w_kernel, dim3(O / kCondO, n), dim3(256), 0, s, table_dev, emb, ids, B, O);
-  if (dc) {
-    hipLaunchKernelGGL(linear_cond_bwd_x_kernel, dim3(O / kCondO, n), dim3(256), 0, s, table_dev, B, O, partials);
+  if (!dc) {
+    hipLaunchKernelGGL(linear_cond_bwd_w_kernel, dim3(O / kCondO, n), dim3(256), 0, s, table_dev, emb, ids, B, O);
+  } else {  // the weight and data gradients in one grid (round 6: two launches)
+    hipLaunchKernelGGL(linear_cond_bwd_kernel, dim3(O / kCondO, 2 * n), dim3(256), 0, s, table_dev, emb, ids, B, O, n,
+                       partials);
     const int64_t ne = (int64_t)B * I;
     hipLaunchKernelGGL(sum_slices_wide_kernel, dim3((unsigned)((ne + 63) / 64)), dim3(256), 0, s, partials,
                        n * (O / kCondO), ne, dc);
