@@ -204,6 +204,28 @@ def committed_traffic(symbol):
     return None, None
 
 
+PROBE_SCHEDULE = ("probed steps on one stream; the others run the encoder and decoder backward on two "
+                  "streams (EngineOptions.bwd_streams)")
+
+
+class one_stream:
+    """The engine's backward on one stream for the block (EngineOptions.bwd_streams
+    off): a probed step stamps the dominant kernel's launches, whose durations on
+    two streams would include the other chain's co-running work -- the per-launch
+    roofline is the kernel's own (the step's throughput is the timed region's)."""
+
+    def __init__(self, eng):
+        self.eng = eng
+
+    def __enter__(self):
+        self.prev = self.eng.opt.bwd_streams
+        self.eng.opt.bwd_streams = False
+
+    def __exit__(self, *exc):
+        self.eng.opt.bwd_streams = self.prev
+        return False
+
+
 def main():
     a = parse()
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
@@ -257,7 +279,8 @@ def main():
         # event-stamped dispatch costs ~4.6 us of queue time)
         probe.clear()
         ops.set_probe(probe)
-        tr.train_step((xs[0], ys[0]))
+        with one_stream(tr.engine):
+            tr.train_step((xs[0], ys[0]))
         ops.set_probe(None)
         per = {}
         for sym, _, sec, _, info in probe.records():
@@ -275,14 +298,20 @@ def main():
     for i in range(a.steps):
         # the GEMM probe samples every `probe_every`-th step of the timed region
         # (an event-stamped dispatch costs ~4.6 us of queue time)
+        probed = probe is not None and i % a.probe_every == a.probe_every // 2
         if probe is not None:
-            ops.set_probe(probe if i % a.probe_every == a.probe_every // 2 else None)
-        _, det = tr.train_step((xs[i % n_batches], ys[i % n_batches]))
+            ops.set_probe(probe if probed else None)
+        if probed:  # a probed step runs on one stream: the stamped kernel's own duration (see one_stream)
+            with one_stream(tr.engine):
+                _, det = tr.train_step((xs[i % n_batches], ys[i % n_batches]))
+        else:
+            _, det = tr.train_step((xs[i % n_batches], ys[i % n_batches]))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     ops.set_probe(None)
+    summ = probe.summary() if probe is not None else None  # the timed region's probed launches
     if probe is not None:
         probe.select(None)
     elapsed = t1 - t0
@@ -321,7 +350,6 @@ def main():
     kernels = None
     if probe is not None:
         n_probed = sum(1 for i in range(a.steps) if i % a.probe_every == a.probe_every // 2)
-        summ = probe.summary()
         kernels = {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                    for k, v in summ.items()}
         dom = max(summ.items(), key=lambda kv: kv[1]["seconds"])
@@ -334,7 +362,8 @@ def main():
                 "traffic_source": tsrc,
                 "probed_steps": n_probed, "launches_per_step": s["launches"] / max(1, n_probed),
                 "avg_launch_us": round(s["avg_us"], 2),
-                "flops_per_launch": s["flops"] / s["launches"]}
+                "flops_per_launch": s["flops"] / s["launches"],
+                "schedule": PROBE_SCHEDULE if tr.engine._bwd_concurrent() else "one stream"}
 
     out = {
         "metric": "mel-frames/sec/GPU VQ-VAE train step (80-dim mel, batch=64x256f) at 1/2/4/8 GPUs",

@@ -673,3 +673,35 @@ def test_fused_step_close_is_bit_identical(name, dtype):
     assert a[0] == b[0]
     for i, (x, y) in enumerate(zip(a[1:5], b[1:5])):
         assert torch.equal(x, y), i
+
+
+@pytest.mark.parametrize("name,dtype", [("vcc20", "bf16"), ("vcc20", "fp32"), ("aishell3", "bf16"),
+                                        ("vcc20_multi", "bf16")])
+def test_concurrent_encoder_decoder_backward_is_bit_identical(name, dtype):
+    """EngineOptions.bwd_streams (the default, round 6): the encoder backward
+    on a second stream beside the decoder backward (the decoder input carries
+    no gradient, so the chains share no data; the encoder has its own
+    scratch).  Three steps give the same losses, gradients, parameters, Adam
+    moments and codebook as the one-stream schedule (the two-stage topology
+    adds the strided convs' separate column sums)."""
+    from oracle.vqvae_cpu import seeded_batch
+    out = []
+    for conc in (True, False):
+        cfg = cfg_of(name, compute_dtype=dtype, engine={"bwd_streams": conc})
+        tr = make_trainer(cfg, 47)
+        eng = tr.engine
+        assert eng._bwd_concurrent() == conc
+        torch.manual_seed(12)
+        np.random.seed(12)
+        dets = []
+        for s in range(3):
+            dets.append(dict(tr.train_step(tuple(t.cuda() for t in seeded_batch(cfg, 4, 128, 95 + s)))[1]))
+            if s == 0:
+                g0 = eng.flat_g.clone()
+        torch.cuda.synchronize()
+        out.append((dets, g0, eng.flat_p.clone(), eng.exp_avg.clone(), eng.exp_avg_sq.clone(),
+                    tr.model.quantizer.embeddings.detach().clone()))
+    a, b = out
+    assert a[0] == b[0]
+    for i, (x, y) in enumerate(zip(a[1:], b[1:])):
+        assert torch.equal(x, y), i

@@ -19,6 +19,10 @@ if [ "$PART" = 1 ]; then
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py \
     --no-cpu-baseline --no-read-loss > $O/prof.log 2>&1 || exit 1
   python3 tools/trace_steps.py $O/prof/run_kernel_trace.csv 45 > $O/rocprof_summary.txt && head -14 $O/rocprof_summary.txt
+  # the one-stream schedule the bench's probed steps use (the roofline kernel's own launch durations)
+  VQX_ENGINE='{"bwd_streams": false}' timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof1 -o run \
+    --output-format csv -- python3 bench.py --no-cpu-baseline --no-read-loss > $O/prof1.log 2>&1 || exit 1
+  python3 tools/trace_steps.py $O/prof1/run_kernel_trace.csv 45 > $O/rocprof_summary_one_stream.txt && head -4 $O/rocprof_summary_one_stream.txt
 else
   bash tools/gpu_pmc_hbm.sh $TAG || exit 1
   bash tools/pmc_units.sh $TAG python3 bench.py --steps 2 --warmup 1 --no-read-loss --no-probe --no-cpu-baseline \

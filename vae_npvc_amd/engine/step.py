@@ -208,6 +208,11 @@ class EngineOptions:
                        transpose) as one launch (vqx_step_prologue) when the
                        last optimizer step left the row norms current; the
                        same bits as the three launches
+      bwd_streams      (one process) the encoder backward on a second stream
+                       beside the decoder backward: the two chains share no
+                       data (the decoder input carries no gradient), so their
+                       launches fill each other's ramps and tails; the same
+                       bits
       fused_close      the forward's closing work -- the log-loss and
                        commitment sums, the step statistics' mailbox publish --
                        in the EMA update's last workgroup
@@ -233,6 +238,7 @@ class EngineOptions:
     early_stats: bool = True
     fused_prologue: bool = True
     fused_close: bool = True
+    bwd_streams: bool = True
 
 
 class _Stage:
@@ -349,6 +355,7 @@ class Workspace:
         self.dg_flat = e(NCd)
         self.du_flat = e(2 * NCd)
         self.gnb_part = e(max(B * 64 * 2, max(1, Nmax // 128) * ((Cmax + 127) // 128) * 4), dt=F32)
+        self.gnb_part_enc = e(self.gnb_part.numel(), dt=F32)  # the encoder backward's own (EngineOptions.bwd_streams)
         Lmax = max([st.L for st in eng.enc_stages] + [1])
         # per-utterance GN-backward sums per stack layer: conv bias, GN weight, GN bias
         self.colsum_b = [e(B * 2 * Cmax, dt=F32) for _ in range(Lmax)]
@@ -374,6 +381,7 @@ class Workspace:
         self.tmp_flat = e(NCe)
         self.dyemb = e(B, d["ydim"], dt=F32)
         self.cs_part = e(64 * max(Cmax, S + Cmax, mel, 1024), dt=F32)
+        self.cs_part_enc = e(self.cs_part.numel(), dt=F32)
         self.cs_skip = e(_tm(self.Nskip), S, dt=F32)  # dL/dskip
         self.cs_f1 = e(_tm(self.Nskip), S, dt=F32)    # dL/d(final conv 1 output)
         # bias-gradient row-part sums of the encoder output conv (from dL/dz) and of the
@@ -1273,7 +1281,7 @@ class VQVAEEngine:
         if not sw.fuse:
             return {}
         gn = self.enc_stages[si].blocks[j].gns[-1]
-        return dict(gn_bwd=w.gnb_part, gn_h=sw.h[j][-1], gn_mr=sw.mr[j][-1], gn_gamma=gn.weight, gn_beta=gn.bias,
+        return dict(gn_bwd=w.gnb_part_enc, gn_h=sw.h[j][-1], gn_mr=sw.mr[j][-1], gn_gamma=gn.weight, gn_beta=gn.bias,
                     gn_groups=1)
 
     @staticmethod
@@ -1346,8 +1354,8 @@ class VQVAEEngine:
                     dg_b = self._bview(self._blk(w, "enc", si, j, "dgam_b", l), B, C)
                     db_b = self._bview(self._blk(w, "enc", si, j, "dbet_b", l), B, C)
                     nparts = self._gnb_parts(sw, C, fused_here) if l == st.L - 1 else 0
-                    ops.gn_bwd(dy, sw.h[j][l], dh, T, 1, False, sw.mr[j][l], gn.weight, gn.bias, w.gnb_part, cs_b,
-                               dg_b, db_b, nparts=nparts)
+                    ops.gn_bwd(dy, sw.h[j][l], dh, T, 1, False, sw.mr[j][l], gn.weight, gn.bias, w.gnb_part_enc,
+                               cs_b, dg_b, db_b, nparts=nparts)
                     src = sw.a[j] if l == 0 else sw.g[j][l - 1]
                     if l > 0:  # into LeakyReLU(GN(h_{l-1})): its derivative from the sign of the stored output
                         self.wgrad_dgrad(Lr, dh, src, dy2, T, mask=sw.g[j][l - 1], mask_slope=0.2)
@@ -1376,7 +1384,7 @@ class VQVAEEngine:
                 pcur = self._enc_cur(w, si - 1, k)
                 if st.conv.kind == KIND_DOWN:  # folded: no column epilogues, colsum separately
                     self.dgrad(st.conv, cur, pcur, T, mask=prev.a[-1], mask_slope=0.2)
-                    ops.colsum(pcur, w.cs_part, prev.cs[-1][0])
+                    ops.colsum(pcur, w.cs_part_enc, prev.cs[-1][0])
                 else:
                     self.dgrad(st.conv, cur, pcur, T, mask=prev.a[-1], mask_slope=0.2,
                                **self._producer_into_enc(w, si - 1, None, prev.cs[-1], True))
@@ -1710,6 +1718,13 @@ class VQVAEEngine:
         return w
 
 
+    def _bwd_concurrent(self):
+        """EngineOptions.bwd_streams applies: one process (a data-parallel
+        backward starts its all-reduces from the compute stream as groups
+        finish), EMA quantizer, batched weight-norm backward."""
+        return (self.opt.bwd_streams and self.comm is None and self.device.type == "cuda" and not self.plain
+                and self.opt.wn_bwd_batch)
+
     def backward(self, w, grad_loss=None):
         """Data parallel: every backward group's gradients are all-reduced as
         soon as its weight-norm backward has finalised them (_wn_bwd), so the
@@ -1727,6 +1742,18 @@ class VQVAEEngine:
                 self.decoder_bwd(w)
                 self.vq_plain_backward(w)
                 self.encoder_bwd(w)
+            elif self._bwd_concurrent():
+                # the encoder backward on a second stream beside the decoder's: the
+                # decoder input carries no gradient (z_vq is a no-grad gather,
+                # layers_vq.py:292,315), so the two chains share no data; the
+                # encoder's scratch is its own (gnb_part_enc, cs_part_enc) and every
+                # group's split-K slabs and column partials have their own region
+                # (wn_bwd_batch)
+                side = self._fork()
+                with torch.cuda.stream(side):
+                    self.encoder_bwd(w)
+                self.decoder_bwd(w)
+                torch.cuda.current_stream().wait_stream(side)
             else:
                 self.encoder_bwd(w)
                 self.decoder_bwd(w)
