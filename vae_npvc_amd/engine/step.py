@@ -213,6 +213,10 @@ class EngineOptions:
                        data (the decoder input carries no gradient), so their
                        launches fill each other's ramps and tails; the same
                        bits
+      wn_bwd_split     (one process, batched) the encoder groups' weight-norm
+                       backward as its own launch right after the encoder
+                       backward (beside the decoder's under bwd_streams):
+                       neutral, off (profiles/r06/bwd_streams_ab.txt)
       fused_close      the forward's closing work -- the log-loss and
                        commitment sums, the step statistics' mailbox publish --
                        in the EMA update's last workgroup
@@ -239,6 +243,7 @@ class EngineOptions:
     fused_prologue: bool = True
     fused_close: bool = True
     bwd_streams: bool = True
+    wn_bwd_split: bool = False
 
 
 class _Stage:
@@ -871,7 +876,9 @@ class VQVAEEngine:
         w.bwd_tables = {k: ops.wn_table(v) for k, v in t.items()}
         w.bwd_entries = t
         w.bwd_table_cache = {}  # group sequence -> table of one batched launch (_wn_run)
-        w.bwd_sq_cache = {}     # ... and its gradient-norm plan (_sq_plan)
+        w.bwd_ents_cache = {}   # ... its entries and gradient-norm partial count
+        w.bwd_sq_cache = {}     # the launches of a backward -> their gradient-norm plan (_sq_finish)
+        w.sq_buf = None
         # parameters whose gradients are final once a group's launch is done
         # (data parallel: their all-reduce is issued right then, parallel/ddp.py)
         w.bwd_params = {k: self._params_written([t_ for e in entries for t_ in (e.get("dv"), e.get("dg"))])
@@ -1208,7 +1215,10 @@ class VQVAEEngine:
 
     def _wn_run(self, w):
         """One launch for the pending groups (their tables concatenated, cached
-        per group sequence), then their gradients are final."""
+        per group sequence), then their gradients are final.  One process
+        (fuse_grad_norm): each launch also leaves its gradient-norm partials in
+        the next part of the workspace's buffer (w.sq_buf; _sq_finish combines
+        the launches of a backward)."""
         keys = tuple(self._wn_pending)
         self._wn_pending = []
         if not keys:
@@ -1219,21 +1229,46 @@ class VQVAEEngine:
             if self.opt.wn_bwd_sort:  # entries are independent: any order gives the same bits
                 ents.sort(key=_wn_block_bytes, reverse=True)
             tab = w.bwd_table_cache[keys] = ops.wn_table(ents)
-            w.bwd_sq_cache[keys] = self._sq_plan(tab, ents)
-        plan = w.bwd_sq_cache.get(keys) if (self.comm is None and self.opt.fuse_grad_norm) else None
-        if plan is not None:
-            ops.weight_norm_bwd(tab, sq_partials=plan[0])
-            self._sq_plan_ready = plan
+            w.bwd_ents_cache[keys] = (ents, ops.weight_norm_bwd_partials(tab))
+        if self.comm is None and self.opt.fuse_grad_norm:
+            n = w.bwd_ents_cache[keys][1]
+            buf = self._sq_buf(w)
+            off = self._sq_off
+            if off + n > buf.numel():
+                raise RuntimeError(f"gradient-norm partials: {off + n} > {buf.numel()}")
+            ops.weight_norm_bwd(tab, sq_partials=buf[off:off + n])
+            self._sq_off = off + n
+            self._sq_runs.append(keys)
         else:
             ops.weight_norm_bwd(tab)
         self._wn_done.update(keys)
         self._grads_final([i for k in keys for i in w.bwd_params[k]])
 
-    def _sq_plan(self, tab, ents):
-        """Gradient-norm plan of one batched weight-norm backward launch:
-        (partials buffer, int64 [n, 2] device ranges of the flat gradient the
-        launch does not write).  None when its writes overlap (an element would
-        be counted twice) -- the step then re-reads the gradient instead."""
+    def _sq_buf(self, w):
+        """Gradient-norm partials of every weight-norm backward entry (their
+        counts add up entry by entry, so any split of the groups fits)."""
+        if getattr(w, "sq_buf", None) is None:
+            ents = [e for k in w.bwd_entries for e in w.bwd_entries[k]]
+            w.sq_buf = self._zeros(max(1, ops.weight_norm_bwd_partials(ops.wn_table(ents))), dtype=F32)
+        return w.sq_buf
+
+    def _sq_finish(self, w):
+        """The gradient-norm plan of this backward's weight-norm launches: their
+        partials (w.sq_buf[:offset]) and the flat ranges none of them wrote."""
+        runs = tuple(self._sq_runs)
+        if not runs:
+            return
+        plan = w.bwd_sq_cache.get(runs, False)
+        if plan is False:
+            ents = [e for k in runs for e in w.bwd_ents_cache[k][0]]
+            plan = w.bwd_sq_cache[runs] = self._sq_plan(ents, w.sq_buf[:self._sq_off])
+        self._sq_plan_ready = plan
+
+    def _sq_plan(self, ents, parts):
+        """Gradient-norm plan of batched weight-norm backward launches:
+        (their partials, int64 [n, 2] device ranges of the flat gradient the
+        launches do not write).  None when their writes overlap (an element
+        would be counted twice) -- the step then re-reads the gradient instead."""
         base = self.flat_g.data_ptr()
         iv = []
         for e in ents:
@@ -1255,7 +1290,6 @@ class VQVAEEngine:
             cur = hi
         if cur < self.n_params:
             rest.append((cur, self.n_params - cur))
-        parts = self._zeros(max(1, ops.weight_norm_bwd_partials(tab)), dtype=F32)
         rng = torch.tensor(rest, dtype=torch.int64).view(-1, 2).to(self.device) if rest else None
         return parts, rng
 
@@ -1718,6 +1752,13 @@ class VQVAEEngine:
         return w
 
 
+    def _wn_enc_run(self, w):
+        """One process: the encoder groups' batched weight-norm backward as a
+        launch of its own, right after the encoder backward (on its stream
+        under bwd_streams), the decoder groups' at the end."""
+        if self.opt.wn_bwd_split and self.comm is None and self._wn_batched():
+            self._wn_run(w)
+
     def _bwd_concurrent(self):
         """EngineOptions.bwd_streams applies: one process (a data-parallel
         backward starts its all-reduces from the compute stream as groups
@@ -1734,6 +1775,9 @@ class VQVAEEngine:
             self._grads_reset()
         self._wn_pending, self._wn_done = [], set()
         self._sq_plan_ready = None
+        self._sq_off, self._sq_runs = 0, []
+        if self.comm is None and self.opt.fuse_grad_norm and self._wn_batched():
+            self._sq_buf(w)  # allocated before any second stream runs
         self._wn_active = True
         self._fix_now = getattr(w, "fix", frozenset())
         try:
@@ -1749,15 +1793,19 @@ class VQVAEEngine:
                 # encoder's scratch is its own (gnb_part_enc, cs_part_enc) and every
                 # group's split-K slabs and column partials have their own region
                 # (wn_bwd_batch)
+                # the encoder groups' weight-norm backward follows them there
                 side = self._fork()
                 with torch.cuda.stream(side):
                     self.encoder_bwd(w)
+                    self._wn_enc_run(w)
                 self.decoder_bwd(w)
                 torch.cuda.current_stream().wait_stream(side)
             else:
                 self.encoder_bwd(w)
+                self._wn_enc_run(w)
                 self.decoder_bwd(w)
             self._wn_bwd_flush(w)
+            self._sq_finish(w)
         finally:
             self._wn_active = False
             self._fix_now = frozenset()
