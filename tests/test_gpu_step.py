@@ -675,19 +675,22 @@ def test_fused_step_close_is_bit_identical(name, dtype):
         assert torch.equal(x, y), i
 
 
-@pytest.mark.parametrize("name,dtype", [("vcc20", "bf16"), ("vcc20", "fp32"), ("aishell3", "bf16"),
-                                        ("vcc20_multi", "bf16")])
-def test_concurrent_encoder_decoder_backward_is_bit_identical(name, dtype):
+@pytest.mark.parametrize("name,dtype,early", [("vcc20", "bf16", False), ("vcc20", "fp32", False),
+                                              ("aishell3", "bf16", False), ("vcc20_multi", "bf16", False),
+                                              ("vcc20", "bf16", True), ("aishell3", "bf16", True)])
+def test_concurrent_encoder_decoder_backward_is_bit_identical(name, dtype, early):
     """EngineOptions.bwd_streams (the default, round 6): the encoder backward
     on a second stream beside the decoder backward (the decoder input carries
     no gradient, so the chains share no data; the encoder has its own
     scratch).  Three steps give the same losses, gradients, parameters, Adam
     moments and codebook as the one-stream schedule (the two-stage topology
-    adds the strided convs' separate column sums)."""
+    adds the strided convs' separate column sums); early: the encoder backward
+    issued right after the VQ forward, beside the decoder forward
+    (enc_bwd_early)."""
     from oracle.vqvae_cpu import seeded_batch
     out = []
     for conc in (True, False):
-        cfg = cfg_of(name, compute_dtype=dtype, engine={"bwd_streams": conc})
+        cfg = cfg_of(name, compute_dtype=dtype, engine={"bwd_streams": conc, "enc_bwd_early": early and conc})
         tr = make_trainer(cfg, 47)
         eng = tr.engine
         assert eng._bwd_concurrent() == conc

@@ -213,6 +213,11 @@ class EngineOptions:
                        data (the decoder input carries no gradient), so their
                        launches fill each other's ramps and tails; the same
                        bits
+      enc_bwd_early    (with bwd_streams, Trainer/engine train_step) the encoder
+                       backward issued on the second stream right after the
+                       VQ forward, beside the decoder forward and backward:
+                       it needs only z, the gathered codes and the encoder's
+                       activations; the same bits
       wn_bwd_split     (one process, batched) the encoder groups' weight-norm
                        backward as its own launch right after the encoder
                        backward (beside the decoder's under bwd_streams):
@@ -244,6 +249,7 @@ class EngineOptions:
     fused_close: bool = True
     bwd_streams: bool = True
     wn_bwd_split: bool = False
+    enc_bwd_early: bool = True
 
 
 class _Stage:
@@ -1671,7 +1677,7 @@ class VQVAEEngine:
         collective is the identity and the step must equal the plain one."""
         self.world, self.rank, self.comm = comm.world, comm.rank, comm
 
-    def forward_train(self, x, y):
+    def forward_train(self, x, y, early_bwd=False):
         """Training forward (saves every activation the backward needs).
         x (B, mel, T) f32 device, y (B, 1) int64 device."""
         B, _, T = x.shape
@@ -1692,6 +1698,8 @@ class VQVAEEngine:
                 self.embed_and_cond(w, w.y_dev)
         self.encoder_fwd(w, x, transposed=fused)
         self.vq_forward_train(w)
+        if early_bwd and self.opt.enc_bwd_early and self._bwd_concurrent():
+            self._enc_bwd_early(w)
         w.zq_in = w.zq_c
         w.jittered = False
         if self.dims["jitter_p"] > 0 and self.m.jitter.training:
@@ -1752,6 +1760,30 @@ class VQVAEEngine:
         return w
 
 
+    def _bwd_begin(self, w):
+        """The backward's bookkeeping (weight-norm groups, gradient-norm partials,
+        split-K reduction layers)."""
+        if self.comm is not None:
+            self._grads_reset()
+        self._wn_pending, self._wn_done = [], set()
+        self._sq_plan_ready = None
+        self._sq_off, self._sq_runs = 0, []
+        self._wn_active = True
+        if self.comm is None and self.opt.fuse_grad_norm and self._wn_batched():
+            self._sq_buf(w)  # allocated before any second stream runs
+        self._fix_now = getattr(w, "fix", frozenset())
+
+    def _enc_bwd_early(self, w):
+        """EngineOptions.enc_bwd_early: the encoder backward issued on the second
+        stream right after the VQ forward, beside the decoder forward (it needs
+        only z, the gathered codes and the encoder's activations)."""
+        self._bwd_begin(w)
+        side = self._fork()
+        with torch.cuda.stream(side):
+            self.encoder_bwd(w)
+            self._wn_enc_run(w)
+        w.enc_bwd_early = True
+
     def _wn_enc_run(self, w):
         """One process: the encoder groups' batched weight-norm backward as a
         launch of its own, right after the encoder backward (on its stream
@@ -1771,17 +1803,16 @@ class VQVAEEngine:
         soon as its weight-norm backward has finalised them (_wn_bwd), so the
         reduces overlap the rest of the backward; the remainder (embedding,
         codebook) is flushed at the end."""
-        if self.comm is not None:
-            self._grads_reset()
-        self._wn_pending, self._wn_done = [], set()
-        self._sq_plan_ready = None
-        self._sq_off, self._sq_runs = 0, []
-        if self.comm is None and self.opt.fuse_grad_norm and self._wn_batched():
-            self._sq_buf(w)  # allocated before any second stream runs
-        self._wn_active = True
-        self._fix_now = getattr(w, "fix", frozenset())
+        early = getattr(w, "enc_bwd_early", False)
+        w.enc_bwd_early = False
+        if not early:
+            self._bwd_begin(w)
         try:
-            if self.plain:
+            if early:
+                # the encoder backward is already on the second stream (forward_train)
+                self.decoder_bwd(w)
+                torch.cuda.current_stream().wait_stream(self._side_stream())
+            elif self.plain:
                 # straight-through: the encoder's gradient comes through the decoder
                 self.decoder_bwd(w)
                 self.vq_plain_backward(w)
@@ -1953,7 +1984,7 @@ class VQVAEEngine:
         vector [x_loss, sqerr, -, -, entropy, used_curr, usage, diff_emb]."""
         if not self.opt_ready:
             raise RuntimeError("init_optimizer() first")
-        w = self.forward_train(x, y)
+        w = self.forward_train(x, y, early_bwd=True)  # this step's backward follows at unit loss scale
         self.backward(w)
         self.optimizer_step()
         self.vq_ema_update(w)
