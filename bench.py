@@ -376,6 +376,8 @@ def main():
                    "global_batch": B_PER_GPU * world, "seq_len": T_FRAMES, "parallelism": f"dp{world}"},
         "step_mfma_frac": round(FLOP_PER_FRAME * value / world / (PEAK_BF16 if a.dtype == "bf16" else PEAK_F32), 4),
         "roofline": roof,
+        "schedule": {"backward_streams": 2 if tr.engine._bwd_concurrent() else 1,
+                     "encoder_backward_early": bool(tr.engine._bwd_concurrent() and tr.engine.opt.enc_bwd_early)},
         "loss": {k: round(v, 4) for k, v in detail.items()},
         "comm": comm_out,
     }

@@ -250,6 +250,7 @@ class EngineOptions:
     bwd_streams: bool = True
     wn_bwd_split: bool = False
     enc_bwd_early: bool = True
+    side_priority: int = 0
 
 
 class _Stage:
@@ -1027,7 +1028,7 @@ class VQVAEEngine:
 
     def _side_stream(self):
         if self._side is None:
-            self._side = torch.cuda.Stream(device=self.device)
+            self._side = torch.cuda.Stream(device=self.device, priority=self.opt.side_priority)
         return self._side
 
     def _join(self):
