@@ -251,6 +251,7 @@ class EngineOptions:
     wn_bwd_split: bool = False
     enc_bwd_early: bool = True
     side_priority: int = 0
+    vq_stats_side: bool = False
 
 
 class _Stage:
@@ -1581,7 +1582,10 @@ class VQVAEEngine:
                          w.src_t if w.jittered else None, w.Tz, self.vq_normalize, float(self.m.beta), 2.0 / w.Nz,
                          w.dz, w.bsum, w.bcnt, emb, w.e_len if self.vq_normalize else None, self.g(q.embeddings))
 
-    def vq_forward_train(self, w):
+    def vq_forward_train(self, w, defer_stats=False):
+        """defer_stats: the EMA statistics are left to the second stream
+        (_enc_bwd_early runs them there before the encoder backward)."""
+        w.stats_deferred = False
         if self.plain:
             return self.vq_plain_forward(w)
         q = self.m.quantizer
@@ -1607,7 +1611,11 @@ class VQVAEEngine:
             ops.zero_(w.ema)
         w.ema_clean = False
         # the commitment partials' sum (stats[1]) is left to the log-loss launch (train_forward)
-        ops.vq_forward(w.z, q.embeddings, w.idx, w.zq, w.zq_c, None, w.vq_part, w.bsum, w.bcnt)
+        if defer_stats:
+            ops.vq_forward(w.z, q.embeddings, w.idx, w.zq, w.zq_c, None, w.vq_part, None, None)
+            w.stats_deferred = True
+        else:
+            ops.vq_forward(w.z, q.embeddings, w.idx, w.zq, w.zq_c, None, w.vq_part, w.bsum, w.bcnt)
         w.vq_sum_pending = (w.Nz + ops.VQ_FRAMES - 1) // ops.VQ_FRAMES
         # one process with the fused close: the rows are read from z inside the EMA launch
         self._ema_rows(w, K, defer=self.opt.fused_close and self.comm is None and K <= 512)
@@ -1664,6 +1672,9 @@ class VQVAEEngine:
         if getattr(self, "_ema_work", None) is not None:
             self.comm.wait(self._ema_work, "ema")
             self._ema_work = None
+        if getattr(w, "ev_stats", None) is not None:  # statistics from the second stream (vq_stats_side)
+            torch.cuda.current_stream().wait_event(w.ev_stats)
+            w.ev_stats = None
         return self._ema_apply(w, sums, publish)
 
     # ------------------------------------------------------------ full step
@@ -1698,8 +1709,9 @@ class VQVAEEngine:
             else:
                 self.embed_and_cond(w, w.y_dev)
         self.encoder_fwd(w, x, transposed=fused)
-        self.vq_forward_train(w)
-        if early_bwd and self.opt.enc_bwd_early and self._bwd_concurrent():
+        early = early_bwd and self.opt.enc_bwd_early and self._bwd_concurrent()
+        self.vq_forward_train(w, defer_stats=early and self.opt.vq_stats_side and not self._side_on)
+        if early:
             self._enc_bwd_early(w)
         w.zq_in = w.zq_c
         w.jittered = False
@@ -1780,7 +1792,12 @@ class VQVAEEngine:
         only z, the gathered codes and the encoder's activations)."""
         self._bwd_begin(w)
         side = self._fork()
+        w.ev_stats = None
         with torch.cuda.stream(side):
+            if getattr(w, "stats_deferred", False):  # the EMA statistics first; the EMA update waits for them
+                ops.vq_stats(w.z, w.idx, self.dims["K"], w.vq_part, w.bsum, w.bcnt)
+                w.ev_stats = side.record_event()
+                w.stats_deferred = False
             self.encoder_bwd(w)
             self._wn_enc_run(w)
         w.enc_bwd_early = True
