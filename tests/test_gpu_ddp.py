@@ -38,7 +38,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(rank, world, port, dtype, prefix, T_override, q):
+def _run(rank, world, port, dtype, prefix, T_override, q, engine=None):
     try:
         import torch.distributed as dist
         from oracle.vqvae_cpu import seeded_batch
@@ -46,7 +46,7 @@ def _run(rank, world, port, dtype, prefix, T_override, q):
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
         meta, _ = load_fixture(prefix)
-        cfg = cfg_of(meta["config"], compute_dtype=dtype)
+        cfg = cfg_of(meta["config"], compute_dtype=dtype, **({"engine": engine} if engine else {}))
         B, T = meta["B"], T_override or meta["T"]
         tr = make_trainer(cfg, meta["wseed"])
         eng = tr.engine
@@ -73,14 +73,15 @@ def _run(rank, world, port, dtype, prefix, T_override, q):
         q.put((rank, None, None, repr(e) + traceback.format_exc(), None, None))
 
 
-def _spawn(dtype, prefix, T_override=None):
+def _spawn(dtype, prefix, T_override=None, engine=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     keep = os.environ.get("MASTER_ADDR")
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     try:
-        ps = [ctx.Process(target=_run, args=(r, WORLD, port, dtype, prefix, T_override, q)) for r in range(WORLD)]
+        ps = [ctx.Process(target=_run, args=(r, WORLD, port, dtype, prefix, T_override, q, engine))
+              for r in range(WORLD)]
         for p in ps:
             p.start()
         res = [q.get(timeout=240) for _ in ps]
@@ -193,3 +194,19 @@ def test_bench_two_ranks_reports_comm_block():
         assert len(c["grad_wait_ms"]) == 2 and len(c["ema_wait_ms"]) == 2, c
     assert lines["end"]["comm"]["bytes_per_step"] == lines["overlap"]["comm"]["bytes_per_step"]
     assert lines["end"]["comm"]["collectives_per_step"] <= lines["overlap"]["comm"]["collectives_per_step"]
+
+
+@pytest.mark.parametrize("prefix,dtype", [("step_vcc20", "bf16"), ("step_aishell3", "fp32")])
+def test_two_rank_two_stream_backward_is_bit_identical(prefix, dtype):
+    """EngineOptions.bwd_streams under data parallel (round 6): the encoder
+    backward on the second stream from the VQ forward on, its gradient runs
+    all-reduced from that stream (_wn_enc_run).  The weights after three steps
+    (SHA-1 of all 31.3M), the codebooks and every loss equal the one-stream
+    schedule's bit for bit on both ranks: the all-reduces sum the same
+    elements in the same rank order, whatever their bucketing."""
+    a = _spawn(dtype, prefix)
+    b = _spawn(dtype, prefix, engine={"bwd_streams": False})
+    for ra, rb in zip(a, b):
+        assert ra[1] == rb[1], ra[0]
+        assert np.array_equal(ra[2], rb[2])
+        assert ra[3] == rb[3]

@@ -252,6 +252,7 @@ class EngineOptions:
     enc_bwd_early: bool = True
     side_priority: int = 0
     vq_stats_side: bool = False
+    bwd_streams_ddp: bool = True
 
 
 class _Stage:
@@ -1799,22 +1800,32 @@ class VQVAEEngine:
                 w.ev_stats = side.record_event()
                 w.stats_deferred = False
             self.encoder_bwd(w)
-            self._wn_enc_run(w)
+            self._wn_enc_run(w, concurrent=True)
         w.enc_bwd_early = True
 
-    def _wn_enc_run(self, w):
-        """One process: the encoder groups' batched weight-norm backward as a
-        launch of its own, right after the encoder backward (on its stream
-        under bwd_streams), the decoder groups' at the end."""
-        if self.opt.wn_bwd_split and self.comm is None and self._wn_batched():
+    def _wn_enc_run(self, w, concurrent=False):
+        """After the encoder backward (on its stream under bwd_streams).  One
+        process: the encoder groups' batched weight-norm backward as a launch of
+        its own (wn_bwd_split), the decoder groups' at the end.  Data parallel on
+        two streams: the encoder's pending groups, and every gradient run then
+        final, leave from the encoder's stream -- an all-reduce waits for the
+        stream it is issued from, so no run may mix the two chains' gradients
+        (the decoder's are not final yet: its backward is issued after)."""
+        if not self._wn_batched():
+            return
+        if self.comm is not None:
+            if concurrent:
+                self._wn_run(w)
+                self._grads_final([], flush=True)
+        elif self.opt.wn_bwd_split:
             self._wn_run(w)
 
     def _bwd_concurrent(self):
-        """EngineOptions.bwd_streams applies: one process (a data-parallel
-        backward starts its all-reduces from the compute stream as groups
-        finish), EMA quantizer, batched weight-norm backward."""
-        return (self.opt.bwd_streams and self.comm is None and self.device.type == "cuda" and not self.plain
-                and self.opt.wn_bwd_batch)
+        """EngineOptions.bwd_streams applies: EMA quantizer, batched weight-norm
+        backward; data parallel with bwd_streams_ddp (the encoder's gradient
+        runs all-reduced from its stream, _wn_enc_run)."""
+        return (self.opt.bwd_streams and self.device.type == "cuda" and not self.plain and self.opt.wn_bwd_batch
+                and (self.comm is None or self.opt.bwd_streams_ddp))
 
     def backward(self, w, grad_loss=None):
         """Data parallel: every backward group's gradients are all-reduced as
@@ -1846,7 +1857,7 @@ class VQVAEEngine:
                 side = self._fork()
                 with torch.cuda.stream(side):
                     self.encoder_bwd(w)
-                    self._wn_enc_run(w)
+                    self._wn_enc_run(w, concurrent=True)
                 self.decoder_bwd(w)
                 torch.cuda.current_stream().wait_stream(side)
             else:
