@@ -955,6 +955,7 @@ class VQVAEEngine:
                          pad=1, **kw)
 
     _fix_now = frozenset()  # the current backward's workspace's Workspace.fix
+    _side_pending = False  # work issued on the side stream since the last join
 
     def wgrad(self, Lr, dy, x, T, pro=L.PRO_NONE, scale=1.0):
         """Weight-gradient slabs from dy (output gradient, T frames per utterance) and the input x."""
@@ -1035,14 +1036,18 @@ class VQVAEEngine:
 
     def _join(self):
         """Order the current stream after all side-stream work issued so far
-        (the previous step's codebook update, its loss diagnostics)."""
-        if self._side is not None:
+        (the previous step's codebook update, its loss diagnostics); nothing to
+        do when no work went there since the last join (a stream wait costs
+        the stream tens of microseconds)."""
+        if self._side is not None and self._side_pending:
             torch.cuda.current_stream().wait_stream(self._side)
+            self._side_pending = False
 
     def _fork(self):
         """The side stream, ordered after everything issued so far on the current stream."""
         side = self._side_stream()
         side.wait_stream(torch.cuda.current_stream())
+        self._side_pending = True
         return side
 
     def _cond_ids(self, w, ids):
@@ -1840,7 +1845,7 @@ class VQVAEEngine:
             if early:
                 # the encoder backward is already on the second stream (forward_train)
                 self.decoder_bwd(w)
-                torch.cuda.current_stream().wait_stream(self._side_stream())
+                self._join()
             elif self.plain:
                 # straight-through: the encoder's gradient comes through the decoder
                 self.decoder_bwd(w)
@@ -1859,7 +1864,7 @@ class VQVAEEngine:
                     self.encoder_bwd(w)
                     self._wn_enc_run(w, concurrent=True)
                 self.decoder_bwd(w)
-                torch.cuda.current_stream().wait_stream(side)
+                self._join()
             else:
                 self.encoder_bwd(w)
                 self._wn_enc_run(w)
