@@ -1037,8 +1037,7 @@ class VQVAEEngine:
     def _join(self):
         """Order the current stream after all side-stream work issued so far
         (the previous step's codebook update, its loss diagnostics); nothing to
-        do when no work went there since the last join (a stream wait costs
-        the stream tens of microseconds)."""
+        do when no work went there since the last join."""
         if self._side is not None and self._side_pending:
             torch.cuda.current_stream().wait_stream(self._side)
             self._side_pending = False
