@@ -3292,11 +3292,15 @@ extern "C" int vqx_linear_batched_bwd_ids(const vqx_linear_layer* table_dev, int
   if (!linear_ids_ok(table_dev, n, emb, ids, B, I, O, "vqx_linear_batched_bwd_ids")) return -1;
   if (dc && !partials) { set_error("vqx_linear_batched_bwd_ids: dc needs partials [n*O/64][B][I]"); return -1; }
   hipStream_t s = (hipStream_t)stream;
-  if (!dc) {
+  if (!dc || 2 * (int64_t)n > 65535) {  // (grid y: 2n)
     hipLaunchKernelGGL(linear_cond_bwd_w_kernel, dim3(O / kCondO, n), dim3(256), 0, s, table_dev, emb, ids, B, O);
+    if (dc)
+      hipLaunchKernelGGL(linear_cond_bwd_x_kernel, dim3(O / kCondO, n), dim3(256), 0, s, table_dev, B, O, partials);
   } else {  // the weight and data gradients in one grid (round 6: two launches)
     hipLaunchKernelGGL(linear_cond_bwd_kernel, dim3(O / kCondO, 2 * n), dim3(256), 0, s, table_dev, emb, ids, B, O, n,
                        partials);
+  }
+  if (dc) {
     const int64_t ne = (int64_t)B * I;
     hipLaunchKernelGGL(sum_slices_wide_kernel, dim3((unsigned)((ne + 63) / 64)), dim3(256), 0, s, partials,
                        n * (O / kCondO), ne, dc);
