@@ -253,7 +253,6 @@ class EngineOptions:
     side_priority: int = 0
     vq_stats_side: bool = False
     bwd_streams_ddp: bool = True
-    ema_side: bool = False
 
 
 class _Stage:
@@ -1766,20 +1765,8 @@ class VQVAEEngine:
                 snap = torch.empty_like(w.stats)  # the device copy, for reads after the slot was reused
             pub_stream = torch.cuda.current_stream()
             if close:  # the sums and the publish in the EMA update's last workgroup
-                ema_side = self.opt.ema_side and getattr(w, "enc_bwd_early", False)
-                if ema_side:
-                    # behind the encoder backward on the second stream, after this
-                    # stream's log-loss partials: off the decoder chain
-                    side = self._side_stream()
-                    side.wait_stream(pub_stream)
-                    self._side_pending = True
-                    pub_stream = side
-                with torch.cuda.stream(pub_stream):
-                    seq, slot = self._ema_finish(w, sums=sums,
-                                                 publish=(self._mailbox, w.stats, snap) if publish else None) \
-                        or (None, None)
-                if ema_side and publish:
-                    snap.record_stream(pub_stream)
+                seq, slot = self._ema_finish(w, sums=sums, publish=(self._mailbox, w.stats, snap) if publish else None) \
+                    or (None, None)
                 w.ema_applied = True
             else:
                 if not self.plain:
