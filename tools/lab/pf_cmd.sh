@@ -1,3 +1,5 @@
+# tap-reuse L2 prefetch lab (round 6, profiles/r06/tr_prefetch_ab.txt).  Variants: git apply
+# tools/lab/tr_prefetch.patch, then python -m vae_npvc_amd.csrc.build --out lab_so/pfN.so -D VQX_TR_PF=N (N = 1, 2)
 set -o pipefail
 mkdir -p gpurun_out/pf
 VQX_LIB=lab_so/pf2.so timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -k "tap_reuse or fused_dgrad" > gpurun_out/pf/t.log 2>&1 || { tail -5 gpurun_out/pf/t.log; exit 1; }
